@@ -1,0 +1,469 @@
+#!/usr/bin/env python3
+"""Generate the golden vectors under tests/golden/ by running the REFERENCE's own Python code.
+
+Test infrastructure only — this script runs in the development container, where the read-only
+reference checkout exists at /root/reference/PocketNeRF. It never runs on the GPU box and nothing
+under indoor-nerf_amd/ imports it. Its outputs (small .npz files of inputs + expected outputs) are
+the pin for oracle/ and for the HIP kernels.
+
+How the reference is imported:
+  * `kornia`, `imageio`, `cv2`, `configargparse`, `lpips`, `seaborn`, `pyvista`, `skimage` are not
+    installed; they are only needed so run_nerf.py's top-level imports resolve (data loaders,
+    metrics, bbox helpers), so they are replaced by empty modules;
+  * utils.py:9-10 builds BOX_OFFSETS with device='cuda' at import; torch.tensor is wrapped during
+    that import so the tensor lands on the CPU;
+  * NeRFSmall reads self.predict_normals before anything sets it (run_nerf_helpers.py:258); the
+    class attribute is set to False, and create_nerf (broken at HEAD, run_nerf.py:249-268) is
+    bypassed by building the modules by hand with the arguments it would pass;
+  * bytecode shipped in the reference's __pycache__ is never loaded: sys.pycache_prefix points to
+    a private temporary directory before the first reference import.
+
+All reference computations run on the CPU in float32, with pytest=True for every random draw.
+
+Usage:  python tests/golden/make_golden.py        (writes tests/golden/*.npz, ~2 MB total)
+"""
+import os
+import sys
+import tempfile
+import types
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REF = os.environ.get("NERF_REFERENCE", "/root/reference/PocketNeRF")
+
+sys.pycache_prefix = tempfile.mkdtemp(prefix="golden_pyc_")
+sys.dont_write_bytecode = True
+sys.path.insert(0, HERE)
+
+import torch  # noqa: E402
+
+from tables import blender_bbox, closed_form_table, synthetic_rays  # noqa: E402
+
+torch.set_default_dtype(torch.float32)
+torch.set_num_threads(8)
+
+
+def _install_stubs():
+    for name in ["imageio", "cv2", "configargparse", "lpips", "seaborn", "pyvista"]:
+        sys.modules.setdefault(name, types.ModuleType(name))
+    sk = types.ModuleType("skimage")
+    skm = types.ModuleType("skimage.metrics")
+    skm.structural_similarity = None
+    sk.metrics = skm
+    sys.modules["skimage"] = sk
+    sys.modules["skimage.metrics"] = skm
+    kornia = types.ModuleType("kornia")
+
+    def create_meshgrid(H, W, normalized_coordinates=True):  # only used by bbox helpers
+        xs = torch.linspace(0, W - 1, W)
+        ys = torch.linspace(0, H - 1, H)
+        gx, gy = torch.meshgrid(xs, ys, indexing="xy")
+        return torch.stack([gx, gy], -1)[None]
+
+    kornia.create_meshgrid = create_meshgrid
+    sys.modules["kornia"] = kornia
+
+
+def load_reference():
+    _install_stubs()
+    sys.path.insert(0, REF)
+    real_tensor = torch.tensor
+
+    def cpu_tensor(*a, **k):
+        if k.get("device") == "cuda":
+            k["device"] = "cpu"
+        return real_tensor(*a, **k)
+
+    torch.tensor = cpu_tensor
+    try:
+        import utils as ref_utils  # noqa: F401
+    finally:
+        torch.tensor = real_tensor
+    import hash_encoding as ref_he
+    import run_nerf_helpers as ref_h
+    import quantization as ref_q
+    import loss as ref_loss
+    import radam as ref_radam
+    import run_nerf as ref_rn
+    ref_h.NeRFSmall.predict_normals = False
+    return types.SimpleNamespace(utils=ref_utils, he=ref_he, h=ref_h, q=ref_q, loss=ref_loss,
+                                 radam=ref_radam, rn=ref_rn)
+
+
+def bbox_t():
+    lo, hi = blender_bbox()
+    return (torch.from_numpy(lo), torch.from_numpy(hi))
+
+
+def make_embedder(ref, finest, table=None):
+    emb = ref.he.HashEmbedder(bbox_t(), n_levels=16, n_features_per_level=2, log2_hashmap_size=19,
+                              base_resolution=16, finest_resolution=finest)
+    if table is not None:
+        with torch.no_grad():
+            for i in range(16):
+                emb.embeddings[i].weight.copy_(torch.from_numpy(table[i]))
+    return emb
+
+
+def make_mlp(ref, seed):
+    torch.manual_seed(seed)
+    # create_nerf's arguments (run_nerf.py:240-247): input_ch = 32 (hash), input_ch_views = 16 (SH deg 4)
+    return ref.h.NeRFSmall(num_layers=2, hidden_dim=64, geo_feat_dim=15, num_layers_color=3,
+                           hidden_dim_color=64, input_ch=32, input_ch_views=16)
+
+
+def mlp_arrays(net, prefix):
+    return {f"{prefix}{k.replace('.', '_')}": v.detach().numpy().copy() for k, v in net.state_dict().items()}
+
+
+def sample_points(n, rng, lo, hi, n_out=0, n_edge=0):
+    """Points inside the bbox, plus points outside it and exactly on its faces/corners."""
+    u = rng.rand(n, 3).astype(np.float32)
+    pts = lo + (hi - lo) * u
+    pts = pts.astype(np.float32)
+    k = 0
+    for _ in range(n_out):          # outside on a random axis
+        ax = rng.randint(3)
+        pts[k, ax] = (hi[ax] + 0.3 * rng.rand()) if rng.rand() < 0.5 else (lo[ax] - 0.3 * rng.rand())
+        k += 1
+    for _ in range(n_edge):         # exactly on the min or max face (tests clamp/floor == res)
+        ax = rng.randint(3)
+        pts[k, ax] = hi[ax] if rng.rand() < 0.5 else lo[ax]
+        k += 1
+    pts[k] = hi                     # the max corner
+    pts[k + 1] = lo                 # the min corner
+    return pts
+
+
+def gen_levels(ref, out):
+    d = {}
+    for finest in (512, 1024):
+        emb = make_embedder(ref, finest)
+        res = np.array([float(torch.floor(emb.base_resolution * emb.b ** i)) for i in range(16)], np.float32)
+        d[f"res_{finest}"] = res
+        d[f"b_{finest}"] = np.float32(emb.b)
+    np.savez_compressed(os.path.join(out, "f1_levels.npz"), **d)
+    return d
+
+
+def gen_voxel(ref, out, levels):
+    rng = np.random.RandomState(1)
+    lo, hi = blender_bbox()
+    xyz = sample_points(1024, rng, lo, hi, n_out=64, n_edge=64)
+    idx, vmin, vmax = [], [], []
+    keep = None
+    x = torch.from_numpy(xyz)
+    for lvl in range(16):
+        res = torch.tensor(levels["res_1024"][lvl])
+        a, b, h, k = ref.utils.get_voxel_vertices(x, bbox_t(), res, 19)
+        idx.append(h.numpy().astype(np.int32))
+        vmin.append(a.numpy())
+        vmax.append(b.numpy())
+        keep = (k.sum(-1) == 3).numpy()
+    np.savez_compressed(os.path.join(out, "f2_voxel.npz"), xyz=xyz, idx=np.stack(idx, 1),
+                        vmin=np.stack(vmin, 1), vmax=np.stack(vmax, 1), keep=keep)
+
+
+def gen_hash(ref, out):
+    table = closed_form_table()
+    rng = np.random.RandomState(2)
+    lo, hi = blender_bbox()
+    d = {}
+    for finest in (512, 1024):
+        emb = make_embedder(ref, finest, table)
+        xyz = sample_points(2048, rng, lo, hi, n_out=96, n_edge=96)
+        with torch.no_grad():
+            feat, keep = emb(torch.from_numpy(xyz))
+        d[f"xyz_{finest}"] = xyz
+        d[f"feat_{finest}"] = feat.numpy()
+        d[f"keep_{finest}"] = keep.numpy()
+    np.savez_compressed(os.path.join(out, "f3_hash_fwd.npz"), **d)
+
+    # backward: sparse dense-grad entries of the 16 nn.Embedding tables
+    emb = make_embedder(ref, 1024, table)
+    rng = np.random.RandomState(3)
+    xyz = sample_points(128, rng, lo, hi, n_out=8, n_edge=8)
+    dfeat = rng.randn(128, 32).astype(np.float32)
+    feat, keep = emb(torch.from_numpy(xyz))
+    (feat * torch.from_numpy(dfeat)).sum().backward()
+    lv, rows, vals = [], [], []
+    for i in range(16):
+        g = emb.embeddings[i].weight.grad.numpy()
+        nz = np.nonzero(np.any(g != 0, axis=1))[0]
+        lv.append(np.full(nz.shape, i, np.int32))
+        rows.append(nz.astype(np.int32))
+        vals.append(g[nz])
+    np.savez_compressed(os.path.join(out, "f4_hash_bwd.npz"), xyz=xyz, dfeat=dfeat,
+                        level=np.concatenate(lv), row=np.concatenate(rows), grad=np.concatenate(vals))
+
+
+def gen_sh(ref, out):
+    rng = np.random.RandomState(4)
+    d = rng.randn(1024, 3).astype(np.float32)
+    d = (torch.from_numpy(d) / torch.norm(torch.from_numpy(d), dim=-1, keepdim=True)).numpy()
+    with torch.no_grad():
+        sh = ref.he.SHEncoder()(torch.from_numpy(d)).numpy()
+    np.savez_compressed(os.path.join(out, "f5_sh.npz"), dirs=d, sh=sh)
+
+
+def gen_mlp(ref, out):
+    net = make_mlp(ref, 0)
+    rng = np.random.RandomState(5)
+    x = (rng.randn(1024, 48) * 0.5).astype(np.float32)
+    g = rng.randn(1024, 4).astype(np.float32)
+    xt = torch.from_numpy(x).requires_grad_(True)
+    raw = net(xt)
+    (raw * torch.from_numpy(g)).sum().backward()
+    d = dict(x=x, g_raw=g, raw=raw.detach().numpy(), dx=xt.grad.numpy())
+    d.update(mlp_arrays(net, "w_"))
+    for k, p in net.named_parameters():
+        d["dw_" + k.replace(".", "_")] = p.grad.numpy().copy()
+    np.savez_compressed(os.path.join(out, "f6_mlp.npz"), **d)
+
+
+def composite_inputs(rng, R, S, degenerate=True):
+    raw = (rng.randn(R, S, 4) * 2.0).astype(np.float32)
+    raw[..., 3] += 0.5
+    near, far = 2.0, 6.0
+    z = np.sort(near + (far - near) * rng.rand(R, S), axis=-1).astype(np.float32)
+    d = rng.randn(R, 3).astype(np.float32)
+    if degenerate:
+        raw[0, :, 3] = -np.abs(raw[0, :, 3]) - 0.1     # all sigma <= 0: weights 0, depth NaN
+        raw[1, :, 3] = 60.0                            # saturated: alpha == 1 from the first sample
+    return raw, z, d
+
+
+def gen_composite(ref, out):
+    rng = np.random.RandomState(6)
+    d = {}
+    for S in (64, 192):
+        for white in (0, 1):
+            raw, z, rd = composite_inputs(rng, 64, S)
+            with torch.no_grad():
+                res = ref.rn.raw2outputs(torch.from_numpy(raw), torch.from_numpy(z), torch.from_numpy(rd),
+                                         0, bool(white), pytest=False)
+            tag = f"S{S}_w{white}"
+            d[f"raw_{tag}"], d[f"z_{tag}"], d[f"d_{tag}"] = raw, z, rd
+            for name, v in zip(["rgb", "disp", "acc", "weights", "depth", "entropy"], res):
+                d[f"{name}_{tag}"] = v.numpy()
+            # backward (rays without the degenerate NaN-depth case)
+            raw2, z2, rd2 = composite_inputs(rng, 64, S, degenerate=False)
+            rt = torch.from_numpy(raw2).requires_grad_(True)
+            res = ref.rn.raw2outputs(rt, torch.from_numpy(z2), torch.from_numpy(rd2), 0, bool(white), pytest=False)
+            gr = rng.randn(64, 3).astype(np.float32)
+            gacc, gdep, gdisp, gent = (rng.randn(64).astype(np.float32) for _ in range(4))
+            gw = (rng.randn(64, S) * 0.1).astype(np.float32)
+            loss = ((res[0] * torch.from_numpy(gr)).sum() + (res[1] * torch.from_numpy(gdisp)).sum()
+                    + (res[2] * torch.from_numpy(gacc)).sum() + (res[3] * torch.from_numpy(gw)).sum()
+                    + (res[4] * torch.from_numpy(gdep)).sum() + (res[5] * torch.from_numpy(gent)).sum())
+            loss.backward()
+            d[f"braw_{tag}"], d[f"bz_{tag}"], d[f"bd_{tag}"] = raw2, z2, rd2
+            d[f"g_rgb_{tag}"], d[f"g_acc_{tag}"], d[f"g_depth_{tag}"] = gr, gacc, gdep
+            d[f"g_disp_{tag}"], d[f"g_ent_{tag}"], d[f"g_w_{tag}"] = gdisp, gent, gw
+            d[f"draw_{tag}"] = rt.grad.numpy()
+    # raw noise, pytest path: np.random.seed(0); rand(R,S) * std   (run_nerf.py:378-385)
+    raw, z, rd = composite_inputs(rng, 64, 64, degenerate=False)
+    with torch.no_grad():
+        res = ref.rn.raw2outputs(torch.from_numpy(raw), torch.from_numpy(z), torch.from_numpy(rd),
+                                 1.0, False, pytest=True)
+    d["raw_noise"], d["z_noise"], d["d_noise"] = raw, z, rd
+    for name, v in zip(["rgb", "disp", "acc", "weights", "depth", "entropy"], res):
+        d[f"{name}_noise"] = v.numpy()
+    np.savez_compressed(os.path.join(out, "f7_composite.npz"), **d)
+
+
+def gen_pdf(ref, out):
+    rng = np.random.RandomState(7)
+    R = 256
+    z = np.sort(2.0 + 4.0 * rng.rand(R, 64), -1).astype(np.float32)
+    bins = (0.5 * (z[:, 1:] + z[:, :-1])).astype(np.float32)
+    w = (rng.rand(R, 62) ** 4).astype(np.float32)
+    w[0] = 0.0                          # all-zero weights row: uniform pdf after +1e-5
+    w[1, :] = 0.0
+    w[1, 30] = 1.0                      # single spike
+    d = dict(bins=bins, weights=w)
+    with torch.no_grad():
+        d["det"] = ref.h.sample_pdf(torch.from_numpy(bins), torch.from_numpy(w), 128, det=True).numpy()
+        d["rand_pytest"] = ref.h.sample_pdf(torch.from_numpy(bins), torch.from_numpy(w), 128,
+                                            det=False, pytest=True).numpy()
+    np.savez_compressed(os.path.join(out, "f8_pdf.npz"), **d)
+
+
+def build_render_kwargs(ref, emb, coarse, fine, n_samples, n_importance, perturb, noise, lindisp):
+    sh = ref.he.SHEncoder()
+    nqf = lambda inputs, viewdirs, network_fn: ref.rn.run_network(  # noqa: E731
+        inputs, viewdirs, network_fn, embed_fn=emb, embeddirs_fn=sh, netchunk=65536)
+    return dict(network_query_fn=nqf, perturb=perturb, N_importance=n_importance, network_fine=fine,
+                N_samples=n_samples, network_fn=coarse, embed_fn=emb, use_viewdirs=True, white_bkgd=True,
+                raw_noise_std=noise, predict_normals=False, ndc=False, lindisp=lindisp, near=2.0, far=6.0)
+
+
+def gen_render(ref, out):
+    table = closed_form_table()
+    d = {}
+    variants = {
+        "A": dict(n_samples=64, n_importance=128, perturb=1.0, noise=0.0, lindisp=False),
+        "B": dict(n_samples=64, n_importance=64, perturb=0.0, noise=1.0, lindisp=True),
+    }
+    for tag, v in variants.items():
+        emb = make_embedder(ref, 1024, table)
+        coarse, fine = make_mlp(ref, 10), make_mlp(ref, 11)
+        ro, rd = synthetic_rays(64, seed=8)
+        kw = build_render_kwargs(ref, emb, coarse, fine, **v)
+        with torch.no_grad():
+            rgb, depth, acc, extras = ref.rn.render(800, 800, None, chunk=32768,
+                                                    rays=(torch.from_numpy(ro), torch.from_numpy(rd)),
+                                                    retraw=True, pytest=True, **kw)
+        d[f"rays_o_{tag}"], d[f"rays_d_{tag}"] = ro, rd
+        d[f"rgb_{tag}"], d[f"depth_{tag}"], d[f"acc_{tag}"] = rgb.numpy(), depth.numpy(), acc.numpy()
+        for k in ["rgb0", "depth0", "acc0", "sparsity_loss", "sparsity_loss0", "z_std", "raw", "pts"]:
+            d[f"{k}_{tag}"] = extras[k].numpy()
+        d.update(mlp_arrays(coarse, f"coarse_{tag}_"))
+        d.update(mlp_arrays(fine, f"fine_{tag}_"))
+    np.savez_compressed(os.path.join(out, "f9_render.npz"), **d)
+
+
+def table_checksums(emb):
+    """Per-level (sum, sum of squares) in float64 plus 64 fixed sampled rows per level."""
+    rows = (np.arange(64, dtype=np.int64) * 8191 + 17) % (1 << 19)
+    cs, samples = [], []
+    for i in range(16):
+        t = emb.embeddings[i].weight.detach().double()
+        cs.append([t.sum().item(), (t * t).sum().item()])
+        samples.append(emb.embeddings[i].weight.detach().numpy()[rows])
+    return np.array(cs), np.stack(samples), rows
+
+
+def gen_train(ref, out):
+    """One reference training iteration (run_nerf.py:1007-1035 without TV, 1161-1162, 1289-1293)
+    and seven RAdam steps on the same batch (RAdam updates parameters from its 6th step)."""
+    table = closed_form_table(scale=1e-4, salt=3)
+    emb = make_embedder(ref, 1024, table)
+    coarse, fine = make_mlp(ref, 20), make_mlp(ref, 21)
+    d = {}
+    d.update(mlp_arrays(coarse, "coarse0_"))
+    d.update(mlp_arrays(fine, "fine0_"))
+    grad_vars = list(coarse.parameters()) + list(fine.parameters())
+    opt = ref.radam.RAdam([{"params": grad_vars, "weight_decay": 1e-6},
+                           {"params": list(emb.parameters()), "eps": 1e-15}], lr=5e-4, betas=(0.9, 0.99))
+    ro, rd = synthetic_rays(64, seed=9)
+    rng = np.random.RandomState(10)
+    target = rng.rand(64, 3).astype(np.float32)
+    d["rays_o"], d["rays_d"], d["target"] = ro, rd, target
+    kw = build_render_kwargs(ref, emb, coarse, fine, 64, 128, 1.0, 0.0, False)
+    losses = []
+    for step in range(7):
+        rgb, depth, acc, extras = ref.rn.render(800, 800, None, chunk=32768,
+                                                rays=(torch.from_numpy(ro), torch.from_numpy(rd)),
+                                                retraw=True, pytest=True, **kw)
+        opt.zero_grad()
+        img_loss = ref.h.img2mse(rgb, torch.from_numpy(target))
+        img_loss0 = ref.h.img2mse(extras["rgb0"], torch.from_numpy(target))
+        sparsity = 1e-10 * (extras["sparsity_loss"].sum() + extras["sparsity_loss0"].sum())
+        loss = img_loss + img_loss0 + sparsity
+        loss.backward()
+        if step == 0:
+            d["loss0"] = np.array([img_loss.item(), img_loss0.item(), sparsity.item(), loss.item()])
+            for name, p in list(coarse.named_parameters()):
+                d["gcoarse_" + name.replace(".", "_")] = p.grad.numpy().copy()
+            for name, p in list(fine.named_parameters()):
+                d["gfine_" + name.replace(".", "_")] = p.grad.numpy().copy()
+            rows = (np.arange(64, dtype=np.int64) * 8191 + 17) % (1 << 19)
+            gs = []
+            for i in range(16):
+                g = emb.embeddings[i].weight.grad.double()
+                gs.append([g.sum().item(), (g * g).sum().item(), g.abs().sum().item()])
+            d["gtable_checksum"] = np.array(gs)
+            d["gtable_rows"] = rows
+        opt.step()
+        new_lrate = 5e-4 * (0.1 ** (step / (500 * 1000)))       # global_step advances by one per iteration
+        for g in opt.param_groups:
+            g["lr"] = new_lrate
+        losses.append(loss.item())
+    d["losses"] = np.array(losses)
+    cs, samples, rows = table_checksums(emb)
+    d["table_checksum"], d["table_samples"], d["table_rows"] = cs, samples, rows
+    d.update(mlp_arrays(coarse, "coarse7_"))
+    d.update(mlp_arrays(fine, "fine7_"))
+    np.savez_compressed(os.path.join(out, "f10_train.npz"), **d)
+
+
+def gen_quant(ref, out):
+    rng = np.random.RandomState(11)
+    d = {}
+    x = (rng.randn(512, 8, 2) * 1e-4).astype(np.float32)
+    q = ref.q.LearnedBitwidthQuantizer(init_bits=8.0, min_bits=2.0, max_bits=32.0, symmetric=False)
+    q.train()
+    xt = torch.from_numpy(x).requires_grad_(True)
+    y = q(xt)
+    y.sum().backward()
+    d.update(asym_x=x, asym_y=y.detach().numpy(), asym_dx=xt.grad.numpy(),
+             asym_range=q.range_scale.detach().numpy(), asym_vmax=q.v_max.detach().numpy())
+    x2 = (rng.randn(512, 8, 2) * 1e-4).astype(np.float32)
+    d.update(asym_x2=x2, asym_y2=q(torch.from_numpy(x2)).detach().numpy())
+    w = (rng.randn(64, 32) * 0.1).astype(np.float32)
+    qs = ref.q.LearnedBitwidthQuantizer(init_bits=8.0, min_bits=2.0, max_bits=32.0, symmetric=True)
+    qs.train()
+    d.update(sym_w=w, sym_y=qs(torch.from_numpy(w)).detach().numpy())
+    np.savez_compressed(os.path.join(out, "f11_quant.npz"), **d)
+
+
+def gen_tv(ref, out):
+    table = closed_form_table(scale=0.05, salt=5)
+    emb = make_embedder(ref, 1024, table)
+    real_randint = torch.randint
+    gen = torch.Generator().manual_seed(12)
+    record = []
+
+    def recording_randint(low, high, size, **k):
+        v = real_randint(int(low), int(high), size, generator=gen)
+        record.append(v.numpy().astype(np.int64))
+        return v
+
+    ref.loss.torch.randint = recording_randint
+    try:
+        losses = []
+        for i in range(16):
+            losses.append(ref.loss.total_variation_loss(emb.embeddings[i], emb.base_resolution,
+                                                        emb.finest_resolution, i, 19, n_levels=16))
+    finally:
+        ref.loss.torch.randint = real_randint
+    total = sum(losses)
+    total.backward()
+    rows_all, lv_all, g_all, cs = [], [], [], []
+    for i in range(16):
+        g = emb.embeddings[i].weight.grad.numpy()
+        gd = g.astype(np.float64)
+        cs.append([gd.sum(), (gd * gd).sum(), np.abs(gd).sum()])
+        if i < 3:                       # full sparse gradient of the three coarsest levels only
+            nz = np.nonzero(np.any(g != 0, axis=1))[0]
+            rows_all.append(nz.astype(np.int32))
+            lv_all.append(np.full(nz.shape, i, np.int32))
+            g_all.append(g[nz])
+    np.savez_compressed(os.path.join(out, "f12_tv.npz"), min_vertex=np.stack(record),
+                        level_loss=np.array([float(v.detach()) for v in losses], np.float64),
+                        grad_checksum=np.array(cs), level=np.concatenate(lv_all), row=np.concatenate(rows_all),
+                        grad=np.concatenate(g_all))
+
+
+def main():
+    out = HERE
+    ref = load_reference()
+    levels = gen_levels(ref, out)
+    gen_voxel(ref, out, levels)
+    gen_hash(ref, out)
+    gen_sh(ref, out)
+    gen_mlp(ref, out)
+    gen_composite(ref, out)
+    gen_pdf(ref, out)
+    gen_render(ref, out)
+    gen_quant(ref, out)
+    gen_tv(ref, out)
+    gen_train(ref, out)
+    tot = sum(os.path.getsize(os.path.join(out, f)) for f in os.listdir(out) if f.endswith(".npz"))
+    print(f"golden fixtures written to {out}: {tot / 1e6:.2f} MB")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,70 @@
+"""Deterministic synthetic inputs shared by the golden-vector generator and the tests.
+
+Test infrastructure only. The golden fixtures must not carry a 64 MiB hash table, so the
+"trained-like" table is a closed-form function of (level, row, feature) that numpy reproduces
+bit-for-bit anywhere (uint64 integer hashing, then one float64 -> float32 rounding).
+"""
+import numpy as np
+
+M32 = np.uint64(0xFFFFFFFF)
+
+
+def _mix32(h):
+    h = h & M32
+    h ^= h >> np.uint64(13)
+    h = (h * np.uint64(0x5BD1E995)) & M32
+    h ^= h >> np.uint64(15)
+    return h
+
+
+def closed_form_table(n_levels=16, log2_T=19, n_feat=2, scale=0.05, salt=0):
+    """[n_levels, 2**log2_T, n_feat] float32 table with values in [-scale, scale)."""
+    T = 1 << log2_T
+    rows = np.arange(T, dtype=np.uint64)
+    out = np.empty((n_levels, T, n_feat), np.float32)
+    for lvl in range(n_levels):
+        for f in range(n_feat):
+            h = rows * np.uint64(2654435761) + np.uint64(lvl * 40503 + f * 9973 + 12345 + salt * 7919)
+            h = _mix32(h)
+            out[lvl, :, f] = (((h.astype(np.float64) / 4294967296.0) * 2.0 - 1.0) * scale).astype(np.float32)
+    return out
+
+
+def blender_bbox():
+    """Scene AABB of the synthetic Blender rig (measured with
+    get_bbox3d_for_blenderobj near=2 far=6 on the lego poses)."""
+    return (np.array([-3.8502, -3.8500, -3.3230], np.float32),
+            np.array([3.8491, 3.8496, 2.6801], np.float32))
+
+
+def pose_spherical(theta_deg, phi_deg, radius):
+    """Camera-to-world of the Blender spiral rig (restated from load_blender.py:12-35)."""
+    t = np.eye(4)
+    t[2, 3] = radius
+    ph = phi_deg / 180.0 * np.pi
+    rot_phi = np.array([[1, 0, 0, 0], [0, np.cos(ph), -np.sin(ph), 0],
+                        [0, np.sin(ph), np.cos(ph), 0], [0, 0, 0, 1]], np.float64)
+    th = theta_deg / 180.0 * np.pi
+    rot_theta = np.array([[np.cos(th), 0, -np.sin(th), 0], [0, 1, 0, 0],
+                          [np.sin(th), 0, np.cos(th), 0], [0, 0, 0, 1]], np.float64)
+    c2w = rot_theta @ rot_phi @ t
+    c2w = np.array([[-1, 0, 0, 0], [0, 0, 1, 0], [0, 1, 0, 0], [0, 0, 0, 1]], np.float64) @ c2w
+    return c2w.astype(np.float32)
+
+
+def synthetic_rays(n_rays, H=800, W=800, pose_index=3, seed=0):
+    """Pinhole rays of one spiral pose, n_rays pixels chosen by a seeded permutation.
+
+    Returns rays_o, rays_d as float32 [n_rays, 3] (d unnormalised, as get_rays makes them)."""
+    camera_angle_x = 0.6911112070083618
+    focal = 0.5 * W / np.tan(0.5 * camera_angle_x)
+    thetas = np.linspace(-180, 180, 101)[:-1]
+    c2w = pose_spherical(thetas[pose_index], -30.0, 4.0311)
+    rng = np.random.RandomState(seed)
+    pix = rng.permutation(H * W)[:n_rays]
+    i = (pix % W).astype(np.float32)
+    j = (pix // W).astype(np.float32)
+    dirs = np.stack([(i - 0.5 * W) / focal, -(j - 0.5 * H) / focal, -np.ones_like(i)], -1).astype(np.float32)
+    rays_d = (dirs[:, None, :] * c2w[None, :3, :3]).sum(-1).astype(np.float32)
+    rays_o = np.broadcast_to(c2w[:3, 3], rays_d.shape).astype(np.float32).copy()
+    return rays_o, rays_d

@@ -1,0 +1,204 @@
+"""Pin the CPU oracle (oracle/nerf_oracle.py) against golden vectors produced by the reference's
+own code (tests/golden/make_golden.py). CPU only."""
+import numpy as np
+import torch
+
+from tables import blender_bbox, closed_form_table
+
+
+def _bbox():
+    lo, hi = blender_bbox()
+    return torch.from_numpy(lo), torch.from_numpy(hi)
+
+
+def _tables(table, requires_grad=False):
+    return [torch.from_numpy(table[i]).clone().requires_grad_(requires_grad) for i in range(table.shape[0])]
+
+
+def _mlp(d, prefix):
+    return {k: torch.from_numpy(d[prefix + k.replace(".", "_")]) for k in
+            ("sigma_net.0.weight", "sigma_net.1.weight", "color_net.0.weight", "color_net.1.weight",
+             "color_net.2.weight")}
+
+
+def test_level_resolutions(golden, oracle):
+    g = golden("f1_levels")
+    for finest in (512, 1024):
+        np.testing.assert_array_equal(oracle.level_resolutions(16, finest).numpy(), g[f"res_{finest}"])
+
+
+def test_voxel_corners_exact(golden, oracle):
+    g = golden("f2_voxel")
+    res = oracle.level_resolutions(16, 1024)
+    x = torch.from_numpy(g["xyz"])
+    bmin, bmax = _bbox()
+    for lvl in range(16):
+        vmin, vmax, idx, inside = oracle.voxel_corners(x, bmin, bmax, res[lvl], 19)
+        np.testing.assert_array_equal(idx.numpy().astype(np.int32), g["idx"][:, lvl])
+        np.testing.assert_array_equal(vmin.numpy(), g["vmin"][:, lvl])
+        np.testing.assert_array_equal(vmax.numpy(), g["vmax"][:, lvl])
+    np.testing.assert_array_equal((inside.sum(-1) == 3).numpy(), g["keep"])
+
+
+def test_hash_encode_fwd_exact(golden, oracle):
+    g = golden("f3_hash_fwd")
+    table = closed_form_table()
+    bmin, bmax = _bbox()
+    for finest in (512, 1024):
+        res = oracle.level_resolutions(16, finest)
+        feat, keep = oracle.hash_encode(torch.from_numpy(g[f"xyz_{finest}"]), _tables(table), bmin, bmax, res)
+        np.testing.assert_array_equal(feat.numpy(), g[f"feat_{finest}"])
+        np.testing.assert_array_equal(keep.numpy(), g[f"keep_{finest}"])
+
+
+def test_hash_encode_bwd(golden, oracle):
+    g = golden("f4_hash_bwd")
+    tabs = _tables(closed_form_table(), requires_grad=True)
+    bmin, bmax = _bbox()
+    feat, _ = oracle.hash_encode(torch.from_numpy(g["xyz"]), tabs, bmin, bmax, oracle.level_resolutions(16, 1024))
+    (feat * torch.from_numpy(g["dfeat"])).sum().backward()
+    dense = np.zeros((16, 1 << 19, 2), np.float32)
+    dense[g["level"], g["row"]] = g["grad"]
+    got = np.stack([t.grad.numpy() for t in tabs])
+    np.testing.assert_allclose(got, dense, rtol=1e-6, atol=1e-7)
+
+
+def test_sh4_exact(golden, oracle):
+    g = golden("f5_sh")
+    np.testing.assert_array_equal(oracle.sh4(torch.from_numpy(g["dirs"])).numpy(), g["sh"])
+
+
+def test_mlp_fwd_bwd(golden, oracle):
+    g = golden("f6_mlp")
+    w = {k: v.clone().requires_grad_(True) for k, v in _mlp(g, "w_").items()}
+    x = torch.from_numpy(g["x"]).requires_grad_(True)
+    raw = oracle.mlp_forward(x, w)
+    np.testing.assert_allclose(raw.detach().numpy(), g["raw"], rtol=1e-5, atol=1e-6)
+    (raw * torch.from_numpy(g["g_raw"])).sum().backward()
+    np.testing.assert_allclose(x.grad.numpy(), g["dx"], rtol=1e-5, atol=1e-6)
+    for k, v in w.items():
+        np.testing.assert_allclose(v.grad.numpy(), g["dw_" + k.replace(".", "_")], rtol=1e-4, atol=1e-5)
+
+
+def test_composite(golden, oracle):
+    g = golden("f7_composite")
+    names = ["rgb", "disp", "acc", "weights", "depth", "entropy"]
+    for S in (64, 192):
+        for white in (0, 1):
+            tag = f"S{S}_w{white}"
+            out = oracle.composite(torch.from_numpy(g[f"raw_{tag}"]), torch.from_numpy(g[f"z_{tag}"]),
+                                   torch.from_numpy(g[f"d_{tag}"]), None, bool(white))
+            for n, v in zip(names, out):
+                np.testing.assert_allclose(v.numpy(), g[f"{n}_{tag}"], rtol=1e-5, atol=1e-6, equal_nan=True)
+            raw = torch.from_numpy(g[f"braw_{tag}"]).requires_grad_(True)
+            out = oracle.composite(raw, torch.from_numpy(g[f"bz_{tag}"]), torch.from_numpy(g[f"bd_{tag}"]),
+                                   None, bool(white))
+            loss = sum((o * torch.from_numpy(g[f"g_{n}_{tag}"])).sum() for o, n in
+                       zip(out, ["rgb", "disp", "acc", "w", "depth", "ent"]))
+            loss.backward()
+            np.testing.assert_allclose(raw.grad.numpy(), g[f"draw_{tag}"], rtol=1e-4, atol=1e-6)
+    noise = oracle.pytest_uniforms(g["raw_noise"].shape[:2]) * 1.0
+    out = oracle.composite(torch.from_numpy(g["raw_noise"]), torch.from_numpy(g["z_noise"]),
+                           torch.from_numpy(g["d_noise"]), noise, False)
+    for n, v in zip(names, out):
+        np.testing.assert_allclose(v.numpy(), g[f"{n}_noise"], rtol=1e-5, atol=1e-6)
+
+
+def test_sample_pdf(golden, oracle):
+    g = golden("f8_pdf")
+    bins, w = torch.from_numpy(g["bins"]), torch.from_numpy(g["weights"])
+    np.testing.assert_allclose(oracle.sample_pdf(bins, w, 128).numpy(), g["det"], rtol=1e-6, atol=1e-6)
+    u = oracle.pytest_uniforms((bins.shape[0], 128))
+    np.testing.assert_allclose(oracle.sample_pdf(bins, w, 128, u).numpy(), g["rand_pytest"], rtol=1e-6, atol=1e-6)
+
+
+def test_render_rays(golden, oracle):
+    g = golden("f9_render")
+    table = closed_form_table()
+    bmin, bmax = _bbox()
+    res = oracle.level_resolutions(16, 1024)
+    cfg = {"A": dict(n_samples=64, n_importance=128, perturb=1.0, raw_noise_std=0.0, lindisp=False),
+           "B": dict(n_samples=64, n_importance=64, perturb=0.0, raw_noise_std=1.0, lindisp=True)}
+    for tag, kw in cfg.items():
+        ro, rd = torch.from_numpy(g[f"rays_o_{tag}"]), torch.from_numpy(g[f"rays_d_{tag}"])
+        with torch.no_grad():
+            out = oracle.render_rays(ro, rd, oracle.viewdirs_of(rd), 2.0, 6.0, _mlp(g, f"coarse_{tag}_"),
+                                     _mlp(g, f"fine_{tag}_"), _tables(table), bmin, bmax, res, **kw)
+        for k in ["rgb", "depth", "acc"]:
+            np.testing.assert_allclose(out[k + "_map"].numpy(), g[f"{k}_{tag}"], rtol=1e-5, atol=1e-5)
+        for k in ["rgb0", "depth0", "acc0", "sparsity_loss", "sparsity_loss0", "z_std", "raw", "pts"]:
+            np.testing.assert_allclose(out[k].numpy(), g[f"{k}_{tag}"], rtol=1e-5, atol=1e-5)
+
+
+def test_quantizer(golden, oracle):
+    g = golden("f11_quant")
+    x = torch.from_numpy(g["asym_x"])
+    rng, vmax = torch.tensor(float(x.max() - x.min())), x.max()
+    np.testing.assert_allclose(rng.numpy(), g["asym_range"], rtol=0, atol=0)
+    y = oracle.lbq_forward(x, 8.0, rng, vmax, symmetric=False)
+    np.testing.assert_array_equal(y.numpy(), g["asym_y"])
+    y2 = oracle.lbq_forward(torch.from_numpy(g["asym_x2"]), 8.0, rng, vmax, symmetric=False)
+    np.testing.assert_array_equal(y2.numpy(), g["asym_y2"])
+    w = torch.from_numpy(g["sym_w"])
+    y3 = oracle.lbq_forward(w, 8.0, 2 * torch.max(w.min().abs(), w.max().abs()), None, symmetric=True)
+    np.testing.assert_array_equal(y3.numpy(), g["sym_y"])
+
+
+def test_tv_loss(golden, oracle):
+    g = golden("f12_tv")
+    tabs = _tables(closed_form_table(scale=0.05, salt=5), requires_grad=True)
+    losses = [oracle.tv_loss(tabs[i], i, torch.from_numpy(g["min_vertex"][i]), 16, 1024) for i in range(16)]
+    np.testing.assert_allclose([float(v) for v in losses], g["level_loss"], rtol=1e-5)
+    sum(losses).backward()
+    for i in range(16):
+        gd = tabs[i].grad.double().numpy()
+        np.testing.assert_allclose([gd.sum(), (gd * gd).sum(), np.abs(gd).sum()], g["grad_checksum"][i],
+                                   rtol=1e-4, atol=1e-9)
+    for i in range(3):
+        sel = g["level"] == i
+        np.testing.assert_allclose(tabs[i].grad.numpy()[g["row"][sel]], g["grad"][sel], rtol=1e-5, atol=1e-9)
+
+
+def test_train_step(golden, oracle):
+    """One reference training iteration and seven RAdam steps (run_nerf.py:1007-1162, 1289-1293)."""
+    g = golden("f10_train")
+    table = closed_form_table(scale=1e-4, salt=3)
+    tabs = _tables(table, requires_grad=True)
+    cw = {k: v.clone().requires_grad_(True) for k, v in _mlp(g, "coarse0_").items()}
+    fw = {k: v.clone().requires_grad_(True) for k, v in _mlp(g, "fine0_").items()}
+    opt = oracle.RAdamOracle([
+        dict(params=list(cw.values()) + list(fw.values()), lr=5e-4, betas=(0.9, 0.99), eps=1e-8, weight_decay=1e-6),
+        dict(params=tabs, lr=5e-4, betas=(0.9, 0.99), eps=1e-15, weight_decay=0)])
+    bmin, bmax = _bbox()
+    res = oracle.level_resolutions(16, 1024)
+    ro, rd, target = (torch.from_numpy(g[k]) for k in ("rays_o", "rays_d", "target"))
+    losses = []
+    for step in range(7):
+        out = oracle.render_rays(ro, rd, oracle.viewdirs_of(rd), 2.0, 6.0, cw, fw, tabs, bmin, bmax, res)
+        for p in list(cw.values()) + list(fw.values()) + tabs:
+            p.grad = None
+        l_img = torch.mean((out["rgb_map"] - target) ** 2)
+        l_img0 = torch.mean((out["rgb0"] - target) ** 2)
+        l_sp = 1e-10 * (out["sparsity_loss"].sum() + out["sparsity_loss0"].sum())
+        loss = l_img + l_img0 + l_sp
+        loss.backward()
+        if step == 0:
+            np.testing.assert_allclose([l_img.item(), l_img0.item(), l_sp.item(), loss.item()], g["loss0"], rtol=1e-5)
+            for k, v in cw.items():
+                np.testing.assert_allclose(v.grad.numpy(), g["gcoarse_" + k.replace(".", "_")], rtol=1e-3, atol=1e-7)
+            for k, v in fw.items():
+                np.testing.assert_allclose(v.grad.numpy(), g["gfine_" + k.replace(".", "_")], rtol=1e-3, atol=1e-7)
+            for i in range(16):
+                gd = tabs[i].grad.double()
+                np.testing.assert_allclose([gd.sum().item(), (gd * gd).sum().item(), gd.abs().sum().item()],
+                                           g["gtable_checksum"][i], rtol=1e-3, atol=1e-12)
+        opt.step()
+        for grp in opt.groups:
+            grp["lr"] = 5e-4 * (0.1 ** (step / (500 * 1000)))
+        losses.append(loss.item())
+    np.testing.assert_allclose(losses, g["losses"], rtol=1e-4)
+    for k, v in cw.items():
+        np.testing.assert_allclose(v.detach().numpy(), g["coarse7_" + k.replace(".", "_")], rtol=1e-4, atol=1e-6)
+    for i in range(16):
+        t = tabs[i].detach()
+        np.testing.assert_allclose(t.numpy()[g["table_rows"]], g["table_samples"][i], rtol=1e-4, atol=1e-7)
