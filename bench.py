@@ -1,0 +1,226 @@
+#!/usr/bin/env python3
+"""Headline benchmark: train rays/sec of the render_rays hot path (BASELINE.json `metric`).
+
+A step = one full training iteration of PocketNeRF's train() on the lego configuration
+(configs/lego.txt + finest_res 1024): 4096 rays (BASELINE's batch), 64 stratified coarse samples,
+128 importance samples (192 fine), L=16 levels, T=2^19, white background, perturb=1, TV loss
+(weight 1e-6, the first 1000 iterations), sparsity loss, backward, RAdam, lr decay. Rays are
+synthetic (the lego rig's spiral poses; no dataset on the box) and resident in HBM before timing.
+
+Multi-GPU (torchrun, one process per GPU): each rank trains its own 4096-ray shard (weak
+scaling); gradients are all-reduced once per step over RCCL (one 67 MB bucket).
+
+Prints ONE JSON line (rank 0) with `roofline` for the dominant kernel (HIP-event timed inside the
+timed region) and `cpu_baseline` (the oracle's CPU training step on a bounded sample, N=1 only).
+"""
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: f32 matrix (v_mfma_f32_32x32x2_f32) dense peak
+
+# Algorithmic cost per unit of each kernel: bytes (HBM-bound) or FLOPs (MFMA).
+#   hash fwd : per point  16 levels x 8 corners x 8 B gathered + 12 B xyz + 128 B features + 1 B keep
+#   hash bwd : per point  16 x 8 x 8 B read+write of the atomically added rows (2 x 1024) + 12 + 128
+#   mlp fwd  : per point  9,344 MACs = 18,688 FLOP
+#   mlp bwd  : per point  2 x 18,688 FLOP (input + weight grads; the recomputed forward is not counted)
+#   composite: per sample 16 B raw + 4 B z + 4 B weights (fwd) / + 16 B grad (bwd)
+UNIT_COST = {
+    "nerf_hash_encode_fwd": ("hbm", 16 * 8 * 8 + 12 + 128 + 1, "point"),
+    "nerf_hash_encode_bwd": ("hbm", 2 * 16 * 8 * 8 + 12 + 128, "point"),
+    "nerf_mlp_fwd": ("mfma", 18688, "point"),
+    "nerf_mlp_bwd": ("mfma", 2 * 18688, "point"),
+    "nerf_composite_fwd": ("hbm", 24, "sample"),
+    "nerf_composite_bwd": ("hbm", 40, "sample"),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=8)
+    ap.add_argument("--rays", type=int, default=4096)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-rays", type=int, default=1024)
+    ap.add_argument("--cpu-steps", type=int, default=3)
+    ap.add_argument("--profile-kernels", type=int, default=1, help="record HIP events per kernel in the timed region")
+    return ap.parse_args()
+
+
+def cpu_baseline(n_rays, steps):
+    """The oracle (CPU PyTorch restatement of the reference) timed on this host: one training
+    iteration = coarse+fine render, losses incl. TV, backward, RAdam; 1 warm-up + `steps` timed."""
+    from oracle import nerf_oracle as orc
+    from indoor_nerf_amd.synthetic import blender_bbox, blender_rays
+    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    threads = max(1, min(cores, 16))
+    torch.set_num_threads(threads)
+    lo, hi = (torch.from_numpy(v) for v in blender_bbox())
+    res = orc.level_resolutions(16, 1024)
+    g = torch.Generator().manual_seed(0)
+    tabs = [((torch.rand(1 << 19, 2, generator=g) * 2 - 1) * 1e-4).requires_grad_(True) for _ in range(16)]
+    cw = {k: v.requires_grad_(True) for k, v in orc.mlp_init(1).items()}
+    fw = {k: v.requires_grad_(True) for k, v in orc.mlp_init(2).items()}
+    opt = orc.RAdamOracle([dict(params=list(cw.values()) + list(fw.values()), lr=5e-4, betas=(0.9, 0.99), eps=1e-8,
+                                weight_decay=1e-6), dict(params=tabs, lr=5e-4, betas=(0.9, 0.99), eps=1e-15,
+                                                         weight_decay=0)])
+    ro, rd = (torch.from_numpy(v) for v in blender_rays(n_rays, seed=11))
+    vd = orc.viewdirs_of(rd)
+    target = torch.rand(n_rays, 3, generator=g)
+
+    def step(i):
+        out = orc.render_rays(ro, rd, vd, 2.0, 6.0, cw, fw, tabs, lo, hi, res)
+        for p in list(cw.values()) + list(fw.values()) + tabs:
+            p.grad = None
+        loss = torch.mean((out["rgb_map"] - target) ** 2) + torch.mean((out["rgb0"] - target) ** 2)
+        loss = loss + 1e-10 * (out["sparsity_loss"].sum() + out["sparsity_loss0"].sum())
+        tv = 0
+        for lvl in range(16):
+            r, cube = orc.tv_cube(lvl, 16, 1024)
+            mv = torch.randint(0, r - cube, (3,), generator=g)
+            tv = tv + orc.tv_loss(tabs[lvl], lvl, mv, 16, 1024)
+        loss = loss + 1e-6 * tv
+        loss.backward()
+        opt.step()
+
+    step(0)
+    times = []
+    for i in range(steps):
+        t0 = time.perf_counter()
+        step(i + 1)
+        times.append(time.perf_counter() - t0)
+    t = float(np.median(times))
+    return {"value": round(n_rays / t, 2), "unit": "rays/s", "cores": threads, "kind": "port",
+            "sample": f"{n_rays} rays x (64+128) samples, finest 1024, full train iteration incl. TV + RAdam; "
+                      f"median of {steps} steps after 1 warm-up ({platform.processor() or platform.machine()})"}
+
+
+def main():
+    a = parse()
+    import indoor_nerf_amd as nerf
+    from indoor_nerf_amd import _lib
+    from indoor_nerf_amd.synthetic import blender_bbox, blender_rays
+
+    rank, world, local = nerf.init_process_group()
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    lo, hi = blender_bbox()
+    args = nerf.make_args(bounding_box=(torch.from_numpy(lo), torch.from_numpy(hi)), finest_res=1024, N_samples=64,
+                          N_importance=128, white_bkgd=True, perturb=1.0, lrate_decay=500, tv_loss_weight=1e-6)
+    torch.manual_seed(0)
+    nerf.manual_seed(1234 + rank)
+    kw, _, _, grad_vars, opt = nerf.create_nerf(args, device=dev)
+    params = grad_vars + list(kw["embed_fn"].parameters())
+    nerf.broadcast_params(params)
+    arena = nerf.GradArena(params)
+    ro, rd = blender_rays(a.rays, seed=100 + rank)
+    rays = (torch.from_numpy(ro).to(dev), torch.from_numpy(rd).to(dev))
+    target = torch.rand(a.rays, 3, device=dev, generator=torch.Generator(device=dev).manual_seed(rank))
+    tv_gen = torch.Generator().manual_seed(7)       # same TV cuboids on every rank
+    hook = (lambda: arena.allreduce_mean()) if world > 1 else None
+
+    def step(i):
+        return nerf.train_step(rays, target, kw, opt, args, i, grad_hook=hook, loss_scale_sparsity=float(world),
+                               tv_generator=tv_gen, zero_grad=arena.zero_)
+
+    it = 1
+    for _ in range(a.warmup):
+        step(it)
+        it += 1
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    if a.profile_kernels:
+        _lib.set_timing(True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        loss, psnr = step(it)
+        it += 1
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    recs = _lib.timing_records()
+    _lib.set_timing(False)
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # per-kernel timing from the timed region
+    per = {}
+    for name, e0, e1 in recs:
+        per.setdefault(name, []).append(e0.elapsed_time(e1) * 1e-3)
+    kernels = {}
+    for name, ts in per.items():
+        kernels[name] = {"launches": len(ts), "avg_ms": 1e3 * float(np.mean(ts)), "total_ms": 1e3 * float(np.sum(ts))}
+    roofline = None
+    if kernels:
+        dom = max(kernels, key=lambda n: kernels[n]["total_ms"])
+        P_coarse, P_fine = a.rays * 64, a.rays * 192
+        units_per_launch = {"point": (P_coarse + P_fine) / 2, "sample": (P_coarse + P_fine) / 2}
+        if dom in UNIT_COST:
+            bound, per_unit, unit = UNIT_COST[dom]
+            units = units_per_launch[unit]
+            avg_s = kernels[dom]["avg_ms"] * 1e-3
+            if bound == "hbm":
+                ach = per_unit * units / avg_s / 1e9
+                roofline = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                            "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                            "per_launch_units": units, "algorithmic_bytes_per_unit": per_unit}
+            else:
+                ach = per_unit * units / avg_s / 1e12
+                roofline = {"kernel": dom, "bound": "mfma", "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
+                            "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+                            "per_launch_units": units, "algorithmic_flops_per_unit": per_unit}
+        else:
+            roofline = {"kernel": dom, "bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": None, "traffic": None}
+
+    value = world * a.rays * a.steps / elapsed
+    out = {
+        "metric": "train rays/sec (4096 rays x 192 samples)",
+        "value": round(value, 1),
+        "unit": "rays/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(1e3 * elapsed / a.steps, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic (lego spiral-pose rays, random-init hash tables and MLPs)",
+        "config": {"workload": "lego train step: 4096 rays/GPU x (64 coarse + 128 fine) samples, finest_res 1024, "
+                               "L=16, F=2, T=2^19, RAdam, TV+sparsity losses",
+                   "rays_per_gpu": a.rays, "global_batch": a.rays * world, "samples": "64+128",
+                   "parallelism": f"dp{world}"},
+        "loss": round(float(loss), 6),
+        "roofline": roofline,
+        "kernels": {k: {kk: round(vv, 4) if isinstance(vv, float) else vv for kk, vv in v.items()}
+                    for k, v in sorted(kernels.items(), key=lambda kv: -kv[1]["total_ms"])},
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(a.cpu_rays, a.cpu_steps)
+    elif rank == 0:
+        out["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,184 @@
+/*
+ * nerf_hip.h — C ABI of libnerfhip.so, the MI355X (gfx950) kernels of the render_rays hot path.
+ *
+ * Boundary: the reference is pure PyTorch; every function below replaces one
+ * implicit eager-op sequence of its Python API. The Python host layer (indoor-nerf_amd/, imported
+ * as indoor_nerf_amd) binds these with ctypes and keeps the reference's module/function names.
+ *
+ * Conventions
+ *   - Every pointer argument named d_* is DEVICE memory, caller-owned, contiguous, float32 unless
+ *     typed otherwise; outputs are caller-allocated. The library allocates nothing and keeps no
+ *     state between calls (reentrant; safe under stream capture).
+ *   - Host arrays (level resolutions, table pointer lists, bbox) are read during the call only.
+ *   - `stream` is a hipStream_t passed as void* (torch.cuda.current_stream().cuda_stream).
+ *   - Return 0 on success, else a NERF_E_* code; nerf_last_error() gives the message (per thread).
+ *   - Random draws: a NULL d_u* argument means "draw in-kernel" from Philox4x32-10 keyed by
+ *     (seed, offset); a non-NULL one supplies the uniforms (the reference's pytest=True path).
+ */
+#ifndef NERF_HIP_H
+#define NERF_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NERF_OK 0
+#define NERF_E_ARG 1        /* bad shape / size / null pointer            */
+#define NERF_E_LAUNCH 2     /* hipLaunchKernel / hipGetLastError failed     */
+#define NERF_E_UNSUPPORTED 3
+
+#define NERF_MAX_LEVELS 16
+
+const char* nerf_last_error(void);
+int nerf_abi_version(void);
+
+/* ---- multi-resolution hash grid -------------------------------------------------------------
+ * Replaces HashEmbedder.forward (PocketNeRF/hash_encoding.py:82-107) = per level
+ * get_voxel_vertices + hash (utils.py:95-117, :13-24), nn.Embedding gather (hash_encoding.py:94)
+ * and trilinear_interp (:56-80); and its autograd backward (embedding_dense_backward).
+ * Feature output element (point p, level l, feature f) is written at
+ *   d_feat[p*feat_stride_point + l*feat_stride_level + f]     (f in {0,1}; n_features == 2)
+ * so [P, 2L] point-major (stride_point=2L, stride_level=2) and [L, P, 2] level-major
+ * (stride_point=2, stride_level=2P) are both supported. d_keep[p] = point inside the bbox on
+ * all three axes (hash_encoding.py:106). level_res: host float[n_levels] = floor(16*b^l) (:89).
+ * Tables: host array of n_levels device pointers, each [2^log2_T, 2] float32.
+ */
+int nerf_hash_encode_fwd(const float* d_xyz, int64_t n_points,
+                         const float* bbox_min3, const float* bbox_max3,
+                         const float* level_res, int n_levels, int log2_T,
+                         const float* const* d_tables,
+                         float* d_feat, int64_t feat_stride_point, int64_t feat_stride_level,
+                         uint8_t* d_keep, void* stream);
+
+/* d_dtables: host array of n_levels device pointers; gradients are ACCUMULATED (atomic adds). */
+int nerf_hash_encode_bwd(const float* d_xyz, int64_t n_points,
+                         const float* bbox_min3, const float* bbox_max3,
+                         const float* level_res, int n_levels, int log2_T,
+                         const float* d_dfeat, int64_t feat_stride_point, int64_t feat_stride_level,
+                         float* const* d_dtables, void* stream);
+
+/* ---- spherical harmonics, degree 4 (SHEncoder.forward, hash_encoding.py:153-191) ---------- */
+int nerf_sh4_fwd(const float* d_dirs, int64_t n, float* d_out /* [n,16] */, void* stream);
+
+/* ---- fused tiny MLP (NeRFSmall.forward, run_nerf_helpers.py:265-306, + run_network's
+ *      sigma := 0 outside the bbox, run_nerf.py:66) on fp32 MFMA (v_mfma_f32_32x32x2_f32) -----
+ * Weights are nn.Linear layouts [out][in], no bias: w0 [64,32], w1 [16,64], c0 [64,31],
+ * c1 [64,64], c2 [3,64] (create_nerf's NeRFSmall(num_layers=2, num_layers_color=3)).
+ * Input point p: hash features x[p][k] = d_feat[p*feat_stride_point + (k/2)*feat_stride_level + k%2]
+ * (k < 32); view encoding: if d_viewdirs != NULL, SH4 of d_viewdirs[p / samples_per_ray] is
+ * computed in-kernel, else sh[p][k] = d_sh[p*sh_stride + k] (k < 16).
+ * d_keep may be NULL (keep all). Output d_raw [P,4] = [rgb_raw(3), sigma_raw].
+ */
+typedef struct {
+    const float* w0;
+    const float* w1;
+    const float* c0;
+    const float* c1;
+    const float* c2;
+} nerf_mlp_weights;
+
+typedef struct {
+    float* w0;
+    float* w1;
+    float* c0;
+    float* c1;
+    float* c2;
+} nerf_mlp_grads;
+
+int nerf_mlp_fwd(const float* d_feat, int64_t feat_stride_point, int64_t feat_stride_level,
+                 const float* d_sh, int64_t sh_stride,
+                 const float* d_viewdirs, int64_t samples_per_ray,
+                 const uint8_t* d_keep, int64_t n_points,
+                 const nerf_mlp_weights* weights, float* d_raw, void* stream);
+
+/* Backward: recomputes the forward, then ACCUMULATES weight grads into *grads (atomic adds) and
+ * WRITES d_dfeat (same strides as d_feat; may be NULL) and d_dsh ([P,16], may be NULL). */
+int nerf_mlp_bwd(const float* d_feat, int64_t feat_stride_point, int64_t feat_stride_level,
+                 const float* d_sh, int64_t sh_stride,
+                 const float* d_viewdirs, int64_t samples_per_ray,
+                 const uint8_t* d_keep, int64_t n_points,
+                 const nerf_mlp_weights* weights, const float* d_graw /* [P,4] */,
+                 const nerf_mlp_grads* grads, float* d_dfeat, float* d_dsh, void* stream);
+
+/* ---- volume compositing (raw2outputs, run_nerf.py:347-411), one wavefront per ray ----------
+ * d_raw [R,S,raw_channels] (4, or 7 with normals), d_z [R,S], d_rays_d [R,3] (unnormalised),
+ * d_noise [R,S] added to sigma (NULL = none). Outputs (any may be NULL except d_weights):
+ * rgb [R,3], disp [R], acc [R], weights [R,S], depth [R], entropy [R], normal [R,3].
+ */
+int nerf_composite_fwd(const float* d_raw, int raw_channels, const float* d_z, const float* d_rays_d,
+                       const float* d_noise, int64_t n_rays, int n_samples, int white_bkgd,
+                       float* d_rgb, float* d_disp, float* d_acc, float* d_weights, float* d_depth,
+                       float* d_entropy, float* d_normal, void* stream);
+
+/* Upstream grads (any may be NULL = zero): g_rgb [R,3], g_disp, g_acc [R], g_weights [R,S],
+ * g_depth, g_entropy [R], g_normal [R,3]. Writes d_graw [R,S,raw_channels]. */
+int nerf_composite_bwd(const float* d_raw, int raw_channels, const float* d_z, const float* d_rays_d,
+                       const float* d_noise, int64_t n_rays, int n_samples, int white_bkgd,
+                       const float* d_g_rgb, const float* d_g_disp, const float* d_g_acc,
+                       const float* d_g_weights, const float* d_g_depth, const float* d_g_entropy,
+                       const float* d_g_normal, float* d_graw, void* stream);
+
+/* ---- ray sampling (render_rays, run_nerf.py:460-490) --------------------------------------
+ * d_rays: packed ray batch [R, ray_stride] = [o(3), d(3), near, far, (viewdir(3))] as render()
+ * builds it (run_nerf.py:134-140). d_t: [S] = torch.linspace(0,1,S) values. perturb != 0 jitters
+ * with d_u [R,S] (NULL = Philox(seed, offset)). Writes d_z [R,S] and d_pts [R,S,3] (may be NULL).
+ */
+int nerf_sample_stratified(const float* d_rays, int64_t ray_stride, int64_t n_rays, int n_samples,
+                           const float* d_t, int lindisp, int perturb, const float* d_u,
+                           uint64_t seed, uint64_t offset, float* d_z, float* d_pts, void* stream);
+
+/* sample_pdf (run_nerf_helpers.py:354-397) on bins [R,n_bins], weights [R,n_bins-1];
+ * det: u = d_t_imp (torch.linspace(0,1,N) values, [N]); else u = d_u [R,N] or Philox. */
+int nerf_sample_pdf(const float* d_bins, int64_t bins_stride, const float* d_weights, int64_t weights_stride,
+                    int64_t n_rays, int n_bins, int n_importance, int det, const float* d_t_imp,
+                    const float* d_u, uint64_t seed, uint64_t offset, float* d_samples, void* stream);
+
+/* Hierarchical step of render_rays (run_nerf.py:508-513, :541) in one launch: z_mid of the
+ * coarse z, sample_pdf on weights[...,1:-1], sort(cat(z, z_samples)), fine points, z_std.
+ * Outputs d_z_fine [R,S+N], d_pts_fine [R,S+N,3] (may be NULL), d_z_std [R] (may be NULL),
+ * d_samples [R,N] (may be NULL). */
+int nerf_sample_fine(const float* d_rays, int64_t ray_stride, const float* d_z, const float* d_weights,
+                     int64_t n_rays, int n_samples, int n_importance, int det, const float* d_t_imp,
+                     const float* d_u, uint64_t seed, uint64_t offset,
+                     float* d_z_fine, float* d_pts_fine, float* d_z_std, float* d_samples, void* stream);
+
+/* ---- RAdam (PocketNeRF/radam.py:28-94), one launch over up to 32 tensor segments ----------
+ * Per segment: p, g, m (exp_avg), v (exp_avg_sq) of n elements. The host evaluates the scalar
+ * algebra of radam.py:56-79 in double, exactly as the reference's Python does, and passes the
+ * float32 roundings of the scalars the tensor ops see:
+ *   beta1, beta2            multipliers of exp_avg / exp_avg_sq (mul_(beta))
+ *   one_minus_beta1/2       float(1 - beta)          (add_/addcmul_ value)
+ *   decay_coef              float(-weight_decay*lr)   (0 = no decay)
+ *   step_coef               float(-step_size*lr)
+ *   mode 2: N_sma >= 5 (p += step_coef*m/(sqrt(v)+eps)), 1: step_size > 0 (p += step_coef*m),
+ *   0: moments only.
+ */
+typedef struct {
+    float* p;
+    const float* g;
+    float* m;
+    float* v;
+    int64_t n;
+    float beta1, beta2, one_minus_beta1, one_minus_beta2, eps, decay_coef, step_coef;
+    int mode;
+} nerf_radam_segment;
+
+int nerf_radam_step(const nerf_radam_segment* segs, int n_segs, void* stream);
+
+/* ---- total-variation loss on one hashed cuboid per level (loss.py:11-43) ------------------
+ * min_vertex: host int64[n_levels][3] (the reference draws it with torch.randint);
+ * cube: host int[n_levels] cuboid edge. fwd: d_loss[l] += TV_l (ACCUMULATED; zero it first).
+ * bwd: d_dtables[l] += d(scale_l * TV_l)/d table, scale: host float[n_levels]. */
+int nerf_tv_fwd(const float* const* d_tables, int n_levels, int log2_T, const int64_t* min_vertex,
+                const int* cube, float* d_loss, void* stream);
+int nerf_tv_bwd(const float* const* d_tables, int n_levels, int log2_T, const int64_t* min_vertex,
+                const int* cube, const float* d_scale /* device [n_levels] */, float* const* d_dtables,
+                void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NERF_HIP_H */

@@ -1,0 +1,149 @@
+"""ctypes binding of libnerfhip.so (include/nerf_hip.h).
+
+The product path has no fallback: if the library is missing, cannot be loaded, or a tensor is not a
+contiguous float32 CUDA tensor, the call raises. Kernel errors raise RuntimeError with the
+library's message (nerf_last_error).
+"""
+import ctypes
+import os
+
+import torch  # must be imported before the library so it binds torch's libamdhip64.so.7
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("NERF_HIP_LIB", os.path.join(_HERE, "libnerfhip.so"))
+
+c_f32p = ctypes.POINTER(ctypes.c_float)
+c_i64 = ctypes.c_int64
+c_vp = ctypes.c_void_p
+c_int = ctypes.c_int
+c_u64 = ctypes.c_uint64
+
+MAX_LEVELS = 16
+
+
+class MlpWeights(ctypes.Structure):
+    _fields_ = [(n, c_vp) for n in ("w0", "w1", "c0", "c1", "c2")]
+
+
+class MlpGrads(ctypes.Structure):
+    _fields_ = [(n, c_vp) for n in ("w0", "w1", "c0", "c1", "c2")]
+
+
+class RAdamSegment(ctypes.Structure):
+    _fields_ = [("p", c_vp), ("g", c_vp), ("m", c_vp), ("v", c_vp), ("n", c_i64),
+                ("beta1", ctypes.c_float), ("beta2", ctypes.c_float),
+                ("one_minus_beta1", ctypes.c_float), ("one_minus_beta2", ctypes.c_float),
+                ("eps", ctypes.c_float), ("decay_coef", ctypes.c_float), ("step_coef", ctypes.c_float),
+                ("mode", c_int)]
+
+
+# name -> argtypes (restype is int for all but the two metadata calls)
+SIGNATURES = {
+    "nerf_hash_encode_fwd": [c_vp, c_i64, c_f32p, c_f32p, c_f32p, c_int, c_int, ctypes.POINTER(c_vp),
+                             c_vp, c_i64, c_i64, c_vp, c_vp],
+    "nerf_hash_encode_bwd": [c_vp, c_i64, c_f32p, c_f32p, c_f32p, c_int, c_int, c_vp, c_i64, c_i64,
+                             ctypes.POINTER(c_vp), c_vp],
+    "nerf_sh4_fwd": [c_vp, c_i64, c_vp, c_vp],
+    "nerf_mlp_fwd": [c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, ctypes.POINTER(MlpWeights),
+                     c_vp, c_vp],
+    "nerf_mlp_bwd": [c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, ctypes.POINTER(MlpWeights),
+                     c_vp, ctypes.POINTER(MlpGrads), c_vp, c_vp, c_vp],
+    "nerf_composite_fwd": [c_vp, c_int, c_vp, c_vp, c_vp, c_i64, c_int, c_int,
+                           c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
+    "nerf_composite_bwd": [c_vp, c_int, c_vp, c_vp, c_vp, c_i64, c_int, c_int,
+                           c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
+    "nerf_sample_stratified": [c_vp, c_i64, c_i64, c_int, c_vp, c_int, c_int, c_vp, c_u64, c_u64, c_vp, c_vp, c_vp],
+    "nerf_sample_pdf": [c_vp, c_i64, c_vp, c_i64, c_i64, c_int, c_int, c_int, c_vp, c_vp, c_u64, c_u64, c_vp, c_vp],
+    "nerf_sample_fine": [c_vp, c_i64, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_vp, c_vp, c_u64, c_u64,
+                         c_vp, c_vp, c_vp, c_vp, c_vp],
+    "nerf_radam_step": [ctypes.POINTER(RAdamSegment), c_int, c_vp],
+    "nerf_tv_fwd": [ctypes.POINTER(c_vp), c_int, c_int, ctypes.POINTER(c_i64), ctypes.POINTER(c_int), c_vp, c_vp],
+    "nerf_tv_bwd": [ctypes.POINTER(c_vp), c_int, c_int, ctypes.POINTER(c_i64), ctypes.POINTER(c_int), c_vp,
+                    ctypes.POINTER(c_vp), c_vp],
+}
+
+_lib = None
+
+
+def load():
+    """Load libnerfhip.so once; raise if it is missing (no CPU fallback exists)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"libnerfhip.so not found at {LIB_PATH}: build it with `python -c "
+                           f"'import __graft_entry__ as g; g.build()'` (hipcc, gfx950)")
+    lib = ctypes.CDLL(LIB_PATH)
+    lib.nerf_last_error.restype = ctypes.c_char_p
+    lib.nerf_last_error.argtypes = []
+    lib.nerf_abi_version.restype = c_int
+    lib.nerf_abi_version.argtypes = []
+    for name, argtypes in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = argtypes
+        fn.restype = c_int
+    _lib = lib
+    return lib
+
+
+def exported_symbols():
+    return ["nerf_last_error", "nerf_abi_version"] + list(SIGNATURES)
+
+
+_TIMING = None   # when a list: (name, start_event, end_event) per launch, recorded on the current stream
+
+
+def set_timing(enabled):
+    """Record a pair of HIP events around every kernel call (bench.py's per-kernel timing)."""
+    global _TIMING
+    _TIMING = [] if enabled else None
+
+
+def timing_records():
+    return _TIMING or []
+
+
+def call(name, *args):
+    lib = load()
+    if _TIMING is not None:
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record()
+        rc = getattr(lib, name)(*args)
+        ev1.record()
+        _TIMING.append((name, ev0, ev1))
+    else:
+        rc = getattr(lib, name)(*args)
+    if rc != 0:
+        msg = lib.nerf_last_error().decode(errors="replace")
+        raise RuntimeError(f"{name} failed (code {rc}): {msg}")
+
+
+def stream():
+    return c_vp(torch.cuda.current_stream().cuda_stream)
+
+
+def ptr(t, name="tensor", dtype=torch.float32, allow_none=False):
+    """Device pointer of a contiguous CUDA tensor of the given dtype (None -> NULL if allowed)."""
+    if t is None:
+        if allow_none:
+            return None
+        raise ValueError(f"{name} must not be None")
+    if not t.is_cuda:
+        raise RuntimeError(f"{name}: indoor_nerf_amd kernels need CUDA (ROCm) tensors, got device {t.device}")
+    if t.dtype != dtype:
+        raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: tensor must be contiguous")
+    return c_vp(t.data_ptr())
+
+
+def host_f32(values):
+    arr = (ctypes.c_float * len(values))(*[float(v) for v in values])
+    return arr
+
+
+def ptr_array(tensors, name="tables"):
+    arr = (c_vp * len(tensors))()
+    for i, t in enumerate(tensors):
+        arr[i] = ptr(t, f"{name}[{i}]").value
+    return arr

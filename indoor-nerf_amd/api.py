@@ -1,0 +1,22 @@
+"""Public API of indoor_nerf_amd: the reference's render_rays-path names (PocketNeRF/run_nerf.py,
+run_nerf_helpers.py, hash_encoding.py, radam.py, loss.py) backed by libnerfhip."""
+from . import _lib
+from .dist import GradArena, broadcast_params, init_process_group, shard
+from .field import NeRFSmall, batchify, run_network
+from .hashgrid import HashEmbedder, SHEncoder, level_resolutions
+from .losses import sigma_sparsity_loss, total_variation_all, total_variation_loss
+from .model import create_nerf, make_args, save_checkpoint, train_step
+from .optim import RAdam
+from .render import (batchify_rays, get_rays, get_rays_np, img2mse, manual_seed, mse2psnr, ndc_rays, raw2outputs,
+                     render, render_rays, sample_pdf, to8b)
+
+__all__ = ["HashEmbedder", "SHEncoder", "NeRFSmall", "RAdam", "run_network", "batchify", "batchify_rays", "render",
+           "render_rays", "raw2outputs", "sample_pdf", "get_rays", "get_rays_np", "ndc_rays", "img2mse", "mse2psnr",
+           "to8b", "create_nerf", "make_args", "save_checkpoint", "train_step", "total_variation_loss",
+           "total_variation_all", "sigma_sparsity_loss", "level_resolutions", "GradArena", "init_process_group",
+           "shard", "broadcast_params", "manual_seed", "load_library"]
+
+
+def load_library():
+    """Load libnerfhip.so (raises if it is missing)."""
+    return _lib.load()

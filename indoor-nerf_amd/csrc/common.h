@@ -1,0 +1,98 @@
+// Shared device/host helpers for libnerfhip (gfx950, wave64). Not part of the public ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#include "../../include/nerf_hip.h"
+
+namespace nerf {
+
+// ---------------------------------------------------------------- host-side error reporting
+void set_error(const char* fmt, ...);
+
+#define NERF_REQUIRE(cond, ...)                 \
+    do {                                        \
+        if (!(cond)) {                          \
+            ::nerf::set_error(__VA_ARGS__);     \
+            return NERF_E_ARG;                  \
+        }                                       \
+    } while (0)
+
+#define NERF_CHECK_LAUNCH(what)                                                             \
+    do {                                                                                    \
+        hipError_t e_ = hipGetLastError();                                                  \
+        if (e_ != hipSuccess) {                                                             \
+            ::nerf::set_error("%s: %s", what, hipGetErrorString(e_));                       \
+            return NERF_E_LAUNCH;                                                           \
+        }                                                                                   \
+    } while (0)
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+constexpr int kWave = 64;
+
+inline unsigned blocks_for(int64_t n, int threads) {
+    return (unsigned)((n + threads - 1) / threads);
+}
+
+// ---------------------------------------------------------------- device helpers
+// Philox4x32-10 (Salmon et al. 2011): counter = (index lo, index hi, offset lo, offset hi),
+// key = seed. Returns 4 uniforms in [0,1) with 24-bit resolution.
+struct U4 { float x, y, z, w; };
+
+__device__ __forceinline__ uint32_t mulhilo(uint32_t a, uint32_t b, uint32_t& hi) {
+    uint64_t p = (uint64_t)a * (uint64_t)b;
+    hi = (uint32_t)(p >> 32);
+    return (uint32_t)p;
+}
+
+__device__ __forceinline__ U4 philox_uniform4(uint64_t seed, uint64_t offset, uint64_t index) {
+    uint32_t c0 = (uint32_t)index, c1 = (uint32_t)(index >> 32);
+    uint32_t c2 = (uint32_t)offset, c3 = (uint32_t)(offset >> 32);
+    uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        uint32_t hi0, hi1;
+        uint32_t lo0 = mulhilo(0xD2511F53u, c0, hi0);
+        uint32_t lo1 = mulhilo(0xCD9E8D57u, c2, hi1);
+        uint32_t n0 = hi1 ^ c1 ^ k0, n1 = lo1, n2 = hi0 ^ c3 ^ k1, n3 = lo0;
+        c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    const float s = 1.0f / 16777216.0f;
+    return U4{(c0 >> 8) * s, (c1 >> 8) * s, (c2 >> 8) * s, (c3 >> 8) * s};
+}
+
+__device__ __forceinline__ float philox_uniform(uint64_t seed, uint64_t offset, uint64_t index) {
+    U4 u = philox_uniform4(seed, offset, index >> 2);
+    switch (index & 3) {
+        case 0: return u.x;
+        case 1: return u.y;
+        case 2: return u.z;
+        default: return u.w;
+    }
+}
+
+// Spatial hash of utils.py:13-24 for 3-D integer corners (uint32 wrap == the reference's int64
+// arithmetic modulo the 2^log2_T mask).
+__device__ __forceinline__ uint32_t spatial_hash3(uint32_t x, uint32_t y, uint32_t z, uint32_t mask) {
+    return (x * 1u ^ y * 2654435761u ^ z * 805459861u) & mask;
+}
+
+// Wave64 reductions / scans through DPP-capable shuffles.
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+}  // namespace nerf

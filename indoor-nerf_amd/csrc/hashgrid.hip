@@ -1,0 +1,232 @@
+// Multi-resolution hash grid: forward gather + trilinear, backward scatter-add.
+//
+// Restates, per (point, level), the reference's eager-op chain
+//   get_voxel_vertices  PocketNeRF/utils.py:95-117  (keep mask, clamp, cell, floor, corners)
+//   hash                PocketNeRF/utils.py:13-24   (x*1 ^ y*2654435761 ^ z*805459861, masked)
+//   nn.Embedding gather PocketNeRF/hash_encoding.py:94
+//   trilinear_interp    PocketNeRF/hash_encoding.py:56-80 (x, then y, then z blends)
+// in one thread, with the reference's op order and no contraction (-ffp-contract=off), so indices,
+// keep mask and features are bit-identical to the fp32 reference.
+//
+// Launch geometry: grid (ceil(P/256), L). Blocks are dispatched x-fastest, so at any moment the
+// whole chip works on one or two levels and each XCD's 4 MiB L2 holds the level's table lines
+// that the current point range touches (tables are 4 MiB per level at log2_T = 19).
+#include "common.h"
+
+namespace nerf {
+
+struct HashParams {
+    const float* tables[NERF_MAX_LEVELS];
+    float res[NERF_MAX_LEVELS];
+    float bmin[3];
+    float bmax[3];
+    uint32_t mask;
+};
+
+struct HashGradParams {
+    float* dtables[NERF_MAX_LEVELS];
+    float res[NERF_MAX_LEVELS];
+    float bmin[3];
+    float bmax[3];
+    uint32_t mask;
+};
+
+// Per-axis voxel math of utils.py:103-112, fp32, exact op order.
+struct AxisCell {
+    int base;      // bottom_left_idx
+    float w;       // (x - vmin) / (vmax - vmin), on the UNclamped x (hash_encoding.py:64)
+    bool inside;   // x == max(min(x, bmax), bmin)
+};
+
+__device__ __forceinline__ AxisCell axis_cell(float x, float lo, float hi, float res) {
+    AxisCell a;
+    a.inside = (x == fmaxf(fminf(x, hi), lo));
+    float xc = fminf(fmaxf(x, lo), hi);            // torch.clamp(min=lo, max=hi)
+    float cell = (hi - lo) / res;                  // grid_size
+    a.base = (int)floorf((xc - lo) / cell);        // floor(...).int()
+    float vmin = (float)a.base * cell + lo;        // bottom_left_idx*grid_size + box_min
+    float vmax = vmin + cell;                      // + 1.0*grid_size
+    a.w = (x - vmin) / (vmax - vmin);
+    return a;
+}
+
+__global__ void __launch_bounds__(256) hash_encode_fwd_kernel(
+    const float* __restrict__ xyz, int64_t n, HashParams hp,
+    float* __restrict__ feat, int64_t sp, int64_t sl, uint8_t* __restrict__ keep) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int lvl = blockIdx.y;
+    if (p >= n) return;
+    const float x = xyz[3 * p + 0], y = xyz[3 * p + 1], z = xyz[3 * p + 2];
+    const float res = hp.res[lvl];
+    const AxisCell ax = axis_cell(x, hp.bmin[0], hp.bmax[0], res);
+    const AxisCell ay = axis_cell(y, hp.bmin[1], hp.bmax[1], res);
+    const AxisCell az = axis_cell(z, hp.bmin[2], hp.bmax[2], res);
+    if (lvl == 0 && keep) keep[p] = (ax.inside && ay.inside && az.inside) ? 1 : 0;
+
+    const float2* __restrict__ tab = reinterpret_cast<const float2*>(hp.tables[lvl]);
+    const uint32_t bx = (uint32_t)ax.base, by = (uint32_t)ay.base, bz = (uint32_t)az.base;
+    // corner c = 4i + 2j + k  <->  offset (i, j, k)  (utils.py:9)
+    float2 e[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        const uint32_t h = spatial_hash3(bx + ((c >> 2) & 1), by + ((c >> 1) & 1), bz + (c & 1), hp.mask);
+        e[c] = tab[h];
+    }
+    const float wx = ax.w, wy = ay.w, wz = az.w;
+    const float ox = 1.0f - wx, oy = 1.0f - wy, oz = 1.0f - wz;
+    float2 out;
+#define NERF_TRI(F)                                                   \
+    {                                                                 \
+        const float c00 = e[0].F * ox + e[4].F * wx;                  \
+        const float c01 = e[1].F * ox + e[5].F * wx;                  \
+        const float c10 = e[2].F * ox + e[6].F * wx;                  \
+        const float c11 = e[3].F * ox + e[7].F * wx;                  \
+        const float c0 = c00 * oy + c10 * wy;                         \
+        const float c1 = c01 * oy + c11 * wy;                         \
+        out.F = c0 * oz + c1 * wz;                                    \
+    }
+    NERF_TRI(x)
+    NERF_TRI(y)
+#undef NERF_TRI
+    float* dst = feat + p * sp + (int64_t)lvl * sl;
+    if (((sp | sl) & 1) == 0) {
+        *reinterpret_cast<float2*>(dst) = out;
+    } else {
+        dst[0] = out.x;
+        dst[1] = out.y;
+    }
+}
+
+// Backward: dL/de_c = ((g*(1-wz or wz))*(1-wy or wy))*(1-wx or wx), the order autograd applies the
+// three blend steps in reverse; scatter-added with fp32 atomics (no-return global_atomic_add_f32).
+// Consecutive threads are consecutive samples of one ray: at coarse levels they usually share the
+// voxel, so a thread first merges runs of equal voxels inside its wave (see below).
+__device__ __forceinline__ void atomic_add_f32(float* p, float v) {
+    __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ void __launch_bounds__(256) hash_encode_bwd_kernel(
+    const float* __restrict__ xyz, int64_t n, HashGradParams hp,
+    const float* __restrict__ dfeat, int64_t sp, int64_t sl) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int lvl = blockIdx.y;
+    const bool valid = p < n;
+    float x = 0.f, y = 0.f, z = 0.f, gx = 0.f, gy = 0.f;
+    if (valid) {
+        x = xyz[3 * p + 0]; y = xyz[3 * p + 1]; z = xyz[3 * p + 2];
+        const float* src = dfeat + p * sp + (int64_t)lvl * sl;
+        gx = src[0];
+        gy = src[1];
+    }
+    const float res = hp.res[lvl];
+    const AxisCell ax = axis_cell(x, hp.bmin[0], hp.bmax[0], res);
+    const AxisCell ay = axis_cell(y, hp.bmin[1], hp.bmax[1], res);
+    const AxisCell az = axis_cell(z, hp.bmin[2], hp.bmax[2], res);
+    const float wx = ax.w, wy = ay.w, wz = az.w;
+    const float ox = 1.0f - wx, oy = 1.0f - wy, oz = 1.0f - wz;
+
+    // Per-corner contributions, corner c = 4i+2j+k.
+    float cgx[8], cgy[8];
+    {
+        const float b0x = gx * oz, b1x = gx * wz, b0y = gy * oz, b1y = gy * wz;  // d c0, d c1
+        const float a00x = b0x * oy, a10x = b0x * wy, a01x = b1x * oy, a11x = b1x * wy;
+        const float a00y = b0y * oy, a10y = b0y * wy, a01y = b1y * oy, a11y = b1y * wy;
+        // c00 <- e0,e4 ; c01 <- e1,e5 ; c10 <- e2,e6 ; c11 <- e3,e7
+        cgx[0] = a00x * ox; cgx[4] = a00x * wx; cgy[0] = a00y * ox; cgy[4] = a00y * wx;
+        cgx[1] = a01x * ox; cgx[5] = a01x * wx; cgy[1] = a01y * ox; cgy[5] = a01y * wx;
+        cgx[2] = a10x * ox; cgx[6] = a10x * wx; cgy[2] = a10y * ox; cgy[6] = a10y * wx;
+        cgx[3] = a11x * ox; cgx[7] = a11x * wx; cgy[3] = a11y * ox; cgy[7] = a11y * wx;
+    }
+
+    // Wave-level run merge: a voxel key equal to the previous lane's continues a run; segmented
+    // inclusive sums (Hillis-Steele over 64 lanes) leave each run's total on its LAST lane, which
+    // alone issues the 16 atomics. Lanes of different runs never mix.
+    const uint32_t key_lo = (uint32_t)ax.base | ((uint32_t)ay.base << 16);
+    const uint32_t key_hi = (uint32_t)az.base | (valid ? 0u : 0x80000000u);
+    const int lane = threadIdx.x & 63;
+    const uint32_t prev_lo = __shfl_up(key_lo, 1, 64), prev_hi = __shfl_up(key_hi, 1, 64);
+    const bool head = (lane == 0) || prev_lo != key_lo || prev_hi != key_hi;
+    // run start lane index, propagated by a max-scan of head positions
+    int start = head ? lane : 0;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int s = __shfl_up(start, o, 64);
+        if (lane >= o) start = max(start, s);
+    }
+    const uint32_t next_lo = __shfl_down(key_lo, 1, 64), next_hi = __shfl_down(key_hi, 1, 64);
+    const bool tail = (lane == 63) || next_lo != key_lo || next_hi != key_hi;
+    const uint64_t ballot_multi = __ballot(!head);
+    if (ballot_multi != 0) {  // some run has length > 1 in this wave: segmented sums
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const bool take = (lane - o) >= start;
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                const float vx = __shfl_up(cgx[c], o, 64);
+                const float vy = __shfl_up(cgy[c], o, 64);
+                if (take) { cgx[c] += vx; cgy[c] += vy; }
+            }
+        }
+    }
+    if (!valid || !tail) return;
+    float* tab = hp.dtables[lvl];
+    const uint32_t bx = (uint32_t)ax.base, by = (uint32_t)ay.base, bz = (uint32_t)az.base;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        const uint32_t h = spatial_hash3(bx + ((c >> 2) & 1), by + ((c >> 1) & 1), bz + (c & 1), hp.mask);
+        atomic_add_f32(tab + 2 * h + 0, cgx[c]);
+        atomic_add_f32(tab + 2 * h + 1, cgy[c]);
+    }
+}
+
+}  // namespace nerf
+
+using namespace nerf;
+
+extern "C" int nerf_hash_encode_fwd(const float* d_xyz, int64_t n_points, const float* bbox_min3,
+                                    const float* bbox_max3, const float* level_res, int n_levels, int log2_T,
+                                    const float* const* d_tables, float* d_feat, int64_t feat_stride_point,
+                                    int64_t feat_stride_level, uint8_t* d_keep, void* stream) {
+    NERF_REQUIRE(n_points >= 0, "hash_encode_fwd: n_points < 0");
+    NERF_REQUIRE(n_levels >= 1 && n_levels <= NERF_MAX_LEVELS, "hash_encode_fwd: n_levels %d", n_levels);
+    NERF_REQUIRE(log2_T >= 1 && log2_T <= 30, "hash_encode_fwd: log2_T %d", log2_T);
+    NERF_REQUIRE(d_xyz && d_feat && d_tables && level_res && bbox_min3 && bbox_max3, "hash_encode_fwd: null arg");
+    if (n_points == 0) return NERF_OK;
+    HashParams hp{};
+    for (int l = 0; l < n_levels; ++l) {
+        NERF_REQUIRE(d_tables[l], "hash_encode_fwd: table %d is null", l);
+        hp.tables[l] = d_tables[l];
+        hp.res[l] = level_res[l];
+    }
+    for (int a = 0; a < 3; ++a) { hp.bmin[a] = bbox_min3[a]; hp.bmax[a] = bbox_max3[a]; }
+    hp.mask = (uint32_t)((1u << log2_T) - 1u);
+    dim3 grid(blocks_for(n_points, 256), n_levels);
+    hipLaunchKernelGGL(hash_encode_fwd_kernel, grid, dim3(256), 0, as_stream(stream), d_xyz, n_points, hp,
+                       d_feat, feat_stride_point, feat_stride_level, d_keep);
+    NERF_CHECK_LAUNCH("hash_encode_fwd");
+    return NERF_OK;
+}
+
+extern "C" int nerf_hash_encode_bwd(const float* d_xyz, int64_t n_points, const float* bbox_min3,
+                                    const float* bbox_max3, const float* level_res, int n_levels, int log2_T,
+                                    const float* d_dfeat, int64_t feat_stride_point, int64_t feat_stride_level,
+                                    float* const* d_dtables, void* stream) {
+    NERF_REQUIRE(n_points >= 0, "hash_encode_bwd: n_points < 0");
+    NERF_REQUIRE(n_levels >= 1 && n_levels <= NERF_MAX_LEVELS, "hash_encode_bwd: n_levels %d", n_levels);
+    NERF_REQUIRE(log2_T >= 1 && log2_T <= 30, "hash_encode_bwd: log2_T %d", log2_T);
+    NERF_REQUIRE(d_xyz && d_dfeat && d_dtables && level_res && bbox_min3 && bbox_max3, "hash_encode_bwd: null arg");
+    if (n_points == 0) return NERF_OK;
+    HashGradParams hp{};
+    for (int l = 0; l < n_levels; ++l) {
+        NERF_REQUIRE(d_dtables[l], "hash_encode_bwd: grad table %d is null", l);
+        hp.dtables[l] = d_dtables[l];
+        hp.res[l] = level_res[l];
+    }
+    for (int a = 0; a < 3; ++a) { hp.bmin[a] = bbox_min3[a]; hp.bmax[a] = bbox_max3[a]; }
+    hp.mask = (uint32_t)((1u << log2_T) - 1u);
+    dim3 grid(blocks_for(n_points, 256), n_levels);
+    hipLaunchKernelGGL(hash_encode_bwd_kernel, grid, dim3(256), 0, as_stream(stream), d_xyz, n_points, hp,
+                       d_dfeat, feat_stride_point, feat_stride_level);
+    NERF_CHECK_LAUNCH("hash_encode_bwd");
+    return NERF_OK;
+}

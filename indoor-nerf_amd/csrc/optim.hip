@@ -1,0 +1,220 @@
+// Fused RAdam step (PocketNeRF/radam.py:28-94) over a list of tensor segments in ONE launch, and
+// the total-variation loss on one hashed cuboid per level (PocketNeRF/loss.py:11-43).
+#include "common.h"
+
+namespace nerf {
+
+constexpr int kMaxSegs = 32;
+constexpr int kRAdamVec = 4;
+constexpr int kRAdamThreads = 256;
+
+struct RAdamSegs {
+    nerf_radam_segment seg[kMaxSegs];
+    int64_t block_start[kMaxSegs + 1];   // first block of each segment
+    int n;
+};
+
+// Elementwise, in the reference's op order (compiled with -ffp-contract=off):
+//   v = v*b2 + ((1-b2)*g)*g            exp_avg_sq.mul_(beta2).addcmul_(1 - beta2, grad, grad)
+//   m = m*b1 + (1-b1)*g                exp_avg.mul_(beta1).add_(1 - beta1, grad)
+//   p = p + (-wd*lr)*p                 weight decay (when wd != 0)
+//   p = p + ((-step*lr)*m)/(sqrt(v)+eps)   addcdiv_ (mode 2), or p + (-step*lr)*m (mode 1)
+__device__ __forceinline__ void radam_elem(const nerf_radam_segment& s, float& p, float g, float& m, float& v) {
+    v = v * s.beta2 + (s.one_minus_beta2 * g) * g;
+    m = m * s.beta1 + s.one_minus_beta1 * g;
+    if (s.mode == 0) return;
+    if (s.decay_coef != 0.f) p = p + s.decay_coef * p;
+    if (s.mode == 2) p = p + (s.step_coef * m) / (sqrtf(v) + s.eps);
+    else p = p + s.step_coef * m;
+}
+
+__global__ void __launch_bounds__(kRAdamThreads) radam_kernel(RAdamSegs S) {
+    const int64_t b = blockIdx.x;
+    int si = 0;
+    while (si + 1 < S.n && b >= S.block_start[si + 1]) ++si;
+    const nerf_radam_segment& s = S.seg[si];
+    const int64_t i0 = ((b - S.block_start[si]) * kRAdamThreads + threadIdx.x) * kRAdamVec;
+    if (i0 >= s.n) return;
+    const bool aligned = ((reinterpret_cast<uintptr_t>(s.p) | reinterpret_cast<uintptr_t>(s.g) |
+                           reinterpret_cast<uintptr_t>(s.m) | reinterpret_cast<uintptr_t>(s.v)) & 15) == 0;
+    if (aligned && i0 + kRAdamVec <= s.n) {
+        float4 p = *reinterpret_cast<const float4*>(s.p + i0);
+        const float4 g = *reinterpret_cast<const float4*>(s.g + i0);
+        float4 m = *reinterpret_cast<const float4*>(s.m + i0);
+        float4 v = *reinterpret_cast<const float4*>(s.v + i0);
+        radam_elem(s, p.x, g.x, m.x, v.x);
+        radam_elem(s, p.y, g.y, m.y, v.y);
+        radam_elem(s, p.z, g.z, m.z, v.z);
+        radam_elem(s, p.w, g.w, m.w, v.w);
+        *reinterpret_cast<float4*>(s.m + i0) = m;
+        *reinterpret_cast<float4*>(s.v + i0) = v;
+        if (s.mode != 0) *reinterpret_cast<float4*>(s.p + i0) = p;
+    } else {
+        for (int64_t i = i0; i < i0 + kRAdamVec && i < s.n; ++i) {
+            float p = s.p[i], m = s.m[i], v = s.v[i];
+            radam_elem(s, p, s.g[i], m, v);
+            s.m[i] = m;
+            s.v[i] = v;
+            if (s.mode != 0) s.p[i] = p;
+        }
+    }
+}
+
+// ---------------------------------------------------------------- TV loss
+struct TVParams {
+    const float* tables[NERF_MAX_LEVELS];
+    float* dtables[NERF_MAX_LEVELS];
+    int mv[NERF_MAX_LEVELS][3];
+    int cube[NERF_MAX_LEVELS];
+    int64_t vstart[NERF_MAX_LEVELS + 1];   // first vertex of each level in the flattened launch
+    int L;
+    uint32_t mask;
+    const float* scale;   // bwd: device [L] upstream gradient per level
+    float* loss;          // fwd: device [L]
+};
+
+__device__ __forceinline__ int tv_level(const TVParams& P, int64_t v) {
+    int l = 0;
+    while (l + 1 < P.L && v >= P.vstart[l + 1]) ++l;
+    return l;
+}
+
+__device__ __forceinline__ float2 tv_fetch(const float2* tab, const int* mv, int i, int j, int k, uint32_t mask) {
+    return tab[spatial_hash3((uint32_t)(mv[0] + i), (uint32_t)(mv[1] + j), (uint32_t)(mv[2] + k), mask)];
+}
+
+// cube vertex (i,j,k) = min_vertex + (i,j,k) in meshgrid 'ij' order (loss.py:25-27)
+__global__ void __launch_bounds__(256) tv_fwd_kernel(TVParams P) {
+    const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t total = P.vstart[P.L];
+    float part = 0.f;
+    int l = 0;
+    if (v < total) {
+        l = tv_level(P, v);
+        const int c = P.cube[l], n1 = c + 1;
+        const int64_t lv = v - P.vstart[l];
+        const int i = (int)(lv / (n1 * n1)), j = (int)((lv / n1) % n1), k = (int)(lv % n1);
+        const float2* tab = reinterpret_cast<const float2*>(P.tables[l]);
+        const float2 e = tv_fetch(tab, P.mv[l], i, j, k, P.mask);
+        if (i < c) { const float2 f = tv_fetch(tab, P.mv[l], i + 1, j, k, P.mask); const float dx = f.x - e.x, dy = f.y - e.y; part += dx * dx + dy * dy; }
+        if (j < c) { const float2 f = tv_fetch(tab, P.mv[l], i, j + 1, k, P.mask); const float dx = f.x - e.x, dy = f.y - e.y; part += dx * dx + dy * dy; }
+        if (k < c) { const float2 f = tv_fetch(tab, P.mv[l], i, j, k + 1, P.mask); const float dx = f.x - e.x, dy = f.y - e.y; part += dx * dx + dy * dy; }
+        part = part / (float)c;
+    }
+    // A wave may straddle two levels: reduce across the wave when it does not, else add per lane.
+    const int lane = threadIdx.x & 63;
+    const int l0 = __shfl(l, 0, 64);
+    const bool uniform = __all(l == l0 || v >= total);
+    if (uniform) {
+        const float s = wave_sum(part);
+        if (lane == 0 && s != 0.f) atomicAdd(P.loss + l0, s);
+    } else if (v < total && part != 0.f) {
+        atomicAdd(P.loss + l, part);
+    }
+}
+
+__global__ void __launch_bounds__(256) tv_bwd_kernel(TVParams P) {
+    const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= P.vstart[P.L]) return;
+    const int l = tv_level(P, v);
+    const int c = P.cube[l], n1 = c + 1;
+    const int64_t lv = v - P.vstart[l];
+    const int i = (int)(lv / (n1 * n1)), j = (int)((lv / n1) % n1), k = (int)(lv % n1);
+    const float2* tab = reinterpret_cast<const float2*>(P.tables[l]);
+    const float2 e = tv_fetch(tab, P.mv[l], i, j, k, P.mask);
+    float gx = 0.f, gy = 0.f;   // sum over pairs of d/de_v of (e_hi - e_lo)^2
+#define NERF_TV_PAIR(cond_lo, di, dj, dk, sign)                                                        \
+    if (cond_lo) {                                                                                      \
+        const float2 f = tv_fetch(tab, P.mv[l], i + (di), j + (dj), k + (dk), P.mask);                \
+        gx += (sign) * 2.0f * (e.x - f.x);                                                              \
+        gy += (sign) * 2.0f * (e.y - f.y);                                                              \
+    }
+    NERF_TV_PAIR(i > 0, -1, 0, 0, 1.0f)
+    NERF_TV_PAIR(i < c, 1, 0, 0, 1.0f)
+    NERF_TV_PAIR(j > 0, 0, -1, 0, 1.0f)
+    NERF_TV_PAIR(j < c, 0, 1, 0, 1.0f)
+    NERF_TV_PAIR(k > 0, 0, 0, -1, 1.0f)
+    NERF_TV_PAIR(k < c, 0, 0, 1, 1.0f)
+#undef NERF_TV_PAIR
+    const float s = P.scale[l] / (float)c;
+    const uint32_t h = spatial_hash3((uint32_t)(P.mv[l][0] + i), (uint32_t)(P.mv[l][1] + j),
+                                     (uint32_t)(P.mv[l][2] + k), P.mask);
+    float* dt = P.dtables[l];
+    __hip_atomic_fetch_add(dt + 2 * h + 0, gx * s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(dt + 2 * h + 1, gy * s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+static int fill_tv(TVParams& P, int n_levels, int log2_T, const int64_t* min_vertex, const int* cube) {
+    NERF_REQUIRE(n_levels >= 1 && n_levels <= NERF_MAX_LEVELS, "tv: n_levels %d", n_levels);
+    NERF_REQUIRE(log2_T >= 1 && log2_T <= 30, "tv: log2_T %d", log2_T);
+    NERF_REQUIRE(min_vertex && cube, "tv: null arg");
+    P.L = n_levels;
+    P.mask = (uint32_t)((1u << log2_T) - 1u);
+    P.vstart[0] = 0;
+    for (int l = 0; l < n_levels; ++l) {
+        NERF_REQUIRE(cube[l] >= 1 && cube[l] <= 1024, "tv: cube[%d] = %d", l, cube[l]);
+        for (int a = 0; a < 3; ++a) P.mv[l][a] = (int)min_vertex[3 * l + a];
+        P.cube[l] = cube[l];
+        const int64_t n1 = cube[l] + 1;
+        P.vstart[l + 1] = P.vstart[l] + n1 * n1 * n1;
+    }
+    return NERF_OK;
+}
+
+}  // namespace nerf
+
+using namespace nerf;
+
+extern "C" int nerf_radam_step(const nerf_radam_segment* segs, int n_segs, void* stream) {
+    NERF_REQUIRE(segs && n_segs >= 0 && n_segs <= kMaxSegs, "radam_step: n_segs %d (max %d)", n_segs, kMaxSegs);
+    RAdamSegs S{};
+    S.n = 0;
+    int64_t blocks = 0;
+    for (int i = 0; i < n_segs; ++i) {
+        if (segs[i].n <= 0) continue;
+        NERF_REQUIRE(segs[i].p && segs[i].g && segs[i].m && segs[i].v, "radam_step: segment %d has a null pointer", i);
+        NERF_REQUIRE(segs[i].mode >= 0 && segs[i].mode <= 2, "radam_step: segment %d mode %d", i, segs[i].mode);
+        S.seg[S.n] = segs[i];
+        S.block_start[S.n] = blocks;
+        blocks += (segs[i].n + (int64_t)kRAdamThreads * kRAdamVec - 1) / ((int64_t)kRAdamThreads * kRAdamVec);
+        S.n++;
+    }
+    S.block_start[S.n] = blocks;
+    if (blocks == 0) return NERF_OK;
+    hipLaunchKernelGGL(radam_kernel, dim3((unsigned)blocks), dim3(kRAdamThreads), 0, as_stream(stream), S);
+    NERF_CHECK_LAUNCH("radam_step");
+    return NERF_OK;
+}
+
+extern "C" int nerf_tv_fwd(const float* const* d_tables, int n_levels, int log2_T, const int64_t* min_vertex,
+                           const int* cube, float* d_loss, void* stream) {
+    TVParams P{};
+    int rc = fill_tv(P, n_levels, log2_T, min_vertex, cube);
+    if (rc) return rc;
+    NERF_REQUIRE(d_tables && d_loss, "tv_fwd: null arg");
+    for (int l = 0; l < n_levels; ++l) {
+        NERF_REQUIRE(d_tables[l], "tv_fwd: table %d null", l);
+        P.tables[l] = d_tables[l];
+    }
+    P.loss = d_loss;
+    hipLaunchKernelGGL(tv_fwd_kernel, dim3(blocks_for(P.vstart[n_levels], 256)), dim3(256), 0, as_stream(stream), P);
+    NERF_CHECK_LAUNCH("tv_fwd");
+    return NERF_OK;
+}
+
+extern "C" int nerf_tv_bwd(const float* const* d_tables, int n_levels, int log2_T, const int64_t* min_vertex,
+                           const int* cube, const float* d_scale, float* const* d_dtables, void* stream) {
+    TVParams P{};
+    int rc = fill_tv(P, n_levels, log2_T, min_vertex, cube);
+    if (rc) return rc;
+    NERF_REQUIRE(d_tables && d_dtables && d_scale, "tv_bwd: null arg");
+    for (int l = 0; l < n_levels; ++l) {
+        NERF_REQUIRE(d_tables[l] && d_dtables[l], "tv_bwd: table %d null", l);
+        P.tables[l] = d_tables[l];
+        P.dtables[l] = d_dtables[l];
+    }
+    P.scale = d_scale;
+    hipLaunchKernelGGL(tv_bwd_kernel, dim3(blocks_for(P.vstart[n_levels], 256)), dim3(256), 0, as_stream(stream), P);
+    NERF_CHECK_LAUNCH("tv_bwd");
+    return NERF_OK;
+}

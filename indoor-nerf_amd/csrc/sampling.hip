@@ -1,0 +1,248 @@
+// Ray sampling of render_rays: stratified depths (PocketNeRF/run_nerf.py:466-490) and the
+// hierarchical step (run_nerf.py:508-513 + sample_pdf, run_nerf_helpers.py:354-397 + z_std :541).
+#include "common.h"
+
+namespace nerf {
+
+struct StratArgs {
+    const float* rays; int64_t stride; int64_t R; int S;
+    const float* t; int lindisp; int perturb; const float* u; uint64_t seed, offset;
+    float* z; float* pts;
+};
+
+__device__ __forceinline__ float base_depth(float near, float far, float t, int lindisp) {
+    if (!lindisp) return near * (1.0f - t) + far * t;
+    return 1.0f / ((1.0f / near) * (1.0f - t) + (1.0f / far) * t);
+}
+
+__global__ void __launch_bounds__(256) sample_stratified_kernel(StratArgs a) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.R * a.S) return;
+    const int64_t r = i / a.S;
+    const int j = (int)(i - r * a.S);
+    const float* ray = a.rays + r * a.stride;
+    const float near = ray[6], far = ray[7];
+    float z = base_depth(near, far, a.t[j], a.lindisp);
+    if (a.perturb) {
+        const float zl = j > 0 ? base_depth(near, far, a.t[j - 1], a.lindisp) : 0.f;
+        const float zh = j + 1 < a.S ? base_depth(near, far, a.t[j + 1], a.lindisp) : 0.f;
+        const float upper = j + 1 < a.S ? 0.5f * (zh + z) : z;
+        const float lower = j > 0 ? 0.5f * (z + zl) : z;
+        const float u = a.u ? a.u[i] : philox_uniform(a.seed, a.offset, (uint64_t)i);
+        z = lower + (upper - lower) * u;
+    }
+    a.z[i] = z;
+    if (a.pts) {
+        a.pts[3 * i + 0] = ray[0] + ray[3] * z;
+        a.pts[3 * i + 1] = ray[1] + ray[4] * z;
+        a.pts[3 * i + 2] = ray[2] + ray[5] * z;
+    }
+}
+
+// ---------------------------------------------------------------- inverse-CDF sampling
+constexpr int kMaxBins = 256;        // coarse samples per ray
+constexpr int kMaxMerged = 1024;     // coarse + importance samples per ray
+
+struct PdfArgs {
+    // source of bins / weights: either explicit arrays (sample_pdf API) or the coarse z/weights
+    const float* bins; int64_t bins_stride;
+    const float* w; int64_t w_stride;
+    int64_t R; int nb;                 // nb = number of bins (cdf entries)
+    int N; int det; const float* t_imp; const float* u; uint64_t seed, offset;
+    float* samples;
+    // fine mode
+    const float* rays; int64_t ray_stride; const float* z; int S;
+    float* z_fine; float* pts_fine; float* z_std;
+};
+
+// Build the CDF of weights (+1e-5, normalised, cumsum in fp64 as the CPU reference does) in LDS and
+// invert it for the wave's ray. bins_l / cdf_l are this wave's LDS slices; w_at(i) gives weight i.
+template <typename WAt>
+__device__ __forceinline__ void build_cdf(int nb, WAt w_at, float* cdf_l, int lane) {
+    const int nw = nb - 1;
+    // sum of (w + 1e-5)
+    double part = 0.0;
+    for (int i = lane; i < nw; i += 64) part += (double)(w_at(i) + 1e-5f);
+    const float wsum = (float)wave_sum_d(part);
+    // contiguous chunk per lane for the prefix sum
+    const int per = (nw + 63) / 64;
+    const int i0 = lane * per;
+    double loc = 0.0;
+    for (int k = 0; k < per; ++k) {
+        const int i = i0 + k;
+        if (i < nw) loc += (double)((w_at(i) + 1e-5f) / wsum);
+    }
+    double incl = loc;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const double y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+    }
+    double run = incl - loc;
+    for (int k = 0; k < per; ++k) {
+        const int i = i0 + k;
+        if (i < nw) {
+            run += (double)((w_at(i) + 1e-5f) / wsum);
+            cdf_l[i + 1] = (float)run;
+        }
+    }
+    if (lane == 0) cdf_l[0] = 0.0f;
+}
+
+__device__ __forceinline__ float invert_cdf(const float* cdf_l, const float* bins_l, int nb, float u) {
+    // searchsorted(cdf, u, right=True): first index with cdf > u
+    int lo = 0, hi = nb;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (cdf_l[mid] <= u) lo = mid + 1; else hi = mid;
+    }
+    const int below = max(lo - 1, 0);
+    const int above = min(lo, nb - 1);
+    const float c0 = cdf_l[below], c1 = cdf_l[above];
+    const float b0 = bins_l[below], b1 = bins_l[above];
+    float denom = c1 - c0;
+    if (denom < 1e-5f) denom = 1.0f;
+    const float t = (u - c0) / denom;
+    return b0 + t * (b1 - b0);
+}
+
+__device__ __forceinline__ float draw_u(const PdfArgs& a, int64_t r, int k) {
+    if (a.det) return a.t_imp[k];
+    const int64_t idx = r * a.N + k;
+    return a.u ? a.u[idx] : philox_uniform(a.seed, a.offset, (uint64_t)idx);
+}
+
+__global__ void __launch_bounds__(256) sample_pdf_kernel(PdfArgs a) {
+    __shared__ float s_cdf[4][kMaxBins];
+    __shared__ float s_bins[4][kMaxBins];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t r = (int64_t)blockIdx.x * 4 + wv;
+    if (r >= a.R) return;
+    float* cdf_l = s_cdf[wv];
+    float* bins_l = s_bins[wv];
+    const float* br = a.bins + r * a.bins_stride;
+    const float* wr = a.w + r * a.w_stride;
+    for (int i = lane; i < a.nb; i += 64) bins_l[i] = br[i];
+    build_cdf(a.nb, [&](int i) { return wr[i]; }, cdf_l, lane);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    for (int k = lane; k < a.N; k += 64)
+        a.samples[r * a.N + k] = invert_cdf(cdf_l, bins_l, a.nb, draw_u(a, r, k));
+}
+
+// Fine-pass sampler: z_mid bins, weights[...,1:-1], importance samples, rank-sort merge, points.
+__global__ void __launch_bounds__(256) sample_fine_kernel(PdfArgs a) {
+    __shared__ float s_cdf[4][kMaxBins];
+    __shared__ float s_bins[4][kMaxBins];
+    __shared__ float s_all[4][kMaxMerged];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t r = (int64_t)blockIdx.x * 4 + wv;
+    if (r >= a.R) return;
+    const int S = a.S, N = a.N, M = S + N, nb = S - 1;
+    float* cdf_l = s_cdf[wv];
+    float* bins_l = s_bins[wv];
+    float* all_l = s_all[wv];
+    const float* zr = a.z + r * S;
+    const float* wr = a.w + r * S;
+    for (int i = lane; i < S; i += 64) {
+        const float zi = zr[i];
+        all_l[i] = zi;
+        if (i + 1 < S) bins_l[i] = 0.5f * (zr[i + 1] + zi);      // .5 * (z[1:] + z[:-1])
+    }
+    build_cdf(nb, [&](int i) { return wr[i + 1]; }, cdf_l, lane);   // weights[..., 1:-1]
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    double sum = 0.0;
+    for (int k = lane; k < N; k += 64) {
+        const float s = invert_cdf(cdf_l, bins_l, nb, draw_u(a, r, k));
+        all_l[S + k] = s;
+        if (a.samples) a.samples[r * N + k] = s;
+        sum += (double)s;
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    if (a.z_std) {
+        const double mean = wave_sum_d(sum) / (double)N;
+        double ss = 0.0;
+        for (int k = lane; k < N; k += 64) {
+            const double d = (double)all_l[S + k] - mean;
+            ss += d * d;
+        }
+        ss = wave_sum_d(ss);
+        if (lane == 0) a.z_std[r] = (float)sqrt(ss / (double)N);
+    }
+    // rank sort (ties broken by position): out[rank(e)] = v_e
+    const float* ray = a.rays + r * a.ray_stride;
+    const float ox = ray[0], oy = ray[1], oz = ray[2], dx = ray[3], dy = ray[4], dz = ray[5];
+    for (int e = lane; e < M; e += 64) {
+        const float v = all_l[e];
+        int rank = 0;
+        for (int i = 0; i < M; ++i) {
+            const float w = all_l[i];
+            rank += (w < v) || (w == v && i < e);
+        }
+        const int64_t o = r * M + rank;
+        a.z_fine[o] = v;
+        if (a.pts_fine) {
+            a.pts_fine[3 * o + 0] = ox + dx * v;
+            a.pts_fine[3 * o + 1] = oy + dy * v;
+            a.pts_fine[3 * o + 2] = oz + dz * v;
+        }
+    }
+}
+
+}  // namespace nerf
+
+using namespace nerf;
+
+extern "C" int nerf_sample_stratified(const float* d_rays, int64_t ray_stride, int64_t n_rays, int n_samples,
+                                      const float* d_t, int lindisp, int perturb, const float* d_u, uint64_t seed,
+                                      uint64_t offset, float* d_z, float* d_pts, void* stream) {
+    NERF_REQUIRE(n_rays >= 0 && n_samples >= 1, "sample_stratified: R=%lld S=%d", (long long)n_rays, n_samples);
+    NERF_REQUIRE(ray_stride >= 8, "sample_stratified: ray_stride %lld < 8", (long long)ray_stride);
+    NERF_REQUIRE(d_rays && d_t && d_z, "sample_stratified: null arg");
+    if (n_rays == 0) return NERF_OK;
+    StratArgs a{d_rays, ray_stride, n_rays, n_samples, d_t, lindisp, perturb, d_u, seed, offset, d_z, d_pts};
+    hipLaunchKernelGGL(sample_stratified_kernel, dim3(blocks_for(n_rays * n_samples, 256)), dim3(256), 0,
+                       as_stream(stream), a);
+    NERF_CHECK_LAUNCH("sample_stratified");
+    return NERF_OK;
+}
+
+extern "C" int nerf_sample_pdf(const float* d_bins, int64_t bins_stride, const float* d_weights,
+                               int64_t weights_stride, int64_t n_rays, int n_bins, int n_importance, int det,
+                               const float* d_t_imp, const float* d_u, uint64_t seed, uint64_t offset,
+                               float* d_samples, void* stream) {
+    NERF_REQUIRE(n_rays >= 0 && n_bins >= 2 && n_bins <= kMaxBins && n_importance >= 1,
+                 "sample_pdf: R=%lld bins=%d N=%d (bins must be 2..%d)", (long long)n_rays, n_bins, n_importance,
+                 kMaxBins);
+    NERF_REQUIRE(d_bins && d_weights && d_samples && (!det || d_t_imp), "sample_pdf: null arg");
+    if (n_rays == 0) return NERF_OK;
+    PdfArgs a{};
+    a.bins = d_bins; a.bins_stride = bins_stride; a.w = d_weights; a.w_stride = weights_stride;
+    a.R = n_rays; a.nb = n_bins; a.N = n_importance; a.det = det; a.t_imp = d_t_imp; a.u = d_u;
+    a.seed = seed; a.offset = offset; a.samples = d_samples;
+    hipLaunchKernelGGL(sample_pdf_kernel, dim3(blocks_for(n_rays, 4)), dim3(256), 0, as_stream(stream), a);
+    NERF_CHECK_LAUNCH("sample_pdf");
+    return NERF_OK;
+}
+
+extern "C" int nerf_sample_fine(const float* d_rays, int64_t ray_stride, const float* d_z, const float* d_weights,
+                                int64_t n_rays, int n_samples, int n_importance, int det, const float* d_t_imp,
+                                const float* d_u, uint64_t seed, uint64_t offset, float* d_z_fine, float* d_pts_fine,
+                                float* d_z_std, float* d_samples, void* stream) {
+    NERF_REQUIRE(n_rays >= 0 && n_samples >= 3 && n_samples <= kMaxBins && n_importance >= 1 &&
+                     n_samples + n_importance <= kMaxMerged,
+                 "sample_fine: R=%lld S=%d N=%d (S in 3..%d, S+N <= %d)", (long long)n_rays, n_samples,
+                 n_importance, kMaxBins, kMaxMerged);
+    NERF_REQUIRE(ray_stride >= 6, "sample_fine: ray_stride %lld < 6", (long long)ray_stride);
+    NERF_REQUIRE(d_rays && d_z && d_weights && d_z_fine && (!det || d_t_imp), "sample_fine: null arg");
+    if (n_rays == 0) return NERF_OK;
+    PdfArgs a{};
+    a.R = n_rays; a.N = n_importance; a.det = det; a.t_imp = d_t_imp; a.u = d_u; a.seed = seed; a.offset = offset;
+    a.samples = d_samples; a.rays = d_rays; a.ray_stride = ray_stride; a.z = d_z; a.w = d_weights; a.S = n_samples;
+    a.z_fine = d_z_fine; a.pts_fine = d_pts_fine; a.z_std = d_z_std;
+    hipLaunchKernelGGL(sample_fine_kernel, dim3(blocks_for(n_rays, 4)), dim3(256), 0, as_stream(stream), a);
+    NERF_CHECK_LAUNCH("sample_fine");
+    return NERF_OK;
+}

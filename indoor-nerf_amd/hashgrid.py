@@ -1,0 +1,143 @@
+"""Multi-resolution hash encoding and SH view encoding on the HIP kernels.
+
+API mirror of PocketNeRF/hash_encoding.py: HashEmbedder (:11-107) and SHEncoder (:110-191), same
+constructor arguments, attributes, parameters (`embeddings.{i}.weight`, nn.Embedding(2^log2T, 2))
+and return values. Forward and backward run in libnerfhip (csrc/hashgrid.hip, csrc/field.hip).
+"""
+import torch
+import torch.nn as nn
+
+from . import _lib
+
+
+def level_resolutions(base_resolution, finest_resolution, n_levels):
+    """floor(base * b**i) in float32 with b = exp((ln F - ln B)/(L-1)) (hash_encoding.py:28, :89),
+    evaluated with the reference's tensor dtypes (int64 base/finest, float32 b) on the CPU."""
+    b_res = torch.as_tensor(base_resolution).cpu()
+    f_res = torch.as_tensor(finest_resolution).cpu()
+    b = torch.exp((torch.log(f_res) - torch.log(b_res)) / (n_levels - 1))
+    return [float(torch.floor(b_res * b ** i)) for i in range(n_levels)], b
+
+
+def _bbox_floats(bounding_box):
+    lo, hi = bounding_box
+    lo = torch.as_tensor(lo, dtype=torch.float32).detach().cpu().reshape(3)
+    hi = torch.as_tensor(hi, dtype=torch.float32).detach().cpu().reshape(3)
+    return [float(v) for v in lo], [float(v) for v in hi]
+
+
+def accumulate_grad_buffers(params):
+    """The fused backward kernels ACCUMULATE straight into .grad (like a fused optimizer's bucket):
+    create zero grads where they are missing and return them."""
+    out = []
+    for p in params:
+        if p.grad is None:
+            p.grad = torch.zeros_like(p, memory_format=torch.contiguous_format)
+        out.append(p.grad)
+    return out
+
+
+class HashEncodeFn(torch.autograd.Function):
+    """xyz [P,3] -> (feat, keep). feat is [P, 2L] (layout 'point') or [L, P, 2] (layout 'level')."""
+
+    @staticmethod
+    def forward(ctx, xyz, meta, layout, *tables):
+        if xyz.requires_grad:
+            raise NotImplementedError("HashEmbedder: gradients w.r.t. positions are not implemented "
+                                      "(the reference never back-propagates into sample positions)")
+        xyz = xyz.contiguous()
+        P, L = xyz.shape[0], len(tables)
+        if layout == "point":
+            feat = torch.empty(P, 2 * L, device=xyz.device, dtype=torch.float32)
+            sp, sl = 2 * L, 2
+        else:
+            feat = torch.empty(L, P, 2, device=xyz.device, dtype=torch.float32)
+            sp, sl = 2, 2 * P
+        keep = torch.empty(P, device=xyz.device, dtype=torch.bool)
+        _lib.call("nerf_hash_encode_fwd", _lib.ptr(xyz, "xyz"), P, meta["bmin"], meta["bmax"], meta["res"], L,
+                  meta["log2_T"], _lib.ptr_array(tables), _lib.ptr(feat, "feat"), sp, sl,
+                  _lib.ptr(keep, "keep", dtype=torch.bool), _lib.stream())
+        ctx.save_for_backward(xyz, *tables)
+        ctx.meta, ctx.sp, ctx.sl = meta, sp, sl
+        ctx.mark_non_differentiable(keep)
+        return feat, keep
+
+    @staticmethod
+    def backward(ctx, g_feat, g_keep):
+        xyz, *tables = ctx.saved_tensors
+        if g_feat is not None and any(t.requires_grad for t in tables):
+            g = g_feat.contiguous()
+            grads = accumulate_grad_buffers(tables)
+            meta = ctx.meta
+            _lib.call("nerf_hash_encode_bwd", _lib.ptr(xyz, "xyz"), xyz.shape[0], meta["bmin"], meta["bmax"],
+                      meta["res"], len(tables), meta["log2_T"], _lib.ptr(g, "grad_feat"), ctx.sp, ctx.sl,
+                      _lib.ptr_array(grads, "grad_tables"), _lib.stream())
+        return (None, None, None) + (None,) * len(tables)
+
+
+class HashEmbedder(nn.Module):
+    """hash_encoding.py:11-107 on MI355X. forward(x [P,3]) -> (feat [P, L*F], keep [P] bool)."""
+
+    def __init__(self, bounding_box, n_levels=16, n_features_per_level=2, log2_hashmap_size=19,
+                 base_resolution=16, finest_resolution=512, use_quantization=False, quantization_bits=8):
+        super().__init__()
+        if n_features_per_level != 2:
+            raise NotImplementedError("HashEmbedder: the HIP kernels implement n_features_per_level == 2")
+        if not 1 <= n_levels <= _lib.MAX_LEVELS:
+            raise ValueError(f"HashEmbedder: n_levels must be 1..{_lib.MAX_LEVELS}")
+        if use_quantization:
+            raise NotImplementedError("HashEmbedder(use_quantization=True): the A-CAQ quantized gather kernel "
+                                      "is not built yet")
+        self.bounding_box = bounding_box
+        self.n_levels = n_levels
+        self.n_features_per_level = n_features_per_level
+        self.log2_hashmap_size = log2_hashmap_size
+        self.base_resolution = torch.tensor(base_resolution)
+        self.finest_resolution = torch.tensor(finest_resolution)
+        self.out_dim = n_levels * n_features_per_level
+        self.use_quantization = use_quantization
+        self.quantizers = None
+        self.warmup_steps = 500
+        self.current_step = 0
+        res, self.b = level_resolutions(self.base_resolution, self.finest_resolution, n_levels)
+        self.embeddings = nn.ModuleList([nn.Embedding(2 ** log2_hashmap_size, n_features_per_level)
+                                         for _ in range(n_levels)])
+        for emb in self.embeddings:
+            nn.init.uniform_(emb.weight, a=-0.0001, b=0.0001)
+        bmin, bmax = _bbox_floats(bounding_box)
+        self._meta = dict(res=_lib.host_f32(res), bmin=_lib.host_f32(bmin), bmax=_lib.host_f32(bmax),
+                          log2_T=log2_hashmap_size)
+        self.level_res = res
+
+    def tables(self):
+        return [e.weight for e in self.embeddings]
+
+    def encode(self, x, layout="point"):
+        return HashEncodeFn.apply(x, self._meta, layout, *self.tables())
+
+    def forward(self, x):
+        if self.training:
+            self.current_step += 1
+        return self.encode(x, "point")
+
+
+class SHEncoder(nn.Module):
+    """hash_encoding.py:110-191 (degree 4 only, the value create_nerf uses)."""
+
+    def __init__(self, input_dim=3, degree=4):
+        super().__init__()
+        assert input_dim == 3
+        if degree != 4:
+            raise NotImplementedError("SHEncoder: the HIP kernel implements degree 4")
+        self.input_dim = input_dim
+        self.degree = degree
+        self.out_dim = degree ** 2
+
+    def forward(self, input, **kwargs):
+        if input.requires_grad:
+            raise NotImplementedError("SHEncoder: gradients w.r.t. directions are not implemented "
+                                      "(the reference never back-propagates into view directions)")
+        d = input.reshape(-1, 3).contiguous().float()
+        out = torch.empty(d.shape[0], 16, device=d.device, dtype=torch.float32)
+        _lib.call("nerf_sh4_fwd", _lib.ptr(d, "dirs"), d.shape[0], _lib.ptr(out, "sh"), _lib.stream())
+        return out.reshape(*input.shape[:-1], 16)

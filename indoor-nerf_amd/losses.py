@@ -1,0 +1,80 @@
+"""Losses of the training step on the HIP kernels.
+
+total_variation_loss mirrors PocketNeRF/loss.py:11-43 (one random hashed cuboid per level; the
+cuboid corner is drawn with torch.randint on the host, like the reference). total_variation_all
+runs all levels of a HashEmbedder in one forward and one backward launch (csrc/optim.hip).
+sigma_sparsity_loss mirrors loss.py:45-47 (plain torch; unused by the reference's training loop).
+"""
+import math
+
+import torch
+
+from . import _lib
+from .hashgrid import accumulate_grad_buffers
+
+
+def tv_cube(level, min_resolution, max_resolution, n_levels):
+    """Resolution and cuboid edge of loss.py:13-22 (python-double b, float32 product, floor)."""
+    b = math.exp((math.log(float(max_resolution)) - math.log(float(min_resolution))) / (n_levels - 1))
+    res = int(torch.floor(torch.as_tensor(min_resolution).cpu() * b ** level).item())
+    min_cube = int(min_resolution) - 1
+    if min_cube > 50:
+        raise ValueError("total_variation_loss: min cuboid size greater than max (loss.py:19-21)")
+    cube = int(torch.floor(torch.clip(torch.tensor(res) / 10.0, min_cube, 50)).item())
+    return res, cube
+
+
+class TVFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, min_vertex, cubes, log2_T, *tables):
+        L = len(tables)
+        mv = (_lib.c_i64 * (3 * L))(*[int(v) for v in min_vertex.reshape(-1).tolist()])
+        cb = (_lib.c_int * L)(*[int(c) for c in cubes])
+        loss = torch.zeros(L, device=tables[0].device, dtype=torch.float32)
+        _lib.call("nerf_tv_fwd", _lib.ptr_array(tables), L, log2_T, mv, cb, _lib.ptr(loss, "loss"), _lib.stream())
+        ctx.save_for_backward(*tables)
+        ctx.mv, ctx.cb, ctx.log2_T = mv, cb, log2_T
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        tables = ctx.saved_tensors
+        if g is not None and any(t.requires_grad for t in tables):
+            grads = accumulate_grad_buffers(tables)
+            _lib.call("nerf_tv_bwd", _lib.ptr_array(tables), len(tables), ctx.log2_T, ctx.mv, ctx.cb,
+                      _lib.ptr(g.contiguous(), "grad_loss"), _lib.ptr_array(grads, "grad_tables"), _lib.stream())
+        return (None, None, None) + (None,) * len(tables)
+
+
+def draw_min_vertices(embedder, generator=None):
+    """One cuboid corner per level: torch.randint(0, res - cube, (3,)) (loss.py:25)."""
+    mvs, cubes = [], []
+    for lvl in range(embedder.n_levels):
+        res, cube = tv_cube(lvl, embedder.base_resolution, embedder.finest_resolution, embedder.n_levels)
+        mvs.append(torch.randint(0, res - cube, (3,), generator=generator))
+        cubes.append(cube)
+    return torch.stack(mvs), cubes
+
+
+def total_variation_all(embedder, min_vertex=None, generator=None):
+    """Per-level TV losses [L] of all levels of `embedder` (sum them for the reference's TV_loss)."""
+    if min_vertex is None:
+        min_vertex, cubes = draw_min_vertices(embedder, generator)
+    else:
+        cubes = [tv_cube(l, embedder.base_resolution, embedder.finest_resolution, embedder.n_levels)[1]
+                 for l in range(embedder.n_levels)]
+    return TVFn.apply(torch.as_tensor(min_vertex), cubes, embedder.log2_hashmap_size, *embedder.tables())
+
+
+def total_variation_loss(embeddings, min_resolution, max_resolution, level, log2_hashmap_size, n_levels=16,
+                         min_vertex=None):
+    """loss.py:11-43 for one level's nn.Embedding."""
+    res, cube = tv_cube(level, min_resolution, max_resolution, n_levels)
+    if min_vertex is None:
+        min_vertex = torch.randint(0, res - cube, (3,))
+    return TVFn.apply(torch.as_tensor(min_vertex).reshape(1, 3), [cube], log2_hashmap_size, embeddings.weight)[0]
+
+
+def sigma_sparsity_loss(sigmas):
+    """loss.py:45-47 (Cauchy sparsity)."""
+    return torch.log(1.0 + 2 * sigmas ** 2).sum(dim=-1)

@@ -1,0 +1,138 @@
+"""create_nerf (PocketNeRF/run_nerf.py:218-344) and the training iteration of train()
+(run_nerf.py:1007-1035, :1161-1162, :1289-1293) on this package's modules.
+
+create_nerf keeps the reference's return value (render_kwargs_train, render_kwargs_test, start,
+grad_vars, optimizer), dict keys, RAdam param groups and checkpoint reload; it fixes the HEAD bugs
+listed in SURVEY.md §0.3 (predict_normals / use_quantization kwargs) by accepting the arguments.
+"""
+import os
+from types import SimpleNamespace
+
+import torch
+
+from .field import NeRFSmall, run_network
+from .hashgrid import HashEmbedder, SHEncoder
+from .losses import total_variation_all
+from .optim import RAdam
+from .render import img2mse, mse2psnr, render
+
+DEFAULTS = dict(multires=10, i_embed=1, i_embed_views=2, multires_views=4, use_viewdirs=True, N_importance=0,
+                N_samples=64, netchunk=1024 * 64, finest_res=512, log2_hashmap_size=19, lrate=5e-4,
+                lrate_decay=250, perturb=1., white_bkgd=False, raw_noise_std=0., predict_normals=False,
+                use_quantization=False, quantization_bits=8, dataset_type="blender", no_ndc=False, lindisp=False,
+                basedir="./logs/", expname="", ft_path=None, no_reload=True, sparse_loss_weight=1e-10,
+                tv_loss_weight=1e-6, chunk=1024 * 32)
+
+
+def make_args(**kw):
+    d = dict(DEFAULTS)
+    d.update(kw)
+    return SimpleNamespace(**d)
+
+
+def create_nerf(args, device=None):
+    device = torch.device(device or ("cuda" if torch.cuda.is_available() else "cpu"))
+    get = lambda k: getattr(args, k, DEFAULTS.get(k))  # noqa: E731
+    if get("i_embed") != 1 or get("i_embed_views") != 2:
+        raise NotImplementedError("create_nerf: only the hash-grid (i_embed=1) + SH (i_embed_views=2) model is "
+                                  "built on the HIP path (the positional-encoding NeRF is out of scope)")
+    use_q, q_bits = get("use_quantization"), get("quantization_bits")
+    embed_fn = HashEmbedder(bounding_box=args.bounding_box, log2_hashmap_size=get("log2_hashmap_size"),
+                            finest_resolution=get("finest_res"), use_quantization=use_q,
+                            quantization_bits=q_bits).to(device)
+    embedding_params = list(embed_fn.parameters())
+    embeddirs_fn = SHEncoder() if get("use_viewdirs") else None
+    input_ch, input_ch_views = embed_fn.out_dim, (embeddirs_fn.out_dim if embeddirs_fn else 0)
+    model = NeRFSmall(num_layers=2, hidden_dim=64, geo_feat_dim=15, num_layers_color=3, hidden_dim_color=64,
+                      input_ch=input_ch, input_ch_views=input_ch_views, use_quantization=use_q,
+                      quantization_bits=q_bits).to(device)
+    grad_vars = list(model.parameters())
+    model_fine = None
+    if get("N_importance") > 0:
+        model_fine = NeRFSmall(num_layers=2, hidden_dim=64, geo_feat_dim=15, num_layers_color=3, hidden_dim_color=64,
+                               input_ch=input_ch, input_ch_views=input_ch_views, use_quantization=use_q,
+                               quantization_bits=q_bits, predict_normals=get("predict_normals")).to(device)
+        grad_vars += list(model_fine.parameters())
+    netchunk = get("netchunk")
+    network_query_fn = lambda inputs, viewdirs, network_fn: run_network(  # noqa: E731
+        inputs, viewdirs, network_fn, embed_fn=embed_fn, embeddirs_fn=embeddirs_fn, netchunk=netchunk)
+    optimizer = RAdam([{"params": grad_vars, "weight_decay": 1e-6},
+                       {"params": embedding_params, "eps": 1e-15}], lr=get("lrate"), betas=(0.9, 0.99))
+    start = 0
+    basedir, expname = get("basedir"), get("expname")
+    ft_path = get("ft_path")
+    if ft_path is not None and ft_path != "None":
+        ckpts = [ft_path]
+    elif basedir and expname and os.path.isdir(os.path.join(basedir, expname)):
+        ckpts = [os.path.join(basedir, expname, f) for f in sorted(os.listdir(os.path.join(basedir, expname)))
+                 if "tar" in f]
+    else:
+        ckpts = []
+    if len(ckpts) > 0 and not get("no_reload"):
+        ckpt = torch.load(ckpts[-1], map_location=device, weights_only=True)
+        start = ckpt["global_step"]
+        optimizer.load_state_dict(ckpt["optimizer_state_dict"])
+        model.load_state_dict(ckpt["network_fn_state_dict"])
+        if model_fine is not None:
+            model_fine.load_state_dict(ckpt["network_fine_state_dict"])
+        embed_fn.load_state_dict(ckpt["embed_fn_state_dict"])
+    render_kwargs_train = {
+        "network_query_fn": network_query_fn, "perturb": get("perturb"), "N_importance": get("N_importance"),
+        "network_fine": model_fine, "N_samples": get("N_samples"), "network_fn": model, "embed_fn": embed_fn,
+        "use_viewdirs": get("use_viewdirs"), "white_bkgd": get("white_bkgd"), "raw_noise_std": get("raw_noise_std"),
+        "predict_normals": get("predict_normals"),
+    }
+    if get("dataset_type") != "llff" or get("no_ndc"):
+        render_kwargs_train["ndc"] = False
+        render_kwargs_train["lindisp"] = get("lindisp")
+    render_kwargs_test = dict(render_kwargs_train)
+    render_kwargs_test["perturb"] = False
+    render_kwargs_test["raw_noise_std"] = 0.
+    return render_kwargs_train, render_kwargs_test, start, grad_vars, optimizer
+
+
+def save_checkpoint(path, global_step, render_kwargs_train, optimizer):
+    """The reference's checkpoint dict (run_nerf.py:1345-1362)."""
+    fine = render_kwargs_train["network_fine"]
+    torch.save({"global_step": global_step,
+                "network_fn_state_dict": render_kwargs_train["network_fn"].state_dict(),
+                "network_fine_state_dict": fine.state_dict() if fine is not None else None,
+                "embed_fn_state_dict": render_kwargs_train["embed_fn"].state_dict(),
+                "optimizer_state_dict": optimizer.state_dict()}, path)
+
+
+def train_step(batch_rays, target_s, render_kwargs_train, optimizer, args, global_step, H=0, W=0, K=None,
+               grad_hook=None, loss_scale_sparsity=1.0, tv_generator=None, zero_grad=None):
+    """One iteration of train() without host bookkeeping: render (coarse+fine), img/img0 MSE,
+    sparsity, TV (run_nerf.py:1007-1037), backward, [grad_hook, e.g. DP all-reduce], RAdam step,
+    lr decay (:1289-1293). Returns (loss, psnr) as device tensors (no host sync)."""
+    get = lambda k: getattr(args, k, DEFAULTS.get(k))  # noqa: E731
+    rgb, depth, acc, extras = render(H, W, K, chunk=get("chunk"), rays=batch_rays, retraw=True,
+                                     **render_kwargs_train)
+    if zero_grad is None:
+        optimizer.zero_grad()
+    else:
+        zero_grad()
+    img_loss = img2mse(rgb, target_s)
+    loss = img_loss
+    psnr = mse2psnr(img_loss)
+    if "rgb0" in extras:
+        loss = loss + img2mse(extras["rgb0"], target_s)
+    sp = extras["sparsity_loss"].sum()
+    if "sparsity_loss0" in extras:
+        sp = sp + extras["sparsity_loss0"].sum()
+    loss = loss + (get("sparse_loss_weight") * loss_scale_sparsity) * sp
+    tv_w = get("tv_loss_weight")
+    if tv_w > 0:
+        loss = loss + tv_w * total_variation_all(render_kwargs_train["embed_fn"], generator=tv_generator).sum()
+    if global_step > 1000:
+        args.tv_loss_weight = 0.0
+    loss.backward()
+    if grad_hook is not None:
+        grad_hook()
+    optimizer.step()
+    decay_steps = get("lrate_decay") * 1000
+    new_lrate = get("lrate") * (0.1 ** (global_step / decay_steps))
+    for g in optimizer.param_groups:
+        g["lr"] = new_lrate
+    return loss.detach(), psnr.detach()

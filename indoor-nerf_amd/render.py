@@ -1,0 +1,258 @@
+"""Volumetric renderer on the HIP kernels.
+
+API mirror of PocketNeRF/run_nerf.py:71-151, :347-549 (batchify_rays, render, raw2outputs,
+render_rays) and PocketNeRF/run_nerf_helpers.py:10-13, :311-397 (img2mse, mse2psnr, to8b,
+get_rays, get_rays_np, ndc_rays, sample_pdf). Sampling, compositing and the hierarchical
+resampling run in libnerfhip (csrc/sampling.hip, csrc/composite.hip); the field query goes
+through network_query_fn (field.run_network -> the fused hash-grid + MLP kernels).
+
+Randomness: pytest=True reproduces the reference's np.random.seed(0) draws exactly; otherwise
+stratified jitter and importance uniforms are drawn in-kernel (Philox4x32-10) from a seed taken
+from torch's CPU generator, and raw noise uses torch.randn like the reference.
+"""
+import numpy as np
+import torch
+
+from . import _lib
+
+img2mse = lambda x, y: torch.mean((x - y) ** 2)  # noqa: E731
+mse2psnr = lambda x: -10. * torch.log(x) / torch.log(torch.tensor([10.], device=x.device))  # noqa: E731
+to8b = lambda x: (255 * np.clip(x, 0, 1)).astype(np.uint8)  # noqa: E731
+
+_LINSPACE = {}
+_SEED_GEN = None
+
+
+def _linspace(n, device):
+    key = (n, str(device))
+    if key not in _LINSPACE:
+        _LINSPACE[key] = torch.linspace(0., 1., steps=n).to(device)   # CPU linspace values, as the reference
+    return _LINSPACE[key]
+
+
+def _draw_seed():
+    global _SEED_GEN
+    if _SEED_GEN is None:
+        _SEED_GEN = torch.Generator().manual_seed(torch.initial_seed() & ((1 << 63) - 1))
+    s = torch.randint(0, 2 ** 62, (2,), generator=_SEED_GEN)
+    return int(s[0]), int(s[1])
+
+
+def manual_seed(seed):
+    """Seed the in-kernel Philox draws (stratified jitter, importance uniforms)."""
+    global _SEED_GEN
+    _SEED_GEN = torch.Generator().manual_seed(int(seed))
+
+
+def _pytest_uniforms(shape, device):
+    np.random.seed(0)
+    return torch.from_numpy(np.random.rand(*shape).astype(np.float32)).to(device)
+
+
+# ---------------------------------------------------------------- compositing
+
+class CompositeFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, raw, z, rays_d, noise, white_bkgd):
+        if z.requires_grad or rays_d.requires_grad:
+            raise NotImplementedError("raw2outputs: gradients w.r.t. z_vals / rays_d are not implemented "
+                                      "(the reference detaches both)")
+        ctx.set_materialize_grads(False)
+        raw = raw.contiguous()
+        z = z.contiguous().float()
+        rays_d = rays_d.contiguous().float()
+        R, S, C = raw.shape
+        dev = raw.device
+        f = dict(device=dev, dtype=torch.float32)
+        rgb, disp, acc = torch.empty(R, 3, **f), torch.empty(R, **f), torch.empty(R, **f)
+        weights, depth, ent = torch.empty(R, S, **f), torch.empty(R, **f), torch.empty(R, **f)
+        normal = torch.empty(R, 3, **f) if C == 7 else None
+        _lib.call("nerf_composite_fwd", _lib.ptr(raw, "raw"), C, _lib.ptr(z, "z_vals"), _lib.ptr(rays_d, "rays_d"),
+                  _lib.ptr(noise, "noise", allow_none=True), R, S, int(bool(white_bkgd)), _lib.ptr(rgb, "rgb"),
+                  _lib.ptr(disp, "disp"), _lib.ptr(acc, "acc"), _lib.ptr(weights, "weights"), _lib.ptr(depth, "depth"),
+                  _lib.ptr(ent, "entropy"), _lib.ptr(normal, "normal", allow_none=True), _lib.stream())
+        ctx.save_for_backward(raw, z, rays_d, noise)
+        ctx.white = int(bool(white_bkgd))
+        outs = (rgb, disp, acc, weights, depth, ent)
+        return outs + ((normal,) if normal is not None else ())
+
+    @staticmethod
+    def backward(ctx, *grads):
+        raw, z, rays_d, noise = ctx.saved_tensors
+        R, S, C = raw.shape
+        names = ["g_rgb", "g_disp", "g_acc", "g_weights", "g_depth", "g_entropy", "g_normal"]
+        gs = [None if g is None else g.contiguous().float() for g in grads] + [None] * (7 - len(grads))
+        graw = torch.empty_like(raw)
+        _lib.call("nerf_composite_bwd", _lib.ptr(raw, "raw"), C, _lib.ptr(z, "z_vals"), _lib.ptr(rays_d, "rays_d"),
+                  _lib.ptr(noise, "noise", allow_none=True), R, S, ctx.white,
+                  *[_lib.ptr(g, n, allow_none=True) for g, n in zip(gs, names)], _lib.ptr(graw, "grad_raw"),
+                  _lib.stream())
+        return graw, None, None, None, None
+
+
+def raw2outputs(raw, z_vals, rays_d, raw_noise_std=0, white_bkgd=False, pytest=False, predict_normals=False):
+    """run_nerf.py:347-411 -> (rgb_map, disp_map, acc_map, weights, depth_map, sparsity_loss[, normal_map])."""
+    R, S = raw.shape[0], raw.shape[1]
+    noise = None
+    if raw_noise_std > 0.:
+        if pytest:
+            noise = _pytest_uniforms((R, S), raw.device) * raw_noise_std
+        else:
+            noise = torch.randn(R, S, device=raw.device) * raw_noise_std
+    if predict_normals and raw.shape[-1] != 7:
+        raise ValueError("raw2outputs(predict_normals=True) needs 7 raw channels")
+    outs = CompositeFn.apply(raw.float(), z_vals, rays_d, noise, white_bkgd)
+    if predict_normals:
+        return outs
+    return outs[:6]
+
+
+# ---------------------------------------------------------------- sampling
+
+def sample_pdf(bins, weights, N_samples, det=False, pytest=False):
+    """run_nerf_helpers.py:354-397 (no gradient: the reference detaches its samples)."""
+    bins = bins.detach().contiguous().float()
+    weights = weights.detach().contiguous().float()
+    R, nb = bins.shape
+    if weights.shape != (R, nb - 1):
+        raise ValueError(f"sample_pdf: weights {tuple(weights.shape)} must be [R, n_bins - 1] = [{R}, {nb - 1}]")
+    out = torch.empty(R, N_samples, device=bins.device, dtype=torch.float32)
+    t_imp = _linspace(N_samples, bins.device) if det else None
+    u = _pytest_uniforms((R, N_samples), bins.device) if (pytest and not det) else None
+    seed, off = _draw_seed()
+    _lib.call("nerf_sample_pdf", _lib.ptr(bins, "bins"), nb, _lib.ptr(weights, "weights"), nb - 1, R, nb, N_samples,
+              int(det), _lib.ptr(t_imp, "t", allow_none=True), _lib.ptr(u, "u", allow_none=True), seed, off,
+              _lib.ptr(out, "samples"), _lib.stream())
+    return out
+
+
+def render_rays(ray_batch, network_fn, network_query_fn, N_samples, embed_fn=None, retraw=False, lindisp=False,
+                perturb=0., N_importance=0, network_fine=None, white_bkgd=False, raw_noise_std=0., verbose=False,
+                pytest=False, predict_normals=False):
+    """run_nerf.py:414-549."""
+    rays = ray_batch.detach().float().contiguous()
+    R, C = rays.shape
+    dev = rays.device
+    f = dict(device=dev, dtype=torch.float32)
+    viewdirs = rays[:, -3:].contiguous() if C > 8 else None
+    rays_d = rays[:, 3:6].contiguous()
+
+    z = torch.empty(R, N_samples, **f)
+    pts = torch.empty(R, N_samples, 3, **f)
+    u = _pytest_uniforms((R, N_samples), dev) if (perturb > 0. and pytest) else None
+    seed, off = _draw_seed()
+    _lib.call("nerf_sample_stratified", _lib.ptr(rays, "ray_batch"), C, R, N_samples, _lib.ptr(_linspace(N_samples, dev)),
+              int(bool(lindisp)), int(perturb > 0.), _lib.ptr(u, "u", allow_none=True), seed, off, _lib.ptr(z, "z"),
+              _lib.ptr(pts, "pts"), _lib.stream())
+
+    raw = network_query_fn(pts, viewdirs, network_fn)
+    outs = raw2outputs(raw, z, rays_d, raw_noise_std, white_bkgd, pytest=pytest, predict_normals=predict_normals)
+    rgb_map, disp_map, acc_map, weights, depth_map, sparsity_loss = outs[:6]
+    normal_map = outs[6] if predict_normals else None
+
+    ret = {}
+    if N_importance > 0:
+        rgb_map_0, depth_map_0, acc_map_0, sparsity_loss_0, normal_map_0 = (rgb_map, depth_map, acc_map,
+                                                                             sparsity_loss, normal_map)
+        det = perturb == 0.
+        M = N_samples + N_importance
+        z_fine = torch.empty(R, M, **f)
+        pts_fine = torch.empty(R, M, 3, **f)
+        z_std = torch.empty(R, **f)
+        t_imp = _linspace(N_importance, dev) if det else None
+        u_imp = _pytest_uniforms((R, N_importance), dev) if (pytest and not det) else None
+        seed, off = _draw_seed()
+        _lib.call("nerf_sample_fine", _lib.ptr(rays, "ray_batch"), C, _lib.ptr(z, "z"),
+                  _lib.ptr(weights.detach().contiguous(), "weights"), R, N_samples, N_importance, int(det),
+                  _lib.ptr(t_imp, "t", allow_none=True), _lib.ptr(u_imp, "u", allow_none=True), seed, off,
+                  _lib.ptr(z_fine, "z_fine"), _lib.ptr(pts_fine, "pts_fine"), _lib.ptr(z_std, "z_std"), None,
+                  _lib.stream())
+        z, pts = z_fine, pts_fine
+        run_fn = network_fn if network_fine is None else network_fine
+        raw = network_query_fn(pts, viewdirs, run_fn)
+        outs = raw2outputs(raw, z, rays_d, raw_noise_std, white_bkgd, pytest=pytest, predict_normals=predict_normals)
+        rgb_map, disp_map, acc_map, weights, depth_map, sparsity_loss = outs[:6]
+        normal_map = outs[6] if predict_normals else None
+        ret.update(rgb0=rgb_map_0, depth0=depth_map_0, acc0=acc_map_0, sparsity_loss0=sparsity_loss_0, z_std=z_std)
+        if predict_normals:
+            ret["normal0"] = normal_map_0
+
+    ret.update(rgb_map=rgb_map, depth_map=depth_map, acc_map=acc_map, sparsity_loss=sparsity_loss, pts=pts,
+               rays_d=rays_d)
+    if predict_normals:
+        ret["normal_map"] = normal_map
+    if retraw:
+        ret["raw"] = raw
+    return ret
+
+
+def batchify_rays(rays_flat, chunk=1024 * 32, **kwargs):
+    """run_nerf.py:71-83."""
+    all_ret = {}
+    for i in range(0, rays_flat.shape[0], chunk):
+        ret = render_rays(rays_flat[i:i + chunk], **kwargs)
+        for k in ret:
+            all_ret.setdefault(k, []).append(ret[k])
+    return {k: (v[0] if len(v) == 1 else torch.cat(v, 0)) for k, v in all_ret.items()}
+
+
+def get_rays(H, W, K, c2w):
+    """run_nerf_helpers.py:311-320 (host-side glue, once per image)."""
+    i, j = torch.meshgrid(torch.linspace(0, W - 1, W, device=c2w.device),
+                          torch.linspace(0, H - 1, H, device=c2w.device), indexing="ij")
+    i, j = i.t(), j.t()
+    dirs = torch.stack([(i - K[0][2]) / K[0][0], -(j - K[1][2]) / K[1][1], -torch.ones_like(i)], -1)
+    rays_d = torch.sum(dirs[..., None, :] * c2w[:3, :3], -1)
+    rays_o = c2w[:3, -1].expand(rays_d.shape)
+    return rays_o, rays_d
+
+
+def get_rays_np(H, W, K, c2w):
+    """run_nerf_helpers.py:323-330."""
+    i, j = np.meshgrid(np.arange(W, dtype=np.float32), np.arange(H, dtype=np.float32), indexing="xy")
+    dirs = np.stack([(i - K[0][2]) / K[0][0], -(j - K[1][2]) / K[1][1], -np.ones_like(i)], -1)
+    rays_d = np.sum(dirs[..., np.newaxis, :] * c2w[:3, :3], -1)
+    rays_o = np.broadcast_to(c2w[:3, -1], np.shape(rays_d))
+    return rays_o, rays_d
+
+
+def ndc_rays(H, W, focal, near, rays_o, rays_d):
+    """run_nerf_helpers.py:333-350."""
+    t = -(near + rays_o[..., 2]) / rays_d[..., 2]
+    rays_o = rays_o + t[..., None] * rays_d
+    o0 = -1. / (W / (2. * focal)) * rays_o[..., 0] / rays_o[..., 2]
+    o1 = -1. / (H / (2. * focal)) * rays_o[..., 1] / rays_o[..., 2]
+    o2 = 1. + 2. * near / rays_o[..., 2]
+    d0 = -1. / (W / (2. * focal)) * (rays_d[..., 0] / rays_d[..., 2] - rays_o[..., 0] / rays_o[..., 2])
+    d1 = -1. / (H / (2. * focal)) * (rays_d[..., 1] / rays_d[..., 2] - rays_o[..., 1] / rays_o[..., 2])
+    d2 = -2. * near / rays_o[..., 2]
+    return torch.stack([o0, o1, o2], -1), torch.stack([d0, d1, d2], -1)
+
+
+def render(H, W, K, chunk=1024 * 32, rays=None, c2w=None, ndc=True, near=0., far=1., use_viewdirs=False,
+           c2w_staticcam=None, **kwargs):
+    """run_nerf.py:86-151 -> [rgb_map, depth_map, acc_map, extras]."""
+    if c2w is not None:
+        rays_o, rays_d = get_rays(H, W, K, c2w)
+    else:
+        rays_o, rays_d = rays
+    if use_viewdirs:
+        viewdirs = rays_d
+        if c2w_staticcam is not None:
+            rays_o, rays_d = get_rays(H, W, K, c2w_staticcam)
+        viewdirs = viewdirs / torch.norm(viewdirs, dim=-1, keepdim=True)
+        viewdirs = torch.reshape(viewdirs, [-1, 3]).float()
+    sh = rays_d.shape
+    if ndc:
+        rays_o, rays_d = ndc_rays(H, W, K[0][0], 1., rays_o, rays_d)
+    rays_o = torch.reshape(rays_o, [-1, 3]).float()
+    rays_d = torch.reshape(rays_d, [-1, 3]).float()
+    near, far = near * torch.ones_like(rays_d[..., :1]), far * torch.ones_like(rays_d[..., :1])
+    rays = torch.cat([rays_o, rays_d, near, far], -1)
+    if use_viewdirs:
+        rays = torch.cat([rays, viewdirs], -1)
+    all_ret = batchify_rays(rays, chunk, **kwargs)
+    for k in all_ret:
+        all_ret[k] = torch.reshape(all_ret[k], list(sh[:-1]) + list(all_ret[k].shape[1:]))
+    k_extract = ["rgb_map", "depth_map", "acc_map"]
+    return [all_ret[k] for k in k_extract] + [{k: all_ret[k] for k in all_ret if k not in k_extract}]

@@ -1,0 +1,35 @@
+"""Synthetic Blender-rig inputs for bench.py and smoke tests (no dataset access on the GPU box).
+
+The lego rig of SURVEY.md §8(d): spiral poses pose_spherical(theta, -30, 4.0311)
+(PocketNeRF/load_blender.py:12-35), camera_angle_x = 0.6911112070083618, near 2, far 6, and the
+scene AABB get_bbox3d_for_blenderobj returns for it (utils.py:27-58)."""
+import numpy as np
+
+CAMERA_ANGLE_X = 0.6911112070083618
+BLENDER_BBOX = ((-3.8502, -3.8500, -3.3230), (3.8491, 3.8496, 2.6801))
+
+
+def pose_spherical(theta_deg, phi_deg, radius):
+    t = np.eye(4)
+    t[2, 3] = radius
+    ph, th = np.deg2rad(phi_deg), np.deg2rad(theta_deg)
+    rot_phi = np.array([[1, 0, 0, 0], [0, np.cos(ph), -np.sin(ph), 0], [0, np.sin(ph), np.cos(ph), 0], [0, 0, 0, 1]])
+    rot_theta = np.array([[np.cos(th), 0, -np.sin(th), 0], [0, 1, 0, 0], [np.sin(th), 0, np.cos(th), 0], [0, 0, 0, 1]])
+    c2w = np.array([[-1, 0, 0, 0], [0, 0, 1, 0], [0, 1, 0, 0], [0, 0, 0, 1]]) @ (rot_theta @ rot_phi @ t)
+    return c2w.astype(np.float32)
+
+
+def blender_rays(n_rays, H=800, W=800, pose_index=3, seed=0):
+    """n_rays pixels of one spiral pose (seeded permutation); returns rays_o, rays_d [n,3] float32."""
+    focal = 0.5 * W / np.tan(0.5 * CAMERA_ANGLE_X)
+    c2w = pose_spherical(np.linspace(-180, 180, 101)[:-1][pose_index], -30.0, 4.0311)
+    pix = np.random.RandomState(seed).permutation(H * W)[:n_rays]
+    i, j = (pix % W).astype(np.float32), (pix // W).astype(np.float32)
+    dirs = np.stack([(i - 0.5 * W) / focal, -(j - 0.5 * H) / focal, -np.ones_like(i)], -1).astype(np.float32)
+    rays_d = (dirs[:, None, :] * c2w[None, :3, :3]).sum(-1).astype(np.float32)
+    rays_o = np.broadcast_to(c2w[:3, 3], rays_d.shape).astype(np.float32).copy()
+    return rays_o, rays_d
+
+
+def blender_bbox():
+    return (np.array(BLENDER_BBOX[0], np.float32), np.array(BLENDER_BBOX[1], np.float32))
