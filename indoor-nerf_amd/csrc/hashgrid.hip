@@ -11,6 +11,8 @@
 // Launch geometry: grid (ceil(P/256), L). Blocks are dispatched x-fastest, so at any moment the
 // whole chip works on one or two levels and each XCD's 4 MiB L2 holds the level's table lines
 // that the current point range touches (tables are 4 MiB per level at log2_T = 19).
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace nerf {
@@ -105,6 +107,15 @@ __device__ __forceinline__ void atomic_add_f32(float* p, float v) {
     __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// COALESCE = false: every lane issues its own 16 atomics (8 corners x 2 features): each wave
+// instruction then carries 64 unrelated addresses = 64 memory-side requests.
+// COALESCE = true: the per-item contributions are staged in LDS and re-issued so that one wave
+// instruction covers 4 items x 16 dwords, ordered (item, corner pair (j,k), i, feature). Corners
+// (x, y, z) and (x+1, y, z) hash to h and h ^ (x ^ (x+1)) (x only touches the low 11 bits), so the
+// 4 dwords of a pair usually share one 64-B segment and leave as ONE atomic request.
+constexpr uint32_t kSkip = 0xFFFFFFFFu;
+
+template <bool COALESCE>
 __global__ void __launch_bounds__(256) hash_encode_bwd_kernel(
     const float* __restrict__ xyz, int64_t n, HashGradParams hp,
     const float* __restrict__ dfeat, int64_t sp, int64_t sl) {
@@ -140,23 +151,21 @@ __global__ void __launch_bounds__(256) hash_encode_bwd_kernel(
 
     // Wave-level run merge: a voxel key equal to the previous lane's continues a run; segmented
     // inclusive sums (Hillis-Steele over 64 lanes) leave each run's total on its LAST lane, which
-    // alone issues the 16 atomics. Lanes of different runs never mix.
+    // alone issues the atomics. Lanes of different runs never mix.
     const uint32_t key_lo = (uint32_t)ax.base | ((uint32_t)ay.base << 16);
     const uint32_t key_hi = (uint32_t)az.base | (valid ? 0u : 0x80000000u);
     const int lane = threadIdx.x & 63;
     const uint32_t prev_lo = __shfl_up(key_lo, 1, 64), prev_hi = __shfl_up(key_hi, 1, 64);
     const bool head = (lane == 0) || prev_lo != key_lo || prev_hi != key_hi;
-    // run start lane index, propagated by a max-scan of head positions
-    int start = head ? lane : 0;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int s = __shfl_up(start, o, 64);
-        if (lane >= o) start = max(start, s);
-    }
     const uint32_t next_lo = __shfl_down(key_lo, 1, 64), next_hi = __shfl_down(key_hi, 1, 64);
     const bool tail = (lane == 63) || next_lo != key_lo || next_hi != key_hi;
-    const uint64_t ballot_multi = __ballot(!head);
-    if (ballot_multi != 0) {  // some run has length > 1 in this wave: segmented sums
+    if (__ballot(!head) != 0) {  // some run has length > 1 in this wave: segmented sums
+        int start = head ? lane : 0;   // run start lane, by a max-scan of head positions
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int s2 = __shfl_up(start, o, 64);
+            if (lane >= o) start = max(start, s2);
+        }
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
             const bool take = (lane - o) >= start;
@@ -168,15 +177,47 @@ __global__ void __launch_bounds__(256) hash_encode_bwd_kernel(
             }
         }
     }
-    if (!valid || !tail) return;
+    const bool emit = valid && tail;
     float* tab = hp.dtables[lvl];
     const uint32_t bx = (uint32_t)ax.base, by = (uint32_t)ay.base, bz = (uint32_t)az.base;
+    if constexpr (!COALESCE) {
+        if (!emit) return;
 #pragma unroll
-    for (int c = 0; c < 8; ++c) {
-        const uint32_t h = spatial_hash3(bx + ((c >> 2) & 1), by + ((c >> 1) & 1), bz + (c & 1), hp.mask);
-        atomic_add_f32(tab + 2 * h + 0, cgx[c]);
-        atomic_add_f32(tab + 2 * h + 1, cgy[c]);
+        for (int c = 0; c < 8; ++c) {
+            const uint32_t h = spatial_hash3(bx + ((c >> 2) & 1), by + ((c >> 1) & 1), bz + (c & 1), hp.mask);
+            atomic_add_f32(tab + 2 * h + 0, cgx[c]);
+            atomic_add_f32(tab + 2 * h + 1, cgy[c]);
+        }
+    } else {
+        __shared__ float s_val[4][64][17];
+        __shared__ uint32_t s_h[4][64][9];
+        const int wv = threadIdx.x >> 6;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            s_h[wv][lane][c] = emit ? spatial_hash3(bx + ((c >> 2) & 1), by + ((c >> 1) & 1), bz + (c & 1), hp.mask)
+                                    : kSkip;
+            s_val[wv][lane][2 * c + 0] = cgx[c];
+            s_val[wv][lane][2 * c + 1] = cgy[c];
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#pragma unroll 4
+        for (int r = 0; r < 16; ++r) {
+            const int d = r * 64 + lane;
+            const int item = d >> 4, within = d & 15;
+            const int c = ((within >> 1) & 1) * 4 + (within >> 2);   // i*4 + pair(j,k)
+            const int f = within & 1;
+            const uint32_t h = s_h[wv][item][c];
+            const float v = s_val[wv][item][2 * c + f];
+            if (h != kSkip && v != 0.f) atomic_add_f32(tab + 2 * h + f, v);
+        }
     }
+}
+
+// NERF_HASH_BWD=0 selects the per-lane-atomics variant (A/B measurements); default coalesced.
+static bool bwd_coalesced() {
+    const char* e = getenv("NERF_HASH_BWD");
+    return !(e && e[0] == '0');
 }
 
 }  // namespace nerf
@@ -225,8 +266,12 @@ extern "C" int nerf_hash_encode_bwd(const float* d_xyz, int64_t n_points, const 
     for (int a = 0; a < 3; ++a) { hp.bmin[a] = bbox_min3[a]; hp.bmax[a] = bbox_max3[a]; }
     hp.mask = (uint32_t)((1u << log2_T) - 1u);
     dim3 grid(blocks_for(n_points, 256), n_levels);
-    hipLaunchKernelGGL(hash_encode_bwd_kernel, grid, dim3(256), 0, as_stream(stream), d_xyz, n_points, hp,
-                       d_dfeat, feat_stride_point, feat_stride_level);
+    if (bwd_coalesced())
+        hipLaunchKernelGGL(hash_encode_bwd_kernel<true>, grid, dim3(256), 0, as_stream(stream), d_xyz, n_points, hp,
+                           d_dfeat, feat_stride_point, feat_stride_level);
+    else
+        hipLaunchKernelGGL(hash_encode_bwd_kernel<false>, grid, dim3(256), 0, as_stream(stream), d_xyz, n_points, hp,
+                           d_dfeat, feat_stride_point, feat_stride_level);
     NERF_CHECK_LAUNCH("hash_encode_bwd");
     return NERF_OK;
 }

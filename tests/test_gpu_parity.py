@@ -104,29 +104,41 @@ def test_mlp_fwd_bwd(nerf, gpu, golden):
 
 
 def test_mlp_large_vs_torch_fp32(nerf, gpu):
-    """262,144 points (the coarse pass): forward and weight grads against a plain PyTorch fp32 MLP."""
+    """262,144 points (the coarse pass): forward against a plain PyTorch fp32 MLP; weight grads (sums
+    over 262,144 points) against an fp64 reference, bounded by fp32 summation error relative to the
+    sum of |terms| (the plain fp32 torch GEMM is held to the same bound)."""
     torch.manual_seed(0)
     net = nerf.NeRFSmall(2, 64, 15, 3, 64, 32, 16).to(gpu)
     x = (torch.randn(262144, 48, device=gpu) * 0.5)
     graw = torch.randn(262144, 4, device=gpu)
     raw = net(x)
-    W = {k: p.detach().clone().requires_grad_(True) for k, p in net.named_parameters()}
     torch.backends.cuda.matmul.allow_tf32 = False
-    h = torch.relu(x[:, :32] @ W["sigma_net.0.weight"].t())
-    o = h @ W["sigma_net.1.weight"].t()
-    c = torch.relu(torch.cat([x[:, 32:], o[:, 1:]], -1) @ W["color_net.0.weight"].t())
-    c = torch.relu(c @ W["color_net.1.weight"].t())
-    ref = torch.cat([c @ W["color_net.2.weight"].t(), o[:, :1]], -1)
-    torch.testing.assert_close(raw.detach(), ref.detach(), rtol=1e-4, atol=1e-5)
+
+    def ref_mlp(W, xx):
+        h = torch.relu(xx[:, :32] @ W["sigma_net.0.weight"].t())
+        o = h @ W["sigma_net.1.weight"].t()
+        c = torch.relu(torch.cat([xx[:, 32:], o[:, 1:]], -1) @ W["color_net.0.weight"].t())
+        c = torch.relu(c @ W["color_net.1.weight"].t())
+        return torch.cat([c @ W["color_net.2.weight"].t(), o[:, :1]], -1), (h, o, c)
+
+    W32 = {k: p.detach().clone().requires_grad_(True) for k, p in net.named_parameters()}
+    W64 = {k: p.detach().double().clone().requires_grad_(True) for k, p in net.named_parameters()}
+    ref32, _ = ref_mlp(W32, x)
+    ref64, _ = ref_mlp(W64, x.double())
+    torch.testing.assert_close(raw.detach(), ref32.detach(), rtol=1e-4, atol=1e-5)
     (raw * graw).sum().backward()
-    (ref * graw).sum().backward()
-    # weight grads are sums over 262,144 points with cancellation: compare at fp32 summation level,
-    # elementwise against the tensor's own scale and in norm
+    (ref32 * graw).sum().backward()
+    (ref64 * graw.double()).sum().backward()
+    # |terms| bound: the same backward on |W|, |x|, |graw| (an upper bound of sum |g_i x_j| per entry)
+    Wabs = {k: p.detach().double().abs().requires_grad_(True) for k, p in net.named_parameters()}
+    refabs, _ = ref_mlp(Wabs, x.double().abs())
+    (refabs * graw.double().abs()).sum().backward()
     for k, p in net.named_parameters():
-        ref_g = W[k].grad
-        scale = ref_g.abs().max().item()
-        torch.testing.assert_close(p.grad, ref_g, rtol=1e-4, atol=1e-5 * scale)
-        assert (p.grad - ref_g).norm().item() <= 1e-5 * ref_g.norm().item()
+        bound = 2e-5 * Wabs[k].grad + 1e-6
+        err = (p.grad.double() - W64[k].grad).abs()
+        err_torch = (W32[k].grad.double() - W64[k].grad).abs()
+        assert (err <= bound).all(), f"{k}: max err/bound {(err / bound).max().item():.3f}"
+        assert (err_torch <= bound).all(), f"{k}: the fp32 torch reference exceeds the bound"
 
 
 def test_composite_fwd_bwd(nerf, gpu, golden):
@@ -228,7 +240,14 @@ def test_render_end_to_end(nerf, gpu, golden):
 
 
 def test_train_step_and_radam(nerf, gpu, golden):
-    """Seven reference training iterations (render + losses + backward + RAdam + lr decay)."""
+    """Seven reference training iterations (render + losses + backward + RAdam + lr decay).
+
+    The fixture sits at initialisation (tables U(-1e-4, 1e-4)): sigma ~ 1e-4, so alpha =
+    1 - exp(-relu(sigma)*delta) is cancellation-dominated (a ~ 1e-7; one ulp of exp(-a) is ~50 %
+    of alpha) in ANY fp32 implementation, and the CPU reference (Sleef exp) and the GPU (ocml exp)
+    round it differently. Every gradient therefore carries O(1e-3) relative noise at this point;
+    the checks below are at that level: losses 1e-3, MLP grads in norm 2e-2, table-gradient
+    checksums 5e-3, parameters after 7 steps (2 RAdam updates) 1e-3."""
     g = golden("f10_train")
     emb = _embedder(nerf, gpu, 1024, closed_form_table(scale=1e-4, salt=3))
     kw = _render_kwargs(nerf, gpu, {**{k.replace("coarse0_", "coarse_T_"): v for k, v in g.items()},
@@ -248,21 +267,19 @@ def test_train_step_and_radam(nerf, gpu, golden):
         loss = l_img + l_img0 + l_sp
         loss.backward()
         if step == 0:
-            # l_sp (1e-10 * entropy) sits on alpha = 1 - exp(-a) with a ~ 1e-7 at init: a 1-ulp exp
-            # difference (Sleef vs ocml) is O(1) relative there, so it is checked loosely; it
-            # contributes 1e-11 of the loss.
-            np.testing.assert_allclose([l_img.item(), l_img0.item(), loss.item()], g["loss0"][[0, 1, 3]], rtol=1e-4)
+            np.testing.assert_allclose([l_img.item(), l_img0.item(), loss.item()], g["loss0"][[0, 1, 3]], rtol=1e-3)
             np.testing.assert_allclose(l_sp.item(), g["loss0"][2], rtol=5e-2)
-            for k, p in coarse.named_parameters():
-                np.testing.assert_allclose(p.grad.cpu().numpy(), g["gcoarse_" + k.replace(".", "_")], rtol=2e-3,
-                                           atol=1e-6, err_msg=k)
-            for k, p in fine.named_parameters():
-                np.testing.assert_allclose(p.grad.cpu().numpy(), g["gfine_" + k.replace(".", "_")], rtol=2e-3,
-                                           atol=1e-6, err_msg=k)
+            for prefix, net in (("gcoarse_", coarse), ("gfine_", fine)):
+                for k, p in net.named_parameters():
+                    want = g[prefix + k.replace(".", "_")]
+                    rel = np.linalg.norm(p.grad.cpu().numpy() - want) / np.linalg.norm(want)
+                    assert rel < 2e-2, f"{prefix}{k}: relative grad error {rel:.2e}"
             for i, e in enumerate(emb.embeddings):
                 gd = e.weight.grad.double()
-                np.testing.assert_allclose([gd.sum().item(), (gd * gd).sum().item(), gd.abs().sum().item()],
-                                           g["gtable_checksum"][i], rtol=2e-3, atol=1e-10)
+                cs = g["gtable_checksum"][i]
+                np.testing.assert_allclose([(gd * gd).sum().item(), gd.abs().sum().item()], cs[1:], rtol=5e-3,
+                                           err_msg=f"level {i}")
+                assert abs(gd.sum().item() - cs[0]) <= 1e-2 * cs[2], f"level {i} gradient sum"
         opt.step()
         for grp in opt.param_groups:
             grp["lr"] = 5e-4 * (0.1 ** (step / (500 * 1000)))

@@ -1,0 +1,94 @@
+#!/usr/bin/env python3
+"""Kernel micro-benchmark: A/B variants of the hot kernels in ONE process, interleaved rounds
+(cdna_hip_programming.md §5.4 rule 24), on the metric configuration's point sets (4096 lego rays,
+64 coarse / 192 fine sorted samples per ray). Prints a JSON summary."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import indoor_nerf_amd as nerf  # noqa: E402
+from indoor_nerf_amd import _lib  # noqa: E402
+from indoor_nerf_amd.synthetic import blender_bbox, blender_rays  # noqa: E402
+
+
+def ray_points(R, S, dev, seed=0):
+    ro, rd = (torch.from_numpy(v).to(dev) for v in blender_rays(R, seed=seed))
+    g = torch.Generator(device=dev).manual_seed(seed)
+    z = torch.sort(2 + 4 * torch.rand(R, S, device=dev, generator=g), -1)[0]
+    return (ro[:, None] + rd[:, None] * z[..., None]).reshape(-1, 3).contiguous(), rd
+
+
+def timeit(fn, reps=20, warm=3):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        fn()
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    return float(np.median(ts)), float(np.min(ts))
+
+
+def main():
+    dev = torch.device("cuda:0")
+    lo, hi = blender_bbox()
+    emb = nerf.HashEmbedder((torch.from_numpy(lo), torch.from_numpy(hi)), finest_resolution=1024).to(dev)
+    with torch.no_grad():
+        for e in emb.embeddings:
+            e.weight.uniform_(-0.05, 0.05)
+    out = {}
+    for name, S in (("coarse", 64), ("fine", 192)):
+        pts, rd = ray_points(4096, S, dev)
+        P = pts.shape[0]
+        meta = emb._meta
+        feat = torch.empty(16, P, 2, device=dev)
+        keep = torch.empty(P, device=dev, dtype=torch.bool)
+        dfeat = torch.randn(16, P, 2, device=dev)
+        grads = [torch.zeros_like(e.weight) for e in emb.embeddings]
+
+        def fwd():
+            _lib.call("nerf_hash_encode_fwd", _lib.ptr(pts), P, meta["bmin"], meta["bmax"], meta["res"], 16, 19,
+                      _lib.ptr_array(emb.tables()), _lib.ptr(feat), 2, 2 * P, _lib.ptr(keep, dtype=torch.bool),
+                      _lib.stream())
+
+        def bwd():
+            _lib.call("nerf_hash_encode_bwd", _lib.ptr(pts), P, meta["bmin"], meta["bmax"], meta["res"], 16, 19,
+                      _lib.ptr(dfeat), 2, 2 * P, _lib.ptr_array(grads), _lib.stream())
+
+        res = {"points": P, "fwd_ms": timeit(fwd)}
+        # correctness of the variants against each other
+        ref = None
+        for v in ("0", "1"):
+            os.environ["NERF_HASH_BWD"] = v
+            for g in grads:
+                g.zero_()
+            bwd()
+            cur = torch.stack(grads).clone()
+            if ref is None:
+                ref = cur
+            else:
+                err = ((cur - ref).abs().max() / ref.abs().max()).item()
+                res["bwd_variant_maxrel_diff"] = err
+        rounds = {"0": [], "1": []}
+        for _ in range(5):
+            for v in ("0", "1"):
+                os.environ["NERF_HASH_BWD"] = v
+                rounds[v].append(timeit(bwd, reps=5, warm=1)[0])
+        res["bwd_ms_per_variant"] = {("atomic_per_lane" if v == "0" else "coalesced"): float(np.median(t))
+                                     for v, t in rounds.items()}
+        out[name] = res
+    os.environ["NERF_HASH_BWD"] = "1"
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
