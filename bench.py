@@ -121,6 +121,7 @@ def main():
     torch.manual_seed(0)
     nerf.manual_seed(1234 + rank)
     kw, _, _, grad_vars, opt = nerf.create_nerf(args, device=dev)
+    kw.update(near=2.0, far=6.0)                     # train() adds the Blender bounds (run_nerf.py:768-770,865-869)
     params = grad_vars + list(kw["embed_fn"].parameters())
     nerf.broadcast_params(params)
     arena = nerf.GradArena(params)

@@ -249,7 +249,7 @@ def test_train_step_and_radam(nerf, gpu, golden):
     the checks below are at that level: losses 1e-3, MLP grads in norm 2e-2, table-gradient
     checksums 5e-3, parameters after 7 steps (2 RAdam updates) 1e-3."""
     g = golden("f10_train")
-    emb = _embedder(nerf, gpu, 1024, closed_form_table(scale=1e-4, salt=3))
+    emb = _embedder(nerf, gpu, 1024, closed_form_table(scale=float(g["table_scale"]), salt=3))
     kw = _render_kwargs(nerf, gpu, {**{k.replace("coarse0_", "coarse_T_"): v for k, v in g.items()},
                                     **{k.replace("fine0_", "fine_T_"): v for k, v in g.items()}},
                         "T", emb, 64, 128, 1.0, 0.0, False)
@@ -337,6 +337,7 @@ def test_train_step_full_size_finite(nerf, gpu):
     args = nerf.make_args(bounding_box=(torch.from_numpy(lo), torch.from_numpy(hi)), finest_res=1024, N_samples=64,
                           N_importance=128, white_bkgd=True)
     kw, _, _, grad_vars, opt = nerf.create_nerf(args, device=gpu)
+    kw.update(near=2.0, far=6.0)
     ro, rd = synthetic_rays(4096, seed=4)
     rays = (torch.from_numpy(ro).to(gpu), torch.from_numpy(rd).to(gpu))
     target = torch.rand(4096, 3, device=gpu)

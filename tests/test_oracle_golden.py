@@ -162,7 +162,7 @@ def test_tv_loss(golden, oracle):
 def test_train_step(golden, oracle):
     """One reference training iteration and seven RAdam steps (run_nerf.py:1007-1162, 1289-1293)."""
     g = golden("f10_train")
-    table = closed_form_table(scale=1e-4, salt=3)
+    table = closed_form_table(scale=float(g["table_scale"]), salt=3)
     tabs = _tables(table, requires_grad=True)
     cw = {k: v.clone().requires_grad_(True) for k, v in _mlp(g, "coarse0_").items()}
     fw = {k: v.clone().requires_grad_(True) for k, v in _mlp(g, "fine0_").items()}

@@ -90,5 +90,39 @@ def main():
     print(json.dumps(out, indent=1))
 
 
+
+
+def mlp_bench():
+    """MLP fwd/bwd kernels on the coarse (262,144) and fine (786,432) point counts."""
+    dev = torch.device("cuda:0")
+    torch.manual_seed(0)
+    net = nerf.NeRFSmall(2, 64, 15, 3, 64, 32, 16).to(dev)
+    out = {}
+    for P in (262144, 786432):
+        feat = torch.randn(16, P, 2, device=dev) * 0.3
+        vd = torch.nn.functional.normalize(torch.randn(P // 64, 3, device=dev), dim=-1)
+        keep = torch.ones(P, device=dev, dtype=torch.bool)
+        raw = torch.empty(P, 4, device=dev)
+        graw = torch.randn(P, 4, device=dev)
+        dfeat = torch.empty_like(feat)
+        from indoor_nerf_amd.field import _grads_struct, _weights_struct
+        W = net.mlp_weights()
+
+        def fwd():
+            _lib.call("nerf_mlp_fwd", _lib.ptr(feat), 2, 2 * P, None, 0, _lib.ptr(vd), 64,
+                      _lib.ptr(keep, dtype=torch.bool), P, _weights_struct(W), _lib.ptr(raw), _lib.stream())
+
+        def bwd():
+            _lib.call("nerf_mlp_bwd", _lib.ptr(feat), 2, 2 * P, None, 0, _lib.ptr(vd), 64,
+                      _lib.ptr(keep, dtype=torch.bool), P, _weights_struct(W), _lib.ptr(graw), _grads_struct(W),
+                      _lib.ptr(dfeat), None, _lib.stream())
+
+        out[P] = {"fwd_ms": timeit(fwd), "bwd_ms": timeit(bwd)}
+    print(json.dumps(out, indent=1))
+
+
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == "mlp":
+        mlp_bench()
+    else:
+        main()
