@@ -117,7 +117,39 @@ def mlp_bench():
                       _lib.ptr(keep, dtype=torch.bool), P, _weights_struct(W), _lib.ptr(graw), _grads_struct(W),
                       _lib.ptr(dfeat), None, _lib.stream())
 
-        out[P] = {"fwd_ms": timeit(fwd), "bwd_ms": timeit(bwd)}
+        res = {}
+        # correctness of the MLP variants against each other (raw and weight grads)
+        outs = {}
+        for v in ("1", "2"):
+            os.environ["NERF_MLP"] = v
+            fwd()
+            for w in W:
+                w.grad = None
+            bwd()
+            outs[v] = (raw.clone(), [w.grad.clone() for w in W], dfeat.clone())
+        res["raw_maxabs_diff"] = (outs["1"][0] - outs["2"][0]).abs().max().item()
+        res["dW_maxrel_diff"] = max(((a - b).abs().max() / b.abs().max()).item() for a, b in zip(outs["1"][1], outs["2"][1]))
+        res["dfeat_maxabs_diff"] = (outs["1"][2] - outs["2"][2]).abs().max().item()
+        res["dfeat_absmax"] = outs["2"][2].abs().max().item()
+        # run-to-run determinism of each variant (dfeat has no atomics: must be bit-identical)
+        for v in ("1", "2"):
+            os.environ["NERF_MLP"] = v
+            fwd()
+            bwd()
+            res[f"v{v}_dfeat_rerun_diff"] = (dfeat - outs[v][2]).abs().max().item()
+        for w in W:
+            w.grad = None
+        _grads_struct(W)
+        rounds = {"1": {"fwd": [], "bwd": []}, "2": {"fwd": [], "bwd": []}}
+        for _ in range(5):
+            for v in ("1", "2"):
+                os.environ["NERF_MLP"] = v
+                rounds[v]["fwd"].append(timeit(fwd, reps=5, warm=1)[0])
+                rounds[v]["bwd"].append(timeit(bwd, reps=5, warm=1)[0])
+        for v, d in rounds.items():
+            res[f"v{v}"] = {k: float(np.median(t)) for k, t in d.items()}
+        out[P] = res
+    os.environ["NERF_MLP"] = "2"
     print(json.dumps(out, indent=1))
 
 
