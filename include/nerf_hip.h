@@ -18,6 +18,7 @@
 #ifndef NERF_HIP_H
 #define NERF_HIP_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -58,6 +59,20 @@ int nerf_hash_encode_bwd(const float* d_xyz, int64_t n_points,
                          const float* level_res, int n_levels, int log2_T,
                          const float* d_dfeat, int64_t feat_stride_point, int64_t feat_stride_level,
                          float* const* d_dtables, void* stream);
+
+/* Same, on the binned ("owner computes") path: the entries are first written, sorted by table
+ * slice, into a caller-owned device workspace (plain stores), then one workgroup per 2^14-row slice
+ * sums them in LDS and adds the slice into d_dtables once. Replaces the memory-side float atomics
+ * of nerf_hash_encode_bwd, whose request rate bounds that path. The workspace needs no
+ * initialisation; calls sharing one must be stream-ordered. workspace_bytes >=
+ * nerf_hash_encode_bwd_workspace_bytes(n_levels, log2_T, n_points) (0: path unavailable for this
+ * log2_T, and a NULL workspace gives nerf_hash_encode_bwd). */
+size_t nerf_hash_encode_bwd_workspace_bytes(int n_levels, int log2_T, int64_t n_points);
+int nerf_hash_encode_bwd_ws(const float* d_xyz, int64_t n_points,
+                            const float* bbox_min3, const float* bbox_max3,
+                            const float* level_res, int n_levels, int log2_T,
+                            const float* d_dfeat, int64_t feat_stride_point, int64_t feat_stride_level,
+                            float* const* d_dtables, void* d_workspace, size_t workspace_bytes, void* stream);
 
 /* ---- spherical harmonics, degree 4 (SHEncoder.forward, hash_encoding.py:153-191) ---------- */
 int nerf_sh4_fwd(const float* d_dirs, int64_t n, float* d_out /* [n,16] */, void* stream);
@@ -176,6 +191,19 @@ int nerf_tv_fwd(const float* const* d_tables, int n_levels, int log2_T, const in
 int nerf_tv_bwd(const float* const* d_tables, int n_levels, int log2_T, const int64_t* min_vertex,
                 const int* cube, const float* d_scale /* device [n_levels] */, float* const* d_dtables,
                 void* stream);
+
+/* ---- training-loss head (run_nerf.py:1011-1037: img2mse of both passes, sparsity, TV, mse2psnr) ----
+ * fwd: device scalars loss, img_loss (fine-pass MSE), psnr; rgb0 / sparsity / sparsity0 / tv may be NULL.
+ *      loss = img + mse(rgb0) + sparse_w * (sum(sp) + sum(sp0)) + tv_w * sum_l tv[l]
+ * bwd: d_grad_loss is a device scalar; outputs d rgb = (g/3R) * 2 (rgb - t), d sp = sparse_w g,
+ *      d tv[l] = tv_w g (NULL outputs are skipped). */
+int nerf_train_loss_fwd(const float* d_rgb, const float* d_rgb0, const float* d_target, int64_t n_rays,
+                        const float* d_sparsity, const float* d_sparsity0, float sparse_w, const float* d_tv,
+                        int n_tv, float tv_w, float* d_loss, float* d_img_loss, float* d_psnr, void* stream);
+int nerf_train_loss_bwd(const float* d_rgb, const float* d_rgb0, const float* d_target, int64_t n_rays,
+                        float sparse_w, int n_tv, float tv_w, const float* d_grad_loss, float* d_grad_rgb,
+                        float* d_grad_rgb0, float* d_grad_sparsity, float* d_grad_sparsity0, float* d_grad_tv,
+                        void* stream);
 
 #ifdef __cplusplus
 }

@@ -43,6 +43,8 @@ SIGNATURES = {
                              c_vp, c_i64, c_i64, c_vp, c_vp],
     "nerf_hash_encode_bwd": [c_vp, c_i64, c_f32p, c_f32p, c_f32p, c_int, c_int, c_vp, c_i64, c_i64,
                              ctypes.POINTER(c_vp), c_vp],
+    "nerf_hash_encode_bwd_ws": [c_vp, c_i64, c_f32p, c_f32p, c_f32p, c_int, c_int, c_vp, c_i64, c_i64,
+                                ctypes.POINTER(c_vp), c_vp, ctypes.c_size_t, c_vp],
     "nerf_sh4_fwd": [c_vp, c_i64, c_vp, c_vp],
     "nerf_mlp_fwd": [c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, ctypes.POINTER(MlpWeights),
                      c_vp, c_vp],
@@ -60,6 +62,10 @@ SIGNATURES = {
     "nerf_tv_fwd": [ctypes.POINTER(c_vp), c_int, c_int, ctypes.POINTER(c_i64), ctypes.POINTER(c_int), c_vp, c_vp],
     "nerf_tv_bwd": [ctypes.POINTER(c_vp), c_int, c_int, ctypes.POINTER(c_i64), ctypes.POINTER(c_int), c_vp,
                     ctypes.POINTER(c_vp), c_vp],
+    "nerf_train_loss_fwd": [c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, ctypes.c_float, c_vp, c_int, ctypes.c_float,
+                            c_vp, c_vp, c_vp, c_vp],
+    "nerf_train_loss_bwd": [c_vp, c_vp, c_vp, c_i64, ctypes.c_float, c_int, ctypes.c_float, c_vp, c_vp, c_vp,
+                            c_vp, c_vp, c_vp, c_vp],
 }
 
 _lib = None
@@ -78,6 +84,8 @@ def load():
     lib.nerf_last_error.argtypes = []
     lib.nerf_abi_version.restype = c_int
     lib.nerf_abi_version.argtypes = []
+    lib.nerf_hash_encode_bwd_workspace_bytes.restype = ctypes.c_size_t
+    lib.nerf_hash_encode_bwd_workspace_bytes.argtypes = [c_int, c_int, c_i64]
     for name, argtypes in SIGNATURES.items():
         fn = getattr(lib, name)
         fn.argtypes = argtypes
@@ -87,7 +95,7 @@ def load():
 
 
 def exported_symbols():
-    return ["nerf_last_error", "nerf_abi_version"] + list(SIGNATURES)
+    return ["nerf_last_error", "nerf_abi_version", "nerf_hash_encode_bwd_workspace_bytes"] + list(SIGNATURES)
 
 
 _TIMING = None   # when a list: (name, start_event, end_event) per launch, recorded on the current stream

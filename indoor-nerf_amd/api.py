@@ -4,7 +4,7 @@ from . import _lib
 from .dist import GradArena, broadcast_params, init_process_group, shard
 from .field import NeRFSmall, batchify, run_network
 from .hashgrid import HashEmbedder, SHEncoder, level_resolutions
-from .losses import sigma_sparsity_loss, total_variation_all, total_variation_loss
+from .losses import sigma_sparsity_loss, total_variation_all, total_variation_loss, train_loss
 from .model import create_nerf, make_args, save_checkpoint, train_step
 from .optim import RAdam
 from .render import (batchify_rays, get_rays, get_rays_np, img2mse, manual_seed, mse2psnr, ndc_rays, raw2outputs,
@@ -13,7 +13,7 @@ from .render import (batchify_rays, get_rays, get_rays_np, img2mse, manual_seed,
 __all__ = ["HashEmbedder", "SHEncoder", "NeRFSmall", "RAdam", "run_network", "batchify", "batchify_rays", "render",
            "render_rays", "raw2outputs", "sample_pdf", "get_rays", "get_rays_np", "ndc_rays", "img2mse", "mse2psnr",
            "to8b", "create_nerf", "make_args", "save_checkpoint", "train_step", "total_variation_loss",
-           "total_variation_all", "sigma_sparsity_loss", "level_resolutions", "GradArena", "init_process_group",
+           "total_variation_all", "train_loss", "sigma_sparsity_loss", "level_resolutions", "GradArena", "init_process_group",
            "shard", "broadcast_params", "manual_seed", "load_library"]
 
 

@@ -31,6 +31,14 @@ struct HashGradParams {
     float bmin[3];
     float bmax[3];
     uint32_t mask;
+    // binned path (MODE 3): per (level, 256-point chunk) a region of kChunkCap entries sorted by
+    // owner slice, plus the slice offsets of each region.
+    uint16_t* bin_h;      // entry row within its owner slice
+    float2* bin_g;        // entry (d feat0, d feat1)
+    int32_t* bin_off;     // [L][nchunks][n_owner + 1]
+    int nchunks;
+    int slice_log2;       // owner slice = 2^slice_log2 rows (LDS: 8 B per row)
+    int owner_log2;       // owners per level = 2^owner_log2
 };
 
 // Per-axis voxel math of utils.py:103-112, fp32, exact op order.
@@ -115,7 +123,20 @@ __device__ __forceinline__ void atomic_add_f32(float* p, float v) {
 // 4 dwords of a pair usually share one 64-B segment and leave as ONE atomic request.
 constexpr uint32_t kSkip = 0xFFFFFFFFu;
 
-template <bool COALESCE>
+// MODE 3 (binned, "owner computes"): float atomics execute at the memory side at one chip-wide
+// rate of 64-B requests (MI355X_MICROARCH.md, Global float atomics), and the hash scatters every
+// corner pair to its own line, so the atomic path is request-bound (plus same-line serialisation
+// at the coarse levels, where every ray crosses the same few thousand voxels). The binned path
+// replaces the memory-side atomics: this kernel writes each (row, d feat) entry into a per-chunk
+// region sorted by owner slice (plain stores), and hash_bwd_owner_kernel sums each slice in LDS.
+constexpr int kChunkCap = 256 * 8;        // entries per 256-point chunk (8 corners per point)
+constexpr int kMaxSliceLog2 = 14;         // owner slice: 2^14 rows x 8 B = 128 KiB of LDS
+constexpr int kMaxOwnersLog2 = 6;
+constexpr int kMaxOwners = 1 << kMaxOwnersLog2;
+
+// MODE 0: per-lane atomics; 1: coalesced re-issue (default); 2: as 1 without the atomics (cost floor,
+// A/B measurement only: results are wrong).
+template <int MODE>
 __global__ void __launch_bounds__(256) hash_encode_bwd_kernel(
     const float* __restrict__ xyz, int64_t n, HashGradParams hp,
     const float* __restrict__ dfeat, int64_t sp, int64_t sl) {
@@ -180,13 +201,56 @@ __global__ void __launch_bounds__(256) hash_encode_bwd_kernel(
     const bool emit = valid && tail;
     float* tab = hp.dtables[lvl];
     const uint32_t bx = (uint32_t)ax.base, by = (uint32_t)ay.base, bz = (uint32_t)az.base;
-    if constexpr (!COALESCE) {
+    if constexpr (MODE == 0) {
         if (!emit) return;
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
             const uint32_t h = spatial_hash3(bx + ((c >> 2) & 1), by + ((c >> 1) & 1), bz + (c & 1), hp.mask);
             atomic_add_f32(tab + 2 * h + 0, cgx[c]);
             atomic_add_f32(tab + 2 * h + 1, cgy[c]);
+        }
+    } else if constexpr (MODE == 3) {
+        // Bin: count this chunk's entries per owner slice (LDS atomics), scan, and store each entry
+        // at its slot of the chunk's region. The region (<= 2048 entries) is written by this block
+        // alone within a few microseconds, so L2 merges the scattered 10-B writes into whole lines.
+        __shared__ uint32_t s_cnt[kMaxOwners];
+        __shared__ uint32_t s_start[kMaxOwners + 1];
+        const int n_own = 1 << hp.owner_log2;
+        if (threadIdx.x < n_own) s_cnt[threadIdx.x] = 0;
+        __syncthreads();
+        uint32_t hh[8], pos[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            hh[c] = spatial_hash3(bx + ((c >> 2) & 1), by + ((c >> 1) & 1), bz + (c & 1), hp.mask);
+            pos[c] = (emit && (cgx[c] != 0.f || cgy[c] != 0.f)) ? atomicAdd(&s_cnt[hh[c] >> hp.slice_log2], 1u)
+                                                                : kSkip;
+        }
+        __syncthreads();
+        const size_t row = (size_t)lvl * hp.nchunks + blockIdx.x;
+        if (threadIdx.x < 64) {   // exclusive scan of <= 64 counters in wave 0
+            const uint32_t v = lane < n_own ? s_cnt[lane] : 0u;
+            uint32_t inc = v;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t t = __shfl_up(inc, o, 64);
+                if (lane >= o) inc += t;
+            }
+            if (lane < n_own) {
+                s_start[lane] = inc - v;
+                hp.bin_off[row * (n_own + 1) + lane] = (int32_t)(inc - v);
+            }
+            if (lane == n_own - 1) hp.bin_off[row * (n_own + 1) + n_own] = (int32_t)inc;
+        }
+        __syncthreads();
+        const size_t base = row * kChunkCap;
+        const uint32_t smask = (1u << hp.slice_log2) - 1u;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            if (pos[c] != kSkip) {
+                const size_t i = base + s_start[hh[c] >> hp.slice_log2] + pos[c];
+                hp.bin_h[i] = (uint16_t)(hh[c] & smask);
+                hp.bin_g[i] = make_float2(cgx[c], cgy[c]);
+            }
         }
     } else {
         __shared__ float s_val[4][64][17];
@@ -209,15 +273,109 @@ __global__ void __launch_bounds__(256) hash_encode_bwd_kernel(
             const int f = within & 1;
             const uint32_t h = s_h[wv][item][c];
             const float v = s_val[wv][item][2 * c + f];
-            if (h != kSkip && v != 0.f) atomic_add_f32(tab + 2 * h + f, v);
+            if constexpr (MODE == 1) {
+                if (h != kSkip && v != 0.f) atomic_add_f32(tab + 2 * h + f, v);
+            } else {
+                if (h != kSkip && v == 1234.5f) tab[2 * h + f] = v;
+            }
         }
     }
 }
 
-// NERF_HASH_BWD=0 selects the per-lane-atomics variant (A/B measurements); default coalesced.
-static bool bwd_coalesced() {
+// ---- owner pass of the binned backward ----------------------------------------------------
+// Block (o, l) owns rows [o * 2^slice_log2, (o+1) * 2^slice_log2) of level l's gradient table: it
+// sums every chunk's segment for that slice into LDS (ds_add_f32; fast, no memory-side requests)
+// and adds the slice into the table once, with plain coalesced loads and stores (sole writer).
+// Each wave takes 4 chunks per step so that 4 segment loads are in flight per lane.
+constexpr int kOwnerThreads = 1024;
+
+__global__ void __launch_bounds__(kOwnerThreads) hash_bwd_owner_kernel(HashGradParams hp) {
+    __shared__ __attribute__((aligned(16))) float2 s_slice[1 << kMaxSliceLog2];
+    const int o = blockIdx.x, lvl = blockIdx.y;
+    const int S = 1 << hp.slice_log2, n_own = 1 << hp.owner_log2;
+    for (int i = threadIdx.x; i < S; i += kOwnerThreads) s_slice[i] = make_float2(0.f, 0.f);
+    __syncthreads();
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    constexpr int kWaves = kOwnerThreads / 64, kGroup = 4;
+    for (int c0 = wave * kGroup; c0 < hp.nchunks; c0 += kWaves * kGroup) {
+        int st[kGroup], cnt[kGroup];
+        size_t base[kGroup];
+        int nmax = 0;
+#pragma unroll
+        for (int k = 0; k < kGroup; ++k) {
+            const int c = c0 + k;
+            cnt[k] = 0;
+            st[k] = 0;
+            base[k] = 0;
+            if (c < hp.nchunks) {
+                const size_t row = (size_t)lvl * hp.nchunks + c;
+                const int32_t* off = hp.bin_off + row * (n_own + 1) + o;
+                st[k] = off[0];
+                cnt[k] = off[1] - off[0];
+                base[k] = row * kChunkCap + st[k];
+            }
+            nmax = max(nmax, cnt[k]);
+        }
+        for (int i = lane; i < nmax; i += 64) {
+            uint16_t h[kGroup];
+            float2 g[kGroup];
+#pragma unroll
+            for (int k = 0; k < kGroup; ++k) {
+                if (i < cnt[k]) {
+                    h[k] = hp.bin_h[base[k] + i];
+                    g[k] = hp.bin_g[base[k] + i];
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < kGroup; ++k) {
+                if (i < cnt[k]) {
+                    atomicAdd(&s_slice[h[k]].x, g[k].x);
+                    atomicAdd(&s_slice[h[k]].y, g[k].y);
+                }
+            }
+        }
+    }
+    __syncthreads();
+    float2* dt = reinterpret_cast<float2*>(hp.dtables[lvl]) + (size_t)o * S;
+    for (int i = threadIdx.x; i < S; i += kOwnerThreads) {
+        const float2 v = s_slice[i];
+        if (v.x != 0.f || v.y != 0.f) {
+            const float2 t = dt[i];
+            dt[i] = make_float2(t.x + v.x, t.y + v.y);
+        }
+    }
+}
+
+struct BinPlan {
+    int slice_log2, owner_log2, nchunks;
+    size_t off_h, off_g, off_off, total;   // byte offsets in the workspace
+};
+
+// Binned path for log2_T in [1, kMaxSliceLog2 + log2(kMaxOwners)]: slices of min(2^14, T) rows.
+static bool make_bin_plan(int n_levels, int log2_T, int64_t n_points, BinPlan& B) {
+    if (log2_T < 1 || log2_T > kMaxSliceLog2 + kMaxOwnersLog2 || n_points < 0) return false;
+    B.slice_log2 = log2_T < kMaxSliceLog2 ? log2_T : kMaxSliceLog2;
+    B.owner_log2 = log2_T - B.slice_log2;
+    B.nchunks = (int)((n_points + 255) / 256);
+    const size_t entries = (size_t)n_levels * B.nchunks * kChunkCap;
+    const size_t offs = (size_t)n_levels * B.nchunks * ((1 << B.owner_log2) + 1);
+    auto up = [](size_t v) { return (v + 255) & ~(size_t)255; };
+    B.off_g = 0;
+    B.off_h = up(entries * sizeof(float2));
+    B.off_off = B.off_h + up(entries * sizeof(uint16_t));
+    B.total = B.off_off + up(offs * sizeof(int32_t));
+    return true;
+}
+
+// NERF_HASH_BWD=0 / 1 / 2 select the per-lane-atomics / coalesced-atomics / no-atomics variants
+// (A/B measurements only; the binned path runs whenever the caller passes a workspace).
+// NERF_HASH_BWD=0 / 2 select the per-lane-atomics / no-atomics variants (A/B measurements only).
+static int bwd_mode() {
     const char* e = getenv("NERF_HASH_BWD");
-    return !(e && e[0] == '0');
+    if (e && e[0] == '0') return 0;
+    if (e && e[0] == '1') return 1;
+    if (e && e[0] == '2') return 2;
+    return 3;
 }
 
 }  // namespace nerf
@@ -248,10 +406,11 @@ extern "C" int nerf_hash_encode_fwd(const float* d_xyz, int64_t n_points, const 
     return NERF_OK;
 }
 
-extern "C" int nerf_hash_encode_bwd(const float* d_xyz, int64_t n_points, const float* bbox_min3,
-                                    const float* bbox_max3, const float* level_res, int n_levels, int log2_T,
-                                    const float* d_dfeat, int64_t feat_stride_point, int64_t feat_stride_level,
-                                    float* const* d_dtables, void* stream) {
+static int hash_encode_bwd_impl(const float* d_xyz, int64_t n_points, const float* bbox_min3,
+                                const float* bbox_max3, const float* level_res, int n_levels, int log2_T,
+                                const float* d_dfeat, int64_t feat_stride_point, int64_t feat_stride_level,
+                                float* const* d_dtables, void* d_workspace, size_t workspace_bytes,
+                                void* stream) {
     NERF_REQUIRE(n_points >= 0, "hash_encode_bwd: n_points < 0");
     NERF_REQUIRE(n_levels >= 1 && n_levels <= NERF_MAX_LEVELS, "hash_encode_bwd: n_levels %d", n_levels);
     NERF_REQUIRE(log2_T >= 1 && log2_T <= 30, "hash_encode_bwd: log2_T %d", log2_T);
@@ -265,13 +424,67 @@ extern "C" int nerf_hash_encode_bwd(const float* d_xyz, int64_t n_points, const 
     }
     for (int a = 0; a < 3; ++a) { hp.bmin[a] = bbox_min3[a]; hp.bmax[a] = bbox_max3[a]; }
     hp.mask = (uint32_t)((1u << log2_T) - 1u);
-    dim3 grid(blocks_for(n_points, 256), n_levels);
-    if (bwd_coalesced())
-        hipLaunchKernelGGL(hash_encode_bwd_kernel<true>, grid, dim3(256), 0, as_stream(stream), d_xyz, n_points, hp,
-                           d_dfeat, feat_stride_point, feat_stride_level);
-    else
-        hipLaunchKernelGGL(hash_encode_bwd_kernel<false>, grid, dim3(256), 0, as_stream(stream), d_xyz, n_points, hp,
-                           d_dfeat, feat_stride_point, feat_stride_level);
+    int mode = bwd_mode();
+    BinPlan B{};
+    if (mode == 3 && !(d_workspace != nullptr && make_bin_plan(n_levels, log2_T, n_points, B))) mode = 1;
+    if (mode == 3) {
+        NERF_REQUIRE(workspace_bytes >= B.total,
+                     "hash_encode_bwd: workspace %zu B < %zu B (nerf_hash_encode_bwd_workspace_bytes)",
+                     workspace_bytes, B.total);
+        char* ws = static_cast<char*>(d_workspace);
+        hp.bin_g = reinterpret_cast<float2*>(ws + B.off_g);
+        hp.bin_h = reinterpret_cast<uint16_t*>(ws + B.off_h);
+        hp.bin_off = reinterpret_cast<int32_t*>(ws + B.off_off);
+        hp.nchunks = B.nchunks;
+        hp.slice_log2 = B.slice_log2;
+        hp.owner_log2 = B.owner_log2;
+    }
+    const dim3 grid(blocks_for(n_points, 256), n_levels);
+    switch (mode) {
+        case 0:
+            hipLaunchKernelGGL(hash_encode_bwd_kernel<0>, grid, dim3(256), 0, as_stream(stream), d_xyz, n_points, hp,
+                               d_dfeat, feat_stride_point, feat_stride_level);
+            break;
+        case 1:
+            hipLaunchKernelGGL(hash_encode_bwd_kernel<1>, grid, dim3(256), 0, as_stream(stream), d_xyz, n_points, hp,
+                               d_dfeat, feat_stride_point, feat_stride_level);
+            break;
+        case 2:
+            hipLaunchKernelGGL(hash_encode_bwd_kernel<2>, grid, dim3(256), 0, as_stream(stream), d_xyz, n_points, hp,
+                               d_dfeat, feat_stride_point, feat_stride_level);
+            break;
+        default:
+            hipLaunchKernelGGL(hash_encode_bwd_kernel<3>, grid, dim3(256), 0, as_stream(stream), d_xyz, n_points, hp,
+                               d_dfeat, feat_stride_point, feat_stride_level);
+            NERF_CHECK_LAUNCH("hash_encode_bwd (bin)");
+            hipLaunchKernelGGL(hash_bwd_owner_kernel, dim3(1u << B.owner_log2, n_levels), dim3(kOwnerThreads), 0,
+                               as_stream(stream), hp);
+            break;
+    }
     NERF_CHECK_LAUNCH("hash_encode_bwd");
     return NERF_OK;
+}
+
+extern "C" size_t nerf_hash_encode_bwd_workspace_bytes(int n_levels, int log2_T, int64_t n_points) {
+    BinPlan B{};
+    if (n_levels < 1 || n_levels > NERF_MAX_LEVELS || !make_bin_plan(n_levels, log2_T, n_points, B)) return 0;
+    return B.total;
+}
+
+extern "C" int nerf_hash_encode_bwd(const float* d_xyz, int64_t n_points, const float* bbox_min3,
+                                    const float* bbox_max3, const float* level_res, int n_levels, int log2_T,
+                                    const float* d_dfeat, int64_t feat_stride_point, int64_t feat_stride_level,
+                                    float* const* d_dtables, void* stream) {
+    return hash_encode_bwd_impl(d_xyz, n_points, bbox_min3, bbox_max3, level_res, n_levels, log2_T, d_dfeat,
+                                feat_stride_point, feat_stride_level, d_dtables, nullptr, 0, stream);
+}
+
+extern "C" int nerf_hash_encode_bwd_ws(const float* d_xyz, int64_t n_points, const float* bbox_min3,
+                                       const float* bbox_max3, const float* level_res, int n_levels, int log2_T,
+                                       const float* d_dfeat, int64_t feat_stride_point, int64_t feat_stride_level,
+                                       float* const* d_dtables, void* d_workspace, size_t workspace_bytes,
+                                       void* stream) {
+    return hash_encode_bwd_impl(d_xyz, n_points, bbox_min3, bbox_max3, level_res, n_levels, log2_T, d_dfeat,
+                                feat_stride_point, feat_stride_level, d_dtables, d_workspace, workspace_bytes,
+                                stream);
 }

@@ -73,75 +73,93 @@ struct TVParams {
     float* loss;          // fwd: device [L]
 };
 
-__device__ __forceinline__ int tv_level(const TVParams& P, int64_t v) {
-    int l = 0;
-    while (l + 1 < P.L && v >= P.vstart[l + 1]) ++l;
-    return l;
-}
-
 __device__ __forceinline__ float2 tv_fetch(const float2* tab, const int* mv, int i, int j, int k, uint32_t mask) {
     return tab[spatial_hash3((uint32_t)(mv[0] + i), (uint32_t)(mv[1] + j), (uint32_t)(mv[2] + k), mask)];
 }
 
+// Grid (kTVBlocks, L): block (b, l) strides over level l's (cube+1)^3 vertices, so a level's partial
+// sums meet in one LDS reduction per block and one atomic per block (not one per wave on 16 addresses).
+constexpr int kTVBlocks = 96;
+constexpr uint32_t kTVSkip = 0xFFFFFFFFu;
+
+__device__ __forceinline__ void tv_vertex(uint32_t lv, int n1, int& i, int& j, int& k) {
+    const uint32_t q = lv / (uint32_t)n1;      // < 1025^3: 32-bit index math
+    k = (int)(lv - q * (uint32_t)n1);
+    j = (int)(q % (uint32_t)n1);
+    i = (int)(q / (uint32_t)n1);
+}
+
 // cube vertex (i,j,k) = min_vertex + (i,j,k) in meshgrid 'ij' order (loss.py:25-27)
 __global__ void __launch_bounds__(256) tv_fwd_kernel(TVParams P) {
-    const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t total = P.vstart[P.L];
+    const int l = blockIdx.y;
+    const int c = P.cube[l], n1 = c + 1;
+    const uint32_t nv = (uint32_t)(P.vstart[l + 1] - P.vstart[l]);
+    const float2* tab = reinterpret_cast<const float2*>(P.tables[l]);
+    const int* mv = P.mv[l];
     float part = 0.f;
-    int l = 0;
-    if (v < total) {
-        l = tv_level(P, v);
-        const int c = P.cube[l], n1 = c + 1;
-        const int64_t lv = v - P.vstart[l];
-        const int i = (int)(lv / (n1 * n1)), j = (int)((lv / n1) % n1), k = (int)(lv % n1);
-        const float2* tab = reinterpret_cast<const float2*>(P.tables[l]);
-        const float2 e = tv_fetch(tab, P.mv[l], i, j, k, P.mask);
-        if (i < c) { const float2 f = tv_fetch(tab, P.mv[l], i + 1, j, k, P.mask); const float dx = f.x - e.x, dy = f.y - e.y; part += dx * dx + dy * dy; }
-        if (j < c) { const float2 f = tv_fetch(tab, P.mv[l], i, j + 1, k, P.mask); const float dx = f.x - e.x, dy = f.y - e.y; part += dx * dx + dy * dy; }
-        if (k < c) { const float2 f = tv_fetch(tab, P.mv[l], i, j, k + 1, P.mask); const float dx = f.x - e.x, dy = f.y - e.y; part += dx * dx + dy * dy; }
-        part = part / (float)c;
+    for (uint32_t lv = blockIdx.x * 256u + threadIdx.x; lv < nv; lv += gridDim.x * 256u) {
+        int i, j, k;
+        tv_vertex(lv, n1, i, j, k);
+        const float2 e = tv_fetch(tab, mv, i, j, k, P.mask);
+        float acc = 0.f;
+        if (i < c) { const float2 f = tv_fetch(tab, mv, i + 1, j, k, P.mask); const float dx = f.x - e.x, dy = f.y - e.y; acc += dx * dx + dy * dy; }
+        if (j < c) { const float2 f = tv_fetch(tab, mv, i, j + 1, k, P.mask); const float dx = f.x - e.x, dy = f.y - e.y; acc += dx * dx + dy * dy; }
+        if (k < c) { const float2 f = tv_fetch(tab, mv, i, j, k + 1, P.mask); const float dx = f.x - e.x, dy = f.y - e.y; acc += dx * dx + dy * dy; }
+        part += acc / (float)c;
     }
-    // A wave may straddle two levels: reduce across the wave when it does not, else add per lane.
-    const int lane = threadIdx.x & 63;
-    const int l0 = __shfl(l, 0, 64);
-    const bool uniform = __all(l == l0 || v >= total);
-    if (uniform) {
-        const float s = wave_sum(part);
-        if (lane == 0 && s != 0.f) atomicAdd(P.loss + l0, s);
-    } else if (v < total && part != 0.f) {
-        atomicAdd(P.loss + l, part);
+    __shared__ float s_part[4];
+    const float w = wave_sum(part);
+    if ((threadIdx.x & 63) == 0) s_part[threadIdx.x >> 6] = w;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const float t = (s_part[0] + s_part[1]) + (s_part[2] + s_part[3]);
+        if (t != 0.f) atomicAdd(P.loss + l, t);
     }
 }
 
 __global__ void __launch_bounds__(256) tv_bwd_kernel(TVParams P) {
-    const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (v >= P.vstart[P.L]) return;
-    const int l = tv_level(P, v);
+    const int l = blockIdx.y;
     const int c = P.cube[l], n1 = c + 1;
-    const int64_t lv = v - P.vstart[l];
-    const int i = (int)(lv / (n1 * n1)), j = (int)((lv / n1) % n1), k = (int)(lv % n1);
+    const uint32_t nv = (uint32_t)(P.vstart[l + 1] - P.vstart[l]);
     const float2* tab = reinterpret_cast<const float2*>(P.tables[l]);
-    const float2 e = tv_fetch(tab, P.mv[l], i, j, k, P.mask);
-    float gx = 0.f, gy = 0.f;   // sum over pairs of d/de_v of (e_hi - e_lo)^2
-#define NERF_TV_PAIR(cond_lo, di, dj, dk, sign)                                                        \
-    if (cond_lo) {                                                                                      \
-        const float2 f = tv_fetch(tab, P.mv[l], i + (di), j + (dj), k + (dk), P.mask);                \
-        gx += (sign) * 2.0f * (e.x - f.x);                                                              \
-        gy += (sign) * 2.0f * (e.y - f.y);                                                              \
-    }
-    NERF_TV_PAIR(i > 0, -1, 0, 0, 1.0f)
-    NERF_TV_PAIR(i < c, 1, 0, 0, 1.0f)
-    NERF_TV_PAIR(j > 0, 0, -1, 0, 1.0f)
-    NERF_TV_PAIR(j < c, 0, 1, 0, 1.0f)
-    NERF_TV_PAIR(k > 0, 0, 0, -1, 1.0f)
-    NERF_TV_PAIR(k < c, 0, 0, 1, 1.0f)
-#undef NERF_TV_PAIR
-    const float s = P.scale[l] / (float)c;
-    const uint32_t h = spatial_hash3((uint32_t)(P.mv[l][0] + i), (uint32_t)(P.mv[l][1] + j),
-                                     (uint32_t)(P.mv[l][2] + k), P.mask);
+    const int* mv = P.mv[l];
     float* dt = P.dtables[l];
-    __hip_atomic_fetch_add(dt + 2 * h + 0, gx * s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_fetch_add(dt + 2 * h + 1, gy * s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const float s = P.scale[l] / (float)c;
+    const int lane = threadIdx.x & 63;
+    // uniform trip count per wave (the re-issue below shuffles across the wave)
+    for (uint32_t base = blockIdx.x * 256u + (threadIdx.x & ~63u); base < nv; base += gridDim.x * 256u) {
+        const uint32_t lv = base + lane;
+        const bool ok = lv < nv;
+        int i = 0, j = 0, k = 0;
+        if (ok) tv_vertex(lv, n1, i, j, k);
+        const float2 e = ok ? tv_fetch(tab, mv, i, j, k, P.mask) : make_float2(0.f, 0.f);
+        float gx = 0.f, gy = 0.f;   // sum over pairs of d/de_v of (e_hi - e_lo)^2
+#define NERF_TV_PAIR(cond, di, dj, dk)                                           \
+        if (ok && (cond)) {                                                              \
+            const float2 f = tv_fetch(tab, mv, i + (di), j + (dj), k + (dk), P.mask); \
+            gx += 2.0f * (e.x - f.x);                                            \
+            gy += 2.0f * (e.y - f.y);                                            \
+        }
+        NERF_TV_PAIR(i > 0, -1, 0, 0)
+        NERF_TV_PAIR(i < c, 1, 0, 0)
+        NERF_TV_PAIR(j > 0, 0, -1, 0)
+        NERF_TV_PAIR(j < c, 0, 1, 0)
+        NERF_TV_PAIR(k > 0, 0, 0, -1)
+        NERF_TV_PAIR(k < c, 0, 0, 1)
+#undef NERF_TV_PAIR
+        const uint32_t h = ok ? spatial_hash3((uint32_t)(mv[0] + i), (uint32_t)(mv[1] + j), (uint32_t)(mv[2] + k), P.mask)
+                              : kTVSkip;
+        // Re-issue so that lanes (2t, 2t+1) add vertex t's two features: one 8-B row per lane pair,
+        // one memory-side atomic request instead of two.
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            const int src = 32 * r + (lane >> 1);
+            const uint32_t hs = (uint32_t)__shfl((int)h, src, 64);
+            const float vx = __shfl(gx, src, 64), vy = __shfl(gy, src, 64);
+            const float v = (lane & 1) ? vy : vx;
+            if (hs != kTVSkip) __hip_atomic_fetch_add(dt + 2 * hs + (lane & 1), v * s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
 }
 
 static int fill_tv(TVParams& P, int n_levels, int log2_T, const int64_t* min_vertex, const int* cube) {
@@ -197,7 +215,7 @@ extern "C" int nerf_tv_fwd(const float* const* d_tables, int n_levels, int log2_
         P.tables[l] = d_tables[l];
     }
     P.loss = d_loss;
-    hipLaunchKernelGGL(tv_fwd_kernel, dim3(blocks_for(P.vstart[n_levels], 256)), dim3(256), 0, as_stream(stream), P);
+    hipLaunchKernelGGL(tv_fwd_kernel, dim3(kTVBlocks, n_levels), dim3(256), 0, as_stream(stream), P);
     NERF_CHECK_LAUNCH("tv_fwd");
     return NERF_OK;
 }
@@ -214,7 +232,7 @@ extern "C" int nerf_tv_bwd(const float* const* d_tables, int n_levels, int log2_
         P.dtables[l] = d_dtables[l];
     }
     P.scale = d_scale;
-    hipLaunchKernelGGL(tv_bwd_kernel, dim3(blocks_for(P.vstart[n_levels], 256)), dim3(256), 0, as_stream(stream), P);
+    hipLaunchKernelGGL(tv_bwd_kernel, dim3(kTVBlocks, n_levels), dim3(256), 0, as_stream(stream), P);
     NERF_CHECK_LAUNCH("tv_bwd");
     return NERF_OK;
 }

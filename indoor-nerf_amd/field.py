@@ -11,7 +11,7 @@ import torch
 import torch.nn as nn
 
 from . import _lib
-from .hashgrid import HashEmbedder, HashEncodeFn, SHEncoder, accumulate_grad_buffers
+from .hashgrid import HashEmbedder, HashEncodeFn, SHEncoder, accumulate_grad_buffers, hash_encode_bwd
 
 
 def _weights_struct(weights):
@@ -114,11 +114,7 @@ class FieldFn(torch.autograd.Function):
                       _lib.ptr(g, "grad_raw"), grads, _lib.ptr(dfeat, "dfeat", allow_none=True), None,
                       _lib.stream())
         if need_tab:
-            meta = ctx.embedder._meta
-            gt = accumulate_grad_buffers(tables)
-            _lib.call("nerf_hash_encode_bwd", _lib.ptr(pts, "pts"), P, meta["bmin"], meta["bmax"], meta["res"],
-                      ctx.n_tab, meta["log2_T"], _lib.ptr(dfeat, "dfeat"), 2, 2 * P, _lib.ptr_array(gt, "grad_tables"),
-                      _lib.stream())
+            hash_encode_bwd(pts, ctx.embedder._meta, dfeat, 2, 2 * P, accumulate_grad_buffers(tables))
         return (None,) * (5 + len(params))
 
 

@@ -67,12 +67,35 @@ class HashEncodeFn(torch.autograd.Function):
         xyz, *tables = ctx.saved_tensors
         if g_feat is not None and any(t.requires_grad for t in tables):
             g = g_feat.contiguous()
-            grads = accumulate_grad_buffers(tables)
-            meta = ctx.meta
-            _lib.call("nerf_hash_encode_bwd", _lib.ptr(xyz, "xyz"), xyz.shape[0], meta["bmin"], meta["bmax"],
-                      meta["res"], len(tables), meta["log2_T"], _lib.ptr(g, "grad_feat"), ctx.sp, ctx.sl,
-                      _lib.ptr_array(grads, "grad_tables"), _lib.stream())
+            hash_encode_bwd(xyz, ctx.meta, g, ctx.sp, ctx.sl, accumulate_grad_buffers(tables))
         return (None, None, None) + (None,) * len(tables)
+
+
+_BWD_WORKSPACE = {}
+
+
+def bwd_workspace(n_levels, log2_T, n_points, device):
+    """Device workspace of nerf_hash_encode_bwd_ws (the binned backward's per-chunk regions), one per
+    device, grown to the largest (n_levels, n_points) seen; calls that share it run in stream order
+    (autograd's backward stream). None when the binned path does not apply (log2_T > 20)."""
+    need = int(_lib.load().nerf_hash_encode_bwd_workspace_bytes(n_levels, log2_T, n_points))
+    if need == 0:
+        return None, 0
+    key = str(device)
+    hit = _BWD_WORKSPACE.get(key)
+    if hit is None or hit[1] < need:
+        _BWD_WORKSPACE.pop(key, None)
+        hit = _BWD_WORKSPACE[key] = (torch.empty(need, dtype=torch.uint8, device=device), need)
+    return hit
+
+
+def hash_encode_bwd(xyz, meta, dfeat, sp, sl, grad_tables):
+    """Scatter-add d feat into the gradient tables (hash_encoding.py:82-107 autograd; csrc/hashgrid.hip)."""
+    ws, nbytes = bwd_workspace(len(grad_tables), meta["log2_T"], xyz.shape[0], xyz.device)
+    _lib.call("nerf_hash_encode_bwd_ws", _lib.ptr(xyz, "xyz"), xyz.shape[0], meta["bmin"], meta["bmax"],
+              meta["res"], len(grad_tables), meta["log2_T"], _lib.ptr(dfeat, "grad_feat"), sp, sl,
+              _lib.ptr_array(grad_tables, "grad_tables"), _lib.ptr(ws, "workspace", dtype=torch.uint8, allow_none=True),
+              nbytes, _lib.stream())
 
 
 class HashEmbedder(nn.Module):

@@ -75,6 +75,47 @@ def total_variation_loss(embeddings, min_resolution, max_resolution, level, log2
     return TVFn.apply(torch.as_tensor(min_vertex).reshape(1, 3), [cube], log2_hashmap_size, embeddings.weight)[0]
 
 
+class TrainLossFn(torch.autograd.Function):
+    """run_nerf.py:1011-1037 in one launch (csrc/loss.hip): returns (loss, img_loss, psnr[1])."""
+    @staticmethod
+    def forward(ctx, rgb, rgb0, target, sp, sp0, tv, sparse_w, tv_w):
+        R = rgb.shape[0]
+        f = dict(device=rgb.device, dtype=torch.float32)
+        rgb, target = rgb.contiguous(), target.contiguous().float()
+        rgb0 = rgb0.contiguous() if rgb0 is not None else None
+        loss, img, psnr = torch.empty((), **f), torch.empty((), **f), torch.empty(1, **f)
+        n_tv = 0 if tv is None else tv.numel()
+        _lib.call("nerf_train_loss_fwd", _lib.ptr(rgb, "rgb"), _lib.ptr(rgb0, "rgb0", allow_none=True),
+                  _lib.ptr(target, "target"), R, _lib.ptr(sp, "sparsity", allow_none=True),
+                  _lib.ptr(sp0, "sparsity0", allow_none=True), float(sparse_w), _lib.ptr(tv, "tv", allow_none=True),
+                  n_tv, float(tv_w), _lib.ptr(loss), _lib.ptr(img), _lib.ptr(psnr), _lib.stream())
+        ctx.save_for_backward(rgb, rgb0, target)
+        ctx.meta = (R, float(sparse_w), n_tv, float(tv_w), sp is not None, sp0 is not None)
+        ctx.mark_non_differentiable(img, psnr)
+        return loss, img, psnr
+
+    @staticmethod
+    def backward(ctx, g, _g_img, _g_psnr):
+        rgb, rgb0, target = ctx.saved_tensors
+        R, sparse_w, n_tv, tv_w, has_sp, has_sp0 = ctx.meta
+        f = dict(device=rgb.device, dtype=torch.float32)
+        d_rgb = torch.empty_like(rgb)
+        d_rgb0 = torch.empty_like(rgb0) if (rgb0 is not None and ctx.needs_input_grad[1]) else None
+        d_sp = torch.empty(R, **f) if has_sp and ctx.needs_input_grad[3] else None
+        d_sp0 = torch.empty(R, **f) if has_sp0 and ctx.needs_input_grad[4] else None
+        d_tv = torch.empty(n_tv, **f) if n_tv and ctx.needs_input_grad[5] else None
+        _lib.call("nerf_train_loss_bwd", _lib.ptr(rgb, "rgb"), _lib.ptr(rgb0, "rgb0", allow_none=True),
+                  _lib.ptr(target, "target"), R, sparse_w, n_tv, tv_w, _lib.ptr(g.contiguous(), "grad_loss"),
+                  _lib.ptr(d_rgb), _lib.ptr(d_rgb0, allow_none=True), _lib.ptr(d_sp, allow_none=True),
+                  _lib.ptr(d_sp0, allow_none=True), _lib.ptr(d_tv, allow_none=True), _lib.stream())
+        return d_rgb, d_rgb0, None, d_sp, d_sp0, d_tv, None, None
+
+
+def train_loss(rgb, rgb0, target, sparsity, sparsity0, tv, sparse_w, tv_w):
+    """Fused loss of one training iteration (see TrainLossFn); any of rgb0/sparsity/sparsity0/tv may be None."""
+    return TrainLossFn.apply(rgb, rgb0, target, sparsity, sparsity0, tv, sparse_w, tv_w)
+
+
 def sigma_sparsity_loss(sigmas):
     """loss.py:45-47 (Cauchy sparsity)."""
     return torch.log(1.0 + 2 * sigmas ** 2).sum(dim=-1)

@@ -12,9 +12,9 @@ import torch
 
 from .field import NeRFSmall, run_network
 from .hashgrid import HashEmbedder, SHEncoder
-from .losses import total_variation_all
+from .losses import total_variation_all, train_loss
 from .optim import RAdam
-from .render import img2mse, mse2psnr, render
+from .render import render
 
 DEFAULTS = dict(multires=10, i_embed=1, i_embed_views=2, multires_views=4, use_viewdirs=True, N_importance=0,
                 N_samples=64, netchunk=1024 * 64, finest_res=512, log2_hashmap_size=19, lrate=5e-4,
@@ -113,18 +113,12 @@ def train_step(batch_rays, target_s, render_kwargs_train, optimizer, args, globa
         optimizer.zero_grad()
     else:
         zero_grad()
-    img_loss = img2mse(rgb, target_s)
-    loss = img_loss
-    psnr = mse2psnr(img_loss)
-    if "rgb0" in extras:
-        loss = loss + img2mse(extras["rgb0"], target_s)
-    sp = extras["sparsity_loss"].sum()
-    if "sparsity_loss0" in extras:
-        sp = sp + extras["sparsity_loss0"].sum()
-    loss = loss + (get("sparse_loss_weight") * loss_scale_sparsity) * sp
+    # run_nerf.py:1011-1037 (img2mse x2, sparsity, TV, mse2psnr) fused into one launch (csrc/loss.hip)
     tv_w = get("tv_loss_weight")
-    if tv_w > 0:
-        loss = loss + tv_w * total_variation_all(render_kwargs_train["embed_fn"], generator=tv_generator).sum()
+    tv = total_variation_all(render_kwargs_train["embed_fn"], generator=tv_generator) if tv_w > 0 else None
+    loss, _img_loss, psnr = train_loss(rgb, extras.get("rgb0"), target_s, extras.get("sparsity_loss"),
+                                       extras.get("sparsity_loss0"), tv, get("sparse_loss_weight") * loss_scale_sparsity,
+                                       tv_w if tv_w > 0 else 0.0)
     if global_step > 1000:
         args.tv_loss_weight = 0.0
     loss.backward()

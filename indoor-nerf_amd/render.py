@@ -16,7 +16,10 @@ import torch
 from . import _lib
 
 img2mse = lambda x, y: torch.mean((x - y) ** 2)  # noqa: E731
-mse2psnr = lambda x: -10. * torch.log(x) / torch.log(torch.tensor([10.], device=x.device))  # noqa: E731
+# The reference divides by torch.log(torch.Tensor([10.])) (a [1] float32 tensor): same value and shape
+# here without creating a device tensor from host data (that copy would synchronise the stream).
+mse2psnr = lambda x: (-10. * torch.log(x) / _LOG10_F32).reshape(1)  # noqa: E731
+_LOG10_F32 = float(np.float32(np.log(10.0)))
 to8b = lambda x: (255 * np.clip(x, 0, 1)).astype(np.uint8)  # noqa: E731
 
 _LINSPACE = {}

@@ -346,3 +346,78 @@ def test_train_step_full_size_finite(nerf, gpu):
     assert torch.isfinite(loss).item()
     for p in grad_vars:
         assert torch.isfinite(p).all().item()
+
+
+@pytest.mark.gpu
+def test_train_loss_head_vs_torch_fp32(nerf, gpu):
+    """Fused loss head (csrc/loss.hip) against the reference's own torch expressions
+    (run_nerf.py:1011-1037) in fp32; gradients bit-exact (same op order as autograd)."""
+    g = torch.Generator().manual_seed(3)
+    R = 4096
+    rgb, rgb0, t = (torch.rand(R, 3, generator=g) for _ in range(3))
+    sp, sp0 = torch.rand(R, generator=g) * 5, torch.rand(R, generator=g) * 5
+    tv = torch.rand(16, generator=g)
+    sw, tw = 1e-4, 1e-3
+    leaves = [x.clone().to(gpu).requires_grad_(True) for x in (rgb, rgb0, sp, sp0, tv)]
+    loss, img, psnr = nerf.train_loss(leaves[0], leaves[1], t.to(gpu), leaves[2], leaves[3], leaves[4], sw, tw)
+    loss.backward()
+    ref_leaves = [x.clone().double().requires_grad_(True) for x in (rgb, rgb0, sp, sp0, tv)]
+    r_rgb, r_rgb0, r_sp, r_sp0, r_tv = ref_leaves
+    td = t.double()
+    r_img = torch.mean((r_rgb - td) ** 2)
+    r_loss = r_img + torch.mean((r_rgb0 - td) ** 2) + sw * (r_sp.sum() + r_sp0.sum()) + tw * sum(r_tv[i] for i in range(16))
+    r_loss.backward()
+    assert abs(float(loss) - float(r_loss)) <= 2e-6 * abs(float(r_loss))
+    assert abs(float(img) - float(r_img)) <= 2e-6 * float(r_img)
+    assert abs(float(psnr) - float(-10 * torch.log10(r_img))) <= 1e-4
+    # fp32 autograd of the same expressions: bit-exact gradients
+    f_leaves = [x.clone().requires_grad_(True) for x in (rgb, rgb0, sp, sp0, tv)]
+    f_rgb, f_rgb0, f_sp, f_sp0, f_tv = f_leaves
+    f_loss = torch.mean((f_rgb - t) ** 2) + torch.mean((f_rgb0 - t) ** 2) + sw * (f_sp.sum() + f_sp0.sum()) \
+        + tw * sum(f_tv[i] for i in range(16))
+    f_loss.backward()
+    for mine, ref in zip(leaves, f_leaves):
+        assert torch.equal(mine.grad.cpu(), ref.grad), float((mine.grad.cpu() - ref.grad).abs().max())
+
+
+@pytest.mark.gpu
+def test_hash_encode_bwd_large_ray_ordered(nerf, gpu, oracle):
+    """The coarse pass at the metric config (4096 lego rays x 64 sorted samples, finest 1024):
+    gradient tables of the binned path (workspace; LDS owner sums) and of the direct atomic path
+    against an fp64 scatter of the oracle's corner indices and weights. Bound per row:
+    |got - ref| <= 2e-6 * sum |contributions| (fp32 products, fp32 atomic sums in any order)."""
+    from indoor_nerf_amd import _lib
+    lo, hi = blender_bbox()
+    ro, rd = synthetic_rays(4096, seed=21)
+    rng = np.random.RandomState(21)
+    z = np.sort(2.0 + 4.0 * rng.rand(4096, 64), axis=1).astype(np.float32)
+    x = (ro[:, None, :] + rd[:, None, :] * z[..., None]).reshape(-1, 3).astype(np.float32)
+    P = x.shape[0]
+    dfeat = rng.randn(16, P, 2).astype(np.float32)
+    emb = _embedder(nerf, gpu, 1024, closed_form_table())
+    xt, dt = torch.from_numpy(x).to(gpu), torch.from_numpy(dfeat).to(gpu)
+    meta = emb._meta
+    got_ws = [torch.zeros(1 << 19, 2, device=gpu) for _ in range(16)]
+    nerf.hashgrid.hash_encode_bwd(xt, meta, dt, 2, 2 * P, got_ws)
+    got_direct = [torch.zeros(1 << 19, 2, device=gpu) for _ in range(16)]
+    _lib.call("nerf_hash_encode_bwd", _lib.ptr(xt), P, meta["bmin"], meta["bmax"], meta["res"], 16, 19,
+              _lib.ptr(dt), 2, 2 * P, _lib.ptr_array(got_direct), _lib.stream())
+    xc = torch.from_numpy(x)
+    bmin, bmax = torch.from_numpy(lo), torch.from_numpy(hi)
+    for lvl in range(16):
+        vmin, vmax, idx, _ = oracle.voxel_corners(xc, bmin, bmax, torch.tensor(emb.level_res[lvl]), 19)
+        w = ((xc - vmin) / (vmax - vmin)).double()
+        wx, wy, wz = w[:, 0:1], w[:, 1:2], w[:, 2:3]
+        g = torch.from_numpy(dfeat[lvl]).double()
+        cw = []
+        for c in range(8):
+            i, j, k = (c >> 2) & 1, (c >> 1) & 1, c & 1
+            cw.append((wz if k else 1 - wz) * (wy if j else 1 - wy) * (wx if i else 1 - wx))
+        contrib = torch.stack([g * cwc for cwc in cw], 1)          # [P, 8, 2]
+        ref = torch.zeros(1 << 19, 2, dtype=torch.float64).index_add_(0, idx.reshape(-1), contrib.reshape(-1, 2))
+        scale = torch.zeros(1 << 19, 2, dtype=torch.float64).index_add_(0, idx.reshape(-1),
+                                                                          contrib.abs().reshape(-1, 2))
+        for name, got in (("workspace", got_ws), ("direct", got_direct)):
+            err = (got[lvl].cpu().double() - ref).abs()
+            bad = err > 2e-6 * scale + 1e-30
+            assert not bool(bad.any()), f"{name} level {lvl}: {int(bad.sum())} rows off, max err {float(err.max()):.3e}"

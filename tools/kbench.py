@@ -64,7 +64,24 @@ def main():
             _lib.call("nerf_hash_encode_bwd", _lib.ptr(pts), P, meta["bmin"], meta["bmax"], meta["res"], 16, 19,
                       _lib.ptr(dfeat), 2, 2 * P, _lib.ptr_array(grads), _lib.stream())
 
+        def bwd_ws():
+            nerf.hashgrid.hash_encode_bwd(pts, meta, dfeat, 2, 2 * P, grads)
+
         res = {"points": P, "fwd_ms": timeit(fwd)}
+        for g in grads:
+            g.zero_()
+        bwd()
+        ref = torch.stack(grads).clone()
+        for g in grads:
+            g.zero_()
+        bwd_ws()
+        cur = torch.stack(grads)
+        res["ws_vs_direct_maxrel_diff"] = ((cur - ref).abs().max() / ref.abs().max()).item()
+        t_direct, t_ws = [], []
+        for _ in range(5):
+            t_direct.append(timeit(bwd, reps=5, warm=1)[0])
+            t_ws.append(timeit(bwd_ws, reps=5, warm=1)[0])
+        res["bwd_direct_ms"], res["bwd_ws_ms"] = float(np.median(t_direct)), float(np.median(t_ws))
         # correctness of the variants against each other
         ref = None
         for v in ("0", "1"):
@@ -153,8 +170,89 @@ def mlp_bench():
     print(json.dumps(out, indent=1))
 
 
+def levels_bench():
+    """Hash fwd/bwd cost per level (one level per launch) on the fine point set: where the backward's
+    atomics go (coarse levels: contention on few rows; fine levels: one request per corner pair)."""
+    dev = torch.device("cuda:0")
+    lo, hi = blender_bbox()
+    emb = nerf.HashEmbedder((torch.from_numpy(lo), torch.from_numpy(hi)), finest_resolution=1024).to(dev)
+    with torch.no_grad():
+        for e in emb.embeddings:
+            e.weight.uniform_(-0.05, 0.05)
+    meta = emb._meta
+    res_all = list(meta["res"])
+    out = {}
+    lo_t, hi_t = torch.tensor(lo, device=dev), torch.tensor(hi, device=dev)
+
+    def morton_order(pts, bits):
+        q = ((pts - lo_t) / (hi_t - lo_t) * (1 << bits)).long().clamp(0, (1 << bits) - 1)
+        key = torch.zeros(pts.shape[0], dtype=torch.long, device=dev)
+        for b in range(bits):
+            for a in range(3):
+                key |= ((q[:, a] >> b) & 1) << (3 * b + a)
+        return torch.sort(key, stable=True)[1]
+
+    cases = [("coarse", 64, 0), ("fine", 192, 0)]
+    for name, S, bits in cases:
+        pts, _ = ray_points(4096, S, dev)
+        P = pts.shape[0]
+        feat = torch.empty(16, P, 2, device=dev)
+        keep = torch.empty(P, device=dev, dtype=torch.bool)
+        dfeat = torch.randn(16, P, 2, device=dev)
+        if bits:
+            perm = morton_order(pts, bits)
+            pts = pts[perm].contiguous()
+            dfeat = dfeat[:, perm].contiguous()
+        grads = [torch.zeros_like(e.weight) for e in emb.embeddings]
+        tabs = emb.tables()
+        rows = []
+        for lvl in range(16):
+            r = _lib.host_f32([res_all[lvl]])
+
+            def fwd():
+                _lib.call("nerf_hash_encode_fwd", _lib.ptr(pts), P, meta["bmin"], meta["bmax"], r, 1, 19,
+                          _lib.ptr_array([tabs[lvl]]), _lib.ptr(feat[lvl]), 2, 2 * P, _lib.ptr(keep, dtype=torch.bool),
+                          _lib.stream())
+
+            def bwd():
+                _lib.call("nerf_hash_encode_bwd", _lib.ptr(pts), P, meta["bmin"], meta["bmax"], r, 1, 19,
+                          _lib.ptr(dfeat[lvl]), 2, 2 * P, _lib.ptr_array([grads[lvl]]), _lib.stream())
+            row = {"level": lvl, "res": res_all[lvl], "fwd_us": 1e3 * timeit(fwd, reps=10)[0]}
+            for v in ("1", "2"):
+                os.environ["NERF_HASH_BWD"] = v
+                row["bwd_us" if v == "1" else "bwd_noatomic_us"] = 1e3 * timeit(bwd, reps=10)[0]
+            os.environ["NERF_HASH_BWD"] = "3"
+            for R in (4, 16, 64):
+                os.environ["NERF_HASH_REPL"] = str(R)
+                row[f"bwd_repl{R}_us"] = 1e3 * timeit(bwd, reps=10)[0]
+            os.environ["NERF_HASH_BWD"] = "1"
+            rows.append(row)
+        out[name] = {"points": P, "levels": rows,
+                     "sum_bwd_us": sum(r["bwd_us"] for r in rows), "sum_fwd_us": sum(r["fwd_us"] for r in rows)}
+    print(json.dumps(out, indent=1))
+
+
+def bwd_only(S=192, reps=10):
+    """Only the workspace (binned) hash backward on one point set, for rocprofv3 kernel traces."""
+    dev = torch.device("cuda:0")
+    lo, hi = blender_bbox()
+    emb = nerf.HashEmbedder((torch.from_numpy(lo), torch.from_numpy(hi)), finest_resolution=1024).to(dev)
+    pts, _ = ray_points(4096, S, dev)
+    P = pts.shape[0]
+    dfeat = torch.randn(16, P, 2, device=dev)
+    grads = [torch.zeros_like(e.weight) for e in emb.embeddings]
+    for _ in range(reps):
+        nerf.hashgrid.hash_encode_bwd(pts, emb._meta, dfeat, 2, 2 * P, grads)
+    torch.cuda.synchronize()
+    print(json.dumps({"points": P, "reps": reps}))
+
+
 if __name__ == "__main__":
-    if len(sys.argv) > 1 and sys.argv[1] == "mlp":
+    if len(sys.argv) > 1 and sys.argv[1] == "bwdws":
+        bwd_only(int(sys.argv[2]) if len(sys.argv) > 2 else 192)
+    elif len(sys.argv) > 1 and sys.argv[1] == "mlp":
         mlp_bench()
+    elif len(sys.argv) > 1 and sys.argv[1] == "levels":
+        levels_bench()
     else:
         main()
