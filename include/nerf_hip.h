@@ -61,7 +61,7 @@ int nerf_hash_encode_bwd(const float* d_xyz, int64_t n_points,
                          float* const* d_dtables, void* stream);
 
 /* Same, on the binned ("owner computes") path: the entries are first written, sorted by table
- * slice, into a caller-owned device workspace (plain stores), then one workgroup per 2^14-row slice
+ * slice, into a caller-owned device workspace (plain stores), then one workgroup per 2^13-row slice
  * sums them in LDS and adds the slice into d_dtables once. Replaces the memory-side float atomics
  * of nerf_hash_encode_bwd, whose request rate bounds that path. The workspace needs no
  * initialisation; calls sharing one must be stream-ordered. workspace_bytes >=

@@ -82,6 +82,38 @@ __device__ __forceinline__ uint32_t spatial_hash3(uint32_t x, uint32_t y, uint32
     return (x * 1u ^ y * 2654435761u ^ z * 805459861u) & mask;
 }
 
+// DPP lane move (VALU, no LDS crossbar): CTRL 0x110+n = row_shr:n, 0x142 = row_bcast:15,
+// 0x143 = row_bcast:31 (GFX9 encodings, valid on gfx950). Lanes with no source / masked rows read 0.
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ float dpp_move(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROW_MASK, 0xF, false));
+}
+
+// Segmented inclusive wave64 sums of N values per lane, runs = lanes [start, lane] (start: first lane
+// of the lane's run). Intra-row Hillis-Steele (row_shr 1,2,4,8) then the row_bcast 15 / 31 carries
+// of the classic DPP scan, each applied only where the source lane lies in the same run.
+template <int N>
+__device__ __forceinline__ void wave_segmented_inclusive_sum(float (&v)[N], int lane, int start) {
+    const int r16 = lane & 15, row = lane >> 4;
+    const bool t1 = r16 >= 1 && lane - 1 >= start;
+    const bool t2 = r16 >= 2 && lane - 2 >= start;
+    const bool t4 = r16 >= 4 && lane - 4 >= start;
+    const bool t8 = r16 >= 8 && lane - 8 >= start;
+    const bool tb15 = (row & 1) && start <= 16 * row - 1;
+    const bool tb31 = row >= 2 && start <= 31;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        float x = v[i], t;
+        t = dpp_move<0x111, 0xF>(x); if (t1) x += t;
+        t = dpp_move<0x112, 0xF>(x); if (t2) x += t;
+        t = dpp_move<0x114, 0xF>(x); if (t4) x += t;
+        t = dpp_move<0x118, 0xF>(x); if (t8) x += t;
+        t = dpp_move<0x142, 0xA>(x); if (tb15) x += t;
+        t = dpp_move<0x143, 0xC>(x); if (tb31) x += t;
+        v[i] = x;
+    }
+}
+
 // Wave64 reductions / scans through DPP-capable shuffles.
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

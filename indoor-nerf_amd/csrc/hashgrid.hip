@@ -35,10 +35,11 @@ struct HashGradParams {
     // owner slice, plus the slice offsets of each region.
     uint16_t* bin_h;      // entry row within its owner slice
     float2* bin_g;        // entry (d feat0, d feat1)
-    int32_t* bin_off;     // [L][nchunks][n_owner + 1]
+    uint32_t* bin_seg;    // [L][n_owner][nchunks]: segment start | count << 16 within the chunk region
     int nchunks;
     int slice_log2;       // owner slice = 2^slice_log2 rows (LDS: 8 B per row)
     int owner_log2;       // owners per level = 2^owner_log2
+    int owner_mode;       // A/B only: 0 normal, 1 plain LDS stores, 2 no global entry loads
 };
 
 // Per-axis voxel math of utils.py:103-112, fp32, exact op order.
@@ -130,7 +131,7 @@ constexpr uint32_t kSkip = 0xFFFFFFFFu;
 // replaces the memory-side atomics: this kernel writes each (row, d feat) entry into a per-chunk
 // region sorted by owner slice (plain stores), and hash_bwd_owner_kernel sums each slice in LDS.
 constexpr int kChunkCap = 256 * 8;        // entries per 256-point chunk (8 corners per point)
-constexpr int kMaxSliceLog2 = 14;         // owner slice: 2^14 rows x 8 B = 128 KiB of LDS
+constexpr int kMaxSliceLog2 = 13;         // owner slice: 2^13 rows x 16 B (fp64 pair) = 128 KiB of LDS
 constexpr int kMaxOwnersLog2 = 6;
 constexpr int kMaxOwners = 1 << kMaxOwnersLog2;
 
@@ -171,32 +172,21 @@ __global__ void __launch_bounds__(256) hash_encode_bwd_kernel(
     }
 
     // Wave-level run merge: a voxel key equal to the previous lane's continues a run; segmented
-    // inclusive sums (Hillis-Steele over 64 lanes) leave each run's total on its LAST lane, which
-    // alone issues the atomics. Lanes of different runs never mix.
+    // inclusive sums leave each run's total on its LAST lane, which alone emits the run's entries.
+    // Run starts / tails come from the ballot of run heads; the sums use DPP (wave_segmented_
+    // inclusive_sum), not the LDS crossbar.
     const uint32_t key_lo = (uint32_t)ax.base | ((uint32_t)ay.base << 16);
     const uint32_t key_hi = (uint32_t)az.base | (valid ? 0u : 0x80000000u);
     const int lane = threadIdx.x & 63;
     const uint32_t prev_lo = __shfl_up(key_lo, 1, 64), prev_hi = __shfl_up(key_hi, 1, 64);
     const bool head = (lane == 0) || prev_lo != key_lo || prev_hi != key_hi;
-    const uint32_t next_lo = __shfl_down(key_lo, 1, 64), next_hi = __shfl_down(key_hi, 1, 64);
-    const bool tail = (lane == 63) || next_lo != key_lo || next_hi != key_hi;
-    if (__ballot(!head) != 0) {  // some run has length > 1 in this wave: segmented sums
-        int start = head ? lane : 0;   // run start lane, by a max-scan of head positions
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int s2 = __shfl_up(start, o, 64);
-            if (lane >= o) start = max(start, s2);
-        }
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const bool take = (lane - o) >= start;
-#pragma unroll
-            for (int c = 0; c < 8; ++c) {
-                const float vx = __shfl_up(cgx[c], o, 64);
-                const float vy = __shfl_up(cgy[c], o, 64);
-                if (take) { cgx[c] += vx; cgy[c] += vy; }
-            }
-        }
+    const uint64_t heads = __ballot(head);
+    const bool tail = (lane == 63) || ((heads >> (lane + 1)) & 1ull);
+    if (heads != ~0ull) {  // some run has length > 1 in this wave
+        const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
+        const int start = 63 - __clzll(heads & upto);
+        wave_segmented_inclusive_sum(cgx, lane, start);
+        wave_segmented_inclusive_sum(cgy, lane, start);
     }
     const bool emit = valid && tail;
     float* tab = hp.dtables[lvl];
@@ -237,9 +227,8 @@ __global__ void __launch_bounds__(256) hash_encode_bwd_kernel(
             }
             if (lane < n_own) {
                 s_start[lane] = inc - v;
-                hp.bin_off[row * (n_own + 1) + lane] = (int32_t)(inc - v);
+                hp.bin_seg[((size_t)lvl * n_own + lane) * hp.nchunks + blockIdx.x] = (inc - v) | (v << 16);
             }
-            if (lane == n_own - 1) hp.bin_off[row * (n_own + 1) + n_own] = (int32_t)inc;
         }
         __syncthreads();
         const size_t base = row * kChunkCap;
@@ -283,65 +272,102 @@ __global__ void __launch_bounds__(256) hash_encode_bwd_kernel(
 }
 
 // ---- owner pass of the binned backward ----------------------------------------------------
-// Block (o, l) owns rows [o * 2^slice_log2, (o+1) * 2^slice_log2) of level l's gradient table: it
-// sums every chunk's segment for that slice into LDS (ds_add_f32; fast, no memory-side requests)
-// and adds the slice into the table once, with plain coalesced loads and stores (sole writer).
-// Each wave takes 4 chunks per step so that 4 segment loads are in flight per lane.
+// Block (o, l) owns rows [o * 2^slice_log2, (o+1) * 2^slice_log2) of level l's gradient table. It
+// walks every chunk's segment for that slice, sums the entries into LDS (ds_add_f64: no
+// memory-side requests) and adds the slice into the table once with plain coalesced loads/stores
+// (it is the slice's only writer). Segments are ~64 entries, so instead of one segment per wave
+// step the entries of a window of chunks are numbered consecutively (exclusive scan of the segment
+// counts in LDS) and every lane takes every 64th entry, 8 per batch: 16 global loads in flight per
+// lane, all lanes busy whatever the segment lengths.
 constexpr int kOwnerThreads = 1024;
+constexpr int kOwnerWindow = 2048;   // chunks per window (LDS: 8 KiB prefix + 4 KiB starts)
 
 __global__ void __launch_bounds__(kOwnerThreads) hash_bwd_owner_kernel(HashGradParams hp) {
-    __shared__ __attribute__((aligned(16))) float2 s_slice[1 << kMaxSliceLog2];
+    // fp64 accumulators: ds_add_f64 runs ~14x the rate of ds_add_f32 on gfx950 (tools/
+    // lds_atomic_bench.hip: 2.24 vs 0.165 row updates per clock per CU, random rows), and the
+    // slice total is rounded to fp32 once.
+    __shared__ __attribute__((aligned(16))) double2 s_slice[1 << kMaxSliceLog2];
+    __shared__ uint32_t s_pre[kOwnerWindow + 1];
+    __shared__ uint16_t s_beg[kOwnerWindow];
+    __shared__ uint32_t s_wsum[kOwnerThreads / 64];
     const int o = blockIdx.x, lvl = blockIdx.y;
     const int S = 1 << hp.slice_log2, n_own = 1 << hp.owner_log2;
-    for (int i = threadIdx.x; i < S; i += kOwnerThreads) s_slice[i] = make_float2(0.f, 0.f);
-    __syncthreads();
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    constexpr int kWaves = kOwnerThreads / 64, kGroup = 4;
-    for (int c0 = wave * kGroup; c0 < hp.nchunks; c0 += kWaves * kGroup) {
-        int st[kGroup], cnt[kGroup];
-        size_t base[kGroup];
-        int nmax = 0;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    for (int i = tid; i < S; i += kOwnerThreads) s_slice[i] = make_double2(0.0, 0.0);
+    const uint32_t* seg = hp.bin_seg + ((size_t)lvl * n_own + o) * hp.nchunks;
+    for (int w0 = 0; w0 < hp.nchunks; w0 += kOwnerWindow) {
+        const int nw = min(kOwnerWindow, hp.nchunks - w0);
+        // segment counts of the window -> exclusive prefix s_pre (2 chunks per thread)
+        uint32_t c0 = 0, c1 = 0;
+        const int i0 = 2 * tid, i1 = 2 * tid + 1;
+        if (i0 < nw) { const uint32_t v = seg[w0 + i0]; c0 = v >> 16; s_beg[i0] = (uint16_t)(v & 0xFFFFu); }
+        if (i1 < nw) { const uint32_t v = seg[w0 + i1]; c1 = v >> 16; s_beg[i1] = (uint16_t)(v & 0xFFFFu); }
+        const uint32_t pair = c0 + c1;
+        uint32_t inc = pair;
 #pragma unroll
-        for (int k = 0; k < kGroup; ++k) {
-            const int c = c0 + k;
-            cnt[k] = 0;
-            st[k] = 0;
-            base[k] = 0;
-            if (c < hp.nchunks) {
-                const size_t row = (size_t)lvl * hp.nchunks + c;
-                const int32_t* off = hp.bin_off + row * (n_own + 1) + o;
-                st[k] = off[0];
-                cnt[k] = off[1] - off[0];
-                base[k] = row * kChunkCap + st[k];
-            }
-            nmax = max(nmax, cnt[k]);
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t t = __shfl_up(inc, d, 64);
+            if (lane >= d) inc += t;
         }
-        for (int i = lane; i < nmax; i += 64) {
-            uint16_t h[kGroup];
-            float2 g[kGroup];
+        if (lane == 63) s_wsum[wave] = inc;
+        __syncthreads();
+        uint32_t wbase = 0;
+        for (int w = 0; w < wave; ++w) wbase += s_wsum[w];
+        const uint32_t ex = wbase + inc - pair;
+        if (i0 <= nw) s_pre[i0] = ex;
+        if (i1 <= nw) s_pre[i1] = ex + c0;
+        if (i1 + 1 == nw) s_pre[nw] = ex + pair;   // nw == kOwnerWindow: no thread has i0 == nw
+        __syncthreads();
+        // entries of the window split by chunk ranges across the waves, lane-strided inside
+        const int cb = (int)((int64_t)nw * wave / (kOwnerThreads / 64));
+        const int ce = (int)((int64_t)nw * (wave + 1) / (kOwnerThreads / 64));
+        const uint32_t e_end = s_pre[ce];
+        int c = cb;
+        for (uint32_t e = s_pre[cb] + lane; e < e_end; e += 64 * 8) {
+            size_t addr[8];
 #pragma unroll
-            for (int k = 0; k < kGroup; ++k) {
-                if (i < cnt[k]) {
-                    h[k] = hp.bin_h[base[k] + i];
-                    g[k] = hp.bin_g[base[k] + i];
+            for (int j = 0; j < 8; ++j) {
+                const uint32_t ej = e + 64u * j;
+                addr[j] = ~(size_t)0;
+                if (ej < e_end) {
+                    while (s_pre[c + 1] <= ej) ++c;
+                    addr[j] = ((size_t)lvl * hp.nchunks + w0 + c) * kChunkCap + s_beg[c] + (ej - s_pre[c]);
+                }
+            }
+            uint16_t h[8];
+            float2 g[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                if (addr[j] != ~(size_t)0) {
+                    if (hp.owner_mode == 2) {
+                        h[j] = (uint16_t)(addr[j] & (size_t)(S - 1));
+                        g[j] = make_float2(1.f, 1.f);
+                    } else {
+                        h[j] = hp.bin_h[addr[j]];
+                        g[j] = hp.bin_g[addr[j]];
+                    }
                 }
             }
 #pragma unroll
-            for (int k = 0; k < kGroup; ++k) {
-                if (i < cnt[k]) {
-                    atomicAdd(&s_slice[h[k]].x, g[k].x);
-                    atomicAdd(&s_slice[h[k]].y, g[k].y);
+            for (int j = 0; j < 8; ++j) {
+                if (addr[j] != ~(size_t)0) {
+                    if (hp.owner_mode == 1) {
+                        s_slice[h[j]] = make_double2(g[j].x, g[j].y);
+                    } else {
+                        atomicAdd(&s_slice[h[j]].x, (double)g[j].x);
+                        atomicAdd(&s_slice[h[j]].y, (double)g[j].y);
+                    }
                 }
             }
         }
+        __syncthreads();   // s_pre / s_beg reused by the next window
     }
-    __syncthreads();
     float2* dt = reinterpret_cast<float2*>(hp.dtables[lvl]) + (size_t)o * S;
-    for (int i = threadIdx.x; i < S; i += kOwnerThreads) {
-        const float2 v = s_slice[i];
-        if (v.x != 0.f || v.y != 0.f) {
+    for (int i = tid; i < S; i += kOwnerThreads) {
+        const double2 v = s_slice[i];
+        if (v.x != 0.0 || v.y != 0.0) {
             const float2 t = dt[i];
-            dt[i] = make_float2(t.x + v.x, t.y + v.y);
+            dt[i] = make_float2((float)((double)t.x + v.x), (float)((double)t.y + v.y));
         }
     }
 }
@@ -351,19 +377,19 @@ struct BinPlan {
     size_t off_h, off_g, off_off, total;   // byte offsets in the workspace
 };
 
-// Binned path for log2_T in [1, kMaxSliceLog2 + log2(kMaxOwners)]: slices of min(2^14, T) rows.
+// Binned path for log2_T in [1, kMaxSliceLog2 + log2(kMaxOwners)]: slices of min(2^13, T) rows.
 static bool make_bin_plan(int n_levels, int log2_T, int64_t n_points, BinPlan& B) {
     if (log2_T < 1 || log2_T > kMaxSliceLog2 + kMaxOwnersLog2 || n_points < 0) return false;
     B.slice_log2 = log2_T < kMaxSliceLog2 ? log2_T : kMaxSliceLog2;
     B.owner_log2 = log2_T - B.slice_log2;
     B.nchunks = (int)((n_points + 255) / 256);
     const size_t entries = (size_t)n_levels * B.nchunks * kChunkCap;
-    const size_t offs = (size_t)n_levels * B.nchunks * ((1 << B.owner_log2) + 1);
+    const size_t offs = (size_t)n_levels * B.nchunks * (1 << B.owner_log2);
     auto up = [](size_t v) { return (v + 255) & ~(size_t)255; };
     B.off_g = 0;
     B.off_h = up(entries * sizeof(float2));
     B.off_off = B.off_h + up(entries * sizeof(uint16_t));
-    B.total = B.off_off + up(offs * sizeof(int32_t));
+    B.total = B.off_off + up(offs * sizeof(uint32_t));
     return true;
 }
 
@@ -434,10 +460,12 @@ static int hash_encode_bwd_impl(const float* d_xyz, int64_t n_points, const floa
         char* ws = static_cast<char*>(d_workspace);
         hp.bin_g = reinterpret_cast<float2*>(ws + B.off_g);
         hp.bin_h = reinterpret_cast<uint16_t*>(ws + B.off_h);
-        hp.bin_off = reinterpret_cast<int32_t*>(ws + B.off_off);
+        hp.bin_seg = reinterpret_cast<uint32_t*>(ws + B.off_off);
         hp.nchunks = B.nchunks;
         hp.slice_log2 = B.slice_log2;
         hp.owner_log2 = B.owner_log2;
+        const char* om = getenv("NERF_OWNER_MODE");
+        hp.owner_mode = om ? atoi(om) : 0;
     }
     const dim3 grid(blocks_for(n_points, 256), n_levels);
     switch (mode) {

@@ -77,7 +77,7 @@ _BWD_WORKSPACE = {}
 def bwd_workspace(n_levels, log2_T, n_points, device):
     """Device workspace of nerf_hash_encode_bwd_ws (the binned backward's per-chunk regions), one per
     device, grown to the largest (n_levels, n_points) seen; calls that share it run in stream order
-    (autograd's backward stream). None when the binned path does not apply (log2_T > 20)."""
+    (autograd's backward stream). None when the binned path does not apply (log2_T > 19)."""
     need = int(_lib.load().nerf_hash_encode_bwd_workspace_bytes(n_levels, log2_T, n_points))
     if need == 0:
         return None, 0

@@ -241,9 +241,12 @@ def bwd_only(S=192, reps=10):
     P = pts.shape[0]
     dfeat = torch.randn(16, P, 2, device=dev)
     grads = [torch.zeros_like(e.weight) for e in emb.embeddings]
-    for _ in range(reps):
-        nerf.hashgrid.hash_encode_bwd(pts, emb._meta, dfeat, 2, 2 * P, grads)
-    torch.cuda.synchronize()
+    for mode in ("0", "1", "2"):
+        os.environ["NERF_OWNER_MODE"] = mode
+        for _ in range(reps):
+            nerf.hashgrid.hash_encode_bwd(pts, emb._meta, dfeat, 2, 2 * P, grads)
+        torch.cuda.synchronize()
+    os.environ["NERF_OWNER_MODE"] = "0"
     print(json.dumps({"points": P, "reps": reps}))
 
 
