@@ -19,7 +19,7 @@ namespace nerf {
 
 struct HashParams {
     const float* tables[NERF_MAX_LEVELS];
-    float res[NERF_MAX_LEVELS];
+    float cell[NERF_MAX_LEVELS][3];   // grid_size = (box_max - box_min) / res, fp32 on the host
     float bmin[3];
     float bmax[3];
     uint32_t mask;
@@ -27,7 +27,7 @@ struct HashParams {
 
 struct HashGradParams {
     float* dtables[NERF_MAX_LEVELS];
-    float res[NERF_MAX_LEVELS];
+    float cell[NERF_MAX_LEVELS][3];
     float bmin[3];
     float bmax[3];
     uint32_t mask;
@@ -49,16 +49,25 @@ struct AxisCell {
     bool inside;   // x == max(min(x, bmax), bmin)
 };
 
-__device__ __forceinline__ AxisCell axis_cell(float x, float lo, float hi, float res) {
+__device__ __forceinline__ AxisCell axis_cell(float x, float lo, float hi, float cell) {
     AxisCell a;
     a.inside = (x == fmaxf(fminf(x, hi), lo));
     float xc = fminf(fmaxf(x, lo), hi);            // torch.clamp(min=lo, max=hi)
-    float cell = (hi - lo) / res;                  // grid_size
     a.base = (int)floorf((xc - lo) / cell);        // floor(...).int()
     float vmin = (float)a.base * cell + lo;        // bottom_left_idx*grid_size + box_min
     float vmax = vmin + cell;                      // + 1.0*grid_size
     a.w = (x - vmin) / (vmax - vmin);
     return a;
+}
+
+// grid_size = (box_max - box_min) / resolution (utils.py:106): the same two fp32 operations,
+// correctly rounded, on the host once per launch instead of per point.
+static void fill_cells(float (*cell)[3], const float* bmin, const float* bmax, const float* res, int n_levels) {
+    for (int l = 0; l < n_levels; ++l)
+        for (int a = 0; a < 3; ++a) {
+            const volatile float d = bmax[a] - bmin[a];
+            cell[l][a] = d / res[l];
+        }
 }
 
 __global__ void __launch_bounds__(256) hash_encode_fwd_kernel(
@@ -68,10 +77,9 @@ __global__ void __launch_bounds__(256) hash_encode_fwd_kernel(
     const int lvl = blockIdx.y;
     if (p >= n) return;
     const float x = xyz[3 * p + 0], y = xyz[3 * p + 1], z = xyz[3 * p + 2];
-    const float res = hp.res[lvl];
-    const AxisCell ax = axis_cell(x, hp.bmin[0], hp.bmax[0], res);
-    const AxisCell ay = axis_cell(y, hp.bmin[1], hp.bmax[1], res);
-    const AxisCell az = axis_cell(z, hp.bmin[2], hp.bmax[2], res);
+    const AxisCell ax = axis_cell(x, hp.bmin[0], hp.bmax[0], hp.cell[lvl][0]);
+    const AxisCell ay = axis_cell(y, hp.bmin[1], hp.bmax[1], hp.cell[lvl][1]);
+    const AxisCell az = axis_cell(z, hp.bmin[2], hp.bmax[2], hp.cell[lvl][2]);
     if (lvl == 0 && keep) keep[p] = (ax.inside && ay.inside && az.inside) ? 1 : 0;
 
     const float2* __restrict__ tab = reinterpret_cast<const float2*>(hp.tables[lvl]);
@@ -151,10 +159,9 @@ __global__ void __launch_bounds__(256) hash_encode_bwd_kernel(
         gx = src[0];
         gy = src[1];
     }
-    const float res = hp.res[lvl];
-    const AxisCell ax = axis_cell(x, hp.bmin[0], hp.bmax[0], res);
-    const AxisCell ay = axis_cell(y, hp.bmin[1], hp.bmax[1], res);
-    const AxisCell az = axis_cell(z, hp.bmin[2], hp.bmax[2], res);
+    const AxisCell ax = axis_cell(x, hp.bmin[0], hp.bmax[0], hp.cell[lvl][0]);
+    const AxisCell ay = axis_cell(y, hp.bmin[1], hp.bmax[1], hp.cell[lvl][1]);
+    const AxisCell az = axis_cell(z, hp.bmin[2], hp.bmax[2], hp.cell[lvl][2]);
     const float wx = ax.w, wy = ay.w, wz = az.w;
     const float ox = 1.0f - wx, oy = 1.0f - wy, oz = 1.0f - wz;
 
@@ -200,11 +207,13 @@ __global__ void __launch_bounds__(256) hash_encode_bwd_kernel(
             atomic_add_f32(tab + 2 * h + 1, cgy[c]);
         }
     } else if constexpr (MODE == 3) {
-        // Bin: count this chunk's entries per owner slice (LDS atomics), scan, and store each entry
-        // at its slot of the chunk's region. The region (<= 2048 entries) is written by this block
-        // alone within a few microseconds, so L2 merges the scattered 10-B writes into whole lines.
+        // Bin: count this chunk's entries per owner slice (LDS atomics), scan, place every entry at
+        // its slot of an LDS image of the chunk's region, then write the image out with 16-B
+        // coalesced stores (scattered per-lane stores were TA-bound: 64 lines per instruction).
         __shared__ uint32_t s_cnt[kMaxOwners];
         __shared__ uint32_t s_start[kMaxOwners + 1];
+        __shared__ __attribute__((aligned(16))) uint16_t s_eh[kChunkCap];
+        __shared__ __attribute__((aligned(16))) float2 s_eg[kChunkCap];
         const int n_own = 1 << hp.owner_log2;
         if (threadIdx.x < n_own) s_cnt[threadIdx.x] = 0;
         __syncthreads();
@@ -216,7 +225,6 @@ __global__ void __launch_bounds__(256) hash_encode_bwd_kernel(
                                                                 : kSkip;
         }
         __syncthreads();
-        const size_t row = (size_t)lvl * hp.nchunks + blockIdx.x;
         if (threadIdx.x < 64) {   // exclusive scan of <= 64 counters in wave 0
             const uint32_t v = lane < n_own ? s_cnt[lane] : 0u;
             uint32_t inc = v;
@@ -229,17 +237,26 @@ __global__ void __launch_bounds__(256) hash_encode_bwd_kernel(
                 s_start[lane] = inc - v;
                 hp.bin_seg[((size_t)lvl * n_own + lane) * hp.nchunks + blockIdx.x] = (inc - v) | (v << 16);
             }
+            if (lane == n_own - 1) s_start[n_own] = inc;
         }
         __syncthreads();
-        const size_t base = row * kChunkCap;
         const uint32_t smask = (1u << hp.slice_log2) - 1u;
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
             if (pos[c] != kSkip) {
-                const size_t i = base + s_start[hh[c] >> hp.slice_log2] + pos[c];
-                hp.bin_h[i] = (uint16_t)(hh[c] & smask);
-                hp.bin_g[i] = make_float2(cgx[c], cgy[c]);
+                const uint32_t k = s_start[hh[c] >> hp.slice_log2] + pos[c];
+                s_eh[k] = (uint16_t)(hh[c] & smask);
+                s_eg[k] = make_float2(cgx[c], cgy[c]);
             }
+        }
+        __syncthreads();
+        const uint32_t total = s_start[n_own];
+        const size_t base = ((size_t)lvl * hp.nchunks + blockIdx.x) * kChunkCap;
+        // two entries per lane: rows as one dword, (d feat) x 2 as one dwordx4; a trailing odd
+        // slot carries stale LDS bytes that no owner reads (owners read < count per segment)
+        for (uint32_t i = 2 * threadIdx.x; i < total; i += 2 * 256) {
+            *reinterpret_cast<uint32_t*>(hp.bin_h + base + i) = *reinterpret_cast<const uint32_t*>(&s_eh[i]);
+            *reinterpret_cast<float4*>(hp.bin_g + base + i) = *reinterpret_cast<const float4*>(&s_eg[i]);
         }
     } else {
         __shared__ float s_val[4][64][17];
@@ -323,19 +340,20 @@ __global__ void __launch_bounds__(kOwnerThreads) hash_bwd_owner_kernel(HashGradP
         const int ce = (int)((int64_t)nw * (wave + 1) / (kOwnerThreads / 64));
         const uint32_t e_end = s_pre[ce];
         int c = cb;
-        for (uint32_t e = s_pre[cb] + lane; e < e_end; e += 64 * 8) {
-            size_t addr[8];
+        const size_t region0 = ((size_t)lvl * hp.nchunks + w0) * kChunkCap;
+        // addresses of entries e, e+64, ..., e+448 (chunk of each by forward tracking in s_pre)
+        auto track = [&](uint32_t e, size_t (&addr)[8]) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const uint32_t ej = e + 64u * j;
                 addr[j] = ~(size_t)0;
                 if (ej < e_end) {
                     while (s_pre[c + 1] <= ej) ++c;
-                    addr[j] = ((size_t)lvl * hp.nchunks + w0 + c) * kChunkCap + s_beg[c] + (ej - s_pre[c]);
+                    addr[j] = region0 + (size_t)c * kChunkCap + s_beg[c] + (ej - s_pre[c]);
                 }
             }
-            uint16_t h[8];
-            float2 g[8];
+        };
+        auto fetch = [&](const size_t (&addr)[8], uint16_t (&h)[8], float2 (&g)[8]) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 if (addr[j] != ~(size_t)0) {
@@ -348,6 +366,21 @@ __global__ void __launch_bounds__(kOwnerThreads) hash_bwd_owner_kernel(HashGradP
                     }
                 }
             }
+        };
+        // software pipeline: the next batch's 16 loads are in flight while this batch's adds run
+        size_t addr[8];
+        uint16_t h[8];
+        float2 g[8];
+        uint32_t e = s_pre[cb] + lane;
+        track(e, addr);
+        fetch(addr, h, g);
+        while (e < e_end) {
+            size_t addr2[8];
+            uint16_t h2[8];
+            float2 g2[8];
+            const uint32_t en = e + 64u * 8;
+            track(en, addr2);
+            fetch(addr2, h2, g2);
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 if (addr[j] != ~(size_t)0) {
@@ -359,6 +392,13 @@ __global__ void __launch_bounds__(kOwnerThreads) hash_bwd_owner_kernel(HashGradP
                     }
                 }
             }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                addr[j] = addr2[j];
+                h[j] = h2[j];
+                g[j] = g2[j];
+            }
+            e = en;
         }
         __syncthreads();   // s_pre / s_beg reused by the next window
     }
@@ -421,9 +461,9 @@ extern "C" int nerf_hash_encode_fwd(const float* d_xyz, int64_t n_points, const 
     for (int l = 0; l < n_levels; ++l) {
         NERF_REQUIRE(d_tables[l], "hash_encode_fwd: table %d is null", l);
         hp.tables[l] = d_tables[l];
-        hp.res[l] = level_res[l];
     }
     for (int a = 0; a < 3; ++a) { hp.bmin[a] = bbox_min3[a]; hp.bmax[a] = bbox_max3[a]; }
+    fill_cells(hp.cell, bbox_min3, bbox_max3, level_res, n_levels);
     hp.mask = (uint32_t)((1u << log2_T) - 1u);
     dim3 grid(blocks_for(n_points, 256), n_levels);
     hipLaunchKernelGGL(hash_encode_fwd_kernel, grid, dim3(256), 0, as_stream(stream), d_xyz, n_points, hp,
@@ -446,9 +486,9 @@ static int hash_encode_bwd_impl(const float* d_xyz, int64_t n_points, const floa
     for (int l = 0; l < n_levels; ++l) {
         NERF_REQUIRE(d_dtables[l], "hash_encode_bwd: grad table %d is null", l);
         hp.dtables[l] = d_dtables[l];
-        hp.res[l] = level_res[l];
     }
     for (int a = 0; a < 3; ++a) { hp.bmin[a] = bbox_min3[a]; hp.bmax[a] = bbox_max3[a]; }
+    fill_cells(hp.cell, bbox_min3, bbox_max3, level_res, n_levels);
     hp.mask = (uint32_t)((1u << log2_T) - 1u);
     int mode = bwd_mode();
     BinPlan B{};
