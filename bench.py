@@ -38,11 +38,32 @@ FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: f32 matrix (v_mfma_f32_32x
 UNIT_COST = {
     "nerf_hash_encode_fwd": ("hbm", 16 * 8 * 8 + 12 + 128 + 1, "point"),
     "nerf_hash_encode_bwd": ("hbm", 2 * 16 * 8 * 8 + 12 + 128, "point"),
+    "nerf_hash_encode_bwd_ws": ("hbm", 2 * 16 * 8 * 8 + 12 + 128, "point"),
     "nerf_mlp_fwd": ("mfma", 18688, "point"),
     "nerf_mlp_bwd": ("mfma", 2 * 18688, "point"),
     "nerf_composite_fwd": ("hbm", 24, "sample"),
     "nerf_composite_bwd": ("hbm", 40, "sample"),
 }
+
+
+# ABI call -> the kernel symbols it launches (rocprofv3 names), to attach PMC traffic per call
+KERNEL_SYMBOLS = {
+    "nerf_hash_encode_fwd": ["nerf::hash_encode_fwd_kernel"],
+    "nerf_hash_encode_bwd_ws": ["nerf::hash_encode_bwd_kernel<3>", "nerf::hash_bwd_owner_kernel"],
+    "nerf_mlp_fwd": ["nerf::mlp_fwd_frag_kernel"],
+    "nerf_mlp_bwd": ["nerf::mlp_bwd_frag_kernel"],
+}
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r01_traffic.json")
+
+
+def pmc_traffic(abi_name):
+    """HBM-side bytes per call of `abi_name` from the committed PMC passes (tools/profile_bench.sh:
+    FETCH_SIZE and WRITE_SIZE in separate rocprofv3 passes of this bench), or None."""
+    if not os.path.exists(TRAFFIC_JSON) or abi_name not in KERNEL_SYMBOLS:
+        return None
+    t = json.load(open(TRAFFIC_JSON))
+    parts = [t.get(k, {}).get("traffic_bytes") for k in KERNEL_SYMBOLS[abi_name]]
+    return None if any(p is None for p in parts) else float(sum(parts))
 
 
 def parse():
@@ -176,16 +197,20 @@ def main():
             bound, per_unit, unit = UNIT_COST[dom]
             units = units_per_launch[unit]
             avg_s = kernels[dom]["avg_ms"] * 1e-3
+            traffic = pmc_traffic(dom)
             if bound == "hbm":
                 ach = per_unit * units / avg_s / 1e9
                 roofline = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-                            "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                            "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
                             "per_launch_units": units, "algorithmic_bytes_per_unit": per_unit}
             else:
                 ach = per_unit * units / avg_s / 1e12
                 roofline = {"kernel": dom, "bound": "mfma", "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
-                            "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+                            "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
                             "per_launch_units": units, "algorithmic_flops_per_unit": per_unit}
+            if traffic is not None:
+                roofline["traffic_source"] = ("profiles/r01_traffic.json: rocprofv3 FETCH_SIZE (x2, gfx950 wide-read "
+                                              "correction) + WRITE_SIZE per call, separate PMC passes of this bench")
         else:
             roofline = {"kernel": dom, "bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": None, "traffic": None}

@@ -39,7 +39,6 @@ struct HashGradParams {
     int nchunks;
     int slice_log2;       // owner slice = 2^slice_log2 rows (LDS: 8 B per row)
     int owner_log2;       // owners per level = 2^owner_log2
-    int owner_mode;       // A/B only: 0 normal, 1 plain LDS stores, 2 no global entry loads
 };
 
 // Per-axis voxel math of utils.py:103-112, fp32, exact op order.
@@ -341,63 +340,59 @@ __global__ void __launch_bounds__(kOwnerThreads) hash_bwd_owner_kernel(HashGradP
         const uint32_t e_end = s_pre[ce];
         int c = cb;
         const size_t region0 = ((size_t)lvl * hp.nchunks + w0) * kChunkCap;
-        // addresses of entries e, e+64, ..., e+448 (chunk of each by forward tracking in s_pre)
-        auto track = [&](uint32_t e, size_t (&addr)[8]) {
+        // addresses of entries e, e+64, ..., e+448 (chunk of each by forward tracking in s_pre);
+        // an entry past the range loads slot 0 of the window (always mapped) and is masked later,
+        // so the loads carry no control flow and stay in flight across the adds
+        auto track = [&](uint32_t e, size_t (&addr)[8], uint32_t& valid) {
+            valid = 0;
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const uint32_t ej = e + 64u * j;
-                addr[j] = ~(size_t)0;
+                addr[j] = region0;
                 if (ej < e_end) {
                     while (s_pre[c + 1] <= ej) ++c;
                     addr[j] = region0 + (size_t)c * kChunkCap + s_beg[c] + (ej - s_pre[c]);
+                    valid |= 1u << j;
                 }
             }
         };
         auto fetch = [&](const size_t (&addr)[8], uint16_t (&h)[8], float2 (&g)[8]) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                if (addr[j] != ~(size_t)0) {
-                    if (hp.owner_mode == 2) {
-                        h[j] = (uint16_t)(addr[j] & (size_t)(S - 1));
-                        g[j] = make_float2(1.f, 1.f);
-                    } else {
-                        h[j] = hp.bin_h[addr[j]];
-                        g[j] = hp.bin_g[addr[j]];
-                    }
-                }
+                h[j] = __builtin_nontemporal_load(hp.bin_h + addr[j]);
+                const float2* gp = hp.bin_g + addr[j];
+                g[j] = make_float2(__builtin_nontemporal_load(&gp->x), __builtin_nontemporal_load(&gp->y));
             }
         };
         // software pipeline: the next batch's 16 loads are in flight while this batch's adds run
         size_t addr[8];
         uint16_t h[8];
         float2 g[8];
+        uint32_t valid;
         uint32_t e = s_pre[cb] + lane;
-        track(e, addr);
+        track(e, addr, valid);
         fetch(addr, h, g);
         while (e < e_end) {
             size_t addr2[8];
             uint16_t h2[8];
             float2 g2[8];
+            uint32_t valid2;
             const uint32_t en = e + 64u * 8;
-            track(en, addr2);
+            track(en, addr2, valid2);
             fetch(addr2, h2, g2);
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                if (addr[j] != ~(size_t)0) {
-                    if (hp.owner_mode == 1) {
-                        s_slice[h[j]] = make_double2(g[j].x, g[j].y);
-                    } else {
-                        atomicAdd(&s_slice[h[j]].x, (double)g[j].x);
-                        atomicAdd(&s_slice[h[j]].y, (double)g[j].y);
-                    }
+                if (valid & (1u << j)) {
+                    atomicAdd(&s_slice[h[j]].x, (double)g[j].x);
+                    atomicAdd(&s_slice[h[j]].y, (double)g[j].y);
                 }
             }
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                addr[j] = addr2[j];
                 h[j] = h2[j];
                 g[j] = g2[j];
             }
+            valid = valid2;
             e = en;
         }
         __syncthreads();   // s_pre / s_beg reused by the next window
@@ -504,8 +499,6 @@ static int hash_encode_bwd_impl(const float* d_xyz, int64_t n_points, const floa
         hp.nchunks = B.nchunks;
         hp.slice_log2 = B.slice_log2;
         hp.owner_log2 = B.owner_log2;
-        const char* om = getenv("NERF_OWNER_MODE");
-        hp.owner_mode = om ? atoi(om) : 0;
     }
     const dim3 grid(blocks_for(n_points, 256), n_levels);
     switch (mode) {

@@ -241,17 +241,39 @@ def bwd_only(S=192, reps=10):
     P = pts.shape[0]
     dfeat = torch.randn(16, P, 2, device=dev)
     grads = [torch.zeros_like(e.weight) for e in emb.embeddings]
-    for mode in ("0", "1", "2"):
-        os.environ["NERF_OWNER_MODE"] = mode
-        for _ in range(reps):
-            nerf.hashgrid.hash_encode_bwd(pts, emb._meta, dfeat, 2, 2 * P, grads)
-        torch.cuda.synchronize()
-    os.environ["NERF_OWNER_MODE"] = "0"
+    for _ in range(reps):
+        nerf.hashgrid.hash_encode_bwd(pts, emb._meta, dfeat, 2, 2 * P, grads)
+    torch.cuda.synchronize()
+    print(json.dumps({"points": P, "reps": reps}))
+
+
+def mlp_only(P=786432, reps=10):
+    """Only the default MLP fwd + bwd kernels at one point count, for rocprofv3 PMC passes."""
+    dev = torch.device("cuda:0")
+    torch.manual_seed(0)
+    net = nerf.NeRFSmall(2, 64, 15, 3, 64, 32, 16).to(dev)
+    from indoor_nerf_amd.field import _grads_struct, _weights_struct
+    feat = torch.randn(16, P, 2, device=dev) * 0.3
+    vd = torch.nn.functional.normalize(torch.randn(P // 64, 3, device=dev), dim=-1)
+    keep = torch.ones(P, device=dev, dtype=torch.bool)
+    raw = torch.empty(P, 4, device=dev)
+    graw = torch.randn(P, 4, device=dev)
+    dfeat = torch.empty_like(feat)
+    W = net.mlp_weights()
+    for _ in range(reps):
+        _lib.call("nerf_mlp_fwd", _lib.ptr(feat), 2, 2 * P, None, 0, _lib.ptr(vd), 64,
+                  _lib.ptr(keep, dtype=torch.bool), P, _weights_struct(W), _lib.ptr(raw), _lib.stream())
+        _lib.call("nerf_mlp_bwd", _lib.ptr(feat), 2, 2 * P, None, 0, _lib.ptr(vd), 64,
+                  _lib.ptr(keep, dtype=torch.bool), P, _weights_struct(W), _lib.ptr(graw), _grads_struct(W),
+                  _lib.ptr(dfeat), None, _lib.stream())
+    torch.cuda.synchronize()
     print(json.dumps({"points": P, "reps": reps}))
 
 
 if __name__ == "__main__":
-    if len(sys.argv) > 1 and sys.argv[1] == "bwdws":
+    if len(sys.argv) > 1 and sys.argv[1] == "mlponly":
+        mlp_only()
+    elif len(sys.argv) > 1 and sys.argv[1] == "bwdws":
         bwd_only(int(sys.argv[2]) if len(sys.argv) > 2 else 192)
     elif len(sys.argv) > 1 and sys.argv[1] == "mlp":
         mlp_bench()
