@@ -102,20 +102,43 @@ typedef struct {
     float* c2;
 } nerf_mlp_grads;
 
+/* d_geo (may be NULL): also write o = [sigma, geo_feat 15] per point, [P,16] — the normals head's
+ * input (run_nerf_helpers.py:287, :300). */
 int nerf_mlp_fwd(const float* d_feat, int64_t feat_stride_point, int64_t feat_stride_level,
                  const float* d_sh, int64_t sh_stride,
                  const float* d_viewdirs, int64_t samples_per_ray,
                  const uint8_t* d_keep, int64_t n_points,
-                 const nerf_mlp_weights* weights, float* d_raw, void* stream);
+                 const nerf_mlp_weights* weights, float* d_raw, float* d_geo, void* stream);
 
 /* Backward: recomputes the forward, then ACCUMULATES weight grads into *grads (atomic adds) and
- * WRITES d_dfeat (same strides as d_feat; may be NULL) and d_dsh ([P,16], may be NULL). */
+ * WRITES d_dfeat (same strides as d_feat; may be NULL) and d_dsh ([P,16], may be NULL).
+ * d_dgeo (may be NULL): extra upstream gradient of o rows 1..15 ([P,16], from the normals head). */
 int nerf_mlp_bwd(const float* d_feat, int64_t feat_stride_point, int64_t feat_stride_level,
                  const float* d_sh, int64_t sh_stride,
                  const float* d_viewdirs, int64_t samples_per_ray,
                  const uint8_t* d_keep, int64_t n_points,
                  const nerf_mlp_weights* weights, const float* d_graw /* [P,4] */,
-                 const nerf_mlp_grads* grads, float* d_dfeat, float* d_dsh, void* stream);
+                 const nerf_mlp_grads* grads, float* d_dfeat, float* d_dsh, const float* d_dgeo, void* stream);
+
+/* ---- normals head (run_nerf_helpers.py:259-263, :298-302): n = normalize(N1 relu(N0 geo + b0) + b1)
+ * nn.Linear layouts: n0 [32,15], b0 [32], n1 [3,32], b1 [3].
+ * fwd: raw7 [P,7] = [raw4, n]; with d_keep, n_z := 0 where !keep (run_network's mask hits the LAST
+ *      channel, run_nerf.py:66). bwd: from graw7 writes graw4 [P,4] (the MLP's upstream grad),
+ *      dgeo [P,16] (row 0 = 0), and the per-point factors of the head's weight gradients:
+ *      hid = relu hidden [P,32], dhid = d pre-ReLU hidden [P,32], dn = d pre-normalize n [P,3]
+ *      (dN0 = dhid^T geo, db0 = sum dhid, dN1 = dn^T hid, db1 = sum dn). */
+typedef struct {
+    const float* n0;
+    const float* b0;
+    const float* n1;
+    const float* b1;
+} nerf_normal_head;
+
+int nerf_normal_head_fwd(const float* d_o16, const float* d_raw4, const uint8_t* d_keep, int64_t n_points,
+                         const nerf_normal_head* head, float* d_raw7, void* stream);
+int nerf_normal_head_bwd(const float* d_o16, const uint8_t* d_keep, int64_t n_points,
+                         const nerf_normal_head* head, const float* d_graw7, float* d_graw4, float* d_dgeo,
+                         float* d_hid, float* d_dhid, float* d_dn, void* stream);
 
 /* ---- volume compositing (raw2outputs, run_nerf.py:347-411), one wavefront per ray ----------
  * d_raw [R,S,raw_channels] (4, or 7 with normals), d_z [R,S], d_rays_d [R,3] (unnormalised),

@@ -29,6 +29,10 @@ class MlpGrads(ctypes.Structure):
     _fields_ = [(n, c_vp) for n in ("w0", "w1", "c0", "c1", "c2")]
 
 
+class NormalHead(ctypes.Structure):
+    _fields_ = [("n0", c_vp), ("b0", c_vp), ("n1", c_vp), ("b1", c_vp)]
+
+
 class RAdamSegment(ctypes.Structure):
     _fields_ = [("p", c_vp), ("g", c_vp), ("m", c_vp), ("v", c_vp), ("n", c_i64),
                 ("beta1", ctypes.c_float), ("beta2", ctypes.c_float),
@@ -47,9 +51,12 @@ SIGNATURES = {
                                 ctypes.POINTER(c_vp), c_vp, ctypes.c_size_t, c_vp],
     "nerf_sh4_fwd": [c_vp, c_i64, c_vp, c_vp],
     "nerf_mlp_fwd": [c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, ctypes.POINTER(MlpWeights),
-                     c_vp, c_vp],
+                     c_vp, c_vp, c_vp],
     "nerf_mlp_bwd": [c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, ctypes.POINTER(MlpWeights),
-                     c_vp, ctypes.POINTER(MlpGrads), c_vp, c_vp, c_vp],
+                     c_vp, ctypes.POINTER(MlpGrads), c_vp, c_vp, c_vp, c_vp],
+    "nerf_normal_head_fwd": [c_vp, c_vp, c_vp, c_i64, ctypes.POINTER(NormalHead), c_vp, c_vp],
+    "nerf_normal_head_bwd": [c_vp, c_vp, c_i64, ctypes.POINTER(NormalHead), c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                             c_vp],
     "nerf_composite_fwd": [c_vp, c_int, c_vp, c_vp, c_vp, c_i64, c_int, c_int,
                            c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
     "nerf_composite_bwd": [c_vp, c_int, c_vp, c_vp, c_vp, c_i64, c_int, c_int,

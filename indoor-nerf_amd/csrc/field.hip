@@ -385,7 +385,7 @@ extern "C" int nerf_sh4_fwd(const float* d_dirs, int64_t n, float* d_out, void* 
 extern "C" int nerf_mlp_fwd(const float* d_feat, int64_t feat_stride_point, int64_t feat_stride_level,
                             const float* d_sh, int64_t sh_stride, const float* d_viewdirs, int64_t samples_per_ray,
                             const uint8_t* d_keep, int64_t n_points, const nerf_mlp_weights* weights, float* d_raw,
-                            void* stream) {
+                            float* d_geo, void* stream) {
     MlpArgs a{};
     int rc = fill_args(a, d_feat, feat_stride_point, feat_stride_level, d_sh, sh_stride, d_viewdirs, samples_per_ray,
                        d_keep, n_points, weights);
@@ -393,7 +393,9 @@ extern "C" int nerf_mlp_fwd(const float* d_feat, int64_t feat_stride_point, int6
     NERF_REQUIRE(d_raw, "mlp_fwd: null output");
     if (n_points == 0) return NERF_OK;
     a.raw = d_raw;
+    a.geo_out = d_geo;
     if (use_frag_mlp()) return launch_mlp_fwd_frag(a, as_stream(stream));
+    NERF_REQUIRE(!d_geo, "mlp_fwd: the geo output needs the default (fragment) MLP kernels");
     const int64_t tiles = (n_points + 31) / 32;
     const int64_t blocks = std::min<int64_t>((tiles + 3) / 4, 256 * 3);
     hipLaunchKernelGGL(mlp_fwd_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), a);
@@ -405,7 +407,7 @@ extern "C" int nerf_mlp_bwd(const float* d_feat, int64_t feat_stride_point, int6
                             const float* d_sh, int64_t sh_stride, const float* d_viewdirs, int64_t samples_per_ray,
                             const uint8_t* d_keep, int64_t n_points, const nerf_mlp_weights* weights,
                             const float* d_graw, const nerf_mlp_grads* grads, float* d_dfeat, float* d_dsh,
-                            void* stream) {
+                            const float* d_dgeo, void* stream) {
     MlpArgs a{};
     int rc = fill_args(a, d_feat, feat_stride_point, feat_stride_level, d_sh, sh_stride, d_viewdirs, samples_per_ray,
                        d_keep, n_points, weights);
@@ -413,8 +415,9 @@ extern "C" int nerf_mlp_bwd(const float* d_feat, int64_t feat_stride_point, int6
     NERF_REQUIRE(d_graw && grads && grads->w0 && grads->w1 && grads->c0 && grads->c1 && grads->c2,
                  "mlp_bwd: null gradient pointer");
     if (n_points == 0) return NERF_OK;
-    a.graw = d_graw; a.G = *grads; a.dfeat = d_dfeat; a.dsh = d_dsh;
+    a.graw = d_graw; a.G = *grads; a.dfeat = d_dfeat; a.dsh = d_dsh; a.dgeo = d_dgeo;
     if (use_frag_mlp()) return launch_mlp_bwd_frag(a, as_stream(stream));
+    NERF_REQUIRE(!d_dgeo, "mlp_bwd: the geo gradient input needs the default (fragment) MLP kernels");
     const int64_t tiles = (n_points + 31) / 32;
     const int64_t blocks = std::min<int64_t>((tiles + BWD_WAVES - 1) / BWD_WAVES, 256);
     hipLaunchKernelGGL(mlp_bwd_kernel, dim3((unsigned)blocks), dim3(64 * BWD_WAVES), 0, as_stream(stream), a);

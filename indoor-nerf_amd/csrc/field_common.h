@@ -49,6 +49,8 @@ struct MlpArgs {
     nerf_mlp_grads G;
     float* dfeat;
     float* dsh;
+    float* geo_out;       // fwd, optional: o = [sigma, geo 15] per point, [P,16] (normals head input)
+    const float* dgeo;    // bwd, optional: upstream d o from the normals head, [P,16] (row 0 ignored)
 };
 
 __device__ inline void load_weight_images(float* lds, const nerf_mlp_weights& W) {

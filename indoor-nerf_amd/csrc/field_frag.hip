@@ -178,6 +178,10 @@ __device__ __forceinline__ void store_raw(const MlpArgs& a, const TileIn& in, co
         const bool keep = a.keep ? a.keep[in.pt] != 0 : true;
         *reinterpret_cast<float4*>(a.raw + 4 * in.pt) = make_float4(v.rgb[0], v.rgb[1], v.rgb[2], keep ? v.o[0] : 0.f);
     }
+    if (a.geo_out && in.valid) {   // o rows 0..15 of this point: registers r with row_of(r, h) < 16
+#pragma unroll
+        for (int r = 0; r < 8; ++r) a.geo_out[in.pt * 16 + row_of(r, h)] = v.o[r];
+    }
 }
 
 __global__ void __launch_bounds__(256, 2) mlp_fwd_frag_kernel(MlpArgs a) {
@@ -368,7 +372,19 @@ __global__ void __launch_bounds__(256, 1) mlp_bwd_frag_kernel(MlpArgs a) {
         NERF_WAVE_SYNC();
 
         // ---- C0: g_o(geo rows) = C0y^T g_a2 ; o-row 0 = g_sigma ; dC0y += g_a2^T y0
+        // The accumulator is seeded rather than patched after the MFMAs: row 0 (sigma) with g_sigma
+        // (the C0GT fragments are zero for row 0) and, with the normals head, rows 1..15 with its
+        // d geo. A VALU read-modify-write of these accumulator registers right after the MFMA chain
+        // produced wrong sums when both terms were non-zero (ROCm 7.2, gfx950).
         floatx16 go = zero16();
+        if (h == 0) go[0] = gsig;
+        if (a.dgeo && in.valid) {
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+                const int row = row_of(r, h);
+                if (row >= 1) go[r] = a.dgeo[in.pt * 16 + row];
+            }
+        }
 #pragma unroll
         for (int ti = 0; ti < 2; ++ti)
 #pragma unroll
@@ -377,7 +393,6 @@ __global__ void __launch_bounds__(256, 1) mlp_bwd_frag_kernel(MlpArgs a) {
 #pragma unroll
                 for (int q = 0; q < 4; ++q) go = NERF_MFMA(q4(w, q), ga2[ti][4 * rg + q], go);
             }
-        if (h == 0) go[0] = gsig;
 #pragma unroll
         for (int s = 0; s < 8; ++s) stA[j * RS_T + 2 * s + h] = in.shv[s];
 #pragma unroll

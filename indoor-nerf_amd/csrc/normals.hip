@@ -1,0 +1,173 @@
+// Normals head of NeRFSmall (run_nerf_helpers.py:259-263, :298-302; ScanNet configuration):
+//   n = normalize(N1 relu(N0 geo + b0) + b1)        N0 [32,15], b0 [32], N1 [3,32], b1 [3]
+// appended to the MLP's raw as channels 4..6 (raw [P,7] = rgb, sigma, n). run_network's mask
+// `outputs_flat[~keep_mask, -1] = 0` (run_nerf.py:66) then zeroes the LAST channel, which with
+// normals is n_z, not sigma: the reference's behaviour, reproduced here (the MLP runs without its
+// sigma mask when the head is on).
+//
+// One thread per point; the 611 head parameters sit in LDS (wave-uniform broadcast reads). The
+// backward writes the per-point quantities the weight gradients are built from (h, d pre-ReLU h,
+// d pre-normalize n): those are (P x 32)^T (P x 15)-shaped sums with K = P, left to the GEMM
+// library by the host (plain library GEMMs, cdna_hip_programming.md: hipBLASLt/rocBLAS for those).
+#include "common.h"
+
+namespace nerf {
+
+constexpr int NH_HID = 32, NH_GEO = 15;
+constexpr int NH_N0 = 0, NH_B0 = NH_N0 + NH_HID * NH_GEO, NH_N1 = NH_B0 + NH_HID, NH_B1 = NH_N1 + 3 * NH_HID,
+              NH_ALL = NH_B1 + 3;   // 611 floats
+
+struct NormalArgs {
+    const float* o16;      // [P,16] = [sigma, geo 15] (MLP geo output)
+    const float* raw4;     // [P,4]
+    const uint8_t* keep;   // [P] or null
+    int64_t P;
+    nerf_normal_head W;
+    float* raw7;           // fwd out [P,7]
+    const float* graw7;    // bwd in [P,7]
+    float* graw4;          // bwd out [P,4]
+    float* dgeo;           // bwd out [P,16] (row 0 = 0)
+    float* hid;            // bwd out [P,32] relu hidden
+    float* dhid;           // bwd out [P,32] d pre-ReLU hidden
+    float* dn;             // bwd out [P,3] d pre-normalize n
+};
+
+__device__ __forceinline__ void load_head(float* s, const nerf_normal_head& W) {
+    for (int i = threadIdx.x; i < NH_ALL; i += blockDim.x) {
+        float v;
+        if (i < NH_B0) v = W.n0[i - NH_N0];
+        else if (i < NH_N1) v = W.b0[i - NH_B0];
+        else if (i < NH_B1) v = W.n1[i - NH_N1];
+        else v = W.b1[i - NH_B1];
+        s[i] = v;
+    }
+    __syncthreads();
+}
+
+// F.linear with bias (addmm: bias + x W^T); fp32 dot products in input order
+__device__ __forceinline__ void head_forward(const float* s, const float* geo, float* h, float* n) {
+#pragma unroll 4
+    for (int i = 0; i < NH_HID; ++i) {
+        float acc = 0.f;
+#pragma unroll
+        for (int k = 0; k < NH_GEO; ++k) acc = fmaf(s[NH_N0 + i * NH_GEO + k], geo[k], acc);
+        h[i] = acc + s[NH_B0 + i];
+    }
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        float acc = 0.f;
+#pragma unroll
+        for (int i = 0; i < NH_HID; ++i) acc = fmaf(s[NH_N1 + c * NH_HID + i], fmaxf(h[i], 0.f), acc);
+        n[c] = acc + s[NH_B1 + c];
+    }
+}
+
+__global__ void __launch_bounds__(256) normal_head_fwd_kernel(NormalArgs a) {
+    __shared__ float s[NH_ALL];
+    load_head(s, a.W);
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= a.P) return;
+    float geo[NH_GEO], h[NH_HID], n[3];
+#pragma unroll
+    for (int k = 0; k < NH_GEO; ++k) geo[k] = a.o16[p * 16 + 1 + k];
+    head_forward(s, geo, h, n);
+    // F.normalize(x, dim=-1): x / max(||x||_2, 1e-12)
+    const float nrm = fmaxf(sqrtf(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]), 1e-12f);
+    const float4 r = *reinterpret_cast<const float4*>(a.raw4 + 4 * p);
+    const bool keep = a.keep ? a.keep[p] != 0 : true;
+    float* o = a.raw7 + 7 * p;
+    o[0] = r.x; o[1] = r.y; o[2] = r.z; o[3] = r.w;
+    o[4] = n[0] / nrm;
+    o[5] = n[1] / nrm;
+    o[6] = keep ? n[2] / nrm : 0.f;
+}
+
+__global__ void __launch_bounds__(256) normal_head_bwd_kernel(NormalArgs a) {
+    __shared__ float s[NH_ALL];
+    load_head(s, a.W);
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= a.P) return;
+    float geo[NH_GEO], h[NH_HID], n[3];
+#pragma unroll
+    for (int k = 0; k < NH_GEO; ++k) geo[k] = a.o16[p * 16 + 1 + k];
+    head_forward(s, geo, h, n);
+    const float* g7 = a.graw7 + 7 * p;
+    *reinterpret_cast<float4*>(a.graw4 + 4 * p) = make_float4(g7[0], g7[1], g7[2], g7[3]);
+    const bool keep = a.keep ? a.keep[p] != 0 : true;
+    const float g[3] = {g7[4], g7[5], keep ? g7[6] : 0.f};
+    // y = x / m, m = max(||x||, eps): dx = g / m - x (g.x) / (m^2 ||x||)  (the norm term only while
+    // ||x|| > eps, where the clamp passes the gradient)
+    const float len = sqrtf(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+    const float m = fmaxf(len, 1e-12f);
+    const float gx = g[0] * n[0] + g[1] * n[1] + g[2] * n[2];
+    float dn[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) dn[c] = g[c] / m - (len > 1e-12f ? n[c] * (gx / (m * m * len)) : 0.f);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) a.dn[p * 3 + c] = dn[c];
+    float dg[NH_GEO];
+#pragma unroll
+    for (int k = 0; k < NH_GEO; ++k) dg[k] = 0.f;
+#pragma unroll 4
+    for (int i = 0; i < NH_HID; ++i) {
+        const float hr = fmaxf(h[i], 0.f);
+        const float dh = h[i] > 0.f ? (s[NH_N1 + i] * dn[0] + s[NH_N1 + NH_HID + i] * dn[1]) +
+                                           s[NH_N1 + 2 * NH_HID + i] * dn[2]
+                                    : 0.f;
+        a.hid[p * NH_HID + i] = hr;
+        a.dhid[p * NH_HID + i] = dh;
+#pragma unroll
+        for (int k = 0; k < NH_GEO; ++k) dg[k] = fmaf(s[NH_N0 + i * NH_GEO + k], dh, dg[k]);
+    }
+    float* d = a.dgeo + p * 16;
+    d[0] = 0.f;
+#pragma unroll
+    for (int k = 0; k < NH_GEO; ++k) d[1 + k] = dg[k];
+}
+
+static int fill_normal(NormalArgs& a, const float* o16, const uint8_t* keep, int64_t P, const nerf_normal_head* W) {
+    NERF_REQUIRE(P >= 0, "normal_head: n_points < 0");
+    NERF_REQUIRE(o16 && W && W->n0 && W->b0 && W->n1 && W->b1, "normal_head: null argument");
+    a.o16 = o16;
+    a.keep = keep;
+    a.P = P;
+    a.W = *W;
+    return NERF_OK;
+}
+
+}  // namespace nerf
+
+using namespace nerf;
+
+extern "C" int nerf_normal_head_fwd(const float* d_o16, const float* d_raw4, const uint8_t* d_keep, int64_t n_points,
+                                    const nerf_normal_head* head, float* d_raw7, void* stream) {
+    NormalArgs a{};
+    int rc = fill_normal(a, d_o16, d_keep, n_points, head);
+    if (rc) return rc;
+    NERF_REQUIRE(d_raw4 && d_raw7, "normal_head_fwd: null buffer");
+    if (n_points == 0) return NERF_OK;
+    a.raw4 = d_raw4;
+    a.raw7 = d_raw7;
+    hipLaunchKernelGGL(normal_head_fwd_kernel, dim3(blocks_for(n_points, 256)), dim3(256), 0, as_stream(stream), a);
+    NERF_CHECK_LAUNCH("normal_head_fwd");
+    return NERF_OK;
+}
+
+extern "C" int nerf_normal_head_bwd(const float* d_o16, const uint8_t* d_keep, int64_t n_points,
+                                    const nerf_normal_head* head, const float* d_graw7, float* d_graw4, float* d_dgeo,
+                                    float* d_hid, float* d_dhid, float* d_dn, void* stream) {
+    NormalArgs a{};
+    int rc = fill_normal(a, d_o16, d_keep, n_points, head);
+    if (rc) return rc;
+    NERF_REQUIRE(d_graw7 && d_graw4 && d_dgeo && d_hid && d_dhid && d_dn, "normal_head_bwd: null buffer");
+    if (n_points == 0) return NERF_OK;
+    a.graw7 = d_graw7;
+    a.graw4 = d_graw4;
+    a.dgeo = d_dgeo;
+    a.hid = d_hid;
+    a.dhid = d_dhid;
+    a.dn = d_dn;
+    hipLaunchKernelGGL(normal_head_bwd_kernel, dim3(blocks_for(n_points, 256)), dim3(256), 0, as_stream(stream), a);
+    NERF_CHECK_LAUNCH("normal_head_bwd");
+    return NERF_OK;
+}

@@ -28,26 +28,68 @@ def _grads_struct(weights):
     return g
 
 
+def _head_struct(head):
+    h = _lib.NormalHead()
+    for name, t in zip(("n0", "b0", "n1", "b1"), head):
+        setattr(h, name, _lib.ptr(t.detach(), "normal_net." + name).value)
+    return h
+
+
+def _head_forward(o16, raw4, keep, head):
+    """raw [P,7] = [raw4, normals] (csrc/normals.hip); keep masks n_z like run_network."""
+    P = raw4.shape[0]
+    raw7 = torch.empty(P, 7, device=raw4.device, dtype=torch.float32)
+    _lib.call("nerf_normal_head_fwd", _lib.ptr(o16, "geo"), _lib.ptr(raw4, "raw4"),
+              _lib.ptr(keep, "keep", dtype=torch.bool, allow_none=True), P, _head_struct(head),
+              _lib.ptr(raw7, "raw7"), _lib.stream())
+    return raw7
+
+
+def _head_backward(o16, keep, head, g7, needs):
+    """-> (graw4 [P,4], dgeo [P,16], grads of (N0, b0, N1, b1) or None each)."""
+    P = o16.shape[0]
+    f = dict(device=o16.device, dtype=torch.float32)
+    graw4, dgeo = torch.empty(P, 4, **f), torch.empty(P, 16, **f)
+    hid, dhid, dn = torch.empty(P, 32, **f), torch.empty(P, 32, **f), torch.empty(P, 3, **f)
+    _lib.call("nerf_normal_head_bwd", _lib.ptr(o16, "geo"), _lib.ptr(keep, "keep", dtype=torch.bool, allow_none=True),
+              P, _head_struct(head), _lib.ptr(g7.contiguous(), "grad_raw"), _lib.ptr(graw4), _lib.ptr(dgeo),
+              _lib.ptr(hid), _lib.ptr(dhid), _lib.ptr(dn), _lib.stream())
+    # weight gradients: sums over points (K = P) -> library GEMMs
+    grads = (dhid.t().mm(o16[:, 1:16]) if needs[0] else None, dhid.sum(0) if needs[1] else None,
+             dn.t().mm(hid) if needs[2] else None, dn.sum(0) if needs[3] else None)
+    return graw4, dgeo, grads
+
+
 class MLPFn(torch.autograd.Function):
-    """x [P, 48] = [hash feat 32 | SH 16] -> raw [P, 4]. Weight grads accumulate into .grad."""
+    """x [P, 48] = [hash feat 32 | SH 16] -> raw [P, 4] (or [P, 7] with the normals head). MLP weight
+    grads accumulate into .grad; the head's are returned to autograd."""
 
     @staticmethod
-    def forward(ctx, x, net, *weights):
+    def forward(ctx, x, net, *params):
+        weights, head = params[:5], params[5:]
         x = x.contiguous()
         P = x.shape[0]
         raw = torch.empty(P, 4, device=x.device, dtype=torch.float32)
+        o16 = torch.empty(P, 16, device=x.device, dtype=torch.float32) if head else None
         xp = _lib.ptr(x, "x")
         sh_ptr = _lib.c_vp(x.data_ptr() + 32 * 4) if P > 0 else xp
         _lib.call("nerf_mlp_fwd", xp, 48, 2, sh_ptr, 48, None, 1, None, P, _weights_struct(weights),
-                  _lib.ptr(raw, "raw"), _lib.stream())
-        ctx.save_for_backward(x, *weights)
+                  _lib.ptr(raw, "raw"), _lib.ptr(o16, "geo", allow_none=True), _lib.stream())
+        if head:
+            raw = _head_forward(o16, raw, None, head)
+        ctx.save_for_backward(x, o16, *params)
+        ctx.n_head = len(head)
         return raw
 
     @staticmethod
     def backward(ctx, g_raw):
-        x, *weights = ctx.saved_tensors
+        x, o16, *params = ctx.saved_tensors
+        weights, head = params[:5], params[5:]
         P = x.shape[0]
         g = g_raw.contiguous()
+        head_grads, dgeo = (None,) * ctx.n_head, None
+        if head:
+            g, dgeo, head_grads = _head_backward(o16, None, head, g, ctx.needs_input_grad[7:11])
         need_x = ctx.needs_input_grad[0]
         dx = torch.zeros_like(x) if need_x else None
         if any(w.requires_grad for w in weights) or need_x:
@@ -60,10 +102,11 @@ class MLPFn(torch.autograd.Function):
                 dsh_t = torch.empty(P, 16, device=x.device, dtype=torch.float32)
                 dsh = _lib.ptr(dsh_t, "dsh")
             _lib.call("nerf_mlp_bwd", xp, 48, 2, sh_ptr, 48, None, 1, None, P, _weights_struct(weights),
-                      _lib.ptr(g, "grad_raw"), grads, dfeat, dsh, _lib.stream())
+                      _lib.ptr(g, "grad_raw"), grads, dfeat, dsh, _lib.ptr(dgeo, "dgeo", allow_none=True),
+                      _lib.stream())
             if need_x:
                 dx[:, 32:] = dsh_t
-        return (dx, None) + (None,) * len(weights)
+        return (dx, None) + (None,) * len(weights) + tuple(head_grads)
 
 
 def _scratch_grads(weights):
@@ -74,14 +117,14 @@ def _scratch_grads(weights):
 
 
 class FieldFn(torch.autograd.Function):
-    """Fused run_network: pts [P,3], viewdirs [R,3] (P = R*S) -> raw [P,4]."""
+    """Fused run_network: pts [P,3], viewdirs [R,3] (P = R*S) -> raw [P,4] ([P,7] with normals)."""
 
     @staticmethod
     def forward(ctx, pts, viewdirs, samples_per_ray, embedder, net, *params):
         if pts.requires_grad or viewdirs.requires_grad:
             raise NotImplementedError("run_network: gradients w.r.t. positions/directions are not implemented")
         n_tab = embedder.n_levels
-        tables, weights = params[:n_tab], params[n_tab:]
+        tables, weights, head = params[:n_tab], params[n_tab:n_tab + 5], params[n_tab + 5:]
         pts = pts.contiguous()
         viewdirs = viewdirs.contiguous()
         P = pts.shape[0]
@@ -92,30 +135,40 @@ class FieldFn(torch.autograd.Function):
                   meta["log2_T"], _lib.ptr_array(tables), _lib.ptr(feat, "feat"), 2, 2 * P,
                   _lib.ptr(keep, "keep", dtype=torch.bool), _lib.stream())
         raw = torch.empty(P, 4, device=pts.device, dtype=torch.float32)
+        o16 = torch.empty(P, 16, device=pts.device, dtype=torch.float32) if head else None
+        # with the normals head, run_network's mask lands on n_z, not sigma (run_nerf.py:66)
         _lib.call("nerf_mlp_fwd", _lib.ptr(feat, "feat"), 2, 2 * P, None, 0, _lib.ptr(viewdirs, "viewdirs"),
-                  samples_per_ray, _lib.ptr(keep, "keep", dtype=torch.bool), P, _weights_struct(weights),
-                  _lib.ptr(raw, "raw"), _lib.stream())
-        ctx.save_for_backward(pts, viewdirs, feat, keep, *params)
-        ctx.spr, ctx.embedder, ctx.n_tab = samples_per_ray, embedder, n_tab
+                  samples_per_ray, None if head else _lib.ptr(keep, "keep", dtype=torch.bool), P,
+                  _weights_struct(weights), _lib.ptr(raw, "raw"), _lib.ptr(o16, "geo", allow_none=True),
+                  _lib.stream())
+        if head:
+            raw = _head_forward(o16, raw, keep, head)
+        ctx.save_for_backward(pts, viewdirs, feat, keep, o16, *params)
+        ctx.spr, ctx.embedder, ctx.n_tab, ctx.n_head = samples_per_ray, embedder, n_tab, len(head)
         return raw
 
     @staticmethod
     def backward(ctx, g_raw):
-        pts, viewdirs, feat, keep, *params = ctx.saved_tensors
-        tables, weights = params[:ctx.n_tab], params[ctx.n_tab:]
+        pts, viewdirs, feat, keep, o16, *params = ctx.saved_tensors
+        n_tab = ctx.n_tab
+        tables, weights, head = params[:n_tab], params[n_tab:n_tab + 5], params[n_tab + 5:]
         P = pts.shape[0]
         g = g_raw.contiguous()
+        head_grads, dgeo = (None,) * ctx.n_head, None
+        if head:
+            g, dgeo, head_grads = _head_backward(o16, keep, head, g, ctx.needs_input_grad[5 + n_tab + 5:])
         need_tab = any(t.requires_grad for t in tables)
         dfeat = torch.empty_like(feat) if need_tab else None
         if any(w.requires_grad for w in weights) or need_tab:
             grads = _grads_struct(weights) if any(w.requires_grad for w in weights) else _scratch_grads(weights)
             _lib.call("nerf_mlp_bwd", _lib.ptr(feat, "feat"), 2, 2 * P, None, 0, _lib.ptr(viewdirs, "viewdirs"),
-                      ctx.spr, _lib.ptr(keep, "keep", dtype=torch.bool), P, _weights_struct(weights),
-                      _lib.ptr(g, "grad_raw"), grads, _lib.ptr(dfeat, "dfeat", allow_none=True), None,
+                      ctx.spr, None if head else _lib.ptr(keep, "keep", dtype=torch.bool), P,
+                      _weights_struct(weights), _lib.ptr(g, "grad_raw"), grads,
+                      _lib.ptr(dfeat, "dfeat", allow_none=True), None, _lib.ptr(dgeo, "dgeo", allow_none=True),
                       _lib.stream())
         if need_tab:
             hash_encode_bwd(pts, ctx.embedder._meta, dfeat, 2, 2 * P, accumulate_grad_buffers(tables))
-        return (None,) * (5 + len(params))
+        return (None,) * (5 + n_tab + len(weights)) + tuple(head_grads)
 
 
 class NeRFSmall(nn.Module):
@@ -132,8 +185,6 @@ class NeRFSmall(nn.Module):
                                       "(2, 64, 15, 3, 64, 32, 16)")
         if use_quantization:
             raise NotImplementedError("NeRFSmall(use_quantization=True): A-CAQ MLP quantizers are not built yet")
-        if predict_normals:
-            raise NotImplementedError("NeRFSmall(predict_normals=True): the normals head is not built yet")
         self.input_ch = input_ch
         self.input_ch_views = input_ch_views
         self.use_quantization = use_quantization
@@ -148,16 +199,33 @@ class NeRFSmall(nn.Module):
         self.color_net = nn.ModuleList([nn.Linear(input_ch_views + geo_feat_dim, hidden_dim_color, bias=False),
                                         nn.Linear(hidden_dim_color, hidden_dim_color, bias=False),
                                         nn.Linear(hidden_dim_color, 3, bias=False)])
+        if predict_normals:   # run_nerf_helpers.py:259-263
+            self.normal_net = nn.Sequential(nn.Linear(geo_feat_dim, hidden_dim // 2), nn.ReLU(),
+                                            nn.Linear(hidden_dim // 2, 3))
 
     def mlp_weights(self):
         return [self.sigma_net[0].weight, self.sigma_net[1].weight, self.color_net[0].weight,
                 self.color_net[1].weight, self.color_net[2].weight]
 
+    def head_params(self):
+        """Normals head parameters (N0, b0, N1, b1), or [] without the head."""
+        if not self.predict_normals:
+            return []
+        return [self.normal_net[0].weight, self.normal_net[0].bias, self.normal_net[2].weight,
+                self.normal_net[2].bias]
+
+    def field_params(self):
+        return self.mlp_weights() + self.head_params()
+
+    @property
+    def raw_channels(self):
+        return 7 if self.predict_normals else 4
+
     def forward(self, x):
-        for w in self.mlp_weights():
+        for w in self.field_params():
             if not w.is_contiguous():
                 raise ValueError("NeRFSmall: weights must be contiguous")
-        return MLPFn.apply(x.float(), self, *self.mlp_weights())
+        return MLPFn.apply(x.float(), self, *self.field_params())
 
 
 def batchify(fn, chunk):
@@ -180,8 +248,8 @@ def run_network(inputs, viewdirs, fn, embed_fn, embeddirs_fn, netchunk=1024 * 64
             embed_fn.current_step += 1
         R, S = inputs.shape[0], inputs.shape[1]
         raw = FieldFn.apply(inputs.reshape(-1, 3), viewdirs, S, embed_fn, fn,
-                            *embed_fn.tables(), *fn.mlp_weights())
-        return raw.reshape(R, S, 4)
+                            *embed_fn.tables(), *fn.field_params())
+        return raw.reshape(R, S, fn.raw_channels)
     inputs_flat = torch.reshape(inputs, [-1, inputs.shape[-1]])
     embedded, keep_mask = embed_fn(inputs_flat)
     if viewdirs is not None:

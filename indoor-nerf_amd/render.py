@@ -102,10 +102,16 @@ def raw2outputs(raw, z_vals, rays_d, raw_noise_std=0, white_bkgd=False, pytest=F
             noise = _pytest_uniforms((R, S), raw.device) * raw_noise_std
         else:
             noise = torch.randn(R, S, device=raw.device) * raw_noise_std
-    if predict_normals and raw.shape[-1] != 7:
-        raise ValueError("raw2outputs(predict_normals=True) needs 7 raw channels")
+    if raw.shape[-1] not in (4, 7):
+        raise ValueError(f"raw2outputs: raw must have 4 or 7 channels, got {raw.shape[-1]}")
+    if not predict_normals and raw.shape[-1] == 7:
+        raw = raw[..., :4]      # the reference reads channels 0..3 only
     outs = CompositeFn.apply(raw.float(), z_vals, rays_d, noise, white_bkgd)
     if predict_normals:
+        if raw.shape[-1] == 4:
+            # the reference slices raw[..., 4:7] of a 4-channel raw (the coarse net has no normals
+            # head, run_nerf.py:240-247 vs :260-268): an empty [R, 0] normal map (run_nerf.py:361,407)
+            return outs + (raw.new_zeros(R, 0),)
         return outs
     return outs[:6]
 

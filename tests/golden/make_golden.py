@@ -417,6 +417,69 @@ def gen_quant(ref, out):
     np.savez_compressed(os.path.join(out, "f11_quant.npz"), **d)
 
 
+def gen_normals(ref, out):
+    """F13: NeRFSmall with the normals head (run_nerf_helpers.py:259-263, :298-302) fwd/bwd, the
+    7-channel raw2outputs fwd/bwd (run_nerf.py:358-411), and run_network's last-channel mask on a
+    7-channel raw (run_nerf.py:66) through a full render with predict_normals=True."""
+    rng = np.random.RandomState(13)
+    d = {}
+    ref.h.NeRFSmall.predict_normals = True          # the class attribute the ctor reads (HEAD bug)
+    try:
+        torch.manual_seed(21)
+        net = ref.h.NeRFSmall(num_layers=2, hidden_dim=64, geo_feat_dim=15, num_layers_color=3,
+                              hidden_dim_color=64, input_ch=32, input_ch_views=16)
+    finally:
+        ref.h.NeRFSmall.predict_normals = False
+    net.predict_normals = True
+    x = (rng.randn(1024, 48) * 0.5).astype(np.float32)
+    g = rng.randn(1024, 7).astype(np.float32)
+    xt = torch.from_numpy(x).requires_grad_(True)
+    raw = net(xt)
+    (raw * torch.from_numpy(g)).sum().backward()
+    d.update(x=x, g_raw=g, raw=raw.detach().numpy(), dx=xt.grad.numpy())
+    d.update(mlp_arrays(net, "w_"))
+    for k, p in net.named_parameters():
+        d["dw_" + k.replace(".", "_")] = p.grad.numpy().copy()
+    # 7-channel compositing with normals
+    R, S = 64, 64
+    raw7, z, rd = composite_inputs(rng, R, S, degenerate=False)
+    raw7 = np.concatenate([raw7, rng.randn(R, S, 3).astype(np.float32)], -1)
+    rt = torch.from_numpy(raw7).requires_grad_(True)
+    res = ref.rn.raw2outputs(rt, torch.from_numpy(z), torch.from_numpy(rd), 0, True, pytest=False,
+                             predict_normals=True)
+    gn = rng.randn(R, 3).astype(np.float32)
+    gr = rng.randn(R, 3).astype(np.float32)
+    ((res[6] * torch.from_numpy(gn)).sum() + (res[0] * torch.from_numpy(gr)).sum()).backward()
+    d.update(c_raw=raw7, c_z=z, c_d=rd, c_gn=gn, c_gr=gr, c_rgb=res[0].detach().numpy(),
+             c_normal=res[6].detach().numpy(), c_draw=rt.grad.numpy())
+    # full render: coarse net without the head, fine net with it (create_nerf, run_nerf.py:240-268)
+    table = closed_form_table()
+    emb = make_embedder(ref, 1024, table)
+    coarse = make_mlp(ref, 22)
+    ref.h.NeRFSmall.predict_normals = True
+    try:
+        torch.manual_seed(23)
+        fine = ref.h.NeRFSmall(num_layers=2, hidden_dim=64, geo_feat_dim=15, num_layers_color=3,
+                               hidden_dim_color=64, input_ch=32, input_ch_views=16)
+    finally:
+        ref.h.NeRFSmall.predict_normals = False
+    fine.predict_normals = True
+    kw = build_render_kwargs(ref, emb, coarse, fine, 64, 64, 1.0, 0.0, False)
+    kw["predict_normals"] = True
+    ro, rd = synthetic_rays(64, seed=14)
+    ro[:4] += np.array([0.0, 0.0, 3.5], np.float32)   # a few rays that leave the bbox: keep mask hits n_z
+    with torch.no_grad():
+        rgb, depth, acc, extras = ref.rn.render(800, 800, None, chunk=32768,
+                                                rays=(torch.from_numpy(ro), torch.from_numpy(rd)),
+                                                retraw=True, pytest=True, **kw)
+    d.update(r_rays_o=ro, r_rays_d=rd, r_rgb=rgb.numpy(), r_normal=extras["normal_map"].numpy(),
+             r_normal0_shape=np.array(extras["normal0"].shape), r_raw=extras["raw"].numpy(),
+             r_rgb0=extras["rgb0"].numpy())
+    d.update(mlp_arrays(coarse, "r_coarse_"))
+    d.update(mlp_arrays(fine, "r_fine_"))
+    np.savez_compressed(os.path.join(out, "f13_normals.npz"), **d)
+
+
 def gen_tv(ref, out):
     table = closed_form_table(scale=0.05, salt=5)
     emb = make_embedder(ref, 1024, table)
@@ -455,23 +518,22 @@ def gen_tv(ref, out):
                         grad=np.concatenate(g_all))
 
 
-def main():
+def main(only=None):
+    """Write every fixture, or only the named generators (e.g. `make_golden.py normals quant`)."""
     out = HERE
     ref = load_reference()
-    levels = gen_levels(ref, out)
-    gen_voxel(ref, out, levels)
-    gen_hash(ref, out)
-    gen_sh(ref, out)
-    gen_mlp(ref, out)
-    gen_composite(ref, out)
-    gen_pdf(ref, out)
-    gen_render(ref, out)
-    gen_quant(ref, out)
-    gen_tv(ref, out)
-    gen_train(ref, out)
+    gens = [("voxel", None), ("hash", gen_hash), ("sh", gen_sh), ("mlp", gen_mlp), ("composite", gen_composite),
+            ("pdf", gen_pdf), ("render", gen_render), ("quant", gen_quant), ("tv", gen_tv), ("train", gen_train),
+            ("normals", gen_normals)]
+    if not only or "levels" in only or "voxel" in only:
+        levels = gen_levels(ref, out)
+        gen_voxel(ref, out, levels)
+    for name, fn in gens:
+        if fn is not None and (not only or name in only):
+            fn(ref, out)
     tot = sum(os.path.getsize(os.path.join(out, f)) for f in os.listdir(out) if f.endswith(".npz"))
     print(f"golden fixtures written to {out}: {tot / 1e6:.2f} MB")
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1:])

@@ -421,3 +421,116 @@ def test_hash_encode_bwd_large_ray_ordered(nerf, gpu, oracle):
             err = (got[lvl].cpu().double() - ref).abs()
             bad = err > 2e-6 * scale + 1e-30
             assert not bool(bad.any()), f"{name} level {lvl}: {int(bad.sum())} rows off, max err {float(err.max()):.3e}"
+
+
+def _mlp_n(nerf, gpu, d, prefix, normals):
+    net = nerf.NeRFSmall(num_layers=2, hidden_dim=64, geo_feat_dim=15, num_layers_color=3, hidden_dim_color=64,
+                         input_ch=32, input_ch_views=16, predict_normals=normals).to(gpu)
+    with torch.no_grad():
+        for k, p in net.named_parameters():
+            p.copy_(torch.from_numpy(d[prefix + k.replace(".", "_")]))
+    return net
+
+
+def test_normals_head_fwd_bwd(nerf, gpu, golden):
+    """NeRFSmall(predict_normals=True) (run_nerf_helpers.py:259-263, :298-302): raw [P,7] and every
+    gradient (MLP weights, normals head weights and biases, inputs) against the reference (F13)."""
+    g = golden("f13_normals")
+    net = _mlp_n(nerf, gpu, g, "w_", True)
+    x = torch.from_numpy(g["x"]).to(gpu).requires_grad_(True)
+    raw = net(x)
+    assert raw.shape == (1024, 7)
+    np.testing.assert_allclose(raw.detach().cpu().numpy(), g["raw"], rtol=1e-4, atol=2e-6)
+    (raw * torch.from_numpy(g["g_raw"]).to(gpu)).sum().backward()
+    np.testing.assert_allclose(x.grad.cpu().numpy(), g["dx"], rtol=1e-4, atol=2e-6)
+    for k, p in net.named_parameters():
+        np.testing.assert_allclose(p.grad.cpu().numpy(), g["dw_" + k.replace(".", "_")], rtol=1e-4, atol=1e-4,
+                                   err_msg=k)
+
+
+def test_composite_normals(nerf, gpu, golden):
+    """raw2outputs(predict_normals=True) on a 7-channel raw: normal map and d raw (F13)."""
+    g = golden("f13_normals")
+    raw = torch.from_numpy(g["c_raw"]).to(gpu).requires_grad_(True)
+    out = nerf.raw2outputs(raw, torch.from_numpy(g["c_z"]).to(gpu), torch.from_numpy(g["c_d"]).to(gpu), 0, True,
+                           predict_normals=True)
+    assert len(out) == 7
+    np.testing.assert_allclose(out[0].detach().cpu().numpy(), g["c_rgb"], rtol=1e-5, atol=2e-6)
+    np.testing.assert_allclose(out[6].detach().cpu().numpy(), g["c_normal"], rtol=1e-4, atol=2e-6)
+    ((out[6] * torch.from_numpy(g["c_gn"]).to(gpu)).sum() + (out[0] * torch.from_numpy(g["c_gr"]).to(gpu)).sum()
+     ).backward()
+    np.testing.assert_allclose(raw.grad.cpu().numpy(), g["c_draw"], rtol=1e-4, atol=1e-5)
+
+
+def test_render_with_normals(nerf, gpu, golden):
+    """Full render with predict_normals=True (coarse net without the head, fine net with it, as
+    create_nerf builds them): normal_map, the empty [R, 0] normal0 of the 4-channel coarse pass, and
+    run_network's mask on the LAST channel (n_z, not sigma) for samples outside the bbox (F13)."""
+    g = golden("f13_normals")
+    emb = _embedder(nerf, gpu, 1024, closed_form_table())
+    coarse, fine = _mlp_n(nerf, gpu, g, "r_coarse_", False), _mlp_n(nerf, gpu, g, "r_fine_", True)
+    sh = nerf.SHEncoder()
+    nqf = lambda inputs, viewdirs, fn: nerf.run_network(inputs, viewdirs, fn, emb, sh)  # noqa: E731
+    kw = dict(network_query_fn=nqf, perturb=1.0, N_importance=64, network_fine=fine, N_samples=64, network_fn=coarse,
+              embed_fn=emb, use_viewdirs=True, white_bkgd=True, raw_noise_std=0.0, predict_normals=True, ndc=False,
+              lindisp=False, near=2.0, far=6.0)
+    ro, rd = (torch.from_numpy(g[f"r_rays_{k}"]).to(gpu) for k in ("o", "d"))
+    with torch.no_grad():
+        rgb, depth, acc, ex = nerf.render(800, 800, None, rays=(ro, rd), retraw=True, pytest=True, **kw)
+    assert tuple(ex["normal0"].shape) == tuple(g["r_normal0_shape"])
+    np.testing.assert_allclose(ex["rgb0"].cpu().numpy(), g["r_rgb0"], rtol=1e-4, atol=1e-4)
+    raw = ex["raw"].cpu().numpy()
+    ref_raw = g["r_raw"]
+    assert raw.shape == ref_raw.shape
+    # fine samples follow sample_pdf (PSNR-equivalent bounds, as test_render_end_to_end)
+    np.testing.assert_allclose(rgb.cpu().numpy(), g["r_rgb"], rtol=0, atol=1e-3)
+    np.testing.assert_allclose(ex["normal_map"].cpu().numpy(), g["r_normal"], rtol=0, atol=2e-3)
+    # the mask: n_z == 0 exactly where the reference has it (out-of-bbox samples), sigma never masked
+    masked = ref_raw[..., 6] == 0
+    assert masked.sum() > 0
+    np.testing.assert_array_equal(raw[..., 6] == 0, masked)
+    assert not np.any((raw[..., 3] == 0) & masked)
+
+
+def test_mlp_bwd_geo_gradient_superposition(nerf, gpu):
+    """The MLP backward's extra d geo input (from the normals head) against torch fp32 autograd of the
+    same MLP with an extra (o * d_geo) term, alone and together with d raw (a VALU patch of the
+    MFMA accumulator once broke only the combined case)."""
+    from indoor_nerf_amd import _lib, field
+    torch.manual_seed(0)
+    net = nerf.NeRFSmall(2, 64, 15, 3, 64, 32, 16).to(gpu)
+    P = 1024
+    x = torch.randn(P, 48, device=gpu) * 0.5
+    W = [w.detach() for w in net.mlp_weights()]
+
+    def ours(gr4, dgeo):
+        dfeat = torch.zeros(P, 48, device=gpu)
+        for w in net.mlp_weights():
+            w.grad = None
+        grads = field._grads_struct(net.mlp_weights())
+        _lib.call("nerf_mlp_bwd", _lib.ptr(x), 48, 2, _lib.c_vp(x.data_ptr() + 128), 48, None, 1, None, P,
+                  field._weights_struct(net.mlp_weights()), _lib.ptr(gr4), grads, _lib.ptr(dfeat), None,
+                  _lib.ptr(dgeo, allow_none=True), _lib.stream())
+        return dfeat[:, :32].clone(), [w.grad.clone() for w in net.mlp_weights()]
+
+    def ref(gr4, dgeo):
+        xr = x.clone().requires_grad_(True)
+        Wr = [w.clone().requires_grad_(True) for w in W]
+        h = torch.relu(xr[:, :32] @ Wr[0].t())
+        o = h @ Wr[1].t()
+        c = torch.relu(torch.cat([xr[:, 32:], o[:, 1:]], -1) @ Wr[2].t())
+        c = torch.relu(c @ Wr[3].t())
+        out = torch.cat([c @ Wr[4].t(), o[:, :1]], -1)
+        ((out * gr4).sum() + (o * dgeo).sum()).backward()
+        return xr.grad[:, :32], [w.grad for w in Wr]
+
+    torch.backends.cuda.matmul.allow_tf32 = False
+    gr4 = torch.randn(P, 4, device=gpu)
+    dgeo = torch.randn(P, 16, device=gpu)
+    dgeo[:, 0] = 0
+    for a, b in ((torch.zeros_like(gr4), dgeo), (gr4, dgeo)):
+        f1, w1 = ours(a, b)
+        f2, w2 = ref(a, b)
+        torch.testing.assert_close(f1, f2, rtol=1e-4, atol=1e-5)
+        for p, q in zip(w1, w2):
+            torch.testing.assert_close(p, q, rtol=1e-4, atol=1e-4)

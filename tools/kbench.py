@@ -127,12 +127,12 @@ def mlp_bench():
 
         def fwd():
             _lib.call("nerf_mlp_fwd", _lib.ptr(feat), 2, 2 * P, None, 0, _lib.ptr(vd), 64,
-                      _lib.ptr(keep, dtype=torch.bool), P, _weights_struct(W), _lib.ptr(raw), _lib.stream())
+                      _lib.ptr(keep, dtype=torch.bool), P, _weights_struct(W), _lib.ptr(raw), None, _lib.stream())
 
         def bwd():
             _lib.call("nerf_mlp_bwd", _lib.ptr(feat), 2, 2 * P, None, 0, _lib.ptr(vd), 64,
                       _lib.ptr(keep, dtype=torch.bool), P, _weights_struct(W), _lib.ptr(graw), _grads_struct(W),
-                      _lib.ptr(dfeat), None, _lib.stream())
+                      _lib.ptr(dfeat), None, None, _lib.stream())
 
         res = {}
         # correctness of the MLP variants against each other (raw and weight grads)
@@ -262,10 +262,10 @@ def mlp_only(P=786432, reps=10):
     W = net.mlp_weights()
     for _ in range(reps):
         _lib.call("nerf_mlp_fwd", _lib.ptr(feat), 2, 2 * P, None, 0, _lib.ptr(vd), 64,
-                  _lib.ptr(keep, dtype=torch.bool), P, _weights_struct(W), _lib.ptr(raw), _lib.stream())
+                  _lib.ptr(keep, dtype=torch.bool), P, _weights_struct(W), _lib.ptr(raw), None, _lib.stream())
         _lib.call("nerf_mlp_bwd", _lib.ptr(feat), 2, 2 * P, None, 0, _lib.ptr(vd), 64,
                   _lib.ptr(keep, dtype=torch.bool), P, _weights_struct(W), _lib.ptr(graw), _grads_struct(W),
-                  _lib.ptr(dfeat), None, _lib.stream())
+                  _lib.ptr(dfeat), None, None, _lib.stream())
     torch.cuda.synchronize()
     print(json.dumps({"points": P, "reps": reps}))
 
