@@ -53,6 +53,17 @@ int nerf_hash_encode_fwd(const float* d_xyz, int64_t n_points,
                          float* d_feat, int64_t feat_stride_point, int64_t feat_stride_level,
                          uint8_t* d_keep, void* stream);
 
+/* Same with the A-CAQ quantizers applied to every gathered corner feature before the trilinear
+ * blend (hash_encoding.py:97-101, LearnedBitwidthQuantizer.forward quantization.py:144-187).
+ * d_qrec: device float[n_levels][8] records from nerf_quant_params (NULL = no quantization). The
+ * backward is unchanged: the quantizer's straight-through estimator passes d feat through. */
+int nerf_hash_encode_fwd_q(const float* d_xyz, int64_t n_points,
+                           const float* bbox_min3, const float* bbox_max3,
+                           const float* level_res, int n_levels, int log2_T,
+                           const float* const* d_tables, const float* d_qrec,
+                           float* d_feat, int64_t feat_stride_point, int64_t feat_stride_level,
+                           uint8_t* d_keep, void* stream);
+
 /* d_dtables: host array of n_levels device pointers; gradients are ACCUMULATED (atomic adds). */
 int nerf_hash_encode_bwd(const float* d_xyz, int64_t n_points,
                          const float* bbox_min3, const float* bbox_max3,
@@ -119,6 +130,28 @@ int nerf_mlp_bwd(const float* d_feat, int64_t feat_stride_point, int64_t feat_st
                  const uint8_t* d_keep, int64_t n_points,
                  const nerf_mlp_weights* weights, const float* d_graw /* [P,4] */,
                  const nerf_mlp_grads* grads, float* d_dfeat, float* d_dsh, const float* d_dgeo, void* stream);
+
+/* A-CAQ variants (NeRFSmall(use_quantization=True), run_nerf_helpers.py:268-284). The caller passes
+ * the fake-quantized W0 (nerf_fake_quant with sigma_weight_quantizer's record) as weights->w0, and
+ * gradients land in the unquantized W0's grad (straight-through). d_act_qrec (NULL = none): record
+ * of sigma_act_quantizers[0], applied to h = relu(x W0^T) before the second sigma layer; the
+ * backward keeps relu'(pre) as the mask and Q(h) as the activation, as the reference's autograd.
+ * fwd with d_act_minmax != NULL is a calibration-only launch: it folds min/max of relu(x W0^T)
+ * over the first act_calib_points points into d_act_minmax (uint32[2], see nerf_quant_minmax)
+ * and writes no outputs. */
+int nerf_mlp_fwd_q(const float* d_feat, int64_t feat_stride_point, int64_t feat_stride_level,
+                   const float* d_sh, int64_t sh_stride,
+                   const float* d_viewdirs, int64_t samples_per_ray,
+                   const uint8_t* d_keep, int64_t n_points,
+                   const nerf_mlp_weights* weights, float* d_raw, float* d_geo,
+                   const float* d_act_qrec, uint32_t* d_act_minmax, int64_t act_calib_points, void* stream);
+int nerf_mlp_bwd_q(const float* d_feat, int64_t feat_stride_point, int64_t feat_stride_level,
+                   const float* d_sh, int64_t sh_stride,
+                   const float* d_viewdirs, int64_t samples_per_ray,
+                   const uint8_t* d_keep, int64_t n_points,
+                   const nerf_mlp_weights* weights, const float* d_graw,
+                   const nerf_mlp_grads* grads, float* d_dfeat, float* d_dsh, const float* d_dgeo,
+                   const float* d_act_qrec, void* stream);
 
 /* ---- normals head (run_nerf_helpers.py:259-263, :298-302): n = normalize(N1 relu(N0 geo + b0) + b1)
  * nn.Linear layouts: n0 [32,15], b0 [32], n1 [3,32], b1 [3].
@@ -227,6 +260,62 @@ int nerf_train_loss_bwd(const float* d_rgb, const float* d_rgb0, const float* d_
                         float sparse_w, int n_tv, float tv_w, const float* d_grad_loss, float* d_grad_rgb,
                         float* d_grad_rgb0, float* d_grad_sparsity, float* d_grad_sparsity0, float* d_grad_tv,
                         void* stream);
+
+/* ---- A-CAQ learned-bitwidth quantization (PocketNeRF/quantization.py:63-187, config 5) --------
+ * A quantizer's state is the reference module's tensors, as caller-owned device scalars (fp32):
+ * soft_bits, range_scale, v_max (NULL for a symmetric quantizer) and the running_min/max buffers.
+ * Quantization record (device float[8]): {scale, scale + 1e-8, zero_point, qmin, qmax, ste, bits, 0}.
+ */
+typedef struct {
+    const float* soft_bits;
+    float* range_scale;
+    float* v_max;          /* NULL: symmetric */
+    float* running_min;
+    float* running_max;
+    float min_bits, max_bits;
+} nerf_quantizer;
+
+#define NERF_MAX_QUANTIZERS 32
+
+/* Records of n quantizers (<= NERF_MAX_QUANTIZERS), as LearnedBitwidthQuantizer.forward derives them
+ * (:158-178): B = clamp(soft_bits) (training) or round(B) (eval); qmin/qmax from round(B);
+ * symmetric scale = range/2^(B-1), zp = 0; asymmetric scale = max(range,1e-8)/(2^B-1),
+ * zp = round(clamp(v_max/scale, qmin, qmax)). ste = training. */
+int nerf_quant_params(const nerf_quantizer* qs, int n, int training, float* d_rec, void* stream);
+
+/* Calibration statistics: d_minmax is device uint32[n][2] holding order-preserving encodings of
+ * (min, max). reset sets n slots to (+inf, -inf); minmax folds d_x[0..count) into slot 0. */
+int nerf_quant_minmax_reset(uint32_t* d_minmax, int n, void* stream);
+int nerf_quant_minmax(const float* d_x, int64_t count, uint32_t* d_minmax, void* stream);
+
+/* Per-level min/max of the gathered corner features [P,8,2] of the hash encoding (the x
+ * LearnedBitwidthQuantizer.calibrate sees, quantization.py:97-119), folded into d_minmax[level]. */
+int nerf_hash_gather_minmax(const float* d_xyz, int64_t n_points, const float* bbox_min3, const float* bbox_max3,
+                            const float* level_res, int n_levels, int log2_T, const float* const* d_tables,
+                            uint32_t* d_minmax, void* stream);
+
+/* calibrate() (:97-119) of n quantizers from the batch statistics d_minmax[n][2]: running min/max,
+ * then range_scale (= max - min, or 2 max|.| when symmetric) and v_max (= running max). */
+int nerf_quant_calibrate(const nerf_quantizer* qs, int n, const uint32_t* d_minmax, void* stream);
+
+/* Elementwise fake quantization y = Q(x) with one record (d_rec); in training mode the STE form
+ * x + (deq - x), whose gradient is the identity. d_y may alias d_x. */
+int nerf_fake_quant(const float* d_x, int64_t count, const float* d_rec, float* d_y, void* stream);
+
+/* Int-packed hash tables for eval-mode rendering (quantizer in eval mode: value = (q - zp) * scale
+ * with q the integer code). Level l's codes take code_bits[l] in {4, 8, 16} bits per feature (two
+ * features per entry: 1, 2 or 4 bytes per entry), or 32 = the dequantized fp32 value itself.
+ * nerf_quant_packed_layout: code_bits and byte offsets (256-B aligned) of each level; returns the
+ * total bytes. pack: codes of every table entry. fwd: the gather + trilinear of
+ * nerf_hash_encode_fwd_q reading codes; bit-identical to it in eval mode. */
+size_t nerf_quant_packed_layout(const int* level_bits, int n_levels, int log2_T, int* code_bits, int64_t* offsets);
+int nerf_quant_pack_tables(const float* const* d_tables, int n_levels, int log2_T, const float* d_qrec,
+                           const int* code_bits, const int64_t* offsets, void* d_packed, void* stream);
+int nerf_hash_encode_fwd_packed(const float* d_xyz, int64_t n_points, const float* bbox_min3, const float* bbox_max3,
+                                const float* level_res, int n_levels, int log2_T, const void* d_packed,
+                                const int* code_bits, const int64_t* offsets, const float* d_qrec,
+                                float* d_feat, int64_t feat_stride_point, int64_t feat_stride_level,
+                                uint8_t* d_keep, void* stream);
 
 #ifdef __cplusplus
 }

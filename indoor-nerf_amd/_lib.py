@@ -41,10 +41,17 @@ class RAdamSegment(ctypes.Structure):
                 ("mode", c_int)]
 
 
+class Quantizer(ctypes.Structure):
+    _fields_ = [("soft_bits", c_vp), ("range_scale", c_vp), ("v_max", c_vp), ("running_min", c_vp),
+                ("running_max", c_vp), ("min_bits", ctypes.c_float), ("max_bits", ctypes.c_float)]
+
+
 # name -> argtypes (restype is int for all but the two metadata calls)
 SIGNATURES = {
     "nerf_hash_encode_fwd": [c_vp, c_i64, c_f32p, c_f32p, c_f32p, c_int, c_int, ctypes.POINTER(c_vp),
                              c_vp, c_i64, c_i64, c_vp, c_vp],
+    "nerf_hash_encode_fwd_q": [c_vp, c_i64, c_f32p, c_f32p, c_f32p, c_int, c_int, ctypes.POINTER(c_vp), c_vp,
+                               c_vp, c_i64, c_i64, c_vp, c_vp],
     "nerf_hash_encode_bwd": [c_vp, c_i64, c_f32p, c_f32p, c_f32p, c_int, c_int, c_vp, c_i64, c_i64,
                              ctypes.POINTER(c_vp), c_vp],
     "nerf_hash_encode_bwd_ws": [c_vp, c_i64, c_f32p, c_f32p, c_f32p, c_int, c_int, c_vp, c_i64, c_i64,
@@ -54,6 +61,10 @@ SIGNATURES = {
                      c_vp, c_vp, c_vp],
     "nerf_mlp_bwd": [c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, ctypes.POINTER(MlpWeights),
                      c_vp, ctypes.POINTER(MlpGrads), c_vp, c_vp, c_vp, c_vp],
+    "nerf_mlp_fwd_q": [c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, ctypes.POINTER(MlpWeights),
+                       c_vp, c_vp, c_vp, c_vp, c_i64, c_vp],
+    "nerf_mlp_bwd_q": [c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, ctypes.POINTER(MlpWeights),
+                       c_vp, ctypes.POINTER(MlpGrads), c_vp, c_vp, c_vp, c_vp, c_vp],
     "nerf_normal_head_fwd": [c_vp, c_vp, c_vp, c_i64, ctypes.POINTER(NormalHead), c_vp, c_vp],
     "nerf_normal_head_bwd": [c_vp, c_vp, c_i64, ctypes.POINTER(NormalHead), c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                              c_vp],
@@ -71,6 +82,16 @@ SIGNATURES = {
                     ctypes.POINTER(c_vp), c_vp],
     "nerf_train_loss_fwd": [c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, ctypes.c_float, c_vp, c_int, ctypes.c_float,
                             c_vp, c_vp, c_vp, c_vp],
+    "nerf_quant_params": [ctypes.POINTER(Quantizer), c_int, c_int, c_vp, c_vp],
+    "nerf_quant_minmax_reset": [c_vp, c_int, c_vp],
+    "nerf_quant_minmax": [c_vp, c_i64, c_vp, c_vp],
+    "nerf_hash_gather_minmax": [c_vp, c_i64, c_f32p, c_f32p, c_f32p, c_int, c_int, ctypes.POINTER(c_vp), c_vp, c_vp],
+    "nerf_quant_calibrate": [ctypes.POINTER(Quantizer), c_int, c_vp, c_vp],
+    "nerf_fake_quant": [c_vp, c_i64, c_vp, c_vp, c_vp],
+    "nerf_quant_pack_tables": [ctypes.POINTER(c_vp), c_int, c_int, c_vp, ctypes.POINTER(c_int),
+                               ctypes.POINTER(c_i64), c_vp, c_vp],
+    "nerf_hash_encode_fwd_packed": [c_vp, c_i64, c_f32p, c_f32p, c_f32p, c_int, c_int, c_vp, ctypes.POINTER(c_int),
+                                    ctypes.POINTER(c_i64), c_vp, c_vp, c_i64, c_i64, c_vp, c_vp],
     "nerf_train_loss_bwd": [c_vp, c_vp, c_vp, c_i64, ctypes.c_float, c_int, ctypes.c_float, c_vp, c_vp, c_vp,
                             c_vp, c_vp, c_vp, c_vp],
 }
@@ -93,6 +114,9 @@ def load():
     lib.nerf_abi_version.argtypes = []
     lib.nerf_hash_encode_bwd_workspace_bytes.restype = ctypes.c_size_t
     lib.nerf_hash_encode_bwd_workspace_bytes.argtypes = [c_int, c_int, c_i64]
+    lib.nerf_quant_packed_layout.restype = ctypes.c_size_t
+    lib.nerf_quant_packed_layout.argtypes = [ctypes.POINTER(c_int), c_int, c_int, ctypes.POINTER(c_int),
+                                             ctypes.POINTER(c_i64)]
     for name, argtypes in SIGNATURES.items():
         fn = getattr(lib, name)
         fn.argtypes = argtypes
@@ -102,7 +126,8 @@ def load():
 
 
 def exported_symbols():
-    return ["nerf_last_error", "nerf_abi_version", "nerf_hash_encode_bwd_workspace_bytes"] + list(SIGNATURES)
+    return ["nerf_last_error", "nerf_abi_version", "nerf_hash_encode_bwd_workspace_bytes",
+            "nerf_quant_packed_layout"] + list(SIGNATURES)
 
 
 _TIMING = None   # when a list: (name, start_event, end_event) per launch, recorded on the current stream

@@ -7,6 +7,7 @@ from .hashgrid import HashEmbedder, SHEncoder, level_resolutions
 from .losses import sigma_sparsity_loss, total_variation_all, total_variation_loss, train_loss
 from .model import create_nerf, make_args, save_checkpoint, train_step
 from .optim import RAdam
+from .quantization import FakeQuantizer, LearnedBitwidthQuantizer, PassthroughQuantizer, calculate_fqr
 from .render import (batchify_rays, get_rays, get_rays_np, img2mse, manual_seed, mse2psnr, ndc_rays, raw2outputs,
                      render, render_rays, sample_pdf, to8b)
 
@@ -14,7 +15,8 @@ __all__ = ["HashEmbedder", "SHEncoder", "NeRFSmall", "RAdam", "run_network", "ba
            "render_rays", "raw2outputs", "sample_pdf", "get_rays", "get_rays_np", "ndc_rays", "img2mse", "mse2psnr",
            "to8b", "create_nerf", "make_args", "save_checkpoint", "train_step", "total_variation_loss",
            "total_variation_all", "train_loss", "sigma_sparsity_loss", "level_resolutions", "GradArena", "init_process_group",
-           "shard", "broadcast_params", "manual_seed", "load_library"]
+           "shard", "broadcast_params", "manual_seed", "load_library", "LearnedBitwidthQuantizer", "FakeQuantizer",
+           "PassthroughQuantizer", "calculate_fqr"]
 
 
 def load_library():

@@ -382,20 +382,25 @@ extern "C" int nerf_sh4_fwd(const float* d_dirs, int64_t n, float* d_out, void* 
     return NERF_OK;
 }
 
-extern "C" int nerf_mlp_fwd(const float* d_feat, int64_t feat_stride_point, int64_t feat_stride_level,
-                            const float* d_sh, int64_t sh_stride, const float* d_viewdirs, int64_t samples_per_ray,
-                            const uint8_t* d_keep, int64_t n_points, const nerf_mlp_weights* weights, float* d_raw,
-                            float* d_geo, void* stream) {
+extern "C" int nerf_mlp_fwd_q(const float* d_feat, int64_t feat_stride_point, int64_t feat_stride_level,
+                              const float* d_sh, int64_t sh_stride, const float* d_viewdirs, int64_t samples_per_ray,
+                              const uint8_t* d_keep, int64_t n_points, const nerf_mlp_weights* weights, float* d_raw,
+                              float* d_geo, const float* d_act_qrec, uint32_t* d_act_minmax, int64_t act_calib_points,
+                              void* stream) {
     MlpArgs a{};
     int rc = fill_args(a, d_feat, feat_stride_point, feat_stride_level, d_sh, sh_stride, d_viewdirs, samples_per_ray,
                        d_keep, n_points, weights);
     if (rc) return rc;
-    NERF_REQUIRE(d_raw, "mlp_fwd: null output");
+    NERF_REQUIRE(d_raw || d_act_minmax, "mlp_fwd: null output");
     if (n_points == 0) return NERF_OK;
     a.raw = d_raw;
     a.geo_out = d_geo;
+    a.aq = reinterpret_cast<const QuantRec*>(d_act_qrec);
+    a.act_minmax = d_act_minmax;
+    a.calib_points = act_calib_points;
     if (use_frag_mlp()) return launch_mlp_fwd_frag(a, as_stream(stream));
     NERF_REQUIRE(!d_geo, "mlp_fwd: the geo output needs the default (fragment) MLP kernels");
+    NERF_REQUIRE(!d_act_qrec && !d_act_minmax, "mlp_fwd: quantization needs the default (fragment) MLP kernels");
     const int64_t tiles = (n_points + 31) / 32;
     const int64_t blocks = std::min<int64_t>((tiles + 3) / 4, 256 * 3);
     hipLaunchKernelGGL(mlp_fwd_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), a);
@@ -403,11 +408,19 @@ extern "C" int nerf_mlp_fwd(const float* d_feat, int64_t feat_stride_point, int6
     return NERF_OK;
 }
 
-extern "C" int nerf_mlp_bwd(const float* d_feat, int64_t feat_stride_point, int64_t feat_stride_level,
+extern "C" int nerf_mlp_fwd(const float* d_feat, int64_t feat_stride_point, int64_t feat_stride_level,
                             const float* d_sh, int64_t sh_stride, const float* d_viewdirs, int64_t samples_per_ray,
-                            const uint8_t* d_keep, int64_t n_points, const nerf_mlp_weights* weights,
-                            const float* d_graw, const nerf_mlp_grads* grads, float* d_dfeat, float* d_dsh,
-                            const float* d_dgeo, void* stream) {
+                            const uint8_t* d_keep, int64_t n_points, const nerf_mlp_weights* weights, float* d_raw,
+                            float* d_geo, void* stream) {
+    return nerf_mlp_fwd_q(d_feat, feat_stride_point, feat_stride_level, d_sh, sh_stride, d_viewdirs, samples_per_ray,
+                          d_keep, n_points, weights, d_raw, d_geo, nullptr, nullptr, 0, stream);
+}
+
+extern "C" int nerf_mlp_bwd_q(const float* d_feat, int64_t feat_stride_point, int64_t feat_stride_level,
+                              const float* d_sh, int64_t sh_stride, const float* d_viewdirs, int64_t samples_per_ray,
+                              const uint8_t* d_keep, int64_t n_points, const nerf_mlp_weights* weights,
+                              const float* d_graw, const nerf_mlp_grads* grads, float* d_dfeat, float* d_dsh,
+                              const float* d_dgeo, const float* d_act_qrec, void* stream) {
     MlpArgs a{};
     int rc = fill_args(a, d_feat, feat_stride_point, feat_stride_level, d_sh, sh_stride, d_viewdirs, samples_per_ray,
                        d_keep, n_points, weights);
@@ -416,11 +429,22 @@ extern "C" int nerf_mlp_bwd(const float* d_feat, int64_t feat_stride_point, int6
                  "mlp_bwd: null gradient pointer");
     if (n_points == 0) return NERF_OK;
     a.graw = d_graw; a.G = *grads; a.dfeat = d_dfeat; a.dsh = d_dsh; a.dgeo = d_dgeo;
+    a.aq = reinterpret_cast<const QuantRec*>(d_act_qrec);
     if (use_frag_mlp()) return launch_mlp_bwd_frag(a, as_stream(stream));
     NERF_REQUIRE(!d_dgeo, "mlp_bwd: the geo gradient input needs the default (fragment) MLP kernels");
+    NERF_REQUIRE(!d_act_qrec, "mlp_bwd: quantization needs the default (fragment) MLP kernels");
     const int64_t tiles = (n_points + 31) / 32;
     const int64_t blocks = std::min<int64_t>((tiles + BWD_WAVES - 1) / BWD_WAVES, 256);
     hipLaunchKernelGGL(mlp_bwd_kernel, dim3((unsigned)blocks), dim3(64 * BWD_WAVES), 0, as_stream(stream), a);
     NERF_CHECK_LAUNCH("mlp_bwd");
     return NERF_OK;
+}
+
+extern "C" int nerf_mlp_bwd(const float* d_feat, int64_t feat_stride_point, int64_t feat_stride_level,
+                            const float* d_sh, int64_t sh_stride, const float* d_viewdirs, int64_t samples_per_ray,
+                            const uint8_t* d_keep, int64_t n_points, const nerf_mlp_weights* weights,
+                            const float* d_graw, const nerf_mlp_grads* grads, float* d_dfeat, float* d_dsh,
+                            const float* d_dgeo, void* stream) {
+    return nerf_mlp_bwd_q(d_feat, feat_stride_point, feat_stride_level, d_sh, sh_stride, d_viewdirs, samples_per_ray,
+                          d_keep, n_points, weights, d_graw, grads, d_dfeat, d_dsh, d_dgeo, nullptr, stream);
 }

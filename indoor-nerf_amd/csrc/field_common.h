@@ -6,7 +6,7 @@
 
 #include <algorithm>
 
-#include "common.h"
+#include "hash_common.h"
 
 namespace nerf {
 
@@ -51,7 +51,17 @@ struct MlpArgs {
     float* dsh;
     float* geo_out;       // fwd, optional: o = [sigma, geo 15] per point, [P,16] (normals head input)
     const float* dgeo;    // bwd, optional: upstream d o from the normals head, [P,16] (row 0 ignored)
+    const QuantRec* aq;   // optional A-CAQ record of the layer-0 activation quantizer
+    uint32_t* act_minmax; // calibration-only launch: min/max of relu(x W0^T) (order-preserving u32)
+    int64_t calib_points;
 };
+
+// A-CAQ activation quantizer on a layer-0 accumulator tile (sigma_act_quantizers[0],
+// run_nerf_helpers.py:280-284).
+__device__ __forceinline__ void fake_quant16(floatx16& v, const QuantRec& q) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = fake_quant(v[r], q);
+}
 
 __device__ inline void load_weight_images(float* lds, const nerf_mlp_weights& W) {
     for (int i = threadIdx.x; i < LDS_W; i += blockDim.x) {

@@ -108,7 +108,9 @@ __device__ __forceinline__ float4 frag4f(const float* img, int f, int lane) {
 
 __device__ __forceinline__ float q4f(const float4& v, int q) { return q == 0 ? v.x : q == 1 ? v.y : q == 2 ? v.z : v.w; }
 
-__device__ __forceinline__ void fwd_tile(const float* img, const TileIn& A, Acts& a, int lane, bool need_rgb) {
+template <bool QUANT>
+__device__ __forceinline__ void fwd_tile(const float* img, const TileIn& A, Acts& a, int lane, bool need_rgb,
+                                         const QuantRec& aq) {
     a.h1[0] = a.h1[1] = zero16();
 #pragma unroll
     for (int sg = 0; sg < 4; ++sg) {
@@ -120,6 +122,7 @@ __device__ __forceinline__ void fwd_tile(const float* img, const TileIn& A, Acts
         }
     }
     relu16(a.h1[0]); relu16(a.h1[1]);
+    if constexpr (QUANT) { fake_quant16(a.h1[0], aq); fake_quant16(a.h1[1], aq); }
     __builtin_amdgcn_sched_barrier(0);
     a.o = zero16();
 #pragma unroll
@@ -184,6 +187,7 @@ __device__ __forceinline__ void store_raw(const MlpArgs& a, const TileIn& in, co
     }
 }
 
+template <bool QUANT>
 __global__ void __launch_bounds__(256, 2) mlp_fwd_frag_kernel(MlpArgs a) {
     __shared__ __attribute__((aligned(16))) float img[LDS_FWD_FR];
     for (int idx = threadIdx.x; idx < LDS_FWD_FR; idx += blockDim.x) {
@@ -192,13 +196,62 @@ __global__ void __launch_bounds__(256, 2) mlp_fwd_frag_kernel(MlpArgs a) {
     }
     __syncthreads();
     const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
+    QuantRec aq{};
+    if constexpr (QUANT) aq = *a.aq;
     const int64_t n_tiles = (a.P + 31) / 32;
     for (int64_t t0 = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); t0 < n_tiles; t0 += (int64_t)gridDim.x * 4) {
         TileIn A;
         load_in(a, t0, j, h, A);
         Acts va;
-        fwd_tile(img, A, va, lane, true);
+        fwd_tile<QUANT>(img, A, va, lane, true, aq);
         store_raw(a, A, va, h);
+    }
+}
+
+// Calibration-only launch of the activation quantizer (quantization.py:97-119 on the first
+// netchunk's h = relu(x W0^T)): layer 0 per tile, wave min/max, one atomic pair per wave.
+__global__ void __launch_bounds__(256) mlp_act_minmax_kernel(MlpArgs a) {
+    __shared__ __attribute__((aligned(16))) float img[32 * 64];
+    for (int idx = threadIdx.x; idx < 32 * 64; idx += blockDim.x) {
+        const int f = idx >> 6, ln = idx & 63;
+        img[(f >> 2) * 256 + ln * 4 + (f & 3)] = frag_value(F_L0 + f, ln, a.W);
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
+    const int64_t n = a.calib_points < a.P ? a.calib_points : a.P;
+    const int64_t n_tiles = (n + 31) / 32;
+    float lo = INFINITY, hi = -INFINITY;
+    for (int64_t t0 = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); t0 < n_tiles; t0 += (int64_t)gridDim.x * 4) {
+        TileIn A;
+        load_in(a, t0, j, h, A);
+        floatx16 h1[2];
+        h1[0] = h1[1] = zero16();
+#pragma unroll
+        for (int sg = 0; sg < 4; ++sg) {
+            const float4 w0 = frag4f(img, F_L0 + 4 * sg, lane), w1 = frag4f(img, F_L0 + 16 + 4 * sg, lane);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                h1[0] = NERF_MFMA(q4f(w0, q), A.x[4 * sg + q], h1[0]);
+                h1[1] = NERF_MFMA(q4f(w1, q), A.x[4 * sg + q], h1[1]);
+            }
+        }
+        relu16(h1[0]); relu16(h1[1]);
+        if (A.pt < n) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                lo = fminf(lo, fminf(h1[0][r], h1[1][r]));
+                hi = fmaxf(hi, fmaxf(h1[0][r], h1[1][r]));
+            }
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        lo = fminf(lo, __shfl_xor(lo, o, 64));
+        hi = fmaxf(hi, __shfl_xor(hi, o, 64));
+    }
+    if (lane == 0 && lo <= hi) {
+        atomicMin(a.act_minmax, f2ord(lo));
+        atomicMax(a.act_minmax + 1, f2ord(hi));
     }
 }
 
@@ -231,6 +284,7 @@ __device__ __forceinline__ void wgrad_acc(floatx16& acc, const float* A, int ai0
     }
 }
 
+template <bool QUANT>
 __global__ void __launch_bounds__(256, 1) mlp_bwd_frag_kernel(MlpArgs a) {
     __shared__ __attribute__((aligned(16))) float lds[LDS_BWD2];
     float* img = lds;
@@ -245,6 +299,8 @@ __global__ void __launch_bounds__(256, 1) mlp_bwd_frag_kernel(MlpArgs a) {
     __syncthreads();
 
     const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
+    QuantRec aq{};
+    if constexpr (QUANT) aq = *a.aq;
     floatx16 dC2[2], dC1[4], dC0[2], dW1[2], dW0[2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) { dC2[i] = zero16(); dC0[i] = zero16(); dW1[i] = zero16(); dW0[i] = zero16(); }
@@ -268,6 +324,15 @@ __global__ void __launch_bounds__(256, 1) mlp_bwd_frag_kernel(MlpArgs a) {
             }
         }
         relu16(f.h1[0]); relu16(f.h1[1]);
+        // with the activation quantizer, h1 holds Q(relu(pre)) and the ReLU mask is kept as bits
+        uint32_t m1 = 0;
+        if constexpr (QUANT) {
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) m1 |= (f.h1[t][r] > 0.f ? 1u : 0u) << (16 * t + r);
+            fake_quant16(f.h1[0], aq); fake_quant16(f.h1[1], aq);
+        }
         __builtin_amdgcn_sched_barrier(0);
         f.o = zero16();
 #pragma unroll
@@ -435,7 +500,10 @@ __global__ void __launch_bounds__(256, 1) mlp_bwd_frag_kernel(MlpArgs a) {
 #pragma unroll
         for (int t = 0; t < 2; ++t)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) ga1[t][r] = f.h1[t][r] > 0.f ? ga1[t][r] : 0.f;
+            for (int r = 0; r < 16; ++r) {
+                const bool on = QUANT ? ((m1 >> (16 * t + r)) & 1u) != 0u : f.h1[t][r] > 0.f;
+                ga1[t][r] = on ? ga1[t][r] : 0.f;
+            }
         stage_tile(stA, f.h1[0], 0, j, h);
         stage_tile(stA, f.h1[1], 1, j, h);
         stage_tile(stG, go, 0, j, h);
@@ -510,7 +578,18 @@ __global__ void __launch_bounds__(256, 1) mlp_bwd_frag_kernel(MlpArgs a) {
 int launch_mlp_fwd_frag(const MlpArgs& a, hipStream_t stream) {
     const int64_t tiles = (a.P + 31) / 32;
     const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((tiles + 3) / 4, 256 * 3));
-    hipLaunchKernelGGL(mlp_fwd_frag_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, a);
+    if (a.act_minmax) {
+        const int64_t n = a.calib_points < a.P ? a.calib_points : a.P;
+        if (n <= 0) return NERF_OK;
+        const int64_t cb = std::max<int64_t>(1, std::min<int64_t>(((n + 31) / 32 + 3) / 4, 256 * 4));
+        hipLaunchKernelGGL(mlp_act_minmax_kernel, dim3((unsigned)cb), dim3(256), 0, stream, a);
+        NERF_CHECK_LAUNCH("mlp_fwd(act calibration)");
+        return NERF_OK;
+    }
+    if (a.aq)
+        hipLaunchKernelGGL(mlp_fwd_frag_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, stream, a);
+    else
+        hipLaunchKernelGGL(mlp_fwd_frag_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, stream, a);
     NERF_CHECK_LAUNCH("mlp_fwd(frag)");
     return NERF_OK;
 }
@@ -518,7 +597,10 @@ int launch_mlp_fwd_frag(const MlpArgs& a, hipStream_t stream) {
 int launch_mlp_bwd_frag(const MlpArgs& a, hipStream_t stream) {
     const int64_t tiles = (a.P + 31) / 32;
     const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((tiles + 3) / 4, 256));
-    hipLaunchKernelGGL(mlp_bwd_frag_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, a);
+    if (a.aq)
+        hipLaunchKernelGGL(mlp_bwd_frag_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, stream, a);
+    else
+        hipLaunchKernelGGL(mlp_bwd_frag_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, stream, a);
     NERF_CHECK_LAUNCH("mlp_bwd(frag)");
     return NERF_OK;
 }

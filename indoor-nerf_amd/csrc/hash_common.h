@@ -1,0 +1,84 @@
+// Shared per-point voxel math of the hash-grid kernels (hashgrid.hip, quant.hip).
+#pragma once
+
+#include "common.h"
+
+namespace nerf {
+
+struct HashParams {
+    const float* tables[NERF_MAX_LEVELS];
+    float cell[NERF_MAX_LEVELS][3];   // grid_size = (box_max - box_min) / res, fp32 on the host
+    float bmin[3];
+    float bmax[3];
+    uint32_t mask;
+};
+
+// Per-axis voxel math of utils.py:103-112, fp32, exact op order.
+struct AxisCell {
+    int base;      // bottom_left_idx
+    float w;       // (x - vmin) / (vmax - vmin), on the UNclamped x (hash_encoding.py:64)
+    bool inside;   // x == max(min(x, bmax), bmin)
+};
+
+__device__ __forceinline__ AxisCell axis_cell(float x, float lo, float hi, float cell) {
+    AxisCell a;
+    a.inside = (x == fmaxf(fminf(x, hi), lo));
+    float xc = fminf(fmaxf(x, lo), hi);            // torch.clamp(min=lo, max=hi)
+    a.base = (int)floorf((xc - lo) / cell);        // floor(...).int()
+    float vmin = (float)a.base * cell + lo;        // bottom_left_idx*grid_size + box_min
+    float vmax = vmin + cell;                      // + 1.0*grid_size
+    a.w = (x - vmin) / (vmax - vmin);
+    return a;
+}
+
+// grid_size = (box_max - box_min) / resolution (utils.py:106): the same two fp32 operations,
+// correctly rounded, on the host once per launch instead of per point.
+static void fill_cells(float (*cell)[3], const float* bmin, const float* bmax, const float* res, int n_levels) {
+    for (int l = 0; l < n_levels; ++l)
+        for (int a = 0; a < 3; ++a) {
+            const volatile float d = bmax[a] - bmin[a];
+            cell[l][a] = d / res[l];
+        }
+}
+
+// ---- A-CAQ quantizer record (quantization.py:144-187), written by nerf_quant_params -------------
+// {scale, scale + 1e-8, zero_point, qmin, qmax, ste, integer bits, 0}: the scalars
+// LearnedBitwidthQuantizer.forward derives from (soft_bits, range_scale, v_max) before touching x.
+struct QuantRec {
+    float scale, scale_eps, zp, qmin, qmax, ste, bits, pad;
+};
+
+// x -> round(x / (scale + 1e-8) + zp) clamped to [qmin, qmax] -> (q - zp) * scale, returned in the
+// training-mode STE form x + (deq - x) (:176-181) or as deq (eval, :183-186); fp32, same op order.
+__device__ __forceinline__ float quant_code(float x, const QuantRec& q) {
+    const float xq = rintf(x / q.scale_eps + q.zp);       // torch.round: half to even
+    return fminf(fmaxf(xq, q.qmin), q.qmax);              // torch.clamp(min, max)
+}
+
+__device__ __forceinline__ float fake_quant(float x, const QuantRec& q) {
+    const float deq = (quant_code(x, q) - q.zp) * q.scale;
+    return q.ste != 0.f ? x + (deq - x) : deq;
+}
+
+// Order-preserving float <-> uint32 map for atomicMin/atomicMax calibration statistics.
+__device__ __forceinline__ uint32_t f2ord(float f) {
+    const uint32_t u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float ord2f(uint32_t u) {
+    return __uint_as_float((u & 0x80000000u) ? (u & 0x7FFFFFFFu) : ~u);
+}
+
+// Trilinear blend of hash_encoding.py:56-80 for one feature (x, then y, then z pairs).
+__device__ __forceinline__ float trilerp(const float (&e)[8], float wx, float wy, float wz) {
+    const float ox = 1.0f - wx, oy = 1.0f - wy, oz = 1.0f - wz;
+    const float c00 = e[0] * ox + e[4] * wx;
+    const float c01 = e[1] * ox + e[5] * wx;
+    const float c10 = e[2] * ox + e[6] * wx;
+    const float c11 = e[3] * ox + e[7] * wx;
+    const float c0 = c00 * oy + c10 * wy;
+    const float c1 = c01 * oy + c11 * wy;
+    return c0 * oz + c1 * wz;
+}
+
+}  // namespace nerf

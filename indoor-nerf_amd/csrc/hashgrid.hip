@@ -13,17 +13,9 @@
 // that the current point range touches (tables are 4 MiB per level at log2_T = 19).
 #include <stdlib.h>
 
-#include "common.h"
+#include "hash_common.h"
 
 namespace nerf {
-
-struct HashParams {
-    const float* tables[NERF_MAX_LEVELS];
-    float cell[NERF_MAX_LEVELS][3];   // grid_size = (box_max - box_min) / res, fp32 on the host
-    float bmin[3];
-    float bmax[3];
-    uint32_t mask;
-};
 
 struct HashGradParams {
     float* dtables[NERF_MAX_LEVELS];
@@ -41,37 +33,13 @@ struct HashGradParams {
     int owner_log2;       // owners per level = 2^owner_log2
 };
 
-// Per-axis voxel math of utils.py:103-112, fp32, exact op order.
-struct AxisCell {
-    int base;      // bottom_left_idx
-    float w;       // (x - vmin) / (vmax - vmin), on the UNclamped x (hash_encoding.py:64)
-    bool inside;   // x == max(min(x, bmax), bmin)
-};
-
-__device__ __forceinline__ AxisCell axis_cell(float x, float lo, float hi, float cell) {
-    AxisCell a;
-    a.inside = (x == fmaxf(fminf(x, hi), lo));
-    float xc = fminf(fmaxf(x, lo), hi);            // torch.clamp(min=lo, max=hi)
-    a.base = (int)floorf((xc - lo) / cell);        // floor(...).int()
-    float vmin = (float)a.base * cell + lo;        // bottom_left_idx*grid_size + box_min
-    float vmax = vmin + cell;                      // + 1.0*grid_size
-    a.w = (x - vmin) / (vmax - vmin);
-    return a;
-}
-
-// grid_size = (box_max - box_min) / resolution (utils.py:106): the same two fp32 operations,
-// correctly rounded, on the host once per launch instead of per point.
-static void fill_cells(float (*cell)[3], const float* bmin, const float* bmax, const float* res, int n_levels) {
-    for (int l = 0; l < n_levels; ++l)
-        for (int a = 0; a < 3; ++a) {
-            const volatile float d = bmax[a] - bmin[a];
-            cell[l][a] = d / res[l];
-        }
-}
-
+// QUANT: every gathered corner feature goes through the level's A-CAQ quantizer first
+// (hash_encoding.py:97-101: quantizers[i](voxel_embedds), elementwise on the [P,8,2] gather).
+template <bool QUANT>
 __global__ void __launch_bounds__(256) hash_encode_fwd_kernel(
     const float* __restrict__ xyz, int64_t n, HashParams hp,
-    float* __restrict__ feat, int64_t sp, int64_t sl, uint8_t* __restrict__ keep) {
+    float* __restrict__ feat, int64_t sp, int64_t sl, uint8_t* __restrict__ keep,
+    const QuantRec* __restrict__ qrec) {
     const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int lvl = blockIdx.y;
     if (p >= n) return;
@@ -89,6 +57,14 @@ __global__ void __launch_bounds__(256) hash_encode_fwd_kernel(
     for (int c = 0; c < 8; ++c) {
         const uint32_t h = spatial_hash3(bx + ((c >> 2) & 1), by + ((c >> 1) & 1), bz + (c & 1), hp.mask);
         e[c] = tab[h];
+    }
+    if constexpr (QUANT) {
+        const QuantRec q = qrec[lvl];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            e[c].x = fake_quant(e[c].x, q);
+            e[c].y = fake_quant(e[c].y, q);
+        }
     }
     const float wx = ax.w, wy = ay.w, wz = az.w;
     const float ox = 1.0f - wx, oy = 1.0f - wy, oz = 1.0f - wz;
@@ -443,10 +419,11 @@ static int bwd_mode() {
 
 using namespace nerf;
 
-extern "C" int nerf_hash_encode_fwd(const float* d_xyz, int64_t n_points, const float* bbox_min3,
-                                    const float* bbox_max3, const float* level_res, int n_levels, int log2_T,
-                                    const float* const* d_tables, float* d_feat, int64_t feat_stride_point,
-                                    int64_t feat_stride_level, uint8_t* d_keep, void* stream) {
+extern "C" int nerf_hash_encode_fwd_q(const float* d_xyz, int64_t n_points, const float* bbox_min3,
+                                      const float* bbox_max3, const float* level_res, int n_levels, int log2_T,
+                                      const float* const* d_tables, const float* d_qrec, float* d_feat,
+                                      int64_t feat_stride_point, int64_t feat_stride_level, uint8_t* d_keep,
+                                      void* stream) {
     NERF_REQUIRE(n_points >= 0, "hash_encode_fwd: n_points < 0");
     NERF_REQUIRE(n_levels >= 1 && n_levels <= NERF_MAX_LEVELS, "hash_encode_fwd: n_levels %d", n_levels);
     NERF_REQUIRE(log2_T >= 1 && log2_T <= 30, "hash_encode_fwd: log2_T %d", log2_T);
@@ -461,10 +438,23 @@ extern "C" int nerf_hash_encode_fwd(const float* d_xyz, int64_t n_points, const 
     fill_cells(hp.cell, bbox_min3, bbox_max3, level_res, n_levels);
     hp.mask = (uint32_t)((1u << log2_T) - 1u);
     dim3 grid(blocks_for(n_points, 256), n_levels);
-    hipLaunchKernelGGL(hash_encode_fwd_kernel, grid, dim3(256), 0, as_stream(stream), d_xyz, n_points, hp,
-                       d_feat, feat_stride_point, feat_stride_level, d_keep);
+    const QuantRec* q = reinterpret_cast<const QuantRec*>(d_qrec);
+    if (q)
+        hipLaunchKernelGGL(hash_encode_fwd_kernel<true>, grid, dim3(256), 0, as_stream(stream), d_xyz, n_points, hp,
+                           d_feat, feat_stride_point, feat_stride_level, d_keep, q);
+    else
+        hipLaunchKernelGGL(hash_encode_fwd_kernel<false>, grid, dim3(256), 0, as_stream(stream), d_xyz, n_points, hp,
+                           d_feat, feat_stride_point, feat_stride_level, d_keep, q);
     NERF_CHECK_LAUNCH("hash_encode_fwd");
     return NERF_OK;
+}
+
+extern "C" int nerf_hash_encode_fwd(const float* d_xyz, int64_t n_points, const float* bbox_min3,
+                                    const float* bbox_max3, const float* level_res, int n_levels, int log2_T,
+                                    const float* const* d_tables, float* d_feat, int64_t feat_stride_point,
+                                    int64_t feat_stride_level, uint8_t* d_keep, void* stream) {
+    return nerf_hash_encode_fwd_q(d_xyz, n_points, bbox_min3, bbox_max3, level_res, n_levels, log2_T, d_tables,
+                                  nullptr, d_feat, feat_stride_point, feat_stride_level, d_keep, stream);
 }
 
 static int hash_encode_bwd_impl(const float* d_xyz, int64_t n_points, const float* bbox_min3,

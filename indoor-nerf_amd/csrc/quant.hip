@@ -1,0 +1,396 @@
+// A-CAQ learned-bitwidth quantization (PocketNeRF/quantization.py:63-187) on the hash-grid path.
+//
+//   nerf_quant_params        LearnedBitwidthQuantizer.forward's scalar algebra (:158-178) for up to
+//                            32 quantizers in one launch (no host sync: the reference's .item() of
+//                            the integer bit width is evaluated on the device, exactly)
+//   nerf_quant_minmax*       calibration statistics (order-preserving uint32 atomics)
+//   nerf_hash_gather_minmax  the [P,8,2] corner gather of every level, reduced to min/max (the x
+//                            the level quantizer calibrates on, hash_encoding.py:94-101)
+//   nerf_quant_calibrate     calibrate() (:97-119)
+//   nerf_fake_quant          the elementwise quantizer (W0 weight quantizer, standalone modules)
+//   packed tables            eval-mode quantizer output (q - zp) * scale depends only on the code
+//                            q, so the tables are stored as 4/8/16-bit codes and the gather reads
+//                            1/2/4 bytes per corner instead of 8 (nerf_hash_encode_fwd_packed).
+#include <math.h>
+
+#include "hash_common.h"
+
+namespace nerf {
+
+struct QuantizerSet {
+    nerf_quantizer q[NERF_MAX_QUANTIZERS];
+};
+
+// 2 ** B for a float tensor exponent: evaluated in double and rounded once, the correctly rounded
+// value glibc's powf returns (torch CPU pow of a 0-dim tensor).
+__device__ __forceinline__ float pow2f_exact(float b) { return (float)exp2((double)b); }
+
+// float(python int) for 2^k - 1 and -(2^(k-1)): int64 -> float32 rounding, as torch casts scalars.
+__device__ __forceinline__ float int_to_f32(int64_t v) { return (float)v; }
+
+__global__ void quant_params_kernel(QuantizerSet set, int n, int training, QuantRec* __restrict__ out) {
+    const int i = threadIdx.x;
+    if (i >= n) return;
+    const nerf_quantizer& d = set.q[i];
+    const bool sym = d.v_max == nullptr;
+    const float bw = fminf(fmaxf(*d.soft_bits, d.min_bits), d.max_bits);   // torch.clamp(soft_bits, min, max)
+    const int bi = (int)rintf(bw);                                           // int(torch.round(bit_width))
+    QuantRec r;
+    if (sym) {
+        r.qmin = int_to_f32(-(int64_t(1) << (bi - 1)));
+        r.qmax = int_to_f32((int64_t(1) << (bi - 1)) - 1);
+    } else {
+        r.qmin = 0.f;
+        r.qmax = int_to_f32((int64_t(1) << bi) - 1);
+    }
+    const float range = *d.range_scale;
+    float scale;
+    if (sym) {
+        // training: range / 2 ** (B - 1) with B a tensor; eval: range / (python int 2 ** (B - 1))
+        const float den = training ? pow2f_exact(bw - 1.0f) : int_to_f32(int64_t(1) << (bi - 1));
+        scale = range / den;
+        r.zp = 0.f;
+    } else {
+        const float rv = fmaxf(range, 1e-8f);                                // clamp(range_scale, min=1e-8)
+        const float den = training ? (pow2f_exact(bw) - 1.0f) : int_to_f32((int64_t(1) << bi) - 1);
+        scale = rv / den;
+        const float z = fminf(fmaxf(*d.v_max / scale, r.qmin), r.qmax);    // clamp(v_max / scale, qmin, qmax)
+        r.zp = rintf(z);
+    }
+    r.scale = scale;
+    r.scale_eps = scale + 1e-8f;
+    r.ste = training ? 1.f : 0.f;
+    r.bits = (float)bi;
+    r.pad = 0.f;
+    out[i] = r;
+}
+
+__global__ void minmax_reset_kernel(uint32_t* mm, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        mm[2 * i] = 0xFFFFFFFFu;   // encodes the largest value (NaN payloads sort above +inf; none expected)
+        mm[2 * i + 1] = 0u;
+    }
+}
+
+__device__ __forceinline__ void block_minmax_commit(float lo, float hi, uint32_t* mm) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        lo = fminf(lo, __shfl_xor(lo, o, 64));
+        hi = fmaxf(hi, __shfl_xor(hi, o, 64));
+    }
+    if ((threadIdx.x & 63) == 0 && lo <= hi) {
+        atomicMin(mm, f2ord(lo));
+        atomicMax(mm + 1, f2ord(hi));
+    }
+}
+
+__global__ void __launch_bounds__(256) minmax_kernel(const float* __restrict__ x, int64_t n, uint32_t* mm) {
+    float lo = INFINITY, hi = -INFINITY;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const float v = x[i];
+        lo = fminf(lo, v);
+        hi = fmaxf(hi, v);
+    }
+    block_minmax_commit(lo, hi, mm);
+}
+
+__global__ void __launch_bounds__(256) hash_gather_minmax_kernel(const float* __restrict__ xyz, int64_t n,
+                                                                 HashParams hp, uint32_t* mm) {
+    const int lvl = blockIdx.y;
+    const float2* __restrict__ tab = reinterpret_cast<const float2*>(hp.tables[lvl]);
+    float lo = INFINITY, hi = -INFINITY;
+    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x) {
+        const AxisCell ax = axis_cell(xyz[3 * p + 0], hp.bmin[0], hp.bmax[0], hp.cell[lvl][0]);
+        const AxisCell ay = axis_cell(xyz[3 * p + 1], hp.bmin[1], hp.bmax[1], hp.cell[lvl][1]);
+        const AxisCell az = axis_cell(xyz[3 * p + 2], hp.bmin[2], hp.bmax[2], hp.cell[lvl][2]);
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const uint32_t h = spatial_hash3((uint32_t)ax.base + ((c >> 2) & 1), (uint32_t)ay.base + ((c >> 1) & 1),
+                                             (uint32_t)az.base + (c & 1), hp.mask);
+            const float2 e = tab[h];
+            lo = fminf(lo, fminf(e.x, e.y));
+            hi = fmaxf(hi, fmaxf(e.x, e.y));
+        }
+    }
+    block_minmax_commit(lo, hi, mm + 2 * lvl);
+}
+
+__global__ void quant_calibrate_kernel(QuantizerSet set, int n, const uint32_t* __restrict__ mm) {
+    const int i = threadIdx.x;
+    if (i >= n) return;
+    const nerf_quantizer& d = set.q[i];
+    const float bmin = ord2f(mm[2 * i]), bmax = ord2f(mm[2 * i + 1]);
+    const float rmin = fminf(*d.running_min, bmin), rmax = fmaxf(*d.running_max, bmax);
+    *d.running_min = rmin;
+    *d.running_max = rmax;
+    if (d.v_max == nullptr) {
+        *d.range_scale = 2.0f * fmaxf(fabsf(rmin), fabsf(rmax));
+    } else {
+        *d.range_scale = rmax - rmin;
+        *d.v_max = rmax;
+    }
+}
+
+__global__ void __launch_bounds__(256) fake_quant_kernel(const float* __restrict__ x, int64_t n,
+                                                         const QuantRec* __restrict__ rec, float* __restrict__ y) {
+    const QuantRec q = *rec;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        y[i] = fake_quant(x[i], q);
+}
+
+// ---- int-packed tables ----------------------------------------------------------------------
+struct PackedLevels {
+    const float* tables[NERF_MAX_LEVELS];
+    int64_t offset[NERF_MAX_LEVELS];   // bytes from the packed base
+    int bits[NERF_MAX_LEVELS];         // 4, 8, 16 (codes) or 32 (fp32 deq values)
+};
+
+// One thread per table entry (2 features). Codes are stored unsigned: q - qmin (qmin = 0 for the
+// asymmetric hash quantizers; symmetric codes are offset so they stay non-negative).
+__global__ void __launch_bounds__(256) pack_tables_kernel(PackedLevels pl, int64_t T, const QuantRec* __restrict__ qrec,
+                                                          uint8_t* __restrict__ packed) {
+    const int lvl = blockIdx.y;
+    const QuantRec q = qrec[lvl];
+    const int bits = pl.bits[lvl];
+    uint8_t* base = packed + pl.offset[lvl];
+    const float2* tab = reinterpret_cast<const float2*>(pl.tables[lvl]);
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < T; r += (int64_t)gridDim.x * blockDim.x) {
+        const float2 e = tab[r];
+        if (bits == 32) {
+            reinterpret_cast<float2*>(base)[r] = make_float2((quant_code(e.x, q) - q.zp) * q.scale,
+                                                             (quant_code(e.y, q) - q.zp) * q.scale);
+            continue;
+        }
+        const uint32_t c0 = (uint32_t)(quant_code(e.x, q) - q.qmin), c1 = (uint32_t)(quant_code(e.y, q) - q.qmin);
+        if (bits == 4) base[r] = (uint8_t)(c0 | (c1 << 4));
+        else if (bits == 8) reinterpret_cast<uint16_t*>(base)[r] = (uint16_t)(c0 | (c1 << 8));
+        else reinterpret_cast<uint32_t*>(base)[r] = c0 | (c1 << 16);
+    }
+}
+
+template <int BITS>
+__device__ __forceinline__ void load_codes(const uint8_t* base, uint32_t h, const QuantRec& q, float& f0, float& f1) {
+    uint32_t c0, c1;
+    if constexpr (BITS == 4) {
+        const uint32_t v = base[h];
+        c0 = v & 15u; c1 = v >> 4;
+    } else if constexpr (BITS == 8) {
+        const uint32_t v = reinterpret_cast<const uint16_t*>(base)[h];
+        c0 = v & 255u; c1 = v >> 8;
+    } else {
+        const uint32_t v = reinterpret_cast<const uint32_t*>(base)[h];
+        c0 = v & 65535u; c1 = v >> 16;
+    }
+    // q = code + qmin is an exact float integer (|q| < 2^17); deq = (q - zp) * scale as :186
+    f0 = (((float)c0 + q.qmin) - q.zp) * q.scale;
+    f1 = (((float)c1 + q.qmin) - q.zp) * q.scale;
+}
+
+template <int BITS>
+__device__ __forceinline__ void gather_level(const uint8_t* base, const uint32_t (&h)[8], const QuantRec& q,
+                                             float (&e0)[8], float (&e1)[8]) {
+    if constexpr (BITS == 32) {
+        const float2* t = reinterpret_cast<const float2*>(base);
+#pragma unroll
+        for (int c = 0; c < 8; ++c) { const float2 v = t[h[c]]; e0[c] = v.x; e1[c] = v.y; }
+    } else {
+#pragma unroll
+        for (int c = 0; c < 8; ++c) load_codes<BITS>(base, h[c], q, e0[c], e1[c]);
+    }
+}
+
+__global__ void __launch_bounds__(256) hash_encode_fwd_packed_kernel(
+    const float* __restrict__ xyz, int64_t n, HashParams hp, PackedLevels pl, const uint8_t* __restrict__ packed,
+    const QuantRec* __restrict__ qrec, float* __restrict__ feat, int64_t sp, int64_t sl, uint8_t* __restrict__ keep) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int lvl = blockIdx.y;
+    if (p >= n) return;
+    const float x = xyz[3 * p + 0], y = xyz[3 * p + 1], z = xyz[3 * p + 2];
+    const AxisCell ax = axis_cell(x, hp.bmin[0], hp.bmax[0], hp.cell[lvl][0]);
+    const AxisCell ay = axis_cell(y, hp.bmin[1], hp.bmax[1], hp.cell[lvl][1]);
+    const AxisCell az = axis_cell(z, hp.bmin[2], hp.bmax[2], hp.cell[lvl][2]);
+    if (lvl == 0 && keep) keep[p] = (ax.inside && ay.inside && az.inside) ? 1 : 0;
+    uint32_t h[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+        h[c] = spatial_hash3((uint32_t)ax.base + ((c >> 2) & 1), (uint32_t)ay.base + ((c >> 1) & 1),
+                             (uint32_t)az.base + (c & 1), hp.mask);
+    const QuantRec q = qrec[lvl];
+    const uint8_t* base = packed + pl.offset[lvl];
+    float e0[8], e1[8];
+    switch (pl.bits[lvl]) {   // uniform per block (one level per blockIdx.y)
+        case 4: gather_level<4>(base, h, q, e0, e1); break;
+        case 8: gather_level<8>(base, h, q, e0, e1); break;
+        case 16: gather_level<16>(base, h, q, e0, e1); break;
+        default: gather_level<32>(base, h, q, e0, e1); break;
+    }
+    const float f0 = trilerp(e0, ax.w, ay.w, az.w), f1 = trilerp(e1, ax.w, ay.w, az.w);
+    float* dst = feat + p * sp + (int64_t)lvl * sl;
+    if (((sp | sl) & 1) == 0) {
+        *reinterpret_cast<float2*>(dst) = make_float2(f0, f1);
+    } else {
+        dst[0] = f0;
+        dst[1] = f1;
+    }
+}
+
+static int fill_set(QuantizerSet& s, const nerf_quantizer* qs, int n, bool need_stats) {
+    NERF_REQUIRE(qs && n >= 1 && n <= NERF_MAX_QUANTIZERS, "quant: n = %d quantizers (1..%d)", n, NERF_MAX_QUANTIZERS);
+    for (int i = 0; i < n; ++i) {
+        NERF_REQUIRE(qs[i].soft_bits && qs[i].range_scale, "quant: quantizer %d has null parameters", i);
+        NERF_REQUIRE(!need_stats || (qs[i].running_min && qs[i].running_max), "quant: quantizer %d has null buffers", i);
+        NERF_REQUIRE(qs[i].min_bits >= 1.f && qs[i].max_bits <= 32.f && qs[i].min_bits <= qs[i].max_bits,
+                     "quant: quantizer %d bit range [%g, %g]", i, qs[i].min_bits, qs[i].max_bits);
+        s.q[i] = qs[i];
+    }
+    return NERF_OK;
+}
+
+static int hash_params(HashParams& hp, const float* bmin, const float* bmax, const float* res, int n_levels,
+                       int log2_T, const float* const* tables) {
+    NERF_REQUIRE(n_levels >= 1 && n_levels <= NERF_MAX_LEVELS, "quant: n_levels %d", n_levels);
+    NERF_REQUIRE(log2_T >= 1 && log2_T <= 30, "quant: log2_T %d", log2_T);
+    NERF_REQUIRE(bmin && bmax && res, "quant: null bbox / resolutions");
+    for (int l = 0; l < n_levels; ++l) hp.tables[l] = tables ? tables[l] : nullptr;
+    for (int a = 0; a < 3; ++a) { hp.bmin[a] = bmin[a]; hp.bmax[a] = bmax[a]; }
+    fill_cells(hp.cell, bmin, bmax, res, n_levels);
+    hp.mask = (uint32_t)((1u << log2_T) - 1u);
+    return NERF_OK;
+}
+
+}  // namespace nerf
+
+using namespace nerf;
+
+extern "C" int nerf_quant_params(const nerf_quantizer* qs, int n, int training, float* d_rec, void* stream) {
+    QuantizerSet s;
+    int rc = fill_set(s, qs, n, false);
+    if (rc) return rc;
+    NERF_REQUIRE(d_rec, "quant_params: null output");
+    hipLaunchKernelGGL(quant_params_kernel, dim3(1), dim3(64), 0, as_stream(stream), s, n, training ? 1 : 0,
+                       reinterpret_cast<QuantRec*>(d_rec));
+    NERF_CHECK_LAUNCH("quant_params");
+    return NERF_OK;
+}
+
+extern "C" int nerf_quant_minmax_reset(uint32_t* d_minmax, int n, void* stream) {
+    NERF_REQUIRE(d_minmax && n >= 1, "quant_minmax_reset: bad args");
+    hipLaunchKernelGGL(minmax_reset_kernel, dim3(blocks_for(n, 64)), dim3(64), 0, as_stream(stream), d_minmax, n);
+    NERF_CHECK_LAUNCH("quant_minmax_reset");
+    return NERF_OK;
+}
+
+extern "C" int nerf_quant_minmax(const float* d_x, int64_t count, uint32_t* d_minmax, void* stream) {
+    NERF_REQUIRE(d_minmax && count >= 0 && (d_x || count == 0), "quant_minmax: bad args");
+    if (count == 0) return NERF_OK;
+    const unsigned blocks = (unsigned)std::min<int64_t>(blocks_for(count, 256), 1024);
+    hipLaunchKernelGGL(minmax_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), d_x, count, d_minmax);
+    NERF_CHECK_LAUNCH("quant_minmax");
+    return NERF_OK;
+}
+
+extern "C" int nerf_hash_gather_minmax(const float* d_xyz, int64_t n_points, const float* bbox_min3,
+                                       const float* bbox_max3, const float* level_res, int n_levels, int log2_T,
+                                       const float* const* d_tables, uint32_t* d_minmax, void* stream) {
+    NERF_REQUIRE(d_xyz && d_tables && d_minmax && n_points >= 0, "hash_gather_minmax: bad args");
+    HashParams hp{};
+    int rc = hash_params(hp, bbox_min3, bbox_max3, level_res, n_levels, log2_T, d_tables);
+    if (rc) return rc;
+    for (int l = 0; l < n_levels; ++l) NERF_REQUIRE(d_tables[l], "hash_gather_minmax: table %d is null", l);
+    if (n_points == 0) return NERF_OK;
+    const unsigned bx = (unsigned)std::min<int64_t>(blocks_for(n_points, 256), 512);
+    hipLaunchKernelGGL(hash_gather_minmax_kernel, dim3(bx, n_levels), dim3(256), 0, as_stream(stream), d_xyz,
+                       n_points, hp, d_minmax);
+    NERF_CHECK_LAUNCH("hash_gather_minmax");
+    return NERF_OK;
+}
+
+extern "C" int nerf_quant_calibrate(const nerf_quantizer* qs, int n, const uint32_t* d_minmax, void* stream) {
+    QuantizerSet s;
+    int rc = fill_set(s, qs, n, true);
+    if (rc) return rc;
+    NERF_REQUIRE(d_minmax, "quant_calibrate: null statistics");
+    hipLaunchKernelGGL(quant_calibrate_kernel, dim3(1), dim3(64), 0, as_stream(stream), s, n, d_minmax);
+    NERF_CHECK_LAUNCH("quant_calibrate");
+    return NERF_OK;
+}
+
+extern "C" int nerf_fake_quant(const float* d_x, int64_t count, const float* d_rec, float* d_y, void* stream) {
+    NERF_REQUIRE(count >= 0 && d_rec && ((d_x && d_y) || count == 0), "fake_quant: bad args");
+    if (count == 0) return NERF_OK;
+    const unsigned blocks = (unsigned)std::min<int64_t>(blocks_for(count, 256), 4096);
+    hipLaunchKernelGGL(fake_quant_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), d_x, count,
+                       reinterpret_cast<const QuantRec*>(d_rec), d_y);
+    NERF_CHECK_LAUNCH("fake_quant");
+    return NERF_OK;
+}
+
+extern "C" size_t nerf_quant_packed_layout(const int* level_bits, int n_levels, int log2_T, int* code_bits,
+                                           int64_t* offsets) {
+    if (!level_bits || !code_bits || !offsets || n_levels < 1 || n_levels > NERF_MAX_LEVELS || log2_T < 1 ||
+        log2_T > 30)
+        return 0;
+    const int64_t T = int64_t(1) << log2_T;
+    int64_t off = 0;
+    for (int l = 0; l < n_levels; ++l) {
+        const int b = level_bits[l];
+        const int cb = b <= 4 ? 4 : b <= 8 ? 8 : b <= 16 ? 16 : 32;
+        code_bits[l] = cb;
+        offsets[l] = off;
+        const int64_t bytes = T * (cb == 4 ? 1 : cb == 8 ? 2 : cb == 16 ? 4 : 8);
+        off += (bytes + 255) & ~int64_t(255);
+    }
+    return (size_t)off;
+}
+
+static int fill_packed(PackedLevels& pl, const float* const* tables, int n_levels, const int* code_bits,
+                       const int64_t* offsets) {
+    NERF_REQUIRE(code_bits && offsets, "packed: null layout");
+    for (int l = 0; l < n_levels; ++l) {
+        NERF_REQUIRE(code_bits[l] == 4 || code_bits[l] == 8 || code_bits[l] == 16 || code_bits[l] == 32,
+                     "packed: level %d code bits %d", l, code_bits[l]);
+        NERF_REQUIRE(offsets[l] >= 0 && (offsets[l] & 255) == 0, "packed: level %d offset", l);
+        pl.tables[l] = tables ? tables[l] : nullptr;
+        pl.offset[l] = offsets[l];
+        pl.bits[l] = code_bits[l];
+    }
+    return NERF_OK;
+}
+
+extern "C" int nerf_quant_pack_tables(const float* const* d_tables, int n_levels, int log2_T, const float* d_qrec,
+                                      const int* code_bits, const int64_t* offsets, void* d_packed, void* stream) {
+    NERF_REQUIRE(d_tables && d_qrec && d_packed && n_levels >= 1 && n_levels <= NERF_MAX_LEVELS && log2_T >= 1 &&
+                 log2_T <= 30, "quant_pack_tables: bad args");
+    PackedLevels pl{};
+    int rc = fill_packed(pl, d_tables, n_levels, code_bits, offsets);
+    if (rc) return rc;
+    for (int l = 0; l < n_levels; ++l) NERF_REQUIRE(d_tables[l], "quant_pack_tables: table %d is null", l);
+    const int64_t T = int64_t(1) << log2_T;
+    const unsigned bx = (unsigned)std::min<int64_t>(blocks_for(T, 256), 2048);
+    hipLaunchKernelGGL(pack_tables_kernel, dim3(bx, n_levels), dim3(256), 0, as_stream(stream), pl, T,
+                       reinterpret_cast<const QuantRec*>(d_qrec), reinterpret_cast<uint8_t*>(d_packed));
+    NERF_CHECK_LAUNCH("quant_pack_tables");
+    return NERF_OK;
+}
+
+extern "C" int nerf_hash_encode_fwd_packed(const float* d_xyz, int64_t n_points, const float* bbox_min3,
+                                           const float* bbox_max3, const float* level_res, int n_levels, int log2_T,
+                                           const void* d_packed, const int* code_bits, const int64_t* offsets,
+                                           const float* d_qrec, float* d_feat, int64_t feat_stride_point,
+                                           int64_t feat_stride_level, uint8_t* d_keep, void* stream) {
+    NERF_REQUIRE(n_points >= 0 && d_xyz && d_packed && d_qrec && d_feat, "hash_encode_fwd_packed: bad args");
+    HashParams hp{};
+    int rc = hash_params(hp, bbox_min3, bbox_max3, level_res, n_levels, log2_T, nullptr);
+    if (rc) return rc;
+    PackedLevels pl{};
+    rc = fill_packed(pl, nullptr, n_levels, code_bits, offsets);
+    if (rc) return rc;
+    if (n_points == 0) return NERF_OK;
+    dim3 grid(blocks_for(n_points, 256), n_levels);
+    hipLaunchKernelGGL(hash_encode_fwd_packed_kernel, grid, dim3(256), 0, as_stream(stream), d_xyz, n_points, hp, pl,
+                       reinterpret_cast<const uint8_t*>(d_packed), reinterpret_cast<const QuantRec*>(d_qrec), d_feat,
+                       feat_stride_point, feat_stride_level, d_keep);
+    NERF_CHECK_LAUNCH("hash_encode_fwd_packed");
+    return NERF_OK;
+}

@@ -46,7 +46,9 @@ class GradArena:
     """One flat fp32 buffer holding the .grad of every parameter (views), in parameter order."""
 
     def __init__(self, params):
-        self.params = [p for p in params if p.requires_grad]
+        # quantizer scalars (soft_bits, range_scale, v_max) never receive a gradient in the
+        # reference (their uses are detached): they keep grad None, so the optimizer skips them
+        self.params = [p for p in params if p.requires_grad and not getattr(p, "_nerf_no_grad", False)]
         total = sum(p.numel() for p in self.params)
         dev = self.params[0].device
         self.flat = torch.zeros(total, device=dev, dtype=torch.float32)

@@ -11,14 +11,33 @@ import torch
 import torch.nn as nn
 
 from . import _lib
-from .hashgrid import HashEmbedder, HashEncodeFn, SHEncoder, accumulate_grad_buffers, hash_encode_bwd
+from .hashgrid import HashEmbedder, SHEncoder, accumulate_grad_buffers, hash_encode_bwd
+from .quantization import LearnedBitwidthQuantizer, calibrate_from_stats, new_stats, quant_records
 
 
-def _weights_struct(weights):
+def _weights_struct(weights, w0q=None):
+    """Kernel weight pointers; with the A-CAQ weight quantizer, layer 0 reads the quantized W0."""
     w = _lib.MlpWeights()
     for name, t in zip(("w0", "w1", "c0", "c1", "c2"), weights):
         setattr(w, name, _lib.ptr(t.detach(), name).value)
+    if w0q is not None:
+        w.w0 = _lib.ptr(w0q, "w0_quantized").value
     return w
+
+
+def _fake_quant(x, rec):
+    y = torch.empty_like(x)
+    _lib.call("nerf_fake_quant", _lib.ptr(x.detach(), "x"), x.numel(), _lib.ptr(rec, "record"), _lib.ptr(y, "y"),
+              _lib.stream())
+    return y
+
+
+def _act_calibration(feat_args, P, weights, w0q, n_calib):
+    """Calibration-only MLP launch: (min, max) of relu(x W0q^T) over the first n_calib points."""
+    st = new_stats(1, w0q.device)
+    _lib.call("nerf_mlp_fwd_q", *feat_args, P, _weights_struct(weights, w0q), None, None, None,
+              _lib.ptr(st, "stats", dtype=torch.int32), n_calib, _lib.stream())
+    return st
 
 
 def _grads_struct(weights):
@@ -73,19 +92,24 @@ class MLPFn(torch.autograd.Function):
         o16 = torch.empty(P, 16, device=x.device, dtype=torch.float32) if head else None
         xp = _lib.ptr(x, "x")
         sh_ptr = _lib.c_vp(x.data_ptr() + 32 * 4) if P > 0 else xp
-        _lib.call("nerf_mlp_fwd", xp, 48, 2, sh_ptr, 48, None, 1, None, P, _weights_struct(weights),
-                  _lib.ptr(raw, "raw"), _lib.ptr(o16, "geo", allow_none=True), _lib.stream())
+        feat_args = (xp, 48, 2, sh_ptr, 48, None, 1, None)
+        w0q, arec = net.quant_state(lambda w0q: _act_calibration(feat_args, P, weights, w0q, P))
+        _lib.call("nerf_mlp_fwd_q", *feat_args, P, _weights_struct(weights, w0q), _lib.ptr(raw, "raw"),
+                  _lib.ptr(o16, "geo", allow_none=True), _lib.ptr(arec, "act_record", allow_none=True), None, 0,
+                  _lib.stream())
         if head:
             raw = _head_forward(o16, raw, None, head)
-        ctx.save_for_backward(x, o16, *params)
+        ctx.save_for_backward(x, o16, w0q, arec, *params)
         ctx.n_head = len(head)
+        ctx.eval_quant = net.use_quantization and not net.training
         return raw
 
     @staticmethod
     def backward(ctx, g_raw):
-        x, o16, *params = ctx.saved_tensors
+        x, o16, w0q, arec, *params = ctx.saved_tensors
         weights, head = params[:5], params[5:]
         P = x.shape[0]
+        _no_eval_quant_grad(ctx)
         g = g_raw.contiguous()
         head_grads, dgeo = (None,) * ctx.n_head, None
         if head:
@@ -101,12 +125,18 @@ class MLPFn(torch.autograd.Function):
             if need_x:
                 dsh_t = torch.empty(P, 16, device=x.device, dtype=torch.float32)
                 dsh = _lib.ptr(dsh_t, "dsh")
-            _lib.call("nerf_mlp_bwd", xp, 48, 2, sh_ptr, 48, None, 1, None, P, _weights_struct(weights),
+            _lib.call("nerf_mlp_bwd_q", xp, 48, 2, sh_ptr, 48, None, 1, None, P, _weights_struct(weights, w0q),
                       _lib.ptr(g, "grad_raw"), grads, dfeat, dsh, _lib.ptr(dgeo, "dgeo", allow_none=True),
-                      _lib.stream())
+                      _lib.ptr(arec, "act_record", allow_none=True), _lib.stream())
             if need_x:
                 dx[:, 32:] = dsh_t
         return (dx, None) + (None,) * len(weights) + tuple(head_grads)
+
+
+def _no_eval_quant_grad(ctx):
+    if ctx.eval_quant:
+        raise NotImplementedError("NeRFSmall: backward through eval-mode A-CAQ quantizers (round(.) with a zero "
+                                  "gradient) is not implemented; train in training mode as the reference does")
 
 
 def _scratch_grads(weights):
@@ -120,7 +150,7 @@ class FieldFn(torch.autograd.Function):
     """Fused run_network: pts [P,3], viewdirs [R,3] (P = R*S) -> raw [P,4] ([P,7] with normals)."""
 
     @staticmethod
-    def forward(ctx, pts, viewdirs, samples_per_ray, embedder, net, *params):
+    def forward(ctx, pts, viewdirs, samples_per_ray, embedder, net, netchunk, *params):
         if pts.requires_grad or viewdirs.requires_grad:
             raise NotImplementedError("run_network: gradients w.r.t. positions/directions are not implemented")
         n_tab = embedder.n_levels
@@ -130,45 +160,52 @@ class FieldFn(torch.autograd.Function):
         P = pts.shape[0]
         feat = torch.empty(n_tab, P, 2, device=pts.device, dtype=torch.float32)
         keep = torch.empty(P, device=pts.device, dtype=torch.bool)
-        meta = embedder._meta
-        _lib.call("nerf_hash_encode_fwd", _lib.ptr(pts, "pts"), P, meta["bmin"], meta["bmax"], meta["res"], n_tab,
-                  meta["log2_T"], _lib.ptr_array(tables), _lib.ptr(feat, "feat"), 2, 2 * P,
-                  _lib.ptr(keep, "keep", dtype=torch.bool), _lib.stream())
+        embedder.encode_into(pts, feat, 2, 2 * P, keep)
         raw = torch.empty(P, 4, device=pts.device, dtype=torch.float32)
         o16 = torch.empty(P, 16, device=pts.device, dtype=torch.float32) if head else None
         # with the normals head, run_network's mask lands on n_z, not sigma (run_nerf.py:66)
-        _lib.call("nerf_mlp_fwd", _lib.ptr(feat, "feat"), 2, 2 * P, None, 0, _lib.ptr(viewdirs, "viewdirs"),
-                  samples_per_ray, None if head else _lib.ptr(keep, "keep", dtype=torch.bool), P,
-                  _weights_struct(weights), _lib.ptr(raw, "raw"), _lib.ptr(o16, "geo", allow_none=True),
+        keep_arg = None if head else _lib.ptr(keep, "keep", dtype=torch.bool)
+        feat_args = (_lib.ptr(feat, "feat"), 2, 2 * P, None, 0, _lib.ptr(viewdirs, "viewdirs"), samples_per_ray,
+                     keep_arg)
+        # the activation quantizer calibrates on the first netchunk points (run_nerf.py:43-50, :64)
+        n_calib = P if netchunk is None else min(P, netchunk)
+        w0q, arec = net.quant_state(lambda w0q: _act_calibration(feat_args, P, weights, w0q, n_calib))
+        _lib.call("nerf_mlp_fwd_q", *feat_args, P, _weights_struct(weights, w0q), _lib.ptr(raw, "raw"),
+                  _lib.ptr(o16, "geo", allow_none=True), _lib.ptr(arec, "act_record", allow_none=True), None, 0,
                   _lib.stream())
         if head:
             raw = _head_forward(o16, raw, keep, head)
-        ctx.save_for_backward(pts, viewdirs, feat, keep, o16, *params)
+        ctx.save_for_backward(pts, viewdirs, feat, keep, o16, w0q, arec, *params)
         ctx.spr, ctx.embedder, ctx.n_tab, ctx.n_head = samples_per_ray, embedder, n_tab, len(head)
+        ctx.eval_quant = net.use_quantization and not net.training
+        ctx.zero_tab_grad = embedder.quantization_active() and not embedder.training
         return raw
 
     @staticmethod
     def backward(ctx, g_raw):
-        pts, viewdirs, feat, keep, o16, *params = ctx.saved_tensors
+        pts, viewdirs, feat, keep, o16, w0q, arec, *params = ctx.saved_tensors
         n_tab = ctx.n_tab
         tables, weights, head = params[:n_tab], params[n_tab:n_tab + 5], params[n_tab + 5:]
         P = pts.shape[0]
+        _no_eval_quant_grad(ctx)
         g = g_raw.contiguous()
         head_grads, dgeo = (None,) * ctx.n_head, None
         if head:
-            g, dgeo, head_grads = _head_backward(o16, keep, head, g, ctx.needs_input_grad[5 + n_tab + 5:])
+            g, dgeo, head_grads = _head_backward(o16, keep, head, g, ctx.needs_input_grad[6 + n_tab + 5:])
         need_tab = any(t.requires_grad for t in tables)
         dfeat = torch.empty_like(feat) if need_tab else None
         if any(w.requires_grad for w in weights) or need_tab:
             grads = _grads_struct(weights) if any(w.requires_grad for w in weights) else _scratch_grads(weights)
-            _lib.call("nerf_mlp_bwd", _lib.ptr(feat, "feat"), 2, 2 * P, None, 0, _lib.ptr(viewdirs, "viewdirs"),
+            _lib.call("nerf_mlp_bwd_q", _lib.ptr(feat, "feat"), 2, 2 * P, None, 0, _lib.ptr(viewdirs, "viewdirs"),
                       ctx.spr, None if head else _lib.ptr(keep, "keep", dtype=torch.bool), P,
-                      _weights_struct(weights), _lib.ptr(g, "grad_raw"), grads,
+                      _weights_struct(weights, w0q), _lib.ptr(g, "grad_raw"), grads,
                       _lib.ptr(dfeat, "dfeat", allow_none=True), None, _lib.ptr(dgeo, "dgeo", allow_none=True),
-                      _lib.stream())
+                      _lib.ptr(arec, "act_record", allow_none=True), _lib.stream())
         if need_tab:
-            hash_encode_bwd(pts, ctx.embedder._meta, dfeat, 2, 2 * P, accumulate_grad_buffers(tables))
-        return (None,) * (5 + n_tab + len(weights)) + tuple(head_grads)
+            tgrads = accumulate_grad_buffers(tables)
+            if not ctx.zero_tab_grad:
+                hash_encode_bwd(pts, ctx.embedder._meta, dfeat, 2, 2 * P, tgrads)
+        return (None,) * (6 + n_tab + len(weights)) + tuple(head_grads)
 
 
 class NeRFSmall(nn.Module):
@@ -183,8 +220,6 @@ class NeRFSmall(nn.Module):
         if shape != (2, 64, 15, 3, 64, 32, 16):
             raise NotImplementedError(f"NeRFSmall{shape}: the HIP MLP implements create_nerf's configuration "
                                       "(2, 64, 15, 3, 64, 32, 16)")
-        if use_quantization:
-            raise NotImplementedError("NeRFSmall(use_quantization=True): A-CAQ MLP quantizers are not built yet")
         self.input_ch = input_ch
         self.input_ch_views = input_ch_views
         self.use_quantization = use_quantization
@@ -192,16 +227,41 @@ class NeRFSmall(nn.Module):
         self.geo_feat_dim = geo_feat_dim
         self.num_layers_color = num_layers_color
         self.predict_normals = predict_normals
-        self.sigma_act_quantizers = None
-        self.sigma_weight_quantizer = None
         self.sigma_net = nn.ModuleList([nn.Linear(input_ch, hidden_dim, bias=False),
                                         nn.Linear(hidden_dim, 1 + geo_feat_dim, bias=False)])
+        if use_quantization:   # run_nerf_helpers.py:207-233
+            self.sigma_act_quantizers = nn.ModuleList([
+                LearnedBitwidthQuantizer(init_bits=float(quantization_bits), min_bits=2.0, max_bits=32.0,
+                                         symmetric=False) for _ in range(num_layers - 1)])
+            self.sigma_weight_quantizer = LearnedBitwidthQuantizer(init_bits=float(quantization_bits), min_bits=2.0,
+                                                                   max_bits=32.0, symmetric=True)
+        else:
+            self.sigma_act_quantizers = None
+            self.sigma_weight_quantizer = None
         self.color_net = nn.ModuleList([nn.Linear(input_ch_views + geo_feat_dim, hidden_dim_color, bias=False),
                                         nn.Linear(hidden_dim_color, hidden_dim_color, bias=False),
                                         nn.Linear(hidden_dim_color, 3, bias=False)])
         if predict_normals:   # run_nerf_helpers.py:259-263
             self.normal_net = nn.Sequential(nn.Linear(geo_feat_dim, hidden_dim // 2), nn.ReLU(),
                                             nn.Linear(hidden_dim // 2, 3))
+
+    def quant_state(self, act_calibration):
+        """(W0q, activation record) for one forward, or (None, None) without quantization.
+        run_nerf_helpers.py:272-284: W0 goes through sigma_weight_quantizer (symmetric) and the
+        layer-0 ReLU output through sigma_act_quantizers[0] (asymmetric), both calibrating on their
+        first training call. act_calibration(W0q) -> stats runs the calibration-only MLP launch."""
+        if not self.use_quantization:
+            return None, None
+        wq, aq = self.sigma_weight_quantizer, self.sigma_act_quantizers[0]
+        W0 = self.sigma_net[0].weight
+        if self.training and not wq.calibrated:
+            wq.calibrate(W0)
+        if self.training and not aq.calibrated:
+            w0q = _fake_quant(W0, wq.record())
+            calibrate_from_stats([aq], act_calibration(w0q))
+            return w0q, aq.record()
+        recs = quant_records([wq, aq], self.training)
+        return _fake_quant(W0, recs[0]), recs[1]
 
     def mlp_weights(self):
         return [self.sigma_net[0].weight, self.sigma_net[1].weight, self.color_net[0].weight,
@@ -247,7 +307,7 @@ def run_network(inputs, viewdirs, fn, embed_fn, embeddirs_fn, netchunk=1024 * 64
         if embed_fn.training:
             embed_fn.current_step += 1
         R, S = inputs.shape[0], inputs.shape[1]
-        raw = FieldFn.apply(inputs.reshape(-1, 3), viewdirs, S, embed_fn, fn,
+        raw = FieldFn.apply(inputs.reshape(-1, 3), viewdirs, S, embed_fn, fn, netchunk,
                             *embed_fn.tables(), *fn.field_params())
         return raw.reshape(R, S, fn.raw_channels)
     inputs_flat = torch.reshape(inputs, [-1, inputs.shape[-1]])

@@ -4,10 +4,13 @@ API mirror of PocketNeRF/hash_encoding.py: HashEmbedder (:11-107) and SHEncoder 
 constructor arguments, attributes, parameters (`embeddings.{i}.weight`, nn.Embedding(2^log2T, 2))
 and return values. Forward and backward run in libnerfhip (csrc/hashgrid.hip, csrc/field.hip).
 """
+import ctypes
+
 import torch
 import torch.nn as nn
 
 from . import _lib
+from .quantization import LearnedBitwidthQuantizer, calibrate_from_stats, new_stats, quant_records
 
 
 def level_resolutions(base_resolution, finest_resolution, n_levels):
@@ -41,7 +44,8 @@ class HashEncodeFn(torch.autograd.Function):
     """xyz [P,3] -> (feat, keep). feat is [P, 2L] (layout 'point') or [L, P, 2] (layout 'level')."""
 
     @staticmethod
-    def forward(ctx, xyz, meta, layout, *tables):
+    def forward(ctx, xyz, embedder, layout, *tables):
+        meta = embedder._meta
         if xyz.requires_grad:
             raise NotImplementedError("HashEmbedder: gradients w.r.t. positions are not implemented "
                                       "(the reference never back-propagates into sample positions)")
@@ -54,11 +58,11 @@ class HashEncodeFn(torch.autograd.Function):
             feat = torch.empty(L, P, 2, device=xyz.device, dtype=torch.float32)
             sp, sl = 2, 2 * P
         keep = torch.empty(P, device=xyz.device, dtype=torch.bool)
-        _lib.call("nerf_hash_encode_fwd", _lib.ptr(xyz, "xyz"), P, meta["bmin"], meta["bmax"], meta["res"], L,
-                  meta["log2_T"], _lib.ptr_array(tables), _lib.ptr(feat, "feat"), sp, sl,
-                  _lib.ptr(keep, "keep", dtype=torch.bool), _lib.stream())
+        embedder.encode_into(xyz, feat, sp, sl, keep)
         ctx.save_for_backward(xyz, *tables)
         ctx.meta, ctx.sp, ctx.sl = meta, sp, sl
+        # eval-mode quantizers return (round(.) - zp) * scale: zero gradient w.r.t. the tables
+        ctx.zero_grad = embedder.quantization_active() and not embedder.training
         ctx.mark_non_differentiable(keep)
         return feat, keep
 
@@ -66,8 +70,9 @@ class HashEncodeFn(torch.autograd.Function):
     def backward(ctx, g_feat, g_keep):
         xyz, *tables = ctx.saved_tensors
         if g_feat is not None and any(t.requires_grad for t in tables):
-            g = g_feat.contiguous()
-            hash_encode_bwd(xyz, ctx.meta, g, ctx.sp, ctx.sl, accumulate_grad_buffers(tables))
+            grads = accumulate_grad_buffers(tables)
+            if not ctx.zero_grad:
+                hash_encode_bwd(xyz, ctx.meta, g_feat.contiguous(), ctx.sp, ctx.sl, grads)
         return (None, None, None) + (None,) * len(tables)
 
 
@@ -108,9 +113,6 @@ class HashEmbedder(nn.Module):
             raise NotImplementedError("HashEmbedder: the HIP kernels implement n_features_per_level == 2")
         if not 1 <= n_levels <= _lib.MAX_LEVELS:
             raise ValueError(f"HashEmbedder: n_levels must be 1..{_lib.MAX_LEVELS}")
-        if use_quantization:
-            raise NotImplementedError("HashEmbedder(use_quantization=True): the A-CAQ quantized gather kernel "
-                                      "is not built yet")
         self.bounding_box = bounding_box
         self.n_levels = n_levels
         self.n_features_per_level = n_features_per_level
@@ -119,7 +121,7 @@ class HashEmbedder(nn.Module):
         self.finest_resolution = torch.tensor(finest_resolution)
         self.out_dim = n_levels * n_features_per_level
         self.use_quantization = use_quantization
-        self.quantizers = None
+        self._packed = None
         self.warmup_steps = 500
         self.current_step = 0
         res, self.b = level_resolutions(self.base_resolution, self.finest_resolution, n_levels)
@@ -127,6 +129,11 @@ class HashEmbedder(nn.Module):
                                          for _ in range(n_levels)])
         for emb in self.embeddings:
             nn.init.uniform_(emb.weight, a=-0.0001, b=0.0001)
+        # A-CAQ (hash_encoding.py:37-53): one asymmetric learned-bitwidth quantizer per level,
+        # registered after the tables as in the reference (parameter order = optimizer state order)
+        self.quantizers = nn.ModuleList([
+            LearnedBitwidthQuantizer(init_bits=float(quantization_bits), min_bits=2.0, max_bits=32.0, symmetric=False)
+            for _ in range(n_levels)]) if use_quantization else None
         bmin, bmax = _bbox_floats(bounding_box)
         self._meta = dict(res=_lib.host_f32(res), bmin=_lib.host_f32(bmin), bmax=_lib.host_f32(bmax),
                           log2_T=log2_hashmap_size)
@@ -135,8 +142,80 @@ class HashEmbedder(nn.Module):
     def tables(self):
         return [e.weight for e in self.embeddings]
 
+    # ---- A-CAQ ------------------------------------------------------------------------------
+    def quantization_active(self):
+        """hash_encoding.py:97-101: quantize unless training inside the warm-up window (the
+        caller has already advanced current_step for this forward)."""
+        return (self.use_quantization and self.quantizers is not None
+                and not (self.training and self.current_step < self.warmup_steps))
+
+    def level_records(self, xyz):
+        """[L, 8] quantizer records for this forward. In training mode, quantizers not yet
+        calibrated first calibrate on this batch's gathered corners (quantization.py:146-147):
+        one gather-min/max launch over all levels."""
+        qs = list(self.quantizers)
+        if self.training:
+            todo = [i for i, q in enumerate(qs) if not q.calibrated]
+            if todo:
+                xyz = xyz.contiguous()
+                st = new_stats(len(qs), xyz.device)
+                meta = self._meta
+                _lib.call("nerf_hash_gather_minmax", _lib.ptr(xyz, "xyz"), xyz.shape[0], meta["bmin"], meta["bmax"],
+                          meta["res"], self.n_levels, meta["log2_T"], _lib.ptr_array(self.tables()),
+                          _lib.ptr(st, "stats", dtype=torch.int32), _lib.stream())
+                if len(todo) == len(qs):
+                    calibrate_from_stats(qs, st)
+                else:
+                    for i in todo:
+                        calibrate_from_stats([qs[i]], st[i:i + 1])
+        return quant_records(qs, self.training)
+
+    def train(self, mode=True):
+        self._packed = None
+        return super().train(mode)
+
+    def packed_tables(self):
+        """Eval-mode int-packed tables (codes of round(B) bits per feature, csrc/quant.hip),
+        rebuilt when a table or a quantizer changed. Returns (buffer, code_bits, offsets, records)."""
+        qs = list(self.quantizers)
+        rec = quant_records(qs, False)
+        host = rec.cpu()                       # one sync (the reference .item()s every level's bits)
+        tabs = self.tables()
+        key = (tuple((t.data_ptr(), t._version) for t in tabs), tuple(host.flatten().tolist()))
+        if self._packed is not None and self._packed[0] == key:
+            return self._packed[1]
+        n = self.n_levels
+        bits = (ctypes.c_int * n)(*[int(v) for v in host[:, 6].tolist()])
+        code_bits, offsets = (ctypes.c_int * n)(), (ctypes.c_int64 * n)()
+        total = _lib.load().nerf_quant_packed_layout(bits, n, self.log2_hashmap_size, code_bits, offsets)
+        if total == 0:
+            raise RuntimeError("HashEmbedder: nerf_quant_packed_layout rejected the level layout")
+        buf = torch.empty(int(total), dtype=torch.uint8, device=tabs[0].device)
+        _lib.call("nerf_quant_pack_tables", _lib.ptr_array(tabs), n, self.log2_hashmap_size, _lib.ptr(rec, "records"),
+                  code_bits, offsets, _lib.ptr(buf, "packed", dtype=torch.uint8), _lib.stream())
+        packed = (buf, code_bits, offsets, rec)
+        self._packed = (key, packed)
+        return packed
+
+    def encode_into(self, xyz, feat, sp, sl, keep):
+        """Forward gather into caller-allocated feat/keep on the path this forward needs: plain,
+        fake-quantized (training / STE) or int-packed (eval-mode quantizers)."""
+        meta = self._meta
+        P = xyz.shape[0]
+        if self.quantization_active() and not self.training:
+            buf, code_bits, offsets, rec = self.packed_tables()
+            _lib.call("nerf_hash_encode_fwd_packed", _lib.ptr(xyz, "xyz"), P, meta["bmin"], meta["bmax"], meta["res"],
+                      self.n_levels, meta["log2_T"], _lib.ptr(buf, "packed", dtype=torch.uint8), code_bits, offsets,
+                      _lib.ptr(rec, "records"), _lib.ptr(feat, "feat"), sp, sl,
+                      _lib.ptr(keep, "keep", dtype=torch.bool), _lib.stream())
+            return
+        rec = self.level_records(xyz) if self.quantization_active() else None
+        _lib.call("nerf_hash_encode_fwd_q", _lib.ptr(xyz, "xyz"), P, meta["bmin"], meta["bmax"], meta["res"],
+                  self.n_levels, meta["log2_T"], _lib.ptr_array(self.tables()), _lib.ptr(rec, "records", allow_none=True),
+                  _lib.ptr(feat, "feat"), sp, sl, _lib.ptr(keep, "keep", dtype=torch.bool), _lib.stream())
+
     def encode(self, x, layout="point"):
-        return HashEncodeFn.apply(x, self._meta, layout, *self.tables())
+        return HashEncodeFn.apply(x, self, layout, *self.tables())
 
     def forward(self, x):
         if self.training:

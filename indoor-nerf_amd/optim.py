@@ -60,7 +60,7 @@ class RAdam(Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
-        segs = []
+        segs, updated = [], []
         for group in self.param_groups:
             beta1, beta2 = group["betas"]
             for p in group["params"]:
@@ -97,8 +97,13 @@ class RAdam(Optimizer):
                 s.step_coef = -step_size * group["lr"] if mode != 0 else 0.0
                 s.mode = mode
                 segs.append(s)
+                updated.append(p)
         for i in range(0, len(segs), _MAX_SEGS):
             chunk = segs[i:i + _MAX_SEGS]
             arr = (_lib.RAdamSegment * len(chunk))(*chunk)
             _lib.call("nerf_radam_step", arr, len(chunk), _lib.stream())
+        # the kernel writes through raw pointers: bump the version counters the reference's
+        # in-place tensor ops would have bumped (cache keys such as HashEmbedder.packed_tables)
+        for p in updated:
+            torch.autograd.graph.increment_version(p)
         return loss

@@ -480,6 +480,112 @@ def gen_normals(ref, out):
     np.savez_compressed(os.path.join(out, "f13_normals.npz"), **d)
 
 
+def make_qmlp(ref, seed):
+    torch.manual_seed(seed)
+    return ref.h.NeRFSmall(num_layers=2, hidden_dim=64, geo_feat_dim=15, num_layers_color=3,
+                           hidden_dim_color=64, input_ch=32, input_ch_views=16, use_quantization=True,
+                           quantization_bits=8)
+
+
+def quantizer_state(emb, coarse, fine):
+    """Calibrated scalars of every A-CAQ quantizer (quantization.py:97-119)."""
+    d = {}
+    for k in ("soft_bits", "range_scale", "v_max", "running_min", "running_max"):
+        d["emb_" + k] = np.array([float(getattr(q, k)) for q in emb.quantizers], np.float32)
+    for tag, net in (("coarse", coarse), ("fine", fine)):
+        a, w = net.sigma_act_quantizers[0], net.sigma_weight_quantizer
+        for k in ("soft_bits", "range_scale", "v_max", "running_min", "running_max"):
+            d[f"{tag}_act_{k}"] = np.float32(float(getattr(a, k)))
+        for k in ("soft_bits", "range_scale", "running_min", "running_max"):
+            d[f"{tag}_w_{k}"] = np.float32(float(getattr(w, k)))
+    return d
+
+
+def gen_acaq(ref, out):
+    """F14: the A-CAQ configuration (BASELINE config 5) through the reference's render path:
+    HashEmbedder(use_quantization=True) past its warm-up (hash_encoding.py:97-101) and
+    NeRFSmall(use_quantization=True) (run_nerf_helpers.py:268-284), coarse + fine.
+      a_*: first quantized training iteration (every quantizer calibrates on it) + backward;
+      b_*: non-integer soft bit widths in training mode (scale from 2**B with B a float), with the
+           activation quantizers re-ranged by hand so they do not collapse every activation to 0
+           (calibration on a ReLU output sets v_max = max, hence zero_point = qmax), + backward;
+      c_*: eval mode (integer bit widths 2..32 across the levels: every packed code width)."""
+    table = closed_form_table(scale=0.3, salt=3)
+    emb = ref.he.HashEmbedder(bbox_t(), n_levels=16, n_features_per_level=2, log2_hashmap_size=19,
+                              base_resolution=16, finest_resolution=1024, use_quantization=True,
+                              quantization_bits=8)
+    with torch.no_grad():
+        for i in range(16):
+            emb.embeddings[i].weight.copy_(torch.from_numpy(table[i]))
+    emb.current_step = 499                          # the next training forward is the first quantized one
+    coarse, fine = make_qmlp(ref, 30), make_qmlp(ref, 31)
+    with torch.no_grad():
+        coarse.sigma_net[1].weight[0] *= 60.0
+        fine.sigma_net[1].weight[0] *= 60.0
+    d = {}
+    d.update(mlp_arrays(coarse, "coarse0_"))
+    d.update(mlp_arrays(fine, "fine0_"))
+    ro, rd = synthetic_rays(64, seed=15)
+    target = np.random.RandomState(16).rand(64, 3).astype(np.float32)
+    d["rays_o"], d["rays_d"], d["target"] = ro, rd, target
+    kw = build_render_kwargs(ref, emb, coarse, fine, 64, 128, 1.0, 0.0, False)
+    params = list(coarse.parameters()) + list(fine.parameters()) + list(emb.parameters())
+
+    def run(tag, grad):
+        for p in params:
+            p.grad = None
+        with torch.set_grad_enabled(grad):
+            rgb, depth, acc, extras = ref.rn.render(800, 800, None, chunk=32768,
+                                                    rays=(torch.from_numpy(ro), torch.from_numpy(rd)),
+                                                    retraw=True, pytest=True, **kw)
+        d[f"{tag}_rgb"], d[f"{tag}_rgb0"] = rgb.detach().numpy(), extras["rgb0"].detach().numpy()
+        d[f"{tag}_raw"], d[f"{tag}_depth"] = extras["raw"].detach().numpy(), depth.detach().numpy()
+        if not grad:
+            return
+        loss = ref.h.img2mse(rgb, torch.from_numpy(target)) + ref.h.img2mse(extras["rgb0"], torch.from_numpy(target))
+        loss.backward()
+        d[f"{tag}_loss"] = np.float32(loss.item())
+        for name, net in (("coarse", coarse), ("fine", fine)):
+            for k, p in net.named_parameters():
+                if p.grad is not None:
+                    d[f"{tag}_g{name}_" + k.replace(".", "_")] = p.grad.numpy().copy()
+        gs = []
+        for i in range(16):
+            g = emb.embeddings[i].weight.grad.double()
+            gs.append([g.sum().item(), (g * g).sum().item(), g.abs().sum().item()])
+        d[f"{tag}_gtable_checksum"] = np.array(gs)
+        d[f"{tag}_qgrad_none"] = np.array([all(q.grad is None for q in m.parameters())
+                                           for m in list(emb.quantizers) + [coarse.sigma_act_quantizers[0],
+                                                                            coarse.sigma_weight_quantizer]])
+
+    run("a", True)
+    d.update({"a_" + k: v for k, v in quantizer_state(emb, coarse, fine).items()})
+    d["a_current_step"] = np.int64(emb.current_step)
+    # b: soft (non-integer) bit widths, activation ranges [0, running_max] with zero_point 0
+    b_bits = np.array([8.0, 7.6, 6.3, 5.5, 9.2, 4.45, 8.0, 6.5, 7.0, 3.7, 10.3, 8.8, 2.4, 12.6, 5.0, 7.5], np.float32)
+    with torch.no_grad():
+        for i, q in enumerate(emb.quantizers):
+            q.soft_bits.fill_(float(b_bits[i]))
+        for net, ab, wb in ((coarse, 6.7, 5.2), (fine, 7.3, 9.6)):
+            a = net.sigma_act_quantizers[0]
+            a.soft_bits.fill_(ab)
+            a.v_max.fill_(0.0)
+            net.sigma_weight_quantizer.soft_bits.fill_(wb)
+    d.update({"b_" + k: v for k, v in quantizer_state(emb, coarse, fine).items()})
+    run("b", True)
+    # c: eval mode, integer bit widths covering the 4/8/16-bit and fp32 packed layouts
+    c_bits = np.array([2, 3, 4, 5, 6, 7, 8, 9, 10, 12, 14, 16, 17, 20, 24, 32], np.float32)
+    with torch.no_grad():
+        for i, q in enumerate(emb.quantizers):
+            q.soft_bits.fill_(float(c_bits[i]))
+    d["c_emb_soft_bits"] = c_bits
+    emb.eval()
+    coarse.eval()
+    fine.eval()
+    run("c", False)
+    np.savez_compressed(os.path.join(out, "f14_acaq.npz"), **d)
+
+
 def gen_tv(ref, out):
     table = closed_form_table(scale=0.05, salt=5)
     emb = make_embedder(ref, 1024, table)
@@ -524,7 +630,7 @@ def main(only=None):
     ref = load_reference()
     gens = [("voxel", None), ("hash", gen_hash), ("sh", gen_sh), ("mlp", gen_mlp), ("composite", gen_composite),
             ("pdf", gen_pdf), ("render", gen_render), ("quant", gen_quant), ("tv", gen_tv), ("train", gen_train),
-            ("normals", gen_normals)]
+            ("normals", gen_normals), ("acaq", gen_acaq)]
     if not only or "levels" in only or "voxel" in only:
         levels = gen_levels(ref, out)
         gen_voxel(ref, out, levels)

@@ -202,3 +202,85 @@ def test_train_step(golden, oracle):
     for i in range(16):
         t = tabs[i].detach()
         np.testing.assert_allclose(t.numpy()[g["table_rows"]], g["table_samples"][i], rtol=1e-4, atol=1e-7)
+
+
+# ---------------------------------------------------------------- A-CAQ (a13, F14)
+
+def _acaq_states(g, p):
+    """Quantizer scalars of state p ('a_' / 'b_') in the oracle's argument form."""
+    lv = [(float(g[p + "emb_soft_bits"][i]), float(g[p + "emb_range_scale"][i]), float(g[p + "emb_v_max"][i]))
+          for i in range(16)]
+    nets = {}
+    for tag in ("coarse", "fine"):
+        nets[tag] = dict(w=(float(g[f"{p}{tag}_w_soft_bits"]), float(g[f"{p}{tag}_w_range_scale"])),
+                         act=(float(g[f"{p}{tag}_act_soft_bits"]), float(g[f"{p}{tag}_act_range_scale"]),
+                              float(g[f"{p}{tag}_act_v_max"])))
+    return lv, nets
+
+
+def _acaq_inputs(g, oracle):
+    table = closed_form_table(scale=0.3, salt=3)
+    bmin, bmax = _bbox()
+    res = oracle.level_resolutions(16, 1024)
+    ro, rd = torch.from_numpy(g["rays_o"]), torch.from_numpy(g["rays_d"])
+    return table, bmin, bmax, res, ro, rd
+
+
+def test_acaq_calibration(golden, oracle):
+    """The first quantized training iteration calibrates every quantizer (quantization.py:97-119):
+    per level on the coarse pass's gathered corners, W0 on its weight, the activation quantizer on
+    the first netchunk's relu(x W0q^T). Reproduced from the oracle's own gathers."""
+    g = golden("f14_acaq")
+    table, bmin, bmax, res, ro, rd = _acaq_inputs(g, oracle)
+    tabs = _tables(table)
+    u = oracle.pytest_uniforms((64, 64))
+    z = oracle.stratified_z(2.0, 6.0, 64, 64, False, u)
+    pts = (ro[:, None, :] + rd[:, None, :] * z[..., :, None]).reshape(-1, 3)
+    for lvl in range(16):
+        _, _, idx, _ = oracle.voxel_corners(pts, bmin, bmax, res[lvl], 19)
+        e = torch.nn.functional.embedding(idx, tabs[lvl])
+        lo, hi = e.min(), e.max()
+        assert float(lo) == g["a_emb_running_min"][lvl] and float(hi) == g["a_emb_running_max"][lvl]
+        assert float(hi - lo) == g["a_emb_range_scale"][lvl] and float(hi) == g["a_emb_v_max"][lvl]
+    cw = _mlp(g, "coarse0_")
+    w0 = cw["sigma_net.0.weight"]
+    assert float(2 * torch.max(w0.min().abs(), w0.max().abs())) == g["a_coarse_w_range_scale"]
+    assert g["a_current_step"] == 501 and bool(np.all(g["a_qgrad_none"]))
+
+
+def test_acaq_render_and_grads(golden, oracle):
+    """b: training mode with float bit widths (scale from 2**B, B a float32 tensor), STE backward;
+    c: eval mode (integer widths 2..32, deq outputs) — oracle vs the reference's render."""
+    g = golden("f14_acaq")
+    table, bmin, bmax, res, ro, rd = _acaq_inputs(g, oracle)
+    target = torch.from_numpy(g["target"])
+    lv, nets = _acaq_states(g, "b_")
+    tabs = _tables(table, requires_grad=True)
+    cw = {k: v.clone().requires_grad_(True) for k, v in _mlp(g, "coarse0_").items()}
+    fw = {k: v.clone().requires_grad_(True) for k, v in _mlp(g, "fine0_").items()}
+    out = oracle.render_rays(ro, rd, oracle.viewdirs_of(rd), 2.0, 6.0, cw, fw, tabs, bmin, bmax, res,
+                             level_q=oracle.level_quantizers(lv), coarse_q=nets["coarse"], fine_q=nets["fine"])
+    np.testing.assert_allclose(out["raw"].detach().numpy(), g["b_raw"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(out["rgb_map"].detach().numpy(), g["b_rgb"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(out["rgb0"].detach().numpy(), g["b_rgb0"], rtol=1e-5, atol=1e-5)
+    loss = torch.mean((out["rgb_map"] - target) ** 2) + torch.mean((out["rgb0"] - target) ** 2)
+    loss.backward()
+    assert abs(loss.item() - float(g["b_loss"])) <= 1e-5 * float(g["b_loss"])
+    for k, v in cw.items():
+        np.testing.assert_allclose(v.grad.numpy(), g["b_gcoarse_" + k.replace(".", "_")], rtol=1e-3, atol=1e-7)
+    for k, v in fw.items():
+        np.testing.assert_allclose(v.grad.numpy(), g["b_gfine_" + k.replace(".", "_")], rtol=1e-3, atol=1e-7)
+    for i in range(16):
+        gd = tabs[i].grad.double()
+        np.testing.assert_allclose([gd.sum().item(), (gd * gd).sum().item(), gd.abs().sum().item()],
+                                   g["b_gtable_checksum"][i], rtol=1e-3, atol=1e-12)
+    # c: eval mode
+    lv_c = [(float(g["c_emb_soft_bits"][i]), lv[i][1], lv[i][2]) for i in range(16)]
+    for q in nets.values():
+        q["training"] = False
+    with torch.no_grad():
+        out = oracle.render_rays(ro, rd, oracle.viewdirs_of(rd), 2.0, 6.0, _mlp(g, "coarse0_"), _mlp(g, "fine0_"),
+                                 _tables(table), bmin, bmax, res, level_q=oracle.level_quantizers(lv_c, False),
+                                 coarse_q=nets["coarse"], fine_q=nets["fine"])
+    np.testing.assert_allclose(out["raw"].numpy(), g["c_raw"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(out["rgb_map"].numpy(), g["c_rgb"], rtol=1e-5, atol=1e-5)
