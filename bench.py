@@ -48,17 +48,24 @@ UNIT_COST = {
 
 # ABI call -> the kernel symbols it launches (rocprofv3 names), to attach PMC traffic per call
 KERNEL_SYMBOLS = {
-    "nerf_hash_encode_fwd": ["nerf::hash_encode_fwd_kernel"],
+    "nerf_hash_encode_fwd": ["nerf::hash_encode_fwd_kernel<false>"],
     "nerf_hash_encode_bwd_ws": ["nerf::hash_encode_bwd_kernel<3>", "nerf::hash_bwd_owner_kernel"],
-    "nerf_mlp_fwd": ["nerf::mlp_fwd_frag_kernel"],
-    "nerf_mlp_bwd": ["nerf::mlp_bwd_frag_kernel"],
+    "nerf_mlp_fwd": ["nerf::mlp_fwd_frag_kernel<false>"],
+    "nerf_mlp_bwd": ["nerf::mlp_bwd_frag_kernel<false>"],
 }
 TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r01_traffic.json")
+
+
+def base_name(abi_name):
+    """nerf_mlp_fwd_q -> nerf_mlp_fwd: the _q entry points are the same kernels with optional
+    A-CAQ records (NULL on the unquantized path)."""
+    return abi_name[:-2] if abi_name.endswith("_q") else abi_name
 
 
 def pmc_traffic(abi_name):
     """HBM-side bytes per call of `abi_name` from the committed PMC passes (tools/profile_bench.sh:
     FETCH_SIZE and WRITE_SIZE in separate rocprofv3 passes of this bench), or None."""
+    abi_name = base_name(abi_name)
     if not os.path.exists(TRAFFIC_JSON) or abi_name not in KERNEL_SYMBOLS:
         return None
     t = json.load(open(TRAFFIC_JSON))
@@ -76,7 +83,32 @@ def parse():
     ap.add_argument("--cpu-rays", type=int, default=1024)
     ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--profile-kernels", type=int, default=1, help="record HIP events per kernel in the timed region")
+    ap.add_argument("--workload", default="lego", choices=sorted(WORKLOADS),
+                    help="BASELINE config: lego (configs[1], the headline), fern (configs[2], LLFF NDC), "
+                         "acaq (configs[4], A-CAQ quantized tables)")
+    ap.add_argument("--mode", default="train", choices=["train", "render"],
+                    help="train: full training iteration (the metric); render: render-only (eval modules, no grad)")
     return ap.parse_args()
+
+
+# BASELINE.json configs measured by this bench (the default line is configs[1], lego)
+WORKLOADS = {
+    "lego": dict(args=dict(finest_res=1024, N_samples=64, N_importance=128, white_bkgd=True, perturb=1.0,
+                           lrate_decay=500, tv_loss_weight=1e-6),
+                 near=2.0, far=6.0, rays="blender",
+                 desc="lego train step: {R} rays/GPU x (64 coarse + 128 fine) samples, finest_res 1024, L=16, F=2, "
+                      "T=2^19, RAdam, TV+sparsity losses"),
+    "fern": dict(args=dict(finest_res=512, N_samples=64, N_importance=64, white_bkgd=False, perturb=1.0,
+                           raw_noise_std=1.0, dataset_type="llff", tv_loss_weight=1e-6),
+                 near=0.0, far=1.0, rays="llff", ndc=True,
+                 desc="fern (LLFF) train step: {R} rays/GPU x (64 coarse + 64 fine) samples, NDC, raw noise 1, "
+                      "finest_res 512, RAdam, TV+sparsity losses"),
+    "acaq": dict(args=dict(finest_res=1024, N_samples=64, N_importance=128, white_bkgd=True, perturb=1.0,
+                           lrate_decay=500, tv_loss_weight=1e-6, use_quantization=True, quantization_bits=8),
+                 near=2.0, far=6.0, rays="blender", quantized=True,
+                 desc="lego + A-CAQ train step: {R} rays/GPU x (64 + 128) samples, 8-bit learned-bitwidth quantizers "
+                      "on the 16 levels, W0 and the hidden activation (past warm-up, calibrated)"),
+}
 
 
 def cpu_baseline(n_rays, steps):
@@ -131,32 +163,61 @@ def main():
     a = parse()
     import indoor_nerf_amd as nerf
     from indoor_nerf_amd import _lib
-    from indoor_nerf_amd.synthetic import blender_bbox, blender_rays
+    from indoor_nerf_amd.synthetic import blender_bbox, blender_rays, llff_bbox, llff_rays
 
+    wl = WORKLOADS[a.workload]
     rank, world, local = nerf.init_process_group()
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
-    lo, hi = blender_bbox()
-    args = nerf.make_args(bounding_box=(torch.from_numpy(lo), torch.from_numpy(hi)), finest_res=1024, N_samples=64,
-                          N_importance=128, white_bkgd=True, perturb=1.0, lrate_decay=500, tv_loss_weight=1e-6)
+    if wl["rays"] == "blender":
+        lo, hi = blender_bbox()
+        ro, rd = blender_rays(a.rays, seed=100 + rank)
+        H = W = 800
+        K = None
+    else:
+        lo, hi = llff_bbox()
+        ro, rd, (H, W, K) = llff_rays(a.rays, seed=100 + rank)
+    args = nerf.make_args(bounding_box=(torch.from_numpy(lo), torch.from_numpy(hi)), **wl["args"])
     torch.manual_seed(0)
     nerf.manual_seed(1234 + rank)
-    kw, _, _, grad_vars, opt = nerf.create_nerf(args, device=dev)
-    kw.update(near=2.0, far=6.0)                     # train() adds the Blender bounds (run_nerf.py:768-770,865-869)
+    kw, kw_test, _, grad_vars, opt = nerf.create_nerf(args, device=dev)
+    for d in (kw, kw_test):
+        d.update(near=wl["near"], far=wl["far"])     # train() adds the scene bounds (run_nerf.py:768-770,865-869)
+    if wl.get("ndc"):
+        for d in (kw, kw_test):
+            d.update(ndc=True, lindisp=False)
+    if wl.get("quantized"):
+        kw["embed_fn"].current_step = kw["embed_fn"].warmup_steps   # past the 500-call warm-up (hash_encoding.py:97)
     params = grad_vars + list(kw["embed_fn"].parameters())
     nerf.broadcast_params(params)
     arena = nerf.GradArena(params)
-    ro, rd = blender_rays(a.rays, seed=100 + rank)
     rays = (torch.from_numpy(ro).to(dev), torch.from_numpy(rd).to(dev))
     target = torch.rand(a.rays, 3, device=dev, generator=torch.Generator(device=dev).manual_seed(rank))
     tv_gen = torch.Generator().manual_seed(7)       # same TV cuboids on every rank
     hook = (lambda: arena.allreduce_mean()) if world > 1 else None
 
-    def step(i):
-        return nerf.train_step(rays, target, kw, opt, args, i, grad_hook=hook, loss_scale_sparsity=float(world),
-                               tv_generator=tv_gen, zero_grad=arena.zero_)
+    if a.mode == "train":
+        def step(i):
+            return nerf.train_step(rays, target, kw, opt, args, i, H=H, W=W, K=K, grad_hook=hook,
+                                   loss_scale_sparsity=float(world), tv_generator=tv_gen, zero_grad=arena.zero_)
+    else:
+        for m in (kw["network_fn"], kw["network_fine"], kw["embed_fn"]):
+            m.eval()
+
+        def step(i):
+            with torch.no_grad():
+                rgb, _, _, _ = nerf.render(H, W, K, chunk=args.chunk, rays=rays, **kw_test)
+            return rgb.mean(), rgb.mean()
 
     it = 1
+    if wl.get("quantized") and a.mode == "render":
+        # calibrate the quantizers with one training iteration first (they calibrate on their
+        # first training call), then switch to eval (int-packed tables)
+        for m in (kw["network_fn"], kw["network_fine"], kw["embed_fn"]):
+            m.train()
+        nerf.train_step(rays, target, kw, opt, args, 1, H=H, W=W, K=K, tv_generator=tv_gen, zero_grad=arena.zero_)
+        for m in (kw["network_fn"], kw["network_fine"], kw["embed_fn"]):
+            m.eval()
     for _ in range(a.warmup):
         step(it)
         it += 1
@@ -191,10 +252,11 @@ def main():
     roofline = None
     if kernels:
         dom = max(kernels, key=lambda n: kernels[n]["total_ms"])
-        P_coarse, P_fine = a.rays * 64, a.rays * 192
+        ns, ni = wl["args"]["N_samples"], wl["args"]["N_importance"]
+        P_coarse, P_fine = a.rays * ns, a.rays * (ns + ni)
         units_per_launch = {"point": (P_coarse + P_fine) / 2, "sample": (P_coarse + P_fine) / 2}
-        if dom in UNIT_COST:
-            bound, per_unit, unit = UNIT_COST[dom]
+        if base_name(dom) in UNIT_COST:
+            bound, per_unit, unit = UNIT_COST[base_name(dom)]
             units = units_per_launch[unit]
             avg_s = kernels[dom]["avg_ms"] * 1e-3
             traffic = pmc_traffic(dom)
@@ -217,7 +279,7 @@ def main():
 
     value = world * a.rays * a.steps / elapsed
     out = {
-        "metric": "train rays/sec (4096 rays x 192 samples)",
+        "metric": "train rays/sec (4096 rays x 192 samples)" if a.mode == "train" else "render rays/sec (eval)",
         "value": round(value, 1),
         "unit": "rays/s",
         "n_gpus": world,
@@ -228,17 +290,17 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "fp32",
-        "data": "synthetic (lego spiral-pose rays, random-init hash tables and MLPs)",
-        "config": {"workload": "lego train step: 4096 rays/GPU x (64 coarse + 128 fine) samples, finest_res 1024, "
-                               "L=16, F=2, T=2^19, RAdam, TV+sparsity losses",
-                   "rays_per_gpu": a.rays, "global_batch": a.rays * world, "samples": "64+128",
-                   "parallelism": f"dp{world}"},
+        "data": "synthetic ({} rays, random-init hash tables and MLPs)".format(
+            "lego spiral-pose" if wl["rays"] == "blender" else "forward-facing LLFF rig"),
+        "config": {"workload": wl["desc"].format(R=a.rays) + ("" if a.mode == "train" else " [render only]"),
+                   "name": a.workload, "rays_per_gpu": a.rays, "global_batch": a.rays * world,
+                   "samples": f"{wl['args']['N_samples']}+{wl['args']['N_importance']}", "parallelism": f"dp{world}"},
         "loss": round(float(loss), 6),
         "roofline": roofline,
         "kernels": {k: {kk: round(vv, 4) if isinstance(vv, float) else vv for kk, vv in v.items()}
                     for k, v in sorted(kernels.items(), key=lambda kv: -kv[1]["total_ms"])},
     }
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+    if rank == 0 and world == 1 and not a.no_cpu_baseline and a.workload == "lego" and a.mode == "train":
         out["cpu_baseline"] = cpu_baseline(a.cpu_rays, a.cpu_steps)
     elif rank == 0:
         out["cpu_baseline"] = None

@@ -215,6 +215,26 @@ int nerf_sample_fine(const float* d_rays, int64_t ray_stride, const float* d_z, 
                      const float* d_u, uint64_t seed, uint64_t offset,
                      float* d_z_fine, float* d_pts_fine, float* d_z_std, float* d_samples, void* stream);
 
+/* ---- rays of the training batch / of a whole image (run_nerf.py:973-1004, run_nerf_helpers.py:311-320)
+ * Camera: c2w = the pose [3,4] as float32 (torch.Tensor(pose)), fx = K[0][0], fy = K[1][1],
+ * cx = K[0][2], cy = K[1][2] rounded to float32 (the scalars get_rays' tensor ops see).
+ * Pixel (row, col) -> dirs = ((col - cx)/fx, -(row - cy)/fy, -1), rays_d = c2w[:3,:3] dirs,
+ * rays_o = c2w[:3,3]. Cells of the crop window [r0, r0+h) x [c0, c0+w) are numbered row-major.
+ * random != 0: n_rays DISTINCT cells drawn uniformly without replacement (np.random.choice(...,
+ * replace=False) of train(); a keyed Feistel permutation from (seed, offset)); random == 0: cells
+ * 0..n_rays-1 in order (the whole image when the window is the image). d_image [H,W,channels]
+ * float32 (may be NULL if d_target is NULL): d_target [n,3] = its first three channels at the
+ * pixel. d_coords [n,2] int32 (row, col), may be NULL. */
+typedef struct {
+    float c2w[12];
+    float fx, fy, cx, cy;
+} nerf_camera;
+
+int nerf_sample_rays(const nerf_camera* cam, int H, int W, int crop_r0, int crop_c0, int crop_h, int crop_w,
+                     int64_t n_rays, int random, uint64_t seed, uint64_t offset,
+                     const float* d_image, int channels, float* d_rays_o, float* d_rays_d, float* d_target,
+                     int32_t* d_coords, void* stream);
+
 /* ---- RAdam (PocketNeRF/radam.py:28-94), one launch over up to 32 tensor segments ----------
  * Per segment: p, g, m (exp_avg), v (exp_avg_sq) of n elements. The host evaluates the scalar
  * algebra of radam.py:56-79 in double, exactly as the reference's Python does, and passes the
@@ -302,20 +322,33 @@ int nerf_quant_calibrate(const nerf_quantizer* qs, int n, const uint32_t* d_minm
  * x + (deq - x), whose gradient is the identity. d_y may alias d_x. */
 int nerf_fake_quant(const float* d_x, int64_t count, const float* d_rec, float* d_y, void* stream);
 
+/* A-CAQ bit-width controller of train() (run_nerf.py:1207-1250), run every 10th iteration from
+ * acaq_start_iter: loss_ratio = img_loss / target (target = target_metric, or 1.2 x the best
+ * img_loss so far, kept in d_best_loss, NaN = unset); per quantizer idx of n:
+ * delta = {-0.3 | -0.1 | +0.2 by ratio < 0.95 / < 1.05 / else} - bit_penalty*bits/8, times
+ * 1 + (idx - n/2)*0.02; soft_bits = clamp(soft_bits + delta, min_bits, max_bits). Writes each
+ * quantizer's soft_bits; d_report (may be NULL): double[2] = (target, ratio). */
+int nerf_acaq_update(const nerf_quantizer* qs, int n, const float* d_img_loss, double* d_best_loss,
+                     int has_target, double target_metric, double bit_penalty, double* d_report, void* stream);
+
 /* Int-packed hash tables for eval-mode rendering (quantizer in eval mode: value = (q - zp) * scale
- * with q the integer code). Level l's codes take code_bits[l] in {4, 8, 16} bits per feature (two
- * features per entry: 1, 2 or 4 bytes per entry), or 32 = the dequantized fp32 value itself.
- * nerf_quant_packed_layout: code_bits and byte offsets (256-B aligned) of each level; returns the
- * total bytes. pack: codes of every table entry. fwd: the gather + trilinear of
- * nerf_hash_encode_fwd_q reading codes; bit-identical to it in eval mode. */
-size_t nerf_quant_packed_layout(const int* level_bits, int n_levels, int log2_T, int* code_bits, int64_t* offsets);
+ * with q the integer code, quantization.py:183-186). Level l occupies bytes [l*T*8, (l+1)*T*8) of
+ * d_packed (nerf_quant_packed_bytes); its entries are stored densely from the region start with
+ * the width of the level's record bits: <= 4 -> 1 byte per entry (two 4-bit codes), <= 8 -> 2,
+ * <= 16 -> 4, else the dequantized fp32 pair (8). The layout never depends on the bit widths, so
+ * no host round trip is needed.
+ * pack: repacks exactly the levels whose record differs from d_prev_rec ([n_levels][8], device;
+ *       initialise with NaNs or pass force=1 when the tables changed), then stores the records
+ *       there; d_dirty: device int[n_levels] scratch.
+ * fwd:  the gather + trilinear of nerf_hash_encode_fwd_q reading codes; bit-identical to it with
+ *       the same eval-mode records. */
+size_t nerf_quant_packed_bytes(int n_levels, int log2_T);
 int nerf_quant_pack_tables(const float* const* d_tables, int n_levels, int log2_T, const float* d_qrec,
-                           const int* code_bits, const int64_t* offsets, void* d_packed, void* stream);
+                           float* d_prev_rec, int force, int* d_dirty, void* d_packed, void* stream);
 int nerf_hash_encode_fwd_packed(const float* d_xyz, int64_t n_points, const float* bbox_min3, const float* bbox_max3,
                                 const float* level_res, int n_levels, int log2_T, const void* d_packed,
-                                const int* code_bits, const int64_t* offsets, const float* d_qrec,
-                                float* d_feat, int64_t feat_stride_point, int64_t feat_stride_level,
-                                uint8_t* d_keep, void* stream);
+                                const float* d_qrec, float* d_feat, int64_t feat_stride_point,
+                                int64_t feat_stride_level, uint8_t* d_keep, void* stream);
 
 #ifdef __cplusplus
 }

@@ -46,6 +46,11 @@ class Quantizer(ctypes.Structure):
                 ("running_max", c_vp), ("min_bits", ctypes.c_float), ("max_bits", ctypes.c_float)]
 
 
+class Camera(ctypes.Structure):
+    _fields_ = [("c2w", ctypes.c_float * 12), ("fx", ctypes.c_float), ("fy", ctypes.c_float),
+                ("cx", ctypes.c_float), ("cy", ctypes.c_float)]
+
+
 # name -> argtypes (restype is int for all but the two metadata calls)
 SIGNATURES = {
     "nerf_hash_encode_fwd": [c_vp, c_i64, c_f32p, c_f32p, c_f32p, c_int, c_int, ctypes.POINTER(c_vp),
@@ -76,6 +81,8 @@ SIGNATURES = {
     "nerf_sample_pdf": [c_vp, c_i64, c_vp, c_i64, c_i64, c_int, c_int, c_int, c_vp, c_vp, c_u64, c_u64, c_vp, c_vp],
     "nerf_sample_fine": [c_vp, c_i64, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_vp, c_vp, c_u64, c_u64,
                          c_vp, c_vp, c_vp, c_vp, c_vp],
+    "nerf_sample_rays": [ctypes.POINTER(Camera), c_int, c_int, c_int, c_int, c_int, c_int, c_i64, c_int, c_u64,
+                         c_u64, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp],
     "nerf_radam_step": [ctypes.POINTER(RAdamSegment), c_int, c_vp],
     "nerf_tv_fwd": [ctypes.POINTER(c_vp), c_int, c_int, ctypes.POINTER(c_i64), ctypes.POINTER(c_int), c_vp, c_vp],
     "nerf_tv_bwd": [ctypes.POINTER(c_vp), c_int, c_int, ctypes.POINTER(c_i64), ctypes.POINTER(c_int), c_vp,
@@ -88,10 +95,11 @@ SIGNATURES = {
     "nerf_hash_gather_minmax": [c_vp, c_i64, c_f32p, c_f32p, c_f32p, c_int, c_int, ctypes.POINTER(c_vp), c_vp, c_vp],
     "nerf_quant_calibrate": [ctypes.POINTER(Quantizer), c_int, c_vp, c_vp],
     "nerf_fake_quant": [c_vp, c_i64, c_vp, c_vp, c_vp],
-    "nerf_quant_pack_tables": [ctypes.POINTER(c_vp), c_int, c_int, c_vp, ctypes.POINTER(c_int),
-                               ctypes.POINTER(c_i64), c_vp, c_vp],
-    "nerf_hash_encode_fwd_packed": [c_vp, c_i64, c_f32p, c_f32p, c_f32p, c_int, c_int, c_vp, ctypes.POINTER(c_int),
-                                    ctypes.POINTER(c_i64), c_vp, c_vp, c_i64, c_i64, c_vp, c_vp],
+    "nerf_acaq_update": [ctypes.POINTER(Quantizer), c_int, c_vp, c_vp, c_int, ctypes.c_double, ctypes.c_double,
+                         c_vp, c_vp],
+    "nerf_quant_pack_tables": [ctypes.POINTER(c_vp), c_int, c_int, c_vp, c_vp, c_int, c_vp, c_vp, c_vp],
+    "nerf_hash_encode_fwd_packed": [c_vp, c_i64, c_f32p, c_f32p, c_f32p, c_int, c_int, c_vp, c_vp, c_vp, c_i64,
+                                    c_i64, c_vp, c_vp],
     "nerf_train_loss_bwd": [c_vp, c_vp, c_vp, c_i64, ctypes.c_float, c_int, ctypes.c_float, c_vp, c_vp, c_vp,
                             c_vp, c_vp, c_vp, c_vp],
 }
@@ -114,9 +122,8 @@ def load():
     lib.nerf_abi_version.argtypes = []
     lib.nerf_hash_encode_bwd_workspace_bytes.restype = ctypes.c_size_t
     lib.nerf_hash_encode_bwd_workspace_bytes.argtypes = [c_int, c_int, c_i64]
-    lib.nerf_quant_packed_layout.restype = ctypes.c_size_t
-    lib.nerf_quant_packed_layout.argtypes = [ctypes.POINTER(c_int), c_int, c_int, ctypes.POINTER(c_int),
-                                             ctypes.POINTER(c_i64)]
+    lib.nerf_quant_packed_bytes.restype = ctypes.c_size_t
+    lib.nerf_quant_packed_bytes.argtypes = [c_int, c_int]
     for name, argtypes in SIGNATURES.items():
         fn = getattr(lib, name)
         fn.argtypes = argtypes
@@ -127,7 +134,7 @@ def load():
 
 def exported_symbols():
     return ["nerf_last_error", "nerf_abi_version", "nerf_hash_encode_bwd_workspace_bytes",
-            "nerf_quant_packed_layout"] + list(SIGNATURES)
+            "nerf_quant_packed_bytes"] + list(SIGNATURES)
 
 
 _TIMING = None   # when a list: (name, start_event, end_event) per launch, recorded on the current stream

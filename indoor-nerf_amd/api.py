@@ -5,10 +5,12 @@ from .dist import GradArena, broadcast_params, init_process_group, shard
 from .field import NeRFSmall, batchify, run_network
 from .hashgrid import HashEmbedder, SHEncoder, level_resolutions
 from .losses import sigma_sparsity_loss, total_variation_all, total_variation_loss, train_loss
-from .model import create_nerf, make_args, save_checkpoint, train_step
+from .model import acaq_quantizers, acaq_update, create_nerf, make_args, save_checkpoint, train_step
 from .optim import RAdam
 from .quantization import FakeQuantizer, LearnedBitwidthQuantizer, PassthroughQuantizer, calculate_fqr
-from .render import (batchify_rays, get_rays, get_rays_np, img2mse, manual_seed, mse2psnr, ndc_rays, raw2outputs,
+from .rays import RaySampler, crop_window
+from .scene import get_bbox3d_for_blenderobj, get_bbox3d_for_llff
+from .render import (batchify_rays, camera, get_rays, get_rays_np, img2mse, manual_seed, mse2psnr, ndc_rays, raw2outputs,
                      render, render_rays, sample_pdf, to8b)
 
 __all__ = ["HashEmbedder", "SHEncoder", "NeRFSmall", "RAdam", "run_network", "batchify", "batchify_rays", "render",
@@ -16,7 +18,8 @@ __all__ = ["HashEmbedder", "SHEncoder", "NeRFSmall", "RAdam", "run_network", "ba
            "to8b", "create_nerf", "make_args", "save_checkpoint", "train_step", "total_variation_loss",
            "total_variation_all", "train_loss", "sigma_sparsity_loss", "level_resolutions", "GradArena", "init_process_group",
            "shard", "broadcast_params", "manual_seed", "load_library", "LearnedBitwidthQuantizer", "FakeQuantizer",
-           "PassthroughQuantizer", "calculate_fqr"]
+           "PassthroughQuantizer", "calculate_fqr", "acaq_update", "acaq_quantizers", "RaySampler", "crop_window", "camera",
+           "get_bbox3d_for_blenderobj", "get_bbox3d_for_llff"]
 
 
 def load_library():

@@ -139,22 +139,77 @@ __global__ void __launch_bounds__(256) fake_quant_kernel(const float* __restrict
         y[i] = fake_quant(x[i], q);
 }
 
+// A-CAQ bit-width controller of train() (run_nerf.py:1207-1250), every 10th iteration, on the
+// device (the reference reads img_loss and every soft_bits with .item()): the same double-precision
+// algebra on the float32 values, then the float32 in-place add and clamp of soft_bits.
+__global__ void acaq_update_kernel(QuantizerSet set, int n, const float* __restrict__ img_loss,
+                                   double* __restrict__ best, int has_target, double target_metric,
+                                   double bit_penalty, double* __restrict__ report) {
+    if (threadIdx.x != 0) return;
+    const double cur = (double)*img_loss;
+    double target;
+    if (has_target) {
+        target = target_metric;
+    } else {
+        const double b = isnan(*best) ? cur : fmin(*best, cur);     // train.best_loss (:1218-1221)
+        *best = b;
+        target = b * 1.2;
+    }
+    const double ratio = cur / target;
+    for (int i = 0; i < n; ++i) {
+        float* sb = const_cast<float*>(set.q[i].soft_bits);
+        const double bits = (double)*sb;
+        double delta = ratio < 0.95 ? -0.3 : (ratio < 1.05 ? -0.1 : 0.2);
+        delta -= bit_penalty * bits / 8.0;
+        delta *= 1.0 + ((double)i - (double)n / 2.0) * 0.02;       // layer_factor
+        const float nb = *sb + (float)delta;                         // soft_bits.data += bit_delta (fp32)
+        *sb = fminf(fmaxf(nb, set.q[i].min_bits), set.q[i].max_bits);
+    }
+    if (report) {
+        report[0] = target;
+        report[1] = ratio;
+    }
+}
+
 // ---- int-packed tables ----------------------------------------------------------------------
-struct PackedLevels {
+// Level l occupies bytes [l * T * 8, (l+1) * T * 8) of the packed buffer (the fp32 table's size, so
+// the layout never depends on the bit widths and needs no host round trip); its entries are stored
+// densely from the region start with the code width of the level's record: B <= 4 -> 1 byte per
+// entry (two 4-bit codes), B <= 8 -> 2 bytes, B <= 16 -> 4 bytes, else the fp32 deq pair (8 bytes).
+__device__ __forceinline__ int code_width(const QuantRec& q) {
+    const int b = (int)q.bits;
+    return b <= 4 ? 4 : b <= 8 ? 8 : b <= 16 ? 16 : 32;
+}
+
+struct PackTables {
     const float* tables[NERF_MAX_LEVELS];
-    int64_t offset[NERF_MAX_LEVELS];   // bytes from the packed base
-    int bits[NERF_MAX_LEVELS];         // 4, 8, 16 (codes) or 32 (fp32 deq values)
 };
+
+// dirty[l] = force || record l differs from the one the level was last packed with; prev := rec.
+__global__ void pack_dirty_kernel(const QuantRec* __restrict__ rec, QuantRec* __restrict__ prev, int n, int force,
+                                  int* __restrict__ dirty) {
+    const int l = threadIdx.x;
+    if (l >= n) return;
+    const float* a = reinterpret_cast<const float*>(rec + l);
+    float* b = reinterpret_cast<float*>(prev + l);
+    bool same = !force;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) same = same && (__float_as_uint(a[k]) == __float_as_uint(b[k]));
+    dirty[l] = same ? 0 : 1;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) b[k] = a[k];
+}
 
 // One thread per table entry (2 features). Codes are stored unsigned: q - qmin (qmin = 0 for the
 // asymmetric hash quantizers; symmetric codes are offset so they stay non-negative).
-__global__ void __launch_bounds__(256) pack_tables_kernel(PackedLevels pl, int64_t T, const QuantRec* __restrict__ qrec,
-                                                          uint8_t* __restrict__ packed) {
+__global__ void __launch_bounds__(256) pack_tables_kernel(PackTables pt, int64_t T, const QuantRec* __restrict__ qrec,
+                                                          const int* __restrict__ dirty, uint8_t* __restrict__ packed) {
     const int lvl = blockIdx.y;
+    if (!dirty[lvl]) return;
     const QuantRec q = qrec[lvl];
-    const int bits = pl.bits[lvl];
-    uint8_t* base = packed + pl.offset[lvl];
-    const float2* tab = reinterpret_cast<const float2*>(pl.tables[lvl]);
+    const int bits = code_width(q);
+    uint8_t* base = packed + (size_t)lvl * (size_t)T * 8;
+    const float2* tab = reinterpret_cast<const float2*>(pt.tables[lvl]);
     for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < T; r += (int64_t)gridDim.x * blockDim.x) {
         const float2 e = tab[r];
         if (bits == 32) {
@@ -201,7 +256,7 @@ __device__ __forceinline__ void gather_level(const uint8_t* base, const uint32_t
 }
 
 __global__ void __launch_bounds__(256) hash_encode_fwd_packed_kernel(
-    const float* __restrict__ xyz, int64_t n, HashParams hp, PackedLevels pl, const uint8_t* __restrict__ packed,
+    const float* __restrict__ xyz, int64_t n, HashParams hp, int64_t T, const uint8_t* __restrict__ packed,
     const QuantRec* __restrict__ qrec, float* __restrict__ feat, int64_t sp, int64_t sl, uint8_t* __restrict__ keep) {
     const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int lvl = blockIdx.y;
@@ -217,9 +272,9 @@ __global__ void __launch_bounds__(256) hash_encode_fwd_packed_kernel(
         h[c] = spatial_hash3((uint32_t)ax.base + ((c >> 2) & 1), (uint32_t)ay.base + ((c >> 1) & 1),
                              (uint32_t)az.base + (c & 1), hp.mask);
     const QuantRec q = qrec[lvl];
-    const uint8_t* base = packed + pl.offset[lvl];
+    const uint8_t* base = packed + (size_t)lvl * (size_t)T * 8;
     float e0[8], e1[8];
-    switch (pl.bits[lvl]) {   // uniform per block (one level per blockIdx.y)
+    switch (code_width(q)) {   // uniform per block (one level per blockIdx.y)
         case 4: gather_level<4>(base, h, q, e0, e1); break;
         case 8: gather_level<8>(base, h, q, e0, e1); break;
         case 16: gather_level<16>(base, h, q, e0, e1); break;
@@ -326,71 +381,60 @@ extern "C" int nerf_fake_quant(const float* d_x, int64_t count, const float* d_r
     return NERF_OK;
 }
 
-extern "C" size_t nerf_quant_packed_layout(const int* level_bits, int n_levels, int log2_T, int* code_bits,
-                                           int64_t* offsets) {
-    if (!level_bits || !code_bits || !offsets || n_levels < 1 || n_levels > NERF_MAX_LEVELS || log2_T < 1 ||
-        log2_T > 30)
-        return 0;
-    const int64_t T = int64_t(1) << log2_T;
-    int64_t off = 0;
-    for (int l = 0; l < n_levels; ++l) {
-        const int b = level_bits[l];
-        const int cb = b <= 4 ? 4 : b <= 8 ? 8 : b <= 16 ? 16 : 32;
-        code_bits[l] = cb;
-        offsets[l] = off;
-        const int64_t bytes = T * (cb == 4 ? 1 : cb == 8 ? 2 : cb == 16 ? 4 : 8);
-        off += (bytes + 255) & ~int64_t(255);
-    }
-    return (size_t)off;
-}
-
-static int fill_packed(PackedLevels& pl, const float* const* tables, int n_levels, const int* code_bits,
-                       const int64_t* offsets) {
-    NERF_REQUIRE(code_bits && offsets, "packed: null layout");
-    for (int l = 0; l < n_levels; ++l) {
-        NERF_REQUIRE(code_bits[l] == 4 || code_bits[l] == 8 || code_bits[l] == 16 || code_bits[l] == 32,
-                     "packed: level %d code bits %d", l, code_bits[l]);
-        NERF_REQUIRE(offsets[l] >= 0 && (offsets[l] & 255) == 0, "packed: level %d offset", l);
-        pl.tables[l] = tables ? tables[l] : nullptr;
-        pl.offset[l] = offsets[l];
-        pl.bits[l] = code_bits[l];
-    }
-    return NERF_OK;
+extern "C" size_t nerf_quant_packed_bytes(int n_levels, int log2_T) {
+    if (n_levels < 1 || n_levels > NERF_MAX_LEVELS || log2_T < 1 || log2_T > 30) return 0;
+    return (size_t)n_levels * ((size_t)1 << log2_T) * 8;
 }
 
 extern "C" int nerf_quant_pack_tables(const float* const* d_tables, int n_levels, int log2_T, const float* d_qrec,
-                                      const int* code_bits, const int64_t* offsets, void* d_packed, void* stream) {
-    NERF_REQUIRE(d_tables && d_qrec && d_packed && n_levels >= 1 && n_levels <= NERF_MAX_LEVELS && log2_T >= 1 &&
-                 log2_T <= 30, "quant_pack_tables: bad args");
-    PackedLevels pl{};
-    int rc = fill_packed(pl, d_tables, n_levels, code_bits, offsets);
-    if (rc) return rc;
-    for (int l = 0; l < n_levels; ++l) NERF_REQUIRE(d_tables[l], "quant_pack_tables: table %d is null", l);
+                                      float* d_prev_rec, int force, int* d_dirty, void* d_packed, void* stream) {
+    NERF_REQUIRE(d_tables && d_qrec && d_prev_rec && d_dirty && d_packed && n_levels >= 1 &&
+                 n_levels <= NERF_MAX_LEVELS && log2_T >= 1 && log2_T <= 30, "quant_pack_tables: bad args");
+    PackTables pt{};
+    for (int l = 0; l < n_levels; ++l) {
+        NERF_REQUIRE(d_tables[l], "quant_pack_tables: table %d is null", l);
+        pt.tables[l] = d_tables[l];
+    }
+    hipLaunchKernelGGL(pack_dirty_kernel, dim3(1), dim3(64), 0, as_stream(stream),
+                       reinterpret_cast<const QuantRec*>(d_qrec), reinterpret_cast<QuantRec*>(d_prev_rec), n_levels,
+                       force ? 1 : 0, d_dirty);
+    NERF_CHECK_LAUNCH("quant_pack_tables(dirty)");
     const int64_t T = int64_t(1) << log2_T;
-    const unsigned bx = (unsigned)std::min<int64_t>(blocks_for(T, 256), 2048);
-    hipLaunchKernelGGL(pack_tables_kernel, dim3(bx, n_levels), dim3(256), 0, as_stream(stream), pl, T,
-                       reinterpret_cast<const QuantRec*>(d_qrec), reinterpret_cast<uint8_t*>(d_packed));
+    const unsigned bx = (unsigned)std::min<int64_t>(blocks_for(T, 256), 512);
+    hipLaunchKernelGGL(pack_tables_kernel, dim3(bx, n_levels), dim3(256), 0, as_stream(stream), pt, T,
+                       reinterpret_cast<const QuantRec*>(d_qrec), d_dirty, reinterpret_cast<uint8_t*>(d_packed));
     NERF_CHECK_LAUNCH("quant_pack_tables");
     return NERF_OK;
 }
 
 extern "C" int nerf_hash_encode_fwd_packed(const float* d_xyz, int64_t n_points, const float* bbox_min3,
                                            const float* bbox_max3, const float* level_res, int n_levels, int log2_T,
-                                           const void* d_packed, const int* code_bits, const int64_t* offsets,
-                                           const float* d_qrec, float* d_feat, int64_t feat_stride_point,
-                                           int64_t feat_stride_level, uint8_t* d_keep, void* stream) {
+                                           const void* d_packed, const float* d_qrec, float* d_feat,
+                                           int64_t feat_stride_point, int64_t feat_stride_level, uint8_t* d_keep,
+                                           void* stream) {
     NERF_REQUIRE(n_points >= 0 && d_xyz && d_packed && d_qrec && d_feat, "hash_encode_fwd_packed: bad args");
     HashParams hp{};
     int rc = hash_params(hp, bbox_min3, bbox_max3, level_res, n_levels, log2_T, nullptr);
     if (rc) return rc;
-    PackedLevels pl{};
-    rc = fill_packed(pl, nullptr, n_levels, code_bits, offsets);
-    if (rc) return rc;
     if (n_points == 0) return NERF_OK;
     dim3 grid(blocks_for(n_points, 256), n_levels);
-    hipLaunchKernelGGL(hash_encode_fwd_packed_kernel, grid, dim3(256), 0, as_stream(stream), d_xyz, n_points, hp, pl,
-                       reinterpret_cast<const uint8_t*>(d_packed), reinterpret_cast<const QuantRec*>(d_qrec), d_feat,
-                       feat_stride_point, feat_stride_level, d_keep);
+    hipLaunchKernelGGL(hash_encode_fwd_packed_kernel, grid, dim3(256), 0, as_stream(stream), d_xyz, n_points, hp,
+                       int64_t(1) << log2_T, reinterpret_cast<const uint8_t*>(d_packed),
+                       reinterpret_cast<const QuantRec*>(d_qrec), d_feat, feat_stride_point, feat_stride_level,
+                       d_keep);
     NERF_CHECK_LAUNCH("hash_encode_fwd_packed");
+    return NERF_OK;
+}
+
+extern "C" int nerf_acaq_update(const nerf_quantizer* qs, int n, const float* d_img_loss, double* d_best_loss,
+                                int has_target, double target_metric, double bit_penalty, double* d_report,
+                                void* stream) {
+    QuantizerSet set;
+    int rc = fill_set(set, qs, n, false);
+    if (rc) return rc;
+    NERF_REQUIRE(d_img_loss && (has_target || d_best_loss), "acaq_update: null loss / best-loss pointer");
+    hipLaunchKernelGGL(acaq_update_kernel, dim3(1), dim3(64), 0, as_stream(stream), set, n, d_img_loss, d_best_loss,
+                       has_target ? 1 : 0, target_metric, bit_penalty, d_report);
+    NERF_CHECK_LAUNCH("acaq_update");
     return NERF_OK;
 }

@@ -1,0 +1,121 @@
+// Ray generation and train()'s per-iteration pixel batch on the device.
+//
+//   nerf_sample_rays  run_nerf.py:973-1004 (use_batching = False): N_rand distinct pixels of one
+//                     training image (optionally inside the precrop window), their rays
+//                     (run_nerf_helpers.get_rays :311-320, evaluated only at those pixels) and
+//                     target colours, in one launch. The reference rebuilds every ray of the
+//                     image, draws np.random.choice(H*W, N_rand, replace=False) on the host and
+//                     gathers (plus a 7.7 MB host->device copy of the image) per iteration.
+//   random = 0        rays of grid cells 0..n-1 in row-major order: get_rays of a whole image
+//                     (render(c2w=...) / render_path) or of the crop window.
+//
+// Sampling without replacement: cell index = pi(t) for lane t, where pi is a keyed 4-round
+// Feistel permutation of [0, 2^(2k)) restricted to [0, n_cells) by cycle walking (a bijection on
+// [0, n_cells), so the N_rand cells are distinct by construction); keys from (seed, offset).
+#include "common.h"
+
+namespace nerf {
+
+struct Cam {
+    float c2w[12];
+    float fx, fy, cx, cy;
+};
+
+__device__ __forceinline__ uint32_t mix32(uint32_t h) {
+    h ^= h >> 16;
+    h *= 0x7feb352du;
+    h ^= h >> 15;
+    h *= 0x846ca68bu;
+    h ^= h >> 16;
+    return h;
+}
+
+__device__ __forceinline__ uint32_t feistel_perm(uint32_t x, int half_bits, const uint32_t (&key)[4]) {
+    const uint32_t mask = (1u << half_bits) - 1u;
+    uint32_t L = x >> half_bits, R = x & mask;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const uint32_t nl = R;
+        R = (L ^ mix32(R ^ key[r])) & mask;
+        L = nl;
+    }
+    return (L << half_bits) | R;
+}
+
+__global__ void __launch_bounds__(256) sample_rays_kernel(Cam cam, int W_img, int r0, int c0, int cw, int64_t n_cells,
+                                                          int64_t n_rays, int random, int half_bits, uint32_t k0,
+                                                          uint32_t k1, uint32_t k2, uint32_t k3,
+                                                          const float* __restrict__ image, int channels,
+                                                          float* __restrict__ rays_o, float* __restrict__ rays_d,
+                                                          float* __restrict__ target, int32_t* __restrict__ coords) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n_rays) return;
+    int64_t cell = t;
+    if (random) {
+        const uint32_t key[4] = {k0, k1, k2, k3};
+        uint32_t x = (uint32_t)t;
+        do {
+            x = feistel_perm(x, half_bits, key);
+        } while ((int64_t)x >= n_cells);
+        cell = x;
+    }
+    const int row = r0 + (int)(cell / cw), col = c0 + (int)(cell % cw);
+    // dirs = [(i - cx)/fx, -(j - cy)/fy, -1]; rays_d = sum(dirs[..., None, :] * c2w[:3,:3], -1)
+    const float i = (float)col, j = (float)row;
+    const float d0 = (i - cam.cx) / cam.fx;
+    const float d1 = -(j - cam.cy) / cam.fy;
+    const float d2 = -1.0f;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const float p0 = d0 * cam.c2w[4 * a + 0], p1 = d1 * cam.c2w[4 * a + 1], p2 = d2 * cam.c2w[4 * a + 2];
+        rays_d[3 * t + a] = (p0 + p1) + p2;
+        rays_o[3 * t + a] = cam.c2w[4 * a + 3];
+    }
+    if (target) {
+        const float* px = image + ((int64_t)row * W_img + col) * channels;
+#pragma unroll
+        for (int a = 0; a < 3; ++a) target[3 * t + a] = px[a];
+    }
+    if (coords) {
+        coords[2 * t] = row;
+        coords[2 * t + 1] = col;
+    }
+}
+
+static uint32_t splitmix(uint64_t& s) {
+    uint64_t z = (s += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return (uint32_t)((z ^ (z >> 31)) >> 16);
+}
+
+}  // namespace nerf
+
+using namespace nerf;
+
+extern "C" int nerf_sample_rays(const nerf_camera* cam, int H, int W, int crop_r0, int crop_c0, int crop_h,
+                                int crop_w, int64_t n_rays, int random, uint64_t seed, uint64_t offset,
+                                const float* d_image, int channels, float* d_rays_o, float* d_rays_d, float* d_target,
+                                int32_t* d_coords, void* stream) {
+    NERF_REQUIRE(cam && d_rays_o && d_rays_d, "sample_rays: null argument");
+    NERF_REQUIRE(H > 0 && W > 0 && crop_r0 >= 0 && crop_c0 >= 0 && crop_h > 0 && crop_w > 0 &&
+                 crop_r0 + crop_h <= H && crop_c0 + crop_w <= W, "sample_rays: crop window outside the %dx%d image", H, W);
+    const int64_t n_cells = (int64_t)crop_h * crop_w;
+    NERF_REQUIRE(n_rays >= 0 && n_rays <= n_cells, "sample_rays: %lld rays from %lld pixels (no replacement)",
+                 (long long)n_rays, (long long)n_cells);
+    NERF_REQUIRE(n_cells <= (int64_t(1) << 30), "sample_rays: crop window too large");
+    NERF_REQUIRE(!d_target || (d_image && channels >= 3), "sample_rays: target needs an image with >= 3 channels");
+    if (n_rays == 0) return NERF_OK;
+    int bits = 2;
+    while ((int64_t(1) << bits) < n_cells) bits += 2;   // even width: two halves of bits/2
+    uint64_t s = seed ^ (offset * 0xD1B54A32D192ED03ull);
+    const uint32_t k0 = splitmix(s), k1 = splitmix(s), k2 = splitmix(s), k3 = splitmix(s);
+    Cam c;
+    for (int k = 0; k < 12; ++k) c.c2w[k] = cam->c2w[k];
+    c.fx = cam->fx; c.fy = cam->fy; c.cx = cam->cx; c.cy = cam->cy;
+    hipLaunchKernelGGL(sample_rays_kernel, dim3(blocks_for(n_rays, 256)), dim3(256), 0, as_stream(stream), c, W,
+                       crop_r0, crop_c0, crop_w, n_cells, n_rays, random ? 1 : 0, bits / 2, k0, k1, k2, k3, d_image,
+                       channels, d_rays_o, d_rays_d, d_target, d_coords);
+    NERF_CHECK_LAUNCH("sample_rays");
+    return NERF_OK;
+}

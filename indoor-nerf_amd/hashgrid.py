@@ -4,8 +4,6 @@ API mirror of PocketNeRF/hash_encoding.py: HashEmbedder (:11-107) and SHEncoder 
 constructor arguments, attributes, parameters (`embeddings.{i}.weight`, nn.Embedding(2^log2T, 2))
 and return values. Forward and backward run in libnerfhip (csrc/hashgrid.hip, csrc/field.hip).
 """
-import ctypes
-
 import torch
 import torch.nn as nn
 
@@ -171,31 +169,32 @@ class HashEmbedder(nn.Module):
         return quant_records(qs, self.training)
 
     def train(self, mode=True):
-        self._packed = None
+        if self._packed is not None:
+            self._packed["key"] = None       # repack everything on the next eval-mode forward
         return super().train(mode)
 
     def packed_tables(self):
-        """Eval-mode int-packed tables (codes of round(B) bits per feature, csrc/quant.hip),
-        rebuilt when a table or a quantizer changed. Returns (buffer, code_bits, offsets, records)."""
+        """Eval-mode int-packed tables (csrc/quant.hip): (buffer, records). No host sync: the
+        records are computed on the device and a level is repacked only when its record changed
+        (checked on the device) or when a table changed (torch version counters; HIP kernels that
+        write tables in place bump them, see optim.RAdam)."""
         qs = list(self.quantizers)
         rec = quant_records(qs, False)
-        host = rec.cpu()                       # one sync (the reference .item()s every level's bits)
         tabs = self.tables()
-        key = (tuple((t.data_ptr(), t._version) for t in tabs), tuple(host.flatten().tolist()))
-        if self._packed is not None and self._packed[0] == key:
-            return self._packed[1]
-        n = self.n_levels
-        bits = (ctypes.c_int * n)(*[int(v) for v in host[:, 6].tolist()])
-        code_bits, offsets = (ctypes.c_int * n)(), (ctypes.c_int64 * n)()
-        total = _lib.load().nerf_quant_packed_layout(bits, n, self.log2_hashmap_size, code_bits, offsets)
-        if total == 0:
-            raise RuntimeError("HashEmbedder: nerf_quant_packed_layout rejected the level layout")
-        buf = torch.empty(int(total), dtype=torch.uint8, device=tabs[0].device)
+        key = tuple((t.data_ptr(), t._version) for t in tabs)
+        n, dev = self.n_levels, tabs[0].device
+        st = self._packed
+        if st is None or st["buf"].device != dev:
+            nbytes = int(_lib.load().nerf_quant_packed_bytes(n, self.log2_hashmap_size))
+            st = self._packed = dict(buf=torch.empty(nbytes, dtype=torch.uint8, device=dev),
+                                     prev=torch.full((n, 8), float("nan"), device=dev),
+                                     dirty=torch.empty(n, dtype=torch.int32, device=dev), key=None)
         _lib.call("nerf_quant_pack_tables", _lib.ptr_array(tabs), n, self.log2_hashmap_size, _lib.ptr(rec, "records"),
-                  code_bits, offsets, _lib.ptr(buf, "packed", dtype=torch.uint8), _lib.stream())
-        packed = (buf, code_bits, offsets, rec)
-        self._packed = (key, packed)
-        return packed
+                  _lib.ptr(st["prev"], "prev_records"), int(st["key"] != key),
+                  _lib.ptr(st["dirty"], "dirty", dtype=torch.int32), _lib.ptr(st["buf"], "packed", dtype=torch.uint8),
+                  _lib.stream())
+        st["key"] = key
+        return st["buf"], rec
 
     def encode_into(self, xyz, feat, sp, sl, keep):
         """Forward gather into caller-allocated feat/keep on the path this forward needs: plain,
@@ -203,9 +202,9 @@ class HashEmbedder(nn.Module):
         meta = self._meta
         P = xyz.shape[0]
         if self.quantization_active() and not self.training:
-            buf, code_bits, offsets, rec = self.packed_tables()
+            buf, rec = self.packed_tables()
             _lib.call("nerf_hash_encode_fwd_packed", _lib.ptr(xyz, "xyz"), P, meta["bmin"], meta["bmax"], meta["res"],
-                      self.n_levels, meta["log2_T"], _lib.ptr(buf, "packed", dtype=torch.uint8), code_bits, offsets,
+                      self.n_levels, meta["log2_T"], _lib.ptr(buf, "packed", dtype=torch.uint8),
                       _lib.ptr(rec, "records"), _lib.ptr(feat, "feat"), sp, sl,
                       _lib.ptr(keep, "keep", dtype=torch.bool), _lib.stream())
             return

@@ -15,11 +15,13 @@ from .hashgrid import HashEmbedder, SHEncoder
 from .losses import total_variation_all, train_loss
 from .optim import RAdam
 from .render import render
+from . import _lib
 
 DEFAULTS = dict(multires=10, i_embed=1, i_embed_views=2, multires_views=4, use_viewdirs=True, N_importance=0,
                 N_samples=64, netchunk=1024 * 64, finest_res=512, log2_hashmap_size=19, lrate=5e-4,
                 lrate_decay=250, perturb=1., white_bkgd=False, raw_noise_std=0., predict_normals=False,
-                use_quantization=False, quantization_bits=8, dataset_type="blender", no_ndc=False, lindisp=False,
+                use_quantization=False, quantization_bits=8, use_acaq=False, target_metric=None, bit_penalty=1e-3,
+                acaq_start_iter=1000, dataset_type="blender", no_ndc=False, lindisp=False,
                 basedir="./logs/", expname="", ft_path=None, no_reload=True, sparse_loss_weight=1e-10,
                 tv_loss_weight=1e-6, chunk=1024 * 32)
 
@@ -101,6 +103,51 @@ def save_checkpoint(path, global_step, render_kwargs_train, optimizer):
                 "optimizer_state_dict": optimizer.state_dict()}, path)
 
 
+def acaq_quantizers(render_kwargs_train):
+    """The quantizers the A-CAQ loop adjusts, in the reference's order (run_nerf.py:1184-1194): the
+    embedder's 16 levels, then the COARSE network's activation and weight quantizers."""
+    qs = []
+    emb, net = render_kwargs_train["embed_fn"], render_kwargs_train["network_fn"]
+    if getattr(emb, "quantizers", None) is not None:
+        qs.extend(emb.quantizers)
+    if getattr(net, "sigma_act_quantizers", None) is not None:
+        qs.extend(net.sigma_act_quantizers)
+    if getattr(net, "sigma_weight_quantizer", None) is not None:
+        qs.append(net.sigma_weight_quantizer)
+    return qs
+
+
+def acaq_update(i, img_loss, render_kwargs_train, args):
+    """A-CAQ bit-width controller of train() (run_nerf.py:1182-1250), after optimizer.step():
+    from acaq_start_iter, every 10th iteration each quantizer's soft_bits moves by a loss-driven
+    delta minus a bit penalty (csrc/quant.hip acaq_update_kernel; no host sync). The best img_loss
+    of the MDL mode (the reference's train.best_loss) lives on the device next to the embedder.
+    Returns the device report [target, loss_ratio] of an update, else None."""
+    get = lambda k, d=None: getattr(args, k, DEFAULTS.get(k, d))  # noqa: E731
+    if not (get("use_acaq", False) and get("use_quantization") and i >= get("acaq_start_iter", 1000)):
+        return None
+    if i % 10 != 0:
+        return None
+    qs = acaq_quantizers(render_kwargs_train)
+    if not qs:
+        return None
+    from .quantization import _descriptors
+    emb = render_kwargs_train["embed_fn"]
+    dev = img_loss.device
+    if getattr(emb, "_acaq_best", None) is None or emb._acaq_best.device != dev:
+        emb._acaq_best = torch.full((1,), float("nan"), dtype=torch.float64, device=dev)
+    report = torch.empty(2, dtype=torch.float64, device=dev)
+    tm = get("target_metric", None)
+    loss32 = img_loss.detach().reshape(()).float().contiguous()
+    _lib.call("nerf_acaq_update", _descriptors(qs), len(qs), _lib.ptr(loss32, "img_loss"),
+              _lib.ptr(emb._acaq_best, "best_loss", dtype=torch.float64), int(tm is not None),
+              float(tm) if tm is not None else 0.0, float(get("bit_penalty", 1e-3)),
+              _lib.ptr(report, "report", dtype=torch.float64), _lib.stream())
+    for q in qs:
+        torch.autograd.graph.increment_version(q.soft_bits)
+    return report
+
+
 def train_step(batch_rays, target_s, render_kwargs_train, optimizer, args, global_step, H=0, W=0, K=None,
                grad_hook=None, loss_scale_sparsity=1.0, tv_generator=None, zero_grad=None):
     """One iteration of train() without host bookkeeping: render (coarse+fine), img/img0 MSE,
@@ -116,7 +163,7 @@ def train_step(batch_rays, target_s, render_kwargs_train, optimizer, args, globa
     # run_nerf.py:1011-1037 (img2mse x2, sparsity, TV, mse2psnr) fused into one launch (csrc/loss.hip)
     tv_w = get("tv_loss_weight")
     tv = total_variation_all(render_kwargs_train["embed_fn"], generator=tv_generator) if tv_w > 0 else None
-    loss, _img_loss, psnr = train_loss(rgb, extras.get("rgb0"), target_s, extras.get("sparsity_loss"),
+    loss, img_loss, psnr = train_loss(rgb, extras.get("rgb0"), target_s, extras.get("sparsity_loss"),
                                        extras.get("sparsity_loss0"), tv, get("sparse_loss_weight") * loss_scale_sparsity,
                                        tv_w if tv_w > 0 else 0.0)
     if global_step > 1000:
@@ -125,6 +172,7 @@ def train_step(batch_rays, target_s, render_kwargs_train, optimizer, args, globa
     if grad_hook is not None:
         grad_hook()
     optimizer.step()
+    acaq_update(global_step, img_loss, render_kwargs_train, args)
     decay_steps = get("lrate_decay") * 1000
     new_lrate = get("lrate") * (0.1 ** (global_step / decay_steps))
     for g in optimizer.param_groups:

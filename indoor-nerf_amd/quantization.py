@@ -47,10 +47,23 @@ def _descriptor(q):
     return d
 
 
+_DESC_CACHE = {}
+
+
 def _descriptors(quantizers):
-    arr = (_lib.Quantizer * len(quantizers))()
-    for i, q in enumerate(quantizers):
-        arr[i] = _descriptor(q)
+    """ctypes array of nerf_quantizer for these modules, cached on the tensors' device addresses
+    (rebuilding 16 descriptors per forward was a measurable share of a render step's host time)."""
+    key = tuple((q.soft_bits.data_ptr(), q.range_scale.data_ptr(),
+                 q.v_max.data_ptr() if q.v_max is not None else 0, q.running_min.data_ptr(),
+                 q.running_max.data_ptr(), q.min_bits, q.max_bits) for q in quantizers)
+    arr = _DESC_CACHE.get(key)
+    if arr is None:
+        if len(_DESC_CACHE) > 64:
+            _DESC_CACHE.clear()
+        arr = (_lib.Quantizer * len(quantizers))()
+        for i, q in enumerate(quantizers):
+            arr[i] = _descriptor(q)
+        _DESC_CACHE[key] = arr
     return arr
 
 

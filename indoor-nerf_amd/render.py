@@ -205,14 +205,28 @@ def batchify_rays(rays_flat, chunk=1024 * 32, **kwargs):
     return {k: (v[0] if len(v) == 1 else torch.cat(v, 0)) for k, v in all_ret.items()}
 
 
-def get_rays(H, W, K, c2w):
-    """run_nerf_helpers.py:311-320 (host-side glue, once per image)."""
-    i, j = torch.meshgrid(torch.linspace(0, W - 1, W, device=c2w.device),
-                          torch.linspace(0, H - 1, H, device=c2w.device), indexing="ij")
-    i, j = i.t(), j.t()
-    dirs = torch.stack([(i - K[0][2]) / K[0][0], -(j - K[1][2]) / K[1][1], -torch.ones_like(i)], -1)
-    rays_d = torch.sum(dirs[..., None, :] * c2w[:3, :3], -1)
-    rays_o = c2w[:3, -1].expand(rays_d.shape)
+def camera(K, c2w):
+    """nerf_camera of a float64 (or float32) K and a [3,4] pose: the float32 values get_rays'
+    tensor ops see (run_nerf_helpers.py:311-320)."""
+    cam = _lib.Camera()
+    pose = torch.as_tensor(c2w, dtype=torch.float32).detach().cpu().reshape(-1, 4)[:3]
+    for k, v in enumerate(pose.reshape(-1).tolist()):
+        cam.c2w[k] = v
+    Kf = [[float(np.float32(float(K[r][c]))) for c in range(3)] for r in range(2)]
+    cam.fx, cam.fy, cam.cx, cam.cy = Kf[0][0], Kf[1][1], Kf[0][2], Kf[1][2]
+    return cam
+
+
+def get_rays(H, W, K, c2w, device=None):
+    """run_nerf_helpers.py:311-320 -> rays_o, rays_d [H, W, 3] on the device (csrc/rays.hip,
+    one launch; the pose is read on the host)."""
+    device = torch.device(device) if device is not None else (c2w.device if torch.is_tensor(c2w) else
+                                                               torch.device("cuda"))
+    H, W = int(H), int(W)
+    rays_o = torch.empty(H, W, 3, device=device, dtype=torch.float32)
+    rays_d = torch.empty(H, W, 3, device=device, dtype=torch.float32)
+    _lib.call("nerf_sample_rays", camera(K, c2w), H, W, 0, 0, H, W, H * W, 0, 0, 0, None, 0,
+              _lib.ptr(rays_o, "rays_o"), _lib.ptr(rays_d, "rays_d"), None, None, _lib.stream())
     return rays_o, rays_d
 
 

@@ -33,3 +33,38 @@ def blender_rays(n_rays, H=800, W=800, pose_index=3, seed=0):
 
 def blender_bbox():
     return (np.array(BLENDER_BBOX[0], np.float32), np.array(BLENDER_BBOX[1], np.float32))
+
+
+# Forward-facing LLFF rig (fern at factor 8: 504 x 378, SURVEY.md §8(d) "Fern: NDC, near 0 far 1"):
+# three cameras looking down -z with small yaw / translation (tests/golden/make_golden.py llff_rig).
+LLFF_HWF = (378, 504, 407.5)
+
+
+def llff_poses():
+    poses = []
+    for yaw, tx in ((-4.0, -0.08), (0.0, 0.0), (5.0, 0.1)):
+        a = np.deg2rad(yaw)
+        R = np.array([[np.cos(a), 0, np.sin(a)], [0, 1, 0], [-np.sin(a), 0, np.cos(a)]])
+        poses.append(np.concatenate([R, np.array([[tx], [0.02 * yaw], [0.0]])], 1))
+    return np.array(poses, np.float32)
+
+
+def llff_rays(n_rays, pose_index=1, seed=0):
+    """n_rays world-space rays of one LLFF camera (NDC conversion happens in render(ndc=True)).
+    Returns rays_o, rays_d [n,3] float32 and (H, W, K) with K float64 as train() builds it."""
+    H, W, focal = LLFF_HWF
+    K = np.array([[focal, 0, 0.5 * W], [0, focal, 0.5 * H], [0, 0, 1]])
+    c2w = llff_poses()[pose_index]
+    pix = np.random.RandomState(seed).permutation(H * W)[:n_rays]
+    i, j = (pix % W).astype(np.float32), (pix // W).astype(np.float32)
+    dirs = np.stack([(i - K[0][2]) / K[0][0], -(j - K[1][2]) / K[1][1], -np.ones_like(i)], -1).astype(np.float32)
+    rays_d = (dirs[:, None, :] * c2w[None, :3, :3]).sum(-1).astype(np.float32)
+    rays_o = np.broadcast_to(c2w[:3, 3], rays_d.shape).astype(np.float32).copy()
+    return rays_o, rays_d, (H, W, K)
+
+
+def llff_bbox():
+    """NDC box of the rig (scene.get_bbox3d_for_llff, utils.py:61-92)."""
+    from .scene import get_bbox3d_for_llff
+    lo, hi = get_bbox3d_for_llff(llff_poses(), LLFF_HWF, near=0.0, far=1.0)
+    return lo.numpy(), hi.numpy()

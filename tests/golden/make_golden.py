@@ -586,6 +586,90 @@ def gen_acaq(ref, out):
     np.savez_compressed(os.path.join(out, "f14_acaq.npz"), **d)
 
 
+def llff_rig():
+    """Synthetic forward-facing rig (fern at factor 8: 504 x 378): three cameras looking down -z
+    with small yaw / translation, LLFF-style recentred poses [3, 3, 4]."""
+    H, W, focal = 378, 504, 407.5
+    poses = []
+    for yaw, tx in ((-4.0, -0.08), (0.0, 0.0), (5.0, 0.1)):
+        a = np.deg2rad(yaw)
+        R = np.array([[np.cos(a), 0, np.sin(a)], [0, 1, 0], [-np.sin(a), 0, np.cos(a)]])
+        poses.append(np.concatenate([R, np.array([[tx], [0.02 * yaw], [0.0]])], 1))
+    return np.array(poses, np.float32), (H, W, focal)
+
+
+def gen_llff(ref, out):
+    """F15: the LLFF 'fern' configuration (configs/fern.txt): NDC rays (render(ndc=True),
+    run_nerf_helpers.py:333-350) in the NDC bbox of get_bbox3d_for_llff (utils.py:61-92),
+    near 0 / far 1, 64 + 64 samples, raw_noise_std 1 (pytest noise), no white background;
+    render + one backward."""
+    poses, (H, W, focal) = llff_rig()
+    bbox = ref.utils.get_bbox3d_for_llff(poses, (H, W, focal), near=0.0, far=1.0)
+    K = np.array([[focal, 0, 0.5 * W], [0, focal, 0.5 * H], [0, 0, 1]])     # float64, as train() builds it
+    table = closed_form_table(scale=0.3, salt=9)
+    emb = ref.he.HashEmbedder(bbox, n_levels=16, n_features_per_level=2, log2_hashmap_size=19,
+                              base_resolution=16, finest_resolution=512)
+    with torch.no_grad():
+        for i in range(16):
+            emb.embeddings[i].weight.copy_(torch.from_numpy(table[i]))
+    coarse, fine = make_mlp(ref, 40), make_mlp(ref, 41)
+    with torch.no_grad():
+        coarse.sigma_net[1].weight[0] *= 60.0
+        fine.sigma_net[1].weight[0] *= 60.0
+    rays_o, rays_d = ref.h.get_rays(H, W, K, torch.from_numpy(poses[1]))
+    pix = np.random.RandomState(17).permutation(H * W)[:64]
+    ro = rays_o.reshape(-1, 3)[pix].numpy().copy()
+    rd = rays_d.reshape(-1, 3)[pix].numpy().copy()
+    kw = build_render_kwargs(ref, emb, coarse, fine, 64, 64, 1.0, 1.0, False)
+    kw.update(white_bkgd=False, ndc=True, near=0.0, far=1.0)
+    rgb, depth, acc, extras = ref.rn.render(H, W, K, chunk=32768,
+                                            rays=(torch.from_numpy(ro), torch.from_numpy(rd)), retraw=True,
+                                            pytest=True, **kw)
+    target = np.random.RandomState(18).rand(64, 3).astype(np.float32)
+    loss = ref.h.img2mse(rgb, torch.from_numpy(target)) + ref.h.img2mse(extras["rgb0"], torch.from_numpy(target))
+    loss.backward()
+    d = dict(poses=poses, hwf=np.array([H, W, focal], np.float32), K=K, bbox_min=bbox[0].numpy(),
+             bbox_max=bbox[1].numpy(), rays_o=ro, rays_d=rd, target=target, loss=np.float32(loss.item()),
+             rgb=rgb.detach().numpy(), depth=depth.detach().numpy(), acc=acc.detach().numpy())
+    for k in ["rgb0", "depth0", "acc0", "z_std", "raw", "pts", "sparsity_loss", "sparsity_loss0"]:
+        d[k] = extras[k].detach().numpy()
+    d.update(mlp_arrays(coarse, "coarse_"))
+    d.update(mlp_arrays(fine, "fine_"))
+    for name, net in (("coarse", coarse), ("fine", fine)):
+        for k, p in net.named_parameters():
+            d[f"g{name}_" + k.replace(".", "_")] = p.grad.numpy().copy()
+    gs = []
+    for i in range(16):
+        g = emb.embeddings[i].weight.grad.double()
+        gs.append([g.sum().item(), (g * g).sum().item(), g.abs().sum().item()])
+    d["gtable_checksum"] = np.array(gs)
+    np.savez_compressed(os.path.join(out, "f15_llff.npz"), **d)
+
+
+def gen_rays(ref, out):
+    """F16: run_nerf_helpers.get_rays (:311-320) for whole small images — the per-pixel values the
+    device ray sampler must reproduce — with train()'s float64 K (run_nerf.py:797-802): a centred
+    Blender-style K and an off-centre anisotropic one (ScanNet-style intrinsics)."""
+    from tables import pose_spherical
+    d = {}
+    H, W = 60, 80
+    cases = {"a": (np.array([[111.1, 0, 0.5 * W], [0, 111.1, 0.5 * H], [0, 0, 1]]),
+                   pose_spherical(-112.0, -30.0, 4.0311)),
+             "b": (np.array([[95.25, 0, 37.3], [0, 97.5, 31.9], [0, 0, 1]]),
+                   pose_spherical(37.0, -12.0, 3.2))}
+    for tag, (K, c2w) in cases.items():
+        ro, rd = ref.h.get_rays(H, W, K, torch.from_numpy(c2w[:3, :4].copy()))
+        d[f"K_{tag}"], d[f"c2w_{tag}"] = K, c2w[:3, :4].copy()
+        d[f"rays_o_{tag}"], d[f"rays_d_{tag}"] = ro.numpy(), rd.numpy()
+    d["H"], d["W"] = np.int64(H), np.int64(W)
+    # precrop coordinate grid of train() (run_nerf.py:985-996) for precrop_frac 0.5
+    dH, dW = int(H // 2 * 0.5), int(W // 2 * 0.5)
+    coords = torch.stack(torch.meshgrid(torch.linspace(H // 2 - dH, H // 2 + dH - 1, 2 * dH),
+                                        torch.linspace(W // 2 - dW, W // 2 + dW - 1, 2 * dW)), -1)
+    d["crop_coords"] = torch.reshape(coords, [-1, 2]).long().numpy()
+    np.savez_compressed(os.path.join(out, "f16_rays.npz"), **d)
+
+
 def gen_tv(ref, out):
     table = closed_form_table(scale=0.05, salt=5)
     emb = make_embedder(ref, 1024, table)
@@ -630,7 +714,8 @@ def main(only=None):
     ref = load_reference()
     gens = [("voxel", None), ("hash", gen_hash), ("sh", gen_sh), ("mlp", gen_mlp), ("composite", gen_composite),
             ("pdf", gen_pdf), ("render", gen_render), ("quant", gen_quant), ("tv", gen_tv), ("train", gen_train),
-            ("normals", gen_normals), ("acaq", gen_acaq)]
+            ("normals", gen_normals), ("acaq", gen_acaq),
+            ("llff", gen_llff), ("rays", gen_rays)]
     if not only or "levels" in only or "voxel" in only:
         levels = gen_levels(ref, out)
         gen_voxel(ref, out, levels)

@@ -99,3 +99,15 @@ def test_hash_bwd_workspace_plan(nerf):
         assert lib.nerf_hash_encode_bwd_workspace_bytes(L, log2_T, P) == expect
     assert lib.nerf_hash_encode_bwd_workspace_bytes(16, 20, 1000) == 0
     assert lib.nerf_hash_encode_bwd_workspace_bytes(0, 19, 1000) == 0
+
+
+def test_crop_window_matches_reference_grid(golden):
+    """RaySampler's cell -> pixel map over the precrop window equals train()'s coords grid
+    (run_nerf.py:985-996), F16 (precrop_frac 0.5 on a 60 x 80 image); full image after precrop."""
+    from indoor_nerf_amd.rays import crop_window
+    g = golden("f16_rays")
+    H, W = int(g["H"]), int(g["W"])
+    r0, c0, h, w = crop_window(H, W, 3, precrop_iters=500, precrop_frac=0.5)
+    k = np.arange(h * w)
+    np.testing.assert_array_equal(np.stack([r0 + k // w, c0 + k % w], -1), g["crop_coords"])
+    assert crop_window(H, W, 500, precrop_iters=500) == (0, 0, H, W)

@@ -229,9 +229,17 @@ def test_packed_equals_fake_quant_full_size(nerf, gpu):
               _lib.stream())
     assert torch.equal(f_packed, f_fq)
     assert torch.equal(k_packed, k_fq)
-    # the packed tables are 4..16-bit codes except the >16-bit levels (fp32)
-    buf = emb._packed[1][0]
-    assert buf.numel() < 16 * (1 << 19) * 8 // 2
+    # a second eval forward after changing one level's bit width repacks that level only
+    with torch.no_grad():
+        emb.quantizers[3].soft_bits.fill_(11.0)
+        f2, _ = emb(x)
+    dirty = emb._packed["dirty"].cpu().numpy()
+    assert dirty.tolist() == [0, 0, 0, 1] + [0] * 12
+    rec2 = quant_records(list(emb.quantizers), False)
+    _lib.call("nerf_hash_encode_fwd_q", _lib.ptr(x), x.shape[0], m["bmin"], m["bmax"], m["res"], 16, 19,
+              _lib.ptr_array(emb.tables()), _lib.ptr(rec2), _lib.ptr(f_fq), 32, 2, _lib.ptr(k_fq, dtype=torch.bool),
+              _lib.stream())
+    assert torch.equal(f2, f_fq)
 
 
 def test_quantizer_module_vs_golden(nerf, gpu, golden):
@@ -250,3 +258,54 @@ def test_quantizer_module_vs_golden(nerf, gpu, golden):
     qs = nerf.LearnedBitwidthQuantizer(init_bits=8.0, symmetric=True).to(gpu)
     np.testing.assert_array_equal(qs(torch.from_numpy(g["sym_w"]).to(gpu)).detach().cpu().numpy(), g["sym_y"])
     assert q.integer_bit_width == 8 and q.get_quantization_params() == (0, 255)
+
+
+def _acaq_reference_step(bits, current_loss, state, target_metric, bit_penalty, min_bits=2.0, max_bits=32.0):
+    """run_nerf.py:1209-1250 restated with Python doubles on float32 soft_bits (the test's oracle)."""
+    if target_metric is not None:
+        target = target_metric
+    else:
+        state["best"] = current_loss if "best" not in state else min(state["best"], current_loss)
+        target = state["best"] * 1.2
+    out = []
+    n = len(bits)
+    for idx, b in enumerate(bits):
+        loss_ratio = current_loss / target
+        delta = -0.3 if loss_ratio < 0.95 else (-0.1 if loss_ratio < 1.05 else 0.2)
+        delta -= bit_penalty * float(b) / 8.0
+        delta *= 1.0 + (idx - n / 2) * 0.02
+        nb = np.float32(np.float32(b) + np.float32(delta))
+        out.append(np.float32(min(max(nb, np.float32(min_bits)), np.float32(max_bits))))
+    return out
+
+
+@pytest.mark.parametrize("target_metric", [None, 0.05])
+def test_acaq_controller_vs_reference_loop(nerf, gpu, target_metric):
+    """acaq_update (device) vs the reference's bit-width loop restated in Python: 18 quantizers
+    (16 levels + the coarse net's two), iterations 1000..1090, a loss sequence that visits all
+    three delta branches; soft_bits equal bit for bit, untouched off the 10-iteration grid."""
+    from types import SimpleNamespace
+    emb = nerf.HashEmbedder(_bbox_t(), use_quantization=True).to(gpu)
+    net = nerf.NeRFSmall(2, 64, 15, 3, 64, 32, 16, use_quantization=True).to(gpu)
+    kw = dict(embed_fn=emb, network_fn=net)
+    qs = nerf.acaq_quantizers(kw)
+    assert len(qs) == 18
+    rng = np.random.RandomState(3)
+    with torch.no_grad():
+        for q in qs:
+            q.soft_bits.fill_(float(np.float32(rng.uniform(3, 12))))
+    args = SimpleNamespace(use_acaq=True, use_quantization=True, acaq_start_iter=1000, target_metric=target_metric,
+                           bit_penalty=1e-3)
+    bits = [np.float32(float(q.soft_bits)) for q in qs]
+    state = {}
+    losses = [0.06, 0.05, 0.045, 0.08, 0.03, 0.052, 0.07, 0.02, 0.05, 0.09, 0.051]
+    for k, loss in enumerate(losses):
+        i = 1000 + 5 * k
+        lt = torch.tensor(np.float32(loss), device=gpu)
+        nerf.acaq_update(i, lt, kw, args)
+        if i % 10 == 0:
+            bits = _acaq_reference_step(bits, float(np.float32(loss)), state, target_metric, 1e-3)
+        got = [np.float32(float(q.soft_bits)) for q in qs]
+        np.testing.assert_array_equal(np.array(got), np.array(bits), err_msg=f"iteration {i}")
+    nerf.acaq_update(999, torch.tensor(0.5, device=gpu), kw, args)     # before acaq_start_iter: no-op
+    np.testing.assert_array_equal(np.array([np.float32(float(q.soft_bits)) for q in qs]), np.array(bits))

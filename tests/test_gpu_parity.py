@@ -534,3 +534,96 @@ def test_mlp_bwd_geo_gradient_superposition(nerf, gpu):
         torch.testing.assert_close(f1, f2, rtol=1e-4, atol=1e-5)
         for p, q in zip(w1, w2):
             torch.testing.assert_close(p, q, rtol=1e-4, atol=1e-4)
+
+
+def test_llff_ndc_render_and_grads(nerf, gpu, golden):
+    """Config 3 (LLFF fern): render(ndc=True) with the NDC bbox, near 0 / far 1, 64 + 64 samples,
+    raw_noise_std 1 (pytest draws), no white background, + one backward (F15). Coarse pass at fp32
+    rounding; fine pass PSNR-equivalent (sample_pdf, as test_render_end_to_end)."""
+    g = golden("f15_llff")
+    H, W, focal = int(g["hwf"][0]), int(g["hwf"][1]), float(g["hwf"][2])
+    bbox = (torch.from_numpy(g["bbox_min"]), torch.from_numpy(g["bbox_max"]))
+    emb = nerf.HashEmbedder(bbox, finest_resolution=512).to(gpu)
+    table = closed_form_table(scale=0.3, salt=9)
+    with torch.no_grad():
+        for i, e in enumerate(emb.embeddings):
+            e.weight.copy_(torch.from_numpy(table[i]))
+    coarse, fine = _mlp(nerf, gpu, g, "coarse_"), _mlp(nerf, gpu, g, "fine_")
+    sh = nerf.SHEncoder()
+    nqf = lambda inputs, viewdirs, fn: nerf.run_network(inputs, viewdirs, fn, emb, sh)  # noqa: E731
+    kw = dict(network_query_fn=nqf, perturb=1.0, N_importance=64, network_fine=fine, N_samples=64, network_fn=coarse,
+              embed_fn=emb, use_viewdirs=True, white_bkgd=False, raw_noise_std=1.0, predict_normals=False, ndc=True,
+              lindisp=False, near=0.0, far=1.0)
+    ro, rd = (torch.from_numpy(g[k]).to(gpu) for k in ("rays_o", "rays_d"))
+    rgb, depth, acc, ex = nerf.render(H, W, g["K"], rays=(ro, rd), retraw=True, pytest=True, **kw)
+    for k in ("rgb0", "depth0", "acc0", "sparsity_loss0"):
+        np.testing.assert_allclose(ex[k].detach().cpu().numpy(), g[k], rtol=1e-4, atol=1e-4, err_msg=k)
+    np.testing.assert_allclose(rgb.detach().cpu().numpy(), g["rgb"], rtol=0, atol=1e-3)
+    np.testing.assert_allclose(acc.detach().cpu().numpy(), g["acc"], rtol=0, atol=1e-3)
+    np.testing.assert_allclose(depth.detach().cpu().numpy(), g["depth"], rtol=1e-3, atol=1e-3)
+    np.testing.assert_allclose(ex["z_std"].detach().cpu().numpy(), g["z_std"], rtol=1e-3, atol=1e-3)
+    target = torch.from_numpy(g["target"]).to(gpu)
+    loss = nerf.img2mse(rgb, target) + nerf.img2mse(ex["rgb0"], target)
+    loss.backward()
+    np.testing.assert_allclose(loss.item(), float(g["loss"]), rtol=1e-3)
+    for prefix, net in (("gcoarse_", coarse), ("gfine_", fine)):
+        for k, p in net.named_parameters():
+            want = g[prefix + k.replace(".", "_")]
+            rel = np.linalg.norm(p.grad.cpu().numpy() - want) / np.linalg.norm(want)
+            assert rel < 2e-2, f"{prefix}{k}: relative grad error {rel:.2e}"
+    for i, e in enumerate(emb.embeddings):
+        gd = e.weight.grad.double()
+        np.testing.assert_allclose([(gd * gd).sum().item(), gd.abs().sum().item()], g["gtable_checksum"][i][1:],
+                                   rtol=2e-2, err_msg=f"level {i}")
+
+
+def test_get_rays_vs_reference(nerf, gpu, golden):
+    """Device get_rays (csrc/rays.hip) vs run_nerf_helpers.get_rays (F16) with train()'s float64 K:
+    a centred and an off-centre anisotropic camera, every pixel of a 60 x 80 image; bit-exact."""
+    g = golden("f16_rays")
+    H, W = int(g["H"]), int(g["W"])
+    for tag in ("a", "b"):
+        ro, rd = nerf.get_rays(H, W, g[f"K_{tag}"], torch.from_numpy(g[f"c2w_{tag}"]).to(gpu))
+        np.testing.assert_array_equal(ro.cpu().numpy(), g[f"rays_o_{tag}"])
+        np.testing.assert_array_equal(rd.cpu().numpy(), g[f"rays_d_{tag}"])
+
+
+def test_ray_sampler_batches(nerf, gpu, golden):
+    """RaySampler (train()'s no_batching batch, run_nerf.py:973-1004): N_rand distinct pixels,
+    inside the precrop window before precrop_iters, rays equal to get_rays at those pixels and
+    targets equal to the image there; over many draws every pixel is drawn about equally often."""
+    g = golden("f16_rays")
+    H, W = int(g["H"]), int(g["W"])
+    rng = np.random.RandomState(0)
+    images = rng.rand(2, H, W, 4).astype(np.float32)
+    poses = np.stack([g["c2w_a"], g["c2w_b"]])
+    K = g["K_a"]
+    sampler = nerf.RaySampler(images, poses, H, W, K, i_train=[0, 1], N_rand=1024, precrop_iters=10,
+                              precrop_frac=0.5, device=gpu)
+    for it, img_i in ((3, 0), (20, 1)):
+        rays, target, coords = sampler.sample(it, img_i=img_i, return_coords=True)
+        c = coords.cpu().numpy()
+        flat = c[:, 0] * W + c[:, 1]
+        assert len(np.unique(flat)) == 1024, "pixels must be drawn without replacement"
+        r0, c0, h, w = nerf.crop_window(H, W, it, 10, 0.5)
+        assert c[:, 0].min() >= r0 and c[:, 0].max() < r0 + h and c[:, 1].min() >= c0 and c[:, 1].max() < c0 + w
+        tag = "a" if img_i == 0 else "b"
+        Kt = g[f"K_{tag}"] if img_i == 1 else K
+        if img_i == 1:
+            sampler.K = Kt
+            sampler._cams.clear()
+            rays, target, coords = sampler.sample(it, img_i=img_i, return_coords=True, seed=5)
+            c = coords.cpu().numpy()
+        np.testing.assert_array_equal(rays[0].cpu().numpy(), g[f"rays_o_{tag}"][c[:, 0], c[:, 1]])
+        np.testing.assert_array_equal(rays[1].cpu().numpy(), g[f"rays_d_{tag}"][c[:, 0], c[:, 1]])
+        np.testing.assert_array_equal(target.cpu().numpy(), images[img_i][c[:, 0], c[:, 1], :3])
+    # uniformity: 300 draws of 1024 of the 4800 pixels -> 64 expected hits per pixel
+    counts = np.zeros(H * W)
+    for s in range(300):
+        _, _, coords = sampler.sample(100 + s, img_i=0, seed=1000 + s, return_coords=True)
+        c = coords.cpu().numpy()
+        counts += np.bincount(c[:, 0] * W + c[:, 1], minlength=H * W)
+    expect = 300 * 1024 / (H * W)
+    z = (counts - expect) / np.sqrt(expect)
+    assert abs(counts.sum() - 300 * 1024) < 1e-6
+    assert np.abs(z).max() < 6.0 and abs(z.mean()) < 0.1 and 0.7 < z.std() < 1.3, (z.min(), z.max(), z.std())
