@@ -53,7 +53,7 @@ KERNEL_SYMBOLS = {
     "nerf_mlp_fwd": ["nerf::mlp_fwd_frag_kernel<false>"],
     "nerf_mlp_bwd": ["nerf::mlp_bwd_frag_kernel<false>"],
 }
-TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r01_traffic.json")
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r01d_traffic.json")
 
 
 def base_name(abi_name):
@@ -271,7 +271,7 @@ def main():
                             "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
                             "per_launch_units": units, "algorithmic_flops_per_unit": per_unit}
             if traffic is not None:
-                roofline["traffic_source"] = ("profiles/r01_traffic.json: rocprofv3 FETCH_SIZE (x2, gfx950 wide-read "
+                roofline["traffic_source"] = ("profiles/r01d_traffic.json: rocprofv3 FETCH_SIZE (x2, gfx950 wide-read "
                                               "correction) + WRITE_SIZE per call, separate PMC passes of this bench")
         else:
             roofline = {"kernel": dom, "bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
