@@ -91,6 +91,59 @@ __global__ void __launch_bounds__(256) hash_encode_fwd_kernel(
     }
 }
 
+// Lane-pair forward: lanes 2m and 2m+1 share point m of the wave and gather the x = 0 and x = 1
+// corners of its voxel. Corners (x,y,z) and (x+1,y,z) hash to h and h ^ (x ^ (x+1)), the same 64-B
+// line for 15 of 16 x, so each gather instruction touches ~32 lines instead of 64 (the vector
+// memory path processes a wave instruction's distinct lines one after another). The x blend
+// c_jk = e(0,j,k)(1-wx) + e(1,j,k)wx becomes a + partner's b (IEEE addition commutes: bit-exact).
+template <bool QUANT>
+__global__ void __launch_bounds__(256) hash_encode_fwd_pair_kernel(
+    const float* __restrict__ xyz, int64_t n, HashParams hp,
+    float* __restrict__ feat, int64_t sp, int64_t sl, uint8_t* __restrict__ keep,
+    const QuantRec* __restrict__ qrec) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t p = t >> 1;
+    const int xb = (int)(t & 1);
+    const int lvl = blockIdx.y;
+    const bool valid = p < n;
+    const int64_t pc = valid ? p : n - 1;             // invalid lanes mirror a valid point (no stores)
+    const float x = xyz[3 * pc + 0], y = xyz[3 * pc + 1], z = xyz[3 * pc + 2];
+    const AxisCell ax = axis_cell(x, hp.bmin[0], hp.bmax[0], hp.cell[lvl][0]);
+    const AxisCell ay = axis_cell(y, hp.bmin[1], hp.bmax[1], hp.cell[lvl][1]);
+    const AxisCell az = axis_cell(z, hp.bmin[2], hp.bmax[2], hp.cell[lvl][2]);
+    const float2* __restrict__ tab = reinterpret_cast<const float2*>(hp.tables[lvl]);
+    const uint32_t bx = (uint32_t)ax.base + (uint32_t)xb, by = (uint32_t)ay.base, bz = (uint32_t)az.base;
+    float2 e[4];   // corners (xb, j, k), index 2j + k
+#pragma unroll
+    for (int c = 0; c < 4; ++c) e[c] = tab[spatial_hash3(bx, by + ((c >> 1) & 1), bz + (c & 1), hp.mask)];
+    if constexpr (QUANT) {
+        const QuantRec q = qrec[lvl];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            e[c].x = fake_quant(e[c].x, q);
+            e[c].y = fake_quant(e[c].y, q);
+        }
+    }
+    const float wx = ax.w, wy = ay.w, wz = az.w;
+    const float fx = xb ? wx : 1.0f - wx;
+    float cx[4], cy[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const float ax_ = e[c].x * fx, ay_ = e[c].y * fx;
+        cx[c] = ax_ + __shfl_xor(ax_, 1, 64);
+        cy[c] = ay_ + __shfl_xor(ay_, 1, 64);
+    }
+    const float oy = 1.0f - wy, oz = 1.0f - wz;
+    // c00 = cx[0], c01 = cx[1], c10 = cx[2], c11 = cx[3]
+    const float c0x = cx[0] * oy + cx[2] * wy, c1x = cx[1] * oy + cx[3] * wy;
+    const float c0y = cy[0] * oy + cy[2] * wy, c1y = cy[1] * oy + cy[3] * wy;
+    const float ox_ = c0x * oz + c1x * wz, oy_ = c0y * oz + c1y * wz;
+    if (!valid) return;
+    if (lvl == 0 && keep && xb == 0) keep[p] = (ax.inside && ay.inside && az.inside) ? 1 : 0;
+    float* dst = feat + p * sp + (int64_t)lvl * sl;
+    dst[xb] = xb ? oy_ : ox_;
+}
+
 // Backward: dL/de_c = ((g*(1-wz or wz))*(1-wy or wy))*(1-wx or wx), the order autograd applies the
 // three blend steps in reverse; scatter-added with fp32 atomics (no-return global_atomic_add_f32).
 // Consecutive threads are consecutive samples of one ray: at coarse levels they usually share the
@@ -415,6 +468,12 @@ static int bwd_mode() {
     return 3;
 }
 
+// NERF_HASH_FWD=0 selects the one-point-per-lane forward (A/B measurements); default: lane pairs.
+static bool fwd_pair() {
+    const char* e = getenv("NERF_HASH_FWD");
+    return !(e && e[0] == '0');
+}
+
 }  // namespace nerf
 
 using namespace nerf;
@@ -437,8 +496,19 @@ extern "C" int nerf_hash_encode_fwd_q(const float* d_xyz, int64_t n_points, cons
     for (int a = 0; a < 3; ++a) { hp.bmin[a] = bbox_min3[a]; hp.bmax[a] = bbox_max3[a]; }
     fill_cells(hp.cell, bbox_min3, bbox_max3, level_res, n_levels);
     hp.mask = (uint32_t)((1u << log2_T) - 1u);
-    dim3 grid(blocks_for(n_points, 256), n_levels);
     const QuantRec* q = reinterpret_cast<const QuantRec*>(d_qrec);
+    if (fwd_pair()) {
+        dim3 grid2(blocks_for(2 * n_points, 256), n_levels);
+        if (q)
+            hipLaunchKernelGGL(hash_encode_fwd_pair_kernel<true>, grid2, dim3(256), 0, as_stream(stream), d_xyz,
+                               n_points, hp, d_feat, feat_stride_point, feat_stride_level, d_keep, q);
+        else
+            hipLaunchKernelGGL(hash_encode_fwd_pair_kernel<false>, grid2, dim3(256), 0, as_stream(stream), d_xyz,
+                               n_points, hp, d_feat, feat_stride_point, feat_stride_level, d_keep, q);
+        NERF_CHECK_LAUNCH("hash_encode_fwd");
+        return NERF_OK;
+    }
+    dim3 grid(blocks_for(n_points, 256), n_levels);
     if (q)
         hipLaunchKernelGGL(hash_encode_fwd_kernel<true>, grid, dim3(256), 0, as_stream(stream), d_xyz, n_points, hp,
                            d_feat, feat_stride_point, feat_stride_level, d_keep, q);
