@@ -86,6 +86,8 @@ def parse():
     ap.add_argument("--workload", default="lego", choices=sorted(WORKLOADS),
                     help="BASELINE config: lego (configs[1], the headline), fern (configs[2], LLFF NDC), "
                          "acaq (configs[4], A-CAQ quantized tables)")
+    ap.add_argument("--graph", type=int, default=1,
+                    help="train mode: replay the iteration from HIP graphs (graphs.GraphedTrainStep); 0 = eager")
     ap.add_argument("--mode", default="train", choices=["train", "render"],
                     help="train: full training iteration (the metric); render: render-only (eval modules, no grad)")
     return ap.parse_args()
@@ -196,7 +198,13 @@ def main():
     tv_gen = torch.Generator().manual_seed(7)       # same TV cuboids on every rank
     hook = (lambda: arena.allreduce_mean()) if world > 1 else None
 
-    if a.mode == "train":
+    gstep = None
+    if a.mode == "train" and a.graph:
+        from indoor_nerf_amd.graphs import GraphedTrainStep
+        gstep = GraphedTrainStep(rays, target, kw, opt, args, H=H, W=W, K=K, grad_hook=hook,
+                                 loss_scale_sparsity=float(world), tv_generator=tv_gen, zero_grad=arena.zero_)
+        step = gstep
+    elif a.mode == "train":
         def step(i):
             return nerf.train_step(rays, target, kw, opt, args, i, H=H, W=W, K=K, grad_hook=hook,
                                    loss_scale_sparsity=float(world), tv_generator=tv_gen, zero_grad=arena.zero_)
@@ -224,7 +232,7 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
-    if a.profile_kernels:
+    if a.profile_kernels and gstep is None:
         _lib.set_timing(True)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -242,8 +250,18 @@ def main():
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # per-kernel timing from the timed region
+    # per-kernel timing: eager -> HIP-event pairs around every launch of the timed region. graph ->
+    # torch on ROCm cannot capture timing events, so K further iterations of the same launches run
+    # eagerly right after the timed region with the event pairs (same kernels, inputs and state)
     per = {}
+    if gstep is not None and a.profile_kernels:
+        _lib.set_timing(True)
+        for _ in range(a.steps):
+            gstep.eager_step(it)
+            it += 1
+        torch.cuda.synchronize()
+        recs = _lib.timing_records()
+        _lib.set_timing(False)
     for name, e0, e1 in recs:
         per.setdefault(name, []).append(e0.elapsed_time(e1) * 1e-3)
     kernels = {}
@@ -295,6 +313,7 @@ def main():
         "config": {"workload": wl["desc"].format(R=a.rays) + ("" if a.mode == "train" else " [render only]"),
                    "name": a.workload, "rays_per_gpu": a.rays, "global_batch": a.rays * world,
                    "samples": f"{wl['args']['N_samples']}+{wl['args']['N_importance']}", "parallelism": f"dp{world}"},
+        "hip_graph": bool(gstep is not None and gstep.captures > 0),
         "loss": round(float(loss), 6),
         "roofline": roofline,
         "kernels": {k: {kk: round(vv, 4) if isinstance(vv, float) else vv for kk, vv in v.items()}

@@ -14,6 +14,10 @@
  *   - Return 0 on success, else a NERF_E_* code; nerf_last_error() gives the message (per thread).
  *   - Random draws: a NULL d_u* argument means "draw in-kernel" from Philox4x32-10 keyed by
  *     (seed, offset); a non-NULL one supplies the uniforms (the reference's pytest=True path).
+ *     A non-NULL d_rng (device uint64[2]) overrides (seed, offset) — used when a whole training
+ *     step is captured in a HIP graph and every replay must draw new numbers.
+ *   - Likewise nerf_tv_* take the cuboid corners from d_min_vertex (device int64[L][3]) and
+ *     nerf_radam_step its per-step scalars from d_coef (device float[n][4]) when non-NULL.
  */
 #ifndef NERF_HIP_H
 #define NERF_HIP_H
@@ -198,13 +202,15 @@ int nerf_composite_bwd(const float* d_raw, int raw_channels, const float* d_z, c
  */
 int nerf_sample_stratified(const float* d_rays, int64_t ray_stride, int64_t n_rays, int n_samples,
                            const float* d_t, int lindisp, int perturb, const float* d_u,
-                           uint64_t seed, uint64_t offset, float* d_z, float* d_pts, void* stream);
+                           uint64_t seed, uint64_t offset, const uint64_t* d_rng,
+                           float* d_z, float* d_pts, void* stream);
 
 /* sample_pdf (run_nerf_helpers.py:354-397) on bins [R,n_bins], weights [R,n_bins-1];
  * det: u = d_t_imp (torch.linspace(0,1,N) values, [N]); else u = d_u [R,N] or Philox. */
 int nerf_sample_pdf(const float* d_bins, int64_t bins_stride, const float* d_weights, int64_t weights_stride,
                     int64_t n_rays, int n_bins, int n_importance, int det, const float* d_t_imp,
-                    const float* d_u, uint64_t seed, uint64_t offset, float* d_samples, void* stream);
+                    const float* d_u, uint64_t seed, uint64_t offset, const uint64_t* d_rng,
+                    float* d_samples, void* stream);
 
 /* Hierarchical step of render_rays (run_nerf.py:508-513, :541) in one launch: z_mid of the
  * coarse z, sample_pdf on weights[...,1:-1], sort(cat(z, z_samples)), fine points, z_std.
@@ -212,7 +218,7 @@ int nerf_sample_pdf(const float* d_bins, int64_t bins_stride, const float* d_wei
  * d_samples [R,N] (may be NULL). */
 int nerf_sample_fine(const float* d_rays, int64_t ray_stride, const float* d_z, const float* d_weights,
                      int64_t n_rays, int n_samples, int n_importance, int det, const float* d_t_imp,
-                     const float* d_u, uint64_t seed, uint64_t offset,
+                     const float* d_u, uint64_t seed, uint64_t offset, const uint64_t* d_rng,
                      float* d_z_fine, float* d_pts_fine, float* d_z_std, float* d_samples, void* stream);
 
 /* ---- rays of the training batch / of a whole image (run_nerf.py:973-1004, run_nerf_helpers.py:311-320)
@@ -235,6 +241,13 @@ int nerf_sample_rays(const nerf_camera* cam, int H, int W, int crop_r0, int crop
                      const float* d_image, int channels, float* d_rays_o, float* d_rays_d, float* d_target,
                      int32_t* d_coords, void* stream);
 
+/* render()'s ray batch (run_nerf.py:115-140): viewdir = d/|d| of the world direction, optional
+ * ndc_rays with near plane 1 (run_nerf_helpers.py:333-350; ndc_coef_w/h = float32 of
+ * -1/(W/(2 focal)) and -1/(H/(2 focal))), then [o(3), d(3), near, far, viewdir(3)] per ray
+ * (8 floats without viewdirs). d_rays_o/d [n,3]; d_out [n, 11 | 8]. */
+int nerf_rays_pack(const float* d_rays_o, const float* d_rays_d, int64_t n_rays, float near, float far,
+                   int ndc, float ndc_coef_w, float ndc_coef_h, int use_viewdirs, float* d_out, void* stream);
+
 /* ---- RAdam (PocketNeRF/radam.py:28-94), one launch over up to 32 tensor segments ----------
  * Per segment: p, g, m (exp_avg), v (exp_avg_sq) of n elements. The host evaluates the scalar
  * algebra of radam.py:56-79 in double, exactly as the reference's Python does, and passes the
@@ -245,6 +258,8 @@ int nerf_sample_rays(const nerf_camera* cam, int H, int W, int crop_r0, int crop
  *   step_coef               float(-step_size*lr)
  *   mode 2: N_sma >= 5 (p += step_coef*m/(sqrt(v)+eps)), 1: step_size > 0 (p += step_coef*m),
  *   0: moments only.
+ * d_coef (may be NULL): device [n_segs][4] = (decay_coef, step_coef, mode, 0) overriding the
+ * by-value ones (a step captured in a HIP graph reads this step's scalars from memory).
  */
 typedef struct {
     float* p;
@@ -256,17 +271,17 @@ typedef struct {
     int mode;
 } nerf_radam_segment;
 
-int nerf_radam_step(const nerf_radam_segment* segs, int n_segs, void* stream);
+int nerf_radam_step(const nerf_radam_segment* segs, int n_segs, const float* d_coef, void* stream);
 
 /* ---- total-variation loss on one hashed cuboid per level (loss.py:11-43) ------------------
  * min_vertex: host int64[n_levels][3] (the reference draws it with torch.randint);
  * cube: host int[n_levels] cuboid edge. fwd: d_loss[l] += TV_l (ACCUMULATED; zero it first).
  * bwd: d_dtables[l] += d(scale_l * TV_l)/d table, scale: host float[n_levels]. */
 int nerf_tv_fwd(const float* const* d_tables, int n_levels, int log2_T, const int64_t* min_vertex,
-                const int* cube, float* d_loss, void* stream);
+                const int64_t* d_min_vertex, const int* cube, float* d_loss, void* stream);
 int nerf_tv_bwd(const float* const* d_tables, int n_levels, int log2_T, const int64_t* min_vertex,
-                const int* cube, const float* d_scale /* device [n_levels] */, float* const* d_dtables,
-                void* stream);
+                const int64_t* d_min_vertex, const int* cube, const float* d_scale /* device [n_levels] */,
+                float* const* d_dtables, void* stream);
 
 /* ---- training-loss head (run_nerf.py:1011-1037: img2mse of both passes, sparsity, TV, mse2psnr) ----
  * fwd: device scalars loss, img_loss (fine-pass MSE), psnr; rgb0 / sparsity / sparsity0 / tv may be NULL.

@@ -77,15 +77,20 @@ SIGNATURES = {
                            c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
     "nerf_composite_bwd": [c_vp, c_int, c_vp, c_vp, c_vp, c_i64, c_int, c_int,
                            c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
-    "nerf_sample_stratified": [c_vp, c_i64, c_i64, c_int, c_vp, c_int, c_int, c_vp, c_u64, c_u64, c_vp, c_vp, c_vp],
-    "nerf_sample_pdf": [c_vp, c_i64, c_vp, c_i64, c_i64, c_int, c_int, c_int, c_vp, c_vp, c_u64, c_u64, c_vp, c_vp],
-    "nerf_sample_fine": [c_vp, c_i64, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_vp, c_vp, c_u64, c_u64,
+    "nerf_sample_stratified": [c_vp, c_i64, c_i64, c_int, c_vp, c_int, c_int, c_vp, c_u64, c_u64, c_vp, c_vp, c_vp,
+                               c_vp],
+    "nerf_sample_pdf": [c_vp, c_i64, c_vp, c_i64, c_i64, c_int, c_int, c_int, c_vp, c_vp, c_u64, c_u64, c_vp, c_vp,
+                        c_vp],
+    "nerf_sample_fine": [c_vp, c_i64, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_vp, c_vp, c_u64, c_u64, c_vp,
                          c_vp, c_vp, c_vp, c_vp, c_vp],
     "nerf_sample_rays": [ctypes.POINTER(Camera), c_int, c_int, c_int, c_int, c_int, c_int, c_i64, c_int, c_u64,
                          c_u64, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp],
-    "nerf_radam_step": [ctypes.POINTER(RAdamSegment), c_int, c_vp],
-    "nerf_tv_fwd": [ctypes.POINTER(c_vp), c_int, c_int, ctypes.POINTER(c_i64), ctypes.POINTER(c_int), c_vp, c_vp],
-    "nerf_tv_bwd": [ctypes.POINTER(c_vp), c_int, c_int, ctypes.POINTER(c_i64), ctypes.POINTER(c_int), c_vp,
+    "nerf_rays_pack": [c_vp, c_vp, c_i64, ctypes.c_float, ctypes.c_float, c_int, ctypes.c_float, ctypes.c_float,
+                       c_int, c_vp, c_vp],
+    "nerf_radam_step": [ctypes.POINTER(RAdamSegment), c_int, c_vp, c_vp],
+    "nerf_tv_fwd": [ctypes.POINTER(c_vp), c_int, c_int, ctypes.POINTER(c_i64), c_vp, ctypes.POINTER(c_int), c_vp,
+                    c_vp],
+    "nerf_tv_bwd": [ctypes.POINTER(c_vp), c_int, c_int, ctypes.POINTER(c_i64), c_vp, ctypes.POINTER(c_int), c_vp,
                     ctypes.POINTER(c_vp), c_vp],
     "nerf_train_loss_fwd": [c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, ctypes.c_float, c_vp, c_int, ctypes.c_float,
                             c_vp, c_vp, c_vp, c_vp],
@@ -146,6 +151,10 @@ def set_timing(enabled):
     _TIMING = [] if enabled else None
 
 
+def timing_enabled():
+    return _TIMING is not None
+
+
 def timing_records():
     return _TIMING or []
 
@@ -153,6 +162,9 @@ def timing_records():
 def call(name, *args):
     lib = load()
     if _TIMING is not None:
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("kernel timing cannot be recorded inside a HIP-graph capture (torch on ROCm "
+                               "refuses external events); time an eager step instead")
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ev0.record()
         rc = getattr(lib, name)(*args)

@@ -10,6 +10,7 @@ constexpr int kRAdamThreads = 256;
 
 struct RAdamSegs {
     nerf_radam_segment seg[kMaxSegs];
+    const float* coef;   // optional device [n][4] = (decay_coef, step_coef, mode, 0) of this step
     int64_t block_start[kMaxSegs + 1];   // first block of each segment
     int n;
 };
@@ -32,7 +33,12 @@ __global__ void __launch_bounds__(kRAdamThreads) radam_kernel(RAdamSegs S) {
     const int64_t b = blockIdx.x;
     int si = 0;
     while (si + 1 < S.n && b >= S.block_start[si + 1]) ++si;
-    const nerf_radam_segment& s = S.seg[si];
+    nerf_radam_segment s = S.seg[si];
+    if (S.coef) {   // per-step scalars from device memory (graph replays)
+        s.decay_coef = S.coef[4 * si];
+        s.step_coef = S.coef[4 * si + 1];
+        s.mode = (int)S.coef[4 * si + 2];
+    }
     const int64_t i0 = ((b - S.block_start[si]) * kRAdamThreads + threadIdx.x) * kRAdamVec;
     if (i0 >= s.n) return;
     const bool aligned = ((reinterpret_cast<uintptr_t>(s.p) | reinterpret_cast<uintptr_t>(s.g) |
@@ -69,6 +75,7 @@ struct TVParams {
     int64_t vstart[NERF_MAX_LEVELS + 1];   // first vertex of each level in the flattened launch
     int L;
     uint32_t mask;
+    const int64_t* dmv;   // optional device [L][3] cuboid corners (graph replays draw new ones)
     const float* scale;   // bwd: device [L] upstream gradient per level
     float* loss;          // fwd: device [L]
 };
@@ -95,7 +102,13 @@ __global__ void __launch_bounds__(256) tv_fwd_kernel(TVParams P) {
     const int c = P.cube[l], n1 = c + 1;
     const uint32_t nv = (uint32_t)(P.vstart[l + 1] - P.vstart[l]);
     const float2* tab = reinterpret_cast<const float2*>(P.tables[l]);
-    const int* mv = P.mv[l];
+    int mvd[3];
+    if (P.dmv) {
+        mvd[0] = (int)P.dmv[3 * l]; mvd[1] = (int)P.dmv[3 * l + 1]; mvd[2] = (int)P.dmv[3 * l + 2];
+    } else {
+        mvd[0] = P.mv[l][0]; mvd[1] = P.mv[l][1]; mvd[2] = P.mv[l][2];
+    }
+    const int* mv = mvd;
     float part = 0.f;
     for (uint32_t lv = blockIdx.x * 256u + threadIdx.x; lv < nv; lv += gridDim.x * 256u) {
         int i, j, k;
@@ -122,7 +135,13 @@ __global__ void __launch_bounds__(256) tv_bwd_kernel(TVParams P) {
     const int c = P.cube[l], n1 = c + 1;
     const uint32_t nv = (uint32_t)(P.vstart[l + 1] - P.vstart[l]);
     const float2* tab = reinterpret_cast<const float2*>(P.tables[l]);
-    const int* mv = P.mv[l];
+    int mvd[3];
+    if (P.dmv) {
+        mvd[0] = (int)P.dmv[3 * l]; mvd[1] = (int)P.dmv[3 * l + 1]; mvd[2] = (int)P.dmv[3 * l + 2];
+    } else {
+        mvd[0] = P.mv[l][0]; mvd[1] = P.mv[l][1]; mvd[2] = P.mv[l][2];
+    }
+    const int* mv = mvd;
     float* dt = P.dtables[l];
     const float s = P.scale[l] / (float)c;
     const int lane = threadIdx.x & 63;
@@ -162,16 +181,18 @@ __global__ void __launch_bounds__(256) tv_bwd_kernel(TVParams P) {
     }
 }
 
-static int fill_tv(TVParams& P, int n_levels, int log2_T, const int64_t* min_vertex, const int* cube) {
+static int fill_tv(TVParams& P, int n_levels, int log2_T, const int64_t* min_vertex, const int64_t* d_min_vertex,
+                   const int* cube) {
     NERF_REQUIRE(n_levels >= 1 && n_levels <= NERF_MAX_LEVELS, "tv: n_levels %d", n_levels);
     NERF_REQUIRE(log2_T >= 1 && log2_T <= 30, "tv: log2_T %d", log2_T);
-    NERF_REQUIRE(min_vertex && cube, "tv: null arg");
+    NERF_REQUIRE((min_vertex || d_min_vertex) && cube, "tv: null arg");
+    P.dmv = d_min_vertex;
     P.L = n_levels;
     P.mask = (uint32_t)((1u << log2_T) - 1u);
     P.vstart[0] = 0;
     for (int l = 0; l < n_levels; ++l) {
         NERF_REQUIRE(cube[l] >= 1 && cube[l] <= 1024, "tv: cube[%d] = %d", l, cube[l]);
-        for (int a = 0; a < 3; ++a) P.mv[l][a] = (int)min_vertex[3 * l + a];
+        for (int a = 0; a < 3; ++a) P.mv[l][a] = min_vertex ? (int)min_vertex[3 * l + a] : 0;
         P.cube[l] = cube[l];
         const int64_t n1 = cube[l] + 1;
         P.vstart[l + 1] = P.vstart[l] + n1 * n1 * n1;
@@ -183,12 +204,14 @@ static int fill_tv(TVParams& P, int n_levels, int log2_T, const int64_t* min_ver
 
 using namespace nerf;
 
-extern "C" int nerf_radam_step(const nerf_radam_segment* segs, int n_segs, void* stream) {
+extern "C" int nerf_radam_step(const nerf_radam_segment* segs, int n_segs, const float* d_coef, void* stream) {
     NERF_REQUIRE(segs && n_segs >= 0 && n_segs <= kMaxSegs, "radam_step: n_segs %d (max %d)", n_segs, kMaxSegs);
     RAdamSegs S{};
     S.n = 0;
+    S.coef = d_coef;
     int64_t blocks = 0;
     for (int i = 0; i < n_segs; ++i) {
+        NERF_REQUIRE(!d_coef || segs[i].n > 0, "radam_step: empty segment %d with device coefficients", i);
         if (segs[i].n <= 0) continue;
         NERF_REQUIRE(segs[i].p && segs[i].g && segs[i].m && segs[i].v, "radam_step: segment %d has a null pointer", i);
         NERF_REQUIRE(segs[i].mode >= 0 && segs[i].mode <= 2, "radam_step: segment %d mode %d", i, segs[i].mode);
@@ -205,9 +228,9 @@ extern "C" int nerf_radam_step(const nerf_radam_segment* segs, int n_segs, void*
 }
 
 extern "C" int nerf_tv_fwd(const float* const* d_tables, int n_levels, int log2_T, const int64_t* min_vertex,
-                           const int* cube, float* d_loss, void* stream) {
+                           const int64_t* d_min_vertex, const int* cube, float* d_loss, void* stream) {
     TVParams P{};
-    int rc = fill_tv(P, n_levels, log2_T, min_vertex, cube);
+    int rc = fill_tv(P, n_levels, log2_T, min_vertex, d_min_vertex, cube);
     if (rc) return rc;
     NERF_REQUIRE(d_tables && d_loss, "tv_fwd: null arg");
     for (int l = 0; l < n_levels; ++l) {
@@ -221,9 +244,10 @@ extern "C" int nerf_tv_fwd(const float* const* d_tables, int n_levels, int log2_
 }
 
 extern "C" int nerf_tv_bwd(const float* const* d_tables, int n_levels, int log2_T, const int64_t* min_vertex,
-                           const int* cube, const float* d_scale, float* const* d_dtables, void* stream) {
+                           const int64_t* d_min_vertex, const int* cube, const float* d_scale,
+                           float* const* d_dtables, void* stream) {
     TVParams P{};
-    int rc = fill_tv(P, n_levels, log2_T, min_vertex, cube);
+    int rc = fill_tv(P, n_levels, log2_T, min_vertex, d_min_vertex, cube);
     if (rc) return rc;
     NERF_REQUIRE(d_tables && d_dtables && d_scale, "tv_bwd: null arg");
     for (int l = 0; l < n_levels; ++l) {

@@ -82,6 +82,49 @@ __global__ void __launch_bounds__(256) sample_rays_kernel(Cam cam, int W_img, in
     }
 }
 
+// render()'s prologue (run_nerf.py:115-140): viewdirs = d / |d| (before NDC), optional ndc_rays
+// (run_nerf_helpers.py:333-350, near plane 1), and the packed ray batch [o, d, near, far, viewdir].
+// The NDC coefficients -1/(W/(2f)), -1/(H/(2f)) are python doubles in the reference that torch
+// rounds to float32 before the tensor ops; the host passes them that way.
+struct PackArgs {
+    const float* o;
+    const float* d;
+    int64_t n;
+    float near, far;
+    int ndc, viewdirs;
+    float cw, ch;          // float32(-1/(W/(2 focal))), float32(-1/(H/(2 focal)))
+    float* out;
+    int stride;            // 8 or 11
+};
+
+__global__ void __launch_bounds__(256) rays_pack_kernel(PackArgs a) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= a.n) return;
+    float ox = a.o[3 * r], oy = a.o[3 * r + 1], oz = a.o[3 * r + 2];
+    float dx = a.d[3 * r], dy = a.d[3 * r + 1], dz = a.d[3 * r + 2];
+    float* dst = a.out + r * a.stride;
+    if (a.viewdirs) {
+        const float nrm = sqrtf((dx * dx + dy * dy) + dz * dz);
+        dst[8] = dx / nrm;
+        dst[9] = dy / nrm;
+        dst[10] = dz / nrm;
+    }
+    if (a.ndc) {
+        const float t = -(1.0f + oz) / dz;
+        ox = ox + t * dx;
+        oy = oy + t * dy;
+        oz = oz + t * dz;
+        const float o0 = a.cw * ox / oz, o1 = a.ch * oy / oz, o2 = 1.0f + 2.0f / oz;
+        const float d0 = a.cw * (dx / dz - ox / oz), d1 = a.ch * (dy / dz - oy / oz), d2 = -2.0f / oz;
+        ox = o0; oy = o1; oz = o2;
+        dx = d0; dy = d1; dz = d2;
+    }
+    dst[0] = ox; dst[1] = oy; dst[2] = oz;
+    dst[3] = dx; dst[4] = dy; dst[5] = dz;
+    dst[6] = a.near;
+    dst[7] = a.far;
+}
+
 static uint32_t splitmix(uint64_t& s) {
     uint64_t z = (s += 0x9E3779B97F4A7C15ull);
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -117,5 +160,17 @@ extern "C" int nerf_sample_rays(const nerf_camera* cam, int H, int W, int crop_r
                        crop_r0, crop_c0, crop_w, n_cells, n_rays, random ? 1 : 0, bits / 2, k0, k1, k2, k3, d_image,
                        channels, d_rays_o, d_rays_d, d_target, d_coords);
     NERF_CHECK_LAUNCH("sample_rays");
+    return NERF_OK;
+}
+
+extern "C" int nerf_rays_pack(const float* d_rays_o, const float* d_rays_d, int64_t n_rays, float near, float far,
+                              int ndc, float ndc_coef_w, float ndc_coef_h, int use_viewdirs, float* d_out,
+                              void* stream) {
+    NERF_REQUIRE(n_rays >= 0 && (n_rays == 0 || (d_rays_o && d_rays_d && d_out)), "rays_pack: bad args");
+    if (n_rays == 0) return NERF_OK;
+    PackArgs a{d_rays_o, d_rays_d, n_rays, near, far, ndc ? 1 : 0, use_viewdirs ? 1 : 0, ndc_coef_w, ndc_coef_h,
+               d_out, use_viewdirs ? 11 : 8};
+    hipLaunchKernelGGL(rays_pack_kernel, dim3(blocks_for(n_rays, 256)), dim3(256), 0, as_stream(stream), a);
+    NERF_CHECK_LAUNCH("rays_pack");
     return NERF_OK;
 }

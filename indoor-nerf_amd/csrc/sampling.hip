@@ -7,6 +7,7 @@ namespace nerf {
 struct StratArgs {
     const float* rays; int64_t stride; int64_t R; int S;
     const float* t; int lindisp; int perturb; const float* u; uint64_t seed, offset;
+    const uint64_t* rng;   // optional device (seed, offset): graph replays draw fresh numbers
     float* z; float* pts;
 };
 
@@ -28,7 +29,9 @@ __global__ void __launch_bounds__(256) sample_stratified_kernel(StratArgs a) {
         const float zh = j + 1 < a.S ? base_depth(near, far, a.t[j + 1], a.lindisp) : 0.f;
         const float upper = j + 1 < a.S ? 0.5f * (zh + z) : z;
         const float lower = j > 0 ? 0.5f * (z + zl) : z;
-        const float u = a.u ? a.u[i] : philox_uniform(a.seed, a.offset, (uint64_t)i);
+        const float u = a.u ? a.u[i]
+                            : (a.rng ? philox_uniform(a.rng[0], a.rng[1], (uint64_t)i)
+                                     : philox_uniform(a.seed, a.offset, (uint64_t)i));
         z = lower + (upper - lower) * u;
     }
     a.z[i] = z;
@@ -49,6 +52,7 @@ struct PdfArgs {
     const float* w; int64_t w_stride;
     int64_t R; int nb;                 // nb = number of bins (cdf entries)
     int N; int det; const float* t_imp; const float* u; uint64_t seed, offset;
+    const uint64_t* rng;   // optional device (seed, offset)
     float* samples;
     // fine mode
     const float* rays; int64_t ray_stride; const float* z; int S;
@@ -109,7 +113,8 @@ __device__ __forceinline__ float invert_cdf(const float* cdf_l, const float* bin
 __device__ __forceinline__ float draw_u(const PdfArgs& a, int64_t r, int k) {
     if (a.det) return a.t_imp[k];
     const int64_t idx = r * a.N + k;
-    return a.u ? a.u[idx] : philox_uniform(a.seed, a.offset, (uint64_t)idx);
+    if (a.u) return a.u[idx];
+    return a.rng ? philox_uniform(a.rng[0], a.rng[1], (uint64_t)idx) : philox_uniform(a.seed, a.offset, (uint64_t)idx);
 }
 
 __global__ void __launch_bounds__(256) sample_pdf_kernel(PdfArgs a) {
@@ -197,12 +202,12 @@ using namespace nerf;
 
 extern "C" int nerf_sample_stratified(const float* d_rays, int64_t ray_stride, int64_t n_rays, int n_samples,
                                       const float* d_t, int lindisp, int perturb, const float* d_u, uint64_t seed,
-                                      uint64_t offset, float* d_z, float* d_pts, void* stream) {
+                                      uint64_t offset, const uint64_t* d_rng, float* d_z, float* d_pts, void* stream) {
     NERF_REQUIRE(n_rays >= 0 && n_samples >= 1, "sample_stratified: R=%lld S=%d", (long long)n_rays, n_samples);
     NERF_REQUIRE(ray_stride >= 8, "sample_stratified: ray_stride %lld < 8", (long long)ray_stride);
     NERF_REQUIRE(d_rays && d_t && d_z, "sample_stratified: null arg");
     if (n_rays == 0) return NERF_OK;
-    StratArgs a{d_rays, ray_stride, n_rays, n_samples, d_t, lindisp, perturb, d_u, seed, offset, d_z, d_pts};
+    StratArgs a{d_rays, ray_stride, n_rays, n_samples, d_t, lindisp, perturb, d_u, seed, offset, d_rng, d_z, d_pts};
     hipLaunchKernelGGL(sample_stratified_kernel, dim3(blocks_for(n_rays * n_samples, 256)), dim3(256), 0,
                        as_stream(stream), a);
     NERF_CHECK_LAUNCH("sample_stratified");
@@ -212,7 +217,7 @@ extern "C" int nerf_sample_stratified(const float* d_rays, int64_t ray_stride, i
 extern "C" int nerf_sample_pdf(const float* d_bins, int64_t bins_stride, const float* d_weights,
                                int64_t weights_stride, int64_t n_rays, int n_bins, int n_importance, int det,
                                const float* d_t_imp, const float* d_u, uint64_t seed, uint64_t offset,
-                               float* d_samples, void* stream) {
+                               const uint64_t* d_rng, float* d_samples, void* stream) {
     NERF_REQUIRE(n_rays >= 0 && n_bins >= 2 && n_bins <= kMaxBins && n_importance >= 1,
                  "sample_pdf: R=%lld bins=%d N=%d (bins must be 2..%d)", (long long)n_rays, n_bins, n_importance,
                  kMaxBins);
@@ -221,7 +226,7 @@ extern "C" int nerf_sample_pdf(const float* d_bins, int64_t bins_stride, const f
     PdfArgs a{};
     a.bins = d_bins; a.bins_stride = bins_stride; a.w = d_weights; a.w_stride = weights_stride;
     a.R = n_rays; a.nb = n_bins; a.N = n_importance; a.det = det; a.t_imp = d_t_imp; a.u = d_u;
-    a.seed = seed; a.offset = offset; a.samples = d_samples;
+    a.seed = seed; a.offset = offset; a.rng = d_rng; a.samples = d_samples;
     hipLaunchKernelGGL(sample_pdf_kernel, dim3(blocks_for(n_rays, 4)), dim3(256), 0, as_stream(stream), a);
     NERF_CHECK_LAUNCH("sample_pdf");
     return NERF_OK;
@@ -229,8 +234,8 @@ extern "C" int nerf_sample_pdf(const float* d_bins, int64_t bins_stride, const f
 
 extern "C" int nerf_sample_fine(const float* d_rays, int64_t ray_stride, const float* d_z, const float* d_weights,
                                 int64_t n_rays, int n_samples, int n_importance, int det, const float* d_t_imp,
-                                const float* d_u, uint64_t seed, uint64_t offset, float* d_z_fine, float* d_pts_fine,
-                                float* d_z_std, float* d_samples, void* stream) {
+                                const float* d_u, uint64_t seed, uint64_t offset, const uint64_t* d_rng,
+                                float* d_z_fine, float* d_pts_fine, float* d_z_std, float* d_samples, void* stream) {
     NERF_REQUIRE(n_rays >= 0 && n_samples >= 3 && n_samples <= kMaxBins && n_importance >= 1 &&
                      n_samples + n_importance <= kMaxMerged,
                  "sample_fine: R=%lld S=%d N=%d (S in 3..%d, S+N <= %d)", (long long)n_rays, n_samples,
@@ -240,6 +245,7 @@ extern "C" int nerf_sample_fine(const float* d_rays, int64_t ray_stride, const f
     if (n_rays == 0) return NERF_OK;
     PdfArgs a{};
     a.R = n_rays; a.N = n_importance; a.det = det; a.t_imp = d_t_imp; a.u = d_u; a.seed = seed; a.offset = offset;
+    a.rng = d_rng;
     a.samples = d_samples; a.rays = d_rays; a.ray_stride = ray_stride; a.z = d_z; a.w = d_weights; a.S = n_samples;
     a.z_fine = d_z_fine; a.pts_fine = d_pts_fine; a.z_std = d_z_std;
     hipLaunchKernelGGL(sample_fine_kernel, dim3(blocks_for(n_rays, 4)), dim3(256), 0, as_stream(stream), a);

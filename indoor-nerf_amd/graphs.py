@@ -1,0 +1,188 @@
+"""The training iteration captured in HIP graphs (torch.cuda.CUDAGraph on ROCm = hipGraph).
+
+A PocketNeRF iteration (run_nerf.py:1007-1037, :1161-1162, :1289-1293) is ~40 kernel launches of
+which many are short; launched one by one from Python the GPU idles between them (the host spends
+~0.2 ms per step in autograd and ctypes). GraphedTrainStep captures the iteration once — forward,
+losses, backward (graph 1) and the RAdam update (graph 2) — and replays it.
+
+What changes from step to step without changing the launch structure lives in device memory and is
+written before each replay (StepScalars): the Philox (seed, offset) of the stratified and
+importance sampling kernels, the TV cuboid corners (drawn on the host with the same generator as
+the eager path), and RAdam's per-step scalars (step count, N_sma, step size, lr decay). Those are
+computed by the same host code as the eager path ("fillers" registered while capturing), written
+into a pinned ring buffer and copied asynchronously ahead of the replay.
+
+The launch structure itself depends on host state that changes rarely: the TV term switches off
+after iteration 1000 (run_nerf.py:1036-1037) and A-CAQ quantization switches on after the
+embedder's warm-up; GraphedTrainStep re-captures when that key changes.
+"""
+from contextlib import contextmanager
+
+import torch
+
+_ACTIVE = None
+
+
+def active():
+    """The StepScalars of the capture in progress, or None (eager execution)."""
+    return _ACTIVE
+
+
+@contextmanager
+def capturing(scalars):
+    global _ACTIVE
+    prev, _ACTIVE = _ACTIVE, scalars
+    try:
+        yield scalars
+    finally:
+        _ACTIVE = prev
+
+
+class StepScalars:
+    """Device-resident per-step scalars of a captured step (int64 and float32 slots)."""
+
+    def __init__(self, device, n_i64=1024, n_f32=1024, ring=4):
+        self.dev_i = torch.zeros(n_i64, dtype=torch.int64, device=device)
+        self.dev_f = torch.zeros(n_f32, dtype=torch.float32, device=device)
+        self.pinned = [(torch.zeros(n_i64, dtype=torch.int64).pin_memory(),
+                        torch.zeros(n_f32, dtype=torch.float32).pin_memory()) for _ in range(ring)]
+        self.events = [None] * ring
+        self.k = 0
+        self.ni = self.nf = 0
+        self.fillers = []
+
+    def alloc_i64(self, n):
+        if self.ni + n > self.dev_i.numel():
+            raise RuntimeError("StepScalars: int64 slots exhausted")
+        off, self.ni = self.ni, self.ni + n
+        return off, self.dev_i.data_ptr() + 8 * off
+
+    def alloc_f32(self, n):
+        if self.nf + n > self.dev_f.numel():
+            raise RuntimeError("StepScalars: float32 slots exhausted")
+        off, self.nf = self.nf, self.nf + n
+        return off, self.dev_f.data_ptr() + 4 * off
+
+    def add_filler(self, fn):
+        """fn(host_int64_numpy, host_float32_numpy) writes this step's values into its slots."""
+        self.fillers.append(fn)
+
+    def upload(self):
+        """Run every filler into the next pinned ring slot and copy it to the device (async,
+        stream-ordered before the replay that reads it)."""
+        k = self.k
+        self.k = (k + 1) % len(self.pinned)
+        if self.events[k] is not None:
+            self.events[k].synchronize()          # the copy that last read this slot has completed
+        hi, hf = self.pinned[k]
+        ni, nf = hi.numpy(), hf.numpy()
+        for fn in self.fillers:
+            fn(ni, nf)
+        self.dev_i.copy_(hi, non_blocking=True)
+        self.dev_f.copy_(hf, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self.events[k] = ev
+
+
+class GraphedTrainStep:
+    """train_step (model.py) as two captured graphs (forward + backward, RAdam) plus the eager
+    grad hook between them (the DP all-reduce stays outside the graphs). Call it like
+    train_step(...) with the same arguments every iteration; it runs `warmup` eager iterations
+    before the first capture (allocations, optimizer state, quantizer calibration)."""
+
+    def __init__(self, batch_rays, target_s, render_kwargs_train, optimizer, args, H=0, W=0, K=None,
+                 grad_hook=None, loss_scale_sparsity=1.0, tv_generator=None, zero_grad=None, warmup=2):
+        self.rays, self.target = batch_rays, target_s
+        self.kw, self.opt, self.args = render_kwargs_train, optimizer, args
+        self.H, self.W, self.K = H, W, K
+        if zero_grad is None:
+            # gradients must live at fixed addresses across replays: one flat arena, zeroed in place
+            from .dist import GradArena
+            arena = GradArena([p for g in optimizer.param_groups for p in g["params"]])
+            zero_grad = arena.zero_
+        self.hook, self.scale_sp, self.tv_gen, self.zero_grad = grad_hook, loss_scale_sparsity, tv_generator, zero_grad
+        self.warmup = warmup
+        self.eager_steps = 0
+        self.key = None
+        self.graphs = None
+        self.captures = 0
+
+    def _n_forwards(self):
+        return 2 if self.kw.get("network_fine") is not None else 1     # coarse + fine embedder calls
+
+    def _structure_key(self):
+        """Host state that changes the launch sequence of a step: the TV term (on until iteration
+        1000) and, per embedder call of the step, whether A-CAQ quantization is active."""
+        from .model import DEFAULTS
+        tv_w = getattr(self.args, "tv_loss_weight", DEFAULTS["tv_loss_weight"])
+        emb = self.kw["embed_fn"]
+        quant = ()
+        if getattr(emb, "use_quantization", False):
+            quant = tuple(emb.current_step + k + 1 >= emb.warmup_steps for k in range(self._n_forwards()))
+        return (tv_w > 0, quant)
+
+    def _capture(self, global_step):
+        from . import _lib
+        from .model import forward_backward, optimizer_update
+        if _lib.timing_enabled():
+            raise RuntimeError("GraphedTrainStep: kernel timing is on; torch on ROCm cannot capture timing "
+                               "events (time eager_step() instead)")
+        dev = self.target.device
+        sc = StepScalars(dev)
+        emb = self.kw["embed_fn"]
+        step0 = emb.current_step           # the captured (not executed) forwards must not count
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        pool = torch.cuda.graph_pool_handle()
+        g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.stream(side):
+            with capturing(sc):
+                with torch.cuda.graph(g1, pool=pool, stream=side):
+                    out = forward_backward(self.rays, self.target, self.kw, self.opt, self.args, global_step,
+                                           H=self.H, W=self.W, K=self.K, loss_scale_sparsity=self.scale_sp,
+                                           tv_generator=self.tv_gen, zero_grad=self.zero_grad, schedule=False)
+                with torch.cuda.graph(g2, pool=pool, stream=side):
+                    optimizer_update(self.opt)
+        torch.cuda.current_stream(dev).wait_stream(side)
+        emb.current_step = step0
+        self.graphs = (g1, g2)
+        self.out = out
+        self.scalars = sc
+        self.params = [p for g in self.opt.param_groups for p in g["params"] if p.grad is not None]
+        self.captures += 1
+
+    def eager_step(self, global_step):
+        """The same iteration launched eagerly (same arguments, host state and gradient arena),
+        e.g. to time its kernels with HIP events, which cannot be captured."""
+        from .model import train_step
+        return train_step(self.rays, self.target, self.kw, self.opt, self.args, global_step, H=self.H, W=self.W,
+                          K=self.K, grad_hook=self.hook, loss_scale_sparsity=self.scale_sp,
+                          tv_generator=self.tv_gen, zero_grad=self.zero_grad)
+
+    def __call__(self, global_step):
+        from .model import acaq_update, lr_schedule
+        key = self._structure_key()
+        if key != self.key:                # new launch structure: eager steps first (allocations,
+            self.key = key                 # quantizer calibration), then a fresh capture
+            self.graphs = None
+            self.eager_steps = 0
+        if self.eager_steps < self.warmup:
+            self.eager_steps += 1
+            return self.eager_step(global_step)
+        if self.graphs is None:
+            self._capture(global_step)
+        self.scalars.upload()
+        self.graphs[0].replay()
+        emb = self.kw["embed_fn"]
+        if emb.training:
+            emb.current_step += self._n_forwards()
+        if self.hook is not None:
+            self.hook()
+        self.graphs[1].replay()
+        for p in self.params:              # the replayed RAdam wrote the parameters in place
+            torch.autograd.graph.increment_version(p)
+        loss, img_loss, psnr = self.out
+        acaq_update(global_step, img_loss, self.kw, self.args)
+        lr_schedule(self.opt, self.args, global_step)
+        return loss.detach(), psnr.detach()

@@ -25,15 +25,20 @@ def tv_cube(level, min_resolution, max_resolution, n_levels):
 
 
 class TVFn(torch.autograd.Function):
+    """min_vertex: host [L,3] cuboid corners, or an int device address of [L,3] int64 slots that a
+    captured step refreshes before every replay (graphs.StepScalars)."""
     @staticmethod
     def forward(ctx, min_vertex, cubes, log2_T, *tables):
         L = len(tables)
-        mv = (_lib.c_i64 * (3 * L))(*[int(v) for v in min_vertex.reshape(-1).tolist()])
+        if isinstance(min_vertex, int):
+            mv, dmv = None, _lib.c_vp(min_vertex)
+        else:
+            mv, dmv = (_lib.c_i64 * (3 * L))(*[int(v) for v in min_vertex.reshape(-1).tolist()]), None
         cb = (_lib.c_int * L)(*[int(c) for c in cubes])
         loss = torch.zeros(L, device=tables[0].device, dtype=torch.float32)
-        _lib.call("nerf_tv_fwd", _lib.ptr_array(tables), L, log2_T, mv, cb, _lib.ptr(loss, "loss"), _lib.stream())
+        _lib.call("nerf_tv_fwd", _lib.ptr_array(tables), L, log2_T, mv, dmv, cb, _lib.ptr(loss, "loss"), _lib.stream())
         ctx.save_for_backward(*tables)
-        ctx.mv, ctx.cb, ctx.log2_T = mv, cb, log2_T
+        ctx.mv, ctx.dmv, ctx.cb, ctx.log2_T = mv, dmv, cb, log2_T
         return loss
 
     @staticmethod
@@ -41,7 +46,7 @@ class TVFn(torch.autograd.Function):
         tables = ctx.saved_tensors
         if g is not None and any(t.requires_grad for t in tables):
             grads = accumulate_grad_buffers(tables)
-            _lib.call("nerf_tv_bwd", _lib.ptr_array(tables), len(tables), ctx.log2_T, ctx.mv, ctx.cb,
+            _lib.call("nerf_tv_bwd", _lib.ptr_array(tables), len(tables), ctx.log2_T, ctx.mv, ctx.dmv, ctx.cb,
                       _lib.ptr(g.contiguous(), "grad_loss"), _lib.ptr_array(grads, "grad_tables"), _lib.stream())
         return (None, None, None) + (None,) * len(tables)
 
@@ -58,6 +63,19 @@ def draw_min_vertices(embedder, generator=None):
 
 def total_variation_all(embedder, min_vertex=None, generator=None):
     """Per-level TV losses [L] of all levels of `embedder` (sum them for the reference's TV_loss)."""
+    from . import graphs
+    sc = graphs.active()
+    if sc is not None and min_vertex is None:
+        # captured step: the corners are drawn by the same host code before every replay
+        L = embedder.n_levels
+        off, ptr = sc.alloc_i64(3 * L)
+
+        def fill(hi, hf, off=off):
+            mv, _ = draw_min_vertices(embedder, generator)
+            hi[off:off + 3 * L] = mv.reshape(-1).numpy()
+        sc.add_filler(fill)
+        cubes = [tv_cube(l, embedder.base_resolution, embedder.finest_resolution, L)[1] for l in range(L)]
+        return TVFn.apply(ptr, cubes, embedder.log2_hashmap_size, *embedder.tables())
     if min_vertex is None:
         min_vertex, cubes = draw_min_vertices(embedder, generator)
     else:
@@ -79,6 +97,7 @@ class TrainLossFn(torch.autograd.Function):
     """run_nerf.py:1011-1037 in one launch (csrc/loss.hip): returns (loss, img_loss, psnr[1])."""
     @staticmethod
     def forward(ctx, rgb, rgb0, target, sp, sp0, tv, sparse_w, tv_w):
+        ctx.set_materialize_grads(False)     # img_loss / psnr carry no gradient: no zero fills
         R = rgb.shape[0]
         f = dict(device=rgb.device, dtype=torch.float32)
         rgb, target = rgb.contiguous(), target.contiguous().float()
@@ -97,6 +116,8 @@ class TrainLossFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g, _g_img, _g_psnr):
         rgb, rgb0, target = ctx.saved_tensors
+        if g is None:
+            return (None,) * 8
         R, sparse_w, n_tv, tv_w, has_sp, has_sp0 = ctx.meta
         f = dict(device=rgb.device, dtype=torch.float32)
         d_rgb = torch.empty_like(rgb)

@@ -148,11 +148,10 @@ def acaq_update(i, img_loss, render_kwargs_train, args):
     return report
 
 
-def train_step(batch_rays, target_s, render_kwargs_train, optimizer, args, global_step, H=0, W=0, K=None,
-               grad_hook=None, loss_scale_sparsity=1.0, tv_generator=None, zero_grad=None):
-    """One iteration of train() without host bookkeeping: render (coarse+fine), img/img0 MSE,
-    sparsity, TV (run_nerf.py:1007-1037), backward, [grad_hook, e.g. DP all-reduce], RAdam step,
-    lr decay (:1289-1293). Returns (loss, psnr) as device tensors (no host sync)."""
+def forward_backward(batch_rays, target_s, render_kwargs_train, optimizer, args, global_step, H=0, W=0, K=None,
+                     loss_scale_sparsity=1.0, tv_generator=None, zero_grad=None, schedule=True):
+    """render (coarse+fine), zero grads, img/img0 MSE + sparsity + TV (run_nerf.py:1007-1037),
+    backward. Returns (loss, img_loss, psnr) device tensors (no host sync)."""
     get = lambda k: getattr(args, k, DEFAULTS.get(k))  # noqa: E731
     rgb, depth, acc, extras = render(H, W, K, chunk=get("chunk"), rays=batch_rays, retraw=True,
                                      **render_kwargs_train)
@@ -164,17 +163,41 @@ def train_step(batch_rays, target_s, render_kwargs_train, optimizer, args, globa
     tv_w = get("tv_loss_weight")
     tv = total_variation_all(render_kwargs_train["embed_fn"], generator=tv_generator) if tv_w > 0 else None
     loss, img_loss, psnr = train_loss(rgb, extras.get("rgb0"), target_s, extras.get("sparsity_loss"),
-                                       extras.get("sparsity_loss0"), tv, get("sparse_loss_weight") * loss_scale_sparsity,
-                                       tv_w if tv_w > 0 else 0.0)
-    if global_step > 1000:
+                                      extras.get("sparsity_loss0"), tv, get("sparse_loss_weight") * loss_scale_sparsity,
+                                      tv_w if tv_w > 0 else 0.0)
+    if schedule and global_step > 1000:
         args.tv_loss_weight = 0.0
     loss.backward()
-    if grad_hook is not None:
-        grad_hook()
+    return loss, img_loss, psnr
+
+
+def optimizer_update(optimizer):
     optimizer.step()
-    acaq_update(global_step, img_loss, render_kwargs_train, args)
+
+
+def lr_schedule(optimizer, args, global_step):
+    """TV switch-off after 1000 iterations (run_nerf.py:1036-1037) and lr decay (:1289-1293)."""
+    get = lambda k: getattr(args, k, DEFAULTS.get(k))  # noqa: E731
+    if global_step > 1000:
+        args.tv_loss_weight = 0.0
     decay_steps = get("lrate_decay") * 1000
     new_lrate = get("lrate") * (0.1 ** (global_step / decay_steps))
     for g in optimizer.param_groups:
         g["lr"] = new_lrate
+
+
+def train_step(batch_rays, target_s, render_kwargs_train, optimizer, args, global_step, H=0, W=0, K=None,
+               grad_hook=None, loss_scale_sparsity=1.0, tv_generator=None, zero_grad=None):
+    """One iteration of train() without host bookkeeping: render (coarse+fine), img/img0 MSE,
+    sparsity, TV (run_nerf.py:1007-1037), backward, [grad_hook, e.g. DP all-reduce], RAdam step,
+    A-CAQ bit widths, lr decay (:1182-1250, :1289-1293). Returns (loss, psnr) as device tensors
+    (no host sync). graphs.GraphedTrainStep replays the same iteration from HIP graphs."""
+    loss, img_loss, psnr = forward_backward(batch_rays, target_s, render_kwargs_train, optimizer, args, global_step,
+                                            H=H, W=W, K=K, loss_scale_sparsity=loss_scale_sparsity,
+                                            tv_generator=tv_generator, zero_grad=zero_grad)
+    if grad_hook is not None:
+        grad_hook()
+    optimizer_update(optimizer)
+    acaq_update(global_step, img_loss, render_kwargs_train, args)
+    lr_schedule(optimizer, args, global_step)
     return loss.detach(), psnr.detach()

@@ -54,15 +54,39 @@ class RAdam(Optimizer):
             buffered[2] = step_size
         return n_sma, step_size
 
-    @torch.no_grad()
-    def step(self, closure=None):
-        loss = None
-        if closure is not None:
-            with torch.enable_grad():
-                loss = closure()
-        segs, updated = [], []
+    def _segment(self, group, p, mode, step_size):
+        beta1, beta2 = group["betas"]
+        state = self.state[p]
+        s = _lib.RAdamSegment()
+        s.p = _lib.ptr(p, "param").value
+        s.g = _lib.ptr(p.grad, "grad").value
+        s.m = _lib.ptr(state["exp_avg"], "exp_avg").value
+        s.v = _lib.ptr(state["exp_avg_sq"], "exp_avg_sq").value
+        s.n = p.numel()
+        s.beta1, s.beta2 = beta1, beta2
+        s.one_minus_beta1, s.one_minus_beta2 = 1 - beta1, 1 - beta2
+        s.eps = group["eps"]
+        s.decay_coef, s.step_coef = self._coefs(group, mode, step_size)
+        s.mode = mode
+        return s
+
+    @staticmethod
+    def _coefs(group, mode, step_size):
+        wd = group["weight_decay"]
+        decay_coef = -wd * group["lr"] if (wd != 0 and mode != 0) else 0.0
+        step_coef = -step_size * group["lr"] if mode != 0 else 0.0
+        return decay_coef, step_coef
+
+    def _advance(self, group, p):
+        """state['step'] += 1 and this step's (mode, step_size) (radam.py:49-79)."""
+        state = self.state[p]
+        state["step"] += 1
+        n_sma, step_size = self._scalars(group, state["step"])
+        mode = 2 if n_sma >= 5 else (1 if step_size > 0 else 0)
+        return mode, step_size
+
+    def _params(self):
         for group in self.param_groups:
-            beta1, beta2 = group["betas"]
             for p in group["params"]:
                 if p.grad is None:
                     continue
@@ -75,35 +99,49 @@ class RAdam(Optimizer):
                     state["step"] = 0
                     state["exp_avg"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
                     state["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
-                state["step"] += 1
-                n_sma, step_size = self._scalars(group, state["step"])
-                if n_sma >= 5:
-                    mode = 2
-                elif step_size > 0:
-                    mode = 1
-                else:
-                    mode = 0
-                wd = group["weight_decay"]
-                s = _lib.RAdamSegment()
-                s.p = _lib.ptr(p, "param").value
-                s.g = _lib.ptr(p.grad, "grad").value
-                s.m = _lib.ptr(state["exp_avg"], "exp_avg").value
-                s.v = _lib.ptr(state["exp_avg_sq"], "exp_avg_sq").value
-                s.n = p.numel()
-                s.beta1, s.beta2 = beta1, beta2
-                s.one_minus_beta1, s.one_minus_beta2 = 1 - beta1, 1 - beta2
-                s.eps = group["eps"]
-                s.decay_coef = -wd * group["lr"] if (wd != 0 and mode != 0) else 0.0
-                s.step_coef = -step_size * group["lr"] if mode != 0 else 0.0
-                s.mode = mode
-                segs.append(s)
-                updated.append(p)
+                yield group, p
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        from . import graphs
+        sc = graphs.active()
+        if sc is not None:
+            self._capture_step(sc)
+            return loss
+        segs, updated = [], []
+        for group, p in self._params():
+            mode, step_size = self._advance(group, p)
+            segs.append(self._segment(group, p, mode, step_size))
+            updated.append(p)
         for i in range(0, len(segs), _MAX_SEGS):
             chunk = segs[i:i + _MAX_SEGS]
             arr = (_lib.RAdamSegment * len(chunk))(*chunk)
-            _lib.call("nerf_radam_step", arr, len(chunk), _lib.stream())
+            _lib.call("nerf_radam_step", arr, len(chunk), None, _lib.stream())
         # the kernel writes through raw pointers: bump the version counters the reference's
         # in-place tensor ops would have bumped (cache keys such as HashEmbedder.packed_tables)
         for p in updated:
             torch.autograd.graph.increment_version(p)
         return loss
+
+    def _capture_step(self, sc):
+        """Captured in a HIP graph (graphs.GraphedTrainStep): the launch reads (decay_coef,
+        step_coef, mode) of each tensor from device slots that a filler computes before every
+        replay with the same host algebra (state['step'] advances there, not at capture)."""
+        pairs = list(self._params())
+        for i in range(0, len(pairs), _MAX_SEGS):
+            chunk = pairs[i:i + _MAX_SEGS]
+            off, dptr = sc.alloc_f32(4 * len(chunk))
+            segs = [self._segment(g, p, 2, 0.0) for g, p in chunk]
+            arr = (_lib.RAdamSegment * len(chunk))(*segs)
+            _lib.call("nerf_radam_step", arr, len(chunk), _lib.c_vp(dptr), _lib.stream())
+
+            def fill(hi, hf, off=off, chunk=chunk):
+                for j, (g, p) in enumerate(chunk):
+                    mode, step_size = self._advance(g, p)
+                    dc, stc = self._coefs(g, mode, step_size)
+                    hf[off + 4 * j:off + 4 * j + 4] = (dc, stc, float(mode), 0.0)
+            sc.add_filler(fill)

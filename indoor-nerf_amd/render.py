@@ -41,6 +41,24 @@ def _draw_seed():
     return int(s[0]), int(s[1])
 
 
+def _rng():
+    """(seed, offset, d_rng) for an in-kernel Philox draw. Eager: a fresh host seed. While a
+    training step is being captured (graphs.GraphedTrainStep): two device slots that a filler
+    refreshes with a fresh seed before every replay."""
+    from . import graphs
+    sc = graphs.active()
+    if sc is None:
+        s, o = _draw_seed()
+        return s, o, None
+    off, ptr = sc.alloc_i64(2)
+
+    def fill(hi, hf, off=off):
+        s, o = _draw_seed()
+        hi[off], hi[off + 1] = s, o
+    sc.add_filler(fill)
+    return 0, 0, _lib.c_vp(ptr)
+
+
 def manual_seed(seed):
     """Seed the in-kernel Philox draws (stratified jitter, importance uniforms)."""
     global _SEED_GEN
@@ -128,9 +146,9 @@ def sample_pdf(bins, weights, N_samples, det=False, pytest=False):
     out = torch.empty(R, N_samples, device=bins.device, dtype=torch.float32)
     t_imp = _linspace(N_samples, bins.device) if det else None
     u = _pytest_uniforms((R, N_samples), bins.device) if (pytest and not det) else None
-    seed, off = _draw_seed()
+    seed, off, rng = _rng()
     _lib.call("nerf_sample_pdf", _lib.ptr(bins, "bins"), nb, _lib.ptr(weights, "weights"), nb - 1, R, nb, N_samples,
-              int(det), _lib.ptr(t_imp, "t", allow_none=True), _lib.ptr(u, "u", allow_none=True), seed, off,
+              int(det), _lib.ptr(t_imp, "t", allow_none=True), _lib.ptr(u, "u", allow_none=True), seed, off, rng,
               _lib.ptr(out, "samples"), _lib.stream())
     return out
 
@@ -149,9 +167,9 @@ def render_rays(ray_batch, network_fn, network_query_fn, N_samples, embed_fn=Non
     z = torch.empty(R, N_samples, **f)
     pts = torch.empty(R, N_samples, 3, **f)
     u = _pytest_uniforms((R, N_samples), dev) if (perturb > 0. and pytest) else None
-    seed, off = _draw_seed()
+    seed, off, rng = (0, 0, None) if (u is not None or not perturb > 0.) else _rng()
     _lib.call("nerf_sample_stratified", _lib.ptr(rays, "ray_batch"), C, R, N_samples, _lib.ptr(_linspace(N_samples, dev)),
-              int(bool(lindisp)), int(perturb > 0.), _lib.ptr(u, "u", allow_none=True), seed, off, _lib.ptr(z, "z"),
+              int(bool(lindisp)), int(perturb > 0.), _lib.ptr(u, "u", allow_none=True), seed, off, rng, _lib.ptr(z, "z"),
               _lib.ptr(pts, "pts"), _lib.stream())
 
     raw = network_query_fn(pts, viewdirs, network_fn)
@@ -170,10 +188,10 @@ def render_rays(ray_batch, network_fn, network_query_fn, N_samples, embed_fn=Non
         z_std = torch.empty(R, **f)
         t_imp = _linspace(N_importance, dev) if det else None
         u_imp = _pytest_uniforms((R, N_importance), dev) if (pytest and not det) else None
-        seed, off = _draw_seed()
+        seed, off, rng = (0, 0, None) if (det or u_imp is not None) else _rng()
         _lib.call("nerf_sample_fine", _lib.ptr(rays, "ray_batch"), C, _lib.ptr(z, "z"),
                   _lib.ptr(weights.detach().contiguous(), "weights"), R, N_samples, N_importance, int(det),
-                  _lib.ptr(t_imp, "t", allow_none=True), _lib.ptr(u_imp, "u", allow_none=True), seed, off,
+                  _lib.ptr(t_imp, "t", allow_none=True), _lib.ptr(u_imp, "u", allow_none=True), seed, off, rng,
                   _lib.ptr(z_fine, "z_fine"), _lib.ptr(pts_fine, "pts_fine"), _lib.ptr(z_std, "z_std"), None,
                   _lib.stream())
         z, pts = z_fine, pts_fine
@@ -252,6 +270,24 @@ def ndc_rays(H, W, focal, near, rays_o, rays_d):
     return torch.stack([o0, o1, o2], -1), torch.stack([d0, d1, d2], -1)
 
 
+def _pack_rays(H, W, K, rays_o, rays_d, near, far, ndc, use_viewdirs):
+    """render()'s prologue (run_nerf.py:115-140) in one launch (csrc/rays.hip nerf_rays_pack):
+    viewdirs = d/|d|, ndc_rays (near plane 1), [o, d, near, far, viewdir] per ray."""
+    o = torch.reshape(rays_o, [-1, 3]).float().contiguous()
+    d = torch.reshape(rays_d, [-1, 3]).float().contiguous()
+    n = d.shape[0]
+    out = torch.empty(n, 11 if use_viewdirs else 8, device=d.device, dtype=torch.float32)
+    cw = ch = 0.0
+    if ndc:
+        focal = K[0][0]
+        # -1./(W/(2.*focal)) is a python double in the reference; torch rounds it to float32
+        cw = float(np.float32(-1. / (W / (2. * float(focal)))))
+        ch = float(np.float32(-1. / (H / (2. * float(focal)))))
+    _lib.call("nerf_rays_pack", _lib.ptr(o, "rays_o"), _lib.ptr(d, "rays_d"), n, float(near), float(far), int(bool(ndc)),
+              cw, ch, int(bool(use_viewdirs)), _lib.ptr(out, "rays"), _lib.stream())
+    return out
+
+
 def render(H, W, K, chunk=1024 * 32, rays=None, c2w=None, ndc=True, near=0., far=1., use_viewdirs=False,
            c2w_staticcam=None, **kwargs):
     """run_nerf.py:86-151 -> [rgb_map, depth_map, acc_map, extras]."""
@@ -259,21 +295,15 @@ def render(H, W, K, chunk=1024 * 32, rays=None, c2w=None, ndc=True, near=0., far
         rays_o, rays_d = get_rays(H, W, K, c2w)
     else:
         rays_o, rays_d = rays
-    if use_viewdirs:
-        viewdirs = rays_d
-        if c2w_staticcam is not None:
-            rays_o, rays_d = get_rays(H, W, K, c2w_staticcam)
-        viewdirs = viewdirs / torch.norm(viewdirs, dim=-1, keepdim=True)
-        viewdirs = torch.reshape(viewdirs, [-1, 3]).float()
     sh = rays_d.shape
-    if ndc:
-        rays_o, rays_d = ndc_rays(H, W, K[0][0], 1., rays_o, rays_d)
-    rays_o = torch.reshape(rays_o, [-1, 3]).float()
-    rays_d = torch.reshape(rays_d, [-1, 3]).float()
-    near, far = near * torch.ones_like(rays_d[..., :1]), far * torch.ones_like(rays_d[..., :1])
-    rays = torch.cat([rays_o, rays_d, near, far], -1)
-    if use_viewdirs:
-        rays = torch.cat([rays, viewdirs], -1)
+    if use_viewdirs and c2w_staticcam is not None:
+        # viewdirs from the moving camera, rays from the static one (run_nerf.py:115-126)
+        vd = rays_d / torch.norm(rays_d, dim=-1, keepdim=True)
+        rays_o, rays_d = get_rays(H, W, K, c2w_staticcam)
+        rays = _pack_rays(H, W, K, rays_o, rays_d, near, far, ndc, False)
+        rays = torch.cat([rays, torch.reshape(vd, [-1, 3]).float()], -1)
+    else:
+        rays = _pack_rays(H, W, K, rays_o, rays_d, near, far, ndc, use_viewdirs)
     all_ret = batchify_rays(rays, chunk, **kwargs)
     for k in all_ret:
         all_ret[k] = torch.reshape(all_ret[k], list(sh[:-1]) + list(all_ret[k].shape[1:]))
