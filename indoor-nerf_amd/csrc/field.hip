@@ -351,11 +351,32 @@ __global__ void __launch_bounds__(256) mlp_bwd_kernel(MlpArgs a) {
 int launch_mlp_fwd_frag(const MlpArgs& a, hipStream_t stream);   // field_frag.hip
 int launch_mlp_bwd_frag(const MlpArgs& a, hipStream_t stream);
 
-// NERF_MLP=1 selects the first MLP version (LDS weight images, per-tile gradient flush) for A/B
-// runs; the default is the fragment-stationary version of field_frag.hip.
-static bool use_frag_mlp() {
+int launch_mlp_fwd_x6(const MlpArgs& a, hipStream_t stream);     // field_x6.hip
+int launch_mlp_bwd_x6(const MlpArgs& a, hipStream_t stream);
+
+// MLP kernel generation, for A/B runs: NERF_MLP=1 the first version (f32 MFMA, LDS weight
+// images), NERF_MLP=2 the fragment-stationary f32-MFMA version (field_frag.hip) for forward and
+// backward, NERF_MLP=3 the fp32-accurate bf16x6 version (field_x6.hip) for both. Default: bf16x6
+// forward (1.27x the f32 forward) + f32-MFMA backward (the bf16x6 backward measured 7 % slower:
+// DESIGN.md §4).
+static int mlp_version() {
     const char* e = getenv("NERF_MLP");
-    return !(e && e[0] == '1');
+    if (e && e[0] >= '1' && e[0] <= '3') return e[0] - '0';
+    return 0;
+}
+
+static bool use_frag_mlp() { return mlp_version() != 1; }
+
+static int launch_mlp_fwd_default(const MlpArgs& a, hipStream_t stream) {
+    // the activation-quantizer calibration launch (layer 0 only) stays on the f32 path
+    const int v = mlp_version();
+    if ((v == 0 || v == 3) && !a.act_minmax) return launch_mlp_fwd_x6(a, stream);
+    return launch_mlp_fwd_frag(a, stream);
+}
+
+static int launch_mlp_bwd_default(const MlpArgs& a, hipStream_t stream) {
+    if (mlp_version() == 3) return launch_mlp_bwd_x6(a, stream);
+    return launch_mlp_bwd_frag(a, stream);
 }
 
 static int fill_args(MlpArgs& a, const float* d_feat, int64_t sp, int64_t sl, const float* d_sh, int64_t sh_stride,
@@ -398,7 +419,7 @@ extern "C" int nerf_mlp_fwd_q(const float* d_feat, int64_t feat_stride_point, in
     a.aq = reinterpret_cast<const QuantRec*>(d_act_qrec);
     a.act_minmax = d_act_minmax;
     a.calib_points = act_calib_points;
-    if (use_frag_mlp()) return launch_mlp_fwd_frag(a, as_stream(stream));
+    if (use_frag_mlp()) return launch_mlp_fwd_default(a, as_stream(stream));
     NERF_REQUIRE(!d_geo, "mlp_fwd: the geo output needs the default (fragment) MLP kernels");
     NERF_REQUIRE(!d_act_qrec && !d_act_minmax, "mlp_fwd: quantization needs the default (fragment) MLP kernels");
     const int64_t tiles = (n_points + 31) / 32;
@@ -430,7 +451,7 @@ extern "C" int nerf_mlp_bwd_q(const float* d_feat, int64_t feat_stride_point, in
     if (n_points == 0) return NERF_OK;
     a.graw = d_graw; a.G = *grads; a.dfeat = d_dfeat; a.dsh = d_dsh; a.dgeo = d_dgeo;
     a.aq = reinterpret_cast<const QuantRec*>(d_act_qrec);
-    if (use_frag_mlp()) return launch_mlp_bwd_frag(a, as_stream(stream));
+    if (use_frag_mlp()) return launch_mlp_bwd_default(a, as_stream(stream));
     NERF_REQUIRE(!d_dgeo, "mlp_bwd: the geo gradient input needs the default (fragment) MLP kernels");
     NERF_REQUIRE(!d_act_qrec, "mlp_bwd: quantization needs the default (fragment) MLP kernels");
     const int64_t tiles = (n_points + 31) / 32;

@@ -1,0 +1,637 @@
+// Field MLP on the bf16 matrix cores with fp32 accuracy ("x6", the default MLP path).
+//
+// gfx950 has no tf32/xf32 MFMA and its f32-input MFMA (v_mfma_f32_32x32x2_f32) runs at 1/16 of
+// the bf16 rate. Every fp32 operand v is therefore split EXACTLY into three bf16 pieces
+//     v = v0 + v1 + v2,   v0 = bf16_rne(v), v1 = bf16_rne(v - v0), v2 = bf16_rne(v - v0 - v1)
+// (|v1| <= 2^-8 |v|, |v2| <= 2^-16 |v|; nothing is left after v2 for normal fp32) and a product
+// a*b is formed by six v_mfma_f32_32x32x16_bf16 terms
+//     a0b0 + a0b1 + a1b0 + a1b1 + a0b2 + a2b0
+// whose dropped terms a1b2 + a2b1 + a2b2 are <= 2^-23 |ab|: the per-product error of an fp32
+// multiply (2^-24 |ab|) within a factor of two, accumulated in fp32 like the f32 MFMA chain.
+// Six 32-cycle bf16 MFMAs per 32x32x16 step replace eight 64-cycle f32 MFMAs (2.7x fewer cycles).
+//
+// Orientation (as field_frag.hip): a layer's activations are a 32x32 accumulator tile
+// X[neuron][point], lane = point. The next layer Y = W X takes X as the B operand with no data
+// movement: the k-chunk c (0, 1) of a 32-row tile is registers 8c..8c+7, element i of lane half
+// h <-> neuron row 16c + 4h + (i&3) + 8(i>>2), and the weight A operand is read with the same
+// permutation from an LDS image of W (two ds_read_b64 per piece). The transposed chain
+// (gX = W^T gY) reads the SAME image with ds_read_b64_tr_b16 (gfx950's transposing LDS read).
+// Weight gradients dW = gY X^T sum over points (the lane index of both tiles): both tiles are
+// staged per wave as [point][neuron] bf16 images and read back transposed, then 6 MFMAs per
+// 16-point chunk accumulate into register-resident dW tiles (reduced once per block).
+//
+// LDS images (bf16, per piece, rows padded by 4 elements so that the 32 row reads of a lane half
+// hit 64 distinct banks): W0 [64][32], W1 [16][64], C0' [64][32] (cols: 0 sigma slot = 0,
+// 1..15 = C0 geo cols 16..30, 16..31 = C0 SH cols 0..15), C1 [64][64], C2 [16][64] (rows 3..15
+// zero).
+#include "field_common.h"
+
+namespace nerf {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+
+// 8 values of an operand fragment as three bf16 pieces; element i = half (i & 1) of dword i >> 1.
+struct S3 {
+    u32x4 p[3];
+};
+
+#define X6_MFMA(a, b, c) \
+    __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, (a)), __builtin_bit_cast(bf16x8, (b)), (c), 0, 0, 0)
+
+__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
+    const bf16x2 v = {(__bf16)a, (__bf16)b};   // v_cvt_pk_bf16_f32: round to nearest even
+    return __builtin_bit_cast(uint32_t, v);
+}
+
+__device__ __forceinline__ float lo_f(uint32_t p) { return __uint_as_float(p << 16); }
+__device__ __forceinline__ float hi_f(uint32_t p) { return __uint_as_float(p & 0xffff0000u); }
+
+// The empty asm statements keep each packed word opaque: otherwise the compiler rewrites
+// lo_f(pk(a, b)) as a second, single-value conversion of a (one extra VALU op per pair).
+__device__ __forceinline__ void split2(float a, float b, uint32_t& p0, uint32_t& p1, uint32_t& p2) {
+    p0 = pk_bf16(a, b);
+    asm("" : "+v"(p0));
+    const float ra = a - lo_f(p0), rb = b - hi_f(p0);      // exact
+    p1 = pk_bf16(ra, rb);
+    asm("" : "+v"(p1));
+    const float sa = ra - lo_f(p1), sb = rb - hi_f(p1);    // exact
+    p2 = pk_bf16(sa, sb);
+}
+
+// ReLU as one v_max_i32 (a negative float is a negative int; +0/-0 -> +0): relu16 of
+// field_common.h compiles to two v_max_f32 per element on MFMA results (a canonicalising max first).
+__device__ __forceinline__ void relu16i(floatx16& v) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int i = __float_as_int(v[r]);
+        v[r] = __int_as_float(i & ~(i >> 31));
+    }
+}
+
+__device__ __forceinline__ S3 split8(float v0, float v1, float v2, float v3, float v4, float v5, float v6, float v7) {
+    uint32_t a[4], b[4], c[4];
+    split2(v0, v1, a[0], b[0], c[0]);
+    split2(v2, v3, a[1], b[1], c[1]);
+    split2(v4, v5, a[2], b[2], c[2]);
+    split2(v6, v7, a[3], b[3], c[3]);
+    S3 s;
+    s.p[0] = u32x4{a[0], a[1], a[2], a[3]};
+    s.p[1] = u32x4{b[0], b[1], b[2], b[3]};
+    s.p[2] = u32x4{c[0], c[1], c[2], c[3]};
+    return s;
+}
+
+// chunk c of a 32-row accumulator tile: registers 8c .. 8c+7
+__device__ __forceinline__ S3 split_chunk(const floatx16& v, int c) {
+    return split8(v[8 * c], v[8 * c + 1], v[8 * c + 2], v[8 * c + 3], v[8 * c + 4], v[8 * c + 5], v[8 * c + 6],
+                  v[8 * c + 7]);
+}
+
+__device__ __forceinline__ S3 split_arr(const float* v) {
+    return split8(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]);
+}
+
+// acc += A B over one 16-deep k-chunk, fp32-accurate (six bf16 products; small terms first)
+__device__ __forceinline__ floatx16 mma6(const S3& A, const S3& B, floatx16 c) {
+    c = X6_MFMA(A.p[0], B.p[2], c);
+    c = X6_MFMA(A.p[2], B.p[0], c);
+    c = X6_MFMA(A.p[1], B.p[1], c);
+    c = X6_MFMA(A.p[0], B.p[1], c);
+    c = X6_MFMA(A.p[1], B.p[0], c);
+    c = X6_MFMA(A.p[0], B.p[0], c);
+    return c;
+}
+
+// ---- LDS images (bf16 elements) ----------------------------------------------------------------
+constexpr int S64 = 68, S32 = 36;            // padded row strides of 64- and 32-column matrices
+constexpr int IM_W0 = 0;                     // [64][S32]
+constexpr int IM_W1 = IM_W0 + 64 * S32;      // [16][S64]
+constexpr int IM_C0 = IM_W1 + 16 * S64;      // [64][S32]
+constexpr int IM_C1 = IM_C0 + 64 * S32;      // [64][S64]
+constexpr int IM_C2 = IM_C1 + 64 * S64;      // [16][S64]
+constexpr int IM_PIECE = IM_C2 + 16 * S64;   // 11,136 elements per piece
+constexpr int IM_BYTES = 3 * IM_PIECE * 2;   // 66,816 B
+// logical (unpadded) element index ranges of the five matrices, for the fill loop
+constexpr int L_W1 = 2048, L_C0 = 3072, L_C1 = 5120, L_C2 = 9216, L_END = 10240;
+// per-wave staging for the weight gradients: activations [32 points][64] and one 32-row
+// gradient tile [32 points][32], three pieces each
+constexpr int STA_PIECE = 32 * S64;
+constexpr int STG_PIECE = 32 * S32;
+constexpr int ST_WAVE = 3 * (STA_PIECE + STG_PIECE);       // 9,984 elements = 19,968 B
+constexpr int X6_BWD_LDS = IM_BYTES + 4 * ST_WAVE * 2;      // 146,688 B
+
+__device__ __forceinline__ float image_value(int idx, const nerf_mlp_weights& W) {
+    if (idx < L_W1) return W.w0[idx];                                     // [64][32]
+    if (idx < L_C0) return W.w1[idx - L_W1];                              // [16][64]
+    if (idx < L_C1) {
+        const int k = idx - L_C0, r = k >> 5, c = k & 31;
+        if (c == 0) return 0.f;                                           // sigma slot
+        return c < 16 ? W.c0[r * 31 + 15 + c] : W.c0[r * 31 + c - 16];    // geo 1..15 | SH 0..15
+    }
+    if (idx < L_C2) return W.c1[idx - L_C1];
+    const int k = idx - L_C2;
+    return (k >> 6) < 3 ? W.c2[k] : 0.f;
+}
+
+__device__ inline void fill_images(__bf16* img, const nerf_mlp_weights& W) {
+    for (int idx = threadIdx.x; idx < L_END; idx += blockDim.x) {
+        int off;
+        if (idx < L_W1) off = IM_W0 + (idx >> 5) * S32 + (idx & 31);
+        else if (idx < L_C0) { const int k = idx - L_W1; off = IM_W1 + (k >> 6) * S64 + (k & 63); }
+        else if (idx < L_C1) { const int k = idx - L_C0; off = IM_C0 + (k >> 5) * S32 + (k & 31); }
+        else if (idx < L_C2) { const int k = idx - L_C1; off = IM_C1 + (k >> 6) * S64 + (k & 63); }
+        else { const int k = idx - L_C2; off = IM_C2 + (k >> 6) * S64 + (k & 63); }
+        const float v = image_value(idx, W);
+        const __bf16 a0 = (__bf16)v;
+        const float r1 = v - (float)a0;
+        const __bf16 a1 = (__bf16)r1;
+        const __bf16 a2 = (__bf16)(r1 - (float)a1);
+        img[off] = a0;
+        img[IM_PIECE + off] = a1;
+        img[2 * IM_PIECE + off] = a2;
+    }
+}
+
+// A operand of Y = M X for the output row r of lane m: elements i <-> columns
+// col0 + (i&3) + 8(i>>2), col0 = 32t + 16c + 4h (two ds_read_b64 per piece).
+__device__ __forceinline__ S3 row_read(const __bf16* img, int base, int S, int r, int col0) {
+    S3 s;
+    const int o0 = base + r * S + col0;
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+        const u32x2 a = *reinterpret_cast<const u32x2*>(img + p * IM_PIECE + o0);
+        const u32x2 b = *reinterpret_cast<const u32x2*>(img + p * IM_PIECE + o0 + 8);
+        s.p[p] = u32x4{a.x, a.y, b.x, b.y};
+    }
+    return s;
+}
+
+// Operand whose k index runs over the ROWS of a row-major image: lane (m = lane&31, h = lane>>5)
+// gets column col0 + m at rows row0 + 4h + (i&3) + 8(i>>2) (row0 = 16 x chunk, col0 = 32 x tile).
+// Two ds_read_b64_tr_b16 per piece: 16-lane group g reads the 4 x 16 block at rows row0 + 4h
+// (+8), columns col0 + 16(g&1); lane 4q+p supplies row q, columns 4p..4p+3, and lane i of the
+// group receives column i of the 4 rows.
+__device__ __forceinline__ S3 tr_read(const __bf16* img, int piece, int base, int S, int row0, int col0, int lane) {
+    const int g = lane >> 4, il = lane & 15, q = il >> 2, p = il & 3, h = g >> 1;
+    const int oa = base + (row0 + 4 * h + q) * S + col0 + 16 * (g & 1) + 4 * p;
+    S3 s;
+#pragma unroll
+    for (int pc = 0; pc < 3; ++pc) {
+        const bf16x4 ta = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(img + pc * piece + oa));
+        const bf16x4 tb = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(img + pc * piece + oa + 8 * S));
+        const u32x2 a = __builtin_bit_cast(u32x2, ta), b = __builtin_bit_cast(u32x2, tb);
+        s.p[pc] = u32x4{a.x, a.y, b.x, b.y};
+    }
+    return s;
+}
+
+// Stage chunk c of a 32-row tile (lane = point j) into a [32 points][S] staging image at
+// columns col_t + 16c + 4h + (i&3) + 8(i>>2).
+__device__ __forceinline__ void stage(__bf16* st, int piece, int S, const S3& s, int col_t, int c, int j, int h) {
+    const int o0 = j * S + col_t + 16 * c + 4 * h;
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+        *reinterpret_cast<u32x2*>(st + p * piece + o0) = u32x2{s.p[p][0], s.p[p][1]};
+        *reinterpret_cast<u32x2*>(st + p * piece + o0 + 8) = u32x2{s.p[p][2], s.p[p][3]};
+    }
+}
+
+__device__ __forceinline__ void stage_act(__bf16* stA, const S3& s, int t, int c, int j, int h) {
+    stage(stA, STA_PIECE, S64, s, 32 * t, c, j, h);
+}
+
+__device__ __forceinline__ void stage_grad(__bf16* stG, const S3& s, int c, int j, int h) {
+    stage(stG, STG_PIECE, S32, s, 0, c, j, h);
+}
+
+// An opaque zero, redefined every tile: the weight images are loop-invariant, and without it the
+// compiler hoists every fragment read out of the tile loop (288 registers of fragments -> spills).
+__device__ __forceinline__ int opaque_zero() {
+    int z = 0;
+    asm volatile("" : "+v"(z));
+    return z;
+}
+
+// Between staging writes and the transposed reads of other lanes of the SAME wave: a wave's LDS
+// instructions execute in issue order, so only the compiler must not reorder them (no s_waitcnt,
+// no scheduling barrier for the VALU/MFMA work around it).
+#define X6_WAVE_SYNC() asm volatile("" ::: "memory")
+
+// dW[t-tile][u] += sum over the 32 staged points of G[m][pt] A[32u + n][pt] (MFMAs chained onto
+// the register-resident sums; a per-tile partial joined with a VALU fp32 add measured the same
+// error and costs three VALU ops per accumulator element)
+template <int NU>
+__device__ __forceinline__ void wgrad_tile(floatx16 (&acc)[NU], const __bf16* stG, const __bf16* stA, int lane) {
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        const S3 A = tr_read(stG, STG_PIECE, 0, S32, 16 * c, 0, lane);
+#pragma unroll
+        for (int u = 0; u < NU; ++u) acc[u] = mma6(A, tr_read(stA, STA_PIECE, 0, S64, 16 * c, 32 * u, lane), acc[u]);
+    }
+}
+
+// ---- per-tile inputs ---------------------------------------------------------------------------
+// x[8c + i] = feature 16c + 4h + (i&3) + 8(i>>2); shv[i] = SH 4h + (i&3) + 8(i>>2)
+struct InX6 {
+    float x[16];
+    float shv[8];
+    uint32_t pt;    // 32-bit indexing (launch_* checks the sizes): one VGPR per address, saddr forms
+    bool valid;
+};
+
+__device__ __forceinline__ void load_x6(const MlpArgs& a, uint32_t pt, bool valid, int h, float (&x)[16], int zero) {
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const int level = 8 * c + 4 * q + 2 * h + e;   // features 2 level, 2 level + 1
+                float2 v = make_float2(0.f, 0.f);
+                if (valid) v = *reinterpret_cast<const float2*>(a.feat + (uint32_t)(pt * (uint32_t)a.sp + level * (uint32_t)a.sl + zero));
+                x[8 * c + 4 * q + 2 * e] = v.x;
+                x[8 * c + 4 * q + 2 * e + 1] = v.y;
+            }
+}
+
+// shv[i] = SH coefficient 4h + (i&3) + 8(i>>2) of the point's view direction
+__device__ __forceinline__ void load_sh6(const MlpArgs& a, uint32_t pt, bool valid, int h, float (&shv)[8], int zero) {
+    float o[16];
+    if (a.viewdirs) {
+        if (valid) {
+            const uint32_t ray = pt / (uint32_t)a.spr * 3u + zero;
+            sh4_eval(a.viewdirs[ray], a.viewdirs[ray + 1], a.viewdirs[ray + 2], o);
+        } else {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) o[k] = 0.f;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) o[k] = valid ? a.sh[(uint32_t)(pt * (uint32_t)a.sh_stride + k + zero)] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {   // static indices + one select (a dynamic o[4h + k] is a 16-way select chain)
+        const int k = (i & 3) + 8 * (i >> 2);
+        shv[i] = h ? o[k + 4] : o[k];
+    }
+}
+
+__device__ __forceinline__ void load_in_x6(const MlpArgs& a, int64_t tile, int j, int h, InX6& in) {
+    in.pt = (uint32_t)(tile * 32 + j);
+    in.valid = tile * 32 + j < a.P;
+    load_x6(a, in.pt, in.valid, h, in.x, 0);
+    load_sh6(a, in.pt, in.valid, h, in.shv, 0);
+}
+
+struct ActX6 {
+    floatx16 h1[2];
+    floatx16 o;
+    floatx16 h2[2];
+    floatx16 h3[2];
+    uint32_t m1;    // A-CAQ: ReLU mask of layer 0 before the activation quantizer
+};
+
+// layer 0: h1 = relu(W0 x) (A-CAQ: Q(relu(.)), m1 = its ReLU mask); lane = point j, half h
+template <bool QUANT>
+__device__ __forceinline__ void layer0(const __bf16* img, const float (&x)[16], floatx16 (&h1)[2], uint32_t& m1,
+                                       int lane, const QuantRec& aq) {
+    const int m = lane & 31, h = lane >> 5;
+    h1[0] = h1[1] = zero16();
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        const S3 xb = split_arr(x + 8 * c);
+#pragma unroll
+        for (int t = 0; t < 2; ++t) h1[t] = mma6(row_read(img, IM_W0, S32, 32 * t + m, 16 * c + 4 * h), xb, h1[t]);
+    }
+    m1 = 0;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        relu16i(h1[t]);
+        if constexpr (QUANT) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) m1 |= (h1[t][r] > 0.f ? 1u : 0u) << (16 * t + r);
+            fake_quant16(h1[t], aq);
+        }
+    }
+}
+
+// forward chain up to h3 (and rgb when need_rgb)
+template <bool QUANT>
+__device__ __forceinline__ void fwd_chain(const __bf16* img, const InX6& in, ActX6& f, floatx16& rgb, int lane,
+                                          bool need_rgb, const QuantRec& aq) {
+    const int m = lane & 31, h = lane >> 5;
+    layer0<QUANT>(img, in.x, f.h1, f.m1, lane, aq);
+    // L1: o = W1 h1 (rows 16..31 of the tile are never read)
+    f.o = zero16();
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+            f.o = mma6(row_read(img, IM_W1, S64, m & 15, 32 * t + 16 * c + 4 * h), split_chunk(f.h1[t], c), f.o);
+    // C0: h2 = relu(C0' [o rows 0..15 ; sh])
+    f.h2[0] = f.h2[1] = zero16();
+    {
+        const S3 O0 = split_chunk(f.o, 0);
+#pragma unroll
+        for (int t = 0; t < 2; ++t) f.h2[t] = mma6(row_read(img, IM_C0, S32, 32 * t + m, 4 * h), O0, f.h2[t]);
+    }
+    {
+        const S3 SH = split_arr(in.shv);
+#pragma unroll
+        for (int t = 0; t < 2; ++t) f.h2[t] = mma6(row_read(img, IM_C0, S32, 32 * t + m, 16 + 4 * h), SH, f.h2[t]);
+    }
+    relu16i(f.h2[0]); relu16i(f.h2[1]);
+    // C1: h3 = relu(C1 h2)
+    f.h3[0] = f.h3[1] = zero16();
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            const S3 hb = split_chunk(f.h2[t], c);
+#pragma unroll
+            for (int to = 0; to < 2; ++to)
+                f.h3[to] = mma6(row_read(img, IM_C1, S64, 32 * to + m, 32 * t + 16 * c + 4 * h), hb, f.h3[to]);
+        }
+    relu16i(f.h3[0]); relu16i(f.h3[1]);
+    if (!need_rgb) return;
+    // C2: rgb = C2 h3 (rows 0..2 used)
+    rgb = zero16();
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+            rgb = mma6(row_read(img, IM_C2, S64, m & 15, 32 * t + 16 * c + 4 * h), split_chunk(f.h3[t], c), rgb);
+}
+
+// ================================================================ forward kernel
+template <bool QUANT>
+__global__ void __launch_bounds__(256, 2) mlp_fwd_x6_kernel(MlpArgs a) {
+    __shared__ __attribute__((aligned(16))) __bf16 img[3 * IM_PIECE];
+    fill_images(img, a.W);
+    __syncthreads();
+    const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
+    QuantRec aq{};
+    if constexpr (QUANT) aq = *a.aq;
+    const int64_t n_tiles = (a.P + 31) / 32;
+    for (int64_t tile = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); tile < n_tiles; tile += (int64_t)gridDim.x * 4) {
+        InX6 in;
+        load_in_x6(a, tile, j, h, in);
+        ActX6 f;
+        floatx16 rgb;
+        fwd_chain<QUANT>(img + opaque_zero(), in, f, rgb, lane, true, aq);
+        if (h == 0 && in.valid) {
+            const bool keep = a.keep ? a.keep[in.pt] != 0 : true;
+            *reinterpret_cast<float4*>(a.raw + 4u * in.pt) = make_float4(rgb[0], rgb[1], rgb[2], keep ? f.o[0] : 0.f);
+        }
+        if (a.geo_out && in.valid) {
+#pragma unroll
+            for (int r = 0; r < 8; ++r) a.geo_out[16u * in.pt + row_of(r, h)] = f.o[r];
+        }
+    }
+}
+
+// ================================================================ backward kernel
+template <bool QUANT>
+__global__ void __launch_bounds__(256, 1) mlp_bwd_x6_kernel(MlpArgs a) {
+    __shared__ __attribute__((aligned(16))) __bf16 lds[X6_BWD_LDS / 2];
+    __bf16* img = lds;
+    const int wv = threadIdx.x >> 6;
+    __bf16* stA = lds + 3 * IM_PIECE + wv * ST_WAVE;
+    __bf16* stG = stA + 3 * STA_PIECE;
+    fill_images(img, a.W);
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
+    QuantRec aq{};
+    if constexpr (QUANT) aq = *a.aq;
+    floatx16 dC2[2], dC1[2][2], dC0[2][1], dW1[2], dW0[2][1];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        dC2[i] = zero16(); dW1[i] = zero16(); dC0[i][0] = zero16(); dW0[i][0] = zero16();
+        dC1[i][0] = zero16(); dC1[i][1] = zero16();
+    }
+
+    const int64_t n_tiles = (a.P + 31) / 32;
+    for (int64_t tile = (int64_t)blockIdx.x * 4 + wv; tile < n_tiles; tile += (int64_t)gridDim.x * 4) {
+        const __bf16* imt = img + opaque_zero();
+        InX6 in;
+        load_in_x6(a, tile, j, h, in);
+        ActX6 f;
+        floatx16 unused;
+        fwd_chain<QUANT>(imt, in, f, unused, lane, false, aq);
+
+        const float4 g4 = in.valid ? *reinterpret_cast<const float4*>(a.graw + 4u * in.pt) : make_float4(0.f, 0.f, 0.f, 0.f);
+        const bool keep = in.valid && (a.keep ? a.keep[in.pt] != 0 : true);
+        const float gsig = keep ? g4.w : 0.f;
+
+        // ---- C2: ga3 = (C2^T g_rgb) * (h3 > 0); dC2 += g_rgb h3^T
+        floatx16 ga3[2];
+        {
+            const S3 GR = h ? split8(0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f)
+                            : split8(g4.x, g4.y, g4.z, 0.f, 0.f, 0.f, 0.f, 0.f);   // rows 0..2 of chunk 0
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                ga3[t] = mma6(tr_read(imt, IM_PIECE, IM_C2, S64, 0, 32 * t, lane), GR, zero16());
+#pragma unroll
+                for (int r = 0; r < 16; ++r) ga3[t][r] = f.h3[t][r] > 0.f ? ga3[t][r] : 0.f;
+            }
+            stage_grad(stG, GR, 0, j, h);      // columns 16..31 stay stale: they only reach dC2 rows >= 16
+        }
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int c = 0; c < 2; ++c) stage_act(stA, split_chunk(f.h3[t], c), t, c, j, h);
+        X6_WAVE_SYNC();
+        wgrad_tile<2>(dC2, stG, stA, lane);
+        X6_WAVE_SYNC();
+
+        // ---- C1: ga2 = (C1^T ga3) * (h2 > 0); dC1 += ga3 h2^T
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int c = 0; c < 2; ++c) stage_act(stA, split_chunk(f.h2[t], c), t, c, j, h);
+        floatx16 ga2[2];
+        ga2[0] = ga2[1] = zero16();
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                const S3 g = split_chunk(ga3[t], c);
+                stage_grad(stG, g, c, j, h);
+#pragma unroll
+                for (int ti = 0; ti < 2; ++ti)
+                    ga2[ti] = mma6(tr_read(imt, IM_PIECE, IM_C1, S64, 32 * t + 16 * c, 32 * ti, lane), g, ga2[ti]);
+            }
+            X6_WAVE_SYNC();
+            wgrad_tile<2>(dC1[t], stG, stA, lane);
+            X6_WAVE_SYNC();
+        }
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) ga2[t][r] = f.h2[t][r] > 0.f ? ga2[t][r] : 0.f;
+
+        // ---- C0: go = C0'^T ga2 (rows 0..15: o = [sigma, geo]; rows 16..31: d sh); dC0 += ga2 [o ; sh]^T
+        // The accumulator is seeded: row 0 (sigma) with g_sigma (C0' column 0 is zero) and, with
+        // the normals head, rows 1..15 with its d geo.
+        floatx16 go = zero16();
+        if (h == 0) go[0] = gsig;
+        if (a.dgeo && in.valid) {
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+                const int row = row_of(r, h);
+                if (row >= 1) go[r] = a.dgeo[16u * in.pt + row];
+            }
+        }
+        stage_act(stA, split_chunk(f.o, 0), 0, 0, j, h);
+        {   // SH re-evaluated (as h1 below, not held through the C2/C1 stages)
+            float shv[8];
+            load_sh6(a, in.pt, in.valid, h, shv, opaque_zero());
+            stage_act(stA, split_arr(shv), 0, 1, j, h);
+        }
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                const S3 g = split_chunk(ga2[t], c);
+                stage_grad(stG, g, c, j, h);
+                go = mma6(tr_read(imt, IM_PIECE, IM_C0, S32, 32 * t + 16 * c, 0, lane), g, go);
+            }
+            X6_WAVE_SYNC();
+            wgrad_tile<1>(dC0[t], stG, stA, lane);
+            X6_WAVE_SYNC();
+        }
+        if (a.dsh && in.valid) {
+#pragma unroll
+            for (int r = 8; r < 16; ++r) a.dsh[16u * in.pt + row_of(r, h) - 16] = go[r];
+        }
+
+        // ---- W1: ga1 = (W1^T go) * (h1 > 0); dW1 += go h1^T
+        // h1 is recomputed here from a reload of x (24 MFMAs) rather than held in 32 registers
+        // through the C-layer stages, where the register peak is (the reload's opaque offset keeps
+        // the compiler from reusing the first load's registers instead)
+        float xr[16];
+        load_x6(a, in.pt, in.valid, h, xr, opaque_zero());
+        floatx16 h1[2];
+        uint32_t m1;
+        layer0<QUANT>(imt, xr, h1, m1, lane, aq);
+        floatx16 ga1[2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int c = 0; c < 2; ++c) stage_act(stA, split_chunk(h1[t], c), t, c, j, h);
+        {
+            const S3 GO = split_chunk(go, 0);
+            stage_grad(stG, GO, 0, j, h);      // columns 16..31 stale: they only reach dW1 rows >= 16
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                floatx16 acc = mma6(tr_read(imt, IM_PIECE, IM_W1, S64, 0, 32 * t, lane), GO, zero16());
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const bool on = QUANT ? ((m1 >> (16 * t + r)) & 1u) != 0u : h1[t][r] > 0.f;
+                    acc[r] = on ? acc[r] : 0.f;
+                }
+                ga1[t] = acc;
+            }
+        }
+        X6_WAVE_SYNC();
+        wgrad_tile<2>(dW1, stG, stA, lane);
+        X6_WAVE_SYNC();
+
+        // ---- W0: gx = W0^T ga1 (-> d features); dW0 += ga1 x^T
+        stage_act(stA, split_arr(xr), 0, 0, j, h);
+        stage_act(stA, split_arr(xr + 8), 0, 1, j, h);
+        floatx16 gx = zero16();
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                const S3 g = split_chunk(ga1[t], c);
+                stage_grad(stG, g, c, j, h);
+                gx = mma6(tr_read(imt, IM_PIECE, IM_W0, S32, 32 * t + 16 * c, 0, lane), g, gx);
+            }
+            X6_WAVE_SYNC();
+            wgrad_tile<1>(dW0[t], stG, stA, lane);
+            X6_WAVE_SYNC();
+        }
+        if (a.dfeat && in.valid) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int fi = row_of(r, h);
+                a.dfeat[in.pt * (uint32_t)a.sp + (fi >> 1) * (uint32_t)a.sl + (fi & 1)] = gx[r];
+            }
+        }
+    }
+
+    // ---- block reduction of the weight gradients (LDS fp32 atomics), one global flush per block
+    __syncthreads();
+    float* gw = reinterpret_cast<float*>(lds);
+    for (int i = threadIdx.x; i < GW_TOTAL; i += blockDim.x) gw[i] = 0.f;
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int rr = row_of(r, h);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            if (rr < 3) atomicAdd(gw + GW_C2 + rr * 64 + 32 * u + j, dC2[u][r]);
+            if (rr < 16) atomicAdd(gw + GW_W1 + rr * 64 + 32 * u + j, dW1[u][r]);
+        }
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const int row = 32 * t + rr;
+#pragma unroll
+            for (int u = 0; u < 2; ++u) atomicAdd(gw + GW_C1 + row * 64 + 32 * u + j, dC1[t][u][r]);
+            // C0' column j: 0 sigma slot (no weight), 1..15 -> C0 col 15 + j, 16..31 -> C0 col j - 16
+            if (j != 0) atomicAdd(gw + GW_C0 + row * 31 + (j < 16 ? 15 + j : j - 16), dC0[t][0][r]);
+            atomicAdd(gw + GW_W0 + row * 32 + j, dW0[t][0][r]);
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < GW_TOTAL; i += blockDim.x) {
+        float* dst;
+        int k;
+        if (i < GW_W1) { dst = a.G.w0; k = i; }
+        else if (i < GW_C0) { dst = a.G.w1; k = i - GW_W1; }
+        else if (i < GW_C1) { dst = a.G.c0; k = i - GW_C0; }
+        else if (i < GW_C2) { dst = a.G.c1; k = i - GW_C1; }
+        else { dst = a.G.c2; k = i - GW_C2; }
+        const float v = gw[i];
+        if (v != 0.f) __hip_atomic_fetch_add(dst + k, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+static bool fits_u32(const MlpArgs& a) {
+    const int64_t lim = (int64_t)1 << 31;
+    return (a.P + 32) * std::max<int64_t>({a.sp, a.sl, a.sh_stride, 16}) < lim && 16 * a.sl < lim;
+}
+
+int launch_mlp_fwd_x6(const MlpArgs& a, hipStream_t stream) {
+    NERF_REQUIRE(fits_u32(a), "mlp_fwd(x6): %lld points exceed 32-bit indexing", (long long)a.P);
+    const int64_t tiles = (a.P + 31) / 32;
+    const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((tiles + 3) / 4, 256 * 4));
+    if (a.aq)
+        hipLaunchKernelGGL(mlp_fwd_x6_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, stream, a);
+    else
+        hipLaunchKernelGGL(mlp_fwd_x6_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, stream, a);
+    NERF_CHECK_LAUNCH("mlp_fwd(x6)");
+    return NERF_OK;
+}
+
+int launch_mlp_bwd_x6(const MlpArgs& a, hipStream_t stream) {
+    NERF_REQUIRE(fits_u32(a), "mlp_bwd(x6): %lld points exceed 32-bit indexing", (long long)a.P);
+    const int64_t tiles = (a.P + 31) / 32;
+    const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((tiles + 3) / 4, 256));
+    if (a.aq)
+        hipLaunchKernelGGL(mlp_bwd_x6_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, stream, a);
+    else
+        hipLaunchKernelGGL(mlp_bwd_x6_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, stream, a);
+    NERF_CHECK_LAUNCH("mlp_bwd(x6)");
+    return NERF_OK;
+}
+
+}  // namespace nerf
