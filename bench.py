@@ -28,6 +28,9 @@ import torch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: f32 matrix (v_mfma_f32_32x32x2_f32) dense peak
+# The default MLP kernels (csrc/field_x6.hip) form each fp32-accurate product from six bf16 MFMA
+# products, so their arithmetic peak is the dense bf16 rate (~2.5 PFLOP/s) / 6.
+X6_PEAK_TFLOPS = 2500.0 / 6
 
 # Algorithmic cost per unit of each kernel: bytes (HBM-bound) or FLOPs (MFMA).
 #   hash fwd : per point  16 levels x 8 corners x 8 B gathered + 12 B xyz + 128 B features + 1 B keep
@@ -50,8 +53,8 @@ UNIT_COST = {
 KERNEL_SYMBOLS = {
     "nerf_hash_encode_fwd": ["nerf::hash_encode_fwd_kernel<false>"],
     "nerf_hash_encode_bwd_ws": ["nerf::hash_encode_bwd_kernel<3>", "nerf::hash_bwd_owner_kernel"],
-    "nerf_mlp_fwd": ["nerf::mlp_fwd_frag_kernel<false>"],
-    "nerf_mlp_bwd": ["nerf::mlp_bwd_frag_kernel<false>"],
+    "nerf_mlp_fwd": ["nerf::mlp_fwd_x6_kernel<false>"],
+    "nerf_mlp_bwd": ["nerf::mlp_bwd_x6_kernel<false>"],
 }
 TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r01d_traffic.json")
 
@@ -285,9 +288,13 @@ def main():
                             "per_launch_units": units, "algorithmic_bytes_per_unit": per_unit}
             else:
                 ach = per_unit * units / avg_s / 1e12
-                roofline = {"kernel": dom, "bound": "mfma", "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
-                            "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
-                            "per_launch_units": units, "algorithmic_flops_per_unit": per_unit}
+                x6 = os.environ.get("NERF_MLP", "3")[:1] not in ("1", "2")
+                peak = X6_PEAK_TFLOPS if x6 else FP32_MFMA_PEAK_TFLOPS
+                roofline = {"kernel": dom, "bound": "mfma", "achieved": round(ach, 2), "peak": round(peak, 1),
+                            "unit": "TFLOP/s", "frac": round(ach / peak, 4), "traffic": traffic,
+                            "per_launch_units": units, "algorithmic_flops_per_unit": per_unit,
+                            "peak_note": ("bf16 dense MFMA peak / 6: each fp32-accurate product is six bf16 products "
+                                          "(csrc/field_x6.hip)") if x6 else "f32 MFMA dense peak"}
             if traffic is not None:
                 roofline["traffic_source"] = ("profiles/r01d_traffic.json: rocprofv3 FETCH_SIZE (x2, gfx950 wide-read "
                                               "correction) + WRITE_SIZE per call, separate PMC passes of this bench")

@@ -355,14 +355,13 @@ int launch_mlp_fwd_x6(const MlpArgs& a, hipStream_t stream);     // field_x6.hip
 int launch_mlp_bwd_x6(const MlpArgs& a, hipStream_t stream);
 
 // MLP kernel generation, for A/B runs: NERF_MLP=1 the first version (f32 MFMA, LDS weight
-// images), NERF_MLP=2 the fragment-stationary f32-MFMA version (field_frag.hip) for forward and
-// backward, NERF_MLP=3 the fp32-accurate bf16x6 version (field_x6.hip) for both. Default: bf16x6
-// forward (1.27x the f32 forward) + f32-MFMA backward (the bf16x6 backward measured 7 % slower:
-// DESIGN.md §4).
+// images), NERF_MLP=2 the fragment-stationary f32-MFMA version (field_frag.hip); default (3): the
+// fp32-accurate bf16x6 version (field_x6.hip), 1.27x (forward) and 1.19x (backward) the f32-MFMA
+// kernels in the lego training step.
 static int mlp_version() {
     const char* e = getenv("NERF_MLP");
     if (e && e[0] >= '1' && e[0] <= '3') return e[0] - '0';
-    return 0;
+    return 3;
 }
 
 static bool use_frag_mlp() { return mlp_version() != 1; }
@@ -370,7 +369,7 @@ static bool use_frag_mlp() { return mlp_version() != 1; }
 static int launch_mlp_fwd_default(const MlpArgs& a, hipStream_t stream) {
     // the activation-quantizer calibration launch (layer 0 only) stays on the f32 path
     const int v = mlp_version();
-    if ((v == 0 || v == 3) && !a.act_minmax) return launch_mlp_fwd_x6(a, stream);
+    if (v == 3 && !a.act_minmax) return launch_mlp_fwd_x6(a, stream);
     return launch_mlp_fwd_frag(a, stream);
 }
 

@@ -217,10 +217,11 @@ __device__ __forceinline__ int opaque_zero() {
     return z;
 }
 
-// Between staging writes and the transposed reads of other lanes of the SAME wave: a wave's LDS
-// instructions execute in issue order, so only the compiler must not reorder them (no s_waitcnt,
-// no scheduling barrier for the VALU/MFMA work around it).
-#define X6_WAVE_SYNC() asm volatile("" ::: "memory")
+// Between staging writes and the transposed reads of other lanes of the SAME wave nothing is
+// needed: a wave's LDS instructions execute in issue order, and the compiler cannot reorder a
+// staging store and a transposed load of the same image (lane-dependent offsets: may alias). An
+// asm barrier here would end the scheduling region and expose every LDS latency.
+#define X6_WAVE_SYNC() ((void)0)
 
 // dW[t-tile][u] += sum over the 32 staged points of G[m][pt] A[32u + n][pt] (MFMAs chained onto
 // the register-resident sums; a per-tile partial joined with a VALU fp32 add measured the same
@@ -252,28 +253,28 @@ __device__ __forceinline__ void load_x6(const MlpArgs& a, uint32_t pt, bool vali
 #pragma unroll
             for (int e = 0; e < 2; ++e) {
                 const int level = 8 * c + 4 * q + 2 * h + e;   // features 2 level, 2 level + 1
-                float2 v = make_float2(0.f, 0.f);
-                if (valid) v = *reinterpret_cast<const float2*>(a.feat + (uint32_t)(pt * (uint32_t)a.sp + level * (uint32_t)a.sl + zero));
-                x[8 * c + 4 * q + 2 * e] = v.x;
-                x[8 * c + 4 * q + 2 * e + 1] = v.y;
+                // branch-free: a tail lane loads the last point and zeroes it (no basic-block split,
+                // so the scheduler keeps one region for the whole tile)
+                const uint32_t pc = valid ? pt : (uint32_t)(a.P - 1);
+                const float2 v = *reinterpret_cast<const float2*>(a.feat + (uint32_t)(pc * (uint32_t)a.sp + level * (uint32_t)a.sl + zero));
+                x[8 * c + 4 * q + 2 * e] = valid ? v.x : 0.f;
+                x[8 * c + 4 * q + 2 * e + 1] = valid ? v.y : 0.f;
             }
 }
 
 // shv[i] = SH coefficient 4h + (i&3) + 8(i>>2) of the point's view direction
 __device__ __forceinline__ void load_sh6(const MlpArgs& a, uint32_t pt, bool valid, int h, float (&shv)[8], int zero) {
     float o[16];
+    const uint32_t pc = valid ? pt : (uint32_t)(a.P - 1);
     if (a.viewdirs) {
-        if (valid) {
-            const uint32_t ray = pt / (uint32_t)a.spr * 3u + zero;
-            sh4_eval(a.viewdirs[ray], a.viewdirs[ray + 1], a.viewdirs[ray + 2], o);
-        } else {
-#pragma unroll
-            for (int k = 0; k < 16; ++k) o[k] = 0.f;
-        }
+        const uint32_t ray = pc / (uint32_t)a.spr * 3u + zero;
+        sh4_eval(a.viewdirs[ray], a.viewdirs[ray + 1], a.viewdirs[ray + 2], o);
     } else {
 #pragma unroll
-        for (int k = 0; k < 16; ++k) o[k] = valid ? a.sh[(uint32_t)(pt * (uint32_t)a.sh_stride + k + zero)] : 0.f;
+        for (int k = 0; k < 16; ++k) o[k] = a.sh[(uint32_t)(pc * (uint32_t)a.sh_stride + k + zero)];
     }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) o[k] = valid ? o[k] : 0.f;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {   // static indices + one select (a dynamic o[4h + k] is a 16-way select chain)
         const int k = (i & 3) + 8 * (i >> 2);
@@ -425,7 +426,8 @@ __global__ void __launch_bounds__(256, 1) mlp_bwd_x6_kernel(MlpArgs a) {
         floatx16 unused;
         fwd_chain<QUANT>(imt, in, f, unused, lane, false, aq);
 
-        const float4 g4 = in.valid ? *reinterpret_cast<const float4*>(a.graw + 4u * in.pt) : make_float4(0.f, 0.f, 0.f, 0.f);
+        float4 g4 = *reinterpret_cast<const float4*>(a.graw + 4u * (in.valid ? in.pt : (uint32_t)(a.P - 1)));
+        if (!in.valid) g4 = make_float4(0.f, 0.f, 0.f, 0.f);
         const bool keep = in.valid && (a.keep ? a.keep[in.pt] != 0 : true);
         const float gsig = keep ? g4.w : 0.f;
 
@@ -605,9 +607,10 @@ __global__ void __launch_bounds__(256, 1) mlp_bwd_x6_kernel(MlpArgs a) {
     }
 }
 
+// every element index the kernels form (feat, sh, raw/graw, geo/dgeo/dsh, dfeat) stays below 2^31
 static bool fits_u32(const MlpArgs& a) {
     const int64_t lim = (int64_t)1 << 31;
-    return (a.P + 32) * std::max<int64_t>({a.sp, a.sl, a.sh_stride, 16}) < lim && 16 * a.sl < lim;
+    return a.P * a.sp + 16 * a.sl < lim && a.P * a.sh_stride + 16 < lim && 16 * (a.P + 32) < lim;
 }
 
 int launch_mlp_fwd_x6(const MlpArgs& a, hipStream_t stream) {
