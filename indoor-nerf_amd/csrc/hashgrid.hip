@@ -167,8 +167,8 @@ constexpr uint32_t kSkip = 0xFFFFFFFFu;
 // replaces the memory-side atomics: this kernel writes each (row, d feat) entry into a per-chunk
 // region sorted by owner slice (plain stores), and hash_bwd_owner_kernel sums each slice in LDS.
 constexpr int kChunkCap = 256 * 8;        // entries per 256-point chunk (8 corners per point)
-constexpr int kMaxSliceLog2 = 13;         // owner slice: 2^13 rows x 16 B (fp64 pair) = 128 KiB of LDS
-constexpr int kMaxOwnersLog2 = 6;
+constexpr int kMaxSliceLog2 = 13;         // owner slice: up to 2^13 rows x 16 B (fp64 pair) = 128 KiB of LDS
+constexpr int kMaxOwnersLog2 = 7;
 constexpr int kMaxOwners = 1 << kMaxOwnersLog2;
 
 // MODE 0: per-lane atomics; 1: coalesced re-issue (default); 2: as 1 without the atomics (cost floor,
@@ -253,19 +253,26 @@ __global__ void __launch_bounds__(256) hash_encode_bwd_kernel(
                                                                 : kSkip;
         }
         __syncthreads();
-        if (threadIdx.x < 64) {   // exclusive scan of <= 64 counters in wave 0
-            const uint32_t v = lane < n_own ? s_cnt[lane] : 0u;
-            uint32_t inc = v;
+        if (threadIdx.x < 64) {   // exclusive scan of <= 128 counters in wave 0, two per lane
+            const int o0 = 2 * lane, o1 = 2 * lane + 1;
+            const uint32_t v0 = o0 < n_own ? s_cnt[o0] : 0u, v1 = o1 < n_own ? s_cnt[o1] : 0u;
+            uint32_t inc = v0 + v1;
 #pragma unroll
             for (int o = 1; o < 64; o <<= 1) {
                 const uint32_t t = __shfl_up(inc, o, 64);
                 if (lane >= o) inc += t;
             }
-            if (lane < n_own) {
-                s_start[lane] = inc - v;
-                hp.bin_seg[((size_t)lvl * n_own + lane) * hp.nchunks + blockIdx.x] = (inc - v) | (v << 16);
+            const uint32_t ex0 = inc - v0 - v1, ex1 = ex0 + v0;
+            if (o0 < n_own) {
+                s_start[o0] = ex0;
+                hp.bin_seg[((size_t)lvl * n_own + o0) * hp.nchunks + blockIdx.x] = ex0 | (v0 << 16);
             }
-            if (lane == n_own - 1) s_start[n_own] = inc;
+            if (o1 < n_own) {
+                s_start[o1] = ex1;
+                hp.bin_seg[((size_t)lvl * n_own + o1) * hp.nchunks + blockIdx.x] = ex1 | (v1 << 16);
+            }
+            if (o0 == n_own - 1) s_start[n_own] = ex1;
+            if (o1 == n_own - 1) s_start[n_own] = ex1 + v1;
         }
         __syncthreads();
         const uint32_t smask = (1u << hp.slice_log2) - 1u;
@@ -324,14 +331,16 @@ __global__ void __launch_bounds__(256) hash_encode_bwd_kernel(
 // step the entries of a window of chunks are numbered consecutively (exclusive scan of the segment
 // counts in LDS) and every lane takes every 64th entry, 8 per batch: 16 global loads in flight per
 // lane, all lanes busy whatever the segment lengths.
-constexpr int kOwnerThreads = 1024;
-constexpr int kOwnerWindow = 2048;   // chunks per window (LDS: 8 KiB prefix + 4 KiB starts)
-
-__global__ void __launch_bounds__(kOwnerThreads) hash_bwd_owner_kernel(HashGradParams hp) {
+// SLICE_LOG2 / THREADS: 2^13-row slices with one 1024-thread block per CU (128 KiB of LDS), or
+// 2^12-row slices (64 KiB) so that two blocks share a CU (NERF_HASH_OWNER, owner_variant()).
+template <int SLICE_LOG2, int THREADS>
+__global__ void __launch_bounds__(THREADS) hash_bwd_owner_kernel(HashGradParams hp) {
+    constexpr int kOwnerThreads = THREADS;
+    constexpr int kOwnerWindow = 2 * THREADS;   // chunks per window: 2 per thread in the scan
     // fp64 accumulators: ds_add_f64 runs ~14x the rate of ds_add_f32 on gfx950 (tools/
     // lds_atomic_bench.hip: 2.24 vs 0.165 row updates per clock per CU, random rows), and the
     // slice total is rounded to fp32 once.
-    __shared__ __attribute__((aligned(16))) double2 s_slice[1 << kMaxSliceLog2];
+    __shared__ __attribute__((aligned(16))) double2 s_slice[1 << SLICE_LOG2];
     __shared__ uint32_t s_pre[kOwnerWindow + 1];
     __shared__ uint16_t s_beg[kOwnerWindow];
     __shared__ uint32_t s_wsum[kOwnerThreads / 64];
@@ -441,10 +450,19 @@ struct BinPlan {
     size_t off_h, off_g, off_off, total;   // byte offsets in the workspace
 };
 
-// Binned path for log2_T in [1, kMaxSliceLog2 + log2(kMaxOwners)]: slices of min(2^13, T) rows.
+// owner-pass geometry: 1 = 2^13-row slices, 1024 threads, one block per CU (default);
+// 0 = 2^12-row slices, 512 threads, two blocks per CU (NERF_HASH_OWNER=12; A/B in the lego step:
+// 0.41 vs 0.34 ms per backward, the doubled per-owner segment scans outweigh the overlap)
+static int owner_variant() {
+    const char* e = getenv("NERF_HASH_OWNER");
+    return (e && e[0] == '1' && e[1] == '2') ? 0 : 1;
+}
+
+// Binned path for log2_T in [1, slice + log2(kMaxOwners)]: slices of min(2^slice, T) rows.
 static bool make_bin_plan(int n_levels, int log2_T, int64_t n_points, BinPlan& B) {
-    if (log2_T < 1 || log2_T > kMaxSliceLog2 + kMaxOwnersLog2 || n_points < 0) return false;
-    B.slice_log2 = log2_T < kMaxSliceLog2 ? log2_T : kMaxSliceLog2;
+    const int slice = owner_variant() == 1 ? 13 : 12;
+    if (log2_T < 1 || log2_T > slice + kMaxOwnersLog2 || n_points < 0) return false;
+    B.slice_log2 = log2_T < slice ? log2_T : slice;
     B.owner_log2 = log2_T - B.slice_log2;
     B.nchunks = (int)((n_points + 255) / 256);
     const size_t entries = (size_t)n_levels * B.nchunks * kChunkCap;
@@ -578,8 +596,12 @@ static int hash_encode_bwd_impl(const float* d_xyz, int64_t n_points, const floa
             hipLaunchKernelGGL(hash_encode_bwd_kernel<3>, grid, dim3(256), 0, as_stream(stream), d_xyz, n_points, hp,
                                d_dfeat, feat_stride_point, feat_stride_level);
             NERF_CHECK_LAUNCH("hash_encode_bwd (bin)");
-            hipLaunchKernelGGL(hash_bwd_owner_kernel, dim3(1u << B.owner_log2, n_levels), dim3(kOwnerThreads), 0,
-                               as_stream(stream), hp);
+            if (owner_variant() == 1)
+                hipLaunchKernelGGL((hash_bwd_owner_kernel<13, 1024>), dim3(1u << B.owner_log2, n_levels), dim3(1024),
+                                   0, as_stream(stream), hp);
+            else
+                hipLaunchKernelGGL((hash_bwd_owner_kernel<12, 512>), dim3(1u << B.owner_log2, n_levels), dim3(512), 0,
+                                   as_stream(stream), hp);
             break;
     }
     NERF_CHECK_LAUNCH("hash_encode_bwd");
