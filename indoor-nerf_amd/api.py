@@ -11,7 +11,8 @@ from .quantization import FakeQuantizer, LearnedBitwidthQuantizer, PassthroughQu
 from .rays import RaySampler, crop_window
 from .scene import get_bbox3d_for_blenderobj, get_bbox3d_for_llff
 from .render import (batchify_rays, camera, get_rays, get_rays_np, img2mse, manual_seed, mse2psnr, ndc_rays, raw2outputs,
-                     render, render_rays, sample_pdf, to8b)
+                     render, render_path, render_rays, sample_pdf, to8b)
+from .data import load_blender_data, load_llff_data, pose_spherical
 
 __all__ = ["HashEmbedder", "SHEncoder", "NeRFSmall", "RAdam", "run_network", "batchify", "batchify_rays", "render",
            "render_rays", "raw2outputs", "sample_pdf", "get_rays", "get_rays_np", "ndc_rays", "img2mse", "mse2psnr",
@@ -19,7 +20,8 @@ __all__ = ["HashEmbedder", "SHEncoder", "NeRFSmall", "RAdam", "run_network", "ba
            "total_variation_all", "train_loss", "sigma_sparsity_loss", "level_resolutions", "GradArena", "init_process_group",
            "shard", "broadcast_params", "manual_seed", "load_library", "LearnedBitwidthQuantizer", "FakeQuantizer",
            "PassthroughQuantizer", "calculate_fqr", "acaq_update", "acaq_quantizers", "RaySampler", "crop_window", "camera",
-           "get_bbox3d_for_blenderobj", "get_bbox3d_for_llff"]
+           "get_bbox3d_for_blenderobj", "get_bbox3d_for_llff", "render_path", "load_blender_data", "load_llff_data",
+           "pose_spherical"]
 
 
 def load_library():

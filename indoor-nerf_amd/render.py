@@ -10,6 +10,8 @@ Randomness: pytest=True reproduces the reference's np.random.seed(0) draws exact
 stratified jitter and importance uniforms are drawn in-kernel (Philox4x32-10) from a seed taken
 from torch's CPU generator, and raw noise uses torch.randn like the reference.
 """
+import os
+
 import numpy as np
 import torch
 
@@ -309,3 +311,44 @@ def render(H, W, K, chunk=1024 * 32, rays=None, c2w=None, ndc=True, near=0., far
         all_ret[k] = torch.reshape(all_ret[k], list(sh[:-1]) + list(all_ret[k].shape[1:]))
     k_extract = ["rgb_map", "depth_map", "acc_map"]
     return [all_ret[k] for k in k_extract] + [{k: all_ret[k] for k in all_ret if k not in k_extract}]
+
+
+def render_path(render_poses, hwf, K, chunk, render_kwargs, gt_imgs=None, savedir=None, render_factor=0):
+    """run_nerf.py:154-215: full frames along a camera path through render() (device ray generation,
+    chunked fused field, compositing) -> (rgbs [N,H,W,3], depths [N,H,W] normalised to [0,1]) as
+    numpy. With gt_imgs (and render_factor 0) the per-view PSNR -10 log10(mean((rgb - gt)^2)) is
+    printed and its average pickled to savedir, as the reference does; savedir also receives each
+    view as 8-bit PNGs ({i:03d}.png colour, {i:03d}_depth.png depth) instead of the reference's
+    matplotlib figure. As the reference, render_factor shrinks H, W and focal but passes K unchanged
+    to render()."""
+    H, W, focal = hwf
+    near, far = render_kwargs["near"], render_kwargs["far"]
+    if render_factor != 0:
+        H, W, focal = H // render_factor, W // render_factor, focal / render_factor
+    rgbs, depths, psnrs = [], [], []
+    for i, c2w in enumerate(render_poses):
+        c2w = c2w if torch.is_tensor(c2w) else torch.as_tensor(np.asarray(c2w, np.float32))
+        with torch.no_grad():
+            rgb, depth, acc, _ = render(H, W, K, chunk=chunk, c2w=c2w[:3, :4], **render_kwargs)
+        rgb_np = rgb.cpu().numpy()
+        rgbs.append(rgb_np)
+        depths.append(((depth - near) / (far - near)).cpu().numpy())
+        if gt_imgs is not None and render_factor == 0:
+            gt = gt_imgs[i].cpu().numpy() if torch.is_tensor(gt_imgs[i]) else np.asarray(gt_imgs[i])
+            p = -10. * np.log10(np.mean(np.square(rgb_np - gt)))
+            print(p)
+            psnrs.append(p)
+        if savedir is not None:
+            from PIL import Image
+            os.makedirs(savedir, exist_ok=True)
+            Image.fromarray(to8b(rgbs[-1])).save(os.path.join(savedir, f"{i:03d}.png"))
+            Image.fromarray(to8b(np.clip(depths[-1], 0, 1))).save(os.path.join(savedir, f"{i:03d}_depth.png"))
+    rgbs, depths = np.stack(rgbs, 0), np.stack(depths, 0)
+    if gt_imgs is not None and render_factor == 0:
+        avg = sum(psnrs) / len(psnrs)
+        print("Avg PSNR over Test set: ", avg)
+        if savedir is not None:
+            import pickle
+            with open(os.path.join(savedir, "test_psnrs_avg{:0.2f}.pkl".format(avg)), "wb") as fp:
+                pickle.dump(psnrs, fp)
+    return rgbs, depths

@@ -708,6 +708,40 @@ def gen_tv(ref, out):
                         grad=np.concatenate(g_all))
 
 
+def gen_data(ref, out):
+    """F17: the dataset loaders (load_blender.py:38-91, load_llff.py:244-319) on tiny on-disk
+    datasets written by tables.make_tiny_{blender,llff}. imageio.imread is stubbed with PIL (the
+    same uint8 arrays for PNG); half_res is not covered (it needs cv2.resize)."""
+    import tempfile
+
+    from PIL import Image
+    from tables import make_tiny_blender, make_tiny_llff
+    sys.modules["imageio"].imread = lambda f, **kw: np.asarray(Image.open(f))
+    import load_blender as ref_lb
+    import load_llff as ref_ll
+    res = {}
+    with tempfile.TemporaryDirectory() as d:
+        bdir, ldir = os.path.join(d, "blender"), os.path.join(d, "llff")
+        os.makedirs(bdir)
+        os.makedirs(ldir)
+        make_tiny_blender(bdir)
+        make_tiny_llff(ldir)
+        for skip in (1, 2):
+            imgs, poses, rposes, hwf, i_split, bbox = ref_lb.load_blender_data(bdir, half_res=False, testskip=skip)
+            tag = f"b{skip}_"
+            res.update({tag + "imgs": imgs, tag + "poses": poses, tag + "render_poses": rposes.numpy(),
+                        tag + "hwf": np.array(hwf, np.float64), tag + "bbox": torch.stack(bbox).numpy()})
+            for k, ix in enumerate(i_split):
+                res[tag + f"split{k}"] = ix
+        for tag, kw in (("l_", {}), ("ls_", {"spherify": True}), ("lnr_", {"recenter": False}),
+                        ("lbd_", {"bd_factor": None})):
+            images, poses, bds, rposes, i_test, bbox = ref_ll.load_llff_data(ldir, factor=4, **kw)
+            res.update({tag + "images": images, tag + "poses": poses, tag + "bds": bds,
+                        tag + "render_poses": rposes, tag + "i_test": np.array(i_test),
+                        tag + "bbox": torch.stack(bbox).numpy()})
+    np.savez_compressed(os.path.join(out, "f17_data.npz"), **res)
+
+
 def main(only=None):
     """Write every fixture, or only the named generators (e.g. `make_golden.py normals quant`)."""
     out = HERE
@@ -715,7 +749,7 @@ def main(only=None):
     gens = [("voxel", None), ("hash", gen_hash), ("sh", gen_sh), ("mlp", gen_mlp), ("composite", gen_composite),
             ("pdf", gen_pdf), ("render", gen_render), ("quant", gen_quant), ("tv", gen_tv), ("train", gen_train),
             ("normals", gen_normals), ("acaq", gen_acaq),
-            ("llff", gen_llff), ("rays", gen_rays)]
+            ("llff", gen_llff), ("rays", gen_rays), ("data", gen_data)]
     if not only or "levels" in only or "voxel" in only:
         levels = gen_levels(ref, out)
         gen_voxel(ref, out, levels)

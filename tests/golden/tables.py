@@ -68,3 +68,51 @@ def synthetic_rays(n_rays, H=800, W=800, pose_index=3, seed=0):
     rays_d = (dirs[:, None, :] * c2w[None, :3, :3]).sum(-1).astype(np.float32)
     rays_o = np.broadcast_to(c2w[:3, 3], rays_d.shape).astype(np.float32).copy()
     return rays_o, rays_d
+
+
+# ---- tiny on-disk datasets for the loader fixtures (F17) ---------------------------------------
+BLENDER_SPLITS = {"train": [0.0, 40.0, 95.0], "val": [150.0, -120.0], "test": [10.0, 200.0, -60.0]}
+
+
+def make_tiny_blender(root, H=10, W=12, seed=0):
+    """transforms_{train,val,test}.json + RGBA PNGs (random pixels) in the nerf_synthetic layout."""
+    import json
+    import os
+
+    from PIL import Image
+    rng = np.random.default_rng(seed)
+    for split, thetas in BLENDER_SPLITS.items():
+        os.makedirs(os.path.join(root, split), exist_ok=True)
+        frames = []
+        for k, th in enumerate(thetas):
+            name = f"./{split}/r_{k}"
+            Image.fromarray(rng.integers(0, 256, (H, W, 4), dtype=np.uint8), "RGBA").save(
+                os.path.join(root, name + ".png"))
+            frames.append({"file_path": name, "transform_matrix": pose_spherical(th, -30.0, 4.0311).tolist()})
+        with open(os.path.join(root, f"transforms_{split}.json"), "w") as fp:
+            json.dump({"camera_angle_x": 0.6911112070083618, "frames": frames}, fp)
+
+
+def make_tiny_llff(root, n_views=5, full=(32, 40), factor=4, seed=1):
+    """poses_bounds.npy (LLFF [down, right, back] columns + hwf, near/far) + images/ and
+    images_<factor>/ RGB PNGs (random pixels; the loader reads images_<factor>/ when present)."""
+    import os
+
+    from PIL import Image
+    rng = np.random.default_rng(seed)
+    H, W = full
+    rows = []
+    for k in range(n_views):
+        yaw = 0.08 * (k - n_views / 2)
+        c, s = np.cos(yaw), np.sin(yaw)
+        right, up, back = np.array([c, 0, -s]), np.array([0.0, 1.0, 0.0]), np.array([s, 0, c])
+        pos = np.array([0.3 * (k - 2), 0.05 * k, 0.1 * k])
+        # LLFF stores [down, right, back, position, hwf]
+        pose = np.stack([-up, right, back, pos, np.array([H, W, 35.0 + k])], 1)
+        rows.append(np.concatenate([pose.reshape(-1), [1.5 + 0.1 * k, 9.0 + k]]))
+    np.save(os.path.join(root, "poses_bounds.npy"), np.array(rows, np.float64))
+    for sub, (h, w) in (("images", (H, W)), (f"images_{factor}", (H // factor, W // factor))):
+        os.makedirs(os.path.join(root, sub), exist_ok=True)
+        for k in range(n_views):
+            Image.fromarray(rng.integers(0, 256, (h, w, 3), dtype=np.uint8), "RGB").save(
+                os.path.join(root, sub, f"IMG_{k:04d}.png"))

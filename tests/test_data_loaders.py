@@ -1,0 +1,71 @@
+"""Dataset loaders (indoor-nerf_amd/data.py) against the reference's load_blender_data /
+load_llff_data on tiny on-disk datasets (golden F17, tests/golden/make_golden.py gen_data).
+
+Tolerances: images, split indices and the held-out view are exact (same uint8 decode, same /255
+in fp32); poses and camera paths are numpy float64/float32 linear algebra written independently
+of the reference, compared at 1e-6 relative (a few ulps); the scene box at 1e-5.
+"""
+import numpy as np
+import pytest
+import torch
+
+from tables import make_tiny_blender, make_tiny_llff
+
+
+@pytest.fixture(scope="module")
+def datasets(tmp_path_factory):
+    root = tmp_path_factory.mktemp("data")
+    b, l = root / "blender", root / "llff"
+    b.mkdir()
+    l.mkdir()
+    make_tiny_blender(str(b))
+    make_tiny_llff(str(l))
+    return str(b), str(l)
+
+
+@pytest.mark.parametrize("skip", [1, 2])
+def test_blender_loader_vs_reference(nerf, golden, datasets, skip):
+    g = golden("f17_data")
+    imgs, poses, rposes, hwf, i_split, bbox = nerf.load_blender_data(datasets[0], half_res=False, testskip=skip)
+    t = f"b{skip}_"
+    np.testing.assert_array_equal(imgs, g[t + "imgs"])
+    np.testing.assert_array_equal(poses, g[t + "poses"])
+    np.testing.assert_allclose(rposes.numpy(), g[t + "render_poses"], rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(np.array(hwf, np.float64), g[t + "hwf"], rtol=1e-12)
+    for k in range(3):
+        np.testing.assert_array_equal(i_split[k], g[t + f"split{k}"])
+    np.testing.assert_allclose(torch.stack(bbox).numpy(), g[t + "bbox"], rtol=1e-5, atol=1e-5)
+
+
+def test_blender_half_res(nerf, datasets):
+    full = nerf.load_blender_data(datasets[0])
+    half = nerf.load_blender_data(datasets[0], half_res=True)
+    H, W, f = half[3]
+    assert (H, W) == (full[3][0] // 2, full[3][1] // 2) and f == full[3][2] / 2
+    assert half[0].dtype == np.float64 and half[0].shape[1:3] == (H, W)
+    box = full[0][:, :2 * H, :2 * W].reshape(-1, H, 2, W, 2, 4).mean((2, 4))
+    np.testing.assert_allclose(half[0], box, atol=1e-7)
+
+
+@pytest.mark.parametrize("tag,kw", [("l_", {}), ("ls_", {"spherify": True}), ("lnr_", {"recenter": False}),
+                                    ("lbd_", {"bd_factor": None})])
+def test_llff_loader_vs_reference(nerf, golden, datasets, tag, kw):
+    g = golden("f17_data")
+    images, poses, bds, rposes, i_test, bbox = nerf.load_llff_data(datasets[1], factor=4, **kw)
+    np.testing.assert_array_equal(images, g[tag + "images"])
+    np.testing.assert_allclose(poses, g[tag + "poses"], rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(bds, g[tag + "bds"], rtol=1e-6)
+    np.testing.assert_allclose(rposes, g[tag + "render_poses"], rtol=1e-6, atol=1e-6)
+    assert int(i_test) == int(g[tag + "i_test"])
+    np.testing.assert_allclose(torch.stack(bbox).numpy(), g[tag + "bbox"], rtol=1e-5, atol=1e-5)
+
+
+def test_llff_missing_factor_dir_downsamples_in_memory(nerf, datasets, tmp_path):
+    """No images_<factor>/: the reference would run ImageMagick; we box-filter in memory."""
+    import shutil
+    d = tmp_path / "llff"
+    shutil.copytree(datasets[1], d)
+    shutil.rmtree(d / "images_4")
+    images, poses, *_ = nerf.load_llff_data(str(d), factor=4)
+    assert images.shape == (5, 8, 10, 3)
+    assert np.allclose(poses[:, :2, 4], [[8, 10]] * 5)
