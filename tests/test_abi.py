@@ -88,16 +88,16 @@ def test_c_oracle_hash_fwd_exact(golden):
 def test_hash_bwd_workspace_plan(nerf):
     """Host-side plan of the binned backward (csrc/hashgrid.hip make_bin_plan): per level and
     256-point chunk a region of 2048 entries (8-B d feat + 2-B row) and n_owner segment words, each
-    array 256-B aligned; owner slices of min(2^13, T) rows, at most 64 owners (log2_T <= 19)."""
+    array 256-B aligned; owner slices of min(2^13, T) rows, at most 128 owners (log2_T <= 20)."""
     lib = nerf.load_library()
     up = lambda v: (v + 255) // 256 * 256  # noqa: E731
-    for L, log2_T, P in ((16, 19, 786432), (16, 19, 262144), (8, 12, 1000), (16, 14, 5)):
+    for L, log2_T, P in ((16, 19, 786432), (16, 19, 262144), (8, 12, 1000), (16, 14, 5), (16, 20, 1000)):
         nch = (P + 255) // 256
         own = 1 << (log2_T - min(13, log2_T))
         ent = L * nch * 2048
         expect = up(ent * 8) + up(ent * 2) + up(L * nch * own * 4)
         assert lib.nerf_hash_encode_bwd_workspace_bytes(L, log2_T, P) == expect
-    assert lib.nerf_hash_encode_bwd_workspace_bytes(16, 20, 1000) == 0
+    assert lib.nerf_hash_encode_bwd_workspace_bytes(16, 21, 1000) == 0
     assert lib.nerf_hash_encode_bwd_workspace_bytes(0, 19, 1000) == 0
 
 
