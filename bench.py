@@ -88,6 +88,7 @@ def parse():
     ap.add_argument("--profile-kernels", type=int, default=1, help="record HIP events per kernel in the timed region")
     ap.add_argument("--workload", default="lego", choices=sorted(WORKLOADS),
                     help="BASELINE config: lego (configs[1], the headline), fern (configs[2], LLFF NDC), "
+                         "scannet (configs[3], normals + structural priors, meant for --gpus 8), "
                          "acaq (configs[4], A-CAQ quantized tables)")
     ap.add_argument("--graph", type=int, default=1,
                     help="train mode: replay the iteration from HIP graphs (graphs.GraphedTrainStep); 0 = eager")
@@ -108,6 +109,13 @@ WORKLOADS = {
                  near=0.0, far=1.0, rays="llff", ndc=True,
                  desc="fern (LLFF) train step: {R} rays/GPU x (64 coarse + 64 fine) samples, NDC, raw noise 1, "
                       "finest_res 512, RAdam, TV+sparsity losses"),
+    "scannet": dict(args=dict(finest_res=512, N_samples=64, N_importance=128, white_bkgd=False, perturb=1.0,
+                              lrate_decay=500, tv_loss_weight=1e-6, use_structural_priors=True,
+                              structural_loss_start_iter=0),
+                    near=0.1, far=10.0, rays="scannet",
+                    desc="ScanNet-like indoor train step: {R} rays/GPU x (64 + 128) samples, near 0.1 far 10, normals "
+                         "head (7-channel compositing), structural priors (Manhattan + planarity + normal "
+                         "consistency, full ramp), RAdam, TV+sparsity losses"),
     "acaq": dict(args=dict(finest_res=1024, N_samples=64, N_importance=128, white_bkgd=True, perturb=1.0,
                            lrate_decay=500, tv_loss_weight=1e-6, use_quantization=True, quantization_bits=8),
                  near=2.0, far=6.0, rays="blender", quantized=True,
@@ -179,6 +187,11 @@ def main():
         ro, rd = blender_rays(a.rays, seed=100 + rank)
         H = W = 800
         K = None
+    elif wl["rays"] == "scannet":
+        from indoor_nerf_amd.synthetic import scannet_bbox, scannet_rays
+        lo, hi = scannet_bbox()
+        ro, rd, _coords = scannet_rays(a.rays, seed=100 + rank)
+        H, W, K = 480, 640, None
     else:
         lo, hi = llff_bbox()
         ro, rd, (H, W, K) = llff_rays(a.rays, seed=100 + rank)
@@ -316,7 +329,7 @@ def main():
         "vs_baseline": None,
         "dtype": "fp32",
         "data": "synthetic ({} rays, random-init hash tables and MLPs)".format(
-            "lego spiral-pose" if wl["rays"] == "blender" else "forward-facing LLFF rig"),
+            {"blender": "lego spiral-pose", "llff": "forward-facing LLFF rig", "scannet": "indoor room"}[wl["rays"]]),
         "config": {"workload": wl["desc"].format(R=a.rays) + ("" if a.mode == "train" else " [render only]"),
                    "name": a.workload, "rays_per_gpu": a.rays, "global_batch": a.rays * world,
                    "samples": f"{wl['args']['N_samples']}+{wl['args']['N_importance']}", "parallelism": f"dp{world}"},

@@ -365,6 +365,13 @@ int nerf_hash_encode_fwd_packed(const float* d_xyz, int64_t n_points, const floa
                                 const float* d_qrec, float* d_feat, int64_t feat_stride_point,
                                 int64_t feat_stride_level, uint8_t* d_keep, void* stream);
 
+/* ---- structural priors (PocketNeRF/structural_priors.py:333-346, the ScanNet configuration) -----
+ * For each query ray q (d_idx1[q], int64), the nearest OTHER ray in pixel space: d_xy [n,2] fp32
+ * pixel coordinates (train()'s select_coords), self excluded, ties to the lowest index
+ * (torch.argmin), d_idx2[q] its index (int64) and d_dist[q] = sqrt of the squared distance. */
+int nerf_nearest_pixel(const float* d_xy, int64_t n, const int64_t* d_idx1, int64_t n_query, int64_t* d_idx2,
+                       float* d_dist, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

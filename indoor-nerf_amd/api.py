@@ -12,7 +12,9 @@ from .rays import RaySampler, crop_window
 from .scene import get_bbox3d_for_blenderobj, get_bbox3d_for_llff
 from .render import (batchify_rays, camera, get_rays, get_rays_np, img2mse, manual_seed, mse2psnr, ndc_rays, raw2outputs,
                      render, render_path, render_rays, sample_pdf, to8b)
-from .data import load_blender_data, load_llff_data, pose_spherical
+from .data import load_blender_data, load_llff_data, load_scannet_data, pose_spherical
+from .priors import (ManhattanFrameEstimator, SemanticPlaneDetector, combine_structural_losses_v2, manhattan_sdf_loss,
+                     spatial_normal_consistency_loss, structured_planarity_loss)
 
 __all__ = ["HashEmbedder", "SHEncoder", "NeRFSmall", "RAdam", "run_network", "batchify", "batchify_rays", "render",
            "render_rays", "raw2outputs", "sample_pdf", "get_rays", "get_rays_np", "ndc_rays", "img2mse", "mse2psnr",
@@ -21,7 +23,9 @@ __all__ = ["HashEmbedder", "SHEncoder", "NeRFSmall", "RAdam", "run_network", "ba
            "shard", "broadcast_params", "manual_seed", "load_library", "LearnedBitwidthQuantizer", "FakeQuantizer",
            "PassthroughQuantizer", "calculate_fqr", "acaq_update", "acaq_quantizers", "RaySampler", "crop_window", "camera",
            "get_bbox3d_for_blenderobj", "get_bbox3d_for_llff", "render_path", "load_blender_data", "load_llff_data",
-           "pose_spherical"]
+           "pose_spherical", "load_scannet_data", "ManhattanFrameEstimator", "SemanticPlaneDetector",
+           "combine_structural_losses_v2", "manhattan_sdf_loss", "spatial_normal_consistency_loss",
+           "structured_planarity_loss"]
 
 
 def load_library():

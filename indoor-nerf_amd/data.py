@@ -273,3 +273,82 @@ def load_llff_data(basedir, factor=8, recenter=True, bd_factor=.75, spherify=Fal
     poses = poses.astype(np.float32)
     bounding_box = get_bbox3d_for_llff(poses[:, :3, :4], poses[0, :3, -1], near=0.0, far=1.0)
     return images, poses, bds, render_poses, i_test, bounding_box
+
+
+# ----------------------------------------------------------------------------------- ScanNet
+_PLY_TYPES = {"char": "i1", "int8": "i1", "uchar": "u1", "uint8": "u1", "short": "i2", "int16": "i2",
+              "ushort": "u2", "uint16": "u2", "int": "i4", "int32": "i4", "uint": "u4", "uint32": "u4",
+              "float": "f4", "float32": "f4", "double": "f8", "float64": "f8"}
+
+
+def ply_vertex_bounds(path):
+    """(min xyz, max xyz) of a PLY mesh's vertices: the part of pyvista.read(...).bounds that
+    load_scannet.py:100-104 uses (pyvista is not in this image). Reads binary little/big-endian
+    and ASCII PLY; the vertex element must come first (as in ScanNet's *_vh_clean.ply)."""
+    with open(path, "rb") as f:
+        if f.readline().strip() != b"ply":
+            raise ValueError(f"{path}: not a PLY file")
+        fmt, n_vert, props, in_vertex = None, 0, [], False
+        while True:
+            line = f.readline()
+            if not line:
+                raise ValueError(f"{path}: truncated PLY header")
+            tok = line.decode("ascii", "replace").split()
+            if not tok:
+                continue
+            if tok[0] == "format":
+                fmt = tok[1]
+            elif tok[0] == "element":
+                in_vertex = tok[1] == "vertex"
+                if in_vertex:
+                    n_vert = int(tok[2])
+            elif tok[0] == "property" and in_vertex:
+                if tok[1] == "list":
+                    raise ValueError(f"{path}: list property in the vertex element")
+                props.append((tok[2], _PLY_TYPES[tok[1]]))
+            elif tok[0] == "end_header":
+                break
+        if fmt == "ascii":
+            rows = np.loadtxt(f, max_rows=n_vert, ndmin=2)
+            names = [p[0] for p in props]
+            xyz = rows[:, [names.index("x"), names.index("y"), names.index("z")]]
+        else:
+            end = "<" if fmt == "binary_little_endian" else ">"
+            dt = np.dtype([(n, end + t) for n, t in props])
+            v = np.frombuffer(f.read(dt.itemsize * n_vert), dtype=dt, count=n_vert)
+            xyz = np.stack([v["x"], v["y"], v["z"]], 1).astype(np.float64)
+    return xyz.min(0), xyz.max(0)
+
+
+def load_scannet_data(basedir, sceneID, half_res=False, trainskip=10, testskip=1):
+    """load_scannet.py:38-106: a ScanNet scene exported in the nerf_synthetic layout
+    (<basedir>/nerfstyle_<sceneID>/transforms_*.json + PNGs) -> imgs [N,H,W,C] fp32, poses [N,4,4]
+    (OpenCV -> OpenGL camera axes: y and z columns negated), render_poses [40,4,4], [H, W, focal],
+    i_split, bounding_box = the scene mesh's vertex bounds (scans/<sceneID>/<sceneID>_vh_clean.ply)
+    padded by 1."""
+    scene = os.path.join(basedir, "nerfstyle_" + sceneID)
+    metas = {}
+    for split in ("train", "val", "test"):
+        with open(os.path.join(scene, f"transforms_{split}.json")) as fp:
+            metas[split] = json.load(fp)
+    img_blocks, pose_blocks, first = [], [], [0]
+    for split in ("train", "val", "test"):
+        frames = metas[split]["frames"][::trainskip if split == "train" else testskip]
+        block = np.array([_imread(os.path.join(scene, fr["file_path"] + ".png")) for fr in frames])
+        poses = np.array([fr["transform_matrix"] for fr in frames], np.float64)
+        poses[:, :3, 1:3] *= -1        # ScanNet poses use the OpenCV convention
+        img_blocks.append((block / 255.).astype(np.float32))
+        pose_blocks.append(poses.astype(np.float32))
+        first.append(first[-1] + len(frames))
+    i_split = [np.arange(first[k], first[k + 1]) for k in range(3)]
+    imgs = np.concatenate(img_blocks, 0)
+    poses = np.concatenate(pose_blocks, 0)
+    H, W = imgs[0].shape[:2]
+    focal = .5 * W / np.tan(.5 * float(metas["test"]["camera_angle_x"]))
+    render_poses = torch.stack([pose_spherical(a, -30.0, 4.0) for a in np.linspace(-180, 180, 41)[:-1]], 0)
+    if half_res:
+        H, W, focal = H // 2, W // 2, focal / 2.
+        imgs = np.stack([_box_half(im) for im in imgs]).astype(np.float64)
+    lo, hi = ply_vertex_bounds(os.path.join(basedir, "scans", sceneID, f"{sceneID}_vh_clean.ply"))
+    bounding_box = (torch.tensor(lo) - 1, torch.tensor(hi) + 1)
+    return imgs, poses, render_poses, [H, W, focal], i_split, bounding_box

@@ -160,8 +160,18 @@ class GraphedTrainStep:
                           K=self.K, grad_hook=self.hook, loss_scale_sparsity=self.scale_sp,
                           tv_generator=self.tv_gen, zero_grad=self.zero_grad)
 
+    def _priors_active(self, global_step):
+        from .model import DEFAULTS
+        get = lambda k: getattr(self.args, k, DEFAULTS.get(k))  # noqa: E731
+        return bool(get("use_structural_priors")) and global_step >= get("structural_loss_start_iter")
+
     def __call__(self, global_step):
         from .model import acaq_update, lr_schedule
+        if self._priors_active(global_step):
+            # the structural priors branch on ray counts read on the host and draw data-dependent
+            # permutations (priors.py): not capturable, the iteration runs eagerly
+            self.graphs, self.key = None, None
+            return self.eager_step(global_step)
         key = self._structure_key()
         if key != self.key:                # new launch structure: eager steps first (allocations,
             self.key = key                 # quantizer calibration), then a fresh capture

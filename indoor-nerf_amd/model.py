@@ -23,7 +23,11 @@ DEFAULTS = dict(multires=10, i_embed=1, i_embed_views=2, multires_views=4, use_v
                 use_quantization=False, quantization_bits=8, use_acaq=False, target_metric=None, bit_penalty=1e-3,
                 acaq_start_iter=1000, dataset_type="blender", no_ndc=False, lindisp=False,
                 basedir="./logs/", expname="", ft_path=None, no_reload=True, sparse_loss_weight=1e-10,
-                tv_loss_weight=1e-6, chunk=1024 * 32)
+                tv_loss_weight=1e-6, chunk=1024 * 32,
+                # structural priors (run_nerf.py:683-703)
+                use_structural_priors=False, depth_prior_weight=0.01, planarity_weight=0.005,
+                manhattan_weight=0.002, normal_consistency_weight=0.001, structural_loss_start_iter=2000,
+                structural_loss_ramp_iters=1000, overfitting_threshold=8.0, min_structural_weight=0.0001)
 
 
 def make_args(**kw):
@@ -38,6 +42,8 @@ def create_nerf(args, device=None):
     if get("i_embed") != 1 or get("i_embed_views") != 2:
         raise NotImplementedError("create_nerf: only the hash-grid (i_embed=1) + SH (i_embed_views=2) model is "
                                   "built on the HIP path (the positional-encoding NeRF is out of scope)")
+    if get("use_structural_priors") and not get("predict_normals"):
+        args.predict_normals = True     # run_nerf.py:723-727: the priors need the normals head
     use_q, q_bits = get("use_quantization"), get("quantization_bits")
     embed_fn = HashEmbedder(bounding_box=args.bounding_box, log2_hashmap_size=get("log2_hashmap_size"),
                             finest_resolution=get("finest_res"), use_quantization=use_q,
@@ -149,7 +155,7 @@ def acaq_update(i, img_loss, render_kwargs_train, args):
 
 
 def forward_backward(batch_rays, target_s, render_kwargs_train, optimizer, args, global_step, H=0, W=0, K=None,
-                     loss_scale_sparsity=1.0, tv_generator=None, zero_grad=None, schedule=True):
+                     loss_scale_sparsity=1.0, tv_generator=None, zero_grad=None, schedule=True, spatial_coords=None):
     """render (coarse+fine), zero grads, img/img0 MSE + sparsity + TV (run_nerf.py:1007-1037),
     backward. Returns (loss, img_loss, psnr) device tensors (no host sync)."""
     get = lambda k: getattr(args, k, DEFAULTS.get(k))  # noqa: E731
@@ -167,8 +173,34 @@ def forward_backward(batch_rays, target_s, render_kwargs_train, optimizer, args,
                                       tv_w if tv_w > 0 else 0.0)
     if schedule and global_step > 1000:
         args.tv_loss_weight = 0.0
+    if get("use_structural_priors") and global_step >= get("structural_loss_start_iter"):
+        loss = loss + structural_loss(depth, extras, args, global_step, spatial_coords)
     loss.backward()
     return loss, img_loss, psnr
+
+
+def structural_loss(depth, extras, args, global_step, spatial_coords=None):
+    """run_nerf.py:1068-1131: the structural-prior weights ramp from 10 % to 100 % over
+    structural_loss_ramp_iters, then combine_structural_losses_v2 (priors.py) on the fine pass's
+    depth and normal maps. The estimators persist across iterations (run_nerf.py:939-940). The
+    overfitting-driven weight reduction (:1073-1094) needs train()'s test-set PSNR history and is
+    left to the caller. Failures are swallowed as in the reference (:1144-1148)."""
+    from .priors import ManhattanFrameEstimator, SemanticPlaneDetector, combine_structural_losses_v2
+    get = lambda k: getattr(args, k, DEFAULTS.get(k))  # noqa: E731
+    if getattr(args, "_priors", None) is None:
+        args._priors = (ManhattanFrameEstimator(confidence_threshold=0.4), SemanticPlaneDetector(normal_threshold=0.5))
+    start = get("structural_loss_start_iter")
+    ramp = 0.1 + 0.9 * min(1.0, (global_step - start) / get("structural_loss_ramp_iters"))
+    weights = {"depth_prior": get("depth_prior_weight") * ramp, "planarity": get("planarity_weight") * ramp,
+               "manhattan": get("manhattan_weight") * ramp, "normal_consistency": get("normal_consistency_weight") * ramp}
+    normals = extras.get("normal_map", None) if get("predict_normals") else None
+    try:
+        total, _ = combine_structural_losses_v2(depth, normals, extras.get("rays_d"), spatial_coords, weights,
+                                                *args._priors)
+    except Exception as e:   # noqa: BLE001 - the reference's policy
+        print(f"  ⚠️  Structural priors V2 failed: {e}")
+        return 0.0
+    return total
 
 
 def optimizer_update(optimizer):
@@ -187,14 +219,15 @@ def lr_schedule(optimizer, args, global_step):
 
 
 def train_step(batch_rays, target_s, render_kwargs_train, optimizer, args, global_step, H=0, W=0, K=None,
-               grad_hook=None, loss_scale_sparsity=1.0, tv_generator=None, zero_grad=None):
+               grad_hook=None, loss_scale_sparsity=1.0, tv_generator=None, zero_grad=None, spatial_coords=None):
     """One iteration of train() without host bookkeeping: render (coarse+fine), img/img0 MSE,
     sparsity, TV (run_nerf.py:1007-1037), backward, [grad_hook, e.g. DP all-reduce], RAdam step,
     A-CAQ bit widths, lr decay (:1182-1250, :1289-1293). Returns (loss, psnr) as device tensors
     (no host sync). graphs.GraphedTrainStep replays the same iteration from HIP graphs."""
     loss, img_loss, psnr = forward_backward(batch_rays, target_s, render_kwargs_train, optimizer, args, global_step,
                                             H=H, W=W, K=K, loss_scale_sparsity=loss_scale_sparsity,
-                                            tv_generator=tv_generator, zero_grad=zero_grad)
+                                            tv_generator=tv_generator, zero_grad=zero_grad,
+                                            spatial_coords=spatial_coords)
     if grad_hook is not None:
         grad_hook()
     optimizer_update(optimizer)

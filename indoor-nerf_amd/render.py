@@ -326,8 +326,9 @@ def render_path(render_poses, hwf, K, chunk, render_kwargs, gt_imgs=None, savedi
     if render_factor != 0:
         H, W, focal = H // render_factor, W // render_factor, focal / render_factor
     rgbs, depths, psnrs = [], [], []
+    dev = next(render_kwargs["network_fn"].parameters()).device     # the reference's default CUDA tensors
     for i, c2w in enumerate(render_poses):
-        c2w = c2w if torch.is_tensor(c2w) else torch.as_tensor(np.asarray(c2w, np.float32))
+        c2w = (c2w if torch.is_tensor(c2w) else torch.as_tensor(np.asarray(c2w, np.float32))).to(dev)
         with torch.no_grad():
             rgb, depth, acc, _ = render(H, W, K, chunk=chunk, c2w=c2w[:3, :4], **render_kwargs)
         rgb_np = rgb.cpu().numpy()

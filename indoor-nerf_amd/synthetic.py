@@ -68,3 +68,34 @@ def llff_bbox():
     from .scene import get_bbox3d_for_llff
     lo, hi = get_bbox3d_for_llff(llff_poses(), LLFF_HWF, near=0.0, far=1.0)
     return lo.numpy(), hi.numpy()
+
+
+# ScanNet-like indoor scene (configs/scannet_scene0000.txt: near 0.1, far 10): a 6 x 5 x 3 m room,
+# the box the loader derives from the mesh bounds padded by 1 (load_scannet.py:100-104), and
+# 640 x 480 cameras (ScanNet's colour intrinsics at that size: focal ~ 577.9) inside it.
+SCANNET_BBOX = ((-1.0, -1.0, -1.0), (7.0, 6.0, 4.0))
+
+
+def scannet_bbox():
+    return (np.array(SCANNET_BBOX[0], np.float32), np.array(SCANNET_BBOX[1], np.float32))
+
+
+def scannet_rays(n_rays, seed=0, H=480, W=640, focal=577.9):
+    """n_rays rays of one camera standing in the room and looking horizontally, with the integer
+    pixel coordinates they came from ([n, 2] row, col: train()'s select_coords)."""
+    rng = np.random.default_rng(seed)
+    yaw = rng.uniform(0, 2 * np.pi)
+    c2w = np.eye(4, dtype=np.float64)
+    # camera looks along -z_cam; world up is +z
+    fwd = np.array([np.cos(yaw), np.sin(yaw), 0.0])
+    right = np.array([np.sin(yaw), -np.cos(yaw), 0.0])
+    up = np.array([0.0, 0.0, 1.0])
+    c2w[:3, 0], c2w[:3, 1], c2w[:3, 2] = right, up, -fwd
+    c2w[:3, 3] = rng.uniform([1.5, 1.5, 1.2], [4.5, 3.5, 1.8])
+    flat = rng.choice(H * W, size=n_rays, replace=False)
+    i, j = (flat % W).astype(np.float32), (flat // W).astype(np.float32)
+    dirs = np.stack([(i - W * .5) / focal, -(j - H * .5) / focal, -np.ones_like(i)], -1)
+    rays_d = (dirs @ c2w[:3, :3].T).astype(np.float32)
+    rays_o = np.broadcast_to(c2w[:3, 3], rays_d.shape).astype(np.float32).copy()
+    coords = np.stack([j, i], -1).astype(np.float32)
+    return rays_o, rays_d, coords

@@ -717,15 +717,30 @@ def gen_data(ref, out):
     from PIL import Image
     from tables import make_tiny_blender, make_tiny_llff
     sys.modules["imageio"].imread = lambda f, **kw: np.asarray(Image.open(f))
+    from tables import make_tiny_scannet
     import load_blender as ref_lb
     import load_llff as ref_ll
+
+    class _Mesh:   # pyvista.read stand-in: bounds (xmin, xmax, ymin, ymax, zmin, zmax) of the vertices
+        def __init__(self, path):
+            v = np.load(os.path.join(os.path.dirname(path), "vertices.npy")).astype(np.float64)
+            self.bounds = tuple(x for a in range(3) for x in (v[:, a].min(), v[:, a].max()))
+    sys.modules["pyvista"].read = _Mesh
+    import load_scannet as ref_ls
     res = {}
     with tempfile.TemporaryDirectory() as d:
-        bdir, ldir = os.path.join(d, "blender"), os.path.join(d, "llff")
+        bdir, ldir, sdir = os.path.join(d, "blender"), os.path.join(d, "llff"), os.path.join(d, "scannet")
         os.makedirs(bdir)
         os.makedirs(ldir)
+        os.makedirs(sdir)
         make_tiny_blender(bdir)
         make_tiny_llff(ldir)
+        make_tiny_scannet(sdir)
+        imgs, poses, rposes, hwf, i_split, bbox = ref_ls.load_scannet_data(sdir, "scene0000_00", False)
+        res.update({"s_imgs": imgs, "s_poses": poses, "s_render_poses": rposes.numpy(),
+                    "s_hwf": np.array(hwf, np.float64), "s_bbox": torch.stack(bbox).numpy()})
+        for k, ix in enumerate(i_split):
+            res[f"s_split{k}"] = ix
         for skip in (1, 2):
             imgs, poses, rposes, hwf, i_split, bbox = ref_lb.load_blender_data(bdir, half_res=False, testskip=skip)
             tag = f"b{skip}_"
@@ -742,6 +757,67 @@ def gen_data(ref, out):
     np.savez_compressed(os.path.join(out, "f17_data.npz"), **res)
 
 
+class RecordRNG:
+    """Wrap torch.randn / randperm / randint and keep every draw (the structural priors' random
+    choices), so that a test can replay them into the HIP-path implementation."""
+
+    def __init__(self):
+        self.draws = []
+
+    def __enter__(self):
+        self.saved = (torch.randn, torch.randperm, torch.randint)
+        rn, rp, ri = self.saved
+
+        def wrap(fn, name):
+            def f(*a, **k):
+                out = fn(*a, **k)
+                self.draws.append((name, out.detach().cpu().numpy().copy()))
+                return out
+            return f
+        torch.randn, torch.randperm, torch.randint = wrap(rn, "randn"), wrap(rp, "randperm"), wrap(ri, "randint")
+        return self
+
+    def __exit__(self, *exc):
+        torch.randn, torch.randperm, torch.randint = self.saved
+
+
+def gen_priors(ref, out):
+    """F18: combine_structural_losses_v2 (structural_priors.py:374-451) with train()'s weights
+    (run_nerf.py:1097-1102 at full ramp, scaled x100 so that gradients are far above rounding) and
+    estimators (:939-940); losses, loss parts, d depth, d normals and the random draws."""
+    from tables import priors_inputs
+    import structural_priors as ref_sp
+    res = {}
+    # f: fewer than 51 floor rays and tight clusters, so the Manhattan total stays below its 0.1
+    # clamp and its gradient (through the k-means centres and the SVD frame) reaches the normals
+    cases = {"a": (512, 1, True, True, 0.15), "b": (512, 2, True, False, 0.15), "c": (64, 3, True, True, 0.15),
+             "d": (40, 4, True, True, 0.15), "e": (1024, 5, True, True, 0.01), "f": (90, 6, False, True, 0.01)}
+    weights = {"depth_prior": 1.0, "planarity": 0.5, "manhattan": 0.2, "normal_consistency": 0.1}
+    for tag, (n, seed, small, coords, spread) in cases.items():
+        depth, normals, xy = priors_inputs(n, seed, small, spread)
+        if tag == "d":
+            normals[5:] = 0.0                         # too few stable normals: empty masks, identity frame
+        d = torch.from_numpy(depth).requires_grad_(True)
+        nm = torch.from_numpy(normals).requires_grad_(True)
+        torch.manual_seed(100 + seed)
+        est = ref_sp.ManhattanFrameEstimator(confidence_threshold=0.4)
+        det = ref_sp.SemanticPlaneDetector(normal_threshold=0.5)
+        with RecordRNG() as rec:
+            total, parts = ref_sp.combine_structural_losses_v2(d, nm, None, torch.from_numpy(xy) if coords else None,
+                                                               weights, est, det)
+        total.backward()
+        res[tag + "_depth"], res[tag + "_normals"], res[tag + "_coords"] = depth, normals, xy
+        res[tag + "_total"] = np.float64(total.item())
+        for k, v in parts.items():
+            res[tag + "_part_" + k] = np.float64(float(v.detach() if torch.is_tensor(v) else v))
+        res[tag + "_dd"] = d.grad.numpy() if d.grad is not None else np.zeros_like(depth)
+        res[tag + "_dn"] = nm.grad.numpy() if nm.grad is not None else np.zeros_like(normals)
+        res[tag + "_draw_names"] = np.array([nm_ for nm_, _ in rec.draws])
+        for i, (_, v) in enumerate(rec.draws):
+            res[tag + f"_draw{i}"] = v
+    np.savez_compressed(os.path.join(out, "f18_priors.npz"), **res)
+
+
 def main(only=None):
     """Write every fixture, or only the named generators (e.g. `make_golden.py normals quant`)."""
     out = HERE
@@ -749,7 +825,7 @@ def main(only=None):
     gens = [("voxel", None), ("hash", gen_hash), ("sh", gen_sh), ("mlp", gen_mlp), ("composite", gen_composite),
             ("pdf", gen_pdf), ("render", gen_render), ("quant", gen_quant), ("tv", gen_tv), ("train", gen_train),
             ("normals", gen_normals), ("acaq", gen_acaq),
-            ("llff", gen_llff), ("rays", gen_rays), ("data", gen_data)]
+            ("llff", gen_llff), ("rays", gen_rays), ("data", gen_data), ("priors", gen_priors)]
     if not only or "levels" in only or "voxel" in only:
         levels = gen_levels(ref, out)
         gen_voxel(ref, out, levels)

@@ -116,3 +116,66 @@ def make_tiny_llff(root, n_views=5, full=(32, 40), factor=4, seed=1):
         for k in range(n_views):
             Image.fromarray(rng.integers(0, 256, (h, w, 3), dtype=np.uint8), "RGB").save(
                 os.path.join(root, sub, f"IMG_{k:04d}.png"))
+
+
+# ---- structural-prior inputs (F18) ------------------------------------------------------------
+def priors_inputs(n, seed, with_small=True, spread=0.15):
+    """A ray batch's depth [n] and normal map [n,3] (unit normals: floor-like, wall-like and random
+    directions, plus zero / short normals of transparent rays), and distinct integer pixel
+    coordinates [n,2] (train()'s select_coords) — float32 numpy."""
+    rng = np.random.default_rng(seed)
+    kind = rng.integers(0, 3, n)
+    v = rng.normal(size=(n, 3))
+    v[kind == 0] = v[kind == 0] * [spread, spread, 1.0]      # near +-z: floor
+    v[kind == 1] = v[kind == 1] * [1.0, 1.0, spread * 0.67]  # near horizontal: walls
+    v /= np.linalg.norm(v, axis=1, keepdims=True)
+    if with_small:
+        v[rng.random(n) < 0.08] = 0.0                        # rays with zero weights
+        short = rng.random(n) < 0.05
+        v[short] *= 0.05
+    depth = rng.uniform(0.5, 6.0, n)
+    flat = rng.choice(64 * 80, size=n, replace=False)
+    coords = np.stack([flat // 80, flat % 80], 1)
+    return depth.astype(np.float32), v.astype(np.float32), coords.astype(np.float32)
+
+
+def make_tiny_scannet(root, scene="scene0000_00", H=12, W=16, seed=2):
+    """A ScanNet scene in the layout load_scannet.py reads: nerfstyle_<scene>/transforms_*.json +
+    RGB PNGs (OpenCV-convention poses) and scans/<scene>/<scene>_vh_clean.ply (binary little-endian,
+    float x y z + uchar colour), with the vertices also saved as vertices.npy (for the golden
+    generator's pyvista stand-in)."""
+    import json
+    import os
+
+    from PIL import Image
+    rng = np.random.default_rng(seed)
+    sdir = os.path.join(root, "nerfstyle_" + scene)
+    for split, n in (("train", 12), ("val", 2), ("test", 3)):
+        os.makedirs(os.path.join(sdir, split), exist_ok=True)
+        frames = []
+        for k in range(n):
+            name = f"./{split}/{k}"
+            Image.fromarray(rng.integers(0, 256, (H, W, 3), dtype=np.uint8), "RGB").save(
+                os.path.join(sdir, name + ".png"))
+            pose = np.eye(4)
+            a = rng.uniform(0, 2 * np.pi)
+            pose[:3, :3] = [[np.cos(a), 0, np.sin(a)], [0, 1, 0], [-np.sin(a), 0, np.cos(a)]]
+            pose[:3, 3] = rng.uniform([0, 0, 0.5], [6, 5, 2.5])
+            frames.append({"file_path": name, "transform_matrix": pose.tolist()})
+        with open(os.path.join(sdir, f"transforms_{split}.json"), "w") as fp:
+            json.dump({"camera_angle_x": 1.0175, "frames": frames}, fp)
+    mdir = os.path.join(root, "scans", scene)
+    os.makedirs(mdir, exist_ok=True)
+    verts = rng.uniform([-0.2, -0.1, -0.05], [6.3, 5.2, 3.1], (50, 3)).astype(np.float32)
+    cols = rng.integers(0, 256, (50, 3), dtype=np.uint8)
+    rec = np.zeros(50, dtype=[("x", "<f4"), ("y", "<f4"), ("z", "<f4"), ("red", "u1"), ("green", "u1"),
+                              ("blue", "u1")])
+    rec["x"], rec["y"], rec["z"] = verts[:, 0], verts[:, 1], verts[:, 2]
+    rec["red"], rec["green"], rec["blue"] = cols[:, 0], cols[:, 1], cols[:, 2]
+    header = ("ply\nformat binary_little_endian 1.0\nelement vertex 50\nproperty float x\nproperty float y\n"
+              "property float z\nproperty uchar red\nproperty uchar green\nproperty uchar blue\n"
+              "element face 0\nproperty list uchar int vertex_indices\nend_header\n")
+    with open(os.path.join(mdir, f"{scene}_vh_clean.ply"), "wb") as f:
+        f.write(header.encode("ascii"))
+        f.write(rec.tobytes())
+    np.save(os.path.join(mdir, "vertices.npy"), verts)

@@ -69,3 +69,18 @@ def test_llff_missing_factor_dir_downsamples_in_memory(nerf, datasets, tmp_path)
     images, poses, *_ = nerf.load_llff_data(str(d), factor=4)
     assert images.shape == (5, 8, 10, 3)
     assert np.allclose(poses[:, :2, 4], [[8, 10]] * 5)
+
+
+def test_scannet_loader_vs_reference(nerf, golden, tmp_path):
+    from tables import make_tiny_scannet
+    g = golden("f17_data")
+    make_tiny_scannet(str(tmp_path))
+    imgs, poses, rposes, hwf, i_split, bbox = nerf.load_scannet_data(str(tmp_path), "scene0000_00", False)
+    np.testing.assert_array_equal(imgs, g["s_imgs"])
+    np.testing.assert_array_equal(poses, g["s_poses"])
+    np.testing.assert_allclose(rposes.numpy(), g["s_render_poses"], rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(np.array(hwf, np.float64), g["s_hwf"], rtol=1e-12)
+    for k in range(3):
+        np.testing.assert_array_equal(i_split[k], g[f"s_split{k}"])
+    # the PLY reader against the vertices the maker wrote (the reference reads them with pyvista)
+    np.testing.assert_array_equal(torch.stack(bbox).numpy(), g["s_bbox"])

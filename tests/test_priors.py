@@ -1,0 +1,124 @@
+"""Structural priors (indoor-nerf_amd/priors.py, csrc/priors.hip) against the reference's
+combine_structural_losses_v2 (golden F18: losses, loss parts, d depth, d normals), replaying the
+reference's random draws (torch.randn / randperm / randint, recorded by make_golden.py) in order.
+
+CPU (case b, no pixel coordinates: torch ops only): losses and gradients to 1e-6 relative. GPU (all
+cases, the nearest-pixel search in the HIP kernel): losses to 1e-5 relative, gradients to 1e-4 of
+each tensor's largest entry (fp32 device reductions in a different order; case e's zero-length
+normals give the reference's 1/eps-sized gradients through F.normalize, reproduced as such).
+"""
+import contextlib
+
+import numpy as np
+import pytest
+import torch
+
+CASES = ["a", "b", "c", "d", "e", "f"]
+
+
+@contextlib.contextmanager
+def replay(g, tag):
+    names = list(g[tag + "_draw_names"])
+    draws = [g[tag + f"_draw{i}"] for i in range(len(names))]
+    saved = (torch.randn, torch.randperm, torch.randint)
+    state = {"i": 0}
+
+    def take(kind, device=None):
+        i = state["i"]
+        assert names[i] == kind, (i, names[i], kind)
+        state["i"] += 1
+        return torch.from_numpy(np.array(draws[i])).to(device if device is not None else "cpu")
+
+    torch.randn = lambda *a, device=None, **k: take("randn", device)
+    torch.randperm = lambda *a, device=None, **k: take("randperm", device)
+    torch.randint = lambda *a, device=None, **k: take("randint", device)
+    try:
+        yield state
+    finally:
+        torch.randn, torch.randperm, torch.randint = saved
+    assert state["i"] == len(names), "not every recorded draw was used"
+
+
+def run_case(nerf, g, tag, device):
+    from indoor_nerf_amd import priors
+    d = torch.from_numpy(g[tag + "_depth"]).to(device).requires_grad_(True)
+    n = torch.from_numpy(g[tag + "_normals"]).to(device).requires_grad_(True)
+    xy = torch.from_numpy(g[tag + "_coords"]).to(device) if tag != "b" else None
+    w = {"depth_prior": 1.0, "planarity": 0.5, "manhattan": 0.2, "normal_consistency": 0.1}
+    with replay(g, tag):
+        total, parts = priors.combine_structural_losses_v2(
+            d, n, None, xy, w, priors.ManhattanFrameEstimator(confidence_threshold=0.4),
+            priors.SemanticPlaneDetector(normal_threshold=0.5))
+    total.backward()
+    dd = d.grad.cpu().numpy() if d.grad is not None else np.zeros(d.shape, np.float32)
+    dn = n.grad.cpu().numpy() if n.grad is not None else np.zeros(n.shape, np.float32)
+    return float(total), {k: float(v.detach() if torch.is_tensor(v) else v) for k, v in parts.items()}, dd, dn
+
+
+def check(g, tag, total, parts, dd, dn, rtol, gtol):
+    np.testing.assert_allclose(total, float(g[tag + "_total"]), rtol=rtol)
+    want = {k[len(tag) + 6:]: float(g[k]) for k in g if k.startswith(tag + "_part_")}
+    assert set(parts) == set(want), (sorted(parts), sorted(want))
+    for k, v in want.items():
+        np.testing.assert_allclose(parts[k], v, rtol=rtol, atol=1e-7, err_msg=k)
+    for got, ref in ((dd, g[tag + "_dd"]), (dn, g[tag + "_dn"])):
+        scale = float(np.abs(ref).max()) + 1e-30
+        assert np.abs(got - ref).max() <= gtol * scale, (tag, np.abs(got - ref).max(), scale)
+
+
+def test_priors_cpu_vs_reference(nerf, golden):
+    g = golden("f18_priors")
+    check(g, "b", *run_case(nerf, g, "b", "cpu"), rtol=1e-6, gtol=1e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tag", CASES)
+def test_priors_gpu_vs_reference(nerf, gpu, golden, tag):
+    g = golden("f18_priors")
+    check(g, tag, *run_case(nerf, g, tag, gpu), rtol=1e-5, gtol=1e-4)
+
+
+@pytest.mark.gpu
+def test_nearest_pixel_vs_cdist(nerf, gpu):
+    from indoor_nerf_amd.priors import nearest_pixel
+    rng = np.random.default_rng(0)
+    flat = rng.choice(128 * 96, size=4096, replace=False)
+    xy = torch.from_numpy(np.stack([flat // 96, flat % 96], 1).astype(np.float32)).to(gpu)
+    idx1 = torch.from_numpy(rng.integers(0, 4096, 200)).to(gpu)
+    idx2, dist = nearest_pixel(xy, idx1)
+    D = torch.cdist(xy[idx1].cpu(), xy.cpu())
+    D[torch.arange(200), idx1.cpu()] = float("inf")
+    ref = torch.argmin(D, dim=-1)
+    assert torch.equal(idx2.cpu(), ref)
+    assert torch.equal(dist.cpu(), D[torch.arange(200), ref])
+
+
+@pytest.mark.gpu
+def test_train_step_with_structural_priors(nerf, gpu):
+    """The ScanNet configuration's iteration (normals head + structural priors at full ramp):
+    finite loss that includes the priors, gradients reach the normals head; GraphedTrainStep
+    runs such iterations eagerly."""
+    from indoor_nerf_amd.graphs import GraphedTrainStep
+    from indoor_nerf_amd.synthetic import scannet_bbox, scannet_rays
+    lo, hi = scannet_bbox()
+    args = nerf.make_args(bounding_box=(torch.from_numpy(lo), torch.from_numpy(hi)), finest_res=512, N_samples=64,
+                          N_importance=128, white_bkgd=False, use_structural_priors=True,
+                          structural_loss_start_iter=0, structural_loss_ramp_iters=1)
+    torch.manual_seed(0)
+    kw, _, _, grad_vars, opt = nerf.create_nerf(args, device=gpu)
+    assert args.predict_normals and kw["network_fine"].predict_normals
+    kw.update(near=0.1, far=10.0)
+    ro, rd, xy = scannet_rays(1024, seed=5)
+    rays = (torch.from_numpy(ro).to(gpu), torch.from_numpy(rd).to(gpu))
+    target = torch.rand(1024, 3, device=gpu)
+    st = GraphedTrainStep(rays, target, kw, opt, args, warmup=0)
+    for it in range(1, 4):
+        loss, psnr = st(it)
+    torch.cuda.synchronize()
+    assert st.captures == 0
+    assert torch.isfinite(loss).item()
+    head = [p for n, p in kw["network_fine"].named_parameters() if "normal" in n]
+    assert head and all(p.grad is not None and torch.isfinite(p.grad).all() for p in head)
+    # with coordinates: the nearest-pixel kernel path
+    loss2, _ = nerf.train_step(rays, target, kw, opt, args, 4, spatial_coords=torch.from_numpy(xy).to(gpu))
+    assert torch.isfinite(loss2).item()
