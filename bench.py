@@ -180,7 +180,7 @@ def main():
 
     wl = WORKLOADS[a.workload]
     rank, world, local = nerf.init_process_group()
-    dev = torch.device("cuda", local)
+    dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))   # ranks > GPUs only in rehearsals
     torch.cuda.set_device(dev)
     if wl["rays"] == "blender":
         lo, hi = blender_bbox()

@@ -26,7 +26,8 @@ def init_process_group(backend=None):
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29517")
     if backend is None:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        # NERF_DIST_BACKEND=gloo: rehearse the multi-rank path on one GPU (ranks share cuda:0)
+        backend = os.environ.get("NERF_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
     if backend == "nccl":
         torch.cuda.set_device(local)
     dist.init_process_group(backend=backend, rank=rank, world_size=world)
