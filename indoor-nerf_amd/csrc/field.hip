@@ -352,16 +352,17 @@ int launch_mlp_fwd_frag(const MlpArgs& a, hipStream_t stream);   // field_frag.h
 int launch_mlp_bwd_frag(const MlpArgs& a, hipStream_t stream);
 
 int launch_mlp_fwd_x6(const MlpArgs& a, hipStream_t stream);     // field_x6.hip
-int launch_mlp_bwd_x6(const MlpArgs& a, hipStream_t stream);
+int launch_mlp_bwd_x6(const MlpArgs& a, hipStream_t stream, bool split_roles);
 
 // MLP kernel generation, for A/B runs: NERF_MLP=1 the first version (f32 MFMA, LDS weight
-// images), NERF_MLP=2 the fragment-stationary f32-MFMA version (field_frag.hip); default (3): the
-// fp32-accurate bf16x6 version (field_x6.hip), 1.27x (forward) and 1.19x (backward) the f32-MFMA
-// kernels in the lego training step.
+// images), NERF_MLP=2 the fragment-stationary f32-MFMA version (field_frag.hip), NERF_MLP=3 the
+// fp32-accurate bf16x6 version (field_x6.hip) with one wave per tile in the backward; default (4):
+// bf16x6 with the backward split into chain / weight-gradient wave pairs (1.27x the one-wave x6
+// backward on the lego fine pass).
 static int mlp_version() {
     const char* e = getenv("NERF_MLP");
-    if (e && e[0] >= '1' && e[0] <= '3') return e[0] - '0';
-    return 3;
+    if (e && e[0] >= '1' && e[0] <= '4') return e[0] - '0';
+    return 4;
 }
 
 static bool use_frag_mlp() { return mlp_version() != 1; }
@@ -369,12 +370,13 @@ static bool use_frag_mlp() { return mlp_version() != 1; }
 static int launch_mlp_fwd_default(const MlpArgs& a, hipStream_t stream) {
     // the activation-quantizer calibration launch (layer 0 only) stays on the f32 path
     const int v = mlp_version();
-    if (v == 3 && !a.act_minmax) return launch_mlp_fwd_x6(a, stream);
+    if (v >= 3 && !a.act_minmax) return launch_mlp_fwd_x6(a, stream);
     return launch_mlp_fwd_frag(a, stream);
 }
 
 static int launch_mlp_bwd_default(const MlpArgs& a, hipStream_t stream) {
-    if (mlp_version() == 3) return launch_mlp_bwd_x6(a, stream);
+    const int v = mlp_version();
+    if (v >= 3) return launch_mlp_bwd_x6(a, stream, v == 4);
     return launch_mlp_bwd_frag(a, stream);
 }
 

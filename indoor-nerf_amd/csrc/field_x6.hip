@@ -171,6 +171,19 @@ __device__ __forceinline__ S3 row_read(const __bf16* img, int base, int S, int r
     return s;
 }
 
+// row_read over a staging image (piece stride `piece`)
+__device__ __forceinline__ S3 row_read_st(const __bf16* st, int piece, int S, int r, int col0) {
+    S3 s;
+    const int o0 = r * S + col0;
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+        const u32x2 a = *reinterpret_cast<const u32x2*>(st + p * piece + o0);
+        const u32x2 b = *reinterpret_cast<const u32x2*>(st + p * piece + o0 + 8);
+        s.p[p] = u32x4{a.x, a.y, b.x, b.y};
+    }
+    return s;
+}
+
 // Operand whose k index runs over the ROWS of a row-major image: lane (m = lane&31, h = lane>>5)
 // gets column col0 + m at rows row0 + 4h + (i&3) + 8(i>>2) (row0 = 16 x chunk, col0 = 32 x tile).
 // Two ds_read_b64_tr_b16 per piece: 16-lane group g reads the 4 x 16 block at rows row0 + 4h
@@ -607,6 +620,410 @@ __global__ void __launch_bounds__(256, 1) mlp_bwd_x6_kernel(MlpArgs a) {
     }
 }
 
+// ================================================================ backward, split roles
+// The one-wave-per-tile backward above runs at one wave per SIMD (its chain state and the twelve
+// dW accumulator tiles need ~470 registers), so every VALU split, LDS latency and dependent MFMA
+// of the tile is exposed. Here each tile is shared by a PAIR of waves on the same SIMD (waves p
+// and p + 4 of a 512-thread block): the chain wave runs the forward recompute and the transposed
+// chain and stages each (gradient tile, activation tile) pair; the wgrad wave holds the dW tiles
+// and turns each staged pair into six-MFMA products. Two waves per SIMD (256 registers each) let
+// one wave's VALU work hide under the other's MFMAs.
+// Hand-off per pair, over the pair's single staging buffer, with two LDS sequence counters:
+// the chain wave waits for ack == k - 1 before it writes stage k and then stores ready = k
+// (release: its staging writes are complete first); the wgrad wave waits for ready == k, reads
+// the stage and stores ack = k (release: its reads have returned). Both waves walk the same tile
+// list with the same eight stages per tile, so every wait is matched and the loop ends together.
+constexpr int CG_STAGES = 8;
+
+#ifdef NERF_X6CG_PROF   // diagnostic build only: wait / loop cycles of the chain and wgrad waves
+__device__ unsigned long long cg_prof[4];
+#define CG_T() __builtin_amdgcn_s_memtime()
+#endif
+
+__device__ __forceinline__ void flag_wait(int* f, int v, unsigned long long* waited = nullptr) {
+#ifdef NERF_X6CG_PROF
+    const unsigned long long t0 = CG_T();
+#endif
+    while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != v) __builtin_amdgcn_s_sleep(1);
+#ifdef NERF_X6CG_PROF
+    *waited += CG_T() - t0;
+#else
+    (void)waited;
+#endif
+}
+__device__ __forceinline__ void flag_set(int* f, int v) {
+    __hip_atomic_store(f, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// ... and with a scheduling barrier behind it, so that the compiler cannot hoist the MFMAs that
+// follow above the store (they do not depend on it), which would hold the partner wave for
+// their whole duration.
+__device__ __forceinline__ void flag_set_now(int* f, int v) {
+    __hip_atomic_store(f, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+template <bool QUANT>
+__device__ __forceinline__ void bwd_chain_role(const MlpArgs& a, const __bf16* img, __bf16* stA, __bf16* stG,
+                                               int* ready, int* ack, int p, int lane, const QuantRec& aq) {
+    const int j = lane & 31, h = lane >> 5;
+    int seq = 0;
+    unsigned long long waited = 0;
+#ifdef NERF_X6CG_PROF
+    const unsigned long long t_start = CG_T();
+#endif
+    auto open = [&]() { flag_wait(ack, seq, &waited); };
+    auto publish = [&]() { flag_set(ready, ++seq); };
+    const int64_t n_tiles = (a.P + 31) / 32;
+    for (int64_t tile = (int64_t)blockIdx.x * 4 + p; tile < n_tiles; tile += (int64_t)gridDim.x * 4) {
+        const __bf16* imt = img + opaque_zero();
+        InX6 in;
+        load_in_x6(a, tile, j, h, in);
+        ActX6 f;
+        floatx16 unused;
+        fwd_chain<QUANT>(imt, in, f, unused, lane, false, aq);
+
+        float4 g4 = *reinterpret_cast<const float4*>(a.graw + 4u * (in.valid ? in.pt : (uint32_t)(a.P - 1)));
+        if (!in.valid) g4 = make_float4(0.f, 0.f, 0.f, 0.f);
+        const bool keep = in.valid && (a.keep ? a.keep[in.pt] != 0 : true);
+        const float gsig = keep ? g4.w : 0.f;
+
+        // stage 1 (dC2): g_rgb, h3
+        floatx16 ga3[2];
+        {
+            const S3 GR = h ? split8(0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f)
+                            : split8(g4.x, g4.y, g4.z, 0.f, 0.f, 0.f, 0.f, 0.f);
+            open();
+            stage_grad(stG, GR, 0, j, h);      // columns 16..31 stale: they only reach dC2 rows >= 16
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int c = 0; c < 2; ++c) stage_act(stA, split_chunk(f.h3[t], c), t, c, j, h);
+            publish();
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                ga3[t] = mma6(tr_read(imt, IM_PIECE, IM_C2, S64, 0, 32 * t, lane), GR, zero16());
+#pragma unroll
+                for (int r = 0; r < 16; ++r) ga3[t][r] = f.h3[t][r] > 0.f ? ga3[t][r] : 0.f;
+            }
+        }
+        // stages 2, 3 (dC1 rows 32t..): ga3 tile t, h2
+        floatx16 ga2[2];
+        ga2[0] = ga2[1] = zero16();
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const S3 g0 = split_chunk(ga3[t], 0), g1 = split_chunk(ga3[t], 1);
+            open();
+            if (t == 0) {
+#pragma unroll
+                for (int ta = 0; ta < 2; ++ta)
+#pragma unroll
+                    for (int c = 0; c < 2; ++c) stage_act(stA, split_chunk(f.h2[ta], c), ta, c, j, h);
+            }
+            stage_grad(stG, g0, 0, j, h);
+            stage_grad(stG, g1, 1, j, h);
+            publish();
+#pragma unroll
+            for (int ti = 0; ti < 2; ++ti) {
+                ga2[ti] = mma6(tr_read(imt, IM_PIECE, IM_C1, S64, 32 * t, 32 * ti, lane), g0, ga2[ti]);
+                ga2[ti] = mma6(tr_read(imt, IM_PIECE, IM_C1, S64, 32 * t + 16, 32 * ti, lane), g1, ga2[ti]);
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) ga2[t][r] = f.h2[t][r] > 0.f ? ga2[t][r] : 0.f;
+
+        // stages 4, 5 (dC0 rows 32t..): ga2 tile t, [o ; sh]
+        floatx16 go = zero16();
+        if (h == 0) go[0] = gsig;
+        if (a.dgeo && in.valid) {
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+                const int row = row_of(r, h);
+                if (row >= 1) go[r] = a.dgeo[16u * in.pt + row];
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const S3 g0 = split_chunk(ga2[t], 0), g1 = split_chunk(ga2[t], 1);
+            open();
+            if (t == 0) {
+                stage_act(stA, split_chunk(f.o, 0), 0, 0, j, h);
+                float shv[8];
+                load_sh6(a, in.pt, in.valid, h, shv, opaque_zero());
+                stage_act(stA, split_arr(shv), 0, 1, j, h);
+            }
+            stage_grad(stG, g0, 0, j, h);
+            stage_grad(stG, g1, 1, j, h);
+            publish();
+            go = mma6(tr_read(imt, IM_PIECE, IM_C0, S32, 32 * t, 0, lane), g0, go);
+            go = mma6(tr_read(imt, IM_PIECE, IM_C0, S32, 32 * t + 16, 0, lane), g1, go);
+        }
+        if (a.dsh && in.valid) {
+#pragma unroll
+            for (int r = 8; r < 16; ++r) a.dsh[16u * in.pt + row_of(r, h) - 16] = go[r];
+        }
+
+        // stage 6 (dW1): go, h1 (recomputed from a reload of x)
+        float xr[16];
+        load_x6(a, in.pt, in.valid, h, xr, opaque_zero());
+        floatx16 h1[2];
+        uint32_t m1;
+        layer0<QUANT>(imt, xr, h1, m1, lane, aq);
+        floatx16 ga1[2];
+        {
+            const S3 GO = split_chunk(go, 0);
+            open();
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int c = 0; c < 2; ++c) stage_act(stA, split_chunk(h1[t], c), t, c, j, h);
+            stage_grad(stG, GO, 0, j, h);      // columns 16..31 stale: they only reach dW1 rows >= 16
+            publish();
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                floatx16 acc = mma6(tr_read(imt, IM_PIECE, IM_W1, S64, 0, 32 * t, lane), GO, zero16());
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const bool on = QUANT ? ((m1 >> (16 * t + r)) & 1u) != 0u : h1[t][r] > 0.f;
+                    acc[r] = on ? acc[r] : 0.f;
+                }
+                ga1[t] = acc;
+            }
+        }
+
+        // stages 7, 8 (dW0 rows 32t..): ga1 tile t, x; the wgrad wave also forms gx = W0^T ga1 from
+        // the staged ga1 (the d features, off this wave's critical path)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const S3 g0 = split_chunk(ga1[t], 0), g1 = split_chunk(ga1[t], 1);
+            open();
+            if (t == 0) {
+                stage_act(stA, split_arr(xr), 0, 0, j, h);
+                stage_act(stA, split_arr(xr + 8), 0, 1, j, h);
+            }
+            stage_grad(stG, g0, 0, j, h);
+            stage_grad(stG, g1, 1, j, h);
+            publish();
+        }
+    }
+#ifdef NERF_X6CG_PROF
+    if (lane == 0) { atomicAdd(&cg_prof[0], waited); atomicAdd(&cg_prof[1], CG_T() - t_start); }
+#endif
+}
+
+// The wgrad wave's operands. C2 (3 rows) and W1 (16 rows) use v_mfma_f32_16x16x32_bf16 tiles
+// (16 rows x 16 columns, all 32 points in one k step): half the matrix-pipe time and half the
+// accumulator registers of 32-row tiles. For a 16x16x32 operand lane l holds row/column
+// col0 + (l & 15) at the 8 points 4g + (i & 3) + 16(i >> 2), g = l >> 4 (any point permutation
+// works as long as both operands use the same one).
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ S3 tr_read16(const __bf16* st, int piece, int S, int col0, int lane) {
+    const int g = lane >> 4, il = lane & 15, q = il >> 2, p = il & 3;
+    const int oa = (4 * g + q) * S + col0 + 4 * p;
+    S3 s;
+#pragma unroll
+    for (int pc = 0; pc < 3; ++pc) {
+        const bf16x4 ta = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(st + pc * piece + oa));
+        const bf16x4 tb = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(st + pc * piece + oa + 16 * S));
+        const u32x2 a = __builtin_bit_cast(u32x2, ta), b = __builtin_bit_cast(u32x2, tb);
+        s.p[pc] = u32x4{a.x, a.y, b.x, b.y};
+    }
+    return s;
+}
+
+#define X6_MFMA16(a, b, c) \
+    __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, (a)), __builtin_bit_cast(bf16x8, (b)), (c), 0, 0, 0)
+
+__device__ __forceinline__ floatx4 mma6_16(const S3& A, const S3& B, floatx4 c) {
+    c = X6_MFMA16(A.p[0], B.p[2], c);
+    c = X6_MFMA16(A.p[2], B.p[0], c);
+    c = X6_MFMA16(A.p[1], B.p[1], c);
+    c = X6_MFMA16(A.p[0], B.p[1], c);
+    c = X6_MFMA16(A.p[1], B.p[0], c);
+    c = X6_MFMA16(A.p[0], B.p[0], c);
+    return c;
+}
+
+struct WgradX6 {
+    floatx4 dC2[4], dW1[4];                      // 16x16 tiles: rows 0..15, columns 16u..16u+15
+    floatx16 dC1[2][2], dC0[2][1], dW0[2][1];    // 32x32 tiles
+};
+
+// A 16-row stage: G columns 0..15 against the 64 staged activation columns.
+struct Ops16 {
+    S3 A, B[4];
+};
+__device__ __forceinline__ void read16(Ops16& o, const __bf16* stG, const __bf16* stA, int lane) {
+    o.A = tr_read16(stG, STG_PIECE, S32, 0, lane);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) o.B[u] = tr_read16(stA, STA_PIECE, S64, 16 * u, lane);
+}
+__device__ __forceinline__ void mma16(floatx4 (&acc)[4], const Ops16& o) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc[u] = mma6_16(o.A, o.B[u], acc[u]);
+}
+
+// A 32-row stage (NU activation tiles of 32 columns), operands for both 16-point chunks.
+template <int NU>
+struct Ops32 {
+    S3 A[2], B[2][NU];
+};
+template <int NU>
+__device__ __forceinline__ void read32(Ops32<NU>& o, const __bf16* stG, const __bf16* stA, int lane) {
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        o.A[c] = tr_read(stG, STG_PIECE, 0, S32, 16 * c, 0, lane);
+#pragma unroll
+        for (int u = 0; u < NU; ++u) o.B[c][u] = tr_read(stA, STA_PIECE, 0, S64, 16 * c, 32 * u, lane);
+    }
+}
+template <int NU>
+__device__ __forceinline__ void mma32(floatx16 (&acc)[NU], const Ops32<NU>& o) {
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int u = 0; u < NU; ++u) acc[u] = mma6(o.A[c], o.B[c][u], acc[u]);
+}
+
+// Every stage: wait for it, read all of its operands, release the buffer (ack), then run the MFMAs,
+// so the chain wave's next staging overlaps them.
+__device__ __forceinline__ void bwd_wgrad_role(const MlpArgs& a, const __bf16* img, const __bf16* stA,
+                                               const __bf16* stG, int* ready, int* ack, int p, int lane, WgradX6& g) {
+    const int j = lane & 31, h = lane >> 5;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) { g.dC2[u] = floatx4{0.f, 0.f, 0.f, 0.f}; g.dW1[u] = floatx4{0.f, 0.f, 0.f, 0.f}; }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        g.dC0[i][0] = zero16(); g.dW0[i][0] = zero16();
+        g.dC1[i][0] = zero16(); g.dC1[i][1] = zero16();
+    }
+    int seq = 0;
+    unsigned long long waited = 0;
+#ifdef NERF_X6CG_PROF
+    const unsigned long long t_start = CG_T();
+#endif
+    auto take = [&]() { flag_wait(ready, seq + 1, &waited); };
+    auto release = [&]() { flag_set_now(ack, ++seq); };
+    const int64_t n_tiles = (a.P + 31) / 32;
+    for (int64_t tile = (int64_t)blockIdx.x * 4 + p; tile < n_tiles; tile += (int64_t)gridDim.x * 4) {
+        {   // 1: dC2
+            Ops16 o;
+            take(); read16(o, stG, stA, lane); release();
+            mma16(g.dC2, o);
+        }
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {   // 2, 3: dC1
+            Ops32<2> o;   // 72 registers of operands: too many to hold beside the sums, no early release
+            take(); read32<2>(o, stG, stA, lane); flag_set(ack, ++seq);
+            mma32<2>(g.dC1[t], o);
+        }
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {   // 4, 5: dC0
+            Ops32<1> o;
+            take(); read32<1>(o, stG, stA, lane); release();
+            mma32<1>(g.dC0[t], o);
+        }
+        {   // 6: dW1
+            Ops16 o;
+            take(); read16(o, stG, stA, lane); release();
+            mma16(g.dW1, o);
+        }
+        floatx16 gx = zero16();
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {   // 7, 8: dW0, and gx = W0^T ga1 (B = the staged ga1, lane = point)
+            Ops32<1> o;
+            S3 gb[2];
+            take();
+            read32<1>(o, stG, stA, lane);
+#pragma unroll
+            for (int c = 0; c < 2; ++c) gb[c] = row_read_st(stG, STG_PIECE, S32, j, 16 * c + 4 * h);
+            flag_set(ack, ++seq);
+            mma32<1>(g.dW0[t], o);
+#pragma unroll
+            for (int c = 0; c < 2; ++c) gx = mma6(tr_read(img, IM_PIECE, IM_W0, S32, 32 * t + 16 * c, 0, lane), gb[c], gx);
+        }
+        const uint32_t pt = (uint32_t)(tile * 32 + j);
+        if (a.dfeat && tile * 32 + j < a.P) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int fi = row_of(r, h);
+                a.dfeat[pt * (uint32_t)a.sp + (fi >> 1) * (uint32_t)a.sl + (fi & 1)] = gx[r];
+            }
+        }
+    }
+    static_assert(CG_STAGES == 8, "stage list above");
+#ifdef NERF_X6CG_PROF
+    if (lane == 0) { atomicAdd(&cg_prof[2], waited); atomicAdd(&cg_prof[3], CG_T() - t_start); }
+#endif
+}
+
+template <bool QUANT>
+__global__ void __launch_bounds__(512, 1) mlp_bwd_x6cg_kernel(MlpArgs a) {
+    __shared__ __attribute__((aligned(16))) __bf16 lds[X6_BWD_LDS / 2];
+    __shared__ int flags[8];   // ready[0..3], ack[0..3]
+    __bf16* img = lds;
+    const int wv = threadIdx.x >> 6, p = wv & 3;
+    const bool wgrad_wave = wv >= 4;
+    __bf16* stA = lds + 3 * IM_PIECE + p * ST_WAVE;
+    __bf16* stG = stA + 3 * STA_PIECE;
+    fill_images(img, a.W);
+    if (threadIdx.x < 8) flags[threadIdx.x] = 0;
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
+    WgradX6 g;   // defined (and live) on the wgrad waves only
+    if (wgrad_wave) {
+        bwd_wgrad_role(a, img, stA, stG, flags + p, flags + 4 + p, p, lane, g);
+    } else {
+        QuantRec aq{};
+        if constexpr (QUANT) aq = *a.aq;
+        bwd_chain_role<QUANT>(a, img, stA, stG, flags + p, flags + 4 + p, p, lane, aq);
+    }
+
+    // ---- block reduction of the wgrad waves' tiles (LDS fp32 atomics), one global flush per block
+    __syncthreads();
+    float* gw = reinterpret_cast<float*>(lds);
+    for (int i = threadIdx.x; i < GW_TOTAL; i += blockDim.x) gw[i] = 0.f;
+    __syncthreads();
+    if (wgrad_wave) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int rr = row_of(r, h);
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                const int row = 32 * t + rr;
+#pragma unroll
+                for (int u = 0; u < 2; ++u) atomicAdd(gw + GW_C1 + row * 64 + 32 * u + j, g.dC1[t][u][r]);
+                if (j != 0) atomicAdd(gw + GW_C0 + row * 31 + (j < 16 ? 15 + j : j - 16), g.dC0[t][0][r]);
+                atomicAdd(gw + GW_W0 + row * 32 + j, g.dW0[t][0][r]);
+            }
+        }
+        // 16x16 tiles: lane l holds rows 4(l >> 4) + i, column 16u + (l & 15)
+        const int r0 = 4 * (lane >> 4), n = lane & 15;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                if (r0 + i < 3) atomicAdd(gw + GW_C2 + (r0 + i) * 64 + 16 * u + n, g.dC2[u][i]);
+                atomicAdd(gw + GW_W1 + (r0 + i) * 64 + 16 * u + n, g.dW1[u][i]);
+            }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < GW_TOTAL; i += blockDim.x) {
+        float* dst;
+        int k;
+        if (i < GW_W1) { dst = a.G.w0; k = i; }
+        else if (i < GW_C0) { dst = a.G.w1; k = i - GW_W1; }
+        else if (i < GW_C1) { dst = a.G.c0; k = i - GW_C0; }
+        else if (i < GW_C2) { dst = a.G.c1; k = i - GW_C1; }
+        else { dst = a.G.c2; k = i - GW_C2; }
+        const float v = gw[i];
+        if (v != 0.f) __hip_atomic_fetch_add(dst + k, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 // every element index the kernels form (feat, sh, raw/graw, geo/dgeo/dsh, dfeat) stays below 2^31
 static bool fits_u32(const MlpArgs& a) {
     const int64_t lim = (int64_t)1 << 31;
@@ -625,11 +1042,25 @@ int launch_mlp_fwd_x6(const MlpArgs& a, hipStream_t stream) {
     return NERF_OK;
 }
 
-int launch_mlp_bwd_x6(const MlpArgs& a, hipStream_t stream) {
+int launch_mlp_bwd_x6(const MlpArgs& a, hipStream_t stream, bool split_roles) {
     NERF_REQUIRE(fits_u32(a), "mlp_bwd(x6): %lld points exceed 32-bit indexing", (long long)a.P);
     const int64_t tiles = (a.P + 31) / 32;
     const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((tiles + 3) / 4, 256));
-    if (a.aq)
+    if (split_roles) {
+        if (a.aq)
+            hipLaunchKernelGGL(mlp_bwd_x6cg_kernel<true>, dim3((unsigned)blocks), dim3(512), 0, stream, a);
+        else
+            hipLaunchKernelGGL(mlp_bwd_x6cg_kernel<false>, dim3((unsigned)blocks), dim3(512), 0, stream, a);
+#ifdef NERF_X6CG_PROF
+        unsigned long long pr[4];
+        (void)hipDeviceSynchronize();
+        (void)hipMemcpyFromSymbol(pr, HIP_SYMBOL(cg_prof), sizeof(pr));
+        fprintf(stderr, "cgprof P=%lld chain wait/total %llu/%llu  wgrad wait/total %llu/%llu (s_memtime ticks, sum over waves)\n",
+                (long long)a.P, pr[0], pr[1], pr[2], pr[3]);
+        const unsigned long long z[4] = {0, 0, 0, 0};
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(cg_prof), z, sizeof(z));
+#endif
+    } else if (a.aq)
         hipLaunchKernelGGL(mlp_bwd_x6_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, stream, a);
     else
         hipLaunchKernelGGL(mlp_bwd_x6_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, stream, a);

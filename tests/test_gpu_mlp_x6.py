@@ -1,6 +1,7 @@
-"""The bf16x6 MLP kernels (csrc/field_x6.hip, NERF_MLP=3; the default forward: bf16 matrix cores,
-operands split into three bf16 pieces, six products per term) against the f32-MFMA kernels
-(field_frag.hip, NERF_MLP=2) and an fp64 reference: the x6 path must be as accurate as fp32.
+"""The bf16x6 MLP kernels (csrc/field_x6.hip; bf16 matrix cores, operands split into three bf16
+pieces, six products per term) against the f32-MFMA kernels (field_frag.hip, NERF_MLP=2) and an
+fp64 reference: the x6 path must be as accurate as fp32. Both x6 backward kernels are checked:
+NERF_MLP=3 (one wave per tile) and NERF_MLP=4 (the default: chain / weight-gradient wave pairs).
 
 Bar: per output / per weight-gradient tensor, the x6 error against fp64 is at most 2x the error of
 the same computation in plain PyTorch fp32 (the reference's own arithmetic; max and RMS), and
@@ -45,14 +46,15 @@ def _run(nerf, net, x, graw, version):
             os.environ["NERF_MLP"] = old
 
 
+@pytest.mark.parametrize("version", ["3", "4"])
 @pytest.mark.parametrize("scale", [0.5, 0.05])
-def test_x6_as_accurate_as_f32_mfma(nerf, gpu, scale):
+def test_x6_as_accurate_as_f32_mfma(nerf, gpu, scale, version):
     torch.manual_seed(1)
     net = nerf.NeRFSmall(2, 64, 15, 3, 64, 32, 16).to(gpu)
     P = 65536
     x = torch.randn(P, 48, device=gpu) * scale
     graw = torch.randn(P, 4, device=gpu)
-    raw6, dx6, g6 = _run(nerf, net, x, graw, "3")
+    raw6, dx6, g6 = _run(nerf, net, x, graw, version)
     raw2, dx2, g2 = _run(nerf, net, x, graw, "2")
     W64 = {k: p.detach().double().clone().requires_grad_(True) for k, p in net.named_parameters()}
     x64 = x.double().clone().requires_grad_(True)
@@ -85,3 +87,21 @@ def test_x6_as_accurate_as_f32_mfma(nerf, gpu, scale):
     for k in g6:
         check(k, g6[k], g2[k], W32[k].grad, W64[k].grad, bound=2e-5 * Wabs[k].grad + 1e-6)
     assert not fails, fails
+
+
+@pytest.mark.parametrize("P", [1, 31, 33, 1000, 4096 * 32 + 17, 300001])
+def test_split_backward_matches_one_wave_backward(nerf, gpu, P):
+    """The wave-pair backward (4) and the one-wave backward (3) do the same products per tile in the
+    same order; only the block-level fp32 reductions differ. Ragged sizes: pairs with no tile, a
+    partial last tile, more tiles than the persistent grid."""
+    torch.manual_seed(2)
+    net = nerf.NeRFSmall(2, 64, 15, 3, 64, 32, 16).to(gpu)
+    x = torch.randn(P, 48, device=gpu) * 0.3
+    graw = torch.randn(P, 4, device=gpu)
+    raw3, dx3, g3 = _run(nerf, net, x, graw, "3")
+    raw4, dx4, g4 = _run(nerf, net, x, graw, "4")
+    assert torch.equal(raw3, raw4)
+    assert torch.equal(dx3, dx4)    # per-point results: identical arithmetic
+    for k in g3:
+        scale = g3[k].abs().max().item() + 1e-30
+        assert (g4[k] - g3[k]).abs().max().item() <= 1e-5 * scale, k

@@ -32,8 +32,18 @@ def main():
         raw = net(xx)
         raw.backward(g)
 
+    vers = sys.argv[2].split(",") if len(sys.argv) > 2 else ["2", "3"]
+    grads = {}
+    for ver in vers:    # same inputs through each generation: max relative gradient difference
+        os.environ["NERF_MLP"] = ver
+        net.zero_grad()
+        xx.grad = None
+        fwdbwd()
+        grads[ver] = [q.grad.detach().clone() for q in net.parameters()] + [xx.grad.detach().clone()]
+    for ver in vers[1:]:
+        res[f"maxrel v{ver} vs v{vers[0]}"] = [max(float((a - b).abs().max() / b.abs().max().clamp_min(1e-30)) for a, b in zip(grads[ver], grads[vers[0]]))]
     for rnd in range(5):
-        for ver in ("2", "3"):
+        for ver in vers:
             os.environ["NERF_MLP"] = ver
             for name, fn in (("fwd", fwd), ("fwd+bwd", fwdbwd)):
                 for _ in range(2):
@@ -48,7 +58,7 @@ def main():
                     torch.cuda.synchronize()
                     ts.append(e0.elapsed_time(e1))
                 res.setdefault(f"v{ver} {name}", []).append(float(np.median(ts)))
-    print(json.dumps({k: round(float(np.median(v)), 4) for k, v in res.items()}))
+    print(json.dumps({k: float("%.4g" % float(np.median(v))) for k, v in res.items()}))
 
 
 if __name__ == "__main__":
