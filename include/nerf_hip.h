@@ -89,6 +89,22 @@ int nerf_hash_encode_bwd_ws(const float* d_xyz, int64_t n_points,
                             const float* d_dfeat, int64_t feat_stride_point, int64_t feat_stride_level,
                             float* const* d_dtables, void* d_workspace, size_t workspace_bytes, void* stream);
 
+/* The binned path split in two, so that several backwards into the same tables (the fine and the
+ * coarse pass of one iteration: two autograd nodes of HashEmbedder.forward, hash_encoding.py:82-107)
+ * share ONE owner pass. The workspace holds chunk_capacity 256-point chunks (workspace_bytes >=
+ * nerf_hash_encode_bwd_workspace_bytes(n_levels, log2_T, 256 * chunk_capacity)); a bin call writes
+ * its ceil(n_points / 256) chunks from chunk_base on, and the owner call sums chunks
+ * [0, n_chunks) into d_dtables (ACCUMULATED). Calls sharing a workspace must be stream-ordered and
+ * use the same n_levels, log2_T and chunk_capacity. */
+int nerf_hash_encode_bwd_bin(const float* d_xyz, int64_t n_points,
+                             const float* bbox_min3, const float* bbox_max3,
+                             const float* level_res, int n_levels, int log2_T,
+                             const float* d_dfeat, int64_t feat_stride_point, int64_t feat_stride_level,
+                             int64_t chunk_base, int64_t chunk_capacity,
+                             void* d_workspace, size_t workspace_bytes, void* stream);
+int nerf_hash_encode_bwd_owner(int n_levels, int log2_T, int64_t n_chunks, int64_t chunk_capacity,
+                               float* const* d_dtables, void* d_workspace, size_t workspace_bytes, void* stream);
+
 /* ---- spherical harmonics, degree 4 (SHEncoder.forward, hash_encoding.py:153-191) ---------- */
 int nerf_sh4_fwd(const float* d_dirs, int64_t n, float* d_out /* [n,16] */, void* stream);
 

@@ -28,7 +28,9 @@ struct HashGradParams {
     uint16_t* bin_h;      // entry row within its owner slice
     float2* bin_g;        // entry (d feat0, d feat1)
     uint32_t* bin_seg;    // [L][n_owner][nchunks]: segment start | count << 16 within the chunk region
-    int nchunks;
+    int nchunks;          // chunks the owner pass walks
+    int chunk_base;       // bin pass: chunk index of this launch's first 256 points
+    int chunk_stride;     // chunk capacity of the workspace (the layout stride)
     int slice_log2;       // owner slice = 2^slice_log2 rows (LDS: 8 B per row)
     int owner_log2;       // owners per level = 2^owner_log2
 };
@@ -265,11 +267,11 @@ __global__ void __launch_bounds__(256) hash_encode_bwd_kernel(
             const uint32_t ex0 = inc - v0 - v1, ex1 = ex0 + v0;
             if (o0 < n_own) {
                 s_start[o0] = ex0;
-                hp.bin_seg[((size_t)lvl * n_own + o0) * hp.nchunks + blockIdx.x] = ex0 | (v0 << 16);
+                hp.bin_seg[((size_t)lvl * n_own + o0) * hp.chunk_stride + hp.chunk_base + blockIdx.x] = ex0 | (v0 << 16);
             }
             if (o1 < n_own) {
                 s_start[o1] = ex1;
-                hp.bin_seg[((size_t)lvl * n_own + o1) * hp.nchunks + blockIdx.x] = ex1 | (v1 << 16);
+                hp.bin_seg[((size_t)lvl * n_own + o1) * hp.chunk_stride + hp.chunk_base + blockIdx.x] = ex1 | (v1 << 16);
             }
             if (o0 == n_own - 1) s_start[n_own] = ex1;
             if (o1 == n_own - 1) s_start[n_own] = ex1 + v1;
@@ -286,7 +288,7 @@ __global__ void __launch_bounds__(256) hash_encode_bwd_kernel(
         }
         __syncthreads();
         const uint32_t total = s_start[n_own];
-        const size_t base = ((size_t)lvl * hp.nchunks + blockIdx.x) * kChunkCap;
+        const size_t base = ((size_t)lvl * hp.chunk_stride + hp.chunk_base + blockIdx.x) * kChunkCap;
         // two entries per lane: rows as one dword, (d feat) x 2 as one dwordx4; a trailing odd
         // slot carries stale LDS bytes that no owner reads (owners read < count per segment)
         for (uint32_t i = 2 * threadIdx.x; i < total; i += 2 * 256) {
@@ -348,7 +350,7 @@ __global__ void __launch_bounds__(THREADS) hash_bwd_owner_kernel(HashGradParams 
     const int S = 1 << hp.slice_log2, n_own = 1 << hp.owner_log2;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     for (int i = tid; i < S; i += kOwnerThreads) s_slice[i] = make_double2(0.0, 0.0);
-    const uint32_t* seg = hp.bin_seg + ((size_t)lvl * n_own + o) * hp.nchunks;
+    const uint32_t* seg = hp.bin_seg + ((size_t)lvl * n_own + o) * hp.chunk_stride;
     for (int w0 = 0; w0 < hp.nchunks; w0 += kOwnerWindow) {
         const int nw = min(kOwnerWindow, hp.nchunks - w0);
         // segment counts of the window -> exclusive prefix s_pre (2 chunks per thread)
@@ -377,7 +379,7 @@ __global__ void __launch_bounds__(THREADS) hash_bwd_owner_kernel(HashGradParams 
         const int ce = (int)((int64_t)nw * (wave + 1) / (kOwnerThreads / 64));
         const uint32_t e_end = s_pre[ce];
         int c = cb;
-        const size_t region0 = ((size_t)lvl * hp.nchunks + w0) * kChunkCap;
+        const size_t region0 = ((size_t)lvl * hp.chunk_stride + w0) * kChunkCap;
         // addresses of entries e, e+64, ..., e+448 (chunk of each by forward tracking in s_pre);
         // an entry past the range loads slot 0 of the window (always mapped) and is masked later,
         // so the loads carry no control flow and stay in flight across the adds
@@ -435,12 +437,28 @@ __global__ void __launch_bounds__(THREADS) hash_bwd_owner_kernel(HashGradParams 
         }
         __syncthreads();   // s_pre / s_beg reused by the next window
     }
+    // Flush: every row's table load is issued before any add (one memory round trip per block,
+    // not one per row batch: a load behind the previous batch's store left 8 serial round trips).
+    __syncthreads();
     float2* dt = reinterpret_cast<float2*>(hp.dtables[lvl]) + (size_t)o * S;
-    for (int i = tid; i < S; i += kOwnerThreads) {
-        const double2 v = s_slice[i];
-        if (v.x != 0.0 || v.y != 0.0) {
-            const float2 t = dt[i];
-            dt[i] = make_float2((float)((double)t.x + v.x), (float)((double)t.y + v.y));
+    constexpr int kRows = (1 << SLICE_LOG2) / kOwnerThreads;
+    if (S == (1 << SLICE_LOG2)) {
+        float2 t[kRows];
+#pragma unroll
+        for (int k = 0; k < kRows; ++k) t[k] = dt[tid + k * kOwnerThreads];
+#pragma unroll
+        for (int k = 0; k < kRows; ++k) {
+            const double2 v = s_slice[tid + k * kOwnerThreads];
+            if (v.x != 0.0 || v.y != 0.0)
+                dt[tid + k * kOwnerThreads] = make_float2((float)((double)t[k].x + v.x), (float)((double)t[k].y + v.y));
+        }
+    } else {   // small tables (log2_T < slice): one partial slice per level
+        for (int i = tid; i < S; i += kOwnerThreads) {
+            const double2 v = s_slice[i];
+            if (v.x != 0.0 || v.y != 0.0) {
+                const float2 t = dt[i];
+                dt[i] = make_float2((float)((double)t.x + v.x), (float)((double)t.y + v.y));
+            }
         }
     }
 }
@@ -575,6 +593,8 @@ static int hash_encode_bwd_impl(const float* d_xyz, int64_t n_points, const floa
         hp.bin_h = reinterpret_cast<uint16_t*>(ws + B.off_h);
         hp.bin_seg = reinterpret_cast<uint32_t*>(ws + B.off_off);
         hp.nchunks = B.nchunks;
+        hp.chunk_base = 0;
+        hp.chunk_stride = B.nchunks;
         hp.slice_log2 = B.slice_log2;
         hp.owner_log2 = B.owner_log2;
     }
@@ -630,4 +650,83 @@ extern "C" int nerf_hash_encode_bwd_ws(const float* d_xyz, int64_t n_points, con
     return hash_encode_bwd_impl(d_xyz, n_points, bbox_min3, bbox_max3, level_res, n_levels, log2_T, d_dfeat,
                                 feat_stride_point, feat_stride_level, d_dtables, d_workspace, workspace_bytes,
                                 stream);
+}
+
+// ---- split binned backward: several bin launches, one owner launch --------------------------
+// The fine and the coarse pass of a training iteration scatter into the same tables; binning both
+// into one workspace (side by side, chunk_base apart) and summing them with ONE owner launch pays
+// the owner's per-launch costs (LDS clear, slice flush = a read-modify-write of every table row)
+// once per iteration instead of once per pass.
+static int bin_layout(const char* who, int n_levels, int log2_T, int64_t chunk_capacity, void* d_workspace,
+                      size_t workspace_bytes, HashGradParams& hp) {
+    NERF_REQUIRE(n_levels >= 1 && n_levels <= NERF_MAX_LEVELS, "%s: n_levels %d", who, n_levels);
+    NERF_REQUIRE(chunk_capacity >= 1 && chunk_capacity <= (int64_t)1 << 26, "%s: chunk_capacity %lld", who,
+                 (long long)chunk_capacity);
+    BinPlan B{};
+    NERF_REQUIRE(make_bin_plan(n_levels, log2_T, chunk_capacity * 256, B), "%s: no binned path for log2_T %d", who,
+                 log2_T);
+    NERF_REQUIRE(d_workspace != nullptr && workspace_bytes >= B.total,
+                 "%s: workspace %zu B < %zu B (nerf_hash_encode_bwd_workspace_bytes(L, log2_T, 256 * capacity))", who,
+                 workspace_bytes, B.total);
+    char* ws = static_cast<char*>(d_workspace);
+    hp.bin_g = reinterpret_cast<float2*>(ws + B.off_g);
+    hp.bin_h = reinterpret_cast<uint16_t*>(ws + B.off_h);
+    hp.bin_seg = reinterpret_cast<uint32_t*>(ws + B.off_off);
+    hp.chunk_stride = B.nchunks;
+    hp.slice_log2 = B.slice_log2;
+    hp.owner_log2 = B.owner_log2;
+    hp.mask = (uint32_t)((1u << log2_T) - 1u);
+    return NERF_OK;
+}
+
+extern "C" int nerf_hash_encode_bwd_bin(const float* d_xyz, int64_t n_points, const float* bbox_min3,
+                                        const float* bbox_max3, const float* level_res, int n_levels, int log2_T,
+                                        const float* d_dfeat, int64_t feat_stride_point, int64_t feat_stride_level,
+                                        int64_t chunk_base, int64_t chunk_capacity, void* d_workspace,
+                                        size_t workspace_bytes, void* stream) {
+    NERF_REQUIRE(n_points >= 0, "hash_encode_bwd_bin: n_points < 0");
+    NERF_REQUIRE(d_xyz && d_dfeat && level_res && bbox_min3 && bbox_max3, "hash_encode_bwd_bin: null arg");
+    HashGradParams hp{};
+    const int rc = bin_layout("hash_encode_bwd_bin", n_levels, log2_T, chunk_capacity, d_workspace, workspace_bytes,
+                              hp);
+    if (rc) return rc;
+    const int64_t nch = (n_points + 255) / 256;
+    NERF_REQUIRE(chunk_base >= 0 && chunk_base + nch <= chunk_capacity,
+                 "hash_encode_bwd_bin: chunks [%lld, %lld) exceed the capacity %lld", (long long)chunk_base,
+                 (long long)(chunk_base + nch), (long long)chunk_capacity);
+    if (n_points == 0) return NERF_OK;
+    for (int a = 0; a < 3; ++a) { hp.bmin[a] = bbox_min3[a]; hp.bmax[a] = bbox_max3[a]; }
+    fill_cells(hp.cell, bbox_min3, bbox_max3, level_res, n_levels);
+    hp.chunk_base = (int)chunk_base;
+    hp.nchunks = (int)(chunk_base + nch);
+    hipLaunchKernelGGL(hash_encode_bwd_kernel<3>, dim3((unsigned)nch, n_levels), dim3(256), 0, as_stream(stream),
+                       d_xyz, n_points, hp, d_dfeat, feat_stride_point, feat_stride_level);
+    NERF_CHECK_LAUNCH("hash_encode_bwd_bin");
+    return NERF_OK;
+}
+
+extern "C" int nerf_hash_encode_bwd_owner(int n_levels, int log2_T, int64_t n_chunks, int64_t chunk_capacity,
+                                          float* const* d_dtables, void* d_workspace, size_t workspace_bytes,
+                                          void* stream) {
+    HashGradParams hp{};
+    const int rc = bin_layout("hash_encode_bwd_owner", n_levels, log2_T, chunk_capacity, d_workspace,
+                              workspace_bytes, hp);
+    if (rc) return rc;
+    NERF_REQUIRE(n_chunks >= 0 && n_chunks <= chunk_capacity, "hash_encode_bwd_owner: n_chunks %lld of %lld",
+                 (long long)n_chunks, (long long)chunk_capacity);
+    NERF_REQUIRE(d_dtables, "hash_encode_bwd_owner: null grad tables");
+    for (int l = 0; l < n_levels; ++l) {
+        NERF_REQUIRE(d_dtables[l], "hash_encode_bwd_owner: grad table %d is null", l);
+        hp.dtables[l] = d_dtables[l];
+    }
+    if (n_chunks == 0) return NERF_OK;
+    hp.nchunks = (int)n_chunks;
+    if (owner_variant() == 1)
+        hipLaunchKernelGGL((hash_bwd_owner_kernel<13, 1024>), dim3(1u << hp.owner_log2, n_levels), dim3(1024), 0,
+                           as_stream(stream), hp);
+    else
+        hipLaunchKernelGGL((hash_bwd_owner_kernel<12, 512>), dim3(1u << hp.owner_log2, n_levels), dim3(512), 0,
+                           as_stream(stream), hp);
+    NERF_CHECK_LAUNCH("hash_encode_bwd_owner");
+    return NERF_OK;
 }

@@ -92,8 +92,67 @@ def bwd_workspace(n_levels, log2_T, n_points, device):
     return hit
 
 
-def hash_encode_bwd(xyz, meta, dfeat, sp, sl, grad_tables):
-    """Scatter-add d feat into the gradient tables (hash_encoding.py:82-107 autograd; csrc/hashgrid.hip)."""
+class _PendingBins:
+    """Binned hash backwards of the running autograd pass that await their owner pass (per device).
+    The fine and the coarse pass of a training iteration are two HashEncode nodes scattering into
+    the same tables: both bin into one workspace, side by side, and ONE owner launch sums them, queued
+    as the pass's final callback (it runs before backward() returns, so .grad is complete, and under
+    a HIP-graph capture it is captured like the rest of the backward)."""
+
+    def __init__(self):
+        self.ws, self.cap, self.used, self.peak = None, 0, 0, 0
+        self.tag = self.grads = self.stream = None
+
+    def flush(self):
+        if self.used == 0:
+            return
+        L, log2_T, _ = self.tag
+        with torch.cuda.stream(self.stream):
+            _lib.call("nerf_hash_encode_bwd_owner", L, log2_T, self.used, self.cap,
+                      _lib.ptr_array(self.grads, "grad_tables"), _lib.ptr(self.ws, "workspace", dtype=torch.uint8),
+                      self.ws.numel(), _lib.stream())
+        cur = torch.cuda.current_stream()
+        if cur != self.stream:
+            cur.wait_stream(self.stream)
+        self.used, self.tag, self.grads = 0, None, None
+
+    def add(self, xyz, meta, dfeat, sp, sl, grad_tables):
+        L, log2_T, P = len(grad_tables), meta["log2_T"], xyz.shape[0]
+        n_ch = (P + 255) // 256
+        tag = (L, log2_T, tuple(g.data_ptr() for g in grad_tables))
+        total = (self.used if self.tag == tag else 0) + n_ch
+        self.peak = max(self.peak, total)     # the next pass sizes its workspace for this
+        if self.used and (self.tag != tag or total > self.cap):
+            self.flush()
+        lib = _lib.load()
+        if self.used == 0:
+            cap = max(self.peak, n_ch)
+            need = int(lib.nerf_hash_encode_bwd_workspace_bytes(L, log2_T, 256 * cap))
+            if self.ws is None or self.ws.numel() < need:
+                self.ws = None
+                self.ws = torch.empty(need, dtype=torch.uint8, device=xyz.device)
+            self.cap = cap
+            self.tag, self.grads, self.stream = tag, list(grad_tables), torch.cuda.current_stream()
+            torch.autograd.Variable._execution_engine.queue_callback(self.flush)
+        _lib.call("nerf_hash_encode_bwd_bin", _lib.ptr(xyz, "xyz"), P, meta["bmin"], meta["bmax"], meta["res"], L,
+                  log2_T, _lib.ptr(dfeat, "grad_feat"), sp, sl, self.used, self.cap,
+                  _lib.ptr(self.ws, "workspace", dtype=torch.uint8), self.ws.numel(), _lib.stream())
+        self.used += n_ch
+
+
+_PENDING = {}
+
+
+def hash_encode_bwd(xyz, meta, dfeat, sp, sl, grad_tables, defer=None):
+    """Scatter-add d feat into the gradient tables (hash_encoding.py:82-107 autograd; csrc/hashgrid.hip).
+    defer (default: inside an autograd backward pass) bins now and leaves the owner pass to the end
+    of the pass (_PendingBins), shared with the other hash backwards of the pass."""
+    L, log2_T, P = len(grad_tables), meta["log2_T"], xyz.shape[0]
+    if defer is None:
+        defer = torch._C._current_graph_task_id() != -1
+    if defer and P > 0 and int(_lib.load().nerf_hash_encode_bwd_workspace_bytes(L, log2_T, P)) > 0:
+        _PENDING.setdefault(str(xyz.device), _PendingBins()).add(xyz, meta, dfeat, sp, sl, grad_tables)
+        return
     ws, nbytes = bwd_workspace(len(grad_tables), meta["log2_T"], xyz.shape[0], xyz.device)
     _lib.call("nerf_hash_encode_bwd_ws", _lib.ptr(xyz, "xyz"), xyz.shape[0], meta["bmin"], meta["bmax"],
               meta["res"], len(grad_tables), meta["log2_T"], _lib.ptr(dfeat, "grad_feat"), sp, sl,

@@ -33,6 +33,16 @@ def test_error_path_reports_message(nerf):
                None, None, 2, 2, None, None)
     with pytest.raises(RuntimeError, match="S must be"):
         L.call("nerf_composite_fwd", None, 4, None, None, None, 4, 1000, 0, *([None] * 7), None)
+    # split binned backward: the chunk range and the workspace size are checked before any launch
+    need = L.load().nerf_hash_encode_bwd_workspace_bytes(16, 19, 256 * 4)
+    fake = ctypes.c_void_p(1 << 20)
+    with pytest.raises(RuntimeError, match="n_chunks 5 of 4"):
+        L.call("nerf_hash_encode_bwd_owner", 16, 19, 5, 4, None, fake, need, None)
+    with pytest.raises(RuntimeError, match="workspace"):
+        L.call("nerf_hash_encode_bwd_owner", 16, 19, 4, 4, None, fake, need - 1, None)
+    with pytest.raises(RuntimeError, match="exceed the capacity"):
+        L.call("nerf_hash_encode_bwd_bin", fake, 3 * 256 + 1, L.host_f32([0] * 3), L.host_f32([1] * 3),
+               L.host_f32([16] * 16), 16, 19, fake, 32, 2, 1, 4, fake, need, None)
 
 
 def _oracle_lib():

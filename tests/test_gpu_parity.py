@@ -381,6 +381,31 @@ def test_train_loss_head_vs_torch_fp32(nerf, gpu):
 
 
 @pytest.mark.gpu
+def test_hash_encode_bwd_deferred_two_passes(nerf, gpu):
+    """Two HashEmbedder forwards in one autograd pass (the coarse and the fine pass of a step) bin
+    into one workspace and share ONE owner launch at the end of the pass (hashgrid._PendingBins):
+    the gradient equals two direct binned backwards (same entries, one fp32 rounding fewer), also
+    when a later, larger pass outgrows the workspace (early flush, then a regrown capacity)."""
+    emb = _embedder(nerf, gpu, 1024, closed_form_table())
+    lo, hi = blender_bbox()
+    rng = np.random.RandomState(7)
+    for sizes in ((70_001, 20_000), (200_000, 70_001, 513), (200_000, 70_001, 513)):
+        xs = [torch.from_numpy((lo + (hi - lo) * rng.rand(n, 3)).astype(np.float32)).to(gpu) for n in sizes]
+        ds = [torch.from_numpy(rng.randn(n, 32).astype(np.float32)).to(gpu) for n in sizes]
+        for e in emb.embeddings:
+            e.weight.grad = None
+        sum((emb(x)[0] * d).sum() for x, d in zip(xs, ds)).backward()
+        got = torch.stack([e.weight.grad for e in emb.embeddings])
+        ref = [torch.zeros(1 << 19, 2, device=gpu) for _ in range(16)]
+        for x, d in zip(xs, ds):
+            nerf.hashgrid.hash_encode_bwd(x, emb._meta, d, 32, 2, ref, defer=False)
+        ref = torch.stack(ref)
+        # the reference rounds each pass's slice sum to fp32 before adding: cancelling rows differ
+        # by a few ulp of the level's largest gradient
+        torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-6 * float(ref.abs().max()))
+
+
+@pytest.mark.gpu
 def test_hash_encode_bwd_large_ray_ordered(nerf, gpu, oracle):
     """The coarse pass at the metric config (4096 lego rays x 64 sorted samples, finest 1024):
     gradient tables of the binned path (workspace; LDS owner sums) and of the direct atomic path

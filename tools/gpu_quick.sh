@@ -1,0 +1,8 @@
+# GPU suite + the lego bench + a kernel-trace profile (outputs under gpurun_out/)
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || exit 1
+timeout -k 10 200 python -u bench.py --no-cpu-baseline > gpurun_out/bench.json 2> gpurun_out/bench.err || exit 2
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/prof_q" -o trace -- \
+    python3 "$GRAFT_REPO_ROOT/bench.py" --no-cpu-baseline --profile-kernels 0 > "$GRAFT_REPO_ROOT/gpurun_out/prof_q/trace_bench.json" 2> /dev/null || exit 3
