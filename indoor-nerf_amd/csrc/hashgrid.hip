@@ -374,51 +374,85 @@ __global__ void __launch_bounds__(THREADS) hash_bwd_owner_kernel(HashGradParams 
         if (i1 <= nw) s_pre[i1] = ex + c0;
         if (i1 + 1 == nw) s_pre[nw] = ex + pair;   // nw == kOwnerWindow: no thread has i0 == nw
         __syncthreads();
-        // entries of the window split by chunk ranges across the waves, lane-strided inside
-        const int cb = (int)((int64_t)nw * wave / (kOwnerThreads / 64));
-        const int ce = (int)((int64_t)nw * (wave + 1) / (kOwnerThreads / 64));
-        const uint32_t e_end = s_pre[ce];
-        int c = cb;
+        // The window's entries split evenly across the waves; a wave walks its range 64 entries
+        // (one per lane) per step. Chunk lookup is wave-cooperative, with no per-lane walk: lane l
+        // holds the boundary s_pre[cw + l] of a 64-chunk window; the chunk of entry e is the last
+        // boundary <= e: a ballot gives the step's first chunk, and the few boundaries that fall
+        // inside the step (read with readlane) move the lanes past them. A step ends at the
+        // window's last boundary; a step starting beyond it reloads the window (binary search).
+        constexpr int kWaves = kOwnerThreads / 64;
+        const uint32_t tot = s_pre[nw];
+        const uint32_t e_beg = (uint32_t)((uint64_t)tot * wave / kWaves);
+        const uint32_t e_end = (uint32_t)((uint64_t)tot * (wave + 1) / kWaves);
         const size_t region0 = ((size_t)lvl * hp.chunk_stride + w0) * kChunkCap;
-        // addresses of entries e, e+64, ..., e+448 (chunk of each by forward tracking in s_pre);
-        // an entry past the range loads slot 0 of the window (always mapped) and is masked later,
-        // so the loads carry no control flow and stay in flight across the adds
-        auto track = [&](uint32_t e, size_t (&addr)[8], uint32_t& valid) {
+        int cw = 0;
+        uint32_t Bw = 0, Gw = 0, B63 = 0;   // B63: first entry beyond the window's chunks cw .. cw+62
+        auto reload = [&](uint32_t E) {
+            int lo = 0, hi = nw;   // s_pre[lo] <= E < s_pre[hi]
+            while (hi - lo > 1) {
+                const int mid = (lo + hi) >> 1;
+                if (s_pre[mid] <= E) lo = mid; else hi = mid;
+            }
+            cw = lo;
+            const int ci = cw + lane;
+            Bw = ci <= nw ? s_pre[ci] : 0xFFFFFFFFu;
+            Gw = ci < nw ? (uint32_t)s_beg[ci] : 0u;
+            B63 = __builtin_amdgcn_readlane(Bw, 63);
+        };
+        // address of entry E + lane (ok: inside [E, end of step)); returns the next step's start
+        auto step = [&](uint32_t E, size_t& addr, bool& ok) -> uint32_t {
+            if (E >= e_end) { addr = region0; ok = false; return E; }
+            if (E >= B63) reload(E);
+            const uint32_t lim = min(min(E + 64u, B63), e_end);
+            const uint32_t e = E + lane;
+            int idx = __popcll(__ballot(Bw <= E)) - 1;
+            uint64_t inner = __ballot(Bw > E && Bw < lim);
+            while (inner) {
+                const int b = __ffsll((unsigned long long)inner) - 1;
+                inner &= inner - 1;
+                idx += e >= (uint32_t)__builtin_amdgcn_readlane(Bw, b) ? 1 : 0;
+            }
+            const uint32_t cur = (uint32_t)__builtin_amdgcn_ds_bpermute(idx << 2, (int)Bw);
+            const uint32_t beg = (uint32_t)__builtin_amdgcn_ds_bpermute(idx << 2, (int)Gw);
+            ok = e < lim;
+            addr = ok ? region0 + (size_t)(cw + idx) * kChunkCap + beg + (e - cur) : region0;
+            return lim;
+        };
+        auto track = [&](uint32_t& E, size_t (&addr)[8], uint32_t& valid) {
             valid = 0;
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                const uint32_t ej = e + 64u * j;
-                addr[j] = region0;
-                if (ej < e_end) {
-                    while (s_pre[c + 1] <= ej) ++c;
-                    addr[j] = region0 + (size_t)c * kChunkCap + s_beg[c] + (ej - s_pre[c]);
-                    valid |= 1u << j;
-                }
+                bool ok;
+                E = step(E, addr[j], ok);
+                valid |= (ok ? 1u : 0u) << j;
             }
         };
         auto fetch = [&](const size_t (&addr)[8], uint16_t (&h)[8], float2 (&g)[8]) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 h[j] = __builtin_nontemporal_load(hp.bin_h + addr[j]);
-                const float2* gp = hp.bin_g + addr[j];
-                g[j] = make_float2(__builtin_nontemporal_load(&gp->x), __builtin_nontemporal_load(&gp->y));
+                // (d feat0, d feat1) as ONE 8-B load
+                const uint64_t gv = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(hp.bin_g + addr[j]));
+                g[j] = make_float2(__uint_as_float((uint32_t)gv), __uint_as_float((uint32_t)(gv >> 32)));
             }
         };
-        // software pipeline: the next batch's 16 loads are in flight while this batch's adds run
+        // software pipeline: the next batch's loads are in flight while this batch's adds run
         size_t addr[8];
         uint16_t h[8];
         float2 g[8];
         uint32_t valid;
-        uint32_t e = s_pre[cb] + lane;
-        track(e, addr, valid);
+        uint32_t E = e_beg;
+        if (E < e_end) reload(E);
+        track(E, addr, valid);
         fetch(addr, h, g);
-        while (e < e_end) {
+        // the loop and step() (ballots, readlane, bpermute) stay wave-uniform: exit only when no
+        // lane of the wave has an entry left
+        while (__ballot(valid != 0u) != 0ull) {
             size_t addr2[8];
             uint16_t h2[8];
             float2 g2[8];
             uint32_t valid2;
-            const uint32_t en = e + 64u * 8;
-            track(en, addr2, valid2);
+            track(E, addr2, valid2);
             fetch(addr2, h2, g2);
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
@@ -433,7 +467,6 @@ __global__ void __launch_bounds__(THREADS) hash_bwd_owner_kernel(HashGradParams 
                 g[j] = g2[j];
             }
             valid = valid2;
-            e = en;
         }
         __syncthreads();   // s_pre / s_beg reused by the next window
     }
