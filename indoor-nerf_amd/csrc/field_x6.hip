@@ -662,10 +662,32 @@ __device__ __forceinline__ void flag_set_now(int* f, int v) {
     __builtin_amdgcn_sched_barrier(0);
 }
 
+// fp32 activation staging of the split-role backward: [64 neurons][SPF] fp32, column = point.
+// The chain wave stores its activation tiles unsplit (one ds_write_b32 per value); the wgrad wave
+// reads each operand fragment with two ds_read_b128, releases the buffer and only then splits it
+// into bf16 pieces, so the split of every staged activation runs on the wave that otherwise waits
+// (measured with NERF_X6CG_PROF before: chain wave busy 75 %, wgrad wave 28 %).
+constexpr int SPF = 36;                                   // row stride: conflict-free b128 reads
+constexpr int ACTF_FLOATS = 64 * SPF;                     // 9,216 B
+constexpr int ST_CG = 2 * ACTF_FLOATS + 3 * STG_PIECE;    // per wave pair, bf16 elements (16,128 B)
+constexpr int X6_CG_LDS = IM_BYTES + 4 * ST_CG * 2;       // 131,328 B
+
+__device__ __forceinline__ void stage_tileF(float* actF, const floatx16& v, int row0, int j, int h) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) actF[(row0 + row_of(r, h)) * SPF + j] = v[r];
+}
+
+// element i of v <-> neuron row0 + 4h + (i&3) + 8(i>>2)
+__device__ __forceinline__ void stage_arrF(float* actF, const float* v, int row0, int j, int h) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) actF[(row0 + 4 * h + (i & 3) + 8 * (i >> 2)) * SPF + j] = v[i];
+}
+
 template <bool QUANT>
 __device__ __forceinline__ void bwd_chain_role(const MlpArgs& a, const __bf16* img, __bf16* stA, __bf16* stG,
                                                int* ready, int* ack, int p, int lane, const QuantRec& aq) {
     const int j = lane & 31, h = lane >> 5;
+    float* actF = reinterpret_cast<float*>(stA);
     int seq = 0;
     unsigned long long waited = 0;
 #ifdef NERF_X6CG_PROF
@@ -695,9 +717,7 @@ __device__ __forceinline__ void bwd_chain_role(const MlpArgs& a, const __bf16* i
             open();
             stage_grad(stG, GR, 0, j, h);      // columns 16..31 stale: they only reach dC2 rows >= 16
 #pragma unroll
-            for (int t = 0; t < 2; ++t)
-#pragma unroll
-                for (int c = 0; c < 2; ++c) stage_act(stA, split_chunk(f.h3[t], c), t, c, j, h);
+            for (int t = 0; t < 2; ++t) stage_tileF(actF, f.h3[t], 32 * t, j, h);
             publish();
 #pragma unroll
             for (int t = 0; t < 2; ++t) {
@@ -715,9 +735,7 @@ __device__ __forceinline__ void bwd_chain_role(const MlpArgs& a, const __bf16* i
             open();
             if (t == 0) {
 #pragma unroll
-                for (int ta = 0; ta < 2; ++ta)
-#pragma unroll
-                    for (int c = 0; c < 2; ++c) stage_act(stA, split_chunk(f.h2[ta], c), ta, c, j, h);
+                for (int ta = 0; ta < 2; ++ta) stage_tileF(actF, f.h2[ta], 32 * ta, j, h);
             }
             stage_grad(stG, g0, 0, j, h);
             stage_grad(stG, g1, 1, j, h);
@@ -748,10 +766,11 @@ __device__ __forceinline__ void bwd_chain_role(const MlpArgs& a, const __bf16* i
             const S3 g0 = split_chunk(ga2[t], 0), g1 = split_chunk(ga2[t], 1);
             open();
             if (t == 0) {
-                stage_act(stA, split_chunk(f.o, 0), 0, 0, j, h);
+#pragma unroll
+                for (int r = 0; r < 8; ++r) actF[row_of(r, h) * SPF + j] = f.o[r];
                 float shv[8];
                 load_sh6(a, in.pt, in.valid, h, shv, opaque_zero());
-                stage_act(stA, split_arr(shv), 0, 1, j, h);
+                stage_arrF(actF, shv, 16, j, h);
             }
             stage_grad(stG, g0, 0, j, h);
             stage_grad(stG, g1, 1, j, h);
@@ -775,9 +794,7 @@ __device__ __forceinline__ void bwd_chain_role(const MlpArgs& a, const __bf16* i
             const S3 GO = split_chunk(go, 0);
             open();
 #pragma unroll
-            for (int t = 0; t < 2; ++t)
-#pragma unroll
-                for (int c = 0; c < 2; ++c) stage_act(stA, split_chunk(h1[t], c), t, c, j, h);
+            for (int t = 0; t < 2; ++t) stage_tileF(actF, h1[t], 32 * t, j, h);
             stage_grad(stG, GO, 0, j, h);      // columns 16..31 stale: they only reach dW1 rows >= 16
             publish();
 #pragma unroll
@@ -799,8 +816,8 @@ __device__ __forceinline__ void bwd_chain_role(const MlpArgs& a, const __bf16* i
             const S3 g0 = split_chunk(ga1[t], 0), g1 = split_chunk(ga1[t], 1);
             open();
             if (t == 0) {
-                stage_act(stA, split_arr(xr), 0, 0, j, h);
-                stage_act(stA, split_arr(xr + 8), 0, 1, j, h);
+                stage_arrF(actF, xr, 0, j, h);
+                stage_arrF(actF, xr + 8, 16, j, h);
             }
             stage_grad(stG, g0, 0, j, h);
             stage_grad(stG, g1, 1, j, h);
@@ -852,31 +869,51 @@ struct WgradX6 {
 };
 
 // A 16-row stage: G columns 0..15 against the 64 staged activation columns.
-struct Ops16 {
-    S3 A, B[4];
+// Raw fp32 activation fragments (8 values), split into pieces after the buffer is released.
+struct Raw8 {
+    float4 a, b;
 };
-__device__ __forceinline__ void read16(Ops16& o, const __bf16* stG, const __bf16* stA, int lane) {
+__device__ __forceinline__ S3 split_raw(const Raw8& v) {
+    return split8(v.a.x, v.a.y, v.a.z, v.a.w, v.b.x, v.b.y, v.b.z, v.b.w);
+}
+// 32x32x16 B operand: lane (m, h) <-> neuron col0 + m at points row0 + 4h + (i&3) + 8(i>>2)
+__device__ __forceinline__ Raw8 act_read32(const float* actF, int row0, int col0, int lane) {
+    const float* q = actF + (col0 + (lane & 31)) * SPF + row0 + 4 * (lane >> 5);
+    return Raw8{*reinterpret_cast<const float4*>(q), *reinterpret_cast<const float4*>(q + 8)};
+}
+// 16x16x32 B operand: lane l <-> neuron col0 + (l & 15) at points 4(l >> 4) + (i&3) + 16(i>>2)
+__device__ __forceinline__ Raw8 act_read16(const float* actF, int col0, int lane) {
+    const float* q = actF + (col0 + (lane & 15)) * SPF + 4 * (lane >> 4);
+    return Raw8{*reinterpret_cast<const float4*>(q), *reinterpret_cast<const float4*>(q + 16)};
+}
+
+struct Ops16 {
+    S3 A;
+    Raw8 B[4];
+};
+__device__ __forceinline__ void read16(Ops16& o, const __bf16* stG, const float* actF, int lane) {
     o.A = tr_read16(stG, STG_PIECE, S32, 0, lane);
 #pragma unroll
-    for (int u = 0; u < 4; ++u) o.B[u] = tr_read16(stA, STA_PIECE, S64, 16 * u, lane);
+    for (int u = 0; u < 4; ++u) o.B[u] = act_read16(actF, 16 * u, lane);
 }
 __device__ __forceinline__ void mma16(floatx4 (&acc)[4], const Ops16& o) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) acc[u] = mma6_16(o.A, o.B[u], acc[u]);
+    for (int u = 0; u < 4; ++u) acc[u] = mma6_16(o.A, split_raw(o.B[u]), acc[u]);
 }
 
 // A 32-row stage (NU activation tiles of 32 columns), operands for both 16-point chunks.
 template <int NU>
 struct Ops32 {
-    S3 A[2], B[2][NU];
+    S3 A[2];
+    Raw8 B[2][NU];
 };
 template <int NU>
-__device__ __forceinline__ void read32(Ops32<NU>& o, const __bf16* stG, const __bf16* stA, int lane) {
+__device__ __forceinline__ void read32(Ops32<NU>& o, const __bf16* stG, const float* actF, int lane) {
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
         o.A[c] = tr_read(stG, STG_PIECE, 0, S32, 16 * c, 0, lane);
 #pragma unroll
-        for (int u = 0; u < NU; ++u) o.B[c][u] = tr_read(stA, STA_PIECE, 0, S64, 16 * c, 32 * u, lane);
+        for (int u = 0; u < NU; ++u) o.B[c][u] = act_read32(actF, 16 * c, 32 * u, lane);
     }
 }
 template <int NU>
@@ -884,7 +921,7 @@ __device__ __forceinline__ void mma32(floatx16 (&acc)[NU], const Ops32<NU>& o) {
 #pragma unroll
     for (int c = 0; c < 2; ++c)
 #pragma unroll
-        for (int u = 0; u < NU; ++u) acc[u] = mma6(o.A[c], o.B[c][u], acc[u]);
+        for (int u = 0; u < NU; ++u) acc[u] = mma6(o.A[c], split_raw(o.B[c][u]), acc[u]);
 }
 
 // Every stage: wait for it, read all of its operands, release the buffer (ack), then run the MFMAs,
@@ -892,6 +929,7 @@ __device__ __forceinline__ void mma32(floatx16 (&acc)[NU], const Ops32<NU>& o) {
 __device__ __forceinline__ void bwd_wgrad_role(const MlpArgs& a, const __bf16* img, const __bf16* stA,
                                                const __bf16* stG, int* ready, int* ack, int p, int lane, WgradX6& g) {
     const int j = lane & 31, h = lane >> 5;
+    const float* actF = reinterpret_cast<const float*>(stA);
 #pragma unroll
     for (int u = 0; u < 4; ++u) { g.dC2[u] = floatx4{0.f, 0.f, 0.f, 0.f}; g.dW1[u] = floatx4{0.f, 0.f, 0.f, 0.f}; }
 #pragma unroll
@@ -910,24 +948,24 @@ __device__ __forceinline__ void bwd_wgrad_role(const MlpArgs& a, const __bf16* i
     for (int64_t tile = (int64_t)blockIdx.x * 4 + p; tile < n_tiles; tile += (int64_t)gridDim.x * 4) {
         {   // 1: dC2
             Ops16 o;
-            take(); read16(o, stG, stA, lane); release();
+            take(); read16(o, stG, actF, lane); release();
             mma16(g.dC2, o);
         }
 #pragma unroll
         for (int t = 0; t < 2; ++t) {   // 2, 3: dC1
             Ops32<2> o;   // 72 registers of operands: too many to hold beside the sums, no early release
-            take(); read32<2>(o, stG, stA, lane); flag_set(ack, ++seq);
+            take(); read32<2>(o, stG, actF, lane); flag_set(ack, ++seq);
             mma32<2>(g.dC1[t], o);
         }
 #pragma unroll
         for (int t = 0; t < 2; ++t) {   // 4, 5: dC0
             Ops32<1> o;
-            take(); read32<1>(o, stG, stA, lane); release();
+            take(); read32<1>(o, stG, actF, lane); release();
             mma32<1>(g.dC0[t], o);
         }
         {   // 6: dW1
             Ops16 o;
-            take(); read16(o, stG, stA, lane); release();
+            take(); read16(o, stG, actF, lane); release();
             mma16(g.dW1, o);
         }
         floatx16 gx = zero16();
@@ -936,7 +974,7 @@ __device__ __forceinline__ void bwd_wgrad_role(const MlpArgs& a, const __bf16* i
             Ops32<1> o;
             S3 gb[2];
             take();
-            read32<1>(o, stG, stA, lane);
+            read32<1>(o, stG, actF, lane);
 #pragma unroll
             for (int c = 0; c < 2; ++c) gb[c] = row_read_st(stG, STG_PIECE, S32, j, 16 * c + 4 * h);
             flag_set(ack, ++seq);
@@ -961,13 +999,13 @@ __device__ __forceinline__ void bwd_wgrad_role(const MlpArgs& a, const __bf16* i
 
 template <bool QUANT>
 __global__ void __launch_bounds__(512, 1) mlp_bwd_x6cg_kernel(MlpArgs a) {
-    __shared__ __attribute__((aligned(16))) __bf16 lds[X6_BWD_LDS / 2];
+    __shared__ __attribute__((aligned(16))) __bf16 lds[X6_CG_LDS / 2];
     __shared__ int flags[8];   // ready[0..3], ack[0..3]
     __bf16* img = lds;
     const int wv = threadIdx.x >> 6, p = wv & 3;
     const bool wgrad_wave = wv >= 4;
-    __bf16* stA = lds + 3 * IM_PIECE + p * ST_WAVE;
-    __bf16* stG = stA + 3 * STA_PIECE;
+    __bf16* stA = lds + 3 * IM_PIECE + p * ST_CG;   // fp32 activation image (actF)
+    __bf16* stG = stA + 2 * ACTF_FLOATS;
     fill_images(img, a.W);
     if (threadIdx.x < 8) flags[threadIdx.x] = 0;
     __syncthreads();
