@@ -430,9 +430,10 @@ __global__ void __launch_bounds__(THREADS) hash_bwd_owner_kernel(HashGradParams 
         auto fetch = [&](const size_t (&addr)[8], uint16_t (&h)[8], float2 (&g)[8]) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                h[j] = __builtin_nontemporal_load(hp.bin_h + addr[j]);
-                // (d feat0, d feat1) as ONE 8-B load
-                const uint64_t gv = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(hp.bin_g + addr[j]));
+// default-policy loads: the coarse pass's bins were written just before this launch and part
+                // of them is still in the Infinity Cache (nontemporal loads: 0.39 vs 0.33 ms per step)
+                h[j] = hp.bin_h[addr[j]];
+                const uint64_t gv = *reinterpret_cast<const uint64_t*>(hp.bin_g + addr[j]);   // (d feat0, d feat1)
                 g[j] = make_float2(__uint_as_float((uint32_t)gv), __uint_as_float((uint32_t)(gv >> 32)));
             }
         };
