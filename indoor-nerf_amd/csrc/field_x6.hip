@@ -644,7 +644,7 @@ __device__ __forceinline__ void flag_wait(int* f, int v, unsigned long long* wai
 #ifdef NERF_X6CG_PROF
     const unsigned long long t0 = CG_T();
 #endif
-    while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != v) __builtin_amdgcn_s_sleep(1);
+    while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < v) __builtin_amdgcn_s_sleep(1);
 #ifdef NERF_X6CG_PROF
     *waited += CG_T() - t0;
 #else
@@ -669,8 +669,9 @@ __device__ __forceinline__ void flag_set_now(int* f, int v) {
 // (measured with NERF_X6CG_PROF before: chain wave busy 75 %, wgrad wave 28 %).
 constexpr int SPF = 36;                                   // row stride: conflict-free b128 reads
 constexpr int ACTF_FLOATS = 64 * SPF;                     // 9,216 B
-constexpr int ST_CG = 2 * ACTF_FLOATS + 3 * STG_PIECE;    // per wave pair, bf16 elements (16,128 B)
-constexpr int X6_CG_LDS = IM_BYTES + 4 * ST_CG * 2;       // 131,328 B
+// per wave pair: the activation image and TWO gradient buffers (stage k uses buffer k & 1)
+constexpr int ST_CG = 2 * ACTF_FLOATS + 6 * STG_PIECE;    // bf16 elements (23,040 B)
+constexpr int X6_CG_LDS = IM_BYTES + 4 * ST_CG * 2;       // 158,976 B
 
 __device__ __forceinline__ void stage_tileF(float* actF, const floatx16& v, int row0, int j, int h) {
 #pragma unroll
@@ -693,7 +694,10 @@ __device__ __forceinline__ void bwd_chain_role(const MlpArgs& a, const __bf16* i
 #ifdef NERF_X6CG_PROF
     const unsigned long long t_start = CG_T();
 #endif
-    auto open = [&]() { flag_wait(ack, seq, &waited); };
+    // stage k writes gradient buffer k & 1 (and, when it stages activations, the one activation
+    // buffer): it may start once the wgrad wave has released stage k - 2 (k - 1 with activations)
+    auto open = [&](bool act) { flag_wait(ack, act ? seq : seq - 1, &waited); };
+    __bf16* const stGb[2] = {stG, stG + 3 * STG_PIECE};
     auto publish = [&]() { flag_set(ready, ++seq); };
     const int64_t n_tiles = (a.P + 31) / 32;
     for (int64_t tile = (int64_t)blockIdx.x * 4 + p; tile < n_tiles; tile += (int64_t)gridDim.x * 4) {
@@ -714,8 +718,8 @@ __device__ __forceinline__ void bwd_chain_role(const MlpArgs& a, const __bf16* i
         {
             const S3 GR = h ? split8(0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f)
                             : split8(g4.x, g4.y, g4.z, 0.f, 0.f, 0.f, 0.f, 0.f);
-            open();
-            stage_grad(stG, GR, 0, j, h);      // columns 16..31 stale: they only reach dC2 rows >= 16
+            open(true);
+            stage_grad(stGb[1], GR, 0, j, h);      // columns 16..31 stale: they only reach dC2 rows >= 16
 #pragma unroll
             for (int t = 0; t < 2; ++t) stage_tileF(actF, f.h3[t], 32 * t, j, h);
             publish();
@@ -732,13 +736,13 @@ __device__ __forceinline__ void bwd_chain_role(const MlpArgs& a, const __bf16* i
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
             const S3 g0 = split_chunk(ga3[t], 0), g1 = split_chunk(ga3[t], 1);
-            open();
+            open(t == 0);
             if (t == 0) {
 #pragma unroll
                 for (int ta = 0; ta < 2; ++ta) stage_tileF(actF, f.h2[ta], 32 * ta, j, h);
             }
-            stage_grad(stG, g0, 0, j, h);
-            stage_grad(stG, g1, 1, j, h);
+            stage_grad(stGb[t], g0, 0, j, h);
+            stage_grad(stGb[t], g1, 1, j, h);
             publish();
 #pragma unroll
             for (int ti = 0; ti < 2; ++ti) {
@@ -764,7 +768,7 @@ __device__ __forceinline__ void bwd_chain_role(const MlpArgs& a, const __bf16* i
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
             const S3 g0 = split_chunk(ga2[t], 0), g1 = split_chunk(ga2[t], 1);
-            open();
+            open(t == 0);
             if (t == 0) {
 #pragma unroll
                 for (int r = 0; r < 8; ++r) actF[row_of(r, h) * SPF + j] = f.o[r];
@@ -772,8 +776,8 @@ __device__ __forceinline__ void bwd_chain_role(const MlpArgs& a, const __bf16* i
                 load_sh6(a, in.pt, in.valid, h, shv, opaque_zero());
                 stage_arrF(actF, shv, 16, j, h);
             }
-            stage_grad(stG, g0, 0, j, h);
-            stage_grad(stG, g1, 1, j, h);
+            stage_grad(stGb[t], g0, 0, j, h);
+            stage_grad(stGb[t], g1, 1, j, h);
             publish();
             go = mma6(tr_read(imt, IM_PIECE, IM_C0, S32, 32 * t, 0, lane), g0, go);
             go = mma6(tr_read(imt, IM_PIECE, IM_C0, S32, 32 * t + 16, 0, lane), g1, go);
@@ -792,10 +796,10 @@ __device__ __forceinline__ void bwd_chain_role(const MlpArgs& a, const __bf16* i
         floatx16 ga1[2];
         {
             const S3 GO = split_chunk(go, 0);
-            open();
+            open(true);
 #pragma unroll
             for (int t = 0; t < 2; ++t) stage_tileF(actF, h1[t], 32 * t, j, h);
-            stage_grad(stG, GO, 0, j, h);      // columns 16..31 stale: they only reach dW1 rows >= 16
+            stage_grad(stGb[0], GO, 0, j, h);      // columns 16..31 stale: they only reach dW1 rows >= 16
             publish();
 #pragma unroll
             for (int t = 0; t < 2; ++t) {
@@ -814,13 +818,13 @@ __device__ __forceinline__ void bwd_chain_role(const MlpArgs& a, const __bf16* i
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
             const S3 g0 = split_chunk(ga1[t], 0), g1 = split_chunk(ga1[t], 1);
-            open();
+            open(t == 0);
             if (t == 0) {
                 stage_arrF(actF, xr, 0, j, h);
                 stage_arrF(actF, xr + 8, 16, j, h);
             }
-            stage_grad(stG, g0, 0, j, h);
-            stage_grad(stG, g1, 1, j, h);
+            stage_grad(stGb[1 - t], g0, 0, j, h);
+            stage_grad(stGb[1 - t], g1, 1, j, h);
             publish();
         }
     }
@@ -948,24 +952,24 @@ __device__ __forceinline__ void bwd_wgrad_role(const MlpArgs& a, const __bf16* i
     for (int64_t tile = (int64_t)blockIdx.x * 4 + p; tile < n_tiles; tile += (int64_t)gridDim.x * 4) {
         {   // 1: dC2
             Ops16 o;
-            take(); read16(o, stG, actF, lane); release();
+            take(); read16(o, stG + 3 * STG_PIECE, actF, lane); release();
             mma16(g.dC2, o);
         }
 #pragma unroll
         for (int t = 0; t < 2; ++t) {   // 2, 3: dC1
             Ops32<2> o;   // 72 registers of operands: too many to hold beside the sums, no early release
-            take(); read32<2>(o, stG, actF, lane); flag_set(ack, ++seq);
+            take(); read32<2>(o, stG + t * 3 * STG_PIECE, actF, lane); flag_set(ack, ++seq);
             mma32<2>(g.dC1[t], o);
         }
 #pragma unroll
         for (int t = 0; t < 2; ++t) {   // 4, 5: dC0
             Ops32<1> o;
-            take(); read32<1>(o, stG, actF, lane); release();
+            take(); read32<1>(o, stG + t * 3 * STG_PIECE, actF, lane); release();
             mma32<1>(g.dC0[t], o);
         }
         {   // 6: dW1
             Ops16 o;
-            take(); read16(o, stG, actF, lane); release();
+            take(); read16(o, stG, actF, lane); release();   // stage 6: gradient buffer 0
             mma16(g.dW1, o);
         }
         floatx16 gx = zero16();
@@ -974,9 +978,10 @@ __device__ __forceinline__ void bwd_wgrad_role(const MlpArgs& a, const __bf16* i
             Ops32<1> o;
             S3 gb[2];
             take();
-            read32<1>(o, stG, actF, lane);
+            const __bf16* sg = stG + (1 - t) * 3 * STG_PIECE;   // stages 7, 8: buffers 1, 0
+            read32<1>(o, sg, actF, lane);
 #pragma unroll
-            for (int c = 0; c < 2; ++c) gb[c] = row_read_st(stG, STG_PIECE, S32, j, 16 * c + 4 * h);
+            for (int c = 0; c < 2; ++c) gb[c] = row_read_st(sg, STG_PIECE, S32, j, 16 * c + 4 * h);
             flag_set(ack, ++seq);
             mma32<1>(g.dW0[t], o);
 #pragma unroll
