@@ -384,7 +384,9 @@ __device__ __forceinline__ void fwd_chain(const __bf16* img, const InX6& in, Act
 
 // ================================================================ forward kernel
 template <bool QUANT>
-__global__ void __launch_bounds__(256, 2) mlp_fwd_x6_kernel(MlpArgs a) {
+// 512-thread blocks: the 66.8 KB weight image is shared by 8 waves, so two blocks per CU give 4
+// waves per SIMD (105 VGPRs) instead of 2 with 256-thread blocks
+__global__ void __launch_bounds__(512, 2) mlp_fwd_x6_kernel(MlpArgs a) {
     __shared__ __attribute__((aligned(16))) __bf16 img[3 * IM_PIECE];
     fill_images(img, a.W);
     __syncthreads();
@@ -392,7 +394,8 @@ __global__ void __launch_bounds__(256, 2) mlp_fwd_x6_kernel(MlpArgs a) {
     QuantRec aq{};
     if constexpr (QUANT) aq = *a.aq;
     const int64_t n_tiles = (a.P + 31) / 32;
-    for (int64_t tile = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); tile < n_tiles; tile += (int64_t)gridDim.x * 4) {
+    const int wpb = blockDim.x >> 6;
+    for (int64_t tile = (int64_t)blockIdx.x * wpb + (threadIdx.x >> 6); tile < n_tiles; tile += (int64_t)gridDim.x * wpb) {
         InX6 in;
         load_in_x6(a, tile, j, h, in);
         ActX6 f;
@@ -1076,11 +1079,11 @@ static bool fits_u32(const MlpArgs& a) {
 int launch_mlp_fwd_x6(const MlpArgs& a, hipStream_t stream) {
     NERF_REQUIRE(fits_u32(a), "mlp_fwd(x6): %lld points exceed 32-bit indexing", (long long)a.P);
     const int64_t tiles = (a.P + 31) / 32;
-    const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((tiles + 3) / 4, 256 * 4));
+    const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((tiles + 7) / 8, 256 * 2));
     if (a.aq)
-        hipLaunchKernelGGL(mlp_fwd_x6_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, stream, a);
+        hipLaunchKernelGGL(mlp_fwd_x6_kernel<true>, dim3((unsigned)blocks), dim3(512), 0, stream, a);
     else
-        hipLaunchKernelGGL(mlp_fwd_x6_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, stream, a);
+        hipLaunchKernelGGL(mlp_fwd_x6_kernel<false>, dim3((unsigned)blocks), dim3(512), 0, stream, a);
     NERF_CHECK_LAUNCH("mlp_fwd(x6)");
     return NERF_OK;
 }
