@@ -54,6 +54,7 @@ struct MlpArgs {
     const QuantRec* aq;   // optional A-CAQ record of the layer-0 activation quantizer
     uint32_t* act_minmax; // calibration-only launch: min/max of relu(x W0^T) (order-preserving u32)
     int64_t calib_points;
+    int flush_skip;       // A/B timing only (NERF_X6CG_FLUSH): 1 = no global flush, 2 = no block reduction either
 };
 
 // A-CAQ activation quantizer on a layer-0 accumulator tile (sigma_act_quantizers[0],

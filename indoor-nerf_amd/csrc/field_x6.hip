@@ -1,3 +1,4 @@
+#include <stdlib.h>
 // Field MLP on the bf16 matrix cores with fp32 accuracy ("x6", the default MLP path).
 //
 // gfx950 has no tf32/xf32 MFMA and its f32-input MFMA (v_mfma_f32_32x32x2_f32) runs at 1/16 of
@@ -1028,12 +1029,16 @@ __global__ void __launch_bounds__(512, 1) mlp_bwd_x6cg_kernel(MlpArgs a) {
         bwd_chain_role<QUANT>(a, img, stA, stG, flags + p, flags + 4 + p, p, lane, aq);
     }
 
-    // ---- block reduction of the wgrad waves' tiles (LDS fp32 atomics), one global flush per block
+    // ---- block reduction of the wgrad waves' tiles, one global flush per block. Each wgrad wave
+    // writes its full weight-gradient image (every index exactly once: the tile maps are fixed) into
+    // its own LDS copy with plain stores; then all 512 threads sum the four copies. LDS fp32 atomics
+    // here (one ds_add_f32 per value and wave into a shared image) cost 49 us per launch.
+    static_assert(4 * GW_TOTAL * (int)sizeof(float) <= X6_CG_LDS, "four weight-gradient images must fit the LDS");
     __syncthreads();
+    if (a.flush_skip == 2) return;
     float* gw = reinterpret_cast<float*>(lds);
-    for (int i = threadIdx.x; i < GW_TOTAL; i += blockDim.x) gw[i] = 0.f;
-    __syncthreads();
     if (wgrad_wave) {
+        float* mine = gw + p * GW_TOTAL;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int rr = row_of(r, h);
@@ -1041,9 +1046,9 @@ __global__ void __launch_bounds__(512, 1) mlp_bwd_x6cg_kernel(MlpArgs a) {
             for (int t = 0; t < 2; ++t) {
                 const int row = 32 * t + rr;
 #pragma unroll
-                for (int u = 0; u < 2; ++u) atomicAdd(gw + GW_C1 + row * 64 + 32 * u + j, g.dC1[t][u][r]);
-                if (j != 0) atomicAdd(gw + GW_C0 + row * 31 + (j < 16 ? 15 + j : j - 16), g.dC0[t][0][r]);
-                atomicAdd(gw + GW_W0 + row * 32 + j, g.dW0[t][0][r]);
+                for (int u = 0; u < 2; ++u) mine[GW_C1 + row * 64 + 32 * u + j] = g.dC1[t][u][r];
+                if (j != 0) mine[GW_C0 + row * 31 + (j < 16 ? 15 + j : j - 16)] = g.dC0[t][0][r];
+                mine[GW_W0 + row * 32 + j] = g.dW0[t][0][r];
             }
         }
         // 16x16 tiles: lane l holds rows 4(l >> 4) + i, column 16u + (l & 15)
@@ -1052,8 +1057,8 @@ __global__ void __launch_bounds__(512, 1) mlp_bwd_x6cg_kernel(MlpArgs a) {
         for (int u = 0; u < 4; ++u)
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                if (r0 + i < 3) atomicAdd(gw + GW_C2 + (r0 + i) * 64 + 16 * u + n, g.dC2[u][i]);
-                atomicAdd(gw + GW_W1 + (r0 + i) * 64 + 16 * u + n, g.dW1[u][i]);
+                if (r0 + i < 3) mine[GW_C2 + (r0 + i) * 64 + 16 * u + n] = g.dC2[u][i];
+                mine[GW_W1 + (r0 + i) * 64 + 16 * u + n] = g.dW1[u][i];
             }
     }
     __syncthreads();
@@ -1065,8 +1070,8 @@ __global__ void __launch_bounds__(512, 1) mlp_bwd_x6cg_kernel(MlpArgs a) {
         else if (i < GW_C1) { dst = a.G.c0; k = i - GW_C0; }
         else if (i < GW_C2) { dst = a.G.c1; k = i - GW_C1; }
         else { dst = a.G.c2; k = i - GW_C2; }
-        const float v = gw[i];
-        if (v != 0.f) __hip_atomic_fetch_add(dst + k, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const float v = (gw[i] + gw[GW_TOTAL + i]) + (gw[2 * GW_TOTAL + i] + gw[3 * GW_TOTAL + i]);
+        if (v != 0.f && a.flush_skip == 0) __hip_atomic_fetch_add(dst + k, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -1088,7 +1093,10 @@ int launch_mlp_fwd_x6(const MlpArgs& a, hipStream_t stream) {
     return NERF_OK;
 }
 
-int launch_mlp_bwd_x6(const MlpArgs& a, hipStream_t stream, bool split_roles) {
+int launch_mlp_bwd_x6(const MlpArgs& a_in, hipStream_t stream, bool split_roles) {
+    MlpArgs a = a_in;
+    const char* fs = getenv("NERF_X6CG_FLUSH");   // A/B timing of the weight-gradient reduction only
+    a.flush_skip = (fs && fs[0] == '1') ? 1 : (fs && fs[0] == '2') ? 2 : 0;
     NERF_REQUIRE(fits_u32(a), "mlp_bwd(x6): %lld points exceed 32-bit indexing", (long long)a.P);
     const int64_t tiles = (a.P + 31) / 32;
     const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((tiles + 3) / 4, 256));
