@@ -58,7 +58,7 @@ KERNEL_SYMBOLS = {
     "nerf_mlp_fwd": ["nerf::mlp_fwd_x6_kernel<false>"],
     "nerf_mlp_bwd": ["nerf::mlp_bwd_x6cg_kernel<false>"],
 }
-TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r01h_traffic.json")
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r01j_traffic.json")
 
 
 def base_name(abi_name):
@@ -311,7 +311,7 @@ def main():
                             "peak_note": ("bf16 dense MFMA peak / 6: each fp32-accurate product is six bf16 products "
                                           "(csrc/field_x6.hip)") if x6 else "f32 MFMA dense peak"}
             if traffic is not None:
-                roofline["traffic_source"] = ("profiles/r01h_traffic.json: rocprofv3 FETCH_SIZE (x2, gfx950 wide-read "
+                roofline["traffic_source"] = ("profiles/r01j_traffic.json: rocprofv3 FETCH_SIZE (x2, gfx950 wide-read "
                                               "correction) + WRITE_SIZE per call, separate PMC passes of this bench")
         else:
             roofline = {"kernel": dom, "bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
