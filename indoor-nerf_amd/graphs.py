@@ -42,10 +42,14 @@ class StepScalars:
     """Device-resident per-step scalars of a captured step (int64 and float32 slots)."""
 
     def __init__(self, device, n_i64=1024, n_f32=1024, ring=4):
-        self.dev_i = torch.zeros(n_i64, dtype=torch.int64, device=device)
-        self.dev_f = torch.zeros(n_f32, dtype=torch.float32, device=device)
-        self.pinned = [(torch.zeros(n_i64, dtype=torch.int64).pin_memory(),
-                        torch.zeros(n_f32, dtype=torch.float32).pin_memory()) for _ in range(ring)]
+        # one byte buffer per side ([int64 slots | float32 slots]), so an upload is ONE copy
+        nb = 8 * n_i64 + 4 * n_f32
+        self.dev = torch.zeros(nb, dtype=torch.uint8, device=device)
+        self.dev_i = self.dev[:8 * n_i64].view(torch.int64)
+        self.dev_f = self.dev[8 * n_i64:].view(torch.float32)
+        self.pinned_bytes = [torch.zeros(nb, dtype=torch.uint8).pin_memory() for _ in range(ring)]
+        self.pinned = [(b[:8 * n_i64].view(torch.int64), b[8 * n_i64:].view(torch.float32))
+                       for b in self.pinned_bytes]
         self.events = [None] * ring
         self.k = 0
         self.ni = self.nf = 0
@@ -78,8 +82,7 @@ class StepScalars:
         ni, nf = hi.numpy(), hf.numpy()
         for fn in self.fillers:
             fn(ni, nf)
-        self.dev_i.copy_(hi, non_blocking=True)
-        self.dev_f.copy_(hf, non_blocking=True)
+        self.dev.copy_(self.pinned_bytes[k], non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
         self.events[k] = ev

@@ -175,8 +175,21 @@ def forward_backward(batch_rays, target_s, render_kwargs_train, optimizer, args,
         args.tv_loss_weight = 0.0
     if get("use_structural_priors") and global_step >= get("structural_loss_start_iter"):
         loss = loss + structural_loss(depth, extras, args, global_step, spatial_coords)
-    loss.backward()
+    loss.backward(_unit_seed(loss))
     return loss, img_loss, psnr
+
+
+_SEEDS = {}
+
+
+def _unit_seed(loss):
+    """d loss / d loss = 1 from a persistent device tensor: loss.backward() would launch a fill
+    kernel for it every iteration (and capture one into the step graph)."""
+    key = (loss.device, loss.dtype, tuple(loss.shape))
+    seed = _SEEDS.get(key)
+    if seed is None:
+        seed = _SEEDS[key] = torch.ones_like(loss, memory_format=torch.contiguous_format)
+    return seed
 
 
 def structural_loss(depth, extras, args, global_step, spatial_coords=None):
