@@ -33,23 +33,13 @@ struct LossArgs {
     float* psnr;
 };
 
-__device__ __forceinline__ double block_sum_d(double v, double* s_red) {
-    v = wave_sum_d(v);
-    const int w = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) s_red[w] = v;
-    __syncthreads();
-    double t = 0.0;
-    if (threadIdx.x == 0)
-        for (int i = 0; i < kLossThreads / 64; ++i) t += s_red[i];
-    __syncthreads();
-    return t;   // valid on thread 0
-}
-
 // Sums in fp64 (one workgroup; the inputs are a few thousand values), rounded once to fp32: closer
 // to the exact mean than torch's fp32 tree, which is what the parity tolerance is written against.
 __global__ void __launch_bounds__(kLossThreads) train_loss_fwd_kernel(LossArgs a) {
-    __shared__ double s_red[kLossThreads / 64];
+    __shared__ double s_red4[4][kLossThreads / 64];
     double se = 0.0, se0 = 0.0, ssp = 0.0, ssp0 = 0.0;
+    // unrolled for load ILP; each thread still adds its elements in index order
+#pragma unroll 4
     for (int64_t i = threadIdx.x; i < a.n_rgb; i += kLossThreads) {
         const float t = a.target[i];
         const float d = a.rgb[i] - t;
@@ -63,10 +53,22 @@ __global__ void __launch_bounds__(kLossThreads) train_loss_fwd_kernel(LossArgs a
         if (a.sp) ssp += (double)a.sp[i];
         if (a.sp0) ssp0 += (double)a.sp0[i];
     }
-    se = block_sum_d(se, s_red);
-    se0 = block_sum_d(se0, s_red);
-    ssp = block_sum_d(ssp, s_red);
-    ssp0 = block_sum_d(ssp0, s_red);
+    // the four block sums share one barrier: wave sums, then thread 0 adds the waves' partials in
+    // wave order (one barrier instead of two per sum)
+    {
+        const double w0 = wave_sum_d(se), w1 = wave_sum_d(se0), w2 = wave_sum_d(ssp), w3 = wave_sum_d(ssp0);
+        const int w = threadIdx.x >> 6;
+        if ((threadIdx.x & 63) == 0) { s_red4[0][w] = w0; s_red4[1][w] = w1; s_red4[2][w] = w2; s_red4[3][w] = w3; }
+        __syncthreads();
+        se = se0 = ssp = ssp0 = 0.0;
+        if (threadIdx.x == 0)
+            for (int i = 0; i < kLossThreads / 64; ++i) {
+                se += s_red4[0][i];
+                se0 += s_red4[1][i];
+                ssp += s_red4[2][i];
+                ssp0 += s_red4[3][i];
+            }
+    }
     if (threadIdx.x == 0) {
         const float n = (float)a.n_rgb;
         const float img = (float)se / n;
