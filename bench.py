@@ -32,33 +32,43 @@ FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: f32 matrix (v_mfma_f32_32x
 # products, so their arithmetic peak is the dense bf16 rate (~2.5 PFLOP/s) / 6.
 X6_PEAK_TFLOPS = 2500.0 / 6
 
-# Algorithmic cost per unit of each kernel: bytes (HBM-bound) or FLOPs (MFMA).
+# Algorithmic cost per unit of each OP: bytes (HBM-bound) or FLOPs (MFMA). An op is
+# one or more ABI calls priced together: the hash backward is the bin pass (once per render pass)
+# plus the owner pass (once per iteration), and only their sum is a complete scatter-add.
 #   hash fwd : per point  16 levels x 8 corners x 8 B gathered + 12 B xyz + 128 B features + 1 B keep
-#   hash bwd : per point  16 x 8 x 8 B read+write of the atomically added rows (2 x 1024) + 12 + 128
+#   hash bwd : per point  16 x 8 x 8 B read+write of the added rows (2 x 1024) + 12 B xyz + 128 B d feat
 #   mlp fwd  : per point  9,344 MACs = 18,688 FLOP
 #   mlp bwd  : per point  2 x 18,688 FLOP (input + weight grads; the recomputed forward is not counted)
 #   composite: per sample 16 B raw + 4 B z + 4 B weights (fwd) / + 16 B grad (bwd)
-UNIT_COST = {
-    "nerf_hash_encode_fwd": ("hbm", 16 * 8 * 8 + 12 + 128 + 1, "point"),
-    "nerf_hash_encode_bwd": ("hbm", 2 * 16 * 8 * 8 + 12 + 128, "point"),
-    "nerf_hash_encode_bwd_ws": ("hbm", 2 * 16 * 8 * 8 + 12 + 128, "point"),
-    "nerf_mlp_fwd": ("mfma", 18688, "point"),
-    "nerf_mlp_bwd": ("mfma", 2 * 18688, "point"),
-    "nerf_composite_fwd": ("hbm", 24, "sample"),
-    "nerf_composite_bwd": ("hbm", 40, "sample"),
+#   radam    : per table/MLP element 28 B (read p, g, m, v; write p, m, v)
+OPS = {
+    "hash_bwd": dict(calls=("nerf_hash_encode_bwd_bin", "nerf_hash_encode_bwd_owner", "nerf_hash_encode_bwd_ws",
+                            "nerf_hash_encode_bwd"), bound="hbm", per_unit=2 * 16 * 8 * 8 + 12 + 128, unit="point"),
+    "hash_fwd": dict(calls=("nerf_hash_encode_fwd",), bound="hbm", per_unit=16 * 8 * 8 + 12 + 128 + 1, unit="point"),
+    "mlp_bwd": dict(calls=("nerf_mlp_bwd",), bound="mfma", per_unit=2 * 18688, unit="point"),
+    "mlp_fwd": dict(calls=("nerf_mlp_fwd",), bound="mfma", per_unit=18688, unit="point"),
+    "composite_fwd": dict(calls=("nerf_composite_fwd",), bound="hbm", per_unit=24, unit="sample"),
+    "composite_bwd": dict(calls=("nerf_composite_bwd",), bound="hbm", per_unit=40, unit="sample"),
+    "radam": dict(calls=("nerf_radam_step",), bound="hbm", per_unit=28, unit="element"),
 }
+# algorithmic HBM bytes of one whole iteration per ray at 64 + 128 samples
+# (256 points x 3,072 B + 8 x 64 MiB dense table traffic / 4096 + 64 B ray I/O): 3,758,358,528 B
+# per 4096-ray step
+STEP_BYTES_PER_POINT = 3 * 1024
+STEP_DENSE_BYTES = 8 * 16 * (1 << 19) * 2 * 4
+STEP_RAY_BYTES = 64
 
 
 # ABI call -> the kernel symbols it launches (rocprofv3 names), to attach PMC traffic per call
 KERNEL_SYMBOLS = {
     "nerf_hash_encode_fwd": ["nerf::hash_encode_fwd_pair_kernel<false>"],
-    "nerf_hash_encode_bwd_ws": ["nerf::hash_encode_bwd_kernel<3>", "nerf::hash_bwd_owner_kernel<13, 1024>"],
     "nerf_hash_encode_bwd_bin": ["nerf::hash_encode_bwd_kernel<3>"],
     "nerf_hash_encode_bwd_owner": ["nerf::hash_bwd_owner_kernel<13, 1024>"],
     "nerf_mlp_fwd": ["nerf::mlp_fwd_x6_kernel<false>"],
     "nerf_mlp_bwd": ["nerf::mlp_bwd_x6cg_kernel<false>"],
+    "nerf_radam_step": ["nerf::radam_kernel"],
 }
-TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r01j_traffic.json")
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r02_traffic.json")
 
 
 def base_name(abi_name):
@@ -67,15 +77,80 @@ def base_name(abi_name):
     return abi_name[:-2] if abi_name.endswith("_q") else abi_name
 
 
+def traffic_file():
+    """The newest committed PMC traffic summary (tools/profile_bench.sh), or None."""
+    for name in ("r02_traffic.json", "r01j_traffic.json"):
+        path = os.path.join(ROOT, "profiles", name)
+        if os.path.exists(path):
+            return path
+    return None
+
+
 def pmc_traffic(abi_name):
     """HBM-side bytes per call of `abi_name` from the committed PMC passes (tools/profile_bench.sh:
     FETCH_SIZE and WRITE_SIZE in separate rocprofv3 passes of this bench), or None."""
     abi_name = base_name(abi_name)
-    if not os.path.exists(TRAFFIC_JSON) or abi_name not in KERNEL_SYMBOLS:
+    path = traffic_file()
+    if path is None or abi_name not in KERNEL_SYMBOLS:
         return None
-    t = json.load(open(TRAFFIC_JSON))
+    t = json.load(open(path))
     parts = [t.get(k, {}).get("traffic_bytes") for k in KERNEL_SYMBOLS[abi_name]]
     return None if any(p is None for p in parts) else float(sum(parts))
+
+
+def gpu_clocks():
+    """Current shader / memory clocks of the visible GPUs (rocm-smi, a child process), so that a
+    box-to-box spread in the bench line can be told apart from a code regression."""
+    import subprocess
+    try:
+        r = subprocess.run(["rocm-smi", "--showclocks", "--json"], capture_output=True, text=True, timeout=20)
+        d = json.loads(r.stdout)
+    except Exception:
+        return None
+    out = {}
+    for card, v in d.items():
+        if isinstance(v, dict):
+            out[card] = {k.split("(")[1].rstrip(")") if "(" in k else k: val for k, val in v.items()
+                         if "sclk" in k or "mclk" in k or "fclk" in k}
+    return out or None
+
+
+def op_rooflines(kernels, steps, units, dense_elems):
+    """Per OP (OPS) per iteration: achieved = algorithmic bytes (FLOPs) of the op's units in one
+    iteration / the op's summed kernel time in one iteration (HIP events), against the MI355X peak;
+    traffic = the committed PMC bytes of the op's kernels per iteration."""
+    out = []
+    for op, d in OPS.items():
+        calls = [c for c in kernels if base_name(c) in d["calls"]]
+        if not calls:
+            continue
+        t_step = sum(kernels[c]["total_ms"] for c in calls) * 1e-3 / steps
+        n = dense_elems if d["unit"] == "element" else units
+        work = d["per_unit"] * n
+        traffic = 0.0
+        for c in calls:
+            tc = pmc_traffic(c)
+            if tc is None:
+                traffic = None
+                break
+            traffic += tc * kernels[c]["launches"] / steps
+        if d["bound"] == "hbm":
+            ach = work / t_step / 1e9
+            r = {"op": op, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None if traffic is None else round(traffic),
+                 "algorithmic_bytes": work}
+        else:
+            ach = work / t_step / 1e12
+            r = {"op": op, "bound": "mfma", "achieved": round(ach, 2), "peak": round(X6_PEAK_TFLOPS, 1),
+                 "unit": "TFLOP/s", "frac": round(ach / X6_PEAK_TFLOPS, 4),
+                 "traffic": None if traffic is None else round(traffic), "algorithmic_flops": work,
+                 "peak_note": "bf16 dense MFMA peak / 6: each fp32-accurate product is six bf16 products "
+                              "(csrc/field_x6.hip)"}
+        r.update(ms_per_step=round(1e3 * t_step, 4), calls={c: kernels[c]["launches"] // max(1, steps) for c in calls},
+                 units_per_step=n, per_unit=d["per_unit"], unit_name=d["unit"])
+        out.append(r)
+    out.sort(key=lambda r: -r["ms_per_step"])
+    return out
 
 
 def parse():
@@ -85,8 +160,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--rays", type=int, default=4096)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-rays", type=int, default=1024)
-    ap.add_argument("--cpu-steps", type=int, default=3)
+    ap.add_argument("--cpu-rays", type=int, default=4096)
+    ap.add_argument("--cpu-steps", type=int, default=2)
     ap.add_argument("--profile-kernels", type=int, default=1, help="record HIP events per kernel in the timed region")
     ap.add_argument("--workload", default="lego", choices=sorted(WORKLOADS),
                     help="BASELINE config: lego (configs[1], the headline), fern (configs[2], LLFF NDC), "
@@ -127,12 +202,15 @@ WORKLOADS = {
 
 
 def cpu_baseline(n_rays, steps):
-    """The oracle (CPU PyTorch restatement of the reference) timed on this host: one training
-    iteration = coarse+fine render, losses incl. TV, backward, RAdam; 1 warm-up + `steps` timed."""
+    """The oracle (CPU PyTorch restatement of the reference) timed on this host on the bench's own
+    batch size: one training iteration = coarse+fine render, losses incl. TV, backward, RAdam;
+    1 warm-up + `steps` timed (median), then one render-only pass (no grad) of the same rays.
+    Threads: the host's CPU share (OMP_NUM_THREADS, 16 on the GPU box) capped by the affinity mask."""
     from oracle import nerf_oracle as orc
     from indoor_nerf_amd.synthetic import blender_bbox, blender_rays
     cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
-    threads = max(1, min(cores, 16))
+    share = int(os.environ.get("OMP_NUM_THREADS", "16") or 16)
+    threads = max(1, min(cores, share))
     torch.set_num_threads(threads)
     lo, hi = (torch.from_numpy(v) for v in blender_bbox())
     res = orc.level_resolutions(16, 1024)
@@ -169,9 +247,15 @@ def cpu_baseline(n_rays, steps):
         step(i + 1)
         times.append(time.perf_counter() - t0)
     t = float(np.median(times))
+    with torch.no_grad():
+        t0 = time.perf_counter()
+        orc.render_rays(ro, rd, vd, 2.0, 6.0, cw, fw, tabs, lo, hi, res)
+        t_render = time.perf_counter() - t0
     return {"value": round(n_rays / t, 2), "unit": "rays/s", "cores": threads, "kind": "port",
-            "sample": f"{n_rays} rays x (64+128) samples, finest 1024, full train iteration incl. TV + RAdam; "
-                      f"median of {steps} steps after 1 warm-up ({platform.processor() or platform.machine()})"}
+            "render_only": {"value": round(n_rays / t_render, 2), "unit": "rays/s"},
+            "sample": f"the bench's batch: {n_rays} rays x (64+128) samples, finest 1024, full train iteration incl. "
+                      f"TV + RAdam; median of {steps} steps after 1 warm-up; render-only = one no-grad pass of the "
+                      f"same rays ({platform.processor() or platform.machine()}, {threads} threads)"}
 
 
 def main():
@@ -261,6 +345,7 @@ def main():
     if world > 1:
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
+    clocks = gpu_clocks() if rank == 0 else None
     recs = _lib.timing_records()
     _lib.set_timing(False)
     if world > 1:
@@ -285,37 +370,32 @@ def main():
     kernels = {}
     for name, ts in per.items():
         kernels[name] = {"launches": len(ts), "avg_ms": 1e3 * float(np.mean(ts)), "total_ms": 1e3 * float(np.sum(ts))}
-    roofline = None
+    roofline, ops = None, []
+    ns, ni = wl["args"]["N_samples"], wl["args"]["N_importance"]
+    points_per_step = a.rays * (ns + (ns + ni if ni else 0))
     if kernels:
-        dom = max(kernels, key=lambda n: kernels[n]["total_ms"])
-        ns, ni = wl["args"]["N_samples"], wl["args"]["N_importance"]
-        P_coarse, P_fine = a.rays * ns, a.rays * (ns + ni)
-        units_per_launch = {"point": (P_coarse + P_fine) / 2, "sample": (P_coarse + P_fine) / 2}
-        if base_name(dom) in UNIT_COST:
-            bound, per_unit, unit = UNIT_COST[base_name(dom)]
-            units = units_per_launch[unit]
-            avg_s = kernels[dom]["avg_ms"] * 1e-3
-            traffic = pmc_traffic(dom)
-            if bound == "hbm":
-                ach = per_unit * units / avg_s / 1e9
-                roofline = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-                            "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
-                            "per_launch_units": units, "algorithmic_bytes_per_unit": per_unit}
-            else:
-                ach = per_unit * units / avg_s / 1e12
-                x6 = os.environ.get("NERF_MLP", "3")[:1] not in ("1", "2")
-                peak = X6_PEAK_TFLOPS if x6 else FP32_MFMA_PEAK_TFLOPS
-                roofline = {"kernel": dom, "bound": "mfma", "achieved": round(ach, 2), "peak": round(peak, 1),
-                            "unit": "TFLOP/s", "frac": round(ach / peak, 4), "traffic": traffic,
-                            "per_launch_units": units, "algorithmic_flops_per_unit": per_unit,
-                            "peak_note": ("bf16 dense MFMA peak / 6: each fp32-accurate product is six bf16 products "
-                                          "(csrc/field_x6.hip)") if x6 else "f32 MFMA dense peak"}
-            if traffic is not None:
-                roofline["traffic_source"] = ("profiles/r01j_traffic.json: rocprofv3 FETCH_SIZE (x2, gfx950 wide-read "
-                                              "correction) + WRITE_SIZE per call, separate PMC passes of this bench")
-        else:
-            roofline = {"kernel": dom, "bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": None, "traffic": None}
+        ops = op_rooflines(kernels, a.steps, points_per_step, sum(p.numel() for p in params))
+        if ops:
+            # the dominant op: largest kernel time per iteration after grouping (hash bwd = bin + owner)
+            d = ops[0]
+            roofline = {k: d[k] for k in ("bound", "achieved", "peak", "unit", "frac", "traffic")}
+            roofline.update(op=d["op"], ms_per_step=d["ms_per_step"], calls_per_step=d["calls"],
+                            units_per_step=d["units_per_step"], per_unit=d["per_unit"], unit_name=d["unit_name"],
+                            top3=[{k: o[k] for k in ("op", "bound", "ms_per_step", "achieved", "unit", "frac")}
+                                  for o in ops[:3]])
+            if d["traffic"] is not None:
+                roofline["traffic_source"] = (os.path.relpath(traffic_file(), ROOT) + ": rocprofv3 FETCH_SIZE (x2, "
+                                              "gfx950 wide-read correction) + WRITE_SIZE per call, separate PMC passes "
+                                              "of this bench, x calls per iteration")
+    step_s = elapsed / a.steps
+    step_bytes = points_per_step * STEP_BYTES_PER_POINT + STEP_DENSE_BYTES + a.rays * STEP_RAY_BYTES
+    step_roofline = None
+    if a.mode == "train":
+        # the whole iteration's algorithmic HBM bytes over its wall time
+        step_roofline = {"bytes_per_step": step_bytes, "achieved": round(step_bytes / step_s / 1e9, 1),
+                         "unit": "GB/s", "peak": HBM_PEAK_GBS,
+                         "frac": round(step_bytes / step_s / 1e9 / HBM_PEAK_GBS, 4),
+                         "bound_ms": round(1e3 * step_bytes / (HBM_PEAK_GBS * 1e9), 4)}
 
     value = world * a.rays * a.steps / elapsed
     out = {
@@ -338,6 +418,9 @@ def main():
         "hip_graph": bool(gstep is not None and gstep.captures > 0),
         "loss": round(float(loss), 6),
         "roofline": roofline,
+        "step_roofline": step_roofline,
+        "ops": ops,
+        "gpu_clocks": clocks,
         "kernels": {k: {kk: round(vv, 4) if isinstance(vv, float) else vv for kk, vv in v.items()}
                     for k, v in sorted(kernels.items(), key=lambda kv: -kv[1]["total_ms"])},
     }
