@@ -169,6 +169,12 @@ def parse():
                          "acaq (configs[4], A-CAQ quantized tables)")
     ap.add_argument("--graph", type=int, default=1,
                     help="train mode: replay the iteration from HIP graphs (graphs.GraphedTrainStep); 0 = eager")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="weak: every rank trains --rays rays (the driver's default); strong: one global batch of "
+                         "--rays rays split evenly over the ranks (dist.shard)")
+    ap.add_argument("--zero", type=int, default=1,
+                    help="N>1: shard the optimizer (reduce-scatter -> RAdam on 1/N -> all-gather, dist.ShardedOptimizer); "
+                         "0 = all-reduce + replicated RAdam")
     ap.add_argument("--mode", default="train", choices=["train", "render"],
                     help="train: full training iteration (the metric); render: render-only (eval modules, no grad)")
     return ap.parse_args()
@@ -268,19 +274,28 @@ def main():
     rank, world, local = nerf.init_process_group()
     dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))   # ranks > GPUs only in rehearsals
     torch.cuda.set_device(dev)
+    strong = a.scaling == "strong"
+    if strong and a.rays % world:
+        raise SystemExit(f"--scaling strong: --rays {a.rays} is not divisible by {world} ranks")
+    # weak: each rank its own batch; strong: the same global batch on every rank, then its shard
+    seed = 100 if strong else 100 + rank
     if wl["rays"] == "blender":
         lo, hi = blender_bbox()
-        ro, rd = blender_rays(a.rays, seed=100 + rank)
+        ro, rd = blender_rays(a.rays, seed=seed)
         H = W = 800
         K = None
     elif wl["rays"] == "scannet":
         from indoor_nerf_amd.synthetic import scannet_bbox, scannet_rays
         lo, hi = scannet_bbox()
-        ro, rd, _coords = scannet_rays(a.rays, seed=100 + rank)
+        ro, rd, _coords = scannet_rays(a.rays, seed=seed)
         H, W, K = 480, 640, None
     else:
         lo, hi = llff_bbox()
-        ro, rd, (H, W, K) = llff_rays(a.rays, seed=100 + rank)
+        ro, rd, (H, W, K) = llff_rays(a.rays, seed=seed)
+    if strong:
+        ro = nerf.shard(torch.from_numpy(ro), rank, world).numpy()
+        rd = nerf.shard(torch.from_numpy(rd), rank, world).numpy()
+    R = ro.shape[0]              # this rank's rays per step
     args = nerf.make_args(bounding_box=(torch.from_numpy(lo), torch.from_numpy(hi)), **wl["args"])
     torch.manual_seed(0)
     nerf.manual_seed(1234 + rank)
@@ -294,22 +309,34 @@ def main():
         kw["embed_fn"].current_step = kw["embed_fn"].warmup_steps   # past the 500-call warm-up (hash_encoding.py:97)
     params = grad_vars + list(kw["embed_fn"].parameters())
     nerf.broadcast_params(params)
-    arena = nerf.GradArena(params)
+    zero = world > 1 and a.zero and a.mode == "train"
+    arena = nerf.GradArena(params, pad_to=world * 64 if zero else 1)
     rays = (torch.from_numpy(ro).to(dev), torch.from_numpy(rd).to(dev))
-    target = torch.rand(a.rays, 3, device=dev, generator=torch.Generator(device=dev).manual_seed(rank))
+    if strong:
+        target = nerf.shard(torch.rand(a.rays, 3, device=dev, generator=torch.Generator(device=dev).manual_seed(0)),
+                            rank, world).contiguous()
+    else:
+        target = torch.rand(R, 3, device=dev, generator=torch.Generator(device=dev).manual_seed(rank))
     tv_gen = torch.Generator().manual_seed(7)       # same TV cuboids on every rank
-    hook = (lambda: arena.allreduce_mean()) if world > 1 else None
+    post = None
+    if zero:
+        sharded = nerf.ShardedOptimizer(opt, arena)
+        hook, post = sharded.reduce_grads, sharded.gather_params
+    else:
+        hook = (lambda: arena.allreduce_mean()) if world > 1 else None
 
     gstep = None
     if a.mode == "train" and a.graph:
         from indoor_nerf_amd.graphs import GraphedTrainStep
         gstep = GraphedTrainStep(rays, target, kw, opt, args, H=H, W=W, K=K, grad_hook=hook,
-                                 loss_scale_sparsity=float(world), tv_generator=tv_gen, zero_grad=arena.zero_)
+                                 loss_scale_sparsity=float(world), tv_generator=tv_gen, zero_grad=arena.zero_,
+                                 post_hook=post)
         step = gstep
     elif a.mode == "train":
         def step(i):
             return nerf.train_step(rays, target, kw, opt, args, i, H=H, W=W, K=K, grad_hook=hook,
-                                   loss_scale_sparsity=float(world), tv_generator=tv_gen, zero_grad=arena.zero_)
+                                   loss_scale_sparsity=float(world), tv_generator=tv_gen, zero_grad=arena.zero_,
+                                   post_hook=post)
     else:
         for m in (kw["network_fn"], kw["network_fine"], kw["embed_fn"]):
             m.eval()
@@ -372,7 +399,7 @@ def main():
         kernels[name] = {"launches": len(ts), "avg_ms": 1e3 * float(np.mean(ts)), "total_ms": 1e3 * float(np.sum(ts))}
     roofline, ops = None, []
     ns, ni = wl["args"]["N_samples"], wl["args"]["N_importance"]
-    points_per_step = a.rays * (ns + (ns + ni if ni else 0))
+    points_per_step = R * (ns + (ns + ni if ni else 0))
     if kernels:
         ops = op_rooflines(kernels, a.steps, points_per_step, sum(p.numel() for p in params))
         if ops:
@@ -388,7 +415,7 @@ def main():
                                               "gfx950 wide-read correction) + WRITE_SIZE per call, separate PMC passes "
                                               "of this bench, x calls per iteration")
     step_s = elapsed / a.steps
-    step_bytes = points_per_step * STEP_BYTES_PER_POINT + STEP_DENSE_BYTES + a.rays * STEP_RAY_BYTES
+    step_bytes = points_per_step * STEP_BYTES_PER_POINT + STEP_DENSE_BYTES + R * STEP_RAY_BYTES
     step_roofline = None
     if a.mode == "train":
         # the whole iteration's algorithmic HBM bytes over its wall time
@@ -397,7 +424,7 @@ def main():
                          "frac": round(step_bytes / step_s / 1e9 / HBM_PEAK_GBS, 4),
                          "bound_ms": round(1e3 * step_bytes / (HBM_PEAK_GBS * 1e9), 4)}
 
-    value = world * a.rays * a.steps / elapsed
+    value = (a.rays if strong else world * a.rays) * a.steps / elapsed
     out = {
         "metric": "train rays/sec (4096 rays x 192 samples)" if a.mode == "train" else "render rays/sec (eval)",
         "value": round(value, 1),
@@ -407,14 +434,15 @@ def main():
         "warmup": a.warmup,
         "ms_per_step": round(1e3 * elapsed / a.steps, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": a.scaling,
         "vs_baseline": None,
         "dtype": "fp32",
         "data": "synthetic ({} rays, random-init hash tables and MLPs)".format(
             {"blender": "lego spiral-pose", "llff": "forward-facing LLFF rig", "scannet": "indoor room"}[wl["rays"]]),
-        "config": {"workload": wl["desc"].format(R=a.rays) + ("" if a.mode == "train" else " [render only]"),
-                   "name": a.workload, "rays_per_gpu": a.rays, "global_batch": a.rays * world,
-                   "samples": f"{wl['args']['N_samples']}+{wl['args']['N_importance']}", "parallelism": f"dp{world}"},
+        "config": {"workload": wl["desc"].format(R=R) + ("" if a.mode == "train" else " [render only]"),
+                   "name": a.workload, "rays_per_gpu": R, "global_batch": R * world,
+                   "samples": f"{wl['args']['N_samples']}+{wl['args']['N_importance']}",
+                   "parallelism": f"dp{world}" + ("-zero1" if zero else "")},
         "hip_graph": bool(gstep is not None and gstep.captures > 0),
         "loss": round(float(loss), 6),
         "roofline": roofline,

@@ -1,7 +1,7 @@
 """Public API of indoor_nerf_amd: the reference's render_rays-path names (PocketNeRF/run_nerf.py,
 run_nerf_helpers.py, hash_encoding.py, radam.py, loss.py) backed by libnerfhip."""
 from . import _lib
-from .dist import GradArena, broadcast_params, init_process_group, shard
+from .dist import GradArena, ShardedOptimizer, broadcast_params, init_process_group, shard
 from .field import NeRFSmall, batchify, run_network
 from .hashgrid import HashEmbedder, SHEncoder, level_resolutions
 from .losses import sigma_sparsity_loss, total_variation_all, total_variation_loss, train_loss
@@ -19,7 +19,7 @@ from .priors import (ManhattanFrameEstimator, SemanticPlaneDetector, combine_str
 __all__ = ["HashEmbedder", "SHEncoder", "NeRFSmall", "RAdam", "run_network", "batchify", "batchify_rays", "render",
            "render_rays", "raw2outputs", "sample_pdf", "get_rays", "get_rays_np", "ndc_rays", "img2mse", "mse2psnr",
            "to8b", "create_nerf", "make_args", "save_checkpoint", "train_step", "total_variation_loss",
-           "total_variation_all", "train_loss", "sigma_sparsity_loss", "level_resolutions", "GradArena", "init_process_group",
+           "total_variation_all", "train_loss", "sigma_sparsity_loss", "level_resolutions", "GradArena", "ShardedOptimizer", "init_process_group",
            "shard", "broadcast_params", "manual_seed", "load_library", "LearnedBitwidthQuantizer", "FakeQuantizer",
            "PassthroughQuantizer", "calculate_fqr", "acaq_update", "acaq_quantizers", "RaySampler", "crop_window", "camera",
            "get_bbox3d_for_blenderobj", "get_bbox3d_for_llff", "render_path", "load_blender_data", "load_llff_data",

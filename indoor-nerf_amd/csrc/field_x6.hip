@@ -64,8 +64,8 @@ __device__ __forceinline__ void split2(float a, float b, uint32_t& p0, uint32_t&
     p2 = pk_bf16(sa, sb);
 }
 
-// ReLU as one v_max_i32 (a negative float is a negative int; +0/-0 -> +0): relu16 of
-// field_common.h compiles to two v_max_f32 per element on MFMA results (a canonicalising max first).
+// ReLU as one integer op per element (a negative float is a negative int; +0/-0 -> +0): a float
+// max compiles to two v_max_f32 per element on MFMA results (a canonicalising max first).
 __device__ __forceinline__ void relu16i(floatx16& v) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -119,12 +119,8 @@ constexpr int IM_PIECE = IM_C2 + 16 * S64;   // 11,136 elements per piece
 constexpr int IM_BYTES = 3 * IM_PIECE * 2;   // 66,816 B
 // logical (unpadded) element index ranges of the five matrices, for the fill loop
 constexpr int L_W1 = 2048, L_C0 = 3072, L_C1 = 5120, L_C2 = 9216, L_END = 10240;
-// per-wave staging for the weight gradients: activations [32 points][64] and one 32-row
-// gradient tile [32 points][32], three pieces each
-constexpr int STA_PIECE = 32 * S64;
+// backward staging of one 32-row gradient tile [32 points][32], three bf16 pieces
 constexpr int STG_PIECE = 32 * S32;
-constexpr int ST_WAVE = 3 * (STA_PIECE + STG_PIECE);       // 9,984 elements = 19,968 B
-constexpr int X6_BWD_LDS = IM_BYTES + 4 * ST_WAVE * 2;      // 146,688 B
 
 __device__ __forceinline__ float image_value(int idx, const nerf_mlp_weights& W) {
     if (idx < L_W1) return W.w0[idx];                                     // [64][32]
@@ -215,10 +211,6 @@ __device__ __forceinline__ void stage(__bf16* st, int piece, int S, const S3& s,
     }
 }
 
-__device__ __forceinline__ void stage_act(__bf16* stA, const S3& s, int t, int c, int j, int h) {
-    stage(stA, STA_PIECE, S64, s, 32 * t, c, j, h);
-}
-
 __device__ __forceinline__ void stage_grad(__bf16* stG, const S3& s, int c, int j, int h) {
     stage(stG, STG_PIECE, S32, s, 0, c, j, h);
 }
@@ -229,25 +221,6 @@ __device__ __forceinline__ int opaque_zero() {
     int z = 0;
     asm volatile("" : "+v"(z));
     return z;
-}
-
-// Between staging writes and the transposed reads of other lanes of the SAME wave nothing is
-// needed: a wave's LDS instructions execute in issue order, and the compiler cannot reorder a
-// staging store and a transposed load of the same image (lane-dependent offsets: may alias). An
-// asm barrier here would end the scheduling region and expose every LDS latency.
-#define X6_WAVE_SYNC() ((void)0)
-
-// dW[t-tile][u] += sum over the 32 staged points of G[m][pt] A[32u + n][pt] (MFMAs chained onto
-// the register-resident sums; a per-tile partial joined with a VALU fp32 add measured the same
-// error and costs three VALU ops per accumulator element)
-template <int NU>
-__device__ __forceinline__ void wgrad_tile(floatx16 (&acc)[NU], const __bf16* stG, const __bf16* stA, int lane) {
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-        const S3 A = tr_read(stG, STG_PIECE, 0, S32, 16 * c, 0, lane);
-#pragma unroll
-        for (int u = 0; u < NU; ++u) acc[u] = mma6(A, tr_read(stA, STA_PIECE, 0, S64, 16 * c, 32 * u, lane), acc[u]);
-    }
 }
 
 // ---- per-tile inputs ---------------------------------------------------------------------------
@@ -413,214 +386,42 @@ __global__ void __launch_bounds__(512, 2) mlp_fwd_x6_kernel(MlpArgs a) {
     }
 }
 
-// ================================================================ backward kernel
-template <bool QUANT>
-__global__ void __launch_bounds__(256, 1) mlp_bwd_x6_kernel(MlpArgs a) {
-    __shared__ __attribute__((aligned(16))) __bf16 lds[X6_BWD_LDS / 2];
-    __bf16* img = lds;
-    const int wv = threadIdx.x >> 6;
-    __bf16* stA = lds + 3 * IM_PIECE + wv * ST_WAVE;
-    __bf16* stG = stA + 3 * STA_PIECE;
+// Calibration-only launch of the activation quantizer (quantization.py:97-119 on the first
+// netchunk's h = relu(x W0^T), run_nerf_helpers.py:280-284): layer 0 per tile, wave min/max, one
+// atomic pair per wave (order-preserving u32 images of the floats).
+__global__ void __launch_bounds__(512, 2) mlp_act_minmax_x6_kernel(MlpArgs a) {
+    __shared__ __attribute__((aligned(16))) __bf16 img[3 * IM_PIECE];
     fill_images(img, a.W);
     __syncthreads();
-
     const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
-    QuantRec aq{};
-    if constexpr (QUANT) aq = *a.aq;
-    floatx16 dC2[2], dC1[2][2], dC0[2][1], dW1[2], dW0[2][1];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        dC2[i] = zero16(); dW1[i] = zero16(); dC0[i][0] = zero16(); dW0[i][0] = zero16();
-        dC1[i][0] = zero16(); dC1[i][1] = zero16();
-    }
-
-    const int64_t n_tiles = (a.P + 31) / 32;
-    for (int64_t tile = (int64_t)blockIdx.x * 4 + wv; tile < n_tiles; tile += (int64_t)gridDim.x * 4) {
-        const __bf16* imt = img + opaque_zero();
-        InX6 in;
-        load_in_x6(a, tile, j, h, in);
-        ActX6 f;
-        floatx16 unused;
-        fwd_chain<QUANT>(imt, in, f, unused, lane, false, aq);
-
-        float4 g4 = *reinterpret_cast<const float4*>(a.graw + 4u * (in.valid ? in.pt : (uint32_t)(a.P - 1)));
-        if (!in.valid) g4 = make_float4(0.f, 0.f, 0.f, 0.f);
-        const bool keep = in.valid && (a.keep ? a.keep[in.pt] != 0 : true);
-        const float gsig = keep ? g4.w : 0.f;
-
-        // ---- C2: ga3 = (C2^T g_rgb) * (h3 > 0); dC2 += g_rgb h3^T
-        floatx16 ga3[2];
-        {
-            const S3 GR = h ? split8(0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f)
-                            : split8(g4.x, g4.y, g4.z, 0.f, 0.f, 0.f, 0.f, 0.f);   // rows 0..2 of chunk 0
-#pragma unroll
-            for (int t = 0; t < 2; ++t) {
-                ga3[t] = mma6(tr_read(imt, IM_PIECE, IM_C2, S64, 0, 32 * t, lane), GR, zero16());
-#pragma unroll
-                for (int r = 0; r < 16; ++r) ga3[t][r] = f.h3[t][r] > 0.f ? ga3[t][r] : 0.f;
-            }
-            stage_grad(stG, GR, 0, j, h);      // columns 16..31 stay stale: they only reach dC2 rows >= 16
-        }
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-            for (int c = 0; c < 2; ++c) stage_act(stA, split_chunk(f.h3[t], c), t, c, j, h);
-        X6_WAVE_SYNC();
-        wgrad_tile<2>(dC2, stG, stA, lane);
-        X6_WAVE_SYNC();
-
-        // ---- C1: ga2 = (C1^T ga3) * (h2 > 0); dC1 += ga3 h2^T
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-            for (int c = 0; c < 2; ++c) stage_act(stA, split_chunk(f.h2[t], c), t, c, j, h);
-        floatx16 ga2[2];
-        ga2[0] = ga2[1] = zero16();
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-#pragma unroll
-            for (int c = 0; c < 2; ++c) {
-                const S3 g = split_chunk(ga3[t], c);
-                stage_grad(stG, g, c, j, h);
-#pragma unroll
-                for (int ti = 0; ti < 2; ++ti)
-                    ga2[ti] = mma6(tr_read(imt, IM_PIECE, IM_C1, S64, 32 * t + 16 * c, 32 * ti, lane), g, ga2[ti]);
-            }
-            X6_WAVE_SYNC();
-            wgrad_tile<2>(dC1[t], stG, stA, lane);
-            X6_WAVE_SYNC();
-        }
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) ga2[t][r] = f.h2[t][r] > 0.f ? ga2[t][r] : 0.f;
-
-        // ---- C0: go = C0'^T ga2 (rows 0..15: o = [sigma, geo]; rows 16..31: d sh); dC0 += ga2 [o ; sh]^T
-        // The accumulator is seeded: row 0 (sigma) with g_sigma (C0' column 0 is zero) and, with
-        // the normals head, rows 1..15 with its d geo.
-        floatx16 go = zero16();
-        if (h == 0) go[0] = gsig;
-        if (a.dgeo && in.valid) {
-#pragma unroll
-            for (int r = 0; r < 8; ++r) {
-                const int row = row_of(r, h);
-                if (row >= 1) go[r] = a.dgeo[16u * in.pt + row];
-            }
-        }
-        stage_act(stA, split_chunk(f.o, 0), 0, 0, j, h);
-        {   // SH re-evaluated (as h1 below, not held through the C2/C1 stages)
-            float shv[8];
-            load_sh6(a, in.pt, in.valid, h, shv, opaque_zero());
-            stage_act(stA, split_arr(shv), 0, 1, j, h);
-        }
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-#pragma unroll
-            for (int c = 0; c < 2; ++c) {
-                const S3 g = split_chunk(ga2[t], c);
-                stage_grad(stG, g, c, j, h);
-                go = mma6(tr_read(imt, IM_PIECE, IM_C0, S32, 32 * t + 16 * c, 0, lane), g, go);
-            }
-            X6_WAVE_SYNC();
-            wgrad_tile<1>(dC0[t], stG, stA, lane);
-            X6_WAVE_SYNC();
-        }
-        if (a.dsh && in.valid) {
-#pragma unroll
-            for (int r = 8; r < 16; ++r) a.dsh[16u * in.pt + row_of(r, h) - 16] = go[r];
-        }
-
-        // ---- W1: ga1 = (W1^T go) * (h1 > 0); dW1 += go h1^T
-        // h1 is recomputed here from a reload of x (24 MFMAs) rather than held in 32 registers
-        // through the C-layer stages, where the register peak is (the reload's opaque offset keeps
-        // the compiler from reusing the first load's registers instead)
-        float xr[16];
-        load_x6(a, in.pt, in.valid, h, xr, opaque_zero());
+    const int64_t n = a.calib_points < a.P ? a.calib_points : a.P;
+    const int64_t n_tiles = (n + 31) / 32;
+    const int wpb = blockDim.x >> 6;
+    float lo = INFINITY, hi = -INFINITY;
+    for (int64_t tile = (int64_t)blockIdx.x * wpb + (threadIdx.x >> 6); tile < n_tiles; tile += (int64_t)gridDim.x * wpb) {
+        const uint32_t pt = (uint32_t)(tile * 32 + j);
+        const bool valid = tile * 32 + j < n;
+        float x[16];
+        load_x6(a, pt, valid, h, x, 0);
         floatx16 h1[2];
         uint32_t m1;
-        layer0<QUANT>(imt, xr, h1, m1, lane, aq);
-        floatx16 ga1[2];
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-            for (int c = 0; c < 2; ++c) stage_act(stA, split_chunk(h1[t], c), t, c, j, h);
-        {
-            const S3 GO = split_chunk(go, 0);
-            stage_grad(stG, GO, 0, j, h);      // columns 16..31 stale: they only reach dW1 rows >= 16
-#pragma unroll
-            for (int t = 0; t < 2; ++t) {
-                floatx16 acc = mma6(tr_read(imt, IM_PIECE, IM_W1, S64, 0, 32 * t, lane), GO, zero16());
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const bool on = QUANT ? ((m1 >> (16 * t + r)) & 1u) != 0u : h1[t][r] > 0.f;
-                    acc[r] = on ? acc[r] : 0.f;
-                }
-                ga1[t] = acc;
-            }
-        }
-        X6_WAVE_SYNC();
-        wgrad_tile<2>(dW1, stG, stA, lane);
-        X6_WAVE_SYNC();
-
-        // ---- W0: gx = W0^T ga1 (-> d features); dW0 += ga1 x^T
-        stage_act(stA, split_arr(xr), 0, 0, j, h);
-        stage_act(stA, split_arr(xr + 8), 0, 1, j, h);
-        floatx16 gx = zero16();
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-#pragma unroll
-            for (int c = 0; c < 2; ++c) {
-                const S3 g = split_chunk(ga1[t], c);
-                stage_grad(stG, g, c, j, h);
-                gx = mma6(tr_read(imt, IM_PIECE, IM_W0, S32, 32 * t + 16 * c, 0, lane), g, gx);
-            }
-            X6_WAVE_SYNC();
-            wgrad_tile<1>(dW0[t], stG, stA, lane);
-            X6_WAVE_SYNC();
-        }
-        if (a.dfeat && in.valid) {
+        layer0<false>(img + opaque_zero(), x, h1, m1, lane, QuantRec{});
+        if (valid) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const int fi = row_of(r, h);
-                a.dfeat[in.pt * (uint32_t)a.sp + (fi >> 1) * (uint32_t)a.sl + (fi & 1)] = gx[r];
+                lo = fminf(lo, fminf(h1[0][r], h1[1][r]));
+                hi = fmaxf(hi, fmaxf(h1[0][r], h1[1][r]));
             }
         }
     }
-
-    // ---- block reduction of the weight gradients (LDS fp32 atomics), one global flush per block
-    __syncthreads();
-    float* gw = reinterpret_cast<float*>(lds);
-    for (int i = threadIdx.x; i < GW_TOTAL; i += blockDim.x) gw[i] = 0.f;
-    __syncthreads();
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int rr = row_of(r, h);
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            if (rr < 3) atomicAdd(gw + GW_C2 + rr * 64 + 32 * u + j, dC2[u][r]);
-            if (rr < 16) atomicAdd(gw + GW_W1 + rr * 64 + 32 * u + j, dW1[u][r]);
-        }
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-            const int row = 32 * t + rr;
-#pragma unroll
-            for (int u = 0; u < 2; ++u) atomicAdd(gw + GW_C1 + row * 64 + 32 * u + j, dC1[t][u][r]);
-            // C0' column j: 0 sigma slot (no weight), 1..15 -> C0 col 15 + j, 16..31 -> C0 col j - 16
-            if (j != 0) atomicAdd(gw + GW_C0 + row * 31 + (j < 16 ? 15 + j : j - 16), dC0[t][0][r]);
-            atomicAdd(gw + GW_W0 + row * 32 + j, dW0[t][0][r]);
-        }
+    for (int o = 32; o > 0; o >>= 1) {
+        lo = fminf(lo, __shfl_xor(lo, o, 64));
+        hi = fmaxf(hi, __shfl_xor(hi, o, 64));
     }
-    __syncthreads();
-    for (int i = threadIdx.x; i < GW_TOTAL; i += blockDim.x) {
-        float* dst;
-        int k;
-        if (i < GW_W1) { dst = a.G.w0; k = i; }
-        else if (i < GW_C0) { dst = a.G.w1; k = i - GW_W1; }
-        else if (i < GW_C1) { dst = a.G.c0; k = i - GW_C0; }
-        else if (i < GW_C2) { dst = a.G.c1; k = i - GW_C1; }
-        else { dst = a.G.c2; k = i - GW_C2; }
-        const float v = gw[i];
-        if (v != 0.f) __hip_atomic_fetch_add(dst + k, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0 && lo <= hi) {
+        atomicMin(a.act_minmax, f2ord(lo));
+        atomicMax(a.act_minmax + 1, f2ord(hi));
     }
 }
 
@@ -1035,7 +836,6 @@ __global__ void __launch_bounds__(512, 1) mlp_bwd_x6cg_kernel(MlpArgs a) {
     // here (one ds_add_f32 per value and wave into a shared image) cost 49 us per launch.
     static_assert(4 * GW_TOTAL * (int)sizeof(float) <= X6_CG_LDS, "four weight-gradient images must fit the LDS");
     __syncthreads();
-    if (a.flush_skip == 2) return;
     float* gw = reinterpret_cast<float*>(lds);
     if (wgrad_wave) {
         float* mine = gw + p * GW_TOTAL;
@@ -1071,7 +871,7 @@ __global__ void __launch_bounds__(512, 1) mlp_bwd_x6cg_kernel(MlpArgs a) {
         else if (i < GW_C2) { dst = a.G.c1; k = i - GW_C1; }
         else { dst = a.G.c2; k = i - GW_C2; }
         const float v = (gw[i] + gw[GW_TOTAL + i]) + (gw[2 * GW_TOTAL + i] + gw[3 * GW_TOTAL + i]);
-        if (v != 0.f && a.flush_skip == 0) __hip_atomic_fetch_add(dst + k, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (v != 0.f) __hip_atomic_fetch_add(dst + k, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -1093,31 +893,34 @@ int launch_mlp_fwd_x6(const MlpArgs& a, hipStream_t stream) {
     return NERF_OK;
 }
 
-int launch_mlp_bwd_x6(const MlpArgs& a_in, hipStream_t stream, bool split_roles) {
-    MlpArgs a = a_in;
-    const char* fs = getenv("NERF_X6CG_FLUSH");   // A/B timing of the weight-gradient reduction only
-    a.flush_skip = (fs && fs[0] == '1') ? 1 : (fs && fs[0] == '2') ? 2 : 0;
+int launch_mlp_act_minmax_x6(const MlpArgs& a, hipStream_t stream) {
+    NERF_REQUIRE(fits_u32(a), "mlp_act_minmax(x6): %lld points exceed 32-bit indexing", (long long)a.P);
+    const int64_t n = a.calib_points < a.P ? a.calib_points : a.P;
+    if (n <= 0) return NERF_OK;
+    const int64_t tiles = (n + 31) / 32;
+    const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((tiles + 7) / 8, 256 * 2));
+    hipLaunchKernelGGL(mlp_act_minmax_x6_kernel, dim3((unsigned)blocks), dim3(512), 0, stream, a);
+    NERF_CHECK_LAUNCH("mlp_act_minmax(x6)");
+    return NERF_OK;
+}
+
+int launch_mlp_bwd_x6(const MlpArgs& a, hipStream_t stream) {
     NERF_REQUIRE(fits_u32(a), "mlp_bwd(x6): %lld points exceed 32-bit indexing", (long long)a.P);
     const int64_t tiles = (a.P + 31) / 32;
     const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((tiles + 3) / 4, 256));
-    if (split_roles) {
-        if (a.aq)
-            hipLaunchKernelGGL(mlp_bwd_x6cg_kernel<true>, dim3((unsigned)blocks), dim3(512), 0, stream, a);
-        else
-            hipLaunchKernelGGL(mlp_bwd_x6cg_kernel<false>, dim3((unsigned)blocks), dim3(512), 0, stream, a);
-#ifdef NERF_X6CG_PROF
-        unsigned long long pr[4];
-        (void)hipDeviceSynchronize();
-        (void)hipMemcpyFromSymbol(pr, HIP_SYMBOL(cg_prof), sizeof(pr));
-        fprintf(stderr, "cgprof P=%lld chain wait/total %llu/%llu  wgrad wait/total %llu/%llu (s_memtime ticks, sum over waves)\n",
-                (long long)a.P, pr[0], pr[1], pr[2], pr[3]);
-        const unsigned long long z[4] = {0, 0, 0, 0};
-        (void)hipMemcpyToSymbol(HIP_SYMBOL(cg_prof), z, sizeof(z));
-#endif
-    } else if (a.aq)
-        hipLaunchKernelGGL(mlp_bwd_x6_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, stream, a);
+    if (a.aq)
+        hipLaunchKernelGGL(mlp_bwd_x6cg_kernel<true>, dim3((unsigned)blocks), dim3(512), 0, stream, a);
     else
-        hipLaunchKernelGGL(mlp_bwd_x6_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, stream, a);
+        hipLaunchKernelGGL(mlp_bwd_x6cg_kernel<false>, dim3((unsigned)blocks), dim3(512), 0, stream, a);
+#ifdef NERF_X6CG_PROF
+    unsigned long long pr[4];
+    (void)hipDeviceSynchronize();
+    (void)hipMemcpyFromSymbol(pr, HIP_SYMBOL(cg_prof), sizeof(pr));
+    fprintf(stderr, "cgprof P=%lld chain wait/total %llu/%llu  wgrad wait/total %llu/%llu (s_memtime ticks, sum over waves)\n",
+            (long long)a.P, pr[0], pr[1], pr[2], pr[3]);
+    const unsigned long long z[4] = {0, 0, 0, 0};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(cg_prof), z, sizeof(z));
+#endif
     NERF_CHECK_LAUNCH("mlp_bwd(x6)");
     return NERF_OK;
 }

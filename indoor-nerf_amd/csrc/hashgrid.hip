@@ -37,62 +37,6 @@ struct HashGradParams {
 
 // QUANT: every gathered corner feature goes through the level's A-CAQ quantizer first
 // (hash_encoding.py:97-101: quantizers[i](voxel_embedds), elementwise on the [P,8,2] gather).
-template <bool QUANT>
-__global__ void __launch_bounds__(256) hash_encode_fwd_kernel(
-    const float* __restrict__ xyz, int64_t n, HashParams hp,
-    float* __restrict__ feat, int64_t sp, int64_t sl, uint8_t* __restrict__ keep,
-    const QuantRec* __restrict__ qrec) {
-    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int lvl = blockIdx.y;
-    if (p >= n) return;
-    const float x = xyz[3 * p + 0], y = xyz[3 * p + 1], z = xyz[3 * p + 2];
-    const AxisCell ax = axis_cell(x, hp.bmin[0], hp.bmax[0], hp.cell[lvl][0]);
-    const AxisCell ay = axis_cell(y, hp.bmin[1], hp.bmax[1], hp.cell[lvl][1]);
-    const AxisCell az = axis_cell(z, hp.bmin[2], hp.bmax[2], hp.cell[lvl][2]);
-    if (lvl == 0 && keep) keep[p] = (ax.inside && ay.inside && az.inside) ? 1 : 0;
-
-    const float2* __restrict__ tab = reinterpret_cast<const float2*>(hp.tables[lvl]);
-    const uint32_t bx = (uint32_t)ax.base, by = (uint32_t)ay.base, bz = (uint32_t)az.base;
-    // corner c = 4i + 2j + k  <->  offset (i, j, k)  (utils.py:9)
-    float2 e[8];
-#pragma unroll
-    for (int c = 0; c < 8; ++c) {
-        const uint32_t h = spatial_hash3(bx + ((c >> 2) & 1), by + ((c >> 1) & 1), bz + (c & 1), hp.mask);
-        e[c] = tab[h];
-    }
-    if constexpr (QUANT) {
-        const QuantRec q = qrec[lvl];
-#pragma unroll
-        for (int c = 0; c < 8; ++c) {
-            e[c].x = fake_quant(e[c].x, q);
-            e[c].y = fake_quant(e[c].y, q);
-        }
-    }
-    const float wx = ax.w, wy = ay.w, wz = az.w;
-    const float ox = 1.0f - wx, oy = 1.0f - wy, oz = 1.0f - wz;
-    float2 out;
-#define NERF_TRI(F)                                                   \
-    {                                                                 \
-        const float c00 = e[0].F * ox + e[4].F * wx;                  \
-        const float c01 = e[1].F * ox + e[5].F * wx;                  \
-        const float c10 = e[2].F * ox + e[6].F * wx;                  \
-        const float c11 = e[3].F * ox + e[7].F * wx;                  \
-        const float c0 = c00 * oy + c10 * wy;                         \
-        const float c1 = c01 * oy + c11 * wy;                         \
-        out.F = c0 * oz + c1 * wz;                                    \
-    }
-    NERF_TRI(x)
-    NERF_TRI(y)
-#undef NERF_TRI
-    float* dst = feat + p * sp + (int64_t)lvl * sl;
-    if (((sp | sl) & 1) == 0) {
-        *reinterpret_cast<float2*>(dst) = out;
-    } else {
-        dst[0] = out.x;
-        dst[1] = out.y;
-    }
-}
-
 // Lane-pair forward: lanes 2m and 2m+1 share point m of the wave and gather the x = 0 and x = 1
 // corners of its voxel. Corners (x,y,z) and (x+1,y,z) hash to h and h ^ (x ^ (x+1)), the same 64-B
 // line for 15 of 16 x, so each gather instruction touches ~32 lines instead of 64 (the vector
@@ -154,12 +98,11 @@ __device__ __forceinline__ void atomic_add_f32(float* p, float v) {
     __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// COALESCE = false: every lane issues its own 16 atomics (8 corners x 2 features): each wave
-// instruction then carries 64 unrelated addresses = 64 memory-side requests.
-// COALESCE = true: the per-item contributions are staged in LDS and re-issued so that one wave
-// instruction covers 4 items x 16 dwords, ordered (item, corner pair (j,k), i, feature). Corners
-// (x, y, z) and (x+1, y, z) hash to h and h ^ (x ^ (x+1)) (x only touches the low 11 bits), so the
-// 4 dwords of a pair usually share one 64-B segment and leave as ONE atomic request.
+// MODE 1 (no workspace): the per-item contributions are staged in LDS and re-issued as float
+// atomics so that one wave instruction covers 4 items x 16 dwords, ordered (item, corner pair
+// (j,k), i, feature). Corners (x, y, z) and (x+1, y, z) hash to h and h ^ (x ^ (x+1)) (x only
+// touches the low 11 bits), so the 4 dwords of a pair usually share one 64-B segment and leave as
+// ONE atomic request.
 constexpr uint32_t kSkip = 0xFFFFFFFFu;
 
 // MODE 3 (binned, "owner computes"): float atomics execute at the memory side at one chip-wide
@@ -169,12 +112,11 @@ constexpr uint32_t kSkip = 0xFFFFFFFFu;
 // replaces the memory-side atomics: this kernel writes each (row, d feat) entry into a per-chunk
 // region sorted by owner slice (plain stores), and hash_bwd_owner_kernel sums each slice in LDS.
 constexpr int kChunkCap = 256 * 8;        // entries per 256-point chunk (8 corners per point)
-constexpr int kMaxSliceLog2 = 13;         // owner slice: up to 2^13 rows x 16 B (fp64 pair) = 128 KiB of LDS
+constexpr int kSliceLog2 = 13;            // owner slice: 2^13 rows x 16 B (fp64 pair) = 128 KiB of LDS
 constexpr int kMaxOwnersLog2 = 7;
 constexpr int kMaxOwners = 1 << kMaxOwnersLog2;
 
-// MODE 0: per-lane atomics; 1: coalesced re-issue (default); 2: as 1 without the atomics (cost floor,
-// A/B measurement only: results are wrong).
+// MODE 1: coalesced float atomics (no workspace); 3: binned (default).
 template <int MODE>
 __global__ void __launch_bounds__(256) hash_encode_bwd_kernel(
     const float* __restrict__ xyz, int64_t n, HashGradParams hp,
@@ -228,15 +170,7 @@ __global__ void __launch_bounds__(256) hash_encode_bwd_kernel(
     const bool emit = valid && tail;
     float* tab = hp.dtables[lvl];
     const uint32_t bx = (uint32_t)ax.base, by = (uint32_t)ay.base, bz = (uint32_t)az.base;
-    if constexpr (MODE == 0) {
-        if (!emit) return;
-#pragma unroll
-        for (int c = 0; c < 8; ++c) {
-            const uint32_t h = spatial_hash3(bx + ((c >> 2) & 1), by + ((c >> 1) & 1), bz + (c & 1), hp.mask);
-            atomic_add_f32(tab + 2 * h + 0, cgx[c]);
-            atomic_add_f32(tab + 2 * h + 1, cgy[c]);
-        }
-    } else if constexpr (MODE == 3) {
+    if constexpr (MODE == 3) {
         // Bin: count this chunk's entries per owner slice (LDS atomics), scan, place every entry at
         // its slot of an LDS image of the chunk's region, then write the image out with 16-B
         // coalesced stores (scattered per-lane stores were TA-bound: 64 lines per instruction).
@@ -316,11 +250,7 @@ __global__ void __launch_bounds__(256) hash_encode_bwd_kernel(
             const int f = within & 1;
             const uint32_t h = s_h[wv][item][c];
             const float v = s_val[wv][item][2 * c + f];
-            if constexpr (MODE == 1) {
-                if (h != kSkip && v != 0.f) atomic_add_f32(tab + 2 * h + f, v);
-            } else {
-                if (h != kSkip && v == 1234.5f) tab[2 * h + f] = v;
-            }
+            if (h != kSkip && v != 0.f) atomic_add_f32(tab + 2 * h + f, v);
         }
     }
 }
@@ -333,8 +263,9 @@ __global__ void __launch_bounds__(256) hash_encode_bwd_kernel(
 // step the entries of a window of chunks are numbered consecutively (exclusive scan of the segment
 // counts in LDS) and every lane takes every 64th entry, 8 per batch: 16 global loads in flight per
 // lane, all lanes busy whatever the segment lengths.
-// SLICE_LOG2 / THREADS: 2^13-row slices with one 1024-thread block per CU (128 KiB of LDS), or
-// 2^12-row slices (64 KiB) so that two blocks share a CU (NERF_HASH_OWNER, owner_variant()).
+// SLICE_LOG2 / THREADS: 2^13-row slices with one 1024-thread block per CU (128 KiB of LDS); 2^12-row
+// slices with two 512-thread blocks per CU measured slower (0.41 vs 0.34 ms per backward: the
+// doubled per-owner segment scans outweigh the overlap).
 template <int SLICE_LOG2, int THREADS>
 __global__ void __launch_bounds__(THREADS) hash_bwd_owner_kernel(HashGradParams hp) {
     constexpr int kOwnerThreads = THREADS;
@@ -430,7 +361,7 @@ __global__ void __launch_bounds__(THREADS) hash_bwd_owner_kernel(HashGradParams 
         auto fetch = [&](const size_t (&addr)[8], uint16_t (&h)[8], float2 (&g)[8]) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-// default-policy loads: the coarse pass's bins were written just before this launch and part
+                // default-policy loads: the coarse pass's bins were written just before this launch and part
                 // of them is still in the Infinity Cache (nontemporal loads: 0.39 vs 0.33 ms per step)
                 h[j] = hp.bin_h[addr[j]];
                 const uint64_t gv = *reinterpret_cast<const uint64_t*>(hp.bin_g + addr[j]);   // (d feat0, d feat1)
@@ -502,17 +433,9 @@ struct BinPlan {
     size_t off_h, off_g, off_off, total;   // byte offsets in the workspace
 };
 
-// owner-pass geometry: 1 = 2^13-row slices, 1024 threads, one block per CU (default);
-// 0 = 2^12-row slices, 512 threads, two blocks per CU (NERF_HASH_OWNER=12; A/B in the lego step:
-// 0.41 vs 0.34 ms per backward, the doubled per-owner segment scans outweigh the overlap)
-static int owner_variant() {
-    const char* e = getenv("NERF_HASH_OWNER");
-    return (e && e[0] == '1' && e[1] == '2') ? 0 : 1;
-}
-
 // Binned path for log2_T in [1, slice + log2(kMaxOwners)]: slices of min(2^slice, T) rows.
 static bool make_bin_plan(int n_levels, int log2_T, int64_t n_points, BinPlan& B) {
-    const int slice = owner_variant() == 1 ? 13 : 12;
+    const int slice = kSliceLog2;
     if (log2_T < 1 || log2_T > slice + kMaxOwnersLog2 || n_points < 0) return false;
     B.slice_log2 = log2_T < slice ? log2_T : slice;
     B.owner_log2 = log2_T - B.slice_log2;
@@ -525,23 +448,6 @@ static bool make_bin_plan(int n_levels, int log2_T, int64_t n_points, BinPlan& B
     B.off_off = B.off_h + up(entries * sizeof(uint16_t));
     B.total = B.off_off + up(offs * sizeof(uint32_t));
     return true;
-}
-
-// NERF_HASH_BWD=0 / 1 / 2 select the per-lane-atomics / coalesced-atomics / no-atomics variants
-// (A/B measurements only; the binned path runs whenever the caller passes a workspace).
-// NERF_HASH_BWD=0 / 2 select the per-lane-atomics / no-atomics variants (A/B measurements only).
-static int bwd_mode() {
-    const char* e = getenv("NERF_HASH_BWD");
-    if (e && e[0] == '0') return 0;
-    if (e && e[0] == '1') return 1;
-    if (e && e[0] == '2') return 2;
-    return 3;
-}
-
-// NERF_HASH_FWD=0 selects the one-point-per-lane forward (A/B measurements); default: lane pairs.
-static bool fwd_pair() {
-    const char* e = getenv("NERF_HASH_FWD");
-    return !(e && e[0] == '0');
 }
 
 }  // namespace nerf
@@ -567,24 +473,13 @@ extern "C" int nerf_hash_encode_fwd_q(const float* d_xyz, int64_t n_points, cons
     fill_cells(hp.cell, bbox_min3, bbox_max3, level_res, n_levels);
     hp.mask = (uint32_t)((1u << log2_T) - 1u);
     const QuantRec* q = reinterpret_cast<const QuantRec*>(d_qrec);
-    if (fwd_pair()) {
-        dim3 grid2(blocks_for(2 * n_points, 256), n_levels);
-        if (q)
-            hipLaunchKernelGGL(hash_encode_fwd_pair_kernel<true>, grid2, dim3(256), 0, as_stream(stream), d_xyz,
-                               n_points, hp, d_feat, feat_stride_point, feat_stride_level, d_keep, q);
-        else
-            hipLaunchKernelGGL(hash_encode_fwd_pair_kernel<false>, grid2, dim3(256), 0, as_stream(stream), d_xyz,
-                               n_points, hp, d_feat, feat_stride_point, feat_stride_level, d_keep, q);
-        NERF_CHECK_LAUNCH("hash_encode_fwd");
-        return NERF_OK;
-    }
-    dim3 grid(blocks_for(n_points, 256), n_levels);
+    dim3 grid2(blocks_for(2 * n_points, 256), n_levels);
     if (q)
-        hipLaunchKernelGGL(hash_encode_fwd_kernel<true>, grid, dim3(256), 0, as_stream(stream), d_xyz, n_points, hp,
-                           d_feat, feat_stride_point, feat_stride_level, d_keep, q);
+        hipLaunchKernelGGL(hash_encode_fwd_pair_kernel<true>, grid2, dim3(256), 0, as_stream(stream), d_xyz,
+                           n_points, hp, d_feat, feat_stride_point, feat_stride_level, d_keep, q);
     else
-        hipLaunchKernelGGL(hash_encode_fwd_kernel<false>, grid, dim3(256), 0, as_stream(stream), d_xyz, n_points, hp,
-                           d_feat, feat_stride_point, feat_stride_level, d_keep, q);
+        hipLaunchKernelGGL(hash_encode_fwd_pair_kernel<false>, grid2, dim3(256), 0, as_stream(stream), d_xyz,
+                           n_points, hp, d_feat, feat_stride_point, feat_stride_level, d_keep, q);
     NERF_CHECK_LAUNCH("hash_encode_fwd");
     return NERF_OK;
 }
@@ -615,9 +510,8 @@ static int hash_encode_bwd_impl(const float* d_xyz, int64_t n_points, const floa
     for (int a = 0; a < 3; ++a) { hp.bmin[a] = bbox_min3[a]; hp.bmax[a] = bbox_max3[a]; }
     fill_cells(hp.cell, bbox_min3, bbox_max3, level_res, n_levels);
     hp.mask = (uint32_t)((1u << log2_T) - 1u);
-    int mode = bwd_mode();
     BinPlan B{};
-    if (mode == 3 && !(d_workspace != nullptr && make_bin_plan(n_levels, log2_T, n_points, B))) mode = 1;
+    const int mode = (d_workspace != nullptr && make_bin_plan(n_levels, log2_T, n_points, B)) ? 3 : 1;
     if (mode == 3) {
         NERF_REQUIRE(workspace_bytes >= B.total,
                      "hash_encode_bwd: workspace %zu B < %zu B (nerf_hash_encode_bwd_workspace_bytes)",
@@ -633,30 +527,15 @@ static int hash_encode_bwd_impl(const float* d_xyz, int64_t n_points, const floa
         hp.owner_log2 = B.owner_log2;
     }
     const dim3 grid(blocks_for(n_points, 256), n_levels);
-    switch (mode) {
-        case 0:
-            hipLaunchKernelGGL(hash_encode_bwd_kernel<0>, grid, dim3(256), 0, as_stream(stream), d_xyz, n_points, hp,
-                               d_dfeat, feat_stride_point, feat_stride_level);
-            break;
-        case 1:
-            hipLaunchKernelGGL(hash_encode_bwd_kernel<1>, grid, dim3(256), 0, as_stream(stream), d_xyz, n_points, hp,
-                               d_dfeat, feat_stride_point, feat_stride_level);
-            break;
-        case 2:
-            hipLaunchKernelGGL(hash_encode_bwd_kernel<2>, grid, dim3(256), 0, as_stream(stream), d_xyz, n_points, hp,
-                               d_dfeat, feat_stride_point, feat_stride_level);
-            break;
-        default:
-            hipLaunchKernelGGL(hash_encode_bwd_kernel<3>, grid, dim3(256), 0, as_stream(stream), d_xyz, n_points, hp,
-                               d_dfeat, feat_stride_point, feat_stride_level);
-            NERF_CHECK_LAUNCH("hash_encode_bwd (bin)");
-            if (owner_variant() == 1)
-                hipLaunchKernelGGL((hash_bwd_owner_kernel<13, 1024>), dim3(1u << B.owner_log2, n_levels), dim3(1024),
-                                   0, as_stream(stream), hp);
-            else
-                hipLaunchKernelGGL((hash_bwd_owner_kernel<12, 512>), dim3(1u << B.owner_log2, n_levels), dim3(512), 0,
-                                   as_stream(stream), hp);
-            break;
+    if (mode == 1) {
+        hipLaunchKernelGGL(hash_encode_bwd_kernel<1>, grid, dim3(256), 0, as_stream(stream), d_xyz, n_points, hp,
+                           d_dfeat, feat_stride_point, feat_stride_level);
+    } else {
+        hipLaunchKernelGGL(hash_encode_bwd_kernel<3>, grid, dim3(256), 0, as_stream(stream), d_xyz, n_points, hp,
+                           d_dfeat, feat_stride_point, feat_stride_level);
+        NERF_CHECK_LAUNCH("hash_encode_bwd (bin)");
+        hipLaunchKernelGGL((hash_bwd_owner_kernel<kSliceLog2, 1024>), dim3(1u << B.owner_log2, n_levels), dim3(1024), 0,
+                           as_stream(stream), hp);
     }
     NERF_CHECK_LAUNCH("hash_encode_bwd");
     return NERF_OK;
@@ -755,12 +634,8 @@ extern "C" int nerf_hash_encode_bwd_owner(int n_levels, int log2_T, int64_t n_ch
     }
     if (n_chunks == 0) return NERF_OK;
     hp.nchunks = (int)n_chunks;
-    if (owner_variant() == 1)
-        hipLaunchKernelGGL((hash_bwd_owner_kernel<13, 1024>), dim3(1u << hp.owner_log2, n_levels), dim3(1024), 0,
-                           as_stream(stream), hp);
-    else
-        hipLaunchKernelGGL((hash_bwd_owner_kernel<12, 512>), dim3(1u << hp.owner_log2, n_levels), dim3(512), 0,
-                           as_stream(stream), hp);
+    hipLaunchKernelGGL((hash_bwd_owner_kernel<kSliceLog2, 1024>), dim3(1u << hp.owner_log2, n_levels), dim3(1024), 0,
+                       as_stream(stream), hp);
     NERF_CHECK_LAUNCH("hash_encode_bwd_owner");
     return NERF_OK;
 }

@@ -43,21 +43,28 @@ def shard(t, rank, world, dim=0):
     return t.narrow(dim, rank * step, step)
 
 
-class GradArena:
-    """One flat fp32 buffer holding the .grad of every parameter (views), in parameter order."""
+_ALIGN = 64      # elements: every rank's shard starts on a 256-B boundary (vectorised RAdam)
 
-    def __init__(self, params):
+
+class GradArena:
+    """One flat fp32 buffer holding the .grad of every parameter (views), in parameter order.
+    pad_to: round the buffer up to a multiple of this many elements (the sharded optimizer needs
+    world x _ALIGN) — the tail is never a gradient and stays zero."""
+
+    def __init__(self, params, pad_to=1):
         # quantizer scalars (soft_bits, range_scale, v_max) never receive a gradient in the
         # reference (their uses are detached): they keep grad None, so the optimizer skips them
         self.params = [p for p in params if p.requires_grad and not getattr(p, "_nerf_no_grad", False)]
-        total = sum(p.numel() for p in self.params)
+        self.numel = sum(p.numel() for p in self.params)
+        total = -(-self.numel // pad_to) * pad_to
         dev = self.params[0].device
         self.flat = torch.zeros(total, device=dev, dtype=torch.float32)
-        self.views = []
+        self.views, self.offsets = [], []
         off = 0
         for p in self.params:
             v = self.flat[off:off + p.numel()].view_as(p)
             self.views.append(v)
+            self.offsets.append(off)
             off += p.numel()
         self.attach()
 
@@ -73,8 +80,152 @@ class GradArena:
         world = dist.get_world_size(group) if dist.is_initialized() else 1
         if world == 1:
             return
-        dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=group)
-        self.flat.mul_(1.0 / world)
+        h = _staged(self.flat)
+        dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
+        h.mul_(1.0 / world)
+        if h is not self.flat:
+            self.flat.copy_(h)
+
+
+def _world():
+    return dist.get_world_size() if (dist.is_available() and dist.is_initialized()) else 1
+
+
+def _staged(t):
+    """gloo collectives run on host memory: stage a device tensor through the CPU (rehearsals and
+    tests only; 'nccl' = RCCL works on the device tensor itself)."""
+    return t.cpu() if (t.is_cuda and dist.get_backend() == "gloo") else t
+
+
+def _capturing(t):
+    return t.is_cuda and torch.cuda.is_current_stream_capturing()
+
+
+def allreduce_calibration_stats(stats):
+    """A-CAQ calibration statistics [n, 2] int32 = order-preserving uint32 images of (min, max)
+    (quantization.new_stats): the elementwise MIN / MAX over ranks, in place, so that every rank
+    calibrates its quantizers on the statistics of the global batch and the replicas stay equal
+    (quantization.py:97-119 run on one process's batch). No-op for a single process."""
+    if _world() == 1 or _capturing(stats):
+        return stats
+    u = _staged(stats).to(torch.int64) & 0xFFFFFFFF          # the uint32 order, exactly, in int64
+    lo, hi = u[:, 0].contiguous(), u[:, 1].contiguous()
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+    out = torch.stack([lo, hi], 1)
+    out = torch.where(out >= 1 << 31, out - (1 << 32), out).to(torch.int32)
+    stats.copy_(out.to(stats.device))
+    return stats
+
+
+def allreduce_mean_(t):
+    """In-place mean over ranks of a small device tensor (the A-CAQ controller's img_loss)."""
+    if _world() == 1 or _capturing(t):
+        return t
+    s = _staged(t)
+    dist.all_reduce(s, op=dist.ReduceOp.SUM)
+    s.mul_(1.0 / _world())
+    if s is not t:
+        t.copy_(s)
+    return t
+
+
+def shard_ranges(offsets, sizes, lo, hi):
+    """Per parameter (flat offset, size): the part of [lo, hi) it holds, as a local element range
+    (a, b), or None. The ranges of all ranks tile every parameter exactly once."""
+    out = []
+    for off, n in zip(offsets, sizes):
+        a, b = max(lo, off), min(hi, off + n)
+        out.append((a - off, b - off) if b > a else None)
+    return out
+
+
+class ShardedOptimizer:
+    """Optimizer-state sharding for data parallelism (ZeRO stage 1).
+
+    The parameters become views of one flat fp32 buffer laid out like the GradArena, padded to a
+    multiple of world x _ALIGN, and rank r owns the contiguous range [r N/G, (r+1) N/G) of it.
+    Per iteration, instead of an all-reduce of the gradients and a dense RAdam pass over all 16.8 M
+    elements on every rank:
+      reduce_grads()   reduce-scatter (sum) of the gradient buffer into this rank's shard, x 1/G
+      optimizer.step() RAdam on the shard only (the HIP kernel on sub-ranges of the tensors)
+      gather_params()  all-gather of the updated parameter shards into every replica
+    The collective bytes equal one all-reduce; the dense optimizer traffic drops by G. Elementwise
+    RAdam on a shard is bit-identical to RAdam on the whole tensor (tests/test_gpu_dist.py).
+    Exp_avg / exp_avg_sq are valid on the rank's own shard only; consolidate_state() assembles
+    them for a checkpoint (model.save_checkpoint)."""
+
+    def __init__(self, optimizer, arena, group=None):
+        self.opt, self.arena, self.group = optimizer, arena, group
+        self.world = dist.get_world_size(group) if (dist.is_available() and dist.is_initialized()) else 1
+        self.rank = dist.get_rank(group) if self.world > 1 else 0
+        n_flat = arena.flat.numel()
+        if n_flat % (self.world * _ALIGN):
+            raise ValueError("ShardedOptimizer: build the GradArena with pad_to=world*64")
+        dev = arena.flat.device
+        # parameters as views of one flat buffer (same layout as the gradients)
+        self.pflat = torch.zeros(n_flat, device=dev, dtype=torch.float32)
+        with torch.no_grad():
+            for p, off in zip(arena.params, arena.offsets):
+                view = self.pflat[off:off + p.numel()].view_as(p)
+                view.copy_(p.data)
+                p.data = view
+        arena.attach()
+        self.count = n_flat // self.world
+        self.lo, self.hi = self.rank * self.count, (self.rank + 1) * self.count
+        self.gshard = torch.zeros(self.count, device=dev, dtype=torch.float32)
+        ranges = shard_ranges(arena.offsets, [p.numel() for p in arena.params], self.lo, self.hi)
+        shard = {}
+        for p, off, r in zip(arena.params, arena.offsets, ranges):
+            if r is not None:
+                a, b = r
+                shard[p] = (a, b, self.gshard[off + a - self.lo:off + b - self.lo])
+        self.ranges = ranges
+        optimizer.set_shard(shard if self.world > 1 else None)
+
+    def reduce_grads(self):
+        """Reduce-scatter of the gradient arena: this rank's shard of the mean gradient."""
+        if self.world == 1:
+            return
+        flat = self.arena.flat
+        if dist.get_backend(self.group) == "gloo":      # no reduce-scatter in gloo: all-reduce + slice
+            h = flat.cpu()
+            dist.all_reduce(h, op=dist.ReduceOp.SUM, group=self.group)
+            self.gshard.copy_(h[self.lo:self.hi].to(self.gshard.device))
+        else:
+            dist.reduce_scatter_tensor(self.gshard, flat, op=dist.ReduceOp.SUM, group=self.group)
+        self.gshard.mul_(1.0 / self.world)
+
+    def gather_params(self):
+        """All-gather of the updated parameter shards (in place: the shard is a view of the output)."""
+        if self.world == 1:
+            return
+        if dist.get_backend(self.group) == "gloo":
+            parts = [torch.empty(self.count) for _ in range(self.world)]
+            dist.all_gather(parts, self.pflat[self.lo:self.hi].cpu(), group=self.group)
+            self.pflat.copy_(torch.cat(parts).to(self.pflat.device))
+        else:
+            dist.all_gather_into_tensor(self.pflat, self.pflat[self.lo:self.hi], group=self.group)
+        for p in self.arena.params:       # the collective wrote the parameters in place
+            torch.autograd.graph.increment_version(p)
+
+    def consolidate_state(self):
+        """Every rank's exp_avg / exp_avg_sq shards summed into full tensors on every rank (each
+        element is owned by exactly one rank; the others contribute zeros)."""
+        if self.world == 1:
+            return
+        for p, r in zip(self.arena.params, self.ranges):
+            st = self.opt.state.get(p)
+            if not st:
+                continue
+            for key in ("exp_avg", "exp_avg_sq"):
+                t = st[key]
+                mine = torch.zeros_like(t).view(-1)
+                if r is not None:
+                    mine[r[0]:r[1]] = t.view(-1)[r[0]:r[1]]
+                h = _staged(mine)
+                dist.all_reduce(h, op=dist.ReduceOp.SUM, group=self.group)
+                t.view(-1).copy_(h.to(t.device))
 
 
 def broadcast_params(params, src=0):
@@ -82,4 +233,7 @@ def broadcast_params(params, src=0):
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return
     for p in params:
-        dist.broadcast(p.data, src=src)
+        h = _staged(p.data)
+        dist.broadcast(h, src=src)
+        if h is not p.data:
+            p.data.copy_(h)

@@ -90,12 +90,14 @@ class StepScalars:
 
 class GraphedTrainStep:
     """train_step (model.py) as two captured graphs (forward + backward, RAdam) plus the eager
-    grad hook between them (the DP all-reduce stays outside the graphs). Call it like
+    grad hook between them and the post hook after the second (the DP collectives stay outside the
+    graphs). Call it like
     train_step(...) with the same arguments every iteration; it runs `warmup` eager iterations
     before the first capture (allocations, optimizer state, quantizer calibration)."""
 
     def __init__(self, batch_rays, target_s, render_kwargs_train, optimizer, args, H=0, W=0, K=None,
-                 grad_hook=None, loss_scale_sparsity=1.0, tv_generator=None, zero_grad=None, warmup=2):
+                 grad_hook=None, loss_scale_sparsity=1.0, tv_generator=None, zero_grad=None, warmup=2,
+                 post_hook=None):
         self.rays, self.target = batch_rays, target_s
         self.kw, self.opt, self.args = render_kwargs_train, optimizer, args
         self.H, self.W, self.K = H, W, K
@@ -105,6 +107,7 @@ class GraphedTrainStep:
             arena = GradArena([p for g in optimizer.param_groups for p in g["params"]])
             zero_grad = arena.zero_
         self.hook, self.scale_sp, self.tv_gen, self.zero_grad = grad_hook, loss_scale_sparsity, tv_generator, zero_grad
+        self.post_hook = post_hook
         self.warmup = warmup
         self.eager_steps = 0
         self.key = None
@@ -161,7 +164,7 @@ class GraphedTrainStep:
         from .model import train_step
         return train_step(self.rays, self.target, self.kw, self.opt, self.args, global_step, H=self.H, W=self.W,
                           K=self.K, grad_hook=self.hook, loss_scale_sparsity=self.scale_sp,
-                          tv_generator=self.tv_gen, zero_grad=self.zero_grad)
+                          tv_generator=self.tv_gen, zero_grad=self.zero_grad, post_hook=self.post_hook)
 
     def _priors_active(self, global_step):
         from .model import DEFAULTS
@@ -195,6 +198,8 @@ class GraphedTrainStep:
         self.graphs[1].replay()
         for p in self.params:              # the replayed RAdam wrote the parameters in place
             torch.autograd.graph.increment_version(p)
+        if self.post_hook is not None:
+            self.post_hook()
         loss, img_loss, psnr = self.out
         acaq_update(global_step, img_loss, self.kw, self.args)
         lr_schedule(self.opt, self.args, global_step)

@@ -75,6 +75,11 @@ class HashEncodeFn(torch.autograd.Function):
 
 
 _BWD_WORKSPACE = {}
+# Workspaces replaced by a larger one are never freed: a HIP graph captured earlier (graphs.
+# GraphedTrainStep) keeps their addresses in its kernel arguments, and the caching allocator would
+# hand the memory to someone else before the next replay. They are kept alive here instead (the
+# workspace only grows, so this holds a few buffers at most).
+_RETIRED = []
 
 
 def bwd_workspace(n_levels, log2_T, n_points, device):
@@ -87,7 +92,9 @@ def bwd_workspace(n_levels, log2_T, n_points, device):
     key = str(device)
     hit = _BWD_WORKSPACE.get(key)
     if hit is None or hit[1] < need:
-        _BWD_WORKSPACE.pop(key, None)
+        old = _BWD_WORKSPACE.pop(key, None)
+        if old is not None:
+            _RETIRED.append(old[0])
         hit = _BWD_WORKSPACE[key] = (torch.empty(need, dtype=torch.uint8, device=device), need)
     return hit
 
@@ -129,7 +136,8 @@ class _PendingBins:
             cap = max(self.peak, n_ch)
             need = int(lib.nerf_hash_encode_bwd_workspace_bytes(L, log2_T, 256 * cap))
             if self.ws is None or self.ws.numel() < need:
-                self.ws = None
+                if self.ws is not None:
+                    _RETIRED.append(self.ws)     # a captured graph may still bin into it
                 self.ws = torch.empty(need, dtype=torch.uint8, device=xyz.device)
             self.cap = cap
             self.tag, self.grads, self.stream = tag, list(grad_tables), torch.cuda.current_stream()

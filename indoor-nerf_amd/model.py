@@ -99,8 +99,11 @@ def create_nerf(args, device=None):
     return render_kwargs_train, render_kwargs_test, start, grad_vars, optimizer
 
 
-def save_checkpoint(path, global_step, render_kwargs_train, optimizer):
-    """The reference's checkpoint dict (run_nerf.py:1345-1362)."""
+def save_checkpoint(path, global_step, render_kwargs_train, optimizer, sharded=None):
+    """The reference's checkpoint dict (run_nerf.py:1345-1362). With a dist.ShardedOptimizer, its
+    per-rank moment shards are first assembled into full tensors on every rank."""
+    if sharded is not None:
+        sharded.consolidate_state()
     fine = render_kwargs_train["network_fine"]
     torch.save({"global_step": global_step,
                 "network_fn_state_dict": render_kwargs_train["network_fn"].state_dict(),
@@ -144,7 +147,9 @@ def acaq_update(i, img_loss, render_kwargs_train, args):
         emb._acaq_best = torch.full((1,), float("nan"), dtype=torch.float64, device=dev)
     report = torch.empty(2, dtype=torch.float64, device=dev)
     tm = get("target_metric", None)
-    loss32 = img_loss.detach().reshape(()).float().contiguous()
+    loss32 = img_loss.detach().reshape(()).float().contiguous().clone()
+    from .dist import allreduce_mean_
+    allreduce_mean_(loss32)        # DP: every replica's controller sees the global batch's loss
     _lib.call("nerf_acaq_update", _descriptors(qs), len(qs), _lib.ptr(loss32, "img_loss"),
               _lib.ptr(emb._acaq_best, "best_loss", dtype=torch.float64), int(tm is not None),
               float(tm) if tm is not None else 0.0, float(get("bit_penalty", 1e-3)),
@@ -232,11 +237,13 @@ def lr_schedule(optimizer, args, global_step):
 
 
 def train_step(batch_rays, target_s, render_kwargs_train, optimizer, args, global_step, H=0, W=0, K=None,
-               grad_hook=None, loss_scale_sparsity=1.0, tv_generator=None, zero_grad=None, spatial_coords=None):
+               grad_hook=None, loss_scale_sparsity=1.0, tv_generator=None, zero_grad=None, spatial_coords=None,
+               post_hook=None):
     """One iteration of train() without host bookkeeping: render (coarse+fine), img/img0 MSE,
-    sparsity, TV (run_nerf.py:1007-1037), backward, [grad_hook, e.g. DP all-reduce], RAdam step,
-    A-CAQ bit widths, lr decay (:1182-1250, :1289-1293). Returns (loss, psnr) as device tensors
-    (no host sync). graphs.GraphedTrainStep replays the same iteration from HIP graphs."""
+    sparsity, TV (run_nerf.py:1007-1037), backward, [grad_hook, e.g. DP all-reduce or reduce-scatter],
+    RAdam step, [post_hook, e.g. the sharded optimizer's parameter all-gather], A-CAQ bit widths,
+    lr decay (:1182-1250, :1289-1293). Returns (loss, psnr) as device tensors (no host sync).
+    graphs.GraphedTrainStep replays the same iteration from HIP graphs."""
     loss, img_loss, psnr = forward_backward(batch_rays, target_s, render_kwargs_train, optimizer, args, global_step,
                                             H=H, W=W, K=K, loss_scale_sparsity=loss_scale_sparsity,
                                             tv_generator=tv_generator, zero_grad=zero_grad,
@@ -244,6 +251,8 @@ def train_step(batch_rays, target_s, render_kwargs_train, optimizer, args, globa
     if grad_hook is not None:
         grad_hook()
     optimizer_update(optimizer)
+    if post_hook is not None:
+        post_hook()
     acaq_update(global_step, img_loss, render_kwargs_train, args)
     lr_schedule(optimizer, args, global_step)
     return loss.detach(), psnr.detach()

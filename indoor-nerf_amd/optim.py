@@ -32,6 +32,15 @@ class RAdam(Optimizer):
         defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay,
                         buffer=[[None, None, None] for _ in range(10)])
         super().__init__(params, defaults)
+        self.shard = None
+
+    def set_shard(self, shard):
+        """Data-parallel optimizer sharding (dist.ShardedOptimizer): `shard` maps a parameter to the
+        (start, end, grad) element range this rank updates, `grad` a flat fp32 tensor of end - start
+        reduced gradients (the rank's reduce-scatter output) or None for p.grad[start:end];
+        parameters missing from the map are not updated here (their step count still advances, as
+        on the rank that owns them). None = every element of every parameter (the default)."""
+        self.shard = shard
 
     def _scalars(self, group, step):
         beta1, beta2 = group["betas"]
@@ -54,15 +63,27 @@ class RAdam(Optimizer):
             buffered[2] = step_size
         return n_sma, step_size
 
-    def _segment(self, group, p, mode, step_size):
+    def _range(self, p):
+        """(start, end, grad pointer) of the elements of p this rank updates, or None."""
+        if self.shard is None:
+            return 0, p.numel(), _lib.ptr(p.grad, "grad").value
+        r = self.shard.get(p)
+        if r is None or r[1] <= r[0]:
+            return None
+        a, b, g = r
+        gp = _lib.ptr(g, "grad_shard").value if g is not None else p.grad.data_ptr() + 4 * a
+        return a, b, gp
+
+    def _segment(self, group, p, mode, step_size, rng=None):
         beta1, beta2 = group["betas"]
         state = self.state[p]
+        a, b, gp = rng if rng is not None else (0, p.numel(), _lib.ptr(p.grad, "grad").value)
         s = _lib.RAdamSegment()
-        s.p = _lib.ptr(p, "param").value
-        s.g = _lib.ptr(p.grad, "grad").value
-        s.m = _lib.ptr(state["exp_avg"], "exp_avg").value
-        s.v = _lib.ptr(state["exp_avg_sq"], "exp_avg_sq").value
-        s.n = p.numel()
+        s.p = _lib.ptr(p, "param").value + 4 * a
+        s.g = gp
+        s.m = _lib.ptr(state["exp_avg"], "exp_avg").value + 4 * a
+        s.v = _lib.ptr(state["exp_avg_sq"], "exp_avg_sq").value + 4 * a
+        s.n = b - a
         s.beta1, s.beta2 = beta1, beta2
         s.one_minus_beta1, s.one_minus_beta2 = 1 - beta1, 1 - beta2
         s.eps = group["eps"]
@@ -115,7 +136,10 @@ class RAdam(Optimizer):
         segs, updated = [], []
         for group, p in self._params():
             mode, step_size = self._advance(group, p)
-            segs.append(self._segment(group, p, mode, step_size))
+            rng = self._range(p)
+            if rng is None:
+                continue
+            segs.append(self._segment(group, p, mode, step_size, rng))
             updated.append(p)
         for i in range(0, len(segs), _MAX_SEGS):
             chunk = segs[i:i + _MAX_SEGS]
@@ -131,11 +155,18 @@ class RAdam(Optimizer):
         """Captured in a HIP graph (graphs.GraphedTrainStep): the launch reads (decay_coef,
         step_coef, mode) of each tensor from device slots that a filler computes before every
         replay with the same host algebra (state['step'] advances there, not at capture)."""
-        pairs = list(self._params())
+        every = list(self._params())
+        pairs = [(g, p) for g, p in every if self._range(p) is not None]
+        others = [(g, p) for g, p in every if self._range(p) is None]
+        if others:
+            def advance(hi, hf, others=others):     # parameters another rank updates: step count only
+                for g, p in others:
+                    self._advance(g, p)
+            sc.add_filler(advance)
         for i in range(0, len(pairs), _MAX_SEGS):
             chunk = pairs[i:i + _MAX_SEGS]
             off, dptr = sc.alloc_f32(4 * len(chunk))
-            segs = [self._segment(g, p, 2, 0.0) for g, p in chunk]
+            segs = [self._segment(g, p, 2, 0.0, self._range(p)) for g, p in chunk]
             arr = (_lib.RAdamSegment * len(chunk))(*segs)
             _lib.call("nerf_radam_step", arr, len(chunk), _lib.c_vp(dptr), _lib.stream())
 

@@ -85,7 +85,11 @@ def new_stats(n, device):
 
 
 def calibrate_from_stats(quantizers, stats):
-    """calibrate() (quantization.py:97-119) of each quantizer from its (min, max) row of `stats`."""
+    """calibrate() (quantization.py:97-119) of each quantizer from its (min, max) row of `stats`.
+    Under data parallelism the statistics are first reduced over ranks (dist.py), so every replica
+    calibrates identically."""
+    from .dist import allreduce_calibration_stats
+    allreduce_calibration_stats(stats)
     _lib.call("nerf_quant_calibrate", _descriptors(quantizers), len(quantizers),
               _lib.ptr(stats, "stats", dtype=torch.int32), _lib.stream())
     for q in quantizers:

@@ -8,7 +8,7 @@
  *   HashEmbedder.forward PocketNeRF/hash_encoding.py:82-107
  * Compiled by __graft_entry__.build() with gcc -O2 -ffp-contract=off (no FMA contraction) into
  * oracle/_build/libhashgrid_ref.so; pinned against tests/golden/f2_voxel.npz and f3_hash_fwd.npz by
- * tests/test_oracle_c.py. Only tests and bench.py's cpu_baseline may load it.
+ * tests/test_abi.py. Only tests and bench.py's cpu_baseline may load it.
  */
 #include <math.h>
 #include <stdint.h>

@@ -83,3 +83,101 @@ def test_shard_layout():
         pass
     else:
         raise AssertionError("uneven shard must raise")
+
+
+def test_shard_ranges_tile_every_parameter():
+    from indoor_nerf_amd.dist import shard_ranges
+    sizes = [2048, 1024, 1984, 4096, 192, 1 << 12, 1 << 12, 5]
+    offsets = list(np.cumsum([0] + sizes[:-1]))
+    total = sum(sizes)
+    for world in (1, 2, 3, 8):
+        count = -(-total // world)
+        covered = [np.zeros(n, np.int32) for n in sizes]
+        for r in range(world):
+            for i, rg in enumerate(shard_ranges(offsets, sizes, r * count, (r + 1) * count)):
+                if rg is not None:
+                    covered[i][rg[0]:rg[1]] += 1
+        assert all((c == 1).all() for c in covered), world
+
+
+class _SgdShard:
+    """Stand-in for RAdam.set_shard/step on CPU: p[a:b] -= 0.5 * grad shard."""
+
+    def __init__(self, params):
+        self.params, self.shard = params, None
+
+    def set_shard(self, shard):
+        self.shard = shard
+
+    def step(self):
+        with torch.no_grad():
+            for p in self.params:
+                if self.shard is None:
+                    p.view(-1).sub_(0.5 * p.grad.view(-1))
+                elif p in self.shard:
+                    a, b, g = self.shard[p]
+                    p.view(-1)[a:b].sub_(0.5 * g)
+
+
+def _zero_worker(rank, world, port, out_dir):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from indoor_nerf_amd.dist import (GradArena, ShardedOptimizer, allreduce_calibration_stats, allreduce_mean_,
+                                      init_process_group)
+    init_process_group(backend="gloo")
+    g = torch.Generator().manual_seed(0)
+    params = [torch.nn.Parameter(torch.randn(n, generator=g)) for n in (300, 77, 1024, 5)]
+    opt = _SgdShard(params)
+    arena = GradArena(params, pad_to=world * 64)
+    sh = ShardedOptimizer(opt, arena)
+    for step in range(3):
+        arena.zero_()
+        gr = torch.Generator().manual_seed(10 * step + rank)
+        for p in params:
+            p.grad.copy_(torch.randn(p.shape, generator=gr))
+        sh.reduce_grads()
+        opt.step()
+        sh.gather_params()
+    np.save(os.path.join(out_dir, f"p_{rank}.npy"), torch.cat([p.detach().view(-1) for p in params]).numpy())
+    # A-CAQ calibration statistics: order-preserving uint32 images of (min, max) in int32
+    vals = torch.tensor([[-3.0 + rank, 2.0 * rank], [0.5 * rank, -1.0 - rank]])
+
+    def f2ord(x):
+        u = x.view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+        u = torch.where(u >= 1 << 31, (~u) & 0xFFFFFFFF, u | (1 << 31))
+        return torch.where(u >= 1 << 31, u - (1 << 32), u).to(torch.int32)
+    st = torch.stack([f2ord(vals[:, 0]), f2ord(vals[:, 1])], 1)
+    allreduce_calibration_stats(st)
+    np.save(os.path.join(out_dir, f"st_{rank}.npy"), st.numpy())
+    m = torch.tensor([1.0 + rank])
+    allreduce_mean_(m)
+    np.save(os.path.join(out_dir, f"m_{rank}.npy"), m.numpy())
+    dist.destroy_process_group()
+
+
+def test_sharded_optimizer_gloo(tmp_path):
+    world = 2
+    mp.start_processes(_zero_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    p0, p1 = np.load(tmp_path / "p_0.npy"), np.load(tmp_path / "p_1.npy")
+    np.testing.assert_array_equal(p0, p1)
+    # single-process reference: full update with the mean gradient
+    g = torch.Generator().manual_seed(0)
+    params = [torch.randn(n, generator=g) for n in (300, 77, 1024, 5)]
+    for step in range(3):
+        grads = []
+        for r in range(world):
+            gr = torch.Generator().manual_seed(10 * step + r)
+            grads.append([torch.randn(p.shape, generator=gr) for p in params])
+        for i, p in enumerate(params):
+            p.sub_(0.5 * ((grads[0][i] + grads[1][i]) * 0.5))
+    np.testing.assert_array_equal(p0, torch.cat(params).numpy())
+    # calibration statistics: elementwise min of mins, max of maxes over the ranks
+    for r in range(world):
+        st = np.load(tmp_path / f"st_{r}.npy").astype(np.int64) & 0xFFFFFFFF
+        u = np.where(st >= 1 << 31, st & 0x7FFFFFFF, (~st) & 0xFFFFFFFF).astype(np.uint32).view(np.float32)
+        np.testing.assert_array_equal(u, np.array([[-3.0, 2.0], [0.0, -1.0]], np.float32))
+        np.testing.assert_allclose(np.load(tmp_path / f"m_{r}.npy"), [1.5])

@@ -102,3 +102,38 @@ def test_timing_refused_inside_capture(nerf, gpu):
             st(2)
     finally:
         _lib.set_timing(False)
+
+
+def test_graph_replay_after_workspace_growth(nerf, gpu):
+    """A captured iteration keeps the hash backward's bin workspace address in its kernel arguments:
+    a larger eager backward in between grows the workspace, and the old one must stay valid (it is
+    retired, never freed). Deterministic configuration (perturb 0, no TV): the replayed backward's
+    gradients equal an eager backward's at the same parameters up to fp32 atomics order."""
+    from indoor_nerf_amd.graphs import GraphedTrainStep
+    from indoor_nerf_amd.model import forward_backward
+    args, kw, opt, rays, target, params, arena = _setup(nerf, gpu, R=512)
+    kw["perturb"] = 0.0
+    args.tv_loss_weight = 0.0
+    st = GraphedTrainStep(rays, target, kw, opt, args, zero_grad=arena.zero_)
+    for it in range(1, 5):
+        st(it)
+    assert st.captures == 1
+    # a 16x larger eager backward: the bin workspace grows past the captured one
+    ro, rd = synthetic_rays(8192, seed=33)
+    big = (torch.from_numpy(ro).to(gpu), torch.from_numpy(rd).to(gpu))
+    big_t = torch.rand(8192, 3, device=gpu)
+    forward_backward(big, big_t, kw, opt, args, 5, zero_grad=arena.zero_)
+    junk = [torch.full((1 << 26,), 1e30, device=gpu) for _ in range(8)]   # grab freed blocks
+    torch.cuda.synchronize()
+    st.scalars.upload()
+    st.graphs[0].replay()
+    torch.cuda.synchronize()
+    g_graph = arena.flat.clone()
+    forward_backward(rays, target, kw, opt, args, 6, zero_grad=arena.zero_)
+    torch.cuda.synchronize()
+    g_eager = arena.flat.clone()
+    del junk
+    assert torch.isfinite(g_graph).all()
+    scale = float(g_eager.abs().max())
+    assert scale > 0
+    assert float((g_graph - g_eager).abs().max()) <= 1e-4 * scale

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""One MLP generation (NERF_MLP env), fwd+bwd on the lego fine pass, a few reps: a short target for
+"""The default MLP kernels, fwd+bwd on the lego fine pass, a few reps: a short target for
 rocprofv3 PMC passes (tools/pmc_mlp.sh)."""
 import os
 import sys
