@@ -45,7 +45,7 @@ OPS = {
     "hash_bwd": dict(calls=("nerf_hash_encode_bwd_bin", "nerf_hash_encode_bwd_owner", "nerf_hash_encode_bwd_ws",
                             "nerf_hash_encode_bwd"), bound="hbm", per_unit=2 * 16 * 8 * 8 + 12 + 128, unit="point"),
     "hash_fwd": dict(calls=("nerf_hash_encode_fwd",), bound="hbm", per_unit=16 * 8 * 8 + 12 + 128 + 1, unit="point"),
-    "mlp_bwd": dict(calls=("nerf_mlp_bwd",), bound="mfma", per_unit=2 * 18688, unit="point"),
+    "mlp_bwd": dict(calls=("nerf_mlp_bwd", "nerf_mlp_bwd_batch"), bound="mfma", per_unit=2 * 18688, unit="point"),
     "mlp_fwd": dict(calls=("nerf_mlp_fwd",), bound="mfma", per_unit=18688, unit="point"),
     "composite_fwd": dict(calls=("nerf_composite_fwd",), bound="hbm", per_unit=24, unit="sample"),
     "composite_bwd": dict(calls=("nerf_composite_bwd",), bound="hbm", per_unit=40, unit="sample"),
@@ -66,6 +66,7 @@ KERNEL_SYMBOLS = {
     "nerf_hash_encode_bwd_owner": ["nerf::hash_bwd_owner_kernel<13, 1024>"],
     "nerf_mlp_fwd": ["nerf::mlp_fwd_x6_kernel<false>"],
     "nerf_mlp_bwd": ["nerf::mlp_bwd_x6cg_kernel<false>"],
+    "nerf_mlp_bwd_batch": ["nerf::mlp_bwd_x6cg_kernel<false>"],
     "nerf_radam_step": ["nerf::radam_kernel"],
 }
 TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r02_traffic.json")

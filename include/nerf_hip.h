@@ -39,6 +39,13 @@ extern "C" {
 const char* nerf_last_error(void);
 int nerf_abi_version(void);
 
+/* ---- numerical check (render_rays' DEBUG test, run_nerf.py:545-547) ----------------------------
+ * d_counts[t] = number of NaN/Inf values among the sizes[t] floats at d_ptrs[t] (host arrays of
+ * n_tensors <= NERF_MAX_CHECK entries; d_counts device int[n_tensors], overwritten). */
+#define NERF_MAX_CHECK 32
+int nerf_count_nonfinite(const float* const* d_ptrs, const int64_t* sizes, int n_tensors, int* d_counts,
+                         void* stream);
+
 /* ---- multi-resolution hash grid -------------------------------------------------------------
  * Replaces HashEmbedder.forward (PocketNeRF/hash_encoding.py:82-107) = per level
  * get_voxel_vertices + hash (utils.py:95-117, :13-24), nn.Embedding gather (hash_encoding.py:94)
@@ -76,40 +83,49 @@ int nerf_hash_encode_bwd(const float* d_xyz, int64_t n_points,
                          float* const* d_dtables, void* stream);
 
 /* Same, on the binned ("owner computes") path: the entries are first written, sorted by table
- * slice, into a caller-owned device workspace (plain stores), then one workgroup per 2^13-row slice
+ * slice, into a caller-owned device workspace (plain stores), then one workgroup per table slice
  * sums them in LDS and adds the slice into d_dtables once. Replaces the memory-side float atomics
  * of nerf_hash_encode_bwd, whose request rate bounds that path. The workspace needs no
  * initialisation; calls sharing one must be stream-ordered. workspace_bytes >=
- * nerf_hash_encode_bwd_workspace_bytes(n_levels, log2_T, n_points) (0: path unavailable for this
- * log2_T, and a NULL workspace gives nerf_hash_encode_bwd). */
-size_t nerf_hash_encode_bwd_workspace_bytes(int n_levels, int log2_T, int64_t n_points);
+ * nerf_hash_encode_bwd_workspace_bytes(n_levels, log2_T, n_points, deterministic) (0: path
+ * unavailable for this log2_T; a NULL workspace gives nerf_hash_encode_bwd, which is never
+ * deterministic).
+ * deterministic != 0: SURVEY.md §8(b)'s `deterministic` flag. The owner pass sums in exact
+ * integer fixed point (two int64 words per value at a per-level scale from the level's largest
+ * entry; ~2^-75 of that entry per term), which is associative, so identical inputs give
+ * bit-identical gradients whatever the scheduling. Needs log2_T <= 19 (2^12-row slices). */
+size_t nerf_hash_encode_bwd_workspace_bytes(int n_levels, int log2_T, int64_t n_points, int deterministic);
 int nerf_hash_encode_bwd_ws(const float* d_xyz, int64_t n_points,
                             const float* bbox_min3, const float* bbox_max3,
                             const float* level_res, int n_levels, int log2_T,
                             const float* d_dfeat, int64_t feat_stride_point, int64_t feat_stride_level,
-                            float* const* d_dtables, void* d_workspace, size_t workspace_bytes, void* stream);
+                            float* const* d_dtables, int deterministic, void* d_workspace, size_t workspace_bytes,
+                            void* stream);
 
 /* The binned path split in two, so that several backwards into the same tables (the fine and the
  * coarse pass of one iteration: two autograd nodes of HashEmbedder.forward, hash_encoding.py:82-107)
  * share ONE owner pass. The workspace holds chunk_capacity 256-point chunks (workspace_bytes >=
- * nerf_hash_encode_bwd_workspace_bytes(n_levels, log2_T, 256 * chunk_capacity)); a bin call writes
- * its ceil(n_points / 256) chunks from chunk_base on, and the owner call sums chunks
+ * nerf_hash_encode_bwd_workspace_bytes(n_levels, log2_T, 256 * chunk_capacity, deterministic)); a
+ * bin call writes its ceil(n_points / 256) chunks from chunk_base on, and the owner call sums chunks
  * [0, n_chunks) into d_dtables (ACCUMULATED). Calls sharing a workspace must be stream-ordered and
- * use the same n_levels, log2_T and chunk_capacity. */
+ * use the same n_levels, log2_T, chunk_capacity and deterministic; the batch starts with the bin call
+ * at chunk_base 0. */
 int nerf_hash_encode_bwd_bin(const float* d_xyz, int64_t n_points,
                              const float* bbox_min3, const float* bbox_max3,
                              const float* level_res, int n_levels, int log2_T,
                              const float* d_dfeat, int64_t feat_stride_point, int64_t feat_stride_level,
-                             int64_t chunk_base, int64_t chunk_capacity,
+                             int64_t chunk_base, int64_t chunk_capacity, int deterministic,
                              void* d_workspace, size_t workspace_bytes, void* stream);
 int nerf_hash_encode_bwd_owner(int n_levels, int log2_T, int64_t n_chunks, int64_t chunk_capacity,
-                               float* const* d_dtables, void* d_workspace, size_t workspace_bytes, void* stream);
+                               float* const* d_dtables, int deterministic, void* d_workspace,
+                               size_t workspace_bytes, void* stream);
 
 /* ---- spherical harmonics, degree 4 (SHEncoder.forward, hash_encoding.py:153-191) ---------- */
 int nerf_sh4_fwd(const float* d_dirs, int64_t n, float* d_out /* [n,16] */, void* stream);
 
 /* ---- fused tiny MLP (NeRFSmall.forward, run_nerf_helpers.py:265-306, + run_network's
- *      sigma := 0 outside the bbox, run_nerf.py:66) on fp32 MFMA (v_mfma_f32_32x32x2_f32) -----
+ *      sigma := 0 outside the bbox, run_nerf.py:66), fp32-accurate on the bf16 matrix cores
+ *      (each fp32 operand split into three bf16 pieces, six v_mfma_f32_32x32x16_bf16 per product) -----
  * Weights are nn.Linear layouts [out][in], no bias: w0 [64,32], w1 [16,64], c0 [64,31],
  * c1 [64,64], c2 [3,64] (create_nerf's NeRFSmall(num_layers=2, num_layers_color=3)).
  * Input point p: hash features x[p][k] = d_feat[p*feat_stride_point + (k/2)*feat_stride_level + k%2]
@@ -172,6 +188,35 @@ int nerf_mlp_bwd_q(const float* d_feat, int64_t feat_stride_point, int64_t feat_
                    const nerf_mlp_weights* weights, const float* d_graw,
                    const nerf_mlp_grads* grads, float* d_dfeat, float* d_dsh, const float* d_dgeo,
                    const float* d_act_qrec, void* stream);
+
+/* Batched backward of up to NERF_MLP_MAX_JOBS nets in ONE launch (the coarse and the fine NeRFSmall
+ * of a training iteration: run_nerf.py:1007-1035 backpropagates both; the reference runs them as
+ * separate autograd subgraphs). Each job carries the arguments of nerf_mlp_bwd_q. Empty jobs are
+ * skipped. d_det_workspace (NULL = off; >= nerf_mlp_bwd_det_workspace_bytes()) selects the
+ * DETERMINISTIC mode: every block's weight-gradient partial sum is stored and reduced over blocks in
+ * a fixed order (no float atomics), so identical inputs give bit-identical gradients. */
+#define NERF_MLP_MAX_JOBS 2
+typedef struct {
+    const float* feat;
+    int64_t feat_stride_point, feat_stride_level;
+    const float* sh;
+    int64_t sh_stride;
+    const float* viewdirs;
+    int64_t samples_per_ray;
+    const uint8_t* keep;
+    int64_t n_points;
+    nerf_mlp_weights weights;
+    const float* graw;
+    nerf_mlp_grads grads;
+    float* dfeat;
+    float* dsh;
+    const float* dgeo;
+    const float* act_qrec;
+} nerf_mlp_bwd_job;
+
+size_t nerf_mlp_bwd_det_workspace_bytes(void);
+int nerf_mlp_bwd_batch(const nerf_mlp_bwd_job* jobs, int n_jobs, float* d_det_workspace,
+                       size_t det_workspace_bytes, void* stream);
 
 /* ---- normals head (run_nerf_helpers.py:259-263, :298-302): n = normalize(N1 relu(N0 geo + b0) + b1)
  * nn.Linear layouts: n0 [32,15], b0 [32], n1 [3,32], b1 [3].

@@ -29,6 +29,18 @@ class MlpGrads(ctypes.Structure):
     _fields_ = [(n, c_vp) for n in ("w0", "w1", "c0", "c1", "c2")]
 
 
+MLP_MAX_JOBS = 2   # NERF_MLP_MAX_JOBS
+MAX_CHECK = 32     # NERF_MAX_CHECK
+
+
+class MlpBwdJob(ctypes.Structure):
+    """nerf_mlp_bwd_job (include/nerf_hip.h): the arguments of nerf_mlp_bwd_q for one net."""
+    _fields_ = [("feat", c_vp), ("feat_stride_point", c_i64), ("feat_stride_level", c_i64), ("sh", c_vp),
+                ("sh_stride", c_i64), ("viewdirs", c_vp), ("samples_per_ray", c_i64), ("keep", c_vp),
+                ("n_points", c_i64), ("weights", MlpWeights), ("graw", c_vp), ("grads", MlpGrads), ("dfeat", c_vp),
+                ("dsh", c_vp), ("dgeo", c_vp), ("act_qrec", c_vp)]
+
+
 class NormalHead(ctypes.Structure):
     _fields_ = [("n0", c_vp), ("b0", c_vp), ("n1", c_vp), ("b1", c_vp)]
 
@@ -60,10 +72,11 @@ SIGNATURES = {
     "nerf_hash_encode_bwd": [c_vp, c_i64, c_f32p, c_f32p, c_f32p, c_int, c_int, c_vp, c_i64, c_i64,
                              ctypes.POINTER(c_vp), c_vp],
     "nerf_hash_encode_bwd_ws": [c_vp, c_i64, c_f32p, c_f32p, c_f32p, c_int, c_int, c_vp, c_i64, c_i64,
-                                ctypes.POINTER(c_vp), c_vp, ctypes.c_size_t, c_vp],
+                                ctypes.POINTER(c_vp), c_int, c_vp, ctypes.c_size_t, c_vp],
     "nerf_hash_encode_bwd_bin": [c_vp, c_i64, c_f32p, c_f32p, c_f32p, c_int, c_int, c_vp, c_i64, c_i64, c_i64,
-                                 c_i64, c_vp, ctypes.c_size_t, c_vp],
-    "nerf_hash_encode_bwd_owner": [c_int, c_int, c_i64, c_i64, ctypes.POINTER(c_vp), c_vp, ctypes.c_size_t, c_vp],
+                                 c_i64, c_int, c_vp, ctypes.c_size_t, c_vp],
+    "nerf_hash_encode_bwd_owner": [c_int, c_int, c_i64, c_i64, ctypes.POINTER(c_vp), c_int, c_vp, ctypes.c_size_t,
+                                   c_vp],
     "nerf_sh4_fwd": [c_vp, c_i64, c_vp, c_vp],
     "nerf_mlp_fwd": [c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, ctypes.POINTER(MlpWeights),
                      c_vp, c_vp, c_vp],
@@ -73,6 +86,8 @@ SIGNATURES = {
                        c_vp, c_vp, c_vp, c_vp, c_i64, c_vp],
     "nerf_mlp_bwd_q": [c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, ctypes.POINTER(MlpWeights),
                        c_vp, ctypes.POINTER(MlpGrads), c_vp, c_vp, c_vp, c_vp, c_vp],
+    "nerf_count_nonfinite": [ctypes.POINTER(c_vp), ctypes.POINTER(c_i64), c_int, c_vp, c_vp],
+    "nerf_mlp_bwd_batch": [ctypes.POINTER(MlpBwdJob), c_int, c_vp, ctypes.c_size_t, c_vp],
     "nerf_normal_head_fwd": [c_vp, c_vp, c_vp, c_i64, ctypes.POINTER(NormalHead), c_vp, c_vp],
     "nerf_normal_head_bwd": [c_vp, c_vp, c_i64, ctypes.POINTER(NormalHead), c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                              c_vp],
@@ -130,7 +145,9 @@ def load():
     lib.nerf_abi_version.restype = c_int
     lib.nerf_abi_version.argtypes = []
     lib.nerf_hash_encode_bwd_workspace_bytes.restype = ctypes.c_size_t
-    lib.nerf_hash_encode_bwd_workspace_bytes.argtypes = [c_int, c_int, c_i64]
+    lib.nerf_hash_encode_bwd_workspace_bytes.argtypes = [c_int, c_int, c_i64, c_int]
+    lib.nerf_mlp_bwd_det_workspace_bytes.restype = ctypes.c_size_t
+    lib.nerf_mlp_bwd_det_workspace_bytes.argtypes = []
     lib.nerf_quant_packed_bytes.restype = ctypes.c_size_t
     lib.nerf_quant_packed_bytes.argtypes = [c_int, c_int]
     for name, argtypes in SIGNATURES.items():
@@ -143,7 +160,7 @@ def load():
 
 def exported_symbols():
     return ["nerf_last_error", "nerf_abi_version", "nerf_hash_encode_bwd_workspace_bytes",
-            "nerf_quant_packed_bytes"] + list(SIGNATURES)
+            "nerf_quant_packed_bytes", "nerf_mlp_bwd_det_workspace_bytes"] + list(SIGNATURES)
 
 
 _TIMING = None   # when a list: (name, start_event, end_event) per launch, recorded on the current stream

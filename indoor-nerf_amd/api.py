@@ -2,7 +2,7 @@
 run_nerf_helpers.py, hash_encoding.py, radam.py, loss.py) backed by libnerfhip."""
 from . import _lib
 from .dist import GradArena, ShardedOptimizer, broadcast_params, init_process_group, shard
-from .field import NeRFSmall, batchify, run_network
+from .field import NeRFSmall, batchify, deterministic, run_network, set_deterministic
 from .hashgrid import HashEmbedder, SHEncoder, level_resolutions
 from .losses import sigma_sparsity_loss, total_variation_all, total_variation_loss, train_loss
 from .model import acaq_quantizers, acaq_update, create_nerf, make_args, save_checkpoint, train_step
@@ -10,7 +10,7 @@ from .optim import RAdam
 from .quantization import FakeQuantizer, LearnedBitwidthQuantizer, PassthroughQuantizer, calculate_fqr
 from .rays import RaySampler, crop_window
 from .scene import get_bbox3d_for_blenderobj, get_bbox3d_for_llff
-from .render import (batchify_rays, camera, get_rays, get_rays_np, img2mse, manual_seed, mse2psnr, ndc_rays, raw2outputs,
+from .render import (batchify_rays, camera, check_numerics, get_rays, get_rays_np, img2mse, manual_seed, mse2psnr, ndc_rays, raw2outputs,
                      render, render_path, render_rays, sample_pdf, to8b)
 from .data import load_blender_data, load_llff_data, load_scannet_data, pose_spherical
 from .priors import (ManhattanFrameEstimator, SemanticPlaneDetector, combine_structural_losses_v2, manhattan_sdf_loss,
@@ -25,7 +25,7 @@ __all__ = ["HashEmbedder", "SHEncoder", "NeRFSmall", "RAdam", "run_network", "ba
            "get_bbox3d_for_blenderobj", "get_bbox3d_for_llff", "render_path", "load_blender_data", "load_llff_data",
            "pose_spherical", "load_scannet_data", "ManhattanFrameEstimator", "SemanticPlaneDetector",
            "combine_structural_losses_v2", "manhattan_sdf_loss", "spatial_normal_consistency_loss",
-           "structured_planarity_loss"]
+           "structured_planarity_loss", "set_deterministic", "deterministic", "check_numerics"]
 
 
 def load_library():

@@ -5,6 +5,8 @@
 #include <stdint.h>
 #include <stdio.h>
 
+#include <algorithm>
+
 #include "../../include/nerf_hip.h"
 
 namespace nerf {

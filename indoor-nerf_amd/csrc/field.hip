@@ -22,7 +22,7 @@ __global__ void __launch_bounds__(256) sh4_fwd_kernel(const float* __restrict__ 
 
 int launch_mlp_fwd_x6(const MlpArgs& a, hipStream_t stream);     // field_x6.hip
 int launch_mlp_act_minmax_x6(const MlpArgs& a, hipStream_t stream);
-int launch_mlp_bwd_x6(const MlpArgs& a, hipStream_t stream);
+int launch_mlp_bwd_x6(const MlpArgs* jobs, int n_jobs, float* det_ws, hipStream_t stream);
 
 static int fill_args(MlpArgs& a, const float* d_feat, int64_t sp, int64_t sl, const float* d_sh, int64_t sh_stride,
                      const float* d_viewdirs, int64_t spr, const uint8_t* d_keep, int64_t n,
@@ -90,7 +90,40 @@ extern "C" int nerf_mlp_bwd_q(const float* d_feat, int64_t feat_stride_point, in
     if (n_points == 0) return NERF_OK;
     a.graw = d_graw; a.G = *grads; a.dfeat = d_dfeat; a.dsh = d_dsh; a.dgeo = d_dgeo;
     a.aq = reinterpret_cast<const QuantRec*>(d_act_qrec);
-    return launch_mlp_bwd_x6(a, as_stream(stream));
+    return launch_mlp_bwd_x6(&a, 1, nullptr, as_stream(stream));
+}
+
+extern "C" size_t nerf_mlp_bwd_det_workspace_bytes(void) {
+    return (size_t)kMlpBwdMaxBlocks * GW_TOTAL * sizeof(float);
+}
+
+extern "C" int nerf_mlp_bwd_batch(const nerf_mlp_bwd_job* jobs, int n_jobs, float* d_det_workspace,
+                                  size_t det_workspace_bytes, void* stream) {
+    NERF_REQUIRE(jobs && n_jobs >= 1 && n_jobs <= NERF_MLP_MAX_JOBS, "mlp_bwd_batch: %d jobs (1..%d)", n_jobs,
+                 NERF_MLP_MAX_JOBS);
+    NERF_REQUIRE(!d_det_workspace || det_workspace_bytes >= nerf_mlp_bwd_det_workspace_bytes(),
+                 "mlp_bwd_batch: deterministic workspace %zu B < %zu B", det_workspace_bytes,
+                 nerf_mlp_bwd_det_workspace_bytes());
+    MlpArgs a[NERF_MLP_MAX_JOBS]{};
+    int n = 0;
+    for (int k = 0; k < n_jobs; ++k) {
+        const nerf_mlp_bwd_job& j = jobs[k];
+        MlpArgs& x = a[n];
+        int rc = fill_args(x, j.feat, j.feat_stride_point, j.feat_stride_level, j.sh, j.sh_stride, j.viewdirs,
+                           j.samples_per_ray, j.keep, j.n_points, &j.weights);
+        if (rc) return rc;
+        const nerf_mlp_grads& g = j.grads;
+        NERF_REQUIRE(j.graw && g.w0 && g.w1 && g.c0 && g.c1 && g.c2, "mlp_bwd_batch: job %d: null gradient pointer", k);
+        x.graw = j.graw; x.G = g; x.dfeat = j.dfeat; x.dsh = j.dsh; x.dgeo = j.dgeo;
+        x.aq = reinterpret_cast<const QuantRec*>(j.act_qrec);
+        if (x.P > 0) ++n;   // empty jobs launch nothing
+    }
+    if (n == 0) return NERF_OK;
+    if (n == 2 && (a[0].aq != nullptr) != (a[1].aq != nullptr)) {   // one quantizer mode per launch
+        int rc = launch_mlp_bwd_x6(&a[0], 1, d_det_workspace, as_stream(stream));
+        return rc ? rc : launch_mlp_bwd_x6(&a[1], 1, d_det_workspace, as_stream(stream));
+    }
+    return launch_mlp_bwd_x6(a, n, d_det_workspace, as_stream(stream));
 }
 
 extern "C" int nerf_mlp_bwd(const float* d_feat, int64_t feat_stride_point, int64_t feat_stride_level,

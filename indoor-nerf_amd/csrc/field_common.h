@@ -18,6 +18,9 @@ __device__ __forceinline__ int row_of(int r, int h) { return (r & 3) + 8 * (r >>
 // C1 [64][64], C2 [3][64]
 constexpr int GW_W0 = 0, GW_W1 = 2048, GW_C0 = 3072, GW_C1 = 5056, GW_C2 = 9152, GW_TOTAL = 9344;
 
+// MLP backward grid cap: one 512-thread block per CU (159 KB of LDS each)
+constexpr int kMlpBwdMaxBlocks = 256;
+
 struct MlpArgs {
     const float* feat; int64_t sp, sl;
     const float* sh; int64_t sh_stride;

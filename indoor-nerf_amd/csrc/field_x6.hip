@@ -491,7 +491,8 @@ __device__ __forceinline__ void stage_arrF(float* actF, const float* v, int row0
 
 template <bool QUANT>
 __device__ __forceinline__ void bwd_chain_role(const MlpArgs& a, const __bf16* img, __bf16* stA, __bf16* stG,
-                                               int* ready, int* ack, int p, int lane, const QuantRec& aq) {
+                                               int* ready, int* ack, int p, int lane, const QuantRec& aq, int blk,
+                                               int nblk) {
     const int j = lane & 31, h = lane >> 5;
     float* actF = reinterpret_cast<float*>(stA);
     int seq = 0;
@@ -505,7 +506,7 @@ __device__ __forceinline__ void bwd_chain_role(const MlpArgs& a, const __bf16* i
     __bf16* const stGb[2] = {stG, stG + 3 * STG_PIECE};
     auto publish = [&]() { flag_set(ready, ++seq); };
     const int64_t n_tiles = (a.P + 31) / 32;
-    for (int64_t tile = (int64_t)blockIdx.x * 4 + p; tile < n_tiles; tile += (int64_t)gridDim.x * 4) {
+    for (int64_t tile = (int64_t)blk * 4 + p; tile < n_tiles; tile += (int64_t)nblk * 4) {
         const __bf16* imt = img + opaque_zero();
         InX6 in;
         load_in_x6(a, tile, j, h, in);
@@ -736,7 +737,8 @@ __device__ __forceinline__ void mma32(floatx16 (&acc)[NU], const Ops32<NU>& o) {
 // Every stage: wait for it, read all of its operands, release the buffer (ack), then run the MFMAs,
 // so the chain wave's next staging overlaps them.
 __device__ __forceinline__ void bwd_wgrad_role(const MlpArgs& a, const __bf16* img, const __bf16* stA,
-                                               const __bf16* stG, int* ready, int* ack, int p, int lane, WgradX6& g) {
+                                               const __bf16* stG, int* ready, int* ack, int p, int lane, WgradX6& g,
+                                               int blk, int nblk) {
     const int j = lane & 31, h = lane >> 5;
     const float* actF = reinterpret_cast<const float*>(stA);
 #pragma unroll
@@ -754,7 +756,7 @@ __device__ __forceinline__ void bwd_wgrad_role(const MlpArgs& a, const __bf16* i
     auto take = [&]() { flag_wait(ready, seq + 1, &waited); };
     auto release = [&]() { flag_set_now(ack, ++seq); };
     const int64_t n_tiles = (a.P + 31) / 32;
-    for (int64_t tile = (int64_t)blockIdx.x * 4 + p; tile < n_tiles; tile += (int64_t)gridDim.x * 4) {
+    for (int64_t tile = (int64_t)blk * 4 + p; tile < n_tiles; tile += (int64_t)nblk * 4) {
         {   // 1: dC2
             Ops16 o;
             take(); read16(o, stG + 3 * STG_PIECE, actF, lane); release();
@@ -807,10 +809,25 @@ __device__ __forceinline__ void bwd_wgrad_role(const MlpArgs& a, const __bf16* i
 #endif
 }
 
+// Up to two nets per launch: the coarse and the fine pass of an iteration are separate NeRFSmall
+// instances (run_nerf.py:254-259) whose backwards are both ready when autograd reaches the first of
+// them (field.py defers them to the end of the pass). Blocks [0, split) run job 0 and the others
+// job 1, each block on its own net's weight image and tiles, so the per-launch fixed costs (weight
+// image build, chain / wgrad pipeline fill and drain, block reduction tail) are paid once per step.
+struct MlpBwdJobs {
+    MlpArgs a[2];
+    int split;       // blocks of job 0
+    float* det_ws;   // deterministic mode: per-block weight-gradient images [gridDim.x][GW_TOTAL]
+};
+
 template <bool QUANT>
-__global__ void __launch_bounds__(512, 1) mlp_bwd_x6cg_kernel(MlpArgs a) {
+__global__ void __launch_bounds__(512, 1) mlp_bwd_x6cg_kernel(MlpBwdJobs jobs) {
     __shared__ __attribute__((aligned(16))) __bf16 lds[X6_CG_LDS / 2];
     __shared__ int flags[8];   // ready[0..3], ack[0..3]
+    const bool second = (int)blockIdx.x >= jobs.split;
+    const MlpArgs& a = second ? jobs.a[1] : jobs.a[0];
+    const int blk = second ? (int)blockIdx.x - jobs.split : (int)blockIdx.x;
+    const int nblk = second ? (int)gridDim.x - jobs.split : jobs.split;
     __bf16* img = lds;
     const int wv = threadIdx.x >> 6, p = wv & 3;
     const bool wgrad_wave = wv >= 4;
@@ -823,17 +840,18 @@ __global__ void __launch_bounds__(512, 1) mlp_bwd_x6cg_kernel(MlpArgs a) {
     const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
     WgradX6 g;   // defined (and live) on the wgrad waves only
     if (wgrad_wave) {
-        bwd_wgrad_role(a, img, stA, stG, flags + p, flags + 4 + p, p, lane, g);
+        bwd_wgrad_role(a, img, stA, stG, flags + p, flags + 4 + p, p, lane, g, blk, nblk);
     } else {
         QuantRec aq{};
         if constexpr (QUANT) aq = *a.aq;
-        bwd_chain_role<QUANT>(a, img, stA, stG, flags + p, flags + 4 + p, p, lane, aq);
+        bwd_chain_role<QUANT>(a, img, stA, stG, flags + p, flags + 4 + p, p, lane, aq, blk, nblk);
     }
 
     // ---- block reduction of the wgrad waves' tiles, one global flush per block. Each wgrad wave
     // writes its full weight-gradient image (every index exactly once: the tile maps are fixed) into
-    // its own LDS copy with plain stores; then all 512 threads sum the four copies. LDS fp32 atomics
-    // here (one ds_add_f32 per value and wave into a shared image) cost 49 us per launch.
+    // its own LDS copy with plain stores; then all 512 threads sum the four copies in a fixed order.
+    // LDS fp32 atomics here (one ds_add_f32 per value and wave into a shared image) cost 49 us per
+    // launch.
     static_assert(4 * GW_TOTAL * (int)sizeof(float) <= X6_CG_LDS, "four weight-gradient images must fit the LDS");
     __syncthreads();
     float* gw = reinterpret_cast<float*>(lds);
@@ -862,17 +880,39 @@ __global__ void __launch_bounds__(512, 1) mlp_bwd_x6cg_kernel(MlpArgs a) {
             }
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < GW_TOTAL; i += blockDim.x) {
-        float* dst;
-        int k;
-        if (i < GW_W1) { dst = a.G.w0; k = i; }
-        else if (i < GW_C0) { dst = a.G.w1; k = i - GW_W1; }
-        else if (i < GW_C1) { dst = a.G.c0; k = i - GW_C0; }
-        else if (i < GW_C2) { dst = a.G.c1; k = i - GW_C1; }
-        else { dst = a.G.c2; k = i - GW_C2; }
-        const float v = (gw[i] + gw[GW_TOTAL + i]) + (gw[2 * GW_TOTAL + i] + gw[3 * GW_TOTAL + i]);
-        if (v != 0.f) __hip_atomic_fetch_add(dst + k, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    auto sum4 = [&](int i) { return (gw[i] + gw[GW_TOTAL + i]) + (gw[2 * GW_TOTAL + i] + gw[3 * GW_TOTAL + i]); };
+    if (jobs.det_ws) {   // deterministic: the block's image, reduced over blocks in order by mlp_wgrad_reduce
+        float* dst = jobs.det_ws + (size_t)blockIdx.x * GW_TOTAL;
+        for (int i = threadIdx.x; i < GW_TOTAL; i += blockDim.x) dst[i] = sum4(i);
+        return;
     }
+    // one loop per matrix: a pointer chosen per index would be a dynamically indexed private array
+    auto flush = [&](float* dst, int off, int n) {
+        for (int k = threadIdx.x; k < n; k += blockDim.x) {
+            const float v = sum4(off + k);
+            if (v != 0.f) __hip_atomic_fetch_add(dst + k, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    };
+    flush(a.G.w0, GW_W0, GW_W1 - GW_W0);
+    flush(a.G.w1, GW_W1, GW_C0 - GW_W1);
+    flush(a.G.c0, GW_C0, GW_C1 - GW_C0);
+    flush(a.G.c1, GW_C1, GW_C2 - GW_C1);
+    flush(a.G.c2, GW_C2, GW_TOTAL - GW_C2);
+}
+
+// Deterministic weight-gradient reduction: value i of a net's gradient image summed over the net's
+// blocks [b0, b0 + nb) in block order, then added to .grad (the sole writer: no atomics).
+__global__ void __launch_bounds__(256) mlp_wgrad_reduce_kernel(const float* __restrict__ ws, int b0, int nb,
+                                                               nerf_mlp_grads G) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= GW_TOTAL) return;
+    float s = 0.f;
+    for (int b = 0; b < nb; ++b) s += ws[(size_t)(b0 + b) * GW_TOTAL + i];
+    if (i < GW_W1) G.w0[i - GW_W0] += s;
+    else if (i < GW_C0) G.w1[i - GW_W1] += s;
+    else if (i < GW_C1) G.c0[i - GW_C0] += s;
+    else if (i < GW_C2) G.c1[i - GW_C1] += s;
+    else G.c2[i - GW_C2] += s;
 }
 
 // every element index the kernels form (feat, sh, raw/graw, geo/dgeo/dsh, dfeat) stays below 2^31
@@ -904,24 +944,47 @@ int launch_mlp_act_minmax_x6(const MlpArgs& a, hipStream_t stream) {
     return NERF_OK;
 }
 
-int launch_mlp_bwd_x6(const MlpArgs& a, hipStream_t stream) {
-    NERF_REQUIRE(fits_u32(a), "mlp_bwd(x6): %lld points exceed 32-bit indexing", (long long)a.P);
-    const int64_t tiles = (a.P + 31) / 32;
-    const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((tiles + 3) / 4, 256));
-    if (a.aq)
-        hipLaunchKernelGGL(mlp_bwd_x6cg_kernel<true>, dim3((unsigned)blocks), dim3(512), 0, stream, a);
+// jobs: 1 or 2 nets (P > 0 each, the same quantizer mode); det_ws (deterministic mode) holds
+// kMlpBwdMaxBlocks x GW_TOTAL floats.
+int launch_mlp_bwd_x6(const MlpArgs* jobs, int n_jobs, float* det_ws, hipStream_t stream) {
+    NERF_REQUIRE(n_jobs == 1 || n_jobs == 2, "mlp_bwd(x6): %d jobs", n_jobs);
+    int64_t want[2] = {0, 0}, tiles[2] = {0, 0};
+    for (int k = 0; k < n_jobs; ++k) {
+        NERF_REQUIRE(fits_u32(jobs[k]), "mlp_bwd(x6): %lld points exceed 32-bit indexing", (long long)jobs[k].P);
+        NERF_REQUIRE(jobs[k].P > 0, "mlp_bwd(x6): empty job");
+        NERF_REQUIRE((jobs[k].aq != nullptr) == (jobs[0].aq != nullptr), "mlp_bwd(x6): mixed quantizer modes");
+        tiles[k] = (jobs[k].P + 31) / 32;
+        want[k] = (tiles[k] + 3) / 4;   // blocks of 4 wave pairs, one tile per pair
+    }
+    MlpBwdJobs J{};
+    J.a[0] = jobs[0];
+    J.a[1] = n_jobs == 2 ? jobs[1] : jobs[0];
+    J.det_ws = det_ws;
+    int64_t blocks;
+    if (n_jobs == 1) {
+        blocks = std::max<int64_t>(1, std::min<int64_t>(want[0], kMlpBwdMaxBlocks));
+        J.split = (int)blocks;
+    } else if (want[0] + want[1] <= kMlpBwdMaxBlocks) {
+        blocks = want[0] + want[1];
+        J.split = (int)want[0];
+    } else {   // one block per CU: blocks in proportion to the tiles, so both nets finish together
+        blocks = kMlpBwdMaxBlocks;
+        const int64_t b0 = (kMlpBwdMaxBlocks * tiles[0] + (tiles[0] + tiles[1]) / 2) / (tiles[0] + tiles[1]);
+        J.split = (int)std::min<int64_t>(std::max<int64_t>(b0, 1), kMlpBwdMaxBlocks - 1);
+    }
+    if (jobs[0].aq)
+        hipLaunchKernelGGL(mlp_bwd_x6cg_kernel<true>, dim3((unsigned)blocks), dim3(512), 0, stream, J);
     else
-        hipLaunchKernelGGL(mlp_bwd_x6cg_kernel<false>, dim3((unsigned)blocks), dim3(512), 0, stream, a);
-#ifdef NERF_X6CG_PROF
-    unsigned long long pr[4];
-    (void)hipDeviceSynchronize();
-    (void)hipMemcpyFromSymbol(pr, HIP_SYMBOL(cg_prof), sizeof(pr));
-    fprintf(stderr, "cgprof P=%lld chain wait/total %llu/%llu  wgrad wait/total %llu/%llu (s_memtime ticks, sum over waves)\n",
-            (long long)a.P, pr[0], pr[1], pr[2], pr[3]);
-    const unsigned long long z[4] = {0, 0, 0, 0};
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(cg_prof), z, sizeof(z));
-#endif
+        hipLaunchKernelGGL(mlp_bwd_x6cg_kernel<false>, dim3((unsigned)blocks), dim3(512), 0, stream, J);
     NERF_CHECK_LAUNCH("mlp_bwd(x6)");
+    if (det_ws) {
+        for (int k = 0; k < n_jobs; ++k) {
+            const int b0 = k == 0 ? 0 : J.split, nb = k == 0 ? J.split : (int)blocks - J.split;
+            hipLaunchKernelGGL(mlp_wgrad_reduce_kernel, dim3((GW_TOTAL + 255) / 256), dim3(256), 0, stream, det_ws, b0,
+                               nb, jobs[k].G);
+        }
+        NERF_CHECK_LAUNCH("mlp_bwd(x6) deterministic reduction");
+    }
     return NERF_OK;
 }
 

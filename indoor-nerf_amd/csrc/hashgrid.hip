@@ -31,8 +31,9 @@ struct HashGradParams {
     int nchunks;          // chunks the owner pass walks
     int chunk_base;       // bin pass: chunk index of this launch's first 256 points
     int chunk_stride;     // chunk capacity of the workspace (the layout stride)
-    int slice_log2;       // owner slice = 2^slice_log2 rows (LDS: 8 B per row)
+    int slice_log2;       // owner slice = 2^slice_log2 rows (LDS: 16 B per row, 32 B deterministic)
     int owner_log2;       // owners per level = 2^owner_log2
+    uint32_t* lvl_max;    // deterministic mode: per level max |entry| (float bits), else null
 };
 
 // QUANT: every gathered corner feature goes through the level's A-CAQ quantizer first
@@ -113,6 +114,7 @@ constexpr uint32_t kSkip = 0xFFFFFFFFu;
 // region sorted by owner slice (plain stores), and hash_bwd_owner_kernel sums each slice in LDS.
 constexpr int kChunkCap = 256 * 8;        // entries per 256-point chunk (8 corners per point)
 constexpr int kSliceLog2 = 13;            // owner slice: 2^13 rows x 16 B (fp64 pair) = 128 KiB of LDS
+constexpr int kSliceLog2Det = 12;         // deterministic: 2^12 rows x 32 B (two int64 words per feature)
 constexpr int kMaxOwnersLog2 = 7;
 constexpr int kMaxOwners = 1 << kMaxOwnersLog2;
 
@@ -220,6 +222,15 @@ __global__ void __launch_bounds__(256) hash_encode_bwd_kernel(
                 s_eg[k] = make_float2(cgx[c], cgy[c]);
             }
         }
+        if (hp.lvl_max) {   // deterministic mode: the level's largest |entry| sets the owners' fixed-point scale
+            float m = 0.f;
+#pragma unroll
+            for (int c = 0; c < 8; ++c)
+                if (pos[c] != kSkip) m = fmaxf(m, fmaxf(fabsf(cgx[c]), fabsf(cgy[c])));
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+            if (lane == 0 && m > 0.f) atomicMax(hp.lvl_max + lvl, __float_as_uint(m));   // non-negative: uint order
+        }
         __syncthreads();
         const uint32_t total = s_start[n_own];
         const size_t base = ((size_t)lvl * hp.chunk_stride + hp.chunk_base + blockIdx.x) * kChunkCap;
@@ -266,21 +277,38 @@ __global__ void __launch_bounds__(256) hash_encode_bwd_kernel(
 // SLICE_LOG2 / THREADS: 2^13-row slices with one 1024-thread block per CU (128 KiB of LDS); 2^12-row
 // slices with two 512-thread blocks per CU measured slower (0.41 vs 0.34 ms per backward: the
 // doubled per-owner segment scans outweigh the overlap).
-template <int SLICE_LOG2, int THREADS>
+//
+// DET (deterministic mode): integer accumulation is associative, so the sums do not depend on the
+// order in which waves add entries. Each entry v becomes two int64 fixed-point words at the level's
+// scale 2^s (s from the level's largest |entry| and the entry-count bound, so no sum can overflow):
+// hi = rint(v 2^s), lo = rint((v 2^s - hi) 2^L); the slice is summed with ds_add_u64 and the row
+// total hi 2^-s + lo 2^-(s+L) (about 2^-75 of the level's largest entry per term) is rounded to fp32
+// once. Slices are 2^12 rows (32 B of LDS per row).
+template <int SLICE_LOG2, int THREADS, bool DET>
 __global__ void __launch_bounds__(THREADS) hash_bwd_owner_kernel(HashGradParams hp) {
     constexpr int kOwnerThreads = THREADS;
     constexpr int kOwnerWindow = 2 * THREADS;   // chunks per window: 2 per thread in the scan
     // fp64 accumulators: ds_add_f64 runs ~14x the rate of ds_add_f32 on gfx950 (tools/
     // lds_atomic_bench.hip: 2.24 vs 0.165 row updates per clock per CU, random rows), and the
     // slice total is rounded to fp32 once.
-    __shared__ __attribute__((aligned(16))) double2 s_slice[1 << SLICE_LOG2];
+    __shared__ __attribute__((aligned(16))) double2 s_slice[(DET ? 2 : 1) << SLICE_LOG2];
+    unsigned long long* s_fix = reinterpret_cast<unsigned long long*>(s_slice);   // DET: [row][hi x, hi y, lo x, lo y]
     __shared__ uint32_t s_pre[kOwnerWindow + 1];
     __shared__ uint16_t s_beg[kOwnerWindow];
     __shared__ uint32_t s_wsum[kOwnerThreads / 64];
     const int o = blockIdx.x, lvl = blockIdx.y;
     const int S = 1 << hp.slice_log2, n_own = 1 << hp.owner_log2;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    for (int i = tid; i < S; i += kOwnerThreads) s_slice[i] = make_double2(0.0, 0.0);
+    for (int i = tid; i < (DET ? 2 : 1) * S; i += kOwnerThreads) s_slice[i] = make_double2(0.0, 0.0);
+    // DET: scale exponents (hi: 2^sh, lo: 2^(sh + L)); a level without entries has lvl_max 0
+    int sh = 0, sl_ = 0;
+    if constexpr (DET) {
+        int E;
+        (void)frexpf(__uint_as_float(hp.lvl_max[lvl]), &E);                 // max |entry| < 2^E
+        const int b = 11 + (32 - __clz((unsigned)max(hp.nchunks - 1, 1)));  // entries <= 2^b
+        sh = 62 - E - b;
+        sl_ = sh + (61 - b);
+    }
     const uint32_t* seg = hp.bin_seg + ((size_t)lvl * n_own + o) * hp.chunk_stride;
     for (int w0 = 0; w0 < hp.nchunks; w0 += kOwnerWindow) {
         const int nw = min(kOwnerWindow, hp.nchunks - w0);
@@ -389,8 +417,20 @@ __global__ void __launch_bounds__(THREADS) hash_bwd_owner_kernel(HashGradParams 
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 if (valid & (1u << j)) {
-                    atomicAdd(&s_slice[h[j]].x, (double)g[j].x);
-                    atomicAdd(&s_slice[h[j]].y, (double)g[j].y);
+                    if constexpr (DET) {
+                        const double tx = ldexp((double)g[j].x, sh), ty = ldexp((double)g[j].y, sh);
+                        const double hx = rint(tx), hy = rint(ty);
+                        const long long lx = (long long)rint(ldexp(tx - hx, sl_ - sh));
+                        const long long ly = (long long)rint(ldexp(ty - hy, sl_ - sh));
+                        unsigned long long* r = s_fix + 4 * h[j];
+                        atomicAdd(r + 0, (unsigned long long)(long long)hx);
+                        atomicAdd(r + 1, (unsigned long long)(long long)hy);
+                        atomicAdd(r + 2, (unsigned long long)lx);
+                        atomicAdd(r + 3, (unsigned long long)ly);
+                    } else {
+                        atomicAdd(&s_slice[h[j]].x, (double)g[j].x);
+                        atomicAdd(&s_slice[h[j]].y, (double)g[j].y);
+                    }
                 }
             }
 #pragma unroll
@@ -407,6 +447,20 @@ __global__ void __launch_bounds__(THREADS) hash_bwd_owner_kernel(HashGradParams 
     __syncthreads();
     float2* dt = reinterpret_cast<float2*>(hp.dtables[lvl]) + (size_t)o * S;
     constexpr int kRows = (1 << SLICE_LOG2) / kOwnerThreads;
+    if constexpr (DET) {
+        auto fixed = [&](int row, int f) {
+            const long long hi = (long long)s_fix[4 * row + f], lo = (long long)s_fix[4 * row + 2 + f];
+            return ldexp((double)hi, -sh) + ldexp((double)lo, -sl_);
+        };
+        for (int i = tid; i < S; i += kOwnerThreads) {
+            const double vx = fixed(i, 0), vy = fixed(i, 1);
+            if (vx != 0.0 || vy != 0.0) {
+                const float2 t = dt[i];
+                dt[i] = make_float2((float)((double)t.x + vx), (float)((double)t.y + vy));
+            }
+        }
+        return;
+    }
     if (S == (1 << SLICE_LOG2)) {
         float2 t[kRows];
 #pragma unroll
@@ -430,12 +484,12 @@ __global__ void __launch_bounds__(THREADS) hash_bwd_owner_kernel(HashGradParams 
 
 struct BinPlan {
     int slice_log2, owner_log2, nchunks;
-    size_t off_h, off_g, off_off, total;   // byte offsets in the workspace
+    size_t off_h, off_g, off_off, off_max, total;   // byte offsets in the workspace
 };
 
 // Binned path for log2_T in [1, slice + log2(kMaxOwners)]: slices of min(2^slice, T) rows.
-static bool make_bin_plan(int n_levels, int log2_T, int64_t n_points, BinPlan& B) {
-    const int slice = kSliceLog2;
+static bool make_bin_plan(int n_levels, int log2_T, int64_t n_points, BinPlan& B, bool det = false) {
+    const int slice = det ? kSliceLog2Det : kSliceLog2;
     if (log2_T < 1 || log2_T > slice + kMaxOwnersLog2 || n_points < 0) return false;
     B.slice_log2 = log2_T < slice ? log2_T : slice;
     B.owner_log2 = log2_T - B.slice_log2;
@@ -446,7 +500,8 @@ static bool make_bin_plan(int n_levels, int log2_T, int64_t n_points, BinPlan& B
     B.off_g = 0;
     B.off_h = up(entries * sizeof(float2));
     B.off_off = B.off_h + up(entries * sizeof(uint16_t));
-    B.total = B.off_off + up(offs * sizeof(uint32_t));
+    B.off_max = B.off_off + up(offs * sizeof(uint32_t));
+    B.total = B.off_max + (det ? up(NERF_MAX_LEVELS * sizeof(uint32_t)) : 0);
     return true;
 }
 
@@ -492,11 +547,107 @@ extern "C" int nerf_hash_encode_fwd(const float* d_xyz, int64_t n_points, const 
                                   nullptr, d_feat, feat_stride_point, feat_stride_level, d_keep, stream);
 }
 
-static int hash_encode_bwd_impl(const float* d_xyz, int64_t n_points, const float* bbox_min3,
-                                const float* bbox_max3, const float* level_res, int n_levels, int log2_T,
-                                const float* d_dfeat, int64_t feat_stride_point, int64_t feat_stride_level,
-                                float* const* d_dtables, void* d_workspace, size_t workspace_bytes,
-                                void* stream) {
+// ---- binned backward: bin launches + one owner launch ---------------------------------------
+// The fine and the coarse pass of a training iteration scatter into the same tables; binning both
+// into one workspace (side by side, chunk_base apart) and summing them with ONE owner launch pays
+// the owner's per-launch costs (LDS clear, slice flush = a read-modify-write of every table row)
+// once per iteration instead of once per pass.
+static int bin_layout(const char* who, int n_levels, int log2_T, int64_t chunk_capacity, int det, void* d_workspace,
+                      size_t workspace_bytes, HashGradParams& hp) {
+    NERF_REQUIRE(n_levels >= 1 && n_levels <= NERF_MAX_LEVELS, "%s: n_levels %d", who, n_levels);
+    NERF_REQUIRE(chunk_capacity >= 1 && chunk_capacity <= (int64_t)1 << 26, "%s: chunk_capacity %lld", who,
+                 (long long)chunk_capacity);
+    BinPlan B{};
+    NERF_REQUIRE(make_bin_plan(n_levels, log2_T, chunk_capacity * 256, B, det != 0),
+                 "%s: no binned path for log2_T %d%s", who, log2_T, det ? " (deterministic)" : "");
+    NERF_REQUIRE(d_workspace != nullptr && workspace_bytes >= B.total,
+                 "%s: workspace %zu B < %zu B (nerf_hash_encode_bwd_workspace_bytes(L, log2_T, 256 * capacity, det))",
+                 who, workspace_bytes, B.total);
+    char* ws = static_cast<char*>(d_workspace);
+    hp.bin_g = reinterpret_cast<float2*>(ws + B.off_g);
+    hp.bin_h = reinterpret_cast<uint16_t*>(ws + B.off_h);
+    hp.bin_seg = reinterpret_cast<uint32_t*>(ws + B.off_off);
+    hp.lvl_max = det ? reinterpret_cast<uint32_t*>(ws + B.off_max) : nullptr;
+    hp.chunk_stride = B.nchunks;
+    hp.slice_log2 = B.slice_log2;
+    hp.owner_log2 = B.owner_log2;
+    hp.mask = (uint32_t)((1u << log2_T) - 1u);
+    return NERF_OK;
+}
+
+extern "C" size_t nerf_hash_encode_bwd_workspace_bytes(int n_levels, int log2_T, int64_t n_points, int deterministic) {
+    BinPlan B{};
+    if (n_levels < 1 || n_levels > NERF_MAX_LEVELS || !make_bin_plan(n_levels, log2_T, n_points, B, deterministic != 0))
+        return 0;
+    return B.total;
+}
+
+extern "C" int nerf_hash_encode_bwd_bin(const float* d_xyz, int64_t n_points, const float* bbox_min3,
+                                        const float* bbox_max3, const float* level_res, int n_levels, int log2_T,
+                                        const float* d_dfeat, int64_t feat_stride_point, int64_t feat_stride_level,
+                                        int64_t chunk_base, int64_t chunk_capacity, int deterministic,
+                                        void* d_workspace, size_t workspace_bytes, void* stream) {
+    NERF_REQUIRE(n_points >= 0, "hash_encode_bwd_bin: n_points < 0");
+    NERF_REQUIRE(d_xyz && d_dfeat && level_res && bbox_min3 && bbox_max3, "hash_encode_bwd_bin: null arg");
+    HashGradParams hp{};
+    const int rc = bin_layout("hash_encode_bwd_bin", n_levels, log2_T, chunk_capacity, deterministic, d_workspace,
+                              workspace_bytes, hp);
+    if (rc) return rc;
+    const int64_t nch = (n_points + 255) / 256;
+    NERF_REQUIRE(chunk_base >= 0 && chunk_base + nch <= chunk_capacity,
+                 "hash_encode_bwd_bin: chunks [%lld, %lld) exceed the capacity %lld", (long long)chunk_base,
+                 (long long)(chunk_base + nch), (long long)chunk_capacity);
+    // deterministic: the first bin call of a batch resets the per-level maxima (a memset node under capture)
+    if (hp.lvl_max && chunk_base == 0) {
+        const hipError_t e = hipMemsetAsync(hp.lvl_max, 0, NERF_MAX_LEVELS * sizeof(uint32_t), as_stream(stream));
+        if (e != hipSuccess) {
+            set_error("hash_encode_bwd_bin: hipMemsetAsync: %s", hipGetErrorString(e));
+            return NERF_E_LAUNCH;
+        }
+    }
+    if (n_points == 0) return NERF_OK;
+    for (int a = 0; a < 3; ++a) { hp.bmin[a] = bbox_min3[a]; hp.bmax[a] = bbox_max3[a]; }
+    fill_cells(hp.cell, bbox_min3, bbox_max3, level_res, n_levels);
+    hp.chunk_base = (int)chunk_base;
+    hp.nchunks = (int)(chunk_base + nch);
+    hipLaunchKernelGGL(hash_encode_bwd_kernel<3>, dim3((unsigned)nch, n_levels), dim3(256), 0, as_stream(stream),
+                       d_xyz, n_points, hp, d_dfeat, feat_stride_point, feat_stride_level);
+    NERF_CHECK_LAUNCH("hash_encode_bwd_bin");
+    return NERF_OK;
+}
+
+extern "C" int nerf_hash_encode_bwd_owner(int n_levels, int log2_T, int64_t n_chunks, int64_t chunk_capacity,
+                                          float* const* d_dtables, int deterministic, void* d_workspace,
+                                          size_t workspace_bytes, void* stream) {
+    HashGradParams hp{};
+    const int rc = bin_layout("hash_encode_bwd_owner", n_levels, log2_T, chunk_capacity, deterministic, d_workspace,
+                              workspace_bytes, hp);
+    if (rc) return rc;
+    NERF_REQUIRE(n_chunks >= 0 && n_chunks <= chunk_capacity, "hash_encode_bwd_owner: n_chunks %lld of %lld",
+                 (long long)n_chunks, (long long)chunk_capacity);
+    NERF_REQUIRE(d_dtables, "hash_encode_bwd_owner: null grad tables");
+    for (int l = 0; l < n_levels; ++l) {
+        NERF_REQUIRE(d_dtables[l], "hash_encode_bwd_owner: grad table %d is null", l);
+        hp.dtables[l] = d_dtables[l];
+    }
+    if (n_chunks == 0) return NERF_OK;
+    hp.nchunks = (int)n_chunks;
+    const dim3 grid(1u << hp.owner_log2, n_levels);
+    if (deterministic)
+        hipLaunchKernelGGL((hash_bwd_owner_kernel<kSliceLog2Det, 1024, true>), grid, dim3(1024), 0, as_stream(stream),
+                           hp);
+    else
+        hipLaunchKernelGGL((hash_bwd_owner_kernel<kSliceLog2, 1024, false>), grid, dim3(1024), 0, as_stream(stream),
+                           hp);
+    NERF_CHECK_LAUNCH("hash_encode_bwd_owner");
+    return NERF_OK;
+}
+
+// No workspace: coalesced memory-side float atomics (never deterministic).
+extern "C" int nerf_hash_encode_bwd(const float* d_xyz, int64_t n_points, const float* bbox_min3,
+                                    const float* bbox_max3, const float* level_res, int n_levels, int log2_T,
+                                    const float* d_dfeat, int64_t feat_stride_point, int64_t feat_stride_level,
+                                    float* const* d_dtables, void* stream) {
     NERF_REQUIRE(n_points >= 0, "hash_encode_bwd: n_points < 0");
     NERF_REQUIRE(n_levels >= 1 && n_levels <= NERF_MAX_LEVELS, "hash_encode_bwd: n_levels %d", n_levels);
     NERF_REQUIRE(log2_T >= 1 && log2_T <= 30, "hash_encode_bwd: log2_T %d", log2_T);
@@ -510,132 +661,35 @@ static int hash_encode_bwd_impl(const float* d_xyz, int64_t n_points, const floa
     for (int a = 0; a < 3; ++a) { hp.bmin[a] = bbox_min3[a]; hp.bmax[a] = bbox_max3[a]; }
     fill_cells(hp.cell, bbox_min3, bbox_max3, level_res, n_levels);
     hp.mask = (uint32_t)((1u << log2_T) - 1u);
-    BinPlan B{};
-    const int mode = (d_workspace != nullptr && make_bin_plan(n_levels, log2_T, n_points, B)) ? 3 : 1;
-    if (mode == 3) {
-        NERF_REQUIRE(workspace_bytes >= B.total,
-                     "hash_encode_bwd: workspace %zu B < %zu B (nerf_hash_encode_bwd_workspace_bytes)",
-                     workspace_bytes, B.total);
-        char* ws = static_cast<char*>(d_workspace);
-        hp.bin_g = reinterpret_cast<float2*>(ws + B.off_g);
-        hp.bin_h = reinterpret_cast<uint16_t*>(ws + B.off_h);
-        hp.bin_seg = reinterpret_cast<uint32_t*>(ws + B.off_off);
-        hp.nchunks = B.nchunks;
-        hp.chunk_base = 0;
-        hp.chunk_stride = B.nchunks;
-        hp.slice_log2 = B.slice_log2;
-        hp.owner_log2 = B.owner_log2;
-    }
-    const dim3 grid(blocks_for(n_points, 256), n_levels);
-    if (mode == 1) {
-        hipLaunchKernelGGL(hash_encode_bwd_kernel<1>, grid, dim3(256), 0, as_stream(stream), d_xyz, n_points, hp,
-                           d_dfeat, feat_stride_point, feat_stride_level);
-    } else {
-        hipLaunchKernelGGL(hash_encode_bwd_kernel<3>, grid, dim3(256), 0, as_stream(stream), d_xyz, n_points, hp,
-                           d_dfeat, feat_stride_point, feat_stride_level);
-        NERF_CHECK_LAUNCH("hash_encode_bwd (bin)");
-        hipLaunchKernelGGL((hash_bwd_owner_kernel<kSliceLog2, 1024>), dim3(1u << B.owner_log2, n_levels), dim3(1024), 0,
-                           as_stream(stream), hp);
-    }
+    hipLaunchKernelGGL(hash_encode_bwd_kernel<1>, dim3(blocks_for(n_points, 256), n_levels), dim3(256), 0,
+                       as_stream(stream), d_xyz, n_points, hp, d_dfeat, feat_stride_point, feat_stride_level);
     NERF_CHECK_LAUNCH("hash_encode_bwd");
     return NERF_OK;
 }
 
-extern "C" size_t nerf_hash_encode_bwd_workspace_bytes(int n_levels, int log2_T, int64_t n_points) {
-    BinPlan B{};
-    if (n_levels < 1 || n_levels > NERF_MAX_LEVELS || !make_bin_plan(n_levels, log2_T, n_points, B)) return 0;
-    return B.total;
-}
-
-extern "C" int nerf_hash_encode_bwd(const float* d_xyz, int64_t n_points, const float* bbox_min3,
-                                    const float* bbox_max3, const float* level_res, int n_levels, int log2_T,
-                                    const float* d_dfeat, int64_t feat_stride_point, int64_t feat_stride_level,
-                                    float* const* d_dtables, void* stream) {
-    return hash_encode_bwd_impl(d_xyz, n_points, bbox_min3, bbox_max3, level_res, n_levels, log2_T, d_dfeat,
-                                feat_stride_point, feat_stride_level, d_dtables, nullptr, 0, stream);
-}
-
+// Binned path in one call: bin chunks [0, n) then the owner pass over them. A NULL workspace (or a
+// log2_T without a binned path and deterministic == 0) falls back to nerf_hash_encode_bwd.
 extern "C" int nerf_hash_encode_bwd_ws(const float* d_xyz, int64_t n_points, const float* bbox_min3,
                                        const float* bbox_max3, const float* level_res, int n_levels, int log2_T,
                                        const float* d_dfeat, int64_t feat_stride_point, int64_t feat_stride_level,
-                                       float* const* d_dtables, void* d_workspace, size_t workspace_bytes,
-                                       void* stream) {
-    return hash_encode_bwd_impl(d_xyz, n_points, bbox_min3, bbox_max3, level_res, n_levels, log2_T, d_dfeat,
-                                feat_stride_point, feat_stride_level, d_dtables, d_workspace, workspace_bytes,
-                                stream);
-}
-
-// ---- split binned backward: several bin launches, one owner launch --------------------------
-// The fine and the coarse pass of a training iteration scatter into the same tables; binning both
-// into one workspace (side by side, chunk_base apart) and summing them with ONE owner launch pays
-// the owner's per-launch costs (LDS clear, slice flush = a read-modify-write of every table row)
-// once per iteration instead of once per pass.
-static int bin_layout(const char* who, int n_levels, int log2_T, int64_t chunk_capacity, void* d_workspace,
-                      size_t workspace_bytes, HashGradParams& hp) {
-    NERF_REQUIRE(n_levels >= 1 && n_levels <= NERF_MAX_LEVELS, "%s: n_levels %d", who, n_levels);
-    NERF_REQUIRE(chunk_capacity >= 1 && chunk_capacity <= (int64_t)1 << 26, "%s: chunk_capacity %lld", who,
-                 (long long)chunk_capacity);
+                                       float* const* d_dtables, int deterministic, void* d_workspace,
+                                       size_t workspace_bytes, void* stream) {
+    NERF_REQUIRE(n_points >= 0, "hash_encode_bwd: n_points < 0");
     BinPlan B{};
-    NERF_REQUIRE(make_bin_plan(n_levels, log2_T, chunk_capacity * 256, B), "%s: no binned path for log2_T %d", who,
-                 log2_T);
-    NERF_REQUIRE(d_workspace != nullptr && workspace_bytes >= B.total,
-                 "%s: workspace %zu B < %zu B (nerf_hash_encode_bwd_workspace_bytes(L, log2_T, 256 * capacity))", who,
-                 workspace_bytes, B.total);
-    char* ws = static_cast<char*>(d_workspace);
-    hp.bin_g = reinterpret_cast<float2*>(ws + B.off_g);
-    hp.bin_h = reinterpret_cast<uint16_t*>(ws + B.off_h);
-    hp.bin_seg = reinterpret_cast<uint32_t*>(ws + B.off_off);
-    hp.chunk_stride = B.nchunks;
-    hp.slice_log2 = B.slice_log2;
-    hp.owner_log2 = B.owner_log2;
-    hp.mask = (uint32_t)((1u << log2_T) - 1u);
-    return NERF_OK;
-}
-
-extern "C" int nerf_hash_encode_bwd_bin(const float* d_xyz, int64_t n_points, const float* bbox_min3,
-                                        const float* bbox_max3, const float* level_res, int n_levels, int log2_T,
-                                        const float* d_dfeat, int64_t feat_stride_point, int64_t feat_stride_level,
-                                        int64_t chunk_base, int64_t chunk_capacity, void* d_workspace,
-                                        size_t workspace_bytes, void* stream) {
-    NERF_REQUIRE(n_points >= 0, "hash_encode_bwd_bin: n_points < 0");
-    NERF_REQUIRE(d_xyz && d_dfeat && level_res && bbox_min3 && bbox_max3, "hash_encode_bwd_bin: null arg");
-    HashGradParams hp{};
-    const int rc = bin_layout("hash_encode_bwd_bin", n_levels, log2_T, chunk_capacity, d_workspace, workspace_bytes,
-                              hp);
-    if (rc) return rc;
-    const int64_t nch = (n_points + 255) / 256;
-    NERF_REQUIRE(chunk_base >= 0 && chunk_base + nch <= chunk_capacity,
-                 "hash_encode_bwd_bin: chunks [%lld, %lld) exceed the capacity %lld", (long long)chunk_base,
-                 (long long)(chunk_base + nch), (long long)chunk_capacity);
-    if (n_points == 0) return NERF_OK;
-    for (int a = 0; a < 3; ++a) { hp.bmin[a] = bbox_min3[a]; hp.bmax[a] = bbox_max3[a]; }
-    fill_cells(hp.cell, bbox_min3, bbox_max3, level_res, n_levels);
-    hp.chunk_base = (int)chunk_base;
-    hp.nchunks = (int)(chunk_base + nch);
-    hipLaunchKernelGGL(hash_encode_bwd_kernel<3>, dim3((unsigned)nch, n_levels), dim3(256), 0, as_stream(stream),
-                       d_xyz, n_points, hp, d_dfeat, feat_stride_point, feat_stride_level);
-    NERF_CHECK_LAUNCH("hash_encode_bwd_bin");
-    return NERF_OK;
-}
-
-extern "C" int nerf_hash_encode_bwd_owner(int n_levels, int log2_T, int64_t n_chunks, int64_t chunk_capacity,
-                                          float* const* d_dtables, void* d_workspace, size_t workspace_bytes,
-                                          void* stream) {
-    HashGradParams hp{};
-    const int rc = bin_layout("hash_encode_bwd_owner", n_levels, log2_T, chunk_capacity, d_workspace,
-                              workspace_bytes, hp);
-    if (rc) return rc;
-    NERF_REQUIRE(n_chunks >= 0 && n_chunks <= chunk_capacity, "hash_encode_bwd_owner: n_chunks %lld of %lld",
-                 (long long)n_chunks, (long long)chunk_capacity);
-    NERF_REQUIRE(d_dtables, "hash_encode_bwd_owner: null grad tables");
-    for (int l = 0; l < n_levels; ++l) {
-        NERF_REQUIRE(d_dtables[l], "hash_encode_bwd_owner: grad table %d is null", l);
-        hp.dtables[l] = d_dtables[l];
+    const bool binned = d_workspace != nullptr && n_levels >= 1 && n_levels <= NERF_MAX_LEVELS &&
+                        make_bin_plan(n_levels, log2_T, n_points, B, deterministic != 0);
+    if (!binned) {
+        NERF_REQUIRE(!deterministic, "hash_encode_bwd: the deterministic mode needs the binned path (a workspace of "
+                                     "nerf_hash_encode_bwd_workspace_bytes(L, log2_T, P, 1) > 0 bytes)");
+        return nerf_hash_encode_bwd(d_xyz, n_points, bbox_min3, bbox_max3, level_res, n_levels, log2_T, d_dfeat,
+                                    feat_stride_point, feat_stride_level, d_dtables, stream);
     }
-    if (n_chunks == 0) return NERF_OK;
-    hp.nchunks = (int)n_chunks;
-    hipLaunchKernelGGL((hash_bwd_owner_kernel<kSliceLog2, 1024>), dim3(1u << hp.owner_log2, n_levels), dim3(1024), 0,
-                       as_stream(stream), hp);
-    NERF_CHECK_LAUNCH("hash_encode_bwd_owner");
-    return NERF_OK;
+    if (n_points == 0) return NERF_OK;
+    const int64_t nch = (n_points + 255) / 256;
+    int rc = nerf_hash_encode_bwd_bin(d_xyz, n_points, bbox_min3, bbox_max3, level_res, n_levels, log2_T, d_dfeat,
+                                      feat_stride_point, feat_stride_level, 0, nch, deterministic, d_workspace,
+                                      workspace_bytes, stream);
+    if (rc) return rc;
+    return nerf_hash_encode_bwd_owner(n_levels, log2_T, nch, nch, d_dtables, deterministic, d_workspace,
+                                      workspace_bytes, stream);
 }

@@ -11,7 +11,7 @@ import torch
 import torch.nn as nn
 
 from . import _lib
-from .hashgrid import HashEmbedder, SHEncoder, accumulate_grad_buffers, hash_encode_bwd
+from .hashgrid import HashEmbedder, SHEncoder, accumulate_grad_buffers, hash_encode_bwd, pending_bins
 from .quantization import LearnedBitwidthQuantizer, calibrate_from_stats, new_stats, quant_records
 
 
@@ -192,20 +192,129 @@ class FieldFn(torch.autograd.Function):
         head_grads, dgeo = (None,) * ctx.n_head, None
         if head:
             g, dgeo, head_grads = _head_backward(o16, keep, head, g, ctx.needs_input_grad[6 + n_tab + 5:])
-        need_tab = any(t.requires_grad for t in tables)
-        dfeat = torch.empty_like(feat) if need_tab else None
-        if any(w.requires_grad for w in weights) or need_tab:
-            grads = _grads_struct(weights) if any(w.requires_grad for w in weights) else _scratch_grads(weights)
-            _lib.call("nerf_mlp_bwd_q", _lib.ptr(feat, "feat"), 2, 2 * P, None, 0, _lib.ptr(viewdirs, "viewdirs"),
-                      ctx.spr, None if head else _lib.ptr(keep, "keep", dtype=torch.bool), P,
-                      _weights_struct(weights, w0q), _lib.ptr(g, "grad_raw"), grads,
-                      _lib.ptr(dfeat, "dfeat", allow_none=True), None, _lib.ptr(dgeo, "dgeo", allow_none=True),
-                      _lib.ptr(arec, "act_record", allow_none=True), _lib.stream())
-        if need_tab:
-            tgrads = accumulate_grad_buffers(tables)
-            if not ctx.zero_tab_grad:
-                hash_encode_bwd(pts, ctx.embedder._meta, dfeat, 2, 2 * P, tgrads)
+        need_tab = any(t.requires_grad for t in tables) and not ctx.zero_tab_grad
+        need_w = any(w.requires_grad for w in weights)
+        if need_w or need_tab:
+            job = _FieldJob(pts, viewdirs, feat, keep, head, w0q, arec, weights, tables, g, dgeo, ctx, need_w,
+                            need_tab)
+            if torch._C._current_graph_task_id() != -1:
+                _pending_field(pts.device).add(job)   # launched with the pass's other FieldFn backwards
+            else:
+                _run_field_jobs([job])
         return (None,) * (6 + n_tab + len(weights)) + tuple(head_grads)
+
+
+class _FieldJob:
+    """Everything one FieldFn backward needs after its autograd node has returned."""
+
+    def __init__(self, pts, viewdirs, feat, keep, head, w0q, arec, weights, tables, g, dgeo, ctx, need_w, need_tab):
+        self.pts, self.viewdirs, self.feat, self.keep, self.head = pts, viewdirs, feat, keep, head
+        self.w0q, self.arec, self.weights, self.tables, self.g, self.dgeo = w0q, arec, weights, tables, g, dgeo
+        self.spr, self.meta, self.need_w, self.need_tab = ctx.spr, ctx.embedder._meta, need_w, need_tab
+        self.stream = torch.cuda.current_stream()
+
+    def mlp_job(self):
+        P = self.pts.shape[0]
+        self.dfeat = torch.empty_like(self.feat) if self.need_tab else None
+        j = _lib.MlpBwdJob()
+        j.feat, j.feat_stride_point, j.feat_stride_level = _lib.ptr(self.feat, "feat"), 2, 2 * P
+        j.viewdirs, j.samples_per_ray = _lib.ptr(self.viewdirs, "viewdirs"), self.spr
+        j.keep = None if self.head else _lib.ptr(self.keep, "keep", dtype=torch.bool)
+        j.n_points = P
+        j.weights = _weights_struct(self.weights, self.w0q)
+        j.graw = _lib.ptr(self.g, "grad_raw")
+        j.grads = _grads_struct(self.weights) if self.need_w else _scratch_grads(self.weights)
+        j.dfeat = _lib.ptr(self.dfeat, "dfeat", allow_none=True)
+        j.dgeo = _lib.ptr(self.dgeo, "dgeo", allow_none=True)
+        j.act_qrec = _lib.ptr(self.arec, "act_record", allow_none=True)
+        return j
+
+
+_DETERMINISTIC = {"on": False, "ws": {}}
+
+
+def set_deterministic(enabled=True):
+    """Bitwise-reproducible backward (the `deterministic` flag of SURVEY.md §8(b)'s hash_encode_bwd):
+    MLP weight gradients reduced over blocks in a fixed order and the hash-table gradients summed in
+    exact integer fixed point (csrc/field_x6.hip mlp_wgrad_reduce, csrc/hashgrid.hip owner<DET>)."""
+    from . import hashgrid
+    _DETERMINISTIC["on"] = bool(enabled)
+    hashgrid.set_deterministic(enabled)
+    if enabled and torch.cuda.is_available():   # allocated now, not inside a later HIP-graph capture
+        _det_workspace(torch.device("cuda", torch.cuda.current_device()))
+
+
+def deterministic():
+    return _DETERMINISTIC["on"]
+
+
+def _det_workspace(device):
+    if not _DETERMINISTIC["on"]:
+        return None
+    key = str(device)
+    ws = _DETERMINISTIC["ws"].get(key)
+    if ws is None:
+        n = int(_lib.load().nerf_mlp_bwd_det_workspace_bytes()) // 4
+        ws = _DETERMINISTIC["ws"][key] = torch.empty(n, device=device, dtype=torch.float32)
+    return ws
+
+
+def _run_field_jobs(jobs):
+    """MLP backwards of up to two nets per launch (nerf_mlp_bwd_batch), then their hash backwards
+    binned side by side and summed by one owner pass."""
+    ws = _det_workspace(jobs[0].pts.device)
+    for k in range(0, len(jobs), _lib.MLP_MAX_JOBS):
+        part = jobs[k:k + _lib.MLP_MAX_JOBS]
+        arr = (_lib.MlpBwdJob * len(part))(*[j.mlp_job() for j in part])
+        _lib.call("nerf_mlp_bwd_batch", arr, len(part), _lib.ptr(ws, "det_workspace", allow_none=True),
+                  0 if ws is None else ws.numel() * 4, _lib.stream())
+    tab_jobs = [j for j in jobs if j.need_tab]
+    if tab_jobs:
+        pending_bins(tab_jobs[0].pts.device).reserve(sum((j.pts.shape[0] + 255) // 256 for j in tab_jobs))
+    for j in tab_jobs:
+        P = j.pts.shape[0]
+        hash_encode_bwd(j.pts, j.meta, j.dfeat, 2, 2 * P, accumulate_grad_buffers(j.tables), defer=True, queue=False)
+    if tab_jobs:
+        pending_bins(tab_jobs[0].pts.device).flush()
+    for j in jobs:
+        j.dfeat = None
+
+
+class _PendingField:
+    """FieldFn backwards of the running autograd pass (per device). The coarse and the fine field of a
+    training iteration are independent autograd subgraphs whose MLP backwards are both ready once
+    autograd reaches the first of them; they are queued here and launched together as the pass's
+    final callback (one nerf_mlp_bwd_batch launch for both nets, then one owner pass for both hash
+    backwards). Under a HIP-graph capture the callback is captured like the rest of the backward."""
+
+    def __init__(self):
+        self.jobs = []
+
+    def add(self, job):
+        if not self.jobs:
+            torch.autograd.Variable._execution_engine.queue_callback(self.flush)
+        self.jobs.append(job)
+
+    def flush(self):
+        jobs, self.jobs = self.jobs, []
+        if not jobs:
+            return
+        stream = jobs[0].stream
+        for j in jobs[1:]:
+            if j.stream != stream:
+                stream.wait_stream(j.stream)
+        with torch.cuda.stream(stream):
+            _run_field_jobs(jobs)
+        cur = torch.cuda.current_stream()
+        if cur != stream:
+            cur.wait_stream(stream)
+
+
+_PENDING_FIELD = {}
+
+
+def _pending_field(device):
+    return _PENDING_FIELD.setdefault(str(device), _PendingField())
 
 
 class NeRFSmall(nn.Module):

@@ -74,6 +74,19 @@ class HashEncodeFn(torch.autograd.Function):
         return (None, None, None) + (None,) * len(tables)
 
 
+_DET = {"on": False}
+
+
+def set_deterministic(enabled=True):
+    """Bitwise-reproducible hash-table gradients: the binned backward's owner pass sums in exact
+    integer fixed point (nerf_hash_encode_bwd_* with deterministic = 1)."""
+    _DET["on"] = bool(enabled)
+
+
+def deterministic():
+    return _DET["on"]
+
+
 _BWD_WORKSPACE = {}
 # Workspaces replaced by a larger one are never freed: a HIP graph captured earlier (graphs.
 # GraphedTrainStep) keeps their addresses in its kernel arguments, and the caching allocator would
@@ -86,8 +99,11 @@ def bwd_workspace(n_levels, log2_T, n_points, device):
     """Device workspace of nerf_hash_encode_bwd_ws (the binned backward's per-chunk regions), one per
     device, grown to the largest (n_levels, n_points) seen; calls that share it run in stream order
     (autograd's backward stream). None when the binned path does not apply (log2_T > 19)."""
-    need = int(_lib.load().nerf_hash_encode_bwd_workspace_bytes(n_levels, log2_T, n_points))
+    det = int(_DET["on"])
+    need = int(_lib.load().nerf_hash_encode_bwd_workspace_bytes(n_levels, log2_T, n_points, det))
     if need == 0:
+        if det:
+            raise NotImplementedError(f"deterministic hash backward: no binned path for log2_T {log2_T} (<= 19)")
         return None, 0
     key = str(device)
     hit = _BWD_WORKSPACE.get(key)
@@ -113,20 +129,27 @@ class _PendingBins:
     def flush(self):
         if self.used == 0:
             return
-        L, log2_T, _ = self.tag
+        L, log2_T, _, det = self.tag
         with torch.cuda.stream(self.stream):
             _lib.call("nerf_hash_encode_bwd_owner", L, log2_T, self.used, self.cap,
-                      _lib.ptr_array(self.grads, "grad_tables"), _lib.ptr(self.ws, "workspace", dtype=torch.uint8),
+                      _lib.ptr_array(self.grads, "grad_tables"), det, _lib.ptr(self.ws, "workspace", dtype=torch.uint8),
                       self.ws.numel(), _lib.stream())
         cur = torch.cuda.current_stream()
         if cur != self.stream:
             cur.wait_stream(self.stream)
         self.used, self.tag, self.grads = 0, None, None
 
-    def add(self, xyz, meta, dfeat, sp, sl, grad_tables):
+    def reserve(self, n_chunks):
+        """Size the next workspace for n_chunks chunks, so that a batch whose total is known up front
+        bins into ONE workspace and is summed by ONE owner pass (the sums then do not depend on the
+        workspace history: the deterministic mode's results are reproducible from the first call)."""
+        self.peak = max(self.peak, n_chunks)
+
+    def add(self, xyz, meta, dfeat, sp, sl, grad_tables, queue=True):
         L, log2_T, P = len(grad_tables), meta["log2_T"], xyz.shape[0]
         n_ch = (P + 255) // 256
-        tag = (L, log2_T, tuple(g.data_ptr() for g in grad_tables))
+        det = int(_DET["on"])
+        tag = (L, log2_T, tuple(g.data_ptr() for g in grad_tables), det)
         total = (self.used if self.tag == tag else 0) + n_ch
         self.peak = max(self.peak, total)     # the next pass sizes its workspace for this
         if self.used and (self.tag != tag or total > self.cap):
@@ -134,16 +157,17 @@ class _PendingBins:
         lib = _lib.load()
         if self.used == 0:
             cap = max(self.peak, n_ch)
-            need = int(lib.nerf_hash_encode_bwd_workspace_bytes(L, log2_T, 256 * cap))
+            need = int(lib.nerf_hash_encode_bwd_workspace_bytes(L, log2_T, 256 * cap, det))
             if self.ws is None or self.ws.numel() < need:
                 if self.ws is not None:
                     _RETIRED.append(self.ws)     # a captured graph may still bin into it
                 self.ws = torch.empty(need, dtype=torch.uint8, device=xyz.device)
             self.cap = cap
             self.tag, self.grads, self.stream = tag, list(grad_tables), torch.cuda.current_stream()
-            torch.autograd.Variable._execution_engine.queue_callback(self.flush)
+            if queue:
+                torch.autograd.Variable._execution_engine.queue_callback(self.flush)
         _lib.call("nerf_hash_encode_bwd_bin", _lib.ptr(xyz, "xyz"), P, meta["bmin"], meta["bmax"], meta["res"], L,
-                  log2_T, _lib.ptr(dfeat, "grad_feat"), sp, sl, self.used, self.cap,
+                  log2_T, _lib.ptr(dfeat, "grad_feat"), sp, sl, self.used, self.cap, det,
                   _lib.ptr(self.ws, "workspace", dtype=torch.uint8), self.ws.numel(), _lib.stream())
         self.used += n_ch
 
@@ -151,21 +175,27 @@ class _PendingBins:
 _PENDING = {}
 
 
-def hash_encode_bwd(xyz, meta, dfeat, sp, sl, grad_tables, defer=None):
+def pending_bins(device):
+    return _PENDING.setdefault(str(device), _PendingBins())
+
+
+def hash_encode_bwd(xyz, meta, dfeat, sp, sl, grad_tables, defer=None, queue=True):
     """Scatter-add d feat into the gradient tables (hash_encoding.py:82-107 autograd; csrc/hashgrid.hip).
     defer (default: inside an autograd backward pass) bins now and leaves the owner pass to the end
-    of the pass (_PendingBins), shared with the other hash backwards of the pass."""
+    of the pass (_PendingBins), shared with the other hash backwards of the pass; queue=False leaves
+    the owner pass to the caller (pending_bins(device).flush())."""
     L, log2_T, P = len(grad_tables), meta["log2_T"], xyz.shape[0]
     if defer is None:
         defer = torch._C._current_graph_task_id() != -1
-    if defer and P > 0 and int(_lib.load().nerf_hash_encode_bwd_workspace_bytes(L, log2_T, P)) > 0:
-        _PENDING.setdefault(str(xyz.device), _PendingBins()).add(xyz, meta, dfeat, sp, sl, grad_tables)
+    det = int(_DET["on"])
+    if defer and P > 0 and int(_lib.load().nerf_hash_encode_bwd_workspace_bytes(L, log2_T, P, det)) > 0:
+        pending_bins(xyz.device).add(xyz, meta, dfeat, sp, sl, grad_tables, queue=queue)
         return
     ws, nbytes = bwd_workspace(len(grad_tables), meta["log2_T"], xyz.shape[0], xyz.device)
     _lib.call("nerf_hash_encode_bwd_ws", _lib.ptr(xyz, "xyz"), xyz.shape[0], meta["bmin"], meta["bmax"],
               meta["res"], len(grad_tables), meta["log2_T"], _lib.ptr(dfeat, "grad_feat"), sp, sl,
-              _lib.ptr_array(grad_tables, "grad_tables"), _lib.ptr(ws, "workspace", dtype=torch.uint8, allow_none=True),
-              nbytes, _lib.stream())
+              _lib.ptr_array(grad_tables, "grad_tables"), det,
+              _lib.ptr(ws, "workspace", dtype=torch.uint8, allow_none=True), nbytes, _lib.stream())
 
 
 class HashEmbedder(nn.Module):
@@ -309,3 +339,4 @@ class SHEncoder(nn.Module):
         out = torch.empty(d.shape[0], 16, device=d.device, dtype=torch.float32)
         _lib.call("nerf_sh4_fwd", _lib.ptr(d, "dirs"), d.shape[0], _lib.ptr(out, "sh"), _lib.stream())
         return out.reshape(*input.shape[:-1], 16)
+

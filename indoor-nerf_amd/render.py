@@ -27,6 +27,27 @@ to8b = lambda x: (255 * np.clip(x, 0, 1)).astype(np.uint8)  # noqa: E731
 _LINSPACE = {}
 _SEED_GEN = None
 
+# run_nerf.py:40 DEBUG: when True, render_rays tests every returned tensor for NaN/Inf (one fused
+# device count, csrc/checks.hip, and one host read per call) and prints the reference's message.
+DEBUG = False
+
+
+def check_numerics(ret):
+    """run_nerf.py:545-547 over the tensors of `ret`; returns the keys that hold NaN/Inf."""
+    items = [(k, v) for k, v in ret.items() if torch.is_tensor(v) and v.dtype == torch.float32 and v.is_cuda]
+    bad = []
+    for i in range(0, len(items), _lib.MAX_CHECK):
+        part = items[i:i + _lib.MAX_CHECK]
+        ts = [v.contiguous() for _, v in part]
+        counts = torch.empty(len(ts), dtype=torch.int32, device=ts[0].device)
+        sizes = (_lib.c_i64 * len(ts))(*[t.numel() for t in ts])
+        _lib.call("nerf_count_nonfinite", _lib.ptr_array(ts, "ret"), sizes, len(ts),
+                  _lib.ptr(counts, "counts", dtype=torch.int32), _lib.stream())
+        bad += [k for (k, _), c in zip(part, counts.tolist()) if c]
+    for k in bad:
+        print(f"! [Numerical Error] {k} contains nan or inf.")
+    return bad
+
 
 def _linspace(n, device):
     key = (n, str(device))
@@ -212,6 +233,8 @@ def render_rays(ray_batch, network_fn, network_query_fn, N_samples, embed_fn=Non
         ret["normal_map"] = normal_map
     if retraw:
         ret["raw"] = raw
+    if DEBUG:
+        check_numerics(ret)
     return ret
 
 

@@ -397,6 +397,94 @@ def gen_train(ref, out):
     np.savez_compressed(os.path.join(out, "f10_train.npz"), **d)
 
 
+CONVERGE = dict(iters=300, R=256, every=20, lrate=5e-3, lrate_decay=500, sparsity=1e-10, table_scale=1e-4,
+                table_salt=19, seeds=(30, 31), batch_seed=20, threads=(8, 4))
+
+
+def converge_run(ref, c, threads):
+    """One reference training run of F19 with `threads` CPU threads (torch's CPU kernels split their
+    reductions by thread, so two thread counts are two runs of the same algorithm whose float sums
+    differ in order: the reference's own run-to-run spread)."""
+    torch.set_num_threads(threads)
+    (ro, rd, rgb), (eo, ed, ergb), (no, nd, nrgb) = tables_convergence()
+    emb = make_embedder(ref, 1024, closed_form_table(scale=c["table_scale"], salt=c["table_salt"]))
+    coarse, fine = make_mlp(ref, c["seeds"][0]), make_mlp(ref, c["seeds"][1])
+    init = {**mlp_arrays(coarse, "coarse0_"), **mlp_arrays(fine, "fine0_")}
+    grad_vars = list(coarse.parameters()) + list(fine.parameters())
+    opt = ref.radam.RAdam([{"params": grad_vars, "weight_decay": 1e-6},
+                           {"params": list(emb.parameters()), "eps": 1e-15}], lr=c["lrate"], betas=(0.9, 0.99))
+    kw = build_render_kwargs(ref, emb, coarse, fine, 64, 128, 1.0, 0.0, False)
+    kw_test = dict(kw, perturb=0.0, raw_noise_std=0.0)
+    rng = np.random.RandomState(c["batch_seed"])
+    batches = np.stack([rng.choice(ro.shape[0], c["R"], replace=False) for _ in range(c["iters"])]).astype(np.int32)
+    train_psnr, eval_psnr, novel_psnr, eval_iters = [], [], [], []
+
+    def psnr_of(o, dd, target):
+        with torch.no_grad():
+            out_rgb, _, _, _ = ref.rn.render(800, 800, None, chunk=32768, rays=(torch.from_numpy(o), torch.from_numpy(dd)),
+                                             **kw_test)
+        return ref.h.mse2psnr(ref.h.img2mse(out_rgb, torch.from_numpy(target))).item()
+
+    def evaluate():
+        eval_psnr.append(psnr_of(eo, ed, ergb))
+        novel_psnr.append(psnr_of(no, nd, nrgb))
+
+    eval_iters.append(0)
+    evaluate()
+    for it in range(1, c["iters"] + 1):
+        idx = batches[it - 1]
+        r_o, r_d, tgt = (torch.from_numpy(a[idx]) for a in (ro, rd, rgb))
+        out_rgb, _, _, extras = ref.rn.render(800, 800, None, chunk=32768, rays=(r_o, r_d), retraw=True, pytest=True,
+                                              **kw)
+        opt.zero_grad()
+        img_loss = ref.h.img2mse(out_rgb, tgt)
+        loss = img_loss + ref.h.img2mse(extras["rgb0"], tgt)
+        loss = loss + c["sparsity"] * (extras["sparsity_loss"].sum() + extras["sparsity_loss0"].sum())
+        loss.backward()
+        opt.step()
+        new_lrate = c["lrate"] * (0.1 ** (it / (c["lrate_decay"] * 1000)))
+        for g in opt.param_groups:
+            g["lr"] = new_lrate
+        train_psnr.append(ref.h.mse2psnr(img_loss.detach()).item())
+        if it % c["every"] == 0:
+            eval_iters.append(it)
+            evaluate()
+            print(f"  converge ({threads} threads) it {it}: train {train_psnr[-1]:.3f} dB, held-out "
+                  f"{eval_psnr[-1]:.3f} dB, novel view {novel_psnr[-1]:.3f} dB", flush=True)
+    torch.set_num_threads(8)
+    return init, batches, np.array(eval_iters), dict(train_psnr=np.array(train_psnr), eval_psnr=np.array(eval_psnr),
+                                                     novel_psnr=np.array(novel_psnr))
+
+
+def gen_converge(ref, out, iters=None):
+    """F19: the reference TRAINED for `iters` iterations on a procedural two-sphere scene
+    (tables.convergence_rays), as train() runs them (run_nerf.py:1007-1037, 1161-1162, 1289-1293):
+    render coarse 64 + fine 128 with pytest=True draws, img + img0 MSE + sparsity, backward, RAdam
+    with the create_nerf param groups, lr decay. R rays per iteration drawn from the pool with a
+    seeded RandomState (the indices are stored). TV loss is off (its torch.randint draws would have
+    to be replayed every iteration). Init: reference-scale tables (closed form, |v| <= 1e-4) and
+    seeded nn.Linear init. Every `every` iterations: PSNR of held-out pixels of the training views
+    and of a novel view, with the test-time kwargs (perturb 0, no noise); plus the PSNR of every
+    training batch. Two runs, with 8 and with 4 CPU threads (keys *_b): the reference's own
+    run-to-run spread, against which the HIP path's deviation is judged."""
+    c = dict(CONVERGE)
+    if iters is not None:
+        c["iters"] = iters
+    d = {}
+    for k, threads in enumerate(c["threads"]):
+        init, batches, eval_iters, curves = converge_run(ref, c, threads)
+        suffix = "" if k == 0 else "_b"
+        d.update({name + suffix: v for name, v in curves.items()})
+    d.update(init)
+    d.update(batches=batches, eval_iters=eval_iters, config=np.array(repr(c)))
+    np.savez_compressed(os.path.join(out, "f19_converge.npz"), **d)
+
+
+def tables_convergence():
+    from tables import convergence_rays
+    return convergence_rays()
+
+
 def gen_quant(ref, out):
     rng = np.random.RandomState(11)
     d = {}
@@ -825,7 +913,8 @@ def main(only=None):
     gens = [("voxel", None), ("hash", gen_hash), ("sh", gen_sh), ("mlp", gen_mlp), ("composite", gen_composite),
             ("pdf", gen_pdf), ("render", gen_render), ("quant", gen_quant), ("tv", gen_tv), ("train", gen_train),
             ("normals", gen_normals), ("acaq", gen_acaq),
-            ("llff", gen_llff), ("rays", gen_rays), ("data", gen_data), ("priors", gen_priors)]
+            ("llff", gen_llff), ("rays", gen_rays), ("data", gen_data), ("priors", gen_priors),
+            ("converge", gen_converge)]
     if not only or "levels" in only or "voxel" in only:
         levels = gen_levels(ref, out)
         gen_voxel(ref, out, levels)

@@ -52,8 +52,9 @@ def pose_spherical(theta_deg, phi_deg, radius):
     return c2w.astype(np.float32)
 
 
-def synthetic_rays(n_rays, H=800, W=800, pose_index=3, seed=0):
-    """Pinhole rays of one spiral pose, n_rays pixels chosen by a seeded permutation.
+def synthetic_rays(n_rays, H=800, W=800, pose_index=3, seed=0, skip=0):
+    """Pinhole rays of one spiral pose, n_rays pixels chosen by a seeded permutation (entries
+    skip .. skip + n_rays of it, so two calls with disjoint ranges give disjoint pixels).
 
     Returns rays_o, rays_d as float32 [n_rays, 3] (d unnormalised, as get_rays makes them)."""
     camera_angle_x = 0.6911112070083618
@@ -61,7 +62,7 @@ def synthetic_rays(n_rays, H=800, W=800, pose_index=3, seed=0):
     thetas = np.linspace(-180, 180, 101)[:-1]
     c2w = pose_spherical(thetas[pose_index], -30.0, 4.0311)
     rng = np.random.RandomState(seed)
-    pix = rng.permutation(H * W)[:n_rays]
+    pix = rng.permutation(H * W)[skip:skip + n_rays]
     i = (pix % W).astype(np.float32)
     j = (pix // W).astype(np.float32)
     dirs = np.stack([(i - 0.5 * W) / focal, -(j - 0.5 * H) / focal, -np.ones_like(i)], -1).astype(np.float32)
@@ -179,3 +180,49 @@ def make_tiny_scannet(root, scene="scene0000_00", H=12, W=16, seed=2):
         f.write(header.encode("ascii"))
         f.write(rec.tobytes())
     np.save(os.path.join(mdir, "vertices.npy"), verts)
+
+
+# ---- procedural scene for the convergence fixture (F19) ----------------------------------------
+# Two opaque spheres inside the lego AABB; a ray's target colour is the colour at its first hit
+# (inside near..far, in units of the unnormalised ray direction as render_rays samples z), else the
+# white background the Blender configs composite onto.
+SCENE_SPHERES = (((0.0, 0.0, 0.2), 1.1), ((1.3, 0.7, 0.4), 0.55))
+
+
+def _sphere_colour(k, n):
+    if k == 0:
+        return np.clip(0.5 + 0.45 * n, 0.0, 1.0)
+    return np.broadcast_to(np.array([0.9, 0.25, 0.1]), n.shape)
+
+
+def procedural_targets(rays_o, rays_d, near=2.0, far=6.0):
+    o, d = rays_o.astype(np.float64), rays_d.astype(np.float64)
+    best = np.full(o.shape[0], np.inf)
+    rgb = np.ones_like(o)
+    for k, (c, r) in enumerate(SCENE_SPHERES):
+        oc = o - np.array(c)
+        a = (d * d).sum(-1)
+        b = 2.0 * (oc * d).sum(-1)
+        cc = (oc * oc).sum(-1) - r * r
+        disc = b * b - 4 * a * cc
+        ok = disc > 0
+        t = np.where(ok, (-b - np.sqrt(np.maximum(disc, 0.0))) / (2 * a), np.inf)
+        hit = ok & (t >= near) & (t <= far) & (t < best)
+        n = (o + d * t[:, None] - np.array(c)) / r
+        rgb[hit] = _sphere_colour(k, n[hit])
+        best = np.where(hit, t, best)
+    return rgb.astype(np.float32)
+
+
+def convergence_rays(train_poses=(3, 15, 28, 40, 53, 65, 78, 90), n_per_pose=4096, n_eval_per_pose=256,
+                     novel_pose=34, n_novel=1024, H=200, W=200):
+    """Training pool (rays_o, rays_d, rgb [N,3]): n_per_pose pixels of each of eight spiral poses at
+    a 200 x 200 sensor. Held-out set: n_eval_per_pose OTHER pixels of the same poses (interpolation,
+    the PSNR the convergence test pins). Novel set: a pose between two training poses."""
+    tr = [synthetic_rays(n_per_pose, H=H, W=W, pose_index=p, seed=100 + p) for p in train_poses]
+    ev = [synthetic_rays(n_eval_per_pose, H=H, W=W, pose_index=p, seed=100 + p, skip=n_per_pose) for p in train_poses]
+    ro, rd = np.concatenate([t[0] for t in tr]), np.concatenate([t[1] for t in tr])
+    eo, ed = np.concatenate([t[0] for t in ev]), np.concatenate([t[1] for t in ev])
+    no, nd = synthetic_rays(n_novel, H=H, W=W, pose_index=novel_pose, seed=99)
+    return ((ro, rd, procedural_targets(ro, rd)), (eo, ed, procedural_targets(eo, ed)),
+            (no, nd, procedural_targets(no, nd)))

@@ -22,7 +22,7 @@ def test_library_exports_every_declared_symbol(nerf):
     for name in declared:
         assert hasattr(lib, name), f"libnerfhip.so does not export {name}"
     assert sorted(L.exported_symbols()) == declared, "ctypes signature table out of sync with the header"
-    assert lib.nerf_abi_version() == 1
+    assert lib.nerf_abi_version() == 2   # 2: deterministic flag of the binned hash backward
 
 
 def test_error_path_reports_message(nerf):
@@ -34,15 +34,25 @@ def test_error_path_reports_message(nerf):
     with pytest.raises(RuntimeError, match="S must be"):
         L.call("nerf_composite_fwd", None, 4, None, None, None, 4, 1000, 0, *([None] * 7), None)
     # split binned backward: the chunk range and the workspace size are checked before any launch
-    need = L.load().nerf_hash_encode_bwd_workspace_bytes(16, 19, 256 * 4)
+    need = L.load().nerf_hash_encode_bwd_workspace_bytes(16, 19, 256 * 4, 0)
     fake = ctypes.c_void_p(1 << 20)
     with pytest.raises(RuntimeError, match="n_chunks 5 of 4"):
-        L.call("nerf_hash_encode_bwd_owner", 16, 19, 5, 4, None, fake, need, None)
+        L.call("nerf_hash_encode_bwd_owner", 16, 19, 5, 4, None, 0, fake, need, None)
     with pytest.raises(RuntimeError, match="workspace"):
-        L.call("nerf_hash_encode_bwd_owner", 16, 19, 4, 4, None, fake, need - 1, None)
+        L.call("nerf_hash_encode_bwd_owner", 16, 19, 4, 4, None, 0, fake, need - 1, None)
     with pytest.raises(RuntimeError, match="exceed the capacity"):
         L.call("nerf_hash_encode_bwd_bin", fake, 3 * 256 + 1, L.host_f32([0] * 3), L.host_f32([1] * 3),
-               L.host_f32([16] * 16), 16, 19, fake, 32, 2, 1, 4, fake, need, None)
+               L.host_f32([16] * 16), 16, 19, fake, 32, 2, 1, 4, 0, fake, need, None)
+    # the deterministic plan is larger (2^12-row slices, per-level maxima): the plain size is refused
+    need_det = L.load().nerf_hash_encode_bwd_workspace_bytes(16, 19, 256 * 4, 1)
+    assert need_det > need
+    with pytest.raises(RuntimeError, match="workspace"):
+        L.call("nerf_hash_encode_bwd_owner", 16, 19, 4, 4, None, 1, fake, need, None)
+    with pytest.raises(RuntimeError, match="deterministic"):
+        L.call("nerf_hash_encode_bwd_ws", fake, 10, L.host_f32([0] * 3), L.host_f32([1] * 3), L.host_f32([16] * 16),
+               16, 19, fake, 32, 2, None, 1, None, 0, None)
+    with pytest.raises(RuntimeError, match="1..2"):
+        L.call("nerf_mlp_bwd_batch", (L.MlpBwdJob * 3)(), 3, None, 0, None)
 
 
 def _oracle_lib():
@@ -102,13 +112,17 @@ def test_hash_bwd_workspace_plan(nerf):
     lib = nerf.load_library()
     up = lambda v: (v + 255) // 256 * 256  # noqa: E731
     for L, log2_T, P in ((16, 19, 786432), (16, 19, 262144), (8, 12, 1000), (16, 14, 5), (16, 20, 1000)):
-        nch = (P + 255) // 256
-        own = 1 << (log2_T - min(13, log2_T))
-        ent = L * nch * 2048
-        expect = up(ent * 8) + up(ent * 2) + up(L * nch * own * 4)
-        assert lib.nerf_hash_encode_bwd_workspace_bytes(L, log2_T, P) == expect
-    assert lib.nerf_hash_encode_bwd_workspace_bytes(16, 21, 1000) == 0
-    assert lib.nerf_hash_encode_bwd_workspace_bytes(0, 19, 1000) == 0
+        for det, slice_log2 in ((0, 13), (1, 12)):   # deterministic: 2^12-row slices + 16 level maxima
+            if det and log2_T > 19:
+                assert lib.nerf_hash_encode_bwd_workspace_bytes(L, log2_T, P, det) == 0
+                continue
+            nch = (P + 255) // 256
+            own = 1 << (log2_T - min(slice_log2, log2_T))
+            ent = L * nch * 2048
+            expect = up(ent * 8) + up(ent * 2) + up(L * nch * own * 4) + (up(16 * 4) if det else 0)
+            assert lib.nerf_hash_encode_bwd_workspace_bytes(L, log2_T, P, det) == expect
+    assert lib.nerf_hash_encode_bwd_workspace_bytes(16, 21, 1000, 0) == 0
+    assert lib.nerf_hash_encode_bwd_workspace_bytes(0, 19, 1000, 0) == 0
 
 
 def test_crop_window_matches_reference_grid(golden):

@@ -27,7 +27,8 @@ def main():
     chunks = [(p.shape[0] + 255) // 256 for p in sets]
     cap = sum(chunks)
     lib = _lib.load()
-    nbytes = int(lib.nerf_hash_encode_bwd_workspace_bytes(16, 19, 256 * cap))
+    det = int(os.environ.get("NERF_DET", "0"))   # 1: time the deterministic owner pass
+    nbytes = int(lib.nerf_hash_encode_bwd_workspace_bytes(16, 19, 256 * cap, det))
     ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
     grads = [torch.zeros(1 << 19, 2, device=dev) for _ in range(16)]
     gp = _lib.ptr_array(grads)
@@ -37,15 +38,14 @@ def main():
         base = 0
         for p, n, d in zip(sets, chunks, ds):
             _lib.call("nerf_hash_encode_bwd_bin", _lib.ptr(p), p.shape[0], meta["bmin"], meta["bmax"], meta["res"], 16, 19,
-                      _lib.ptr(d), 2, 2 * p.shape[0], base, cap, _lib.ptr(ws, dtype=torch.uint8), nbytes,
+                      _lib.ptr(d), 2, 2 * p.shape[0], base, cap, det, _lib.ptr(ws, dtype=torch.uint8), nbytes,
                       _lib.stream())
             base += n
 
-    os.environ["NERF_BIN_EXP"] = "0"
     bins()
 
     def owner():
-        _lib.call("nerf_hash_encode_bwd_owner", 16, 19, cap, cap, gp, _lib.ptr(ws, dtype=torch.uint8), nbytes,
+        _lib.call("nerf_hash_encode_bwd_owner", 16, 19, cap, cap, gp, det, _lib.ptr(ws, dtype=torch.uint8), nbytes,
                   _lib.stream())
 
     vers = sys.argv[1].split(",") if len(sys.argv) > 1 else ["owner", "bin0", "bin1", "bin2", "bin3"]
@@ -56,8 +56,7 @@ def main():
                 os.environ["NERF_BIN_EXP"] = v[3:]
                 fn = bins
             else:
-                os.environ["NERF_BIN_EXP"] = "0"
-                bins()
+                            bins()
                 fn = owner
             for _ in range(2):
                 fn()
