@@ -195,7 +195,7 @@ WORKLOADS = {
                       "finest_res 512, RAdam, TV+sparsity losses"),
     "scannet": dict(args=dict(finest_res=512, N_samples=64, N_importance=128, white_bkgd=False, perturb=1.0,
                               lrate_decay=500, tv_loss_weight=1e-6, use_structural_priors=True,
-                              structural_loss_start_iter=0),
+                              structural_loss_start_iter=0, structural_loss_ramp_iters=1),
                     near=0.1, far=10.0, rays="scannet",
                     desc="ScanNet-like indoor train step: {R} rays/GPU x (64 + 128) samples, near 0.1 far 10, normals "
                          "head (7-channel compositing), structural priors (Manhattan + planarity + normal "

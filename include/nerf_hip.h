@@ -221,10 +221,9 @@ int nerf_mlp_bwd_batch(const nerf_mlp_bwd_job* jobs, int n_jobs, float* d_det_wo
 /* ---- normals head (run_nerf_helpers.py:259-263, :298-302): n = normalize(N1 relu(N0 geo + b0) + b1)
  * nn.Linear layouts: n0 [32,15], b0 [32], n1 [3,32], b1 [3].
  * fwd: raw7 [P,7] = [raw4, n]; with d_keep, n_z := 0 where !keep (run_network's mask hits the LAST
- *      channel, run_nerf.py:66). bwd: from graw7 writes graw4 [P,4] (the MLP's upstream grad),
- *      dgeo [P,16] (row 0 = 0), and the per-point factors of the head's weight gradients:
- *      hid = relu hidden [P,32], dhid = d pre-ReLU hidden [P,32], dn = d pre-normalize n [P,3]
- *      (dN0 = dhid^T geo, db0 = sum dhid, dN1 = dn^T hid, db1 = sum dn). */
+ *      channel, run_nerf.py:66). bwd: from graw7 writes graw4 [P,4] (the MLP's upstream grad) and
+ *      dgeo [P,16] (row 0 = 0), and ACCUMULATES the head's weight gradients into *grads
+ *      (dN0 = dhid^T geo, db0 = sum dhid, dN1 = dn^T hid, db1 = sum dn, summed in-kernel). */
 typedef struct {
     const float* n0;
     const float* b0;
@@ -232,11 +231,18 @@ typedef struct {
     const float* b1;
 } nerf_normal_head;
 
+typedef struct {
+    float* n0;
+    float* b0;
+    float* n1;
+    float* b1;
+} nerf_normal_head_grads;
+
 int nerf_normal_head_fwd(const float* d_o16, const float* d_raw4, const uint8_t* d_keep, int64_t n_points,
                          const nerf_normal_head* head, float* d_raw7, void* stream);
 int nerf_normal_head_bwd(const float* d_o16, const uint8_t* d_keep, int64_t n_points,
                          const nerf_normal_head* head, const float* d_graw7, float* d_graw4, float* d_dgeo,
-                         float* d_hid, float* d_dhid, float* d_dn, void* stream);
+                         const nerf_normal_head_grads* grads, void* stream);
 
 /* ---- volume compositing (raw2outputs, run_nerf.py:347-411), one wavefront per ray ----------
  * d_raw [R,S,raw_channels] (4, or 7 with normals), d_z [R,S], d_rays_d [R,3] (unnormalised),
@@ -425,6 +431,44 @@ int nerf_hash_encode_fwd_packed(const float* d_xyz, int64_t n_points, const floa
                                 const float* level_res, int n_levels, int log2_T, const void* d_packed,
                                 const float* d_qrec, float* d_feat, int64_t feat_stride_point,
                                 int64_t feat_stride_level, uint8_t* d_keep, void* stream);
+
+/* ---- structural priors on the device (combine_structural_losses_v2, structural_priors.py:374-451,
+ *      with detect_planes :86-155, estimate_frame :16-77, manhattan_sdf_loss :194-256,
+ *      structured_planarity_loss :259-318, spatial_normal_consistency_loss :321-371) -----------------
+ * Three single-workgroup launches over n_rays <= NERF_PRIORS_MAX_RAYS rays, no host synchronisation
+ * (capturable): prep (masks, counts, 10-round k-means, device 3x3 SVD unless cfg->usv), loss (frame,
+ * the three losses; d_loss [1], d_parts [7] = floor, wall, general, manhattan, planarity,
+ * consistency, total, may be NULL), bwd (d depth [n], d normals [n,3] from d_grad_loss [1]). The
+ * workspace (nerf_priors_workspace_bytes) carries the state between the three calls.
+ * Randomness: cfg->centres0 ([3,3] torch.randn), cfg->perm ([3][2*cap] randperm positions per class,
+ * caps 100/100/50) and cfg->idx1 (torch.randint queries) replay the reference's draws; NULL draws them
+ * from Philox (seed, offset | d_rng). cfg->usv ([21]: U, S, V of svd(centres^T)) replaces the device
+ * SVD (prep's d_centres_out [9] gives the centres for it). d_coords NULL = sequential neighbours. */
+#define NERF_PRIORS_MAX_RAYS 8192
+typedef struct {
+    int use_manhattan, use_planarity, use_consistency;
+    float w_manhattan, w_planarity, w_consistency;
+    const float* d_scale;              /* device multiplier of the weights (the ramp), NULL = 1 */
+    float confidence_threshold;        /* ManhattanFrameEstimator (0.4 in combine) */
+    float normal_threshold;            /* SemanticPlaneDetector (0.5 in combine) */
+    const float* centres0;
+    const int32_t* perm;
+    const int32_t* idx1;
+    const float* usv;
+    uint64_t seed, offset;
+    const uint64_t* d_rng;
+} nerf_priors_config;
+
+size_t nerf_priors_workspace_bytes(int64_t n_rays);
+int nerf_priors_prep(const float* d_depth, const float* d_normals, const float* d_coords, int64_t n_rays,
+                     const nerf_priors_config* cfg, void* d_workspace, size_t workspace_bytes, float* d_centres_out,
+                     void* stream);
+int nerf_priors_loss(const float* d_depth, const float* d_normals, const float* d_coords, int64_t n_rays,
+                     const nerf_priors_config* cfg, void* d_workspace, size_t workspace_bytes, float* d_loss,
+                     float* d_parts, void* stream);
+int nerf_priors_bwd(const float* d_depth, const float* d_normals, const float* d_coords, int64_t n_rays,
+                    const nerf_priors_config* cfg, void* d_workspace, size_t workspace_bytes,
+                    const float* d_grad_loss, float* d_grad_depth, float* d_grad_normals, void* stream);
 
 /* ---- structural priors (PocketNeRF/structural_priors.py:333-346, the ScanNet configuration) -----
  * For each query ray q (d_idx1[q], int64), the nearest OTHER ray in pixel space: d_xy [n,2] fp32

@@ -41,7 +41,23 @@ class MlpBwdJob(ctypes.Structure):
                 ("dsh", c_vp), ("dgeo", c_vp), ("act_qrec", c_vp)]
 
 
+PRIORS_MAX_RAYS = 8192   # NERF_PRIORS_MAX_RAYS
+
+
+class PriorsConfig(ctypes.Structure):
+    """nerf_priors_config (include/nerf_hip.h)."""
+    _fields_ = [("use_manhattan", c_int), ("use_planarity", c_int), ("use_consistency", c_int),
+                ("w_manhattan", ctypes.c_float), ("w_planarity", ctypes.c_float), ("w_consistency", ctypes.c_float),
+                ("d_scale", c_vp), ("confidence_threshold", ctypes.c_float), ("normal_threshold", ctypes.c_float),
+                ("centres0", c_vp), ("perm", c_vp), ("idx1", c_vp), ("usv", c_vp), ("seed", c_u64),
+                ("offset", c_u64), ("d_rng", c_vp)]
+
+
 class NormalHead(ctypes.Structure):
+    _fields_ = [("n0", c_vp), ("b0", c_vp), ("n1", c_vp), ("b1", c_vp)]
+
+
+class NormalHeadGrads(ctypes.Structure):
     _fields_ = [("n0", c_vp), ("b0", c_vp), ("n1", c_vp), ("b1", c_vp)]
 
 
@@ -87,10 +103,15 @@ SIGNATURES = {
     "nerf_mlp_bwd_q": [c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, ctypes.POINTER(MlpWeights),
                        c_vp, ctypes.POINTER(MlpGrads), c_vp, c_vp, c_vp, c_vp, c_vp],
     "nerf_count_nonfinite": [ctypes.POINTER(c_vp), ctypes.POINTER(c_i64), c_int, c_vp, c_vp],
+    "nerf_priors_prep": [c_vp, c_vp, c_vp, c_i64, ctypes.POINTER(PriorsConfig), c_vp, ctypes.c_size_t, c_vp, c_vp],
+    "nerf_priors_loss": [c_vp, c_vp, c_vp, c_i64, ctypes.POINTER(PriorsConfig), c_vp, ctypes.c_size_t, c_vp, c_vp,
+                         c_vp],
+    "nerf_priors_bwd": [c_vp, c_vp, c_vp, c_i64, ctypes.POINTER(PriorsConfig), c_vp, ctypes.c_size_t, c_vp, c_vp,
+                        c_vp, c_vp],
     "nerf_mlp_bwd_batch": [ctypes.POINTER(MlpBwdJob), c_int, c_vp, ctypes.c_size_t, c_vp],
     "nerf_normal_head_fwd": [c_vp, c_vp, c_vp, c_i64, ctypes.POINTER(NormalHead), c_vp, c_vp],
-    "nerf_normal_head_bwd": [c_vp, c_vp, c_i64, ctypes.POINTER(NormalHead), c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
-                             c_vp],
+    "nerf_normal_head_bwd": [c_vp, c_vp, c_i64, ctypes.POINTER(NormalHead), c_vp, c_vp, c_vp,
+                             ctypes.POINTER(NormalHeadGrads), c_vp],
     "nerf_composite_fwd": [c_vp, c_int, c_vp, c_vp, c_vp, c_i64, c_int, c_int,
                            c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
     "nerf_composite_bwd": [c_vp, c_int, c_vp, c_vp, c_vp, c_i64, c_int, c_int,
@@ -146,6 +167,8 @@ def load():
     lib.nerf_abi_version.argtypes = []
     lib.nerf_hash_encode_bwd_workspace_bytes.restype = ctypes.c_size_t
     lib.nerf_hash_encode_bwd_workspace_bytes.argtypes = [c_int, c_int, c_i64, c_int]
+    lib.nerf_priors_workspace_bytes.restype = ctypes.c_size_t
+    lib.nerf_priors_workspace_bytes.argtypes = [c_i64]
     lib.nerf_mlp_bwd_det_workspace_bytes.restype = ctypes.c_size_t
     lib.nerf_mlp_bwd_det_workspace_bytes.argtypes = []
     lib.nerf_quant_packed_bytes.restype = ctypes.c_size_t
@@ -160,7 +183,7 @@ def load():
 
 def exported_symbols():
     return ["nerf_last_error", "nerf_abi_version", "nerf_hash_encode_bwd_workspace_bytes",
-            "nerf_quant_packed_bytes", "nerf_mlp_bwd_det_workspace_bytes"] + list(SIGNATURES)
+            "nerf_quant_packed_bytes", "nerf_mlp_bwd_det_workspace_bytes", "nerf_priors_workspace_bytes"] + list(SIGNATURES)
 
 
 _TIMING = None   # when a list: (name, start_event, end_event) per launch, recorded on the current stream

@@ -6,9 +6,11 @@
 // sigma mask when the head is on).
 //
 // One thread per point; the 611 head parameters sit in LDS (wave-uniform broadcast reads). The
-// backward writes the per-point quantities the weight gradients are built from (h, d pre-ReLU h,
-// d pre-normalize n): those are (P x 32)^T (P x 15)-shaped sums with K = P, left to the GEMM
-// library by the host (plain library GEMMs, cdna_hip_programming.md: hipBLASLt/rocBLAS for those).
+// backward also forms the head's weight gradients, sums over all points (dN0 = dh^T geo, db0 = sum
+// dh, dN1 = dn^T relu(h), db1 = sum dn): a persistent grid of 128-point tiles stages each tile's
+// per-point factors in LDS, every thread owns ~5 of the 611 gradient values and accumulates them
+// over the tiles in registers, and each block adds its totals into .grad once (no [P,32] buffers
+// in HBM and no K = P library GEMMs afterwards).
 #include "common.h"
 
 namespace nerf {
@@ -27,9 +29,7 @@ struct NormalArgs {
     const float* graw7;    // bwd in [P,7]
     float* graw4;          // bwd out [P,4]
     float* dgeo;           // bwd out [P,16] (row 0 = 0)
-    float* hid;            // bwd out [P,32] relu hidden
-    float* dhid;           // bwd out [P,32] d pre-ReLU hidden
-    float* dn;             // bwd out [P,3] d pre-normalize n
+    nerf_normal_head_grads G;   // bwd: accumulated weight gradients
 };
 
 __device__ __forceinline__ void load_head(float* s, const nerf_normal_head& W) {
@@ -82,47 +82,96 @@ __global__ void __launch_bounds__(256) normal_head_fwd_kernel(NormalArgs a) {
     o[6] = keep ? n[2] / nrm : 0.f;
 }
 
-__global__ void __launch_bounds__(256) normal_head_bwd_kernel(NormalArgs a) {
+constexpr int NH_TILE = 128;
+constexpr int NH_OWN = (NH_ALL + NH_TILE - 1) / NH_TILE;   // gradient values per thread (5)
+
+__global__ void __launch_bounds__(NH_TILE) normal_head_bwd_kernel(NormalArgs a) {
     __shared__ float s[NH_ALL];
+    __shared__ float s_dh[NH_TILE][NH_HID + 1];   // d pre-ReLU hidden
+    __shared__ float s_hr[NH_TILE][NH_HID + 1];   // relu hidden
+    __shared__ float s_geo[NH_TILE][NH_GEO + 1];
+    __shared__ float s_dn[NH_TILE][4];            // d pre-normalize n
     load_head(s, a.W);
-    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= a.P) return;
-    float geo[NH_GEO], h[NH_HID], n[3];
+    const int tid = threadIdx.x;
+    float acc[NH_OWN];
 #pragma unroll
-    for (int k = 0; k < NH_GEO; ++k) geo[k] = a.o16[p * 16 + 1 + k];
-    head_forward(s, geo, h, n);
-    const float* g7 = a.graw7 + 7 * p;
-    *reinterpret_cast<float4*>(a.graw4 + 4 * p) = make_float4(g7[0], g7[1], g7[2], g7[3]);
-    const bool keep = a.keep ? a.keep[p] != 0 : true;
-    const float g[3] = {g7[4], g7[5], keep ? g7[6] : 0.f};
-    // y = x / m, m = max(||x||, eps): dx = g / m - x (g.x) / (m^2 ||x||)  (the norm term only while
-    // ||x|| > eps, where the clamp passes the gradient)
-    const float len = sqrtf(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
-    const float m = fmaxf(len, 1e-12f);
-    const float gx = g[0] * n[0] + g[1] * n[1] + g[2] * n[2];
-    float dn[3];
+    for (int j = 0; j < NH_OWN; ++j) acc[j] = 0.f;
+    for (int64_t base = (int64_t)blockIdx.x * NH_TILE; base < a.P; base += (int64_t)gridDim.x * NH_TILE) {
+        const int64_t p = base + tid;
+        float geo[NH_GEO], h[NH_HID], n[3], dn[3] = {0.f, 0.f, 0.f};
+        if (p < a.P) {
 #pragma unroll
-    for (int c = 0; c < 3; ++c) dn[c] = g[c] / m - (len > 1e-12f ? n[c] * (gx / (m * m * len)) : 0.f);
+            for (int k = 0; k < NH_GEO; ++k) geo[k] = a.o16[p * 16 + 1 + k];
+            head_forward(s, geo, h, n);
+            const float* g7 = a.graw7 + 7 * p;
+            *reinterpret_cast<float4*>(a.graw4 + 4 * p) = make_float4(g7[0], g7[1], g7[2], g7[3]);
+            const bool keep = a.keep ? a.keep[p] != 0 : true;
+            const float g[3] = {g7[4], g7[5], keep ? g7[6] : 0.f};
+            // y = x / m, m = max(||x||, eps): dx = g / m - x (g.x) / (m^2 ||x||)  (the norm term only
+            // while ||x|| > eps, where the clamp passes the gradient)
+            const float len = sqrtf(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+            const float m = fmaxf(len, 1e-12f);
+            const float gx = g[0] * n[0] + g[1] * n[1] + g[2] * n[2];
 #pragma unroll
-    for (int c = 0; c < 3; ++c) a.dn[p * 3 + c] = dn[c];
-    float dg[NH_GEO];
+            for (int c = 0; c < 3; ++c) dn[c] = g[c] / m - (len > 1e-12f ? n[c] * (gx / (m * m * len)) : 0.f);
+        } else {
 #pragma unroll
-    for (int k = 0; k < NH_GEO; ++k) dg[k] = 0.f;
+            for (int k = 0; k < NH_GEO; ++k) geo[k] = 0.f;
+#pragma unroll
+            for (int i = 0; i < NH_HID; ++i) h[i] = 0.f;
+        }
+        float dg[NH_GEO];
+#pragma unroll
+        for (int k = 0; k < NH_GEO; ++k) dg[k] = 0.f;
 #pragma unroll 4
-    for (int i = 0; i < NH_HID; ++i) {
-        const float hr = fmaxf(h[i], 0.f);
-        const float dh = h[i] > 0.f ? (s[NH_N1 + i] * dn[0] + s[NH_N1 + NH_HID + i] * dn[1]) +
-                                           s[NH_N1 + 2 * NH_HID + i] * dn[2]
-                                    : 0.f;
-        a.hid[p * NH_HID + i] = hr;
-        a.dhid[p * NH_HID + i] = dh;
+        for (int i = 0; i < NH_HID; ++i) {
+            const float dh = h[i] > 0.f ? (s[NH_N1 + i] * dn[0] + s[NH_N1 + NH_HID + i] * dn[1]) +
+                                               s[NH_N1 + 2 * NH_HID + i] * dn[2]
+                                        : 0.f;
+            s_dh[tid][i] = dh;
+            s_hr[tid][i] = fmaxf(h[i], 0.f);
 #pragma unroll
-        for (int k = 0; k < NH_GEO; ++k) dg[k] = fmaf(s[NH_N0 + i * NH_GEO + k], dh, dg[k]);
+            for (int k = 0; k < NH_GEO; ++k) dg[k] = fmaf(s[NH_N0 + i * NH_GEO + k], dh, dg[k]);
+        }
+#pragma unroll
+        for (int k = 0; k < NH_GEO; ++k) s_geo[tid][k] = geo[k];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) s_dn[tid][c] = dn[c];
+        if (p < a.P) {
+            float* d = a.dgeo + p * 16;
+            d[0] = 0.f;
+#pragma unroll
+            for (int k = 0; k < NH_GEO; ++k) d[1 + k] = dg[k];
+        }
+        __syncthreads();
+        // gradient value v = tid + NH_TILE j: N0 [i][k] | b0 [i] | N1 [c][i] | b1 [c], summed over the tile
+#pragma unroll
+        for (int j = 0; j < NH_OWN; ++j) {
+            const int v = tid + NH_TILE * j;
+            float t = 0.f;
+            if (v < NH_B0) {
+                const int i = v / NH_GEO, k = v % NH_GEO;
+                for (int q = 0; q < NH_TILE; ++q) t = fmaf(s_dh[q][i], s_geo[q][k], t);
+            } else if (v < NH_N1) {
+                for (int q = 0; q < NH_TILE; ++q) t += s_dh[q][v - NH_B0];
+            } else if (v < NH_B1) {
+                const int c = (v - NH_N1) / NH_HID, i = (v - NH_N1) % NH_HID;
+                for (int q = 0; q < NH_TILE; ++q) t = fmaf(s_dn[q][c], s_hr[q][i], t);
+            } else if (v < NH_ALL) {
+                for (int q = 0; q < NH_TILE; ++q) t += s_dn[q][v - NH_B1];
+            }
+            acc[j] += t;
+        }
+        __syncthreads();
     }
-    float* d = a.dgeo + p * 16;
-    d[0] = 0.f;
 #pragma unroll
-    for (int k = 0; k < NH_GEO; ++k) d[1 + k] = dg[k];
+    for (int j = 0; j < NH_OWN; ++j) {
+        const int v = tid + NH_TILE * j;
+        if (v >= NH_ALL || acc[j] == 0.f) continue;
+        float* dst = v < NH_B0 ? a.G.n0 + v : v < NH_N1 ? a.G.b0 + (v - NH_B0) : v < NH_B1 ? a.G.n1 + (v - NH_N1)
+                                                                                          : a.G.b1 + (v - NH_B1);
+        __hip_atomic_fetch_add(dst, acc[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 }
 
 static int fill_normal(NormalArgs& a, const float* o16, const uint8_t* keep, int64_t P, const nerf_normal_head* W) {
@@ -155,19 +204,19 @@ extern "C" int nerf_normal_head_fwd(const float* d_o16, const float* d_raw4, con
 
 extern "C" int nerf_normal_head_bwd(const float* d_o16, const uint8_t* d_keep, int64_t n_points,
                                     const nerf_normal_head* head, const float* d_graw7, float* d_graw4, float* d_dgeo,
-                                    float* d_hid, float* d_dhid, float* d_dn, void* stream) {
+                                    const nerf_normal_head_grads* grads, void* stream) {
     NormalArgs a{};
     int rc = fill_normal(a, d_o16, d_keep, n_points, head);
     if (rc) return rc;
-    NERF_REQUIRE(d_graw7 && d_graw4 && d_dgeo && d_hid && d_dhid && d_dn, "normal_head_bwd: null buffer");
+    NERF_REQUIRE(d_graw7 && d_graw4 && d_dgeo && grads && grads->n0 && grads->b0 && grads->n1 && grads->b1,
+                 "normal_head_bwd: null buffer");
     if (n_points == 0) return NERF_OK;
     a.graw7 = d_graw7;
     a.graw4 = d_graw4;
     a.dgeo = d_dgeo;
-    a.hid = d_hid;
-    a.dhid = d_dhid;
-    a.dn = d_dn;
-    hipLaunchKernelGGL(normal_head_bwd_kernel, dim3(blocks_for(n_points, 256)), dim3(256), 0, as_stream(stream), a);
+    a.G = *grads;
+    const unsigned blocks = (unsigned)std::min<int64_t>(blocks_for(n_points, NH_TILE), 1024);
+    hipLaunchKernelGGL(normal_head_bwd_kernel, dim3(blocks), dim3(NH_TILE), 0, as_stream(stream), a);
     NERF_CHECK_LAUNCH("normal_head_bwd");
     return NERF_OK;
 }

@@ -65,18 +65,20 @@ def _head_forward(o16, raw4, keep, head):
 
 
 def _head_backward(o16, keep, head, g7, needs):
-    """-> (graw4 [P,4], dgeo [P,16], grads of (N0, b0, N1, b1) or None each)."""
+    """-> (graw4 [P,4], dgeo [P,16]); the head's weight gradients are ACCUMULATED into .grad by the
+    kernel (csrc/normals.hip sums them over the points in-kernel), for those of (N0, b0, N1, b1) that
+    require grad (the others go to scratch)."""
     P = o16.shape[0]
     f = dict(device=o16.device, dtype=torch.float32)
     graw4, dgeo = torch.empty(P, 4, **f), torch.empty(P, 16, **f)
-    hid, dhid, dn = torch.empty(P, 32, **f), torch.empty(P, 32, **f), torch.empty(P, 3, **f)
+    g = _lib.NormalHeadGrads()
+    bufs = [accumulate_grad_buffers([t])[0] if need else torch.zeros_like(t) for t, need in zip(head, needs)]
+    for name, t in zip(("n0", "b0", "n1", "b1"), bufs):
+        setattr(g, name, _lib.ptr(t, "grad_normal_net." + name).value)
     _lib.call("nerf_normal_head_bwd", _lib.ptr(o16, "geo"), _lib.ptr(keep, "keep", dtype=torch.bool, allow_none=True),
-              P, _head_struct(head), _lib.ptr(g7.contiguous(), "grad_raw"), _lib.ptr(graw4), _lib.ptr(dgeo),
-              _lib.ptr(hid), _lib.ptr(dhid), _lib.ptr(dn), _lib.stream())
-    # weight gradients: sums over points (K = P) -> library GEMMs
-    grads = (dhid.t().mm(o16[:, 1:16]) if needs[0] else None, dhid.sum(0) if needs[1] else None,
-             dn.t().mm(hid) if needs[2] else None, dn.sum(0) if needs[3] else None)
-    return graw4, dgeo, grads
+              P, _head_struct(head), _lib.ptr(g7.contiguous(), "grad_raw"), _lib.ptr(graw4), _lib.ptr(dgeo), g,
+              _lib.stream())
+    return graw4, dgeo
 
 
 class MLPFn(torch.autograd.Function):
@@ -113,7 +115,7 @@ class MLPFn(torch.autograd.Function):
         g = g_raw.contiguous()
         head_grads, dgeo = (None,) * ctx.n_head, None
         if head:
-            g, dgeo, head_grads = _head_backward(o16, None, head, g, ctx.needs_input_grad[7:11])
+            g, dgeo = _head_backward(o16, None, head, g, ctx.needs_input_grad[7:11])
         need_x = ctx.needs_input_grad[0]
         dx = torch.zeros_like(x) if need_x else None
         if any(w.requires_grad for w in weights) or need_x:
@@ -191,7 +193,7 @@ class FieldFn(torch.autograd.Function):
         g = g_raw.contiguous()
         head_grads, dgeo = (None,) * ctx.n_head, None
         if head:
-            g, dgeo, head_grads = _head_backward(o16, keep, head, g, ctx.needs_input_grad[6 + n_tab + 5:])
+            g, dgeo = _head_backward(o16, keep, head, g, ctx.needs_input_grad[6 + n_tab + 5:])
         need_tab = any(t.requires_grad for t in tables) and not ctx.zero_tab_grad
         need_w = any(w.requires_grad for w in weights)
         if need_w or need_tab:

@@ -52,6 +52,7 @@ class StepScalars:
                        for b in self.pinned_bytes]
         self.events = [None] * ring
         self.k = 0
+        self.step = 0      # the global step of the replay being prepared (fillers may read it)
         self.ni = self.nf = 0
         self.fillers = []
 
@@ -117,16 +118,23 @@ class GraphedTrainStep:
     def _n_forwards(self):
         return 2 if self.kw.get("network_fine") is not None else 1     # coarse + fine embedder calls
 
-    def _structure_key(self):
+    def _structure_key(self, global_step):
         """Host state that changes the launch sequence of a step: the TV term (on until iteration
-        1000) and, per embedder call of the step, whether A-CAQ quantization is active."""
+        1000), per embedder call of the step whether A-CAQ quantization is active, and whether the
+        structural priors are on (with the weights baked into their launch)."""
         from .model import DEFAULTS
-        tv_w = getattr(self.args, "tv_loss_weight", DEFAULTS["tv_loss_weight"])
+        get = lambda k: getattr(self.args, k, DEFAULTS.get(k))  # noqa: E731
+        tv_w = get("tv_loss_weight")
         emb = self.kw["embed_fn"]
         quant = ()
         if getattr(emb, "use_quantization", False):
             quant = tuple(emb.current_step + k + 1 >= emb.warmup_steps for k in range(self._n_forwards()))
-        return (tv_w > 0, quant)
+        priors = ()
+        if self._priors_active(global_step):
+            priors = (get("depth_prior_weight"), get("planarity_weight"), get("manhattan_weight"),
+                      get("normal_consistency_weight"), get("structural_loss_start_iter"),
+                      get("structural_loss_ramp_iters"))
+        return (tv_w > 0, quant, priors)
 
     def _capture(self, global_step):
         from . import _lib
@@ -173,12 +181,11 @@ class GraphedTrainStep:
 
     def __call__(self, global_step):
         from .model import acaq_update, lr_schedule
-        if self._priors_active(global_step):
-            # the structural priors branch on ray counts read on the host and draw data-dependent
-            # permutations (priors.py): not capturable, the iteration runs eagerly
+        if self._priors_active(global_step) and not getattr(self.args, "fused_priors", True):
+            # the eager priors path branches on host counts and draws host permutations: not capturable
             self.graphs, self.key = None, None
             return self.eager_step(global_step)
-        key = self._structure_key()
+        key = self._structure_key(global_step)
         if key != self.key:                # new launch structure: eager steps first (allocations,
             self.key = key                 # quantizer calibration), then a fresh capture
             self.graphs = None
@@ -188,6 +195,7 @@ class GraphedTrainStep:
             return self.eager_step(global_step)
         if self.graphs is None:
             self._capture(global_step)
+        self.scalars.step = global_step
         self.scalars.upload()
         self.graphs[0].replay()
         emb = self.kw["embed_fn"]

@@ -199,19 +199,40 @@ def _unit_seed(loss):
 
 def structural_loss(depth, extras, args, global_step, spatial_coords=None):
     """run_nerf.py:1068-1131: the structural-prior weights ramp from 10 % to 100 % over
-    structural_loss_ramp_iters, then combine_structural_losses_v2 (priors.py) on the fine pass's
-    depth and normal maps. The estimators persist across iterations (run_nerf.py:939-940). The
-    overfitting-driven weight reduction (:1073-1094) needs train()'s test-set PSNR history and is
-    left to the caller. Failures are swallowed as in the reference (:1144-1148)."""
-    from .priors import ManhattanFrameEstimator, SemanticPlaneDetector, combine_structural_losses_v2
+    structural_loss_ramp_iters, then combine_structural_losses_v2 on the fine pass's depth and normal
+    maps. Default: the device path (priors.fused_structural_losses, csrc/priors_fused.hip: no host
+    synchronisation, so graphs.GraphedTrainStep captures these iterations too; the ramp is a device
+    scalar, a per-step graph slot under capture). args.fused_priors = False selects the eager torch
+    path (priors.combine_structural_losses_v2, the reference's RNG draws; its estimators persist
+    across iterations, run_nerf.py:939-940). The overfitting-driven weight reduction (:1073-1094)
+    needs train()'s test-set PSNR history and is left to the caller. Failures are swallowed as in
+    the reference (:1144-1148)."""
+    from . import graphs
+    from .priors import (ManhattanFrameEstimator, SemanticPlaneDetector, combine_structural_losses_v2,
+                         fused_structural_losses)
     get = lambda k: getattr(args, k, DEFAULTS.get(k))  # noqa: E731
+    start = get("structural_loss_start_iter")
+    ramp_of = lambda step: 0.1 + 0.9 * min(1.0, (step - start) / get("structural_loss_ramp_iters"))  # noqa: E731
+    base = {"depth_prior": get("depth_prior_weight"), "planarity": get("planarity_weight"),
+            "manhattan": get("manhattan_weight"), "normal_consistency": get("normal_consistency_weight")}
+    normals = extras.get("normal_map", None) if get("predict_normals") else None
+    if getattr(args, "fused_priors", True) and normals is not None and 1 <= depth.shape[0] <= _lib.PRIORS_MAX_RAYS:
+        sc = graphs.active()
+        if sc is not None:   # captured: the ramp of the replayed step, written before every replay
+            off, ptr = sc.alloc_f32(1)
+
+            def fill(hi, hf, off=off):
+                hf[off] = ramp_of(sc.step)
+            sc.add_filler(fill)
+            scale = sc.dev_f[off:off + 1]
+        else:
+            scale = torch.full((1,), ramp_of(global_step), device=depth.device)
+        total, _ = fused_structural_losses(depth, normals, spatial_coords, base, 0.4, 0.5, scale=scale)
+        return total
     if getattr(args, "_priors", None) is None:
         args._priors = (ManhattanFrameEstimator(confidence_threshold=0.4), SemanticPlaneDetector(normal_threshold=0.5))
-    start = get("structural_loss_start_iter")
-    ramp = 0.1 + 0.9 * min(1.0, (global_step - start) / get("structural_loss_ramp_iters"))
-    weights = {"depth_prior": get("depth_prior_weight") * ramp, "planarity": get("planarity_weight") * ramp,
-               "manhattan": get("manhattan_weight") * ramp, "normal_consistency": get("normal_consistency_weight") * ramp}
-    normals = extras.get("normal_map", None) if get("predict_normals") else None
+    ramp = ramp_of(global_step)
+    weights = {k: v * ramp for k, v in base.items()}
     try:
         total, _ = combine_structural_losses_v2(depth, normals, extras.get("rays_d"), spatial_coords, weights,
                                                 *args._priors)

@@ -256,3 +256,147 @@ def combine_structural_losses_v2(depth_pred, normals, rays_d, spatial_coords=Non
         print(f"⚠️  Structural priors computation failed: {e}")
         return torch.tensor(0.0, device=dev), {"error": str(e)}
     return total, out
+
+
+# ---- device path: the whole combine_structural_losses_v2 in three launches (csrc/priors_fused.hip) ----
+_FUSED_WS = {}
+_FUSED_RETIRED = []   # workspaces a captured graph may still reference (never freed, see hashgrid._RETIRED)
+_CAPS = (100, 100, 50)
+
+
+def _fused_workspace(n, device):
+    need = int(_lib.load().nerf_priors_workspace_bytes(n))
+    key = str(device)
+    ws = _FUSED_WS.get(key)
+    if ws is None or ws.numel() < need:
+        if ws is not None:
+            _FUSED_RETIRED.append(ws)
+        ws = _FUSED_WS[key] = torch.empty(need, dtype=torch.uint8, device=device)
+    return ws
+
+
+class _FusedPriorsFn(torch.autograd.Function):
+    """(depth [N], normals [N,3]) -> total structural loss (0-dim), d depth / d normals in backward."""
+
+    @staticmethod
+    def forward(ctx, depth, normals, coords, spec):
+        dev = depth.device
+        N = depth.shape[0]
+        d = depth.detach().float().contiguous()
+        n = normals.detach().float().contiguous()
+        xy = coords.detach().float().contiguous() if coords is not None else None
+        ws = _fused_workspace(N, dev)
+        cfg = _lib.PriorsConfig()
+        w = spec["weights"]
+        cfg.use_manhattan, cfg.use_planarity, cfg.use_consistency = (int(k in w) for k in
+                                                                     ("manhattan", "planarity", "normal_consistency"))
+        cfg.w_manhattan = float(w.get("manhattan", 0.0))
+        cfg.w_planarity = float(w.get("planarity", 0.0))
+        cfg.w_consistency = float(w.get("normal_consistency", 0.0))
+        scale = spec.get("scale")
+        cfg.d_scale = _lib.ptr(scale, "scale", allow_none=True)
+        cfg.confidence_threshold, cfg.normal_threshold = spec["confidence"], spec["normal_threshold"]
+        keep_alive = []
+        args = (_lib.ptr(d, "depth"), _lib.ptr(n, "normals"), _lib.ptr(xy, "coords", allow_none=True), N)
+        wsp = (_lib.ptr(ws, "workspace", dtype=torch.uint8), ws.numel())
+        if spec["replay"]:
+            _replay_draws(cfg, n, xy, N, spec, keep_alive)
+            centres = torch.empty(9, device=dev)
+            usv = torch.zeros(21, device=dev)
+            keep_alive += [centres, usv]
+            cfg.usv = _lib.ptr(usv, "usv")
+            _lib.call("nerf_priors_prep", *args, ctypes_ref(cfg), *wsp, _lib.ptr(centres, "centres"), _lib.stream())
+            if spec["kmeans"]:   # the frame's SVD on the host (LAPACK: the reference's sign convention, F18)
+                U, S, V = torch.svd(centres.reshape(3, 3).T.cpu())
+                usv.copy_(torch.cat([U.reshape(-1), S, V.reshape(-1)]))
+        else:
+            from .render import _rng
+            cfg.seed, cfg.offset, rng = _rng()
+            cfg.d_rng = rng
+            _lib.call("nerf_priors_prep", *args, ctypes_ref(cfg), *wsp, None, _lib.stream())
+        loss = torch.empty(1, device=dev)
+        parts = torch.empty(7, device=dev)
+        _lib.call("nerf_priors_loss", *args, ctypes_ref(cfg), *wsp, _lib.ptr(loss, "loss"), _lib.ptr(parts, "parts"),
+                  _lib.stream())
+        ctx.save_for_backward(d, n, xy if xy is not None else torch.empty(0, device=dev))
+        ctx.cfg, ctx.ws, ctx.keep, ctx.has_xy, ctx.parts = cfg, ws, keep_alive, xy is not None, parts
+        spec["parts"] = parts
+        return loss.reshape(())
+
+    @staticmethod
+    def backward(ctx, g):
+        d, n, xy = ctx.saved_tensors
+        N = d.shape[0]
+        gd, gn = torch.empty_like(d), torch.empty_like(n)
+        g1 = g.detach().float().reshape(1).contiguous()
+        _lib.call("nerf_priors_bwd", _lib.ptr(d, "depth"), _lib.ptr(n, "normals"),
+                  _lib.ptr(xy, "coords") if ctx.has_xy else None, N, ctypes_ref(ctx.cfg),
+                  _lib.ptr(ctx.ws, "workspace", dtype=torch.uint8), ctx.ws.numel(), _lib.ptr(g1, "grad_loss"),
+                  _lib.ptr(gd, "grad_depth"), _lib.ptr(gn, "grad_normals"), _lib.stream())
+        return gd, gn, None, None
+
+
+def ctypes_ref(cfg):
+    import ctypes
+    return ctypes.byref(cfg)
+
+
+def _replay_draws(cfg, n, xy, N, spec, keep_alive):
+    """The reference's draws in its order (torch.randn for the k-means init, torch.randperm per
+    planarity class, torch.randint for the consistency queries), decided with host counts exactly
+    where the reference's branches read them (this mode synchronises; it pins the device path to
+    the reference's randomness, golden F18)."""
+    dev = n.device
+    nrm = torch.norm(n, dim=-1)
+    nz = F.normalize(n, dim=-1)
+    stable = nrm > 0.1
+    t = spec["normal_threshold"]
+    if int(stable.sum()) < 10:
+        floor = wall = torch.zeros(N, dtype=torch.bool, device=dev)
+    else:
+        az = nz[:, 2].abs()
+        floor, wall = stable & (az > t), stable & (az < 1 - t)
+    n_keep = int((nrm > spec["confidence"]).sum())
+    spec["kmeans"] = n_keep >= 30
+    if spec["kmeans"]:
+        c0 = torch.randn(3, 3, device=dev).float().contiguous()
+        keep_alive.append(c0)
+        cfg.centres0 = _lib.ptr(c0, "centres0")
+    perm = torch.zeros(3, 2 * max(_CAPS), dtype=torch.int32, device=dev)
+    if N >= 10:
+        other = ~(floor | wall)
+        counts = (int(floor.sum()), int(wall.sum()), int(other.sum()))
+        for k, (cnt, cap) in enumerate(zip(counts, _CAPS)):
+            if cnt > 5:
+                n_pairs = min(cap, cnt // 2)
+                p = torch.randperm(cnt)[:2 * n_pairs]
+                perm.view(-1)[2 * sum(_CAPS[:k]):2 * sum(_CAPS[:k]) + p.numel()] = p.to(dev, torch.int32)
+    keep_alive.append(perm)
+    cfg.perm = _lib.ptr(perm, "perm", dtype=torch.int32)
+    if N >= 10:
+        if xy is not None:
+            idx1 = torch.randint(0, N, (min(200, N // 2),), device=dev)
+        else:
+            idx1 = torch.randint(0, N - 1, (min(100, N - 1),), device=dev)
+        idx1 = idx1.to(torch.int32).contiguous()
+        keep_alive.append(idx1)
+        cfg.idx1 = _lib.ptr(idx1, "idx1", dtype=torch.int32)
+
+
+def fused_structural_losses(depth_pred, normals, spatial_coords=None, weights=None, confidence_threshold=0.4,
+                            normal_threshold=0.5, scale=None, replay=False):
+    """combine_structural_losses_v2 on the device (csrc/priors_fused.hip): same losses, branches and
+    autograd graph, no host synchronisation (capturable in a HIP graph). scale: optional device [1]
+    multiplier of the weights (the train() ramp, a per-step graph slot). replay=True draws the
+    reference's torch.randn/randperm/randint in its order and takes the frame's SVD from LAPACK
+    (host syncs; the golden F18 parity mode). Returns (total, parts) with parts a device [7] tensor
+    (floor, wall, general, manhattan, planarity, consistency, total)."""
+    if weights is None:
+        weights = {"manhattan": 1.0, "planarity": 1.0, "normal_consistency": 0.5}
+    N = depth_pred.shape[0]
+    if not (1 <= N <= _lib.PRIORS_MAX_RAYS) or normals is None or normals.shape != (N, 3):
+        raise ValueError(f"fused_structural_losses: need depth [N] and normals [N,3], 1 <= N <= {_lib.PRIORS_MAX_RAYS}")
+    spec = dict(weights=weights, confidence=float(confidence_threshold), normal_threshold=float(normal_threshold),
+                scale=scale, replay=bool(replay))
+    total = _FusedPriorsFn.apply(depth_pred, normals, spatial_coords, spec)
+    return total, spec["parts"]

@@ -96,8 +96,9 @@ def test_nearest_pixel_vs_cdist(nerf, gpu):
 @pytest.mark.gpu
 def test_train_step_with_structural_priors(nerf, gpu):
     """The ScanNet configuration's iteration (normals head + structural priors at full ramp):
-    finite loss that includes the priors, gradients reach the normals head; GraphedTrainStep
-    runs such iterations eagerly."""
+    finite loss that includes the priors, gradients reach the normals head. GraphedTrainStep
+    captures such iterations (the device priors path, no host sync); the eager torch path
+    (args.fused_priors = False) runs them eagerly."""
     from indoor_nerf_amd.graphs import GraphedTrainStep
     from indoor_nerf_amd.synthetic import scannet_bbox, scannet_rays
     lo, hi = scannet_bbox()
@@ -111,14 +112,122 @@ def test_train_step_with_structural_priors(nerf, gpu):
     ro, rd, xy = scannet_rays(1024, seed=5)
     rays = (torch.from_numpy(ro).to(gpu), torch.from_numpy(rd).to(gpu))
     target = torch.rand(1024, 3, device=gpu)
-    st = GraphedTrainStep(rays, target, kw, opt, args, warmup=0)
+    st = GraphedTrainStep(rays, target, kw, opt, args, warmup=1)
     for it in range(1, 4):
         loss, psnr = st(it)
     torch.cuda.synchronize()
-    assert st.captures == 0
+    assert st.captures == 1
     assert torch.isfinite(loss).item()
+    args.fused_priors = False
+    loss_e, _ = st(4)
+    assert st.graphs is None and torch.isfinite(loss_e).item()
+    args.fused_priors = True
     head = [p for n, p in kw["network_fine"].named_parameters() if "normal" in n]
     assert head and all(p.grad is not None and torch.isfinite(p.grad).all() for p in head)
     # with coordinates: the nearest-pixel kernel path
     loss2, _ = nerf.train_step(rays, target, kw, opt, args, 4, spatial_coords=torch.from_numpy(xy).to(gpu))
     assert torch.isfinite(loss2).item()
+
+
+def run_fused(nerf, g, tag, device, replay_draws=True):
+    from indoor_nerf_amd import priors
+    d = torch.from_numpy(g[tag + "_depth"]).to(device).requires_grad_(True)
+    n = torch.from_numpy(g[tag + "_normals"]).to(device).requires_grad_(True)
+    xy = torch.from_numpy(g[tag + "_coords"]).to(device) if tag != "b" else None
+    w = {"depth_prior": 1.0, "planarity": 0.5, "manhattan": 0.2, "normal_consistency": 0.1}
+    with replay(g, tag):
+        total, parts = priors.fused_structural_losses(d, n, xy, w, 0.4, 0.5, replay=True)
+    total.backward()
+    return d, n, total, parts
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tag", CASES)
+def test_fused_priors_vs_reference(nerf, gpu, golden, tag):
+    """The device path (csrc/priors_fused.hip: three launches, every branch on the device) in replay
+    mode — the reference's draws and its LAPACK SVD of the k-means centres — against F18: losses to
+    1e-5, gradients to 1e-4 of each tensor's largest entry (as the eager GPU path above)."""
+    g = golden("f18_priors")
+    d, n, total, parts = run_fused(nerf, g, tag, gpu)
+    np.testing.assert_allclose(float(total), float(g[tag + "_total"]), rtol=1e-5)
+    p = parts.cpu().numpy()
+    got = {"manhattan_floor": p[0], "manhattan_wall": p[1], "manhattan_general": p[2], "planarity": p[4],
+           "normal_consistency": p[5]}
+    for k in got:
+        key = f"{tag}_part_{k}"
+        np.testing.assert_allclose(got[k], float(g[key]) if key in g else 0.0, rtol=1e-5, atol=1e-7, err_msg=k)
+    for t, ref in ((d, g[tag + "_dd"]), (n, g[tag + "_dn"])):
+        got_g = t.grad.cpu().numpy()
+        scale = float(np.abs(ref).max()) + 1e-30
+        assert np.abs(got_g - ref).max() <= 1e-4 * scale, (tag, np.abs(got_g - ref).max(), scale)
+
+
+@pytest.mark.gpu
+def test_fused_priors_device_mode(nerf, gpu, golden):
+    """Device mode (Philox draws, device 3x3 SVD): the SVD of the k-means centres is a valid SVD in
+    the documented convention (singular values descending, each V column's largest component
+    positive), the frame is U @ V with the det flip, the pairs are distinct members of their class,
+    and the loss is a deterministic function of (seed, offset)."""
+    from indoor_nerf_amd import priors
+    g = golden("f18_priors")
+    d = torch.from_numpy(g["a_depth"]).to(gpu).requires_grad_(True)
+    n = torch.from_numpy(g["a_normals"]).to(gpu).requires_grad_(True)
+    xy = torch.from_numpy(g["a_coords"]).to(gpu)
+    nerf.manual_seed(5)
+    t1, _ = priors.fused_structural_losses(d, n, xy)
+    t1.backward()
+    st = priors._FUSED_WS[str(gpu)][:1024].view(torch.float32).cpu()
+    sti = st.view(torch.int32)
+    assert int(sti[6]) == 1, "k-means ran"
+    # PriorsState (csrc/priors_fused.hip): 14 ints, M, parts[7], centres[9], means[9], 6 ints, U, S, V, frame
+    centres = st[22:31].reshape(3, 3).double()
+    U, S, V, frame = (st[46:55].reshape(3, 3).double(), st[55:58].double(), st[58:67].reshape(3, 3).double(),
+                      st[67:76].reshape(3, 3).double())
+    A = centres.T
+    assert torch.allclose(U @ torch.diag(S) @ V.T, A, atol=1e-5)
+    assert torch.allclose(U.T @ U, torch.eye(3, dtype=torch.float64), atol=1e-5)
+    assert torch.allclose(V.T @ V, torch.eye(3, dtype=torch.float64), atol=1e-5)
+    assert S[0] >= S[1] >= S[2]
+    for k in range(3):
+        assert V[V[:, k].abs().argmax(), k] > 0
+    F_ = U @ V
+    if torch.det(F_) < 0:
+        F_[:, 2] *= -1
+    assert torch.allclose(frame, F_, atol=1e-5)
+    assert torch.isfinite(d.grad).all() and torch.isfinite(n.grad).all()
+    assert float(d.grad.abs().sum()) > 0 and float(n.grad.abs().sum()) > 0
+    nerf.manual_seed(5)
+    d2, n2 = d.detach().clone().requires_grad_(True), n.detach().clone().requires_grad_(True)
+    t2, _ = priors.fused_structural_losses(d2, n2, xy)
+    assert float(t1) == float(t2)
+
+
+@pytest.mark.gpu
+def test_graphed_priors_step_matches_eager(nerf, gpu):
+    """A captured ScanNet iteration (device priors, ramp as a per-step graph slot) against the same
+    iteration launched eagerly from the same state and seed: same loss (the ramp moves every step)."""
+    import copy
+    from indoor_nerf_amd.graphs import GraphedTrainStep
+    from indoor_nerf_amd.synthetic import scannet_bbox, scannet_rays
+    lo, hi = scannet_bbox()
+    losses = {}
+    for mode in ("graph", "eager"):
+        args = nerf.make_args(bounding_box=(torch.from_numpy(lo), torch.from_numpy(hi)), finest_res=512,
+                              N_samples=64, N_importance=64, white_bkgd=False, use_structural_priors=True,
+                              structural_loss_start_iter=0, structural_loss_ramp_iters=10, tv_loss_weight=0.0)
+        torch.manual_seed(0)
+        nerf.manual_seed(11)
+        kw, _, _, grad_vars, opt = nerf.create_nerf(args, device=gpu)
+        kw.update(near=0.1, far=10.0)
+        ro, rd, _ = scannet_rays(1024, seed=6)
+        rays = (torch.from_numpy(ro).to(gpu), torch.from_numpy(rd).to(gpu))
+        target = torch.rand(1024, 3, device=gpu, generator=torch.Generator(device=gpu).manual_seed(1))
+        st = GraphedTrainStep(rays, target, kw, opt, args, warmup=1)
+        out = []
+        for it in range(1, 6):
+            loss, _ = (st(it) if mode == "graph" else st.eager_step(it))
+            out.append(float(loss))
+        if mode == "graph":
+            assert st.captures == 1
+        losses[mode] = out
+    np.testing.assert_allclose(losses["graph"], losses["eager"], rtol=2e-4)
