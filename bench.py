@@ -176,6 +176,9 @@ def parse():
     ap.add_argument("--zero", type=int, default=1,
                     help="N>1: shard the optimizer (reduce-scatter -> RAdam on 1/N -> all-gather, dist.ShardedOptimizer); "
                          "0 = all-reduce + replicated RAdam")
+    ap.add_argument("--deterministic", type=int, default=0,
+                    help="1: bitwise-reproducible backward (nerf.set_deterministic: fixed-point hash owner pass, "
+                         "ordered MLP weight-gradient reduction)")
     ap.add_argument("--mode", default="train", choices=["train", "render"],
                     help="train: full training iteration (the metric); render: render-only (eval modules, no grad)")
     return ap.parse_args()
@@ -300,6 +303,8 @@ def main():
     args = nerf.make_args(bounding_box=(torch.from_numpy(lo), torch.from_numpy(hi)), **wl["args"])
     torch.manual_seed(0)
     nerf.manual_seed(1234 + rank)
+    if a.deterministic:
+        nerf.set_deterministic(True)
     kw, kw_test, _, grad_vars, opt = nerf.create_nerf(args, device=dev)
     for d in (kw, kw_test):
         d.update(near=wl["near"], far=wl["far"])     # train() adds the scene bounds (run_nerf.py:768-770,865-869)
@@ -453,6 +458,16 @@ def main():
         "kernels": {k: {kk: round(vv, 4) if isinstance(vv, float) else vv for kk, vv in v.items()}
                     for k, v in sorted(kernels.items(), key=lambda kv: -kv[1]["total_ms"])},
     }
+    if a.deterministic:
+        out["deterministic"] = True
+    # north star "PSNR within 0.1 dB of reference": the committed result of tests/test_gpu_converge.py
+    # (the reference trained on F19 six times vs six HIP runs; late-phase mean PSNR difference per metric)
+    pv = os.path.join(ROOT, "profiles", "r02_psnr_vs_reference.json")
+    if os.path.exists(pv):
+        pj = json.load(open(pv))
+        out["psnr_vs_reference"] = {k: {"d_db": v["d_db"], "reference_db": v["reference_db"], "hip_db": v["hip_db"]}
+                                    for k, v in pj.items() if isinstance(v, dict)}
+        out["psnr_vs_reference"]["source"] = "profiles/r02_psnr_vs_reference.json"
     if rank == 0 and world == 1 and not a.no_cpu_baseline and a.workload == "lego" and a.mode == "train":
         out["cpu_baseline"] = cpu_baseline(a.cpu_rays, a.cpu_steps)
     elif rank == 0:

@@ -108,8 +108,7 @@ int nerf_hash_encode_bwd_ws(const float* d_xyz, int64_t n_points,
  * nerf_hash_encode_bwd_workspace_bytes(n_levels, log2_T, 256 * chunk_capacity, deterministic)); a
  * bin call writes its ceil(n_points / 256) chunks from chunk_base on, and the owner call sums chunks
  * [0, n_chunks) into d_dtables (ACCUMULATED). Calls sharing a workspace must be stream-ordered and
- * use the same n_levels, log2_T, chunk_capacity and deterministic; the batch starts with the bin call
- * at chunk_base 0. */
+ * use the same n_levels, log2_T, chunk_capacity and deterministic. */
 int nerf_hash_encode_bwd_bin(const float* d_xyz, int64_t n_points,
                              const float* bbox_min3, const float* bbox_max3,
                              const float* level_res, int n_levels, int log2_T,
@@ -223,7 +222,8 @@ int nerf_mlp_bwd_batch(const nerf_mlp_bwd_job* jobs, int n_jobs, float* d_det_wo
  * fwd: raw7 [P,7] = [raw4, n]; with d_keep, n_z := 0 where !keep (run_network's mask hits the LAST
  *      channel, run_nerf.py:66). bwd: from graw7 writes graw4 [P,4] (the MLP's upstream grad) and
  *      dgeo [P,16] (row 0 = 0), and ACCUMULATES the head's weight gradients into *grads
- *      (dN0 = dhid^T geo, db0 = sum dhid, dN1 = dn^T hid, db1 = sum dn, summed in-kernel). */
+ *      (dN0 = dhid^T geo, db0 = sum dhid, dN1 = dn^T hid, db1 = sum dn, summed in-kernel; per-block
+ *      sums in d_workspace (>= nerf_normal_head_bwd_workspace_bytes()) reduced in a fixed order). */
 typedef struct {
     const float* n0;
     const float* b0;
@@ -240,9 +240,11 @@ typedef struct {
 
 int nerf_normal_head_fwd(const float* d_o16, const float* d_raw4, const uint8_t* d_keep, int64_t n_points,
                          const nerf_normal_head* head, float* d_raw7, void* stream);
+size_t nerf_normal_head_bwd_workspace_bytes(void);
 int nerf_normal_head_bwd(const float* d_o16, const uint8_t* d_keep, int64_t n_points,
                          const nerf_normal_head* head, const float* d_graw7, float* d_graw4, float* d_dgeo,
-                         const nerf_normal_head_grads* grads, void* stream);
+                         const nerf_normal_head_grads* grads, float* d_workspace, size_t workspace_bytes,
+                         void* stream);
 
 /* ---- volume compositing (raw2outputs, run_nerf.py:347-411), one wavefront per ray ----------
  * d_raw [R,S,raw_channels] (4, or 7 with normals), d_z [R,S], d_rays_d [R,3] (unnormalised),

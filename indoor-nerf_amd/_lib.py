@@ -111,7 +111,7 @@ SIGNATURES = {
     "nerf_mlp_bwd_batch": [ctypes.POINTER(MlpBwdJob), c_int, c_vp, ctypes.c_size_t, c_vp],
     "nerf_normal_head_fwd": [c_vp, c_vp, c_vp, c_i64, ctypes.POINTER(NormalHead), c_vp, c_vp],
     "nerf_normal_head_bwd": [c_vp, c_vp, c_i64, ctypes.POINTER(NormalHead), c_vp, c_vp, c_vp,
-                             ctypes.POINTER(NormalHeadGrads), c_vp],
+                             ctypes.POINTER(NormalHeadGrads), c_vp, ctypes.c_size_t, c_vp],
     "nerf_composite_fwd": [c_vp, c_int, c_vp, c_vp, c_vp, c_i64, c_int, c_int,
                            c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
     "nerf_composite_bwd": [c_vp, c_int, c_vp, c_vp, c_vp, c_i64, c_int, c_int,
@@ -167,6 +167,8 @@ def load():
     lib.nerf_abi_version.argtypes = []
     lib.nerf_hash_encode_bwd_workspace_bytes.restype = ctypes.c_size_t
     lib.nerf_hash_encode_bwd_workspace_bytes.argtypes = [c_int, c_int, c_i64, c_int]
+    lib.nerf_normal_head_bwd_workspace_bytes.restype = ctypes.c_size_t
+    lib.nerf_normal_head_bwd_workspace_bytes.argtypes = []
     lib.nerf_priors_workspace_bytes.restype = ctypes.c_size_t
     lib.nerf_priors_workspace_bytes.argtypes = [c_i64]
     lib.nerf_mlp_bwd_det_workspace_bytes.restype = ctypes.c_size_t
@@ -183,7 +185,8 @@ def load():
 
 def exported_symbols():
     return ["nerf_last_error", "nerf_abi_version", "nerf_hash_encode_bwd_workspace_bytes",
-            "nerf_quant_packed_bytes", "nerf_mlp_bwd_det_workspace_bytes", "nerf_priors_workspace_bytes"] + list(SIGNATURES)
+            "nerf_quant_packed_bytes", "nerf_mlp_bwd_det_workspace_bytes", "nerf_priors_workspace_bytes",
+            "nerf_normal_head_bwd_workspace_bytes"] + list(SIGNATURES)
 
 
 _TIMING = None   # when a list: (name, start_event, end_event) per launch, recorded on the current stream

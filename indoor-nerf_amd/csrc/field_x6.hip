@@ -901,13 +901,17 @@ __global__ void __launch_bounds__(512, 1) mlp_bwd_x6cg_kernel(MlpBwdJobs jobs) {
 }
 
 // Deterministic weight-gradient reduction: value i of a net's gradient image summed over the net's
-// blocks [b0, b0 + nb) in block order, then added to .grad (the sole writer: no atomics).
+// blocks [b0, b0 + nb) — one wave per value, lane l taking blocks l, l + 64, ... in order, then a
+// fixed-order wave tree — and added to .grad (the sole writer: no atomics).
 __global__ void __launch_bounds__(256) mlp_wgrad_reduce_kernel(const float* __restrict__ ws, int b0, int nb,
                                                                nerf_mlp_grads G) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (i >= GW_TOTAL) return;
     float s = 0.f;
-    for (int b = 0; b < nb; ++b) s += ws[(size_t)(b0 + b) * GW_TOTAL + i];
+    for (int b = lane; b < nb; b += 64) s += ws[(size_t)(b0 + b) * GW_TOTAL + i];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    if (lane != 0) return;
     if (i < GW_W1) G.w0[i - GW_W0] += s;
     else if (i < GW_C0) G.w1[i - GW_W1] += s;
     else if (i < GW_C1) G.c0[i - GW_C0] += s;
@@ -980,8 +984,8 @@ int launch_mlp_bwd_x6(const MlpArgs* jobs, int n_jobs, float* det_ws, hipStream_
     if (det_ws) {
         for (int k = 0; k < n_jobs; ++k) {
             const int b0 = k == 0 ? 0 : J.split, nb = k == 0 ? J.split : (int)blocks - J.split;
-            hipLaunchKernelGGL(mlp_wgrad_reduce_kernel, dim3((GW_TOTAL + 255) / 256), dim3(256), 0, stream, det_ws, b0,
-                               nb, jobs[k].G);
+            hipLaunchKernelGGL(mlp_wgrad_reduce_kernel, dim3((GW_TOTAL + 3) / 4), dim3(256), 0, stream, det_ws, b0, nb,
+                               jobs[k].G);
         }
         NERF_CHECK_LAUNCH("mlp_bwd(x6) deterministic reduction");
     }

@@ -33,7 +33,7 @@ struct HashGradParams {
     int chunk_stride;     // chunk capacity of the workspace (the layout stride)
     int slice_log2;       // owner slice = 2^slice_log2 rows (LDS: 16 B per row, 32 B deterministic)
     int owner_log2;       // owners per level = 2^owner_log2
-    uint32_t* lvl_max;    // deterministic mode: per level max |entry| (float bits), else null
+    float* chunk_max;     // deterministic mode: [L][chunk_stride] max |entry| of each chunk, else null
 };
 
 // QUANT: every gathered corner feature goes through the level's A-CAQ quantizer first
@@ -222,14 +222,19 @@ __global__ void __launch_bounds__(256) hash_encode_bwd_kernel(
                 s_eg[k] = make_float2(cgx[c], cgy[c]);
             }
         }
-        if (hp.lvl_max) {   // deterministic mode: the level's largest |entry| sets the owners' fixed-point scale
+        if (hp.chunk_max) {   // deterministic mode: the level's largest |entry| sets the owners' fixed-point scale
             float m = 0.f;
 #pragma unroll
             for (int c = 0; c < 8; ++c)
                 if (pos[c] != kSkip) m = fmaxf(m, fmaxf(fabsf(cgx[c]), fabsf(cgy[c])));
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
-            if (lane == 0 && m > 0.f) atomicMax(hp.lvl_max + lvl, __float_as_uint(m));   // non-negative: uint order
+            __shared__ float s_wmax[4];
+            if (lane == 0) s_wmax[threadIdx.x >> 6] = m;
+            __syncthreads();
+            if (threadIdx.x == 0)   // one plain store per chunk (per-level atomics serialise 4096 blocks)
+                hp.chunk_max[(size_t)lvl * hp.chunk_stride + hp.chunk_base + blockIdx.x] =
+                    fmaxf(fmaxf(s_wmax[0], s_wmax[1]), fmaxf(s_wmax[2], s_wmax[3]));
         }
         __syncthreads();
         const uint32_t total = s_start[n_own];
@@ -300,11 +305,20 @@ __global__ void __launch_bounds__(THREADS) hash_bwd_owner_kernel(HashGradParams 
     const int S = 1 << hp.slice_log2, n_own = 1 << hp.owner_log2;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     for (int i = tid; i < (DET ? 2 : 1) * S; i += kOwnerThreads) s_slice[i] = make_double2(0.0, 0.0);
-    // DET: scale exponents (hi: 2^sh, lo: 2^(sh + L)); a level without entries has lvl_max 0
+    // DET: scale exponents (hi: 2^sh, lo: 2^(sh + L)) from the level's largest |entry| (the max of
+    // the chunks' maxima; a level without entries has max 0)
     int sh = 0, sl_ = 0;
     if constexpr (DET) {
+        float m = 0.f;
+        for (int c = tid; c < hp.nchunks; c += kOwnerThreads) m = fmaxf(m, hp.chunk_max[(size_t)lvl * hp.chunk_stride + c]);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+        if (lane == 0) s_wsum[wave] = __float_as_uint(m);
+        __syncthreads();
+        for (int w = 0; w < kOwnerThreads / 64; ++w) m = fmaxf(m, __uint_as_float(s_wsum[w]));
+        __syncthreads();   // s_wsum is reused by the window scans
         int E;
-        (void)frexpf(__uint_as_float(hp.lvl_max[lvl]), &E);                 // max |entry| < 2^E
+        (void)frexpf(m, &E);                                                // max |entry| < 2^E
         const int b = 11 + (32 - __clz((unsigned)max(hp.nchunks - 1, 1)));  // entries <= 2^b
         sh = 62 - E - b;
         sl_ = sh + (61 - b);
@@ -501,7 +515,7 @@ static bool make_bin_plan(int n_levels, int log2_T, int64_t n_points, BinPlan& B
     B.off_h = up(entries * sizeof(float2));
     B.off_off = B.off_h + up(entries * sizeof(uint16_t));
     B.off_max = B.off_off + up(offs * sizeof(uint32_t));
-    B.total = B.off_max + (det ? up(NERF_MAX_LEVELS * sizeof(uint32_t)) : 0);
+    B.total = B.off_max + (det ? up((size_t)n_levels * B.nchunks * sizeof(float)) : 0);
     return true;
 }
 
@@ -567,7 +581,7 @@ static int bin_layout(const char* who, int n_levels, int log2_T, int64_t chunk_c
     hp.bin_g = reinterpret_cast<float2*>(ws + B.off_g);
     hp.bin_h = reinterpret_cast<uint16_t*>(ws + B.off_h);
     hp.bin_seg = reinterpret_cast<uint32_t*>(ws + B.off_off);
-    hp.lvl_max = det ? reinterpret_cast<uint32_t*>(ws + B.off_max) : nullptr;
+    hp.chunk_max = det ? reinterpret_cast<float*>(ws + B.off_max) : nullptr;
     hp.chunk_stride = B.nchunks;
     hp.slice_log2 = B.slice_log2;
     hp.owner_log2 = B.owner_log2;
@@ -597,14 +611,6 @@ extern "C" int nerf_hash_encode_bwd_bin(const float* d_xyz, int64_t n_points, co
     NERF_REQUIRE(chunk_base >= 0 && chunk_base + nch <= chunk_capacity,
                  "hash_encode_bwd_bin: chunks [%lld, %lld) exceed the capacity %lld", (long long)chunk_base,
                  (long long)(chunk_base + nch), (long long)chunk_capacity);
-    // deterministic: the first bin call of a batch resets the per-level maxima (a memset node under capture)
-    if (hp.lvl_max && chunk_base == 0) {
-        const hipError_t e = hipMemsetAsync(hp.lvl_max, 0, NERF_MAX_LEVELS * sizeof(uint32_t), as_stream(stream));
-        if (e != hipSuccess) {
-            set_error("hash_encode_bwd_bin: hipMemsetAsync: %s", hipGetErrorString(e));
-            return NERF_E_LAUNCH;
-        }
-    }
     if (n_points == 0) return NERF_OK;
     for (int a = 0; a < 3; ++a) { hp.bmin[a] = bbox_min3[a]; hp.bmax[a] = bbox_max3[a]; }
     fill_cells(hp.cell, bbox_min3, bbox_max3, level_res, n_levels);

@@ -97,25 +97,38 @@ __device__ T block_sum(T v, T* red) {
     return t;
 }
 
-// K sums at once (one barrier pair instead of K): red holds 16 x K floats
+// wave64 total through DPP (row_shr 1/2/4/8 scan, then row_bcast 15/31: lane 63 holds the sum),
+// read back as a wave-uniform value: no LDS crossbar and no per-step lane-address registers
+__device__ __forceinline__ float wave_total(float x) {
+    x += dpp_move<0x111, 0xF>(x);
+    x += dpp_move<0x112, 0xF>(x);
+    x += dpp_move<0x114, 0xF>(x);
+    x += dpp_move<0x118, 0xF>(x);
+    x += dpp_move<0x142, 0xA>(x);
+    x += dpp_move<0x143, 0xC>(x);
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 63));
+}
+
+// K sums at once (two barriers instead of two per sum): red holds 16 x K + K floats; thread k < K
+// adds the 16 wave totals of value k, then every thread reads the K block totals
 template <int K>
 __device__ void block_sum_vec(float (&v)[K], float* red) {
 #pragma unroll
-    for (int k = 0; k < K; ++k)
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o, 64);
+    for (int k = 0; k < K; ++k) v[k] = wave_total(v[k]);
     const int w = threadIdx.x >> 6;
     __syncthreads();
     if ((threadIdx.x & 63) == 0)
 #pragma unroll
         for (int k = 0; k < K; ++k) red[w * K + k] = v[k];
     __syncthreads();
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
+    if (threadIdx.x < K) {
         float t = 0.f;
-        for (int j = 0; j < kPT / 64; ++j) t += red[j * K + k];
-        v[k] = t;
+        for (int j = 0; j < kPT / 64; ++j) t += red[j * K + threadIdx.x];
+        red[16 * K + threadIdx.x] = t;
     }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < K; ++k) v[k] = red[16 * K + k];
 }
 
 // exclusive prefix of a 0/1 flag over the block's ray range [base, base + kPT), + block total
@@ -160,22 +173,27 @@ __device__ void svd3(const float* A_, float* U, float* S, float* V) {
     for (int sweep = 0; sweep < 30; ++sweep) {   // cyclic Jacobi on B = A^T A
         double off = fabs(B[0][1]) + fabs(B[0][2]) + fabs(B[1][2]);
         if (off < 1e-30) break;
+#pragma unroll
         for (int p = 0; p < 2; ++p)
+#pragma unroll
             for (int q = p + 1; q < 3; ++q) {
                 if (fabs(B[p][q]) < 1e-300) continue;
                 const double th = (B[q][q] - B[p][p]) / (2.0 * B[p][q]);
                 const double t = (th >= 0 ? 1.0 : -1.0) / (fabs(th) + sqrt(th * th + 1.0));
                 const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
+#pragma unroll
                 for (int k = 0; k < 3; ++k) {   // B <- J^T B J
                     const double bkp = B[k][p], bkq = B[k][q];
                     B[k][p] = c * bkp - s * bkq;
                     B[k][q] = s * bkp + c * bkq;
                 }
+#pragma unroll
                 for (int k = 0; k < 3; ++k) {
                     const double bpk = B[p][k], bqk = B[q][k];
                     B[p][k] = c * bpk - s * bqk;
                     B[q][k] = s * bpk + c * bqk;
                 }
+#pragma unroll
                 for (int k = 0; k < 3; ++k) {
                     const double qkp = Q[k][p], qkq = Q[k][q];
                     Q[k][p] = c * qkp - s * qkq;
@@ -183,21 +201,30 @@ __device__ void svd3(const float* A_, float* U, float* S, float* V) {
                 }
             }
     }
-    int ord[3] = {0, 1, 2};   // descending eigenvalues
-    for (int i = 0; i < 3; ++i)
-        for (int j = i + 1; j < 3; ++j)
-            if (B[ord[j]][ord[j]] > B[ord[i]][ord[i]]) { const int t = ord[i]; ord[i] = ord[j]; ord[j] = t; }
+    // descending eigenvalues: a 3-element sorting network of column swaps (constant indices only,
+    // so the matrices stay in registers)
+    double e[3] = {B[0][0], B[1][1], B[2][2]};
+    auto swapcol = [&](int i, int j) {
+        const double t = e[i]; e[i] = e[j]; e[j] = t;
+#pragma unroll
+        for (int r = 0; r < 3; ++r) { const double q = Q[r][i]; Q[r][i] = Q[r][j]; Q[r][j] = q; }
+    };
+    if (e[1] > e[0]) swapcol(0, 1);
+    if (e[2] > e[0]) swapcol(0, 2);
+    if (e[2] > e[1]) swapcol(1, 2);
     double v[3][3], u[3][3], s[3];
+#pragma unroll
     for (int k = 0; k < 3; ++k) {
-        const int o = ord[k];
-        int big = 0;
-        for (int r = 1; r < 3; ++r)
-            if (fabs(Q[r][o]) > fabs(Q[big][o])) big = r;
-        const double sg = Q[big][o] < 0 ? -1.0 : 1.0;   // sign convention: largest |component| positive
-        for (int r = 0; r < 3; ++r) v[r][k] = sg * Q[r][o];
-        s[k] = sqrt(fmax(B[o][o], 0.0));
+        const double a0 = fabs(Q[0][k]), a1 = fabs(Q[1][k]), a2 = fabs(Q[2][k]);
+        const double pick = (a0 >= a1 && a0 >= a2) ? Q[0][k] : (a1 >= a2 ? Q[1][k] : Q[2][k]);
+        const double sg = pick < 0 ? -1.0 : 1.0;   // sign convention: largest |component| positive
+#pragma unroll
+        for (int r = 0; r < 3; ++r) v[r][k] = sg * Q[r][k];
+        s[k] = sqrt(fmax(e[k], 0.0));
     }
+#pragma unroll
     for (int k = 0; k < 3; ++k) {
+#pragma unroll
         for (int r = 0; r < 3; ++r) u[r][k] = A[r][0] * v[0][k] + A[r][1] * v[1][k] + A[r][2] * v[2][k];
         const double l = sqrt(u[0][k] * u[0][k] + u[1][k] * u[1][k] + u[2][k] * u[2][k]);
         if (s[k] > 1e-12 * fmax(s[0], 1e-300) && l > 0) {
@@ -227,9 +254,9 @@ __device__ void svd3(const float* A_, float* U, float* S, float* V) {
 
 // ================================================================ prep: masks, counts, k-means, SVD
 __global__ void __launch_bounds__(kPT) priors_prep_kernel(PriorsArgs a) {
-    __shared__ float s_red[16 * 12];
-    __shared__ int s_ired[16];
+    __shared__ float s_red[17 * 12];
     __shared__ float s_c[9];
+    extern __shared__ float s_nz[];   // [N][3] normalised normals: the 10 k-means rounds read them from LDS
     PriorsState& st = *a.st;
     const int N = a.N, tid = threadIdx.x;
     int ns = 0, nf = 0, nw = 0, nk = 0;
@@ -241,6 +268,7 @@ __global__ void __launch_bounds__(kPT) priors_prep_kernel(PriorsArgs a) {
         const bool fl = stable && az > a.normal_thr, wa = stable && az < 1.0f - a.normal_thr;
         const bool keep = len > a.conf_thr;
         a.cls[i] = (uint8_t)((fl ? 1 : 0) | (wa ? 2 : 0) | (stable ? 4 : 0) | (keep ? 8 : 0));
+        s_nz[3 * i] = n[0]; s_nz[3 * i + 1] = n[1]; s_nz[3 * i + 2] = keep ? n[2] : NAN;   // NaN z: not kept
         ns += stable; nf += fl; nw += wa; nk += keep;
     }
     {
@@ -271,8 +299,9 @@ __global__ void __launch_bounds__(kPT) priors_prep_kernel(PriorsArgs a) {
             const U4 u0 = philox_uniform4(sd, of, 2 * tid), u1 = philox_uniform4(sd, of, 2 * tid + 1);
             const float uu[4] = {u0.x, u0.y, u0.z, u0.w}, vv[4] = {u1.x, u1.y, u1.z, u1.w};
             for (int c = 0; c < 3; ++c) {
-                const float m = sqrtf(-2.0f * logf(fmaxf(uu[c], 1e-12f)));
-                r[c] = m * cosf(6.283185307179586f * vv[c]);
+                // v_cos_f32 takes revolutions: cos(2 pi v) without the full-range reduction of cosf
+                const float m = sqrtf(-2.0f * __logf(fmaxf(uu[c], 1e-12f)));
+                r[c] = m * __builtin_amdgcn_cosf(vv[c]);
             }
         }
         const float d = fmaxf(norm3(r[0], r[1], r[2]), 1e-12f);
@@ -280,52 +309,54 @@ __global__ void __launch_bounds__(kPT) priors_prep_kernel(PriorsArgs a) {
     }
     __syncthreads();
     for (int it = 0; it < 10; ++it) {
-        float acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-        int cnt[3] = {0, 0, 0};
+        float red[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};   // 9 coordinate sums + 3 counts (exact in fp32)
+        const float c00 = s_c[0], c01 = s_c[1], c02 = s_c[2], c10 = s_c[3], c11 = s_c[4], c12 = s_c[5],
+                    c20 = s_c[6], c21 = s_c[7], c22 = s_c[8];
         for (int i = tid; i < N; i += kPT) {
+            const float x = s_nz[3 * i], y = s_nz[3 * i + 1], z = s_nz[3 * i + 2];
             int8_t asg = -1;
-            if (a.cls[i] & 8) {
-                float n[3], len;
-                load_nz(a, i, n, len);
-                float best = dot3(n, s_c);
-                asg = 0;
-                for (int k = 1; k < 3; ++k) {   // torch.argmax: first maximum
-                    const float s = dot3(n, s_c + 3 * k);
-                    if (s > best) { best = s; asg = (int8_t)k; }
-                }
-                for (int c = 0; c < 3; ++c) acc[3 * asg + c] += n[c];
-                ++cnt[asg];
+            if (z == z) {   // kept
+                const float d0 = (x * c00 + y * c01) + z * c02, d1 = (x * c10 + y * c11) + z * c12,
+                            d2 = (x * c20 + y * c21) + z * c22;
+                asg = 0;   // torch.argmax: first maximum
+                float best = d0;
+                if (d1 > best) { best = d1; asg = 1; }
+                if (d2 > best) asg = 2;
+#pragma unroll
+                for (int k = 0; k < 3; ++k)
+                    if (asg == k) { red[3 * k] += x; red[3 * k + 1] += y; red[3 * k + 2] += z; red[9 + k] += 1.f; }
             }
             a.assign[(size_t)it * N + i] = asg;
         }
-        float red[12];   // 9 coordinate sums + 3 counts (exact in fp32)
-        for (int k = 0; k < 9; ++k) red[k] = acc[k];
-        for (int k = 0; k < 3; ++k) red[9 + k] = (float)cnt[k];
         block_sum_vec<12>(red, s_red);
-        const float* sums = red;
-        int counts[3];
-        for (int k = 0; k < 3; ++k) counts[k] = (int)red[9 + k];
         __syncthreads();
-        if (tid < 3 && counts[tid] > 0) {   // centre = F.normalize(mean); an empty cluster keeps its centre
-            float m[3];
-            for (int c = 0; c < 3; ++c) m[c] = sums[3 * tid + c] / (float)counts[tid];
-            const float d = fmaxf(norm3(m[0], m[1], m[2]), 1e-12f);
-            for (int c = 0; c < 3; ++c) {
-                s_c[3 * tid + c] = m[c] / d;
-                st.means[3 * tid + c] = m[c];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {   // centre = F.normalize(mean); an empty cluster keeps its centre
+            if (tid == k && red[9 + k] > 0.f) {
+                const float m[3] = {red[3 * k] / red[9 + k], red[3 * k + 1] / red[9 + k], red[3 * k + 2] / red[9 + k]};
+                const float d = fmaxf(norm3(m[0], m[1], m[2]), 1e-12f);
+                for (int c = 0; c < 3; ++c) {
+                    s_c[3 * k + c] = m[c] / d;
+                    st.means[3 * k + c] = m[c];
+                }
+                st.centre_iter[k] = it;
+                st.centre_count[k] = (int)red[9 + k];
             }
-            st.centre_iter[tid] = it;
-            st.centre_count[tid] = counts[tid];
         }
         __syncthreads();
     }
     if (tid < 9) st.centres[tid] = s_c[tid];
-    if (tid == 0 && !a.usv) {   // device SVD of A = centres^T
-        float A[9];
-        for (int r = 0; r < 3; ++r)
-            for (int c = 0; c < 3; ++c) A[3 * r + c] = s_c[3 * c + r];
-        svd3(A, st.U, st.S, st.V);
-    }
+}
+
+// Device SVD of A = centres^T (fp64 Jacobi), its own one-wave launch: inside the 1024-thread prep
+// kernel (128 VGPRs per lane) the fp64 matrices spill to scratch.
+__global__ void __launch_bounds__(64) priors_svd_kernel(PriorsArgs a) {
+    PriorsState& st = *a.st;
+    if (threadIdx.x != 0 || !st.kmeans) return;
+    float A[9];
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) A[3 * r + c] = st.centres[3 * c + r];
+    svd3(A, st.U, st.S, st.V);
 }
 
 // ---- bitonic sort of up to 8192 64-bit keys in LDS (device-mode randperm) ------------------------
@@ -346,7 +377,7 @@ __device__ void bitonic_sort(uint64_t* k, int M) {
 
 // ================================================================ losses
 __global__ void __launch_bounds__(kPT) priors_loss_kernel(PriorsArgs a) {
-    __shared__ float s_red[16 * 4];
+    __shared__ float s_red[17 * 4];
     __shared__ int s_ired[16];
     __shared__ float s_f[9];
     __shared__ int s_cnt[3];
@@ -559,7 +590,7 @@ __device__ __forceinline__ void tr3(const double* A, double* T) {
 
 __global__ void __launch_bounds__(kPT) priors_bwd_kernel(PriorsArgs a) {
     extern __shared__ float s_g[];    // [N][4]: d nz (3), d depth
-    __shared__ float s_red[16 * 9];
+    __shared__ float s_red[17 * 9];
     __shared__ float s_gF[9];
     __shared__ float s_gmean[9];
     const PriorsState& st = *a.st;
@@ -787,8 +818,12 @@ extern "C" int nerf_priors_prep(const float* d_depth, const float* d_normals, co
     PriorsArgs a{};
     int rc = priors_args(a, d_depth, d_normals, d_coords, n_rays, cfg, d_workspace, workspace_bytes);
     if (rc) return rc;
-    hipLaunchKernelGGL(priors_prep_kernel, dim3(1), dim3(kPT), 0, as_stream(stream), a);
+    hipLaunchKernelGGL(priors_prep_kernel, dim3(1), dim3(kPT), (size_t)3 * n_rays * sizeof(float), as_stream(stream), a);
     NERF_CHECK_LAUNCH("priors_prep");
+    if (!cfg->usv) {
+        hipLaunchKernelGGL(priors_svd_kernel, dim3(1), dim3(64), 0, as_stream(stream), a);
+        NERF_CHECK_LAUNCH("priors_prep (svd)");
+    }
     if (d_centres_out) {   // the final k-means centres [3,3] (rows), for the host SVD of replay mode
         const hipError_t e = hipMemcpyAsync(d_centres_out, a.st->centres, 9 * sizeof(float), hipMemcpyDeviceToDevice,
                                             as_stream(stream));

@@ -47,25 +47,25 @@ _ALIGN = 64      # elements: every rank's shard starts on a 256-B boundary (vect
 
 
 class GradArena:
-    """One flat fp32 buffer holding the .grad of every parameter (views), in parameter order.
-    pad_to: round the buffer up to a multiple of this many elements (the sharded optimizer needs
-    world x _ALIGN) — the tail is never a gradient and stays zero."""
+    """One flat fp32 buffer holding the .grad of every parameter (views), in parameter order, each
+    starting on a 256-B boundary (_ALIGN elements: the fused RAdam's float4 path needs 16-B aligned
+    tensors, and a 3-element bias would otherwise misalign every gradient after it). pad_to: round
+    the buffer up to a multiple of this many elements (the sharded optimizer needs world x _ALIGN)
+    — the gaps and the tail are never a gradient and stay zero."""
 
     def __init__(self, params, pad_to=1):
         # quantizer scalars (soft_bits, range_scale, v_max) never receive a gradient in the
         # reference (their uses are detached): they keep grad None, so the optimizer skips them
         self.params = [p for p in params if p.requires_grad and not getattr(p, "_nerf_no_grad", False)]
-        self.numel = sum(p.numel() for p in self.params)
+        self.offsets, off = [], 0
+        for p in self.params:
+            self.offsets.append(off)
+            off += -(-p.numel() // _ALIGN) * _ALIGN
+        self.numel = off
         total = -(-self.numel // pad_to) * pad_to
         dev = self.params[0].device
         self.flat = torch.zeros(total, device=dev, dtype=torch.float32)
-        self.views, self.offsets = [], []
-        off = 0
-        for p in self.params:
-            v = self.flat[off:off + p.numel()].view_as(p)
-            self.views.append(v)
-            self.offsets.append(off)
-            off += p.numel()
+        self.views = [self.flat[o:o + p.numel()].view_as(p) for p, o in zip(self.params, self.offsets)]
         self.attach()
 
     def attach(self):

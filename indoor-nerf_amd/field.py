@@ -75,10 +75,23 @@ def _head_backward(o16, keep, head, g7, needs):
     bufs = [accumulate_grad_buffers([t])[0] if need else torch.zeros_like(t) for t, need in zip(head, needs)]
     for name, t in zip(("n0", "b0", "n1", "b1"), bufs):
         setattr(g, name, _lib.ptr(t, "grad_normal_net." + name).value)
+    ws = _head_workspace(o16.device)
     _lib.call("nerf_normal_head_bwd", _lib.ptr(o16, "geo"), _lib.ptr(keep, "keep", dtype=torch.bool, allow_none=True),
               P, _head_struct(head), _lib.ptr(g7.contiguous(), "grad_raw"), _lib.ptr(graw4), _lib.ptr(dgeo), g,
-              _lib.stream())
+              _lib.ptr(ws, "head_workspace"), ws.numel() * 4, _lib.stream())
     return graw4, dgeo
+
+
+_HEAD_WS = {}
+
+
+def _head_workspace(device):
+    """Per-block partial sums of the head's weight gradients (one per device, fixed size; a captured
+    graph keeps its address, so it is never replaced)."""
+    key = str(device)
+    if key not in _HEAD_WS:
+        _HEAD_WS[key] = torch.empty(int(_lib.load().nerf_normal_head_bwd_workspace_bytes()) // 4, device=device)
+    return _HEAD_WS[key]
 
 
 class MLPFn(torch.autograd.Function):

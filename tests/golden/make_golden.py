@@ -398,7 +398,7 @@ def gen_train(ref, out):
 
 
 CONVERGE = dict(iters=300, R=256, every=20, lrate=5e-3, lrate_decay=500, sparsity=1e-10, table_scale=1e-4,
-                table_salt=19, seeds=(30, 31), batch_seed=20, threads=(8, 4))
+                table_salt=19, seeds=(30, 31), batch_seed=20, threads=(8, 4, 6, 2, 3, 5))
 
 
 def converge_run(ref, c, threads):
@@ -465,15 +465,15 @@ def gen_converge(ref, out, iters=None):
     to be replayed every iteration). Init: reference-scale tables (closed form, |v| <= 1e-4) and
     seeded nn.Linear init. Every `every` iterations: PSNR of held-out pixels of the training views
     and of a novel view, with the test-time kwargs (perturb 0, no noise); plus the PSNR of every
-    training batch. Two runs, with 8 and with 4 CPU threads (keys *_b): the reference's own
-    run-to-run spread, against which the HIP path's deviation is judged."""
+    training batch. Six runs, with 8, 4, 6, 2, 3 and 5 CPU threads (keys '', _b .. _f): the
+    reference's own run-to-run spread, against which the HIP path's deviation is judged."""
     c = dict(CONVERGE)
     if iters is not None:
         c["iters"] = iters
     d = {}
     for k, threads in enumerate(c["threads"]):
         init, batches, eval_iters, curves = converge_run(ref, c, threads)
-        suffix = "" if k == 0 else "_b"
+        suffix = "" if k == 0 else "_" + "bcdef"[k - 1]
         d.update({name + suffix: v for name, v in curves.items()})
     d.update(init)
     d.update(batches=batches, eval_iters=eval_iters, config=np.array(repr(c)))

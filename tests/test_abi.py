@@ -112,14 +112,14 @@ def test_hash_bwd_workspace_plan(nerf):
     lib = nerf.load_library()
     up = lambda v: (v + 255) // 256 * 256  # noqa: E731
     for L, log2_T, P in ((16, 19, 786432), (16, 19, 262144), (8, 12, 1000), (16, 14, 5), (16, 20, 1000)):
-        for det, slice_log2 in ((0, 13), (1, 12)):   # deterministic: 2^12-row slices + 16 level maxima
+        for det, slice_log2 in ((0, 13), (1, 12)):   # deterministic: 2^12-row slices + per-chunk maxima
             if det and log2_T > 19:
                 assert lib.nerf_hash_encode_bwd_workspace_bytes(L, log2_T, P, det) == 0
                 continue
             nch = (P + 255) // 256
             own = 1 << (log2_T - min(slice_log2, log2_T))
             ent = L * nch * 2048
-            expect = up(ent * 8) + up(ent * 2) + up(L * nch * own * 4) + (up(16 * 4) if det else 0)
+            expect = up(ent * 8) + up(ent * 2) + up(L * nch * own * 4) + (up(L * nch * 4) if det else 0)
             assert lib.nerf_hash_encode_bwd_workspace_bytes(L, log2_T, P, det) == expect
     assert lib.nerf_hash_encode_bwd_workspace_bytes(16, 21, 1000, 0) == 0
     assert lib.nerf_hash_encode_bwd_workspace_bytes(0, 19, 1000, 0) == 0

@@ -63,9 +63,9 @@ def main(K=6, det=False):
         res.append(dict(eval=float(np.mean(np.array(ev)[late])), novel=float(np.mean(np.array(nv)[late])),
                         train=float(tr[199:].mean()), eval_curve=[round(x, 3) for x in ev]))
         print(json.dumps(res[-1]), flush=True)
-    refs = {name: [float(g[name + s][late].mean()) for s in ("", "_b", "_c", "_d") if name + s in g]
+    refs = {name: [float(g[name + s][late].mean()) for s in ("", "_b", "_c", "_d", "_e", "_f") if name + s in g]
             for name in ("eval_psnr", "novel_psnr")}
-    refs["train_psnr"] = [float(g["train_psnr" + s][199:].mean()) for s in ("", "_b", "_c", "_d") if "train_psnr" + s in g]
+    refs["train_psnr"] = [float(g["train_psnr" + s][199:].mean()) for s in ("", "_b", "_c", "_d", "_e", "_f") if "train_psnr" + s in g]
     print(json.dumps({"hip_mean": {k: float(np.mean([r[k] for r in res])) for k in ("eval", "novel", "train")},
                       "hip_std": {k: float(np.std([r[k] for r in res], ddof=1)) for k in ("eval", "novel", "train")},
                       "ref": refs, "det": det}))
