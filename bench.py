@@ -63,7 +63,7 @@ STEP_RAY_BYTES = 64
 KERNEL_SYMBOLS = {
     "nerf_hash_encode_fwd": ["nerf::hash_encode_fwd_pair_kernel<false>"],
     "nerf_hash_encode_bwd_bin": ["nerf::hash_encode_bwd_kernel<3>"],
-    "nerf_hash_encode_bwd_owner": ["nerf::hash_bwd_owner_kernel<13, 1024>"],
+    "nerf_hash_encode_bwd_owner": ["nerf::hash_bwd_owner_kernel<13, 1024, false>"],
     "nerf_mlp_fwd": ["nerf::mlp_fwd_x6_kernel<false>"],
     "nerf_mlp_bwd": ["nerf::mlp_bwd_x6cg_kernel<false>"],
     "nerf_mlp_bwd_batch": ["nerf::mlp_bwd_x6cg_kernel<false>"],
