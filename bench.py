@@ -62,7 +62,8 @@ STEP_RAY_BYTES = 64
 # ABI call -> the kernel symbols it launches (rocprofv3 names), to attach PMC traffic per call
 KERNEL_SYMBOLS = {
     "nerf_hash_encode_fwd": ["nerf::hash_encode_fwd_pair_kernel<false>"],
-    "nerf_hash_encode_bwd_bin": ["nerf::hash_encode_bwd_kernel<3>"],
+    "nerf_hash_encode_bwd_bin": ["nerf::hash_encode_bwd_kernel<3, 512>"],
+    "nerf_tv_bwd_bin": ["nerf::tv_bwd_bin_kernel<512>"],
     "nerf_hash_encode_bwd_owner": ["nerf::hash_bwd_owner_kernel<13, 1024, false>"],
     "nerf_mlp_fwd": ["nerf::mlp_fwd_x6_kernel<false>"],
     "nerf_mlp_bwd": ["nerf::mlp_bwd_x6cg_kernel<false>"],

@@ -104,11 +104,16 @@ int nerf_hash_encode_bwd_ws(const float* d_xyz, int64_t n_points,
 
 /* The binned path split in two, so that several backwards into the same tables (the fine and the
  * coarse pass of one iteration: two autograd nodes of HashEmbedder.forward, hash_encoding.py:82-107)
- * share ONE owner pass. The workspace holds chunk_capacity 256-point chunks (workspace_bytes >=
- * nerf_hash_encode_bwd_workspace_bytes(n_levels, log2_T, 256 * chunk_capacity, deterministic)); a
- * bin call writes its ceil(n_points / 256) chunks from chunk_base on, and the owner call sums chunks
+ * share ONE owner pass. The workspace holds chunk_capacity chunks of C = nerf_hash_bwd_chunk_points()
+ * (= NERF_HASH_CHUNK_POINTS) points (workspace_bytes >= nerf_hash_encode_bwd_workspace_bytes(n_levels,
+ * log2_T, C * chunk_capacity, deterministic)); a bin call writes its ceil(n_points / C) chunks from
+ * chunk_base on, and the owner call sums chunks
  * [0, n_chunks) into d_dtables (ACCUMULATED). Calls sharing a workspace must be stream-ordered and
  * use the same n_levels, log2_T, chunk_capacity and deterministic. */
+#ifndef NERF_HASH_CHUNK_POINTS
+#define NERF_HASH_CHUNK_POINTS 512
+#endif
+int nerf_hash_bwd_chunk_points(void);
 int nerf_hash_encode_bwd_bin(const float* d_xyz, int64_t n_points,
                              const float* bbox_min3, const float* bbox_max3,
                              const float* level_res, int n_levels, int log2_T,
@@ -351,6 +356,16 @@ int nerf_tv_fwd(const float* const* d_tables, int n_levels, int log2_T, const in
 int nerf_tv_bwd(const float* const* d_tables, int n_levels, int log2_T, const int64_t* min_vertex,
                 const int64_t* d_min_vertex, const int* cube, const float* d_scale /* device [n_levels] */,
                 float* const* d_dtables, void* stream);
+/* Binned TV backward: the same gradient as nerf_tv_bwd, written as entries into a binned hash-backward
+ * workspace (chunks [chunk_base, chunk_base + nerf_tv_bwd_bin_chunks(n_levels, cube)), one entry per
+ * cuboid vertex) and summed into the tables by nerf_hash_encode_bwd_owner together with the hash
+ * backwards binned beside it: no float atomics, bit-reproducible under deterministic = 1. Workspace
+ * rules as nerf_hash_encode_bwd_bin. nerf_tv_bwd_bin_chunks returns 0 for invalid arguments. */
+int64_t nerf_tv_bwd_bin_chunks(int n_levels, const int* cube);
+int nerf_tv_bwd_bin(const float* const* d_tables, int n_levels, int log2_T, const int64_t* min_vertex,
+                    const int64_t* d_min_vertex, const int* cube, const float* d_scale /* device [n_levels] */,
+                    int64_t chunk_base, int64_t chunk_capacity, int deterministic, void* d_workspace,
+                    size_t workspace_bytes, void* stream);
 
 /* ---- training-loss head (run_nerf.py:1011-1037: img2mse of both passes, sparsity, TV, mse2psnr) ----
  * fwd: device scalars loss, img_loss (fine-pass MSE), psnr; rgb0 / sparsity / sparsity0 / tv may be NULL.

@@ -93,27 +93,43 @@ __device__ __forceinline__ float dpp_move(float v) {
 
 // Segmented inclusive wave64 sums of N values per lane, runs = lanes [start, lane] (start: first lane
 // of the lane's run). Intra-row Hillis-Steele (row_shr 1,2,4,8) then the row_bcast 15 / 31 carries
-// of the classic DPP scan, each applied only where the source lane lies in the same run.
-template <int N>
-__device__ __forceinline__ void wave_segmented_inclusive_sum(float (&v)[N], int lane, int start) {
-    const int r16 = lane & 15, row = lane >> 4;
-    const bool t1 = r16 >= 1 && lane - 1 >= start;
-    const bool t2 = r16 >= 2 && lane - 2 >= start;
-    const bool t4 = r16 >= 4 && lane - 4 >= start;
-    const bool t8 = r16 >= 8 && lane - 8 >= start;
+// of the classic DPP scan, each applied only where the source lane lies in the same run. STEPS: the
+// intra-row distances 1 .. 2^(STEPS-1) are applied (enough when every run is shorter than 2^STEPS
+// lanes); CROSS: the carries across rows.
+template <int N, int STEPS, bool CROSS>
+__device__ __forceinline__ void wave_segmented_scan_steps(float (&v)[N], int lane, int start) {
+    const int r16 = lane & 15, row = lane >> 4, span = lane - start;
+    const bool t1 = r16 >= 1 && span >= 1;
+    const bool t2 = r16 >= 2 && span >= 2;
+    const bool t4 = r16 >= 4 && span >= 4;
+    const bool t8 = r16 >= 8 && span >= 8;
     const bool tb15 = (row & 1) && start <= 16 * row - 1;
     const bool tb31 = row >= 2 && start <= 31;
 #pragma unroll
     for (int i = 0; i < N; ++i) {
         float x = v[i], t;
         t = dpp_move<0x111, 0xF>(x); if (t1) x += t;
-        t = dpp_move<0x112, 0xF>(x); if (t2) x += t;
-        t = dpp_move<0x114, 0xF>(x); if (t4) x += t;
-        t = dpp_move<0x118, 0xF>(x); if (t8) x += t;
-        t = dpp_move<0x142, 0xA>(x); if (tb15) x += t;
-        t = dpp_move<0x143, 0xC>(x); if (tb31) x += t;
+        if constexpr (STEPS >= 2) { t = dpp_move<0x112, 0xF>(x); if (t2) x += t; }
+        if constexpr (STEPS >= 3) { t = dpp_move<0x114, 0xF>(x); if (t4) x += t; }
+        if constexpr (STEPS >= 4) { t = dpp_move<0x118, 0xF>(x); if (t8) x += t; }
+        if constexpr (CROSS) {
+            t = dpp_move<0x142, 0xA>(x); if (tb15) x += t;
+            t = dpp_move<0x143, 0xC>(x); if (tb31) x += t;
+        }
         v[i] = x;
     }
+}
+
+// The full scan, or a shorter one chosen once per wave (ballots): runs of consecutive samples in
+// one voxel are mostly 2-4 lanes long and seldom cross a 16-lane row, so most waves need one or two
+// of the six steps.
+template <int N>
+__device__ __forceinline__ void wave_segmented_inclusive_sum(float (&v)[N], int lane, int start) {
+    const int span = lane - start;
+    const bool cross = __ballot(start < (lane & ~15)) != 0ull;   // a run continues across a row boundary
+    if (!cross && __ballot(span >= 2) == 0ull) wave_segmented_scan_steps<N, 1, false>(v, lane, start);
+    else if (!cross && __ballot(span >= 4) == 0ull) wave_segmented_scan_steps<N, 2, false>(v, lane, start);
+    else wave_segmented_scan_steps<N, 4, true>(v, lane, start);
 }
 
 // Wave64 reductions / scans through DPP-capable shuffles.

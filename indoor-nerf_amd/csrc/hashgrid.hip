@@ -13,6 +13,8 @@
 // that the current point range touches (tables are 4 MiB per level at log2_T = 19).
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include "hash_common.h"
 
 namespace nerf {
@@ -29,7 +31,7 @@ struct HashGradParams {
     float2* bin_g;        // entry (d feat0, d feat1)
     uint32_t* bin_seg;    // [L][n_owner][nchunks]: segment start | count << 16 within the chunk region
     int nchunks;          // chunks the owner pass walks
-    int chunk_base;       // bin pass: chunk index of this launch's first 256 points
+    int chunk_base;       // bin pass: chunk index of this launch's first kChunkPts points
     int chunk_stride;     // chunk capacity of the workspace (the layout stride)
     int slice_log2;       // owner slice = 2^slice_log2 rows (LDS: 16 B per row, 32 B deterministic)
     int owner_log2;       // owners per level = 2^owner_log2
@@ -112,15 +114,97 @@ constexpr uint32_t kSkip = 0xFFFFFFFFu;
 // at the coarse levels, where every ray crosses the same few thousand voxels). The binned path
 // replaces the memory-side atomics: this kernel writes each (row, d feat) entry into a per-chunk
 // region sorted by owner slice (plain stores), and hash_bwd_owner_kernel sums each slice in LDS.
-constexpr int kChunkCap = 256 * 8;        // entries per 256-point chunk (8 corners per point)
+constexpr int kChunkPts = NERF_HASH_CHUNK_POINTS;   // points per chunk = threads per bin block
+constexpr int kChunkCap = kChunkPts * 8;            // entries per chunk (8 corners per point)
+constexpr int kChunkCapLog2 = kChunkPts == 256 ? 11 : kChunkPts == 512 ? 12 : 13;
+static_assert(kChunkPts == 256 || kChunkPts == 512 || kChunkPts == 1024, "chunk of 256, 512 or 1024 points");
 constexpr int kSliceLog2 = 13;            // owner slice: 2^13 rows x 16 B (fp64 pair) = 128 KiB of LDS
 constexpr int kSliceLog2Det = 12;         // deterministic: 2^12 rows x 32 B (two int64 words per feature)
 constexpr int kMaxOwnersLog2 = 7;
 constexpr int kMaxOwners = 1 << kMaxOwnersLog2;
 
+// Bin one chunk: count the block's entries per owner slice (LDS atomics), scan, place every entry
+// at its slot of an LDS image of the chunk's region, then write the image out with 16-B coalesced
+// stores (scattered per-lane stores were TA-bound: 64 lines per instruction). Every (level, chunk)
+// in [0, n_chunks) gets its n_owner segment words, empty ones included. NE entries per thread
+// (8 corners of a point; 1 TV vertex), at most kChunkCap per chunk.
+template <int THREADS, int NE>
+__device__ __forceinline__ void bin_chunk(const HashGradParams& hp, int lvl, int chunk, const uint32_t (&hh)[NE],
+                                          const float (&vx)[NE], const float (&vy)[NE], const bool (&on)[NE]) {
+    constexpr int CAP = THREADS * NE;
+    static_assert(CAP <= kChunkCap, "chunk region");
+    __shared__ uint32_t s_cnt[kMaxOwners];
+    __shared__ uint32_t s_start[kMaxOwners + 1];
+    __shared__ __attribute__((aligned(16))) uint16_t s_eh[CAP];
+    __shared__ __attribute__((aligned(16))) float2 s_eg[CAP];
+    const int lane = threadIdx.x & 63;
+    const int n_own = 1 << hp.owner_log2;
+    if (threadIdx.x < n_own) s_cnt[threadIdx.x] = 0;
+    __syncthreads();
+    uint32_t pos[NE];
+#pragma unroll
+    for (int c = 0; c < NE; ++c) pos[c] = on[c] ? atomicAdd(&s_cnt[hh[c] >> hp.slice_log2], 1u) : kSkip;
+    __syncthreads();
+    if (threadIdx.x < 64) {   // exclusive scan of <= 128 counters in wave 0, two per lane
+        const int o0 = 2 * lane, o1 = 2 * lane + 1;
+        const uint32_t v0 = o0 < n_own ? s_cnt[o0] : 0u, v1 = o1 < n_own ? s_cnt[o1] : 0u;
+        uint32_t inc = v0 + v1;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t t = __shfl_up(inc, o, 64);
+            if (lane >= o) inc += t;
+        }
+        const uint32_t ex0 = inc - v0 - v1, ex1 = ex0 + v0;
+        if (o0 < n_own) {
+            s_start[o0] = ex0;
+            hp.bin_seg[((size_t)lvl * n_own + o0) * hp.chunk_stride + chunk] = ex0 | (v0 << 16);
+        }
+        if (o1 < n_own) {
+            s_start[o1] = ex1;
+            hp.bin_seg[((size_t)lvl * n_own + o1) * hp.chunk_stride + chunk] = ex1 | (v1 << 16);
+        }
+        if (o0 == n_own - 1) s_start[n_own] = ex1;
+        if (o1 == n_own - 1) s_start[n_own] = ex1 + v1;
+    }
+    __syncthreads();
+    const uint32_t smask = (1u << hp.slice_log2) - 1u;
+#pragma unroll
+    for (int c = 0; c < NE; ++c) {
+        if (pos[c] != kSkip) {
+            const uint32_t k = s_start[hh[c] >> hp.slice_log2] + pos[c];
+            s_eh[k] = (uint16_t)(hh[c] & smask);
+            s_eg[k] = make_float2(vx[c], vy[c]);
+        }
+    }
+    if (hp.chunk_max) {   // deterministic mode: the level's largest |entry| sets the owners' fixed-point scale
+        float m = 0.f;
+#pragma unroll
+        for (int c = 0; c < NE; ++c)
+            if (pos[c] != kSkip) m = fmaxf(m, fmaxf(fabsf(vx[c]), fabsf(vy[c])));
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+        __shared__ float s_wmax[THREADS / 64];
+        if (lane == 0) s_wmax[threadIdx.x >> 6] = m;
+        __syncthreads();
+        if (threadIdx.x == 0) {   // one plain store per chunk (per-level atomics serialise the blocks)
+            for (int w = 1; w < THREADS / 64; ++w) m = fmaxf(m, s_wmax[w]);
+            hp.chunk_max[(size_t)lvl * hp.chunk_stride + chunk] = m;
+        }
+    }
+    __syncthreads();
+    const uint32_t total = s_start[n_own];
+    const size_t base = ((size_t)lvl * hp.chunk_stride + chunk) * kChunkCap;
+    // two entries per lane: rows as one dword, (d feat) x 2 as one dwordx4; a trailing odd
+    // slot carries stale LDS bytes that no owner reads (owners read < count per segment)
+    for (uint32_t i = 2 * threadIdx.x; i < total; i += 2 * THREADS) {
+        *reinterpret_cast<uint32_t*>(hp.bin_h + base + i) = *reinterpret_cast<const uint32_t*>(&s_eh[i]);
+        *reinterpret_cast<float4*>(hp.bin_g + base + i) = *reinterpret_cast<const float4*>(&s_eg[i]);
+    }
+}
+
 // MODE 1: coalesced float atomics (no workspace); 3: binned (default).
-template <int MODE>
-__global__ void __launch_bounds__(256) hash_encode_bwd_kernel(
+template <int MODE, int THREADS>
+__global__ void __launch_bounds__(THREADS) hash_encode_bwd_kernel(
     const float* __restrict__ xyz, int64_t n, HashGradParams hp,
     const float* __restrict__ dfeat, int64_t sp, int64_t sl) {
     const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -166,85 +250,25 @@ __global__ void __launch_bounds__(256) hash_encode_bwd_kernel(
     if (heads != ~0ull) {  // some run has length > 1 in this wave
         const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
         const int start = 63 - __clzll(heads & upto);
-        wave_segmented_inclusive_sum(cgx, lane, start);
-        wave_segmented_inclusive_sum(cgy, lane, start);
+        float cg[16];   // one scan over both features: the step choice is made once
+#pragma unroll
+        for (int c = 0; c < 8; ++c) { cg[c] = cgx[c]; cg[8 + c] = cgy[c]; }
+        wave_segmented_inclusive_sum(cg, lane, start);
+#pragma unroll
+        for (int c = 0; c < 8; ++c) { cgx[c] = cg[c]; cgy[c] = cg[8 + c]; }
     }
     const bool emit = valid && tail;
     float* tab = hp.dtables[lvl];
     const uint32_t bx = (uint32_t)ax.base, by = (uint32_t)ay.base, bz = (uint32_t)az.base;
     if constexpr (MODE == 3) {
-        // Bin: count this chunk's entries per owner slice (LDS atomics), scan, place every entry at
-        // its slot of an LDS image of the chunk's region, then write the image out with 16-B
-        // coalesced stores (scattered per-lane stores were TA-bound: 64 lines per instruction).
-        __shared__ uint32_t s_cnt[kMaxOwners];
-        __shared__ uint32_t s_start[kMaxOwners + 1];
-        __shared__ __attribute__((aligned(16))) uint16_t s_eh[kChunkCap];
-        __shared__ __attribute__((aligned(16))) float2 s_eg[kChunkCap];
-        const int n_own = 1 << hp.owner_log2;
-        if (threadIdx.x < n_own) s_cnt[threadIdx.x] = 0;
-        __syncthreads();
-        uint32_t hh[8], pos[8];
+        uint32_t hh[8];
+        bool on[8];
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
             hh[c] = spatial_hash3(bx + ((c >> 2) & 1), by + ((c >> 1) & 1), bz + (c & 1), hp.mask);
-            pos[c] = (emit && (cgx[c] != 0.f || cgy[c] != 0.f)) ? atomicAdd(&s_cnt[hh[c] >> hp.slice_log2], 1u)
-                                                                : kSkip;
+            on[c] = emit && (cgx[c] != 0.f || cgy[c] != 0.f);
         }
-        __syncthreads();
-        if (threadIdx.x < 64) {   // exclusive scan of <= 128 counters in wave 0, two per lane
-            const int o0 = 2 * lane, o1 = 2 * lane + 1;
-            const uint32_t v0 = o0 < n_own ? s_cnt[o0] : 0u, v1 = o1 < n_own ? s_cnt[o1] : 0u;
-            uint32_t inc = v0 + v1;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t t = __shfl_up(inc, o, 64);
-                if (lane >= o) inc += t;
-            }
-            const uint32_t ex0 = inc - v0 - v1, ex1 = ex0 + v0;
-            if (o0 < n_own) {
-                s_start[o0] = ex0;
-                hp.bin_seg[((size_t)lvl * n_own + o0) * hp.chunk_stride + hp.chunk_base + blockIdx.x] = ex0 | (v0 << 16);
-            }
-            if (o1 < n_own) {
-                s_start[o1] = ex1;
-                hp.bin_seg[((size_t)lvl * n_own + o1) * hp.chunk_stride + hp.chunk_base + blockIdx.x] = ex1 | (v1 << 16);
-            }
-            if (o0 == n_own - 1) s_start[n_own] = ex1;
-            if (o1 == n_own - 1) s_start[n_own] = ex1 + v1;
-        }
-        __syncthreads();
-        const uint32_t smask = (1u << hp.slice_log2) - 1u;
-#pragma unroll
-        for (int c = 0; c < 8; ++c) {
-            if (pos[c] != kSkip) {
-                const uint32_t k = s_start[hh[c] >> hp.slice_log2] + pos[c];
-                s_eh[k] = (uint16_t)(hh[c] & smask);
-                s_eg[k] = make_float2(cgx[c], cgy[c]);
-            }
-        }
-        if (hp.chunk_max) {   // deterministic mode: the level's largest |entry| sets the owners' fixed-point scale
-            float m = 0.f;
-#pragma unroll
-            for (int c = 0; c < 8; ++c)
-                if (pos[c] != kSkip) m = fmaxf(m, fmaxf(fabsf(cgx[c]), fabsf(cgy[c])));
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
-            __shared__ float s_wmax[4];
-            if (lane == 0) s_wmax[threadIdx.x >> 6] = m;
-            __syncthreads();
-            if (threadIdx.x == 0)   // one plain store per chunk (per-level atomics serialise 4096 blocks)
-                hp.chunk_max[(size_t)lvl * hp.chunk_stride + hp.chunk_base + blockIdx.x] =
-                    fmaxf(fmaxf(s_wmax[0], s_wmax[1]), fmaxf(s_wmax[2], s_wmax[3]));
-        }
-        __syncthreads();
-        const uint32_t total = s_start[n_own];
-        const size_t base = ((size_t)lvl * hp.chunk_stride + hp.chunk_base + blockIdx.x) * kChunkCap;
-        // two entries per lane: rows as one dword, (d feat) x 2 as one dwordx4; a trailing odd
-        // slot carries stale LDS bytes that no owner reads (owners read < count per segment)
-        for (uint32_t i = 2 * threadIdx.x; i < total; i += 2 * 256) {
-            *reinterpret_cast<uint32_t*>(hp.bin_h + base + i) = *reinterpret_cast<const uint32_t*>(&s_eh[i]);
-            *reinterpret_cast<float4*>(hp.bin_g + base + i) = *reinterpret_cast<const float4*>(&s_eg[i]);
-        }
+        bin_chunk<THREADS, 8>(hp, lvl, hp.chunk_base + (int)blockIdx.x, hh, cgx, cgy, on);
     } else {
         __shared__ float s_val[4][64][17];
         __shared__ uint32_t s_h[4][64][9];
@@ -269,6 +293,49 @@ __global__ void __launch_bounds__(256) hash_encode_bwd_kernel(
             if (h != kSkip && v != 0.f) atomic_add_f32(tab + 2 * h + f, v);
         }
     }
+}
+
+// TV backward (loss.py:11-43 autograd) into the binned workspace, summed by the same owner pass as
+// the hash backward: no memory-side float atomics, and deterministic with it. Chunk k of level l
+// holds vertices [k C, (k + 1) C) of the level's (cube + 1)^3 cuboid (C = kChunkPts; chunks past a
+// level's last vertex are empty), one entry per vertex: row hash(min_vertex + (i, j, k)), value
+// (sum over the in-cuboid neighbours n of 2 (e_v - e_n)) x scale[l] / cube — the per-vertex terms
+// and op order of the atomic tv_bwd_kernel (optim.hip).
+template <int THREADS>
+__global__ void __launch_bounds__(THREADS) tv_bwd_bin_kernel(TVParams P, HashGradParams hp) {
+    const int l = blockIdx.y;
+    const int c = P.cube[l], n1 = c + 1;
+    const uint32_t nv = (uint32_t)(P.vstart[l + 1] - P.vstart[l]);
+    const float2* tab = reinterpret_cast<const float2*>(P.tables[l]);
+    int mv[3];
+    tv_corner(P, l, mv);
+    const uint32_t lv = blockIdx.x * (uint32_t)THREADS + threadIdx.x;
+    const bool ok = lv < nv;
+    int i = 0, j = 0, k = 0;
+    float gx = 0.f, gy = 0.f;
+    uint32_t h = 0;
+    if (ok) {
+        tv_vertex(lv, n1, i, j, k);
+        const float2 e = tv_fetch(tab, mv, i, j, k, P.mask);
+        auto pair = [&](bool cond, int di, int dj, int dk) {
+            if (!cond) return;
+            const float2 f = tv_fetch(tab, mv, i + di, j + dj, k + dk, P.mask);
+            gx += 2.0f * (e.x - f.x);
+            gy += 2.0f * (e.y - f.y);
+        };
+        pair(i > 0, -1, 0, 0);
+        pair(i < c, 1, 0, 0);
+        pair(j > 0, 0, -1, 0);
+        pair(j < c, 0, 1, 0);
+        pair(k > 0, 0, 0, -1);
+        pair(k < c, 0, 0, 1);
+        h = spatial_hash3((uint32_t)(mv[0] + i), (uint32_t)(mv[1] + j), (uint32_t)(mv[2] + k), P.mask);
+    }
+    const float s = P.scale[l] / (float)c;
+    const uint32_t hh[1] = {h};
+    const float vx[1] = {gx * s}, vy[1] = {gy * s};
+    const bool on[1] = {ok && (vx[0] != 0.f || vy[0] != 0.f)};
+    bin_chunk<THREADS, 1>(hp, l, hp.chunk_base + (int)blockIdx.x, hh, vx, vy, on);
 }
 
 // ---- owner pass of the binned backward ----------------------------------------------------
@@ -319,7 +386,7 @@ __global__ void __launch_bounds__(THREADS) hash_bwd_owner_kernel(HashGradParams 
         __syncthreads();   // s_wsum is reused by the window scans
         int E;
         (void)frexpf(m, &E);                                                // max |entry| < 2^E
-        const int b = 11 + (32 - __clz((unsigned)max(hp.nchunks - 1, 1)));  // entries <= 2^b
+        const int b = kChunkCapLog2 + (32 - __clz((unsigned)max(hp.nchunks - 1, 1)));  // entries <= 2^b
         sh = 62 - E - b;
         sl_ = sh + (61 - b);
     }
@@ -507,7 +574,7 @@ static bool make_bin_plan(int n_levels, int log2_T, int64_t n_points, BinPlan& B
     if (log2_T < 1 || log2_T > slice + kMaxOwnersLog2 || n_points < 0) return false;
     B.slice_log2 = log2_T < slice ? log2_T : slice;
     B.owner_log2 = log2_T - B.slice_log2;
-    B.nchunks = (int)((n_points + 255) / 256);
+    B.nchunks = (int)((n_points + kChunkPts - 1) / kChunkPts);
     const size_t entries = (size_t)n_levels * B.nchunks * kChunkCap;
     const size_t offs = (size_t)n_levels * B.nchunks * (1 << B.owner_log2);
     auto up = [](size_t v) { return (v + 255) & ~(size_t)255; };
@@ -572,10 +639,10 @@ static int bin_layout(const char* who, int n_levels, int log2_T, int64_t chunk_c
     NERF_REQUIRE(chunk_capacity >= 1 && chunk_capacity <= (int64_t)1 << 26, "%s: chunk_capacity %lld", who,
                  (long long)chunk_capacity);
     BinPlan B{};
-    NERF_REQUIRE(make_bin_plan(n_levels, log2_T, chunk_capacity * 256, B, det != 0),
+    NERF_REQUIRE(make_bin_plan(n_levels, log2_T, chunk_capacity * kChunkPts, B, det != 0),
                  "%s: no binned path for log2_T %d%s", who, log2_T, det ? " (deterministic)" : "");
     NERF_REQUIRE(d_workspace != nullptr && workspace_bytes >= B.total,
-                 "%s: workspace %zu B < %zu B (nerf_hash_encode_bwd_workspace_bytes(L, log2_T, 256 * capacity, det))",
+                 "%s: workspace %zu B < %zu B (nerf_hash_encode_bwd_workspace_bytes(L, log2_T, NERF_HASH_CHUNK_POINTS * capacity, det))",
                  who, workspace_bytes, B.total);
     char* ws = static_cast<char*>(d_workspace);
     hp.bin_g = reinterpret_cast<float2*>(ws + B.off_g);
@@ -588,6 +655,8 @@ static int bin_layout(const char* who, int n_levels, int log2_T, int64_t chunk_c
     hp.mask = (uint32_t)((1u << log2_T) - 1u);
     return NERF_OK;
 }
+
+extern "C" int nerf_hash_bwd_chunk_points(void) { return kChunkPts; }
 
 extern "C" size_t nerf_hash_encode_bwd_workspace_bytes(int n_levels, int log2_T, int64_t n_points, int deterministic) {
     BinPlan B{};
@@ -607,7 +676,7 @@ extern "C" int nerf_hash_encode_bwd_bin(const float* d_xyz, int64_t n_points, co
     const int rc = bin_layout("hash_encode_bwd_bin", n_levels, log2_T, chunk_capacity, deterministic, d_workspace,
                               workspace_bytes, hp);
     if (rc) return rc;
-    const int64_t nch = (n_points + 255) / 256;
+    const int64_t nch = (n_points + kChunkPts - 1) / kChunkPts;
     NERF_REQUIRE(chunk_base >= 0 && chunk_base + nch <= chunk_capacity,
                  "hash_encode_bwd_bin: chunks [%lld, %lld) exceed the capacity %lld", (long long)chunk_base,
                  (long long)(chunk_base + nch), (long long)chunk_capacity);
@@ -616,9 +685,52 @@ extern "C" int nerf_hash_encode_bwd_bin(const float* d_xyz, int64_t n_points, co
     fill_cells(hp.cell, bbox_min3, bbox_max3, level_res, n_levels);
     hp.chunk_base = (int)chunk_base;
     hp.nchunks = (int)(chunk_base + nch);
-    hipLaunchKernelGGL(hash_encode_bwd_kernel<3>, dim3((unsigned)nch, n_levels), dim3(256), 0, as_stream(stream),
+    hipLaunchKernelGGL((hash_encode_bwd_kernel<3, kChunkPts>), dim3((unsigned)nch, n_levels), dim3(kChunkPts), 0, as_stream(stream),
                        d_xyz, n_points, hp, d_dfeat, feat_stride_point, feat_stride_level);
     NERF_CHECK_LAUNCH("hash_encode_bwd_bin");
+    return NERF_OK;
+}
+
+static int64_t tv_bin_chunks(int n_levels, const int* cube) {
+    int64_t most = 0;
+    for (int l = 0; l < n_levels; ++l) {
+        const int64_t n1 = (int64_t)cube[l] + 1;
+        most = std::max<int64_t>(most, (n1 * n1 * n1 + kChunkPts - 1) / kChunkPts);
+    }
+    return most;
+}
+
+extern "C" int64_t nerf_tv_bwd_bin_chunks(int n_levels, const int* cube) {
+    if (n_levels < 1 || n_levels > NERF_MAX_LEVELS || !cube) return 0;
+    for (int l = 0; l < n_levels; ++l)
+        if (cube[l] < 1 || cube[l] > 1024) return 0;
+    return tv_bin_chunks(n_levels, cube);
+}
+
+extern "C" int nerf_tv_bwd_bin(const float* const* d_tables, int n_levels, int log2_T, const int64_t* min_vertex,
+                               const int64_t* d_min_vertex, const int* cube, const float* d_scale, int64_t chunk_base,
+                               int64_t chunk_capacity, int deterministic, void* d_workspace, size_t workspace_bytes,
+                               void* stream) {
+    TVParams P{};
+    int rc = fill_tv(P, n_levels, log2_T, min_vertex, d_min_vertex, cube);
+    if (rc) return rc;
+    NERF_REQUIRE(d_tables && d_scale, "tv_bwd_bin: null arg");
+    for (int l = 0; l < n_levels; ++l) {
+        NERF_REQUIRE(d_tables[l], "tv_bwd_bin: table %d null", l);
+        P.tables[l] = d_tables[l];
+    }
+    P.scale = d_scale;
+    HashGradParams hp{};
+    rc = bin_layout("tv_bwd_bin", n_levels, log2_T, chunk_capacity, deterministic, d_workspace, workspace_bytes, hp);
+    if (rc) return rc;
+    const int64_t nch = tv_bin_chunks(n_levels, cube);
+    NERF_REQUIRE(chunk_base >= 0 && chunk_base + nch <= chunk_capacity,
+                 "tv_bwd_bin: chunks [%lld, %lld) exceed the capacity %lld", (long long)chunk_base,
+                 (long long)(chunk_base + nch), (long long)chunk_capacity);
+    hp.chunk_base = (int)chunk_base;
+    hipLaunchKernelGGL((tv_bwd_bin_kernel<kChunkPts>), dim3((unsigned)nch, n_levels), dim3(kChunkPts), 0,
+                       as_stream(stream), P, hp);
+    NERF_CHECK_LAUNCH("tv_bwd_bin");
     return NERF_OK;
 }
 
@@ -667,7 +779,7 @@ extern "C" int nerf_hash_encode_bwd(const float* d_xyz, int64_t n_points, const 
     for (int a = 0; a < 3; ++a) { hp.bmin[a] = bbox_min3[a]; hp.bmax[a] = bbox_max3[a]; }
     fill_cells(hp.cell, bbox_min3, bbox_max3, level_res, n_levels);
     hp.mask = (uint32_t)((1u << log2_T) - 1u);
-    hipLaunchKernelGGL(hash_encode_bwd_kernel<1>, dim3(blocks_for(n_points, 256), n_levels), dim3(256), 0,
+    hipLaunchKernelGGL((hash_encode_bwd_kernel<1, 256>), dim3(blocks_for(n_points, 256), n_levels), dim3(256), 0,
                        as_stream(stream), d_xyz, n_points, hp, d_dfeat, feat_stride_point, feat_stride_level);
     NERF_CHECK_LAUNCH("hash_encode_bwd");
     return NERF_OK;
@@ -691,7 +803,7 @@ extern "C" int nerf_hash_encode_bwd_ws(const float* d_xyz, int64_t n_points, con
                                     feat_stride_point, feat_stride_level, d_dtables, stream);
     }
     if (n_points == 0) return NERF_OK;
-    const int64_t nch = (n_points + 255) / 256;
+    const int64_t nch = (n_points + kChunkPts - 1) / kChunkPts;
     int rc = nerf_hash_encode_bwd_bin(d_xyz, n_points, bbox_min3, bbox_max3, level_res, n_levels, log2_T, d_dfeat,
                                       feat_stride_point, feat_stride_level, 0, nch, deterministic, d_workspace,
                                       workspace_bytes, stream);

@@ -1,6 +1,6 @@
 // Fused RAdam step (PocketNeRF/radam.py:28-94) over a list of tensor segments in ONE launch, and
 // the total-variation loss on one hashed cuboid per level (PocketNeRF/loss.py:11-43).
-#include "common.h"
+#include "hash_common.h"
 
 namespace nerf {
 
@@ -67,34 +67,10 @@ __global__ void __launch_bounds__(kRAdamThreads) radam_kernel(RAdamSegs S) {
 }
 
 // ---------------------------------------------------------------- TV loss
-struct TVParams {
-    const float* tables[NERF_MAX_LEVELS];
-    float* dtables[NERF_MAX_LEVELS];
-    int mv[NERF_MAX_LEVELS][3];
-    int cube[NERF_MAX_LEVELS];
-    int64_t vstart[NERF_MAX_LEVELS + 1];   // first vertex of each level in the flattened launch
-    int L;
-    uint32_t mask;
-    const int64_t* dmv;   // optional device [L][3] cuboid corners (graph replays draw new ones)
-    const float* scale;   // bwd: device [L] upstream gradient per level
-    float* loss;          // fwd: device [L]
-};
-
-__device__ __forceinline__ float2 tv_fetch(const float2* tab, const int* mv, int i, int j, int k, uint32_t mask) {
-    return tab[spatial_hash3((uint32_t)(mv[0] + i), (uint32_t)(mv[1] + j), (uint32_t)(mv[2] + k), mask)];
-}
-
 // Grid (kTVBlocks, L): block (b, l) strides over level l's (cube+1)^3 vertices, so a level's partial
 // sums meet in one LDS reduction per block and one atomic per block (not one per wave on 16 addresses).
 constexpr int kTVBlocks = 96;
 constexpr uint32_t kTVSkip = 0xFFFFFFFFu;
-
-__device__ __forceinline__ void tv_vertex(uint32_t lv, int n1, int& i, int& j, int& k) {
-    const uint32_t q = lv / (uint32_t)n1;      // < 1025^3: 32-bit index math
-    k = (int)(lv - q * (uint32_t)n1);
-    j = (int)(q % (uint32_t)n1);
-    i = (int)(q / (uint32_t)n1);
-}
 
 // cube vertex (i,j,k) = min_vertex + (i,j,k) in meshgrid 'ij' order (loss.py:25-27)
 __global__ void __launch_bounds__(256) tv_fwd_kernel(TVParams P) {
@@ -103,11 +79,7 @@ __global__ void __launch_bounds__(256) tv_fwd_kernel(TVParams P) {
     const uint32_t nv = (uint32_t)(P.vstart[l + 1] - P.vstart[l]);
     const float2* tab = reinterpret_cast<const float2*>(P.tables[l]);
     int mvd[3];
-    if (P.dmv) {
-        mvd[0] = (int)P.dmv[3 * l]; mvd[1] = (int)P.dmv[3 * l + 1]; mvd[2] = (int)P.dmv[3 * l + 2];
-    } else {
-        mvd[0] = P.mv[l][0]; mvd[1] = P.mv[l][1]; mvd[2] = P.mv[l][2];
-    }
+    tv_corner(P, l, mvd);
     const int* mv = mvd;
     float part = 0.f;
     for (uint32_t lv = blockIdx.x * 256u + threadIdx.x; lv < nv; lv += gridDim.x * 256u) {
@@ -136,11 +108,7 @@ __global__ void __launch_bounds__(256) tv_bwd_kernel(TVParams P) {
     const uint32_t nv = (uint32_t)(P.vstart[l + 1] - P.vstart[l]);
     const float2* tab = reinterpret_cast<const float2*>(P.tables[l]);
     int mvd[3];
-    if (P.dmv) {
-        mvd[0] = (int)P.dmv[3 * l]; mvd[1] = (int)P.dmv[3 * l + 1]; mvd[2] = (int)P.dmv[3 * l + 2];
-    } else {
-        mvd[0] = P.mv[l][0]; mvd[1] = P.mv[l][1]; mvd[2] = P.mv[l][2];
-    }
+    tv_corner(P, l, mvd);
     const int* mv = mvd;
     float* dt = P.dtables[l];
     const float s = P.scale[l] / (float)c;
@@ -181,24 +149,6 @@ __global__ void __launch_bounds__(256) tv_bwd_kernel(TVParams P) {
     }
 }
 
-static int fill_tv(TVParams& P, int n_levels, int log2_T, const int64_t* min_vertex, const int64_t* d_min_vertex,
-                   const int* cube) {
-    NERF_REQUIRE(n_levels >= 1 && n_levels <= NERF_MAX_LEVELS, "tv: n_levels %d", n_levels);
-    NERF_REQUIRE(log2_T >= 1 && log2_T <= 30, "tv: log2_T %d", log2_T);
-    NERF_REQUIRE((min_vertex || d_min_vertex) && cube, "tv: null arg");
-    P.dmv = d_min_vertex;
-    P.L = n_levels;
-    P.mask = (uint32_t)((1u << log2_T) - 1u);
-    P.vstart[0] = 0;
-    for (int l = 0; l < n_levels; ++l) {
-        NERF_REQUIRE(cube[l] >= 1 && cube[l] <= 1024, "tv: cube[%d] = %d", l, cube[l]);
-        for (int a = 0; a < 3; ++a) P.mv[l][a] = min_vertex ? (int)min_vertex[3 * l + a] : 0;
-        P.cube[l] = cube[l];
-        const int64_t n1 = cube[l] + 1;
-        P.vstart[l + 1] = P.vstart[l] + n1 * n1 * n1;
-    }
-    return NERF_OK;
-}
 
 }  // namespace nerf
 

@@ -11,7 +11,7 @@ import torch
 import torch.nn as nn
 
 from . import _lib
-from .hashgrid import HashEmbedder, SHEncoder, accumulate_grad_buffers, hash_encode_bwd, pending_bins
+from .hashgrid import HashEmbedder, SHEncoder, accumulate_grad_buffers, bin_chunks, hash_encode_bwd, pending_bins
 from .quantization import LearnedBitwidthQuantizer, calibrate_from_stats, new_stats, quant_records
 
 
@@ -275,22 +275,29 @@ def _det_workspace(device):
 
 
 def _run_field_jobs(jobs):
-    """MLP backwards of up to two nets per launch (nerf_mlp_bwd_batch), then their hash backwards
-    binned side by side and summed by one owner pass."""
-    ws = _det_workspace(jobs[0].pts.device)
-    for k in range(0, len(jobs), _lib.MLP_MAX_JOBS):
-        part = jobs[k:k + _lib.MLP_MAX_JOBS]
-        arr = (_lib.MlpBwdJob * len(part))(*[j.mlp_job() for j in part])
-        _lib.call("nerf_mlp_bwd_batch", arr, len(part), _lib.ptr(ws, "det_workspace", allow_none=True),
-                  0 if ws is None else ws.numel() * 4, _lib.stream())
+    """MLP backwards of up to two nets per launch (nerf_mlp_bwd_batch), then the hash backwards (and
+    the pass's TV backwards, losses.TVBinJob) binned side by side and summed by one owner pass."""
+    tv_jobs = [j for j in jobs if not isinstance(j, _FieldJob)]
+    jobs = [j for j in jobs if isinstance(j, _FieldJob)]
+    if jobs:
+        ws = _det_workspace(jobs[0].pts.device)
+        for k in range(0, len(jobs), _lib.MLP_MAX_JOBS):
+            part = jobs[k:k + _lib.MLP_MAX_JOBS]
+            arr = (_lib.MlpBwdJob * len(part))(*[j.mlp_job() for j in part])
+            _lib.call("nerf_mlp_bwd_batch", arr, len(part), _lib.ptr(ws, "det_workspace", allow_none=True),
+                      0 if ws is None else ws.numel() * 4, _lib.stream())
     tab_jobs = [j for j in jobs if j.need_tab]
-    if tab_jobs:
-        pending_bins(tab_jobs[0].pts.device).reserve(sum((j.pts.shape[0] + 255) // 256 for j in tab_jobs))
-    for j in tab_jobs:
-        P = j.pts.shape[0]
-        hash_encode_bwd(j.pts, j.meta, j.dfeat, 2, 2 * P, accumulate_grad_buffers(j.tables), defer=True, queue=False)
-    if tab_jobs:
-        pending_bins(tab_jobs[0].pts.device).flush()
+    if tab_jobs or tv_jobs:
+        dev = (tab_jobs[0].pts if tab_jobs else tv_jobs[0].g).device
+        pb = pending_bins(dev)
+        pb.reserve(sum(bin_chunks(j.pts.shape[0]) for j in tab_jobs) + sum(j.n_chunks for j in tv_jobs))
+        for j in tv_jobs:
+            pb.add_tv(j, queue=False)
+        for j in tab_jobs:
+            P = j.pts.shape[0]
+            hash_encode_bwd(j.pts, j.meta, j.dfeat, 2, 2 * P, accumulate_grad_buffers(j.tables), defer=True,
+                            queue=False)
+        pb.flush()
     for j in jobs:
         j.dfeat = None
 

@@ -145,31 +145,53 @@ class _PendingBins:
         workspace history: the deterministic mode's results are reproducible from the first call)."""
         self.peak = max(self.peak, n_chunks)
 
-    def add(self, xyz, meta, dfeat, sp, sl, grad_tables, queue=True):
-        L, log2_T, P = len(grad_tables), meta["log2_T"], xyz.shape[0]
-        n_ch = (P + 255) // 256
+    def _slot(self, L, log2_T, grad_tables, n_ch, device, queue):
+        """Chunks [base, base + n_ch) of the open workspace for a bin launch into grad_tables: opens
+        a workspace (flushing the previous one if it is for other tables or too small)."""
+        lib = _lib.load()
         det = int(_DET["on"])
         tag = (L, log2_T, tuple(g.data_ptr() for g in grad_tables), det)
         total = (self.used if self.tag == tag else 0) + n_ch
         self.peak = max(self.peak, total)     # the next pass sizes its workspace for this
         if self.used and (self.tag != tag or total > self.cap):
             self.flush()
-        lib = _lib.load()
         if self.used == 0:
             cap = max(self.peak, n_ch)
-            need = int(lib.nerf_hash_encode_bwd_workspace_bytes(L, log2_T, 256 * cap, det))
+            C = int(lib.nerf_hash_bwd_chunk_points())
+            need = int(lib.nerf_hash_encode_bwd_workspace_bytes(L, log2_T, C * cap, det))
             if self.ws is None or self.ws.numel() < need:
                 if self.ws is not None:
                     _RETIRED.append(self.ws)     # a captured graph may still bin into it
-                self.ws = torch.empty(need, dtype=torch.uint8, device=xyz.device)
+                self.ws = torch.empty(need, dtype=torch.uint8, device=device)
             self.cap = cap
             self.tag, self.grads, self.stream = tag, list(grad_tables), torch.cuda.current_stream()
             if queue:
                 torch.autograd.Variable._execution_engine.queue_callback(self.flush)
-        _lib.call("nerf_hash_encode_bwd_bin", _lib.ptr(xyz, "xyz"), P, meta["bmin"], meta["bmax"], meta["res"], L,
-                  log2_T, _lib.ptr(dfeat, "grad_feat"), sp, sl, self.used, self.cap, det,
-                  _lib.ptr(self.ws, "workspace", dtype=torch.uint8), self.ws.numel(), _lib.stream())
+        base = self.used
         self.used += n_ch
+        return base, det
+
+    def add(self, xyz, meta, dfeat, sp, sl, grad_tables, queue=True):
+        L, log2_T, P = len(grad_tables), meta["log2_T"], xyz.shape[0]
+        base, det = self._slot(L, log2_T, grad_tables, bin_chunks(P), xyz.device, queue)
+        _lib.call("nerf_hash_encode_bwd_bin", _lib.ptr(xyz, "xyz"), P, meta["bmin"], meta["bmax"], meta["res"], L,
+                  log2_T, _lib.ptr(dfeat, "grad_feat"), sp, sl, base, self.cap, det,
+                  _lib.ptr(self.ws, "workspace", dtype=torch.uint8), self.ws.numel(), _lib.stream())
+
+    def add_tv(self, job, queue=True):
+        """Bin a TV backward (losses.TVBinJob) into the open workspace: its gradient is summed by the
+        same owner pass as the hash backwards of the iteration."""
+        L = len(job.tables)
+        base, det = self._slot(L, job.log2_T, job.grads, job.n_chunks, job.tables[0].device, queue)
+        _lib.call("nerf_tv_bwd_bin", _lib.ptr_array(job.tables), L, job.log2_T, job.mv, job.dmv, job.cb,
+                  _lib.ptr(job.g, "grad_loss"), base, self.cap, det,
+                  _lib.ptr(self.ws, "workspace", dtype=torch.uint8), self.ws.numel(), _lib.stream())
+
+
+def bin_chunks(n_points):
+    """Chunks of the binned backward's workspace that n_points occupy (csrc/hashgrid.hip kChunkPts)."""
+    C = int(_lib.load().nerf_hash_bwd_chunk_points())
+    return (n_points + C - 1) // C
 
 
 _PENDING = {}

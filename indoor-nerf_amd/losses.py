@@ -9,7 +9,7 @@ import math
 
 import torch
 
-from . import _lib
+from . import _lib, hashgrid
 from .hashgrid import accumulate_grad_buffers
 
 
@@ -46,9 +46,39 @@ class TVFn(torch.autograd.Function):
         tables = ctx.saved_tensors
         if g is not None and any(t.requires_grad for t in tables):
             grads = accumulate_grad_buffers(tables)
-            _lib.call("nerf_tv_bwd", _lib.ptr_array(tables), len(tables), ctx.log2_T, ctx.mv, ctx.dmv, ctx.cb,
-                      _lib.ptr(g.contiguous(), "grad_loss"), _lib.ptr_array(grads, "grad_tables"), _lib.stream())
+            g = g.contiguous()
+            L = len(tables)
+            n_ch = int(_lib.load().nerf_tv_bwd_bin_chunks(L, ctx.cb))
+            det = int(hashgrid.deterministic())
+            binned = n_ch > 0 and int(_lib.load().nerf_hash_encode_bwd_workspace_bytes(L, ctx.log2_T, 1, det)) > 0
+            if binned:
+                job = TVBinJob(tables, grads, g, ctx.mv, ctx.dmv, ctx.cb, ctx.log2_T, n_ch)
+                if torch._C._current_graph_task_id() != -1:
+                    # summed by the pass's owner launch with the hash backwards (field._PendingField)
+                    from .field import _pending_field
+                    _pending_field(g.device).add(job)
+                else:
+                    pb = hashgrid.pending_bins(g.device)
+                    pb.reserve(n_ch)
+                    pb.add_tv(job, queue=False)
+                    pb.flush()
+            else:
+                if det:
+                    raise NotImplementedError(f"deterministic TV backward: no binned path for log2_T {ctx.log2_T}")
+                _lib.call("nerf_tv_bwd", _lib.ptr_array(tables), L, ctx.log2_T, ctx.mv, ctx.dmv, ctx.cb,
+                          _lib.ptr(g, "grad_loss"), _lib.ptr_array(grads, "grad_tables"), _lib.stream())
         return (None, None, None) + (None,) * len(tables)
+
+
+class TVBinJob:
+    """A TV backward awaiting its bin launch (csrc/hashgrid.hip tv_bwd_bin_kernel): binned into the
+    iteration's hash-backward workspace and summed by the same owner pass (no float atomics; exact
+    under the deterministic mode)."""
+
+    def __init__(self, tables, grads, g, mv, dmv, cb, log2_T, n_chunks):
+        self.tables, self.grads, self.g = tables, grads, g
+        self.mv, self.dmv, self.cb, self.log2_T, self.n_chunks = mv, dmv, cb, log2_T, n_chunks
+        self.stream = torch.cuda.current_stream() if g.is_cuda else None
 
 
 def draw_min_vertices(embedder, generator=None):

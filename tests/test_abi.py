@@ -11,7 +11,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def _declared_symbols():
     txt = open(os.path.join(ROOT, "include", "nerf_hip.h")).read()
-    return sorted(set(re.findall(r"^\s*(?:const char\*|int|size_t)\s+(nerf_\w+)\s*\(", txt, flags=re.M)))
+    return sorted(set(re.findall(r"^\s*(?:const char\*|int|int64_t|size_t)\s+(nerf_\w+)\s*\(", txt, flags=re.M)))
 
 
 def test_library_exports_every_declared_symbol(nerf):
@@ -34,17 +34,18 @@ def test_error_path_reports_message(nerf):
     with pytest.raises(RuntimeError, match="S must be"):
         L.call("nerf_composite_fwd", None, 4, None, None, None, 4, 1000, 0, *([None] * 7), None)
     # split binned backward: the chunk range and the workspace size are checked before any launch
-    need = L.load().nerf_hash_encode_bwd_workspace_bytes(16, 19, 256 * 4, 0)
+    C = L.load().nerf_hash_bwd_chunk_points()
+    need = L.load().nerf_hash_encode_bwd_workspace_bytes(16, 19, C * 4, 0)
     fake = ctypes.c_void_p(1 << 20)
     with pytest.raises(RuntimeError, match="n_chunks 5 of 4"):
         L.call("nerf_hash_encode_bwd_owner", 16, 19, 5, 4, None, 0, fake, need, None)
     with pytest.raises(RuntimeError, match="workspace"):
         L.call("nerf_hash_encode_bwd_owner", 16, 19, 4, 4, None, 0, fake, need - 1, None)
     with pytest.raises(RuntimeError, match="exceed the capacity"):
-        L.call("nerf_hash_encode_bwd_bin", fake, 3 * 256 + 1, L.host_f32([0] * 3), L.host_f32([1] * 3),
+        L.call("nerf_hash_encode_bwd_bin", fake, 3 * C + 1, L.host_f32([0] * 3), L.host_f32([1] * 3),
                L.host_f32([16] * 16), 16, 19, fake, 32, 2, 1, 4, 0, fake, need, None)
     # the deterministic plan is larger (2^12-row slices, per-level maxima): the plain size is refused
-    need_det = L.load().nerf_hash_encode_bwd_workspace_bytes(16, 19, 256 * 4, 1)
+    need_det = L.load().nerf_hash_encode_bwd_workspace_bytes(16, 19, C * 4, 1)
     assert need_det > need
     with pytest.raises(RuntimeError, match="workspace"):
         L.call("nerf_hash_encode_bwd_owner", 16, 19, 4, 4, None, 1, fake, need, None)
@@ -107,18 +108,20 @@ def test_c_oracle_hash_fwd_exact(golden):
 
 def test_hash_bwd_workspace_plan(nerf):
     """Host-side plan of the binned backward (csrc/hashgrid.hip make_bin_plan): per level and
-    256-point chunk a region of 2048 entries (8-B d feat + 2-B row) and n_owner segment words, each
+    C-point chunk (C = nerf_hash_bwd_chunk_points()) a region of 8 C entries (8-B d feat + 2-B row) and n_owner segment words, each
     array 256-B aligned; owner slices of min(2^13, T) rows, at most 128 owners (log2_T <= 20)."""
     lib = nerf.load_library()
+    C = lib.nerf_hash_bwd_chunk_points()
+    assert C in (256, 512, 1024)
     up = lambda v: (v + 255) // 256 * 256  # noqa: E731
     for L, log2_T, P in ((16, 19, 786432), (16, 19, 262144), (8, 12, 1000), (16, 14, 5), (16, 20, 1000)):
         for det, slice_log2 in ((0, 13), (1, 12)):   # deterministic: 2^12-row slices + per-chunk maxima
             if det and log2_T > 19:
                 assert lib.nerf_hash_encode_bwd_workspace_bytes(L, log2_T, P, det) == 0
                 continue
-            nch = (P + 255) // 256
+            nch = (P + C - 1) // C
             own = 1 << (log2_T - min(slice_log2, log2_T))
-            ent = L * nch * 2048
+            ent = L * nch * 8 * C
             expect = up(ent * 8) + up(ent * 2) + up(L * nch * own * 4) + (up(L * nch * 4) if det else 0)
             assert lib.nerf_hash_encode_bwd_workspace_bytes(L, log2_T, P, det) == expect
     assert lib.nerf_hash_encode_bwd_workspace_bytes(16, 21, 1000, 0) == 0

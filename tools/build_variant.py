@@ -1,0 +1,31 @@
+#!/usr/bin/env python3
+"""Build a variant of libnerfhip.so with extra -D flags into build/variants/<name>/libnerfhip.so, for
+A/B timing on the GPU (NERF_HIP_LIB=<path>). Usage: build_variant.py NAME -DNERF_HASH_CHUNK_POINTS=512"""
+import os
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import __graft_entry__ as g  # noqa: E402
+
+
+def main():
+    name, defs = sys.argv[1], sys.argv[2:]
+    out = os.path.join(ROOT, "build", "variants", name)
+    os.makedirs(out, exist_ok=True)
+    cmds, objs = [], []
+    for src in g._sources():
+        obj = os.path.join(out, os.path.basename(src) + ".o")
+        objs.append(obj)
+        cmds.append([g.HIPCC] + g.HIP_FLAGS + g.EXTRA_FLAGS.get(os.path.basename(src), []) + defs + ["-c", src, "-o", obj])
+    with ThreadPoolExecutor(max_workers=8) as ex:
+        list(ex.map(g._run, cmds))
+    lib = os.path.join(out, "libnerfhip.so")
+    subprocess.run([g.HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", lib] + objs, check=True)
+    print(lib)
+
+
+if __name__ == "__main__":
+    main()

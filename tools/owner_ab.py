@@ -1,21 +1,29 @@
 #!/usr/bin/env python3
-"""A/B of the hash backward's owner pass (NERF_OWNER_EXP variants) on the lego step's bins: the fine
-(4096 x 192) and coarse (4096 x 64) point sets binned side by side, then the owner launch alone,
-interleaved rounds, HIP-event medians. JSON out."""
+"""Timing of the binned hash backward on the lego step's point sets: the fine (4096 x 192) and coarse
+(4096 x 64) sets binned side by side ("bin": both bin launches), then the owner launch alone
+("owner"), HIP-event medians. JSON out. A/B of library builds: run once per build with
+NERF_HIP_LIB=<path> (e.g. chunk sizes: tools/build_variant.py); NERF_DET=1 times the
+deterministic mode."""
 import json
 import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-sys.path.insert(0, os.path.join(ROOT, "tools"))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 import indoor_nerf_amd as nerf  # noqa: E402
 from indoor_nerf_amd import _lib  # noqa: E402
-from indoor_nerf_amd.synthetic import blender_bbox  # noqa: E402
-from kbench import ray_points  # noqa: E402
+from indoor_nerf_amd.synthetic import blender_bbox, blender_rays  # noqa: E402
+
+
+def ray_points(R, S, dev, seed=0):
+    """R synthetic Blender rays, S sorted depths in [2, 6) each: [R S, 3] sample points."""
+    ro, rd = (torch.from_numpy(v).to(dev) for v in blender_rays(R, seed=seed))
+    g = torch.Generator(device=dev).manual_seed(seed)
+    z = torch.sort(2 + 4 * torch.rand(R, S, device=dev, generator=g), -1)[0]
+    return (ro[:, None] + rd[:, None] * z[..., None]).reshape(-1, 3).contiguous(), rd
 
 
 def main():
@@ -24,11 +32,12 @@ def main():
     emb = nerf.HashEmbedder((torch.from_numpy(lo), torch.from_numpy(hi)), finest_resolution=1024).to(dev)
     meta = emb._meta
     sets = [ray_points(4096, 192, dev, seed=1)[0], ray_points(4096, 64, dev, seed=2)[0]]
-    chunks = [(p.shape[0] + 255) // 256 for p in sets]
-    cap = sum(chunks)
     lib = _lib.load()
+    C = int(lib.nerf_hash_bwd_chunk_points())
+    chunks = [(p.shape[0] + C - 1) // C for p in sets]
+    cap = sum(chunks)
     det = int(os.environ.get("NERF_DET", "0"))   # 1: time the deterministic owner pass
-    nbytes = int(lib.nerf_hash_encode_bwd_workspace_bytes(16, 19, 256 * cap, det))
+    nbytes = int(lib.nerf_hash_encode_bwd_workspace_bytes(16, 19, C * cap, det))
     ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
     grads = [torch.zeros(1 << 19, 2, device=dev) for _ in range(16)]
     gp = _lib.ptr_array(grads)
@@ -48,16 +57,11 @@ def main():
         _lib.call("nerf_hash_encode_bwd_owner", 16, 19, cap, cap, gp, det, _lib.ptr(ws, dtype=torch.uint8), nbytes,
                   _lib.stream())
 
-    vers = sys.argv[1].split(",") if len(sys.argv) > 1 else ["owner", "bin0", "bin1", "bin2", "bin3"]
     res = {}
     for rnd in range(5):
-        for v in vers:
-            if v.startswith("bin"):
-                os.environ["NERF_BIN_EXP"] = v[3:]
-                fn = bins
-            else:
-                            bins()
-                fn = owner
+        for v, fn in (("bin", bins), ("owner", owner)):
+            if v == "owner":
+                bins()
             for _ in range(2):
                 fn()
             torch.cuda.synchronize()
@@ -70,7 +74,7 @@ def main():
                 torch.cuda.synchronize()
                 ts.append(e0.elapsed_time(e1))
             res.setdefault(v, []).append(float(np.median(ts)))
-    print(json.dumps({k: round(float(np.median(v)) * 1e3, 1) for k, v in res.items()} | {"unit": "us", "chunks": cap}))
+    print(json.dumps({k: round(float(np.median(v)) * 1e3, 1) for k, v in res.items()} | {"unit": "us", "chunks": cap, "chunk_points": C, "det": det}))
 
 
 if __name__ == "__main__":
