@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Build a variant of libnerfhip.so with extra -D flags into build/variants/<name>/libnerfhip.so, for
-A/B timing on the GPU (NERF_HIP_LIB=<path>). Usage: build_variant.py NAME -DNERF_HASH_CHUNK_POINTS=512"""
+A/B timing on the GPU (NERF_HIP_LIB=<path>). Usage: build_variant.py NAME [--rev GITREV] [-Dflags...]
+(--rev: build the sources of that revision, checked out into a temporary worktree)"""
 import os
 import subprocess
 import sys
@@ -15,8 +16,16 @@ def main():
     name, defs = sys.argv[1], sys.argv[2:]
     out = os.path.join(ROOT, "build", "variants", name)
     os.makedirs(out, exist_ok=True)
+    srcs = g._sources()
+    if defs[:1] == ["--rev"]:
+        rev, defs = defs[1], defs[2:]
+        wt = os.path.join("/tmp", "nerf_variant_" + name)
+        subprocess.run(["git", "-C", ROOT, "worktree", "remove", "--force", wt], capture_output=True)
+        subprocess.run(["git", "-C", ROOT, "worktree", "add", "--detach", wt, rev], check=True, capture_output=True)
+        csrc = os.path.join(wt, "indoor-nerf_amd", "csrc")
+        srcs = sorted(os.path.join(csrc, f) for f in os.listdir(csrc) if f.endswith((".hip", ".cpp")))
     cmds, objs = [], []
-    for src in g._sources():
+    for src in srcs:
         obj = os.path.join(out, os.path.basename(src) + ".o")
         objs.append(obj)
         cmds.append([g.HIPCC] + g.HIP_FLAGS + g.EXTRA_FLAGS.get(os.path.basename(src), []) + defs + ["-c", src, "-o", obj])
