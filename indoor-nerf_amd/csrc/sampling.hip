@@ -176,16 +176,9 @@ __global__ void __launch_bounds__(256) sample_fine_kernel(PdfArgs a) {
         ss = wave_sum_d(ss);
         if (lane == 0) a.z_std[r] = (float)sqrt(ss / (double)N);
     }
-    // rank sort (ties broken by position): out[rank(e)] = v_e
     const float* ray = a.rays + r * a.ray_stride;
     const float ox = ray[0], oy = ray[1], oz = ray[2], dx = ray[3], dy = ray[4], dz = ray[5];
-    for (int e = lane; e < M; e += 64) {
-        const float v = all_l[e];
-        int rank = 0;
-        for (int i = 0; i < M; ++i) {
-            const float w = all_l[i];
-            rank += (w < v) || (w == v && i < e);
-        }
+    auto emit = [&](int rank, float v) {
         const int64_t o = r * M + rank;
         a.z_fine[o] = v;
         if (a.pts_fine) {
@@ -193,6 +186,60 @@ __global__ void __launch_bounds__(256) sample_fine_kernel(PdfArgs a) {
             a.pts_fine[3 * o + 1] = oy + dy * v;
             a.pts_fine[3 * o + 2] = oz + dz * v;
         }
+    };
+    // torch.sort(cat(z_vals, z_samples)) (run_nerf.py:573). The stratified coarse depths are already
+    // ascending; the importance samples are sorted in place (bitonic, padded with +inf to a power of
+    // two in the LDS row after them) and the two runs merged by rank: rank = own index + the count of
+    // the other run below it (binary search; coarse first on ties). Sorted output values do not depend
+    // on how ties are ordered, so this equals the rank sort below, which remains for unsorted coarse
+    // depths (callers passing their own z).
+    bool coarse_sorted = true;
+    for (int i = lane; i + 1 < S; i += 64) coarse_sorted &= !(zr[i + 1] < zr[i]);
+    int P2 = 1;
+    while (P2 < N) P2 <<= 1;
+    if (__ballot(!coarse_sorted) == 0ull && S + P2 <= kMaxMerged) {
+        float* f = all_l + S;
+        for (int i = N + lane; i < P2; i += 64) f[i] = INFINITY;
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        for (int k = 2; k <= P2; k <<= 1) {
+            for (int j = k >> 1; j > 0; j >>= 1) {
+                for (int i = lane; i < P2; i += 64) {
+                    const int l = i ^ j;
+                    if (l > i) {
+                        const float x = f[i], y = f[l];
+                        const bool up = (i & k) == 0;
+                        if (up ? (y < x) : (x < y)) { f[i] = y; f[l] = x; }
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            }
+        }
+        // coarse i: i + #{fine < v}; fine j: j + #{coarse <= v}
+        for (int i = lane; i < S; i += 64) {
+            const float v = all_l[i];
+            int lo = 0, hi = N;
+            while (lo < hi) { const int mid = (lo + hi) >> 1; if (f[mid] < v) lo = mid + 1; else hi = mid; }
+            emit(i + lo, v);
+        }
+        for (int j = lane; j < N; j += 64) {
+            const float v = f[j];
+            int lo = 0, hi = S;
+            while (lo < hi) { const int mid = (lo + hi) >> 1; if (all_l[mid] <= v) lo = mid + 1; else hi = mid; }
+            emit(j + lo, v);
+        }
+        return;
+    }
+    // rank sort (ties broken by position): out[rank(e)] = v_e
+    for (int e = lane; e < M; e += 64) {
+        const float v = all_l[e];
+        int rank = 0;
+        for (int i = 0; i < M; ++i) {
+            const float w = all_l[i];
+            rank += (w < v) || (w == v && i < e);
+        }
+        emit(rank, v);
     }
 }
 

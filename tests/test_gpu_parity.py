@@ -693,12 +693,16 @@ def test_ray_sampler_batches(nerf, gpu, golden):
     assert np.abs(z).max() < 6.0 and abs(z.mean()) < 0.1 and 0.7 < z.std() < 1.3, (z.min(), z.max(), z.std())
 
 
-@pytest.mark.parametrize("S,N", [(64, 128), (37, 30), (16, 9), (64, 256)])
-def test_sample_fine_merge_vs_torch_sort(nerf, gpu, S, N):
+@pytest.mark.parametrize("S,N,det,shuffle", [(64, 128, 1, False), (37, 30, 1, False), (16, 9, 1, False),
+                                              (64, 256, 1, False), (64, 128, 0, False), (37, 30, 0, False),
+                                              (64, 128, 0, True)])
+def test_sample_fine_merge_vs_torch_sort(nerf, gpu, S, N, det, shuffle):
     """nerf_sample_fine's merged z / points vs torch.sort(cat(z, samples)) (run_nerf.py:486-490).
 
     Ragged sizes (M = S + N from 25 to 320, M % 4 != 0) with tied z values (coarse z quantised to
-    1/8, det samples at bin edges): ties are broken by position, as a stable sort would.
+    1/8, det samples at bin edges): ties are broken by position, as a stable sort would. det=0 draws
+    unsorted importance samples (Philox), which the kernel sorts (bitonic) before the merge; shuffle
+    passes unsorted coarse z, which takes the kernel's rank-sort path.
     Sorting is exact: z_fine must equal the sorted values bit for bit; the points are o + d * z in
     fp32 (one rounding each, no contraction) and are compared at 1 ulp-level tolerance."""
     from indoor_nerf_amd import _lib
@@ -706,17 +710,22 @@ def test_sample_fine_merge_vs_torch_sort(nerf, gpu, S, N):
     g = torch.Generator().manual_seed(S * 1000 + N)
     rays = torch.rand(R, C, generator=g).to(gpu)
     z = torch.sort(torch.round(torch.rand(R, S, generator=g) * 8 * 6) / 8 + 0.5, dim=1).values.to(gpu)
+    if shuffle:
+        z = z[:, torch.randperm(S, generator=g).to(gpu)].contiguous()
     w = torch.rand(R, S, generator=g).to(gpu)
     t_imp = torch.linspace(0.0, 1.0, N).to(gpu)
     z_fine = torch.empty(R, S + N, device=gpu)
     pts = torch.empty(R, S + N, 3, device=gpu)
     z_std = torch.empty(R, device=gpu)
     samples = torch.empty(R, N, device=gpu)
-    _lib.call("nerf_sample_fine", _lib.ptr(rays), C, _lib.ptr(z), _lib.ptr(w), R, S, N, 1, _lib.ptr(t_imp), None,
-              0, 0, None, _lib.ptr(z_fine), _lib.ptr(pts), _lib.ptr(z_std), _lib.ptr(samples), _lib.stream())
+    _lib.call("nerf_sample_fine", _lib.ptr(rays), C, _lib.ptr(z), _lib.ptr(w), R, S, N, det, _lib.ptr(t_imp), None,
+              7, 3, None, _lib.ptr(z_fine), _lib.ptr(pts), _lib.ptr(z_std), _lib.ptr(samples), _lib.stream())
     torch.cuda.synchronize()
     want = torch.sort(torch.cat([z, samples], -1), -1).values
     assert torch.equal(z_fine, want)
     want_pts = rays[:, None, 0:3] + rays[:, None, 3:6] * want[..., None]
     torch.testing.assert_close(pts, want_pts, rtol=1e-6, atol=1e-6)
-    assert (want[:, 1:] == want[:, :-1]).any(), "the case must contain ties"
+    if det:
+        assert (want[:, 1:] == want[:, :-1]).any(), "the case must contain ties"
+    else:
+        assert not bool((samples[:, 1:] >= samples[:, :-1]).all()), "importance samples must arrive unsorted"
