@@ -352,7 +352,9 @@ int nerf_radam_step(const nerf_radam_segment* segs, int n_segs, const float* d_c
  * cube: host int[n_levels] cuboid edge. fwd: d_loss[l] += TV_l (ACCUMULATED; zero it first).
  * bwd: d_dtables[l] += d(scale_l * TV_l)/d table, scale: host float[n_levels]. */
 int nerf_tv_fwd(const float* const* d_tables, int n_levels, int log2_T, const int64_t* min_vertex,
-                const int64_t* d_min_vertex, const int* cube, float* d_loss, void* stream);
+                const int64_t* d_min_vertex, const int* cube, float* d_loss,
+                float* d_verts /* optional out: float2[sum_l (cube_l+1)^3], the vertices' table rows */,
+                void* stream);
 int nerf_tv_bwd(const float* const* d_tables, int n_levels, int log2_T, const int64_t* min_vertex,
                 const int64_t* d_min_vertex, const int* cube, const float* d_scale /* device [n_levels] */,
                 float* const* d_dtables, void* stream);
@@ -364,6 +366,7 @@ int nerf_tv_bwd(const float* const* d_tables, int n_levels, int log2_T, const in
 int64_t nerf_tv_bwd_bin_chunks(int n_levels, const int* cube);
 int nerf_tv_bwd_bin(const float* const* d_tables, int n_levels, int log2_T, const int64_t* min_vertex,
                     const int64_t* d_min_vertex, const int* cube, const float* d_scale /* device [n_levels] */,
+                    const float* d_verts /* optional: nerf_tv_fwd's d_verts of the same tables and cuboids */,
                     int64_t chunk_base, int64_t chunk_capacity, int deterministic, void* d_workspace,
                     size_t workspace_bytes, void* stream);
 

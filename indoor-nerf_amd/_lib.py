@@ -129,11 +129,11 @@ SIGNATURES = {
     "nerf_radam_step": [ctypes.POINTER(RAdamSegment), c_int, c_vp, c_vp],
     "nerf_nearest_pixel": [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp],
     "nerf_tv_fwd": [ctypes.POINTER(c_vp), c_int, c_int, ctypes.POINTER(c_i64), c_vp, ctypes.POINTER(c_int), c_vp,
-                    c_vp],
+                    c_vp, c_vp],
     "nerf_tv_bwd": [ctypes.POINTER(c_vp), c_int, c_int, ctypes.POINTER(c_i64), c_vp, ctypes.POINTER(c_int), c_vp,
                     ctypes.POINTER(c_vp), c_vp],
     "nerf_tv_bwd_bin": [ctypes.POINTER(c_vp), c_int, c_int, ctypes.POINTER(c_i64), c_vp, ctypes.POINTER(c_int), c_vp,
-                        c_i64, c_i64, c_int, c_vp, ctypes.c_size_t, c_vp],
+                        c_vp, c_i64, c_i64, c_int, c_vp, ctypes.c_size_t, c_vp],
     "nerf_train_loss_fwd": [c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, ctypes.c_float, c_vp, c_int, ctypes.c_float,
                             c_vp, c_vp, c_vp, c_vp],
     "nerf_quant_params": [ctypes.POINTER(Quantizer), c_int, c_int, c_vp, c_vp],

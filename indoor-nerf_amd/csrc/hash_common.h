@@ -94,6 +94,8 @@ struct TVParams {
     const int64_t* dmv;   // optional device [L][3] cuboid corners (graph replays draw new ones)
     const float* scale;   // bwd: device [L] upstream gradient per level
     float* loss;          // fwd: device [L]
+    float2* verts;        // optional: the cuboid vertices' table rows, level l at verts + vstart[l]
+                          // (written by tv_fwd, read by tv_bwd_bin in place of the hashed gathers)
 };
 
 __device__ __forceinline__ float2 tv_fetch(const float2* tab, const int* mv, int i, int j, int k, uint32_t mask) {

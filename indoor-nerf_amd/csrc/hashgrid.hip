@@ -297,45 +297,55 @@ __global__ void __launch_bounds__(THREADS) hash_encode_bwd_kernel(
 
 // TV backward (loss.py:11-43 autograd) into the binned workspace, summed by the same owner pass as
 // the hash backward: no memory-side float atomics, and deterministic with it. Chunk k of level l
-// holds vertices [k C, (k + 1) C) of the level's (cube + 1)^3 cuboid (C = kChunkPts; chunks past a
-// level's last vertex are empty), one entry per vertex: row hash(min_vertex + (i, j, k)), value
-// (sum over the in-cuboid neighbours n of 2 (e_v - e_n)) x scale[l] / cube — the per-vertex terms
-// and op order of the atomic tv_bwd_kernel (optim.hip).
+// holds vertices [k C, (k + 1) C) of the level's (cube + 1)^3 cuboid (C = kChunkCap, 8 vertices per
+// thread; chunks past a level's last vertex are empty), one entry per vertex: row hash(min_vertex +
+// (i, j, k)), value (sum over the in-cuboid neighbours n of 2 (e_v - e_n)) x scale[l] / cube — the
+// per-vertex terms and op order of the atomic tv_bwd_kernel (optim.hip).
 template <int THREADS>
 __global__ void __launch_bounds__(THREADS) tv_bwd_bin_kernel(TVParams P, HashGradParams hp) {
+    constexpr int NE = 8;   // vertices per thread: chunks of kChunkCap entries, like the hash bins
     const int l = blockIdx.y;
     const int c = P.cube[l], n1 = c + 1;
     const uint32_t nv = (uint32_t)(P.vstart[l + 1] - P.vstart[l]);
     const float2* tab = reinterpret_cast<const float2*>(P.tables[l]);
     int mv[3];
     tv_corner(P, l, mv);
-    const uint32_t lv = blockIdx.x * (uint32_t)THREADS + threadIdx.x;
-    const bool ok = lv < nv;
-    int i = 0, j = 0, k = 0;
-    float gx = 0.f, gy = 0.f;
-    uint32_t h = 0;
-    if (ok) {
-        tv_vertex(lv, n1, i, j, k);
-        const float2 e = tv_fetch(tab, mv, i, j, k, P.mask);
-        auto pair = [&](bool cond, int di, int dj, int dk) {
-            if (!cond) return;
-            const float2 f = tv_fetch(tab, mv, i + di, j + dj, k + dk, P.mask);
-            gx += 2.0f * (e.x - f.x);
-            gy += 2.0f * (e.y - f.y);
-        };
-        pair(i > 0, -1, 0, 0);
-        pair(i < c, 1, 0, 0);
-        pair(j > 0, 0, -1, 0);
-        pair(j < c, 0, 1, 0);
-        pair(k > 0, 0, 0, -1);
-        pair(k < c, 0, 0, 1);
-        h = spatial_hash3((uint32_t)(mv[0] + i), (uint32_t)(mv[1] + j), (uint32_t)(mv[2] + k), P.mask);
-    }
     const float s = P.scale[l] / (float)c;
-    const uint32_t hh[1] = {h};
-    const float vx[1] = {gx * s}, vy[1] = {gy * s};
-    const bool on[1] = {ok && (vx[0] != 0.f || vy[0] != 0.f)};
-    bin_chunk<THREADS, 1>(hp, l, hp.chunk_base + (int)blockIdx.x, hh, vx, vy, on);
+    uint32_t hh[NE];
+    float vx[NE], vy[NE];
+    bool on[NE];
+#pragma unroll
+    for (int q = 0; q < NE; ++q) {
+        const uint32_t lv = blockIdx.x * (uint32_t)(NE * THREADS) + q * THREADS + threadIdx.x;
+        float gx = 0.f, gy = 0.f;
+        hh[q] = 0;
+        on[q] = false;
+        if (lv < nv) {
+            int i, j, k;
+            tv_vertex(lv, n1, i, j, k);
+            // the forward's gathered rows (dense, vertex order: neighbours are lv +- 1, n1, n1^2), or
+            // the hashed table rows
+            const float2* V = P.verts ? P.verts + P.vstart[l] : nullptr;
+            const float2 e = V ? V[lv] : tv_fetch(tab, mv, i, j, k, P.mask);
+            auto pair = [&](bool cond, int di, int dj, int dk) {
+                if (!cond) return;
+                const float2 f = V ? V[(int)lv + (di * n1 + dj) * n1 + dk] : tv_fetch(tab, mv, i + di, j + dj, k + dk, P.mask);
+                gx += 2.0f * (e.x - f.x);
+                gy += 2.0f * (e.y - f.y);
+            };
+            pair(i > 0, -1, 0, 0);
+            pair(i < c, 1, 0, 0);
+            pair(j > 0, 0, -1, 0);
+            pair(j < c, 0, 1, 0);
+            pair(k > 0, 0, 0, -1);
+            pair(k < c, 0, 0, 1);
+            hh[q] = spatial_hash3((uint32_t)(mv[0] + i), (uint32_t)(mv[1] + j), (uint32_t)(mv[2] + k), P.mask);
+        }
+        vx[q] = gx * s;
+        vy[q] = gy * s;
+        on[q] = lv < nv && (vx[q] != 0.f || vy[q] != 0.f);
+    }
+    bin_chunk<THREADS, NE>(hp, l, hp.chunk_base + (int)blockIdx.x, hh, vx, vy, on);
 }
 
 // ---- owner pass of the binned backward ----------------------------------------------------
@@ -359,7 +369,9 @@ __global__ void __launch_bounds__(THREADS) tv_bwd_bin_kernel(TVParams P, HashGra
 template <int SLICE_LOG2, int THREADS, bool DET>
 __global__ void __launch_bounds__(THREADS) hash_bwd_owner_kernel(HashGradParams hp) {
     constexpr int kOwnerThreads = THREADS;
-    constexpr int kOwnerWindow = 2 * THREADS;   // chunks per window: 2 per thread in the scan
+    constexpr int kScanPer = 4;                            // chunks per thread in the window scan
+    constexpr int kOwnerWindow = kScanPer * THREADS;       // chunks per window (the fine + coarse + TV
+                                                           // chunks of a 4096-ray step fit one window)
     // fp64 accumulators: ds_add_f64 runs ~14x the rate of ds_add_f32 on gfx950 (tools/
     // lds_atomic_bench.hip: 2.24 vs 0.165 row updates per clock per CU, random rows), and the
     // slice total is rounded to fp32 once.
@@ -393,13 +405,16 @@ __global__ void __launch_bounds__(THREADS) hash_bwd_owner_kernel(HashGradParams 
     const uint32_t* seg = hp.bin_seg + ((size_t)lvl * n_own + o) * hp.chunk_stride;
     for (int w0 = 0; w0 < hp.nchunks; w0 += kOwnerWindow) {
         const int nw = min(kOwnerWindow, hp.nchunks - w0);
-        // segment counts of the window -> exclusive prefix s_pre (2 chunks per thread)
-        uint32_t c0 = 0, c1 = 0;
-        const int i0 = 2 * tid, i1 = 2 * tid + 1;
-        if (i0 < nw) { const uint32_t v = seg[w0 + i0]; c0 = v >> 16; s_beg[i0] = (uint16_t)(v & 0xFFFFu); }
-        if (i1 < nw) { const uint32_t v = seg[w0 + i1]; c1 = v >> 16; s_beg[i1] = (uint16_t)(v & 0xFFFFu); }
-        const uint32_t pair = c0 + c1;
-        uint32_t inc = pair;
+        // segment counts of the window -> exclusive prefix s_pre (kScanPer consecutive chunks per thread)
+        uint32_t cnt[kScanPer], part = 0;
+#pragma unroll
+        for (int k = 0; k < kScanPer; ++k) {
+            const int i = kScanPer * tid + k;
+            cnt[k] = 0;
+            if (i < nw) { const uint32_t v = seg[w0 + i]; cnt[k] = v >> 16; s_beg[i] = (uint16_t)(v & 0xFFFFu); }
+            part += cnt[k];
+        }
+        uint32_t inc = part;
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
             const uint32_t t = __shfl_up(inc, d, 64);
@@ -407,12 +422,15 @@ __global__ void __launch_bounds__(THREADS) hash_bwd_owner_kernel(HashGradParams 
         }
         if (lane == 63) s_wsum[wave] = inc;
         __syncthreads();
-        uint32_t wbase = 0;
-        for (int w = 0; w < wave; ++w) wbase += s_wsum[w];
-        const uint32_t ex = wbase + inc - pair;
-        if (i0 <= nw) s_pre[i0] = ex;
-        if (i1 <= nw) s_pre[i1] = ex + c0;
-        if (i1 + 1 == nw) s_pre[nw] = ex + pair;   // nw == kOwnerWindow: no thread has i0 == nw
+        uint32_t ex = inc - part;
+        for (int w = 0; w < wave; ++w) ex += s_wsum[w];
+#pragma unroll
+        for (int k = 0; k < kScanPer; ++k) {
+            const int i = kScanPer * tid + k;
+            if (i <= nw) s_pre[i] = ex;      // i == nw: the window total
+            ex += cnt[k];
+        }
+        if (nw == kOwnerWindow && tid == kOwnerThreads - 1) s_pre[nw] = ex;   // no thread holds i == nw
         __syncthreads();
         // The window's entries split evenly across the waves; a wave walks its range 64 entries
         // (one per lane) per step. Chunk lookup is wave-cooperative, with no per-lane walk: lane l
@@ -695,7 +713,7 @@ static int64_t tv_bin_chunks(int n_levels, const int* cube) {
     int64_t most = 0;
     for (int l = 0; l < n_levels; ++l) {
         const int64_t n1 = (int64_t)cube[l] + 1;
-        most = std::max<int64_t>(most, (n1 * n1 * n1 + kChunkPts - 1) / kChunkPts);
+        most = std::max<int64_t>(most, (n1 * n1 * n1 + kChunkCap - 1) / kChunkCap);
     }
     return most;
 }
@@ -708,9 +726,9 @@ extern "C" int64_t nerf_tv_bwd_bin_chunks(int n_levels, const int* cube) {
 }
 
 extern "C" int nerf_tv_bwd_bin(const float* const* d_tables, int n_levels, int log2_T, const int64_t* min_vertex,
-                               const int64_t* d_min_vertex, const int* cube, const float* d_scale, int64_t chunk_base,
-                               int64_t chunk_capacity, int deterministic, void* d_workspace, size_t workspace_bytes,
-                               void* stream) {
+                               const int64_t* d_min_vertex, const int* cube, const float* d_scale,
+                               const float* d_verts, int64_t chunk_base, int64_t chunk_capacity, int deterministic,
+                               void* d_workspace, size_t workspace_bytes, void* stream) {
     TVParams P{};
     int rc = fill_tv(P, n_levels, log2_T, min_vertex, d_min_vertex, cube);
     if (rc) return rc;
@@ -720,6 +738,7 @@ extern "C" int nerf_tv_bwd_bin(const float* const* d_tables, int n_levels, int l
         P.tables[l] = d_tables[l];
     }
     P.scale = d_scale;
+    P.verts = const_cast<float2*>(reinterpret_cast<const float2*>(d_verts));
     HashGradParams hp{};
     rc = bin_layout("tv_bwd_bin", n_levels, log2_T, chunk_capacity, deterministic, d_workspace, workspace_bytes, hp);
     if (rc) return rc;

@@ -86,6 +86,7 @@ __global__ void __launch_bounds__(256) tv_fwd_kernel(TVParams P) {
         int i, j, k;
         tv_vertex(lv, n1, i, j, k);
         const float2 e = tv_fetch(tab, mv, i, j, k, P.mask);
+        if (P.verts) P.verts[P.vstart[l] + lv] = e;
         float acc = 0.f;
         if (i < c) { const float2 f = tv_fetch(tab, mv, i + 1, j, k, P.mask); const float dx = f.x - e.x, dy = f.y - e.y; acc += dx * dx + dy * dy; }
         if (j < c) { const float2 f = tv_fetch(tab, mv, i, j + 1, k, P.mask); const float dx = f.x - e.x, dy = f.y - e.y; acc += dx * dx + dy * dy; }
@@ -178,7 +179,8 @@ extern "C" int nerf_radam_step(const nerf_radam_segment* segs, int n_segs, const
 }
 
 extern "C" int nerf_tv_fwd(const float* const* d_tables, int n_levels, int log2_T, const int64_t* min_vertex,
-                           const int64_t* d_min_vertex, const int* cube, float* d_loss, void* stream) {
+                           const int64_t* d_min_vertex, const int* cube, float* d_loss, float* d_verts,
+                           void* stream) {
     TVParams P{};
     int rc = fill_tv(P, n_levels, log2_T, min_vertex, d_min_vertex, cube);
     if (rc) return rc;
@@ -188,6 +190,7 @@ extern "C" int nerf_tv_fwd(const float* const* d_tables, int n_levels, int log2_
         P.tables[l] = d_tables[l];
     }
     P.loss = d_loss;
+    P.verts = reinterpret_cast<float2*>(d_verts);
     hipLaunchKernelGGL(tv_fwd_kernel, dim3(kTVBlocks, n_levels), dim3(256), 0, as_stream(stream), P);
     NERF_CHECK_LAUNCH("tv_fwd");
     return NERF_OK;

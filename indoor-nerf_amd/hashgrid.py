@@ -184,7 +184,7 @@ class _PendingBins:
         L = len(job.tables)
         base, det = self._slot(L, job.log2_T, job.grads, job.n_chunks, job.tables[0].device, queue)
         _lib.call("nerf_tv_bwd_bin", _lib.ptr_array(job.tables), L, job.log2_T, job.mv, job.dmv, job.cb,
-                  _lib.ptr(job.g, "grad_loss"), base, self.cap, det,
+                  _lib.ptr(job.g, "grad_loss"), _lib.ptr(job.verts, "tv_verts", allow_none=True), base, self.cap, det,
                   _lib.ptr(self.ws, "workspace", dtype=torch.uint8), self.ws.numel(), _lib.stream())
 
 

@@ -36,9 +36,12 @@ class TVFn(torch.autograd.Function):
             mv, dmv = (_lib.c_i64 * (3 * L))(*[int(v) for v in min_vertex.reshape(-1).tolist()]), None
         cb = (_lib.c_int * L)(*[int(c) for c in cubes])
         loss = torch.zeros(L, device=tables[0].device, dtype=torch.float32)
-        _lib.call("nerf_tv_fwd", _lib.ptr_array(tables), L, log2_T, mv, dmv, cb, _lib.ptr(loss, "loss"), _lib.stream())
+        # the cuboid vertices' rows, gathered once here: the backward's stencil reads them densely
+        verts = torch.empty(2 * sum((int(c) + 1) ** 3 for c in cubes), device=tables[0].device, dtype=torch.float32)
+        _lib.call("nerf_tv_fwd", _lib.ptr_array(tables), L, log2_T, mv, dmv, cb, _lib.ptr(loss, "loss"),
+                  _lib.ptr(verts, "tv_verts"), _lib.stream())
         ctx.save_for_backward(*tables)
-        ctx.mv, ctx.dmv, ctx.cb, ctx.log2_T = mv, dmv, cb, log2_T
+        ctx.mv, ctx.dmv, ctx.cb, ctx.log2_T, ctx.verts = mv, dmv, cb, log2_T, verts
         return loss
 
     @staticmethod
@@ -52,7 +55,7 @@ class TVFn(torch.autograd.Function):
             det = int(hashgrid.deterministic())
             binned = n_ch > 0 and int(_lib.load().nerf_hash_encode_bwd_workspace_bytes(L, ctx.log2_T, 1, det)) > 0
             if binned:
-                job = TVBinJob(tables, grads, g, ctx.mv, ctx.dmv, ctx.cb, ctx.log2_T, n_ch)
+                job = TVBinJob(tables, grads, g, ctx.mv, ctx.dmv, ctx.cb, ctx.log2_T, n_ch, ctx.verts)
                 if torch._C._current_graph_task_id() != -1:
                     # summed by the pass's owner launch with the hash backwards (field._PendingField)
                     from .field import _pending_field
@@ -75,8 +78,8 @@ class TVBinJob:
     iteration's hash-backward workspace and summed by the same owner pass (no float atomics; exact
     under the deterministic mode)."""
 
-    def __init__(self, tables, grads, g, mv, dmv, cb, log2_T, n_chunks):
-        self.tables, self.grads, self.g = tables, grads, g
+    def __init__(self, tables, grads, g, mv, dmv, cb, log2_T, n_chunks, verts=None):
+        self.tables, self.grads, self.g, self.verts = tables, grads, g, verts
         self.mv, self.dmv, self.cb, self.log2_T, self.n_chunks = mv, dmv, cb, log2_T, n_chunks
         self.stream = torch.cuda.current_stream() if g.is_cuda else None
 

@@ -22,7 +22,7 @@ def test_library_exports_every_declared_symbol(nerf):
     for name in declared:
         assert hasattr(lib, name), f"libnerfhip.so does not export {name}"
     assert sorted(L.exported_symbols()) == declared, "ctypes signature table out of sync with the header"
-    assert lib.nerf_abi_version() == 2   # 2: deterministic flag of the binned hash backward
+    assert lib.nerf_abi_version() == 3   # 3: binned TV backward, nerf_tv_fwd vertex rows
 
 
 def test_error_path_reports_message(nerf):
@@ -126,6 +126,19 @@ def test_hash_bwd_workspace_plan(nerf):
             assert lib.nerf_hash_encode_bwd_workspace_bytes(L, log2_T, P, det) == expect
     assert lib.nerf_hash_encode_bwd_workspace_bytes(16, 21, 1000, 0) == 0
     assert lib.nerf_hash_encode_bwd_workspace_bytes(0, 19, 1000, 0) == 0
+
+
+def test_tv_bin_chunks(nerf):
+    """nerf_tv_bwd_bin_chunks: the chunks of the binned TV backward = max over levels of
+    ceil((cube + 1)^3 / (8 C)) (8 vertices per thread of a C-thread bin block); 0 for bad input."""
+    import indoor_nerf_amd._lib as L
+    lib = nerf.load_library()
+    C = lib.nerf_hash_bwd_chunk_points()
+    cubes = [15] * 9 + [19, 25, 33, 44, 50, 50, 50]
+    arr = (L.c_int * 16)(*cubes)
+    assert lib.nerf_tv_bwd_bin_chunks(16, arr) == max(-(-(c + 1) ** 3 // (8 * C)) for c in cubes)
+    assert lib.nerf_tv_bwd_bin_chunks(0, arr) == 0
+    assert lib.nerf_tv_bwd_bin_chunks(1, (L.c_int * 1)(0)) == 0
 
 
 def test_crop_window_matches_reference_grid(golden):

@@ -368,6 +368,20 @@ def test_tv_binned_matches_atomic(nerf, gpu, golden):
     for a, b, r in zip(d1, d2, ref):
         assert torch.equal(a, b)
         torch.testing.assert_close(a, r, rtol=1e-5, atol=1e-9)
+    # without the forward's vertex rows (d_verts NULL): the kernel gathers the hashed rows itself
+    from indoor_nerf_amd import hashgrid
+    from indoor_nerf_amd.losses import TVBinJob
+    grads = [torch.zeros_like(t) for t in tables]
+    cb = (_lib.c_int * L)(*cubes)
+    mvh = (_lib.c_i64 * (3 * L))(*[int(v) for v in mv.reshape(-1).tolist()])
+    n_ch = int(_lib.load().nerf_tv_bwd_bin_chunks(L, cb))
+    pb = hashgrid.pending_bins(gpu)
+    pb.reserve(n_ch)
+    pb.add_tv(TVBinJob(tables, grads, scale, mvh, None, cb, emb.log2_hashmap_size, n_ch), queue=False)
+    pb.flush()
+    torch.cuda.synchronize()
+    for a, r in zip(grads, got):
+        torch.testing.assert_close(a, r, rtol=1e-6, atol=1e-12)
 
 
 def test_train_step_full_size_finite(nerf, gpu):
