@@ -437,8 +437,8 @@ __global__ void __launch_bounds__(512, 2) mlp_act_minmax_x6_kernel(MlpArgs a) {
 // the chain wave waits for ack == k - 1 before it writes stage k and then stores ready = k
 // (release: its staging writes are complete first); the wgrad wave waits for ready == k, reads
 // the stage and stores ack = k (release: its reads have returned). Both waves walk the same tile
-// list with the same eight stages per tile, so every wait is matched and the loop ends together.
-constexpr int CG_STAGES = 8;
+// list with the same seven stages per tile, so every wait is matched and the loop ends together.
+constexpr int CG_STAGES = 7;
 
 #ifdef NERF_X6CG_PROF   // diagnostic build only: wait / loop cycles of the chain and wgrad waves
 __device__ unsigned long long cg_prof[4];
@@ -593,46 +593,35 @@ __device__ __forceinline__ void bwd_chain_role(const MlpArgs& a, const __bf16* i
             for (int r = 8; r < 16; ++r) a.dsh[16u * in.pt + row_of(r, h) - 16] = go[r];
         }
 
-        // stage 6 (dW1): go, h1 (recomputed from a reload of x)
+        // stage 6 (dW1): go, h1 (recomputed from a reload of x) and layer 0's ReLU mask m1 (with QUANT:
+        // before the activation quantizer) in the unused columns 16.. of the gradient tile.
+        // The wgrad wave forms ga1 = mask(W1^T go) itself (it waits on the chain wave otherwise).
         float xr[16];
         load_x6(a, in.pt, in.valid, h, xr, opaque_zero());
-        floatx16 h1[2];
-        uint32_t m1;
-        layer0<QUANT>(imt, xr, h1, m1, lane, aq);
-        floatx16 ga1[2];
         {
+            floatx16 h1[2];
+            uint32_t m1;
+            layer0<QUANT>(imt, xr, h1, m1, lane, aq);
             const S3 GO = split_chunk(go, 0);
             open(true);
 #pragma unroll
             for (int t = 0; t < 2; ++t) stage_tileF(actF, h1[t], 32 * t, j, h);
             stage_grad(stGb[0], GO, 0, j, h);      // columns 16..31 stale: they only reach dW1 rows >= 16
-            publish();
+            if constexpr (!QUANT) {
+                m1 = 0;
 #pragma unroll
-            for (int t = 0; t < 2; ++t) {
-                floatx16 acc = mma6(tr_read(imt, IM_PIECE, IM_W1, S64, 0, 32 * t, lane), GO, zero16());
+                for (int t = 0; t < 2; ++t)
 #pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const bool on = QUANT ? ((m1 >> (16 * t + r)) & 1u) != 0u : h1[t][r] > 0.f;
-                    acc[r] = on ? acc[r] : 0.f;
-                }
-                ga1[t] = acc;
+                    for (int r = 0; r < 16; ++r) m1 |= (h1[t][r] > 0.f ? 1u : 0u) << (16 * t + r);
             }
-        }
-
-        // stages 7, 8 (dW0 rows 32t..): ga1 tile t, x; the wgrad wave also forms gx = W0^T ga1 from
-        // the staged ga1 (the d features, off this wave's critical path)
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-            const S3 g0 = split_chunk(ga1[t], 0), g1 = split_chunk(ga1[t], 1);
-            open(t == 0);
-            if (t == 0) {
-                stage_arrF(actF, xr, 0, j, h);
-                stage_arrF(actF, xr + 8, 16, j, h);
-            }
-            stage_grad(stGb[1 - t], g0, 0, j, h);
-            stage_grad(stGb[1 - t], g1, 1, j, h);
+            *reinterpret_cast<uint32_t*>(stGb[0] + j * S32 + 16 + 2 * h) = m1;
             publish();
         }
+        // stage 7 (dW0): x
+        open(true);
+        stage_arrF(actF, xr, 0, j, h);
+        stage_arrF(actF, xr + 8, 16, j, h);
+        publish();
     }
 #ifdef NERF_X6CG_PROF
     if (lane == 0) { atomicAdd(&cg_prof[0], waited); atomicAdd(&cg_prof[1], CG_T() - t_start); }
@@ -736,8 +725,9 @@ __device__ __forceinline__ void mma32(floatx16 (&acc)[NU], const Ops32<NU>& o) {
 
 // Every stage: wait for it, read all of its operands, release the buffer (ack), then run the MFMAs,
 // so the chain wave's next staging overlaps them.
+template <bool QUANT>
 __device__ __forceinline__ void bwd_wgrad_role(const MlpArgs& a, const __bf16* img, const __bf16* stA,
-                                               const __bf16* stG, int* ready, int* ack, int p, int lane, WgradX6& g,
+                                               __bf16* stG, int* ready, int* ack, int p, int lane, WgradX6& g,
                                                int blk, int nblk) {
     const int j = lane & 31, h = lane >> 5;
     const float* actF = reinterpret_cast<const float*>(stA);
@@ -774,36 +764,57 @@ __device__ __forceinline__ void bwd_wgrad_role(const MlpArgs& a, const __bf16* i
             take(); read32<1>(o, stG + t * 3 * STG_PIECE, actF, lane); release();
             mma32<1>(g.dC0[t], o);
         }
-        {   // 6: dW1
-            Ops16 o;
-            take(); read16(o, stG, actF, lane); release();   // stage 6: gradient buffer 0
-            mma16(g.dW1, o);
-        }
+        // 6: dW1, and ga1 = W1^T go masked by layer 0's ReLU (go read in the B layout: lane = point).
+        // From here until stage 7 is released both gradient buffers are this wave's (the chain wave
+        // stages only x at stage 7, and its next gradient write waits for stage 7's release): ga1 is
+        // staged there, tile t in buffer 1 - t, for dW0 and gx = W0^T ga1 (the d features).
         floatx16 gx = zero16();
+        {
+            Ops16 o;
+            take();
+            read16(o, stG, actF, lane);   // stage 6: gradient buffer 0
+            const S3 GOb = row_read_st(stG, STG_PIECE, S32, j, 4 * h);
+            const uint32_t m1 = *reinterpret_cast<const uint32_t*>(stG + j * S32 + 16 + 2 * h);
+            release();
+            mma16(g.dW1, o);
 #pragma unroll
-        for (int t = 0; t < 2; ++t) {   // 7, 8: dW0, and gx = W0^T ga1 (B = the staged ga1, lane = point)
+            for (int t = 0; t < 2; ++t) {
+                floatx16 ga1 = mma6(tr_read(img, IM_PIECE, IM_W1, S64, 0, 32 * t, lane), GOb, zero16());
+#pragma unroll
+                for (int r = 0; r < 16; ++r) ga1[r] = ((m1 >> (16 * t + r)) & 1u) ? ga1[r] : 0.f;
+                stage_grad(stG + (1 - t) * 3 * STG_PIECE, split_chunk(ga1, 0), 0, j, h);
+                stage_grad(stG + (1 - t) * 3 * STG_PIECE, split_chunk(ga1, 1), 1, j, h);
+            }
+        }
+        take();   // 7: dW0 = ga1 x^T and gx = W0^T ga1 (B = the staged ga1, lane = point)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
             Ops32<1> o;
             S3 gb[2];
-            take();
-            const __bf16* sg = stG + (1 - t) * 3 * STG_PIECE;   // stages 7, 8: buffers 1, 0
+            const __bf16* sg = stG + (1 - t) * 3 * STG_PIECE;
             read32<1>(o, sg, actF, lane);
 #pragma unroll
             for (int c = 0; c < 2; ++c) gb[c] = row_read_st(sg, STG_PIECE, S32, j, 16 * c + 4 * h);
-            flag_set(ack, ++seq);
+            if (t == 1) flag_set(ack, ++seq);
             mma32<1>(g.dW0[t], o);
 #pragma unroll
             for (int c = 0; c < 2; ++c) gx = mma6(tr_read(img, IM_PIECE, IM_W0, S32, 32 * t + 16 * c, 0, lane), gb[c], gx);
         }
         const uint32_t pt = (uint32_t)(tile * 32 + j);
         if (a.dfeat && tile * 32 + j < a.P) {
+            // offsets formed per tile (opaque stride): hoisted out of the loop they pin 16 registers
+            const uint32_t sl = (uint32_t)a.sl + (uint32_t)opaque_zero(), base = pt * (uint32_t)a.sp;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int fi = row_of(r, h);
-                a.dfeat[pt * (uint32_t)a.sp + (fi >> 1) * (uint32_t)a.sl + (fi & 1)] = gx[r];
+                a.dfeat[base + (fi >> 1) * sl + (fi & 1)] = gx[r];
             }
         }
     }
-    static_assert(CG_STAGES == 8, "stage list above");
+    static_assert(CG_STAGES == 7, "stage list above");
 #ifdef NERF_X6CG_PROF
     if (lane == 0) { atomicAdd(&cg_prof[2], waited); atomicAdd(&cg_prof[3], CG_T() - t_start); }
 #endif
@@ -840,7 +851,7 @@ __global__ void __launch_bounds__(512, 1) mlp_bwd_x6cg_kernel(MlpBwdJobs jobs) {
     const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
     WgradX6 g;   // defined (and live) on the wgrad waves only
     if (wgrad_wave) {
-        bwd_wgrad_role(a, img, stA, stG, flags + p, flags + 4 + p, p, lane, g, blk, nblk);
+        bwd_wgrad_role<QUANT>(a, img, stA, stG, flags + p, flags + 4 + p, p, lane, g, blk, nblk);
     } else {
         QuantRec aq{};
         if constexpr (QUANT) aq = *a.aq;
@@ -991,5 +1002,15 @@ int launch_mlp_bwd_x6(const MlpArgs* jobs, int n_jobs, float* det_ws, hipStream_
     }
     return NERF_OK;
 }
+
+#ifdef NERF_X6CG_PROF
+// diagnostic builds only: the chain / wgrad waves' wait and loop cycles summed over all waves since
+// the last call (s_memtime units), then reset
+extern "C" int nerf_x6cg_prof(unsigned long long* out4) {
+    if (hipMemcpyFromSymbol(out4, HIP_SYMBOL(cg_prof), sizeof(cg_prof)) != hipSuccess) return 1;
+    const unsigned long long zero[4] = {0, 0, 0, 0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(cg_prof), zero, sizeof(zero)) == hipSuccess ? 0 : 1;
+}
+#endif
 
 }  // namespace nerf
