@@ -442,6 +442,7 @@ constexpr int CG_STAGES = 7;
 
 #ifdef NERF_X6CG_PROF   // diagnostic build only: wait / loop cycles of the chain and wgrad waves
 __device__ unsigned long long cg_prof[4];
+__device__ unsigned long long cg_stage_wait[8];   // chain wave's wait before each stage of a tile
 #define CG_T() __builtin_amdgcn_s_memtime()
 #endif
 
@@ -502,7 +503,17 @@ __device__ __forceinline__ void bwd_chain_role(const MlpArgs& a, const __bf16* i
 #endif
     // stage k writes gradient buffer k & 1 (and, when it stages activations, the one activation
     // buffer): it may start once the wgrad wave has released stage k - 2 (k - 1 with activations)
-    auto open = [&](bool act) { flag_wait(ack, act ? seq : seq - 1, &waited); };
+#ifdef NERF_X6CG_PROF
+    unsigned long long sw[CG_STAGES] = {};
+    auto open = [&](bool act, int k) {   // k: the stage (1..7) of the tile, a constant after unrolling
+        unsigned long long w = 0;
+        flag_wait(ack, act ? seq : seq - 1, &w);
+        waited += w;
+        sw[k - 1] += w;
+    };
+#else
+    auto open = [&](bool act, int) { flag_wait(ack, act ? seq : seq - 1, &waited); };
+#endif
     __bf16* const stGb[2] = {stG, stG + 3 * STG_PIECE};
     auto publish = [&]() { flag_set(ready, ++seq); };
     const int64_t n_tiles = (a.P + 31) / 32;
@@ -524,7 +535,7 @@ __device__ __forceinline__ void bwd_chain_role(const MlpArgs& a, const __bf16* i
         {
             const S3 GR = h ? split8(0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f)
                             : split8(g4.x, g4.y, g4.z, 0.f, 0.f, 0.f, 0.f, 0.f);
-            open(true);
+            open(true, 1);
             stage_grad(stGb[1], GR, 0, j, h);      // columns 16..31 stale: they only reach dC2 rows >= 16
 #pragma unroll
             for (int t = 0; t < 2; ++t) stage_tileF(actF, f.h3[t], 32 * t, j, h);
@@ -542,7 +553,7 @@ __device__ __forceinline__ void bwd_chain_role(const MlpArgs& a, const __bf16* i
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
             const S3 g0 = split_chunk(ga3[t], 0), g1 = split_chunk(ga3[t], 1);
-            open(t == 0);
+            open(t == 0, 2 + t);
             if (t == 0) {
 #pragma unroll
                 for (int ta = 0; ta < 2; ++ta) stage_tileF(actF, f.h2[ta], 32 * ta, j, h);
@@ -574,7 +585,7 @@ __device__ __forceinline__ void bwd_chain_role(const MlpArgs& a, const __bf16* i
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
             const S3 g0 = split_chunk(ga2[t], 0), g1 = split_chunk(ga2[t], 1);
-            open(t == 0);
+            open(t == 0, 4 + t);
             if (t == 0) {
 #pragma unroll
                 for (int r = 0; r < 8; ++r) actF[row_of(r, h) * SPF + j] = f.o[r];
@@ -603,7 +614,7 @@ __device__ __forceinline__ void bwd_chain_role(const MlpArgs& a, const __bf16* i
             uint32_t m1;
             layer0<QUANT>(imt, xr, h1, m1, lane, aq);
             const S3 GO = split_chunk(go, 0);
-            open(true);
+            open(true, 6);
 #pragma unroll
             for (int t = 0; t < 2; ++t) stage_tileF(actF, h1[t], 32 * t, j, h);
             stage_grad(stGb[0], GO, 0, j, h);      // columns 16..31 stale: they only reach dW1 rows >= 16
@@ -618,13 +629,17 @@ __device__ __forceinline__ void bwd_chain_role(const MlpArgs& a, const __bf16* i
             publish();
         }
         // stage 7 (dW0): x
-        open(true);
+        open(true, 7);
         stage_arrF(actF, xr, 0, j, h);
         stage_arrF(actF, xr + 8, 16, j, h);
         publish();
     }
 #ifdef NERF_X6CG_PROF
-    if (lane == 0) { atomicAdd(&cg_prof[0], waited); atomicAdd(&cg_prof[1], CG_T() - t_start); }
+    if (lane == 0) {
+        atomicAdd(&cg_prof[0], waited);
+        atomicAdd(&cg_prof[1], CG_T() - t_start);
+        for (int k = 0; k < CG_STAGES; ++k) atomicAdd(&cg_stage_wait[k], sw[k]);
+    }
 #endif
 }
 
@@ -1005,11 +1020,13 @@ int launch_mlp_bwd_x6(const MlpArgs* jobs, int n_jobs, float* det_ws, hipStream_
 
 #ifdef NERF_X6CG_PROF
 // diagnostic builds only: the chain / wgrad waves' wait and loop cycles summed over all waves since
-// the last call (s_memtime units), then reset
-extern "C" int nerf_x6cg_prof(unsigned long long* out4) {
-    if (hipMemcpyFromSymbol(out4, HIP_SYMBOL(cg_prof), sizeof(cg_prof)) != hipSuccess) return 1;
-    const unsigned long long zero[4] = {0, 0, 0, 0};
-    return hipMemcpyToSymbol(HIP_SYMBOL(cg_prof), zero, sizeof(zero)) == hipSuccess ? 0 : 1;
+// the last call (s_memtime units), then the chain wave's waits per stage; all reset
+extern "C" int nerf_x6cg_prof(unsigned long long* out12) {
+    if (hipMemcpyFromSymbol(out12, HIP_SYMBOL(cg_prof), sizeof(cg_prof)) != hipSuccess) return 1;
+    if (hipMemcpyFromSymbol(out12 + 4, HIP_SYMBOL(cg_stage_wait), sizeof(cg_stage_wait)) != hipSuccess) return 1;
+    const unsigned long long zero[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(cg_prof), zero, sizeof(cg_prof)) != hipSuccess) return 1;
+    return hipMemcpyToSymbol(HIP_SYMBOL(cg_stage_wait), zero, sizeof(cg_stage_wait)) == hipSuccess ? 0 : 1;
 }
 #endif
 

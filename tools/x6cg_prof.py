@@ -25,16 +25,19 @@ def main():
     fn = lib.nerf_x6cg_prof
     fn.restype = ctypes.c_int
     fn.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
-    out = (ctypes.c_ulonglong * 4)()
+    out = (ctypes.c_ulonglong * 12)()
     for it in range(4):
         loss = sum((net(x) * g).sum() for net, x, g in zip(nets, xs, gs))
         loss.backward()
         torch.cuda.synchronize()
         assert fn(out) == 0
-    chain_wait, chain_total, wg_wait, wg_total = (int(v) for v in out)
+    chain_wait, chain_total, wg_wait, wg_total = (int(v) for v in out[:4])
+    stage = [int(v) for v in out[4:11]]
     print(json.dumps({"chain_wait_frac": round(chain_wait / max(chain_total, 1), 3),
                       "wgrad_wait_frac": round(wg_wait / max(wg_total, 1), 3),
-                      "chain_total": chain_total, "wgrad_total": wg_total}))
+                      "chain_total": chain_total, "wgrad_total": wg_total,
+                      # chain wave's wait before stage k (1..7) of a tile, as a share of its total time
+                      "chain_wait_by_stage": [round(w / max(chain_total, 1), 3) for w in stage]}))
 
 
 if __name__ == "__main__":
