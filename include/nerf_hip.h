@@ -277,7 +277,10 @@ int nerf_composite_bwd(const float* d_raw, int raw_channels, const float* d_z, c
 int nerf_sample_stratified(const float* d_rays, int64_t ray_stride, int64_t n_rays, int n_samples,
                            const float* d_t, int lindisp, int perturb, const float* d_u,
                            uint64_t seed, uint64_t offset, const uint64_t* d_rng,
-                           float* d_z, float* d_pts, void* stream);
+                           float* d_z, float* d_pts,
+                           float* d_dirs /* optional [R,3]: ray columns 3..5, contiguous */,
+                           float* d_viewdirs /* optional [R,3]: the last 3 ray columns (stride > 8) */,
+                           void* stream);
 
 /* sample_pdf (run_nerf_helpers.py:354-397) on bins [R,n_bins], weights [R,n_bins-1];
  * det: u = d_t_imp (torch.linspace(0,1,N) values, [N]); else u = d_u [R,N] or Philox. */

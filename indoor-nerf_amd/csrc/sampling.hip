@@ -9,6 +9,8 @@ struct StratArgs {
     const float* t; int lindisp; int perturb; const float* u; uint64_t seed, offset;
     const uint64_t* rng;   // optional device (seed, offset): graph replays draw fresh numbers
     float* z; float* pts;
+    float* dirs;       // optional [R,3]: the rays' directions (columns 3..5), contiguous
+    float* viewdirs;   // optional [R,3]: the rays' view directions (the last three columns)
 };
 
 __device__ __forceinline__ float base_depth(float near, float far, float t, int lindisp) {
@@ -35,6 +37,15 @@ __global__ void __launch_bounds__(256) sample_stratified_kernel(StratArgs a) {
         z = lower + (upper - lower) * u;
     }
     a.z[i] = z;
+    if (j == 0) {   // the contiguous per-ray copies render_rays hands to the field and compositing
+        if (a.dirs) {
+            a.dirs[3 * r + 0] = ray[3]; a.dirs[3 * r + 1] = ray[4]; a.dirs[3 * r + 2] = ray[5];
+        }
+        if (a.viewdirs) {
+            const float* v = ray + a.stride - 3;
+            a.viewdirs[3 * r + 0] = v[0]; a.viewdirs[3 * r + 1] = v[1]; a.viewdirs[3 * r + 2] = v[2];
+        }
+    }
     if (a.pts) {
         a.pts[3 * i + 0] = ray[0] + ray[3] * z;
         a.pts[3 * i + 1] = ray[1] + ray[4] * z;
@@ -249,12 +260,16 @@ using namespace nerf;
 
 extern "C" int nerf_sample_stratified(const float* d_rays, int64_t ray_stride, int64_t n_rays, int n_samples,
                                       const float* d_t, int lindisp, int perturb, const float* d_u, uint64_t seed,
-                                      uint64_t offset, const uint64_t* d_rng, float* d_z, float* d_pts, void* stream) {
+                                      uint64_t offset, const uint64_t* d_rng, float* d_z, float* d_pts,
+                                      float* d_dirs, float* d_viewdirs, void* stream) {
     NERF_REQUIRE(n_rays >= 0 && n_samples >= 1, "sample_stratified: R=%lld S=%d", (long long)n_rays, n_samples);
     NERF_REQUIRE(ray_stride >= 8, "sample_stratified: ray_stride %lld < 8", (long long)ray_stride);
     NERF_REQUIRE(d_rays && d_t && d_z, "sample_stratified: null arg");
     if (n_rays == 0) return NERF_OK;
-    StratArgs a{d_rays, ray_stride, n_rays, n_samples, d_t, lindisp, perturb, d_u, seed, offset, d_rng, d_z, d_pts};
+    NERF_REQUIRE(!d_viewdirs || ray_stride > 8, "sample_stratified: viewdirs need ray_stride > 8 (got %lld)",
+                 (long long)ray_stride);
+    StratArgs a{d_rays, ray_stride, n_rays, n_samples, d_t, lindisp, perturb, d_u, seed, offset, d_rng, d_z, d_pts,
+                d_dirs, d_viewdirs};
     hipLaunchKernelGGL(sample_stratified_kernel, dim3(blocks_for(n_rays * n_samples, 256)), dim3(256), 0,
                        as_stream(stream), a);
     NERF_CHECK_LAUNCH("sample_stratified");

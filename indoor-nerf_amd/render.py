@@ -184,8 +184,10 @@ def render_rays(ray_batch, network_fn, network_query_fn, N_samples, embed_fn=Non
     R, C = rays.shape
     dev = rays.device
     f = dict(device=dev, dtype=torch.float32)
-    viewdirs = rays[:, -3:].contiguous() if C > 8 else None
-    rays_d = rays[:, 3:6].contiguous()
+    # contiguous copies of the directions (compositing) and view directions (field), written by the
+    # sampler launch instead of two slicing copies
+    viewdirs = torch.empty(R, 3, **f) if C > 8 else None
+    rays_d = torch.empty(R, 3, **f)
 
     z = torch.empty(R, N_samples, **f)
     pts = torch.empty(R, N_samples, 3, **f)
@@ -193,7 +195,8 @@ def render_rays(ray_batch, network_fn, network_query_fn, N_samples, embed_fn=Non
     seed, off, rng = (0, 0, None) if (u is not None or not perturb > 0.) else _rng()
     _lib.call("nerf_sample_stratified", _lib.ptr(rays, "ray_batch"), C, R, N_samples, _lib.ptr(_linspace(N_samples, dev)),
               int(bool(lindisp)), int(perturb > 0.), _lib.ptr(u, "u", allow_none=True), seed, off, rng, _lib.ptr(z, "z"),
-              _lib.ptr(pts, "pts"), _lib.stream())
+              _lib.ptr(pts, "pts"), _lib.ptr(rays_d, "rays_d"), _lib.ptr(viewdirs, "viewdirs", allow_none=True),
+              _lib.stream())
 
     raw = network_query_fn(pts, viewdirs, network_fn)
     outs = raw2outputs(raw, z, rays_d, raw_noise_std, white_bkgd, pytest=pytest, predict_normals=predict_normals)
