@@ -127,8 +127,11 @@ constexpr int kMaxOwners = 1 << kMaxOwnersLog2;
 // at its slot of an LDS image of the chunk's region, then write the image out with 16-B coalesced
 // stores (scattered per-lane stores were TA-bound: 64 lines per instruction). Every (level, chunk)
 // in [0, n_chunks) gets its n_owner segment words, empty ones included. NE entries per thread
-// (8 corners of a point; 1 TV vertex), at most kChunkCap per chunk.
-template <int THREADS, int NE>
+// (8 corners of a point; 1 TV vertex), at most kChunkCap per chunk. PAIRED: entries (2p, 2p+1) usually
+// share an owner slice (a point's corners (x, y, z) and (x+1, y, z) hash to h and h ^ (x ^ (x+1)),
+// which differ below bit 13 whenever x < 8191): such a pair takes its two slots with ONE counting
+// atomic — the contended LDS counters are a quarter of the bin pass's time.
+template <int THREADS, int NE, bool PAIRED = false>
 __device__ __forceinline__ void bin_chunk(const HashGradParams& hp, int lvl, int chunk, const uint32_t (&hh)[NE],
                                           const float (&vx)[NE], const float (&vy)[NE], const bool (&on)[NE]) {
     constexpr int CAP = THREADS * NE;
@@ -142,8 +145,22 @@ __device__ __forceinline__ void bin_chunk(const HashGradParams& hp, int lvl, int
     if (threadIdx.x < n_own) s_cnt[threadIdx.x] = 0;
     __syncthreads();
     uint32_t pos[NE];
+    if constexpr (PAIRED) {
+        static_assert(NE % 2 == 0, "pairs");
 #pragma unroll
-    for (int c = 0; c < NE; ++c) pos[c] = on[c] ? atomicAdd(&s_cnt[hh[c] >> hp.slice_log2], 1u) : kSkip;
+        for (int c = 0; c < NE; c += 2) {
+            const uint32_t o0 = hh[c] >> hp.slice_log2, o1 = hh[c + 1] >> hp.slice_log2;
+            const bool same = o0 == o1;
+            const uint32_t n0 = (on[c] ? 1u : 0u) + (on[c + 1] && same ? 1u : 0u);
+            const uint32_t b0 = n0 ? atomicAdd(&s_cnt[on[c] ? o0 : o1], n0) : 0u;
+            const uint32_t b1 = (on[c + 1] && !same) ? atomicAdd(&s_cnt[o1], 1u) : 0u;
+            pos[c] = on[c] ? b0 : kSkip;
+            pos[c + 1] = on[c + 1] ? (same ? b0 + (on[c] ? 1u : 0u) : b1) : kSkip;
+        }
+    } else {
+#pragma unroll
+        for (int c = 0; c < NE; ++c) pos[c] = on[c] ? atomicAdd(&s_cnt[hh[c] >> hp.slice_log2], 1u) : kSkip;
+    }
     __syncthreads();
     if (threadIdx.x < 64) {   // exclusive scan of <= 128 counters in wave 0, two per lane
         const int o0 = 2 * lane, o1 = 2 * lane + 1;
@@ -261,14 +278,19 @@ __global__ void __launch_bounds__(THREADS) hash_encode_bwd_kernel(
     float* tab = hp.dtables[lvl];
     const uint32_t bx = (uint32_t)ax.base, by = (uint32_t)ay.base, bz = (uint32_t)az.base;
     if constexpr (MODE == 3) {
+        // entries in x-pairs: slot 2q + i holds corner 4i + q ((x, y, z) then (x+1, y, z))
         uint32_t hh[8];
         bool on[8];
+        float ex[8], ey[8];
 #pragma unroll
-        for (int c = 0; c < 8; ++c) {
-            hh[c] = spatial_hash3(bx + ((c >> 2) & 1), by + ((c >> 1) & 1), bz + (c & 1), hp.mask);
-            on[c] = emit && (cgx[c] != 0.f || cgy[c] != 0.f);
+        for (int e = 0; e < 8; ++e) {
+            const int c = 4 * (e & 1) + (e >> 1);
+            hh[e] = spatial_hash3(bx + ((c >> 2) & 1), by + ((c >> 1) & 1), bz + (c & 1), hp.mask);
+            ex[e] = cgx[c];
+            ey[e] = cgy[c];
+            on[e] = emit && (ex[e] != 0.f || ey[e] != 0.f);
         }
-        bin_chunk<THREADS, 8>(hp, lvl, hp.chunk_base + (int)blockIdx.x, hh, cgx, cgy, on);
+        bin_chunk<THREADS, 8, true>(hp, lvl, hp.chunk_base + (int)blockIdx.x, hh, ex, ey, on);
     } else {
         __shared__ float s_val[4][64][17];
         __shared__ uint32_t s_h[4][64][9];
