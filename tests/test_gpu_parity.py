@@ -242,12 +242,12 @@ def test_render_end_to_end(nerf, gpu, golden):
 def test_train_step_and_radam(nerf, gpu, golden):
     """Seven reference training iterations (render + losses + backward + RAdam + lr decay).
 
-    The fixture sits at initialisation (tables U(-1e-4, 1e-4)): sigma ~ 1e-4, so alpha =
-    1 - exp(-relu(sigma)*delta) is cancellation-dominated (a ~ 1e-7; one ulp of exp(-a) is ~50 %
-    of alpha) in ANY fp32 implementation, and the CPU reference (Sleef exp) and the GPU (ocml exp)
-    round it differently. Every gradient therefore carries O(1e-3) relative noise at this point;
-    the checks below are at that level: losses 1e-3, MLP grads in norm 2e-2, table-gradient
-    checksums 5e-3, parameters after 7 steps (2 RAdam updates) 1e-3."""
+    F10 is a well-conditioned, trained-like state (tests/golden/make_golden.py: tables U(-0.3, 0.3),
+    the sigma output rows scaled by 60, so sigma ~ O(1-10) and alpha = 1 - exp(-sigma delta) is not
+    cancellation-dominated). Measured on the MI355X (r02an): losses equal to the printed precision,
+    MLP gradients within 2e-5 (fine net) / 9e-7 (coarse) relative in norm, table-gradient checksums
+    within 1e-6, parameters after the 7 steps (2 RAdam updates) within 4e-8 absolute. The bars are
+    ~10x those: losses 1e-5, MLP grads 2e-4, checksums 1e-5, parameters 2e-5 rel + 1e-7 abs."""
     g = golden("f10_train")
     emb = _embedder(nerf, gpu, 1024, closed_form_table(scale=float(g["table_scale"]), salt=3))
     kw = _render_kwargs(nerf, gpu, {**{k.replace("coarse0_", "coarse_T_"): v for k, v in g.items()},
@@ -267,29 +267,29 @@ def test_train_step_and_radam(nerf, gpu, golden):
         loss = l_img + l_img0 + l_sp
         loss.backward()
         if step == 0:
-            np.testing.assert_allclose([l_img.item(), l_img0.item(), loss.item()], g["loss0"][[0, 1, 3]], rtol=1e-3)
-            np.testing.assert_allclose(l_sp.item(), g["loss0"][2], rtol=5e-2)
+            np.testing.assert_allclose([l_img.item(), l_img0.item(), loss.item()], g["loss0"][[0, 1, 3]], rtol=1e-5)
+            np.testing.assert_allclose(l_sp.item(), g["loss0"][2], rtol=1e-4)
             for prefix, net in (("gcoarse_", coarse), ("gfine_", fine)):
                 for k, p in net.named_parameters():
                     want = g[prefix + k.replace(".", "_")]
                     rel = np.linalg.norm(p.grad.cpu().numpy() - want) / np.linalg.norm(want)
-                    assert rel < 2e-2, f"{prefix}{k}: relative grad error {rel:.2e}"
+                    assert rel < 2e-4, f"{prefix}{k}: relative grad error {rel:.2e}"
             for i, e in enumerate(emb.embeddings):
                 gd = e.weight.grad.double()
                 cs = g["gtable_checksum"][i]
-                np.testing.assert_allclose([(gd * gd).sum().item(), gd.abs().sum().item()], cs[1:], rtol=5e-3,
+                np.testing.assert_allclose([(gd * gd).sum().item(), gd.abs().sum().item()], cs[1:], rtol=1e-5,
                                            err_msg=f"level {i}")
-                assert abs(gd.sum().item() - cs[0]) <= 1e-2 * cs[2], f"level {i} gradient sum"
+                assert abs(gd.sum().item() - cs[0]) <= 1e-5 * cs[2], f"level {i} gradient sum"
         opt.step()
         for grp in opt.param_groups:
             grp["lr"] = 5e-4 * (0.1 ** (step / (500 * 1000)))
         losses.append(loss.item())
-    np.testing.assert_allclose(losses, g["losses"], rtol=1e-3)
+    np.testing.assert_allclose(losses, g["losses"], rtol=1e-5)
     for k, p in coarse.named_parameters():
-        np.testing.assert_allclose(p.detach().cpu().numpy(), g["coarse7_" + k.replace(".", "_")], rtol=1e-3, atol=1e-6)
+        np.testing.assert_allclose(p.detach().cpu().numpy(), g["coarse7_" + k.replace(".", "_")], rtol=2e-5, atol=1e-7)
     for i, e in enumerate(emb.embeddings):
         np.testing.assert_allclose(e.weight.detach().cpu().numpy()[g["table_rows"]], g["table_samples"][i],
-                                   rtol=1e-3, atol=1e-7)
+                                   rtol=2e-5, atol=1e-7)
 
 
 def test_radam_vs_oracle(nerf, gpu, oracle):
