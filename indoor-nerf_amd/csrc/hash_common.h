@@ -11,7 +11,37 @@ struct HashParams {
     float bmin[3];
     float bmax[3];
     uint32_t mask;
+    uint32_t fastdiv;                 // fill_cells: the box and cells admit div_rn<true> (below)
 };
+
+// Correctly rounded fp32 n / d. FAST is the core of the compiler's IEEE division sequence
+// (v_rcp, one Newton step on the reciprocal, quotient, two residual corrections) without its
+// v_div_scale / v_div_fmas scaling and v_div_fixup special-case steps (11 -> 8 VALU): those change
+// nothing when n = 0 or 2^-96 <= |n| <= 2^42 and 2^-41 <= d <= 2^41 (no operand or residual
+// leaves the normal range), so FAST returns the bits of n / d there. axis_cell's callers take
+// FAST only when fill_cells accepted the box and cells and every coordinate of the wave passes
+// fastdiv_point_ok, which together bound both numerators and denominators to that range.
+template <bool FAST>
+__device__ __forceinline__ float div_rn(float n, float d) {
+    if constexpr (FAST) {
+        float r = __builtin_amdgcn_rcpf(d);
+        r = fmaf(fmaf(-d, r, 1.0f), r, r);
+        float q = n * r;
+        q = fmaf(fmaf(-d, q, n), r, q);
+        return fmaf(fmaf(-d, q, n), r, q);
+    } else {
+        return n / d;
+    }
+}
+
+// A point admits the fast division when every |coordinate| is in [2^-72, 2^40] (NaN/Inf fail):
+// then x - vmin and clamp(x) - lo are 0 or >= 2^-95 in magnitude (vmin = base * cell + lo is 0
+// or >= 2^-63 given fill_cells' bounds on lo and cell) and both quotients stay normal.
+__device__ __forceinline__ bool fastdiv_point_ok(float x, float y, float z) {
+    const float m = fminf(fminf(fabsf(x), fabsf(y)), fabsf(z));
+    const float s = fabsf(x) + fabsf(y) + fabsf(z);
+    return m >= 0x1p-72f && s <= 0x1p40f;
+}
 
 // Per-axis voxel math of utils.py:103-112, fp32, exact op order.
 struct AxisCell {
@@ -20,25 +50,39 @@ struct AxisCell {
     bool inside;   // x == max(min(x, bmax), bmin)
 };
 
+template <bool FAST = false>
 __device__ __forceinline__ AxisCell axis_cell(float x, float lo, float hi, float cell) {
     AxisCell a;
     a.inside = (x == fmaxf(fminf(x, hi), lo));
-    float xc = fminf(fmaxf(x, lo), hi);            // torch.clamp(min=lo, max=hi)
-    a.base = (int)floorf((xc - lo) / cell);        // floor(...).int()
-    float vmin = (float)a.base * cell + lo;        // bottom_left_idx*grid_size + box_min
-    float vmax = vmin + cell;                      // + 1.0*grid_size
-    a.w = (x - vmin) / (vmax - vmin);
+    float xc = fminf(fmaxf(x, lo), hi);                   // torch.clamp(min=lo, max=hi)
+    a.base = (int)floorf(div_rn<FAST>(xc - lo, cell));    // floor(...).int()
+    float vmin = (float)a.base * cell + lo;               // bottom_left_idx*grid_size + box_min
+    float vmax = vmin + cell;                             // + 1.0*grid_size
+    a.w = div_rn<FAST>(x - vmin, vmax - vmin);
     return a;
 }
 
 // grid_size = (box_max - box_min) / resolution (utils.py:106): the same two fp32 operations,
-// correctly rounded, on the host once per launch instead of per point.
-static void fill_cells(float (*cell)[3], const float* bmin, const float* bmax, const float* res, int n_levels) {
+// correctly rounded, on the host once per launch instead of per point. Returns whether the box and
+// the cells admit div_rn<true>: |box bounds| 0 or in [2^-40, 2^40], cells in [2^-40, 2^40] and at
+// least 2^-16 of the largest |bound| (so vmax - vmin stays within 2^-7 of the cell).
+static bool fill_cells(float (*cell)[3], const float* bmin, const float* bmax, const float* res, int n_levels) {
+    bool ok = true;
+    float big = 0.f;
+    for (int a = 0; a < 3; ++a)
+        for (const float b : {bmin[a], bmax[a]}) {
+            const float m = b < 0.f ? -b : b;
+            ok = ok && (m == 0.f || (m >= 0x1p-40f && m <= 0x1p40f));
+            big = m > big ? m : big;
+        }
     for (int l = 0; l < n_levels; ++l)
         for (int a = 0; a < 3; ++a) {
             const volatile float d = bmax[a] - bmin[a];
             cell[l][a] = d / res[l];
+            const float c = cell[l][a];
+            ok = ok && c >= 0x1p-40f && c <= 0x1p40f && c >= big * 0x1p-16f;
         }
+    return ok;
 }
 
 // ---- A-CAQ quantizer record (quantization.py:144-187), written by nerf_quant_params -------------

@@ -25,6 +25,7 @@ struct HashGradParams {
     float bmin[3];
     float bmax[3];
     uint32_t mask;
+    uint32_t fastdiv;     // fill_cells accepted the box and cells for div_rn<true>
     // binned path (MODE 3): per (level, 256-point chunk) a region of kChunkCap entries sorted by
     // owner slice, plus the slice offsets of each region.
     uint16_t* bin_h;      // entry row within its owner slice
@@ -45,6 +46,30 @@ struct HashGradParams {
 // line for 15 of 16 x, so each gather instruction touches ~32 lines instead of 64 (the vector
 // memory path processes a wave instruction's distinct lines one after another). The x blend
 // c_jk = e(0,j,k)(1-wx) + e(1,j,k)wx becomes a + partner's b (IEEE addition commutes: bit-exact).
+// value of the other lane of the pair (lanes 2m <-> 2m+1): DPP quad_perm [1,0,3,2], no LDS round
+// trip (ds_bpermute)
+__device__ __forceinline__ int pair_swap_i(int v) { return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false); }
+__device__ __forceinline__ float pair_swap(float v) { return __int_as_float(pair_swap_i(__float_as_int(v))); }
+
+// The three axes of a point for lane xb of its pair: both lanes need all three, so lane 0 computes
+// (x, y) and lane 1 (x, z) and they swap the y / z results (4 divisions per lane, not 6).
+template <bool FAST>
+__device__ __forceinline__ void fwd_axes(float x, float y, float z, const HashParams& hp, int lvl, int xb,
+                                         AxisCell& ax, AxisCell& ay, AxisCell& az) {
+    ax = axis_cell<FAST>(x, hp.bmin[0], hp.bmax[0], hp.cell[lvl][0]);
+    const AxisCell a2 = axis_cell<FAST>(xb ? z : y, xb ? hp.bmin[2] : hp.bmin[1], xb ? hp.bmax[2] : hp.bmax[1],
+                                        xb ? hp.cell[lvl][2] : hp.cell[lvl][1]);
+    const int pk = a2.base | (a2.inside ? 0x40000000 : 0);   // 0 <= base <= res < 2^30
+    const int opk = pair_swap_i(pk);
+    const float ow = pair_swap(a2.w);
+    AxisCell o;
+    o.base = opk & 0x3FFFFFFF;
+    o.inside = (opk & 0x40000000) != 0;
+    o.w = ow;
+    ay = xb ? o : a2;
+    az = xb ? a2 : o;
+}
+
 template <bool QUANT>
 __global__ void __launch_bounds__(256) hash_encode_fwd_pair_kernel(
     const float* __restrict__ xyz, int64_t n, HashParams hp,
@@ -57,9 +82,11 @@ __global__ void __launch_bounds__(256) hash_encode_fwd_pair_kernel(
     const bool valid = p < n;
     const int64_t pc = valid ? p : n - 1;             // invalid lanes mirror a valid point (no stores)
     const float x = xyz[3 * pc + 0], y = xyz[3 * pc + 1], z = xyz[3 * pc + 2];
-    const AxisCell ax = axis_cell(x, hp.bmin[0], hp.bmax[0], hp.cell[lvl][0]);
-    const AxisCell ay = axis_cell(y, hp.bmin[1], hp.bmax[1], hp.cell[lvl][1]);
-    const AxisCell az = axis_cell(z, hp.bmin[2], hp.bmax[2], hp.cell[lvl][2]);
+    AxisCell ax, ay, az;
+    if (hp.fastdiv && __ballot(!fastdiv_point_ok(x, y, z)) == 0ull)   // wave-uniform
+        fwd_axes<true>(x, y, z, hp, lvl, xb, ax, ay, az);
+    else
+        fwd_axes<false>(x, y, z, hp, lvl, xb, ax, ay, az);
     const float2* __restrict__ tab = reinterpret_cast<const float2*>(hp.tables[lvl]);
     const uint32_t bx = (uint32_t)ax.base + (uint32_t)xb, by = (uint32_t)ay.base, bz = (uint32_t)az.base;
     float2 e[4];   // corners (xb, j, k), index 2j + k
@@ -79,8 +106,8 @@ __global__ void __launch_bounds__(256) hash_encode_fwd_pair_kernel(
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
         const float ax_ = e[c].x * fx, ay_ = e[c].y * fx;
-        cx[c] = ax_ + __shfl_xor(ax_, 1, 64);
-        cy[c] = ay_ + __shfl_xor(ay_, 1, 64);
+        cx[c] = ax_ + pair_swap(ax_);
+        cy[c] = ay_ + pair_swap(ay_);
     }
     const float oy = 1.0f - wy, oz = 1.0f - wz;
     // c00 = cx[0], c01 = cx[1], c10 = cx[2], c11 = cx[3]
@@ -234,9 +261,16 @@ __global__ void __launch_bounds__(THREADS) hash_encode_bwd_kernel(
         gx = src[0];
         gy = src[1];
     }
-    const AxisCell ax = axis_cell(x, hp.bmin[0], hp.bmax[0], hp.cell[lvl][0]);
-    const AxisCell ay = axis_cell(y, hp.bmin[1], hp.bmax[1], hp.cell[lvl][1]);
-    const AxisCell az = axis_cell(z, hp.bmin[2], hp.bmax[2], hp.cell[lvl][2]);
+    AxisCell ax, ay, az;
+    if (hp.fastdiv && __ballot(valid && !fastdiv_point_ok(x, y, z)) == 0ull) {   // wave-uniform
+        ax = axis_cell<true>(x, hp.bmin[0], hp.bmax[0], hp.cell[lvl][0]);
+        ay = axis_cell<true>(y, hp.bmin[1], hp.bmax[1], hp.cell[lvl][1]);
+        az = axis_cell<true>(z, hp.bmin[2], hp.bmax[2], hp.cell[lvl][2]);
+    } else {
+        ax = axis_cell(x, hp.bmin[0], hp.bmax[0], hp.cell[lvl][0]);
+        ay = axis_cell(y, hp.bmin[1], hp.bmax[1], hp.cell[lvl][1]);
+        az = axis_cell(z, hp.bmin[2], hp.bmax[2], hp.cell[lvl][2]);
+    }
     const float wx = ax.w, wy = ay.w, wz = az.w;
     const float ox = 1.0f - wx, oy = 1.0f - wy, oz = 1.0f - wz;
 
@@ -646,7 +680,7 @@ extern "C" int nerf_hash_encode_fwd_q(const float* d_xyz, int64_t n_points, cons
         hp.tables[l] = d_tables[l];
     }
     for (int a = 0; a < 3; ++a) { hp.bmin[a] = bbox_min3[a]; hp.bmax[a] = bbox_max3[a]; }
-    fill_cells(hp.cell, bbox_min3, bbox_max3, level_res, n_levels);
+    hp.fastdiv = fill_cells(hp.cell, bbox_min3, bbox_max3, level_res, n_levels) ? 1u : 0u;
     hp.mask = (uint32_t)((1u << log2_T) - 1u);
     const QuantRec* q = reinterpret_cast<const QuantRec*>(d_qrec);
     dim3 grid2(blocks_for(2 * n_points, 256), n_levels);
@@ -722,7 +756,7 @@ extern "C" int nerf_hash_encode_bwd_bin(const float* d_xyz, int64_t n_points, co
                  (long long)(chunk_base + nch), (long long)chunk_capacity);
     if (n_points == 0) return NERF_OK;
     for (int a = 0; a < 3; ++a) { hp.bmin[a] = bbox_min3[a]; hp.bmax[a] = bbox_max3[a]; }
-    fill_cells(hp.cell, bbox_min3, bbox_max3, level_res, n_levels);
+    hp.fastdiv = fill_cells(hp.cell, bbox_min3, bbox_max3, level_res, n_levels) ? 1u : 0u;
     hp.chunk_base = (int)chunk_base;
     hp.nchunks = (int)(chunk_base + nch);
     hipLaunchKernelGGL((hash_encode_bwd_kernel<3, kChunkPts>), dim3((unsigned)nch, n_levels), dim3(kChunkPts), 0, as_stream(stream),
@@ -818,7 +852,7 @@ extern "C" int nerf_hash_encode_bwd(const float* d_xyz, int64_t n_points, const 
         hp.dtables[l] = d_dtables[l];
     }
     for (int a = 0; a < 3; ++a) { hp.bmin[a] = bbox_min3[a]; hp.bmax[a] = bbox_max3[a]; }
-    fill_cells(hp.cell, bbox_min3, bbox_max3, level_res, n_levels);
+    hp.fastdiv = fill_cells(hp.cell, bbox_min3, bbox_max3, level_res, n_levels) ? 1u : 0u;
     hp.mask = (uint32_t)((1u << log2_T) - 1u);
     hipLaunchKernelGGL((hash_encode_bwd_kernel<1, 256>), dim3(blocks_for(n_points, 256), n_levels), dim3(256), 0,
                        as_stream(stream), d_xyz, n_points, hp, d_dfeat, feat_stride_point, feat_stride_level);

@@ -84,6 +84,46 @@ def test_hash_encode_large_vs_c_oracle(nerf, gpu):
     np.testing.assert_array_equal(keep.cpu().numpy(), inside)
 
 
+def test_hash_encode_edge_points_vs_c_oracle(nerf, gpu):
+    """Every point bit-exact against the C oracle (IEEE division) where the voxel math is most
+    fragile: points exactly on grid vertices of every level, on and outside the box bounds, zero,
+    subnormal, tiny and huge coordinates, spread over waves and in runs. The kernels' fast division
+    (div_rn<true>, csrc/hash_common.h) serves the waves whose coordinates pass fastdiv_point_ok and
+    the IEEE division the others; both must reproduce utils.py:103-112 bit for bit."""
+    from test_abi import _c_hash
+    table = closed_form_table()
+    emb = _embedder(nerf, gpu, 1024, table)
+    lo, hi = blender_bbox()
+    rng = np.random.RandomState(11)
+    n = 1 << 20
+    x = (lo - 0.3 + (hi - lo + 0.6) * rng.rand(n, 3)).astype(np.float32)
+    res = np.asarray(emb.level_res, np.float32)
+    cell = ((hi.astype(np.float32) - lo.astype(np.float32))[None, :] / res[:, None]).astype(np.float32)   # [L, 3]
+    # grid vertices: base * cell + lo in fp32 (the kernels' vmin), every level, random axes
+    m = n // 4
+    lv = rng.randint(0, len(res), m)
+    k = np.floor(rng.rand(m, 3) * res[lv][:, None]).astype(np.float32)
+    verts = (k * cell[lv] + lo.astype(np.float32)).astype(np.float32)
+    axes = rng.rand(m, 3) < 0.6
+    x[:m][axes] = verts[axes]
+    specials = np.array([0.0, -0.0, 1e-30, -1e-30, 1e-40, 1e-45, 3e-22, 1e30, -1e30, 1e-6, -1e-6],
+                        np.float32)
+    sel = rng.rand(n, 3) < 0.002                                   # scattered: one wave in ~10
+    x[sel] = rng.choice(specials, int(sel.sum()))
+    for a in range(3):                                             # exact box bounds
+        b = rng.rand(n) < 0.01
+        x[b, a] = np.where(rng.rand(int(b.sum())) < 0.5, lo[a], hi[a]).astype(np.float32)
+    x[n - 4096:n - 2048, 1] = 0.0                                   # a run of zero coordinates
+    x[n - 2048:, 2] = 1e-38
+    perm = rng.permutation(n - 4096)
+    x[:n - 4096] = x[perm]
+    with torch.no_grad():
+        feat, keep = emb(torch.from_numpy(x).to(gpu))
+    ref, ref_keep, *_ = _c_hash(x, emb.level_res, table)
+    np.testing.assert_array_equal(feat.cpu().numpy(), ref)
+    np.testing.assert_array_equal(keep.cpu().numpy(), ref_keep)
+
+
 def test_sh4_bit_exact(nerf, gpu, golden):
     g = golden("f5_sh")
     with torch.no_grad():
