@@ -75,10 +75,15 @@ __global__ void __launch_bounds__(256) hash_encode_fwd_pair_kernel(
     const float* __restrict__ xyz, int64_t n, HashParams hp,
     float* __restrict__ feat, int64_t sp, int64_t sl, uint8_t* __restrict__ keep,
     const QuantRec* __restrict__ qrec) {
+#ifdef NERF_AB_FWD_POINT_MAJOR   // A/B only: all levels of a point block dispatched together
+    const int64_t t = (int64_t)blockIdx.y * blockDim.x + threadIdx.x;
+    const int lvl = blockIdx.x;
+#else
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int lvl = blockIdx.y;
+#endif
     const int64_t p = t >> 1;
     const int xb = (int)(t & 1);
-    const int lvl = blockIdx.y;
     const bool valid = p < n;
     const int64_t pc = valid ? p : n - 1;             // invalid lanes mirror a valid point (no stores)
     const float x = xyz[3 * pc + 0], y = xyz[3 * pc + 1], z = xyz[3 * pc + 2];
@@ -683,7 +688,11 @@ extern "C" int nerf_hash_encode_fwd_q(const float* d_xyz, int64_t n_points, cons
     hp.fastdiv = fill_cells(hp.cell, bbox_min3, bbox_max3, level_res, n_levels) ? 1u : 0u;
     hp.mask = (uint32_t)((1u << log2_T) - 1u);
     const QuantRec* q = reinterpret_cast<const QuantRec*>(d_qrec);
+#ifdef NERF_AB_FWD_POINT_MAJOR
+    dim3 grid2(n_levels, blocks_for(2 * n_points, 256));
+#else
     dim3 grid2(blocks_for(2 * n_points, 256), n_levels);
+#endif
     if (q)
         hipLaunchKernelGGL(hash_encode_fwd_pair_kernel<true>, grid2, dim3(256), 0, as_stream(stream), d_xyz,
                            n_points, hp, d_feat, feat_stride_point, feat_stride_level, d_keep, q);
