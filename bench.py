@@ -102,8 +102,12 @@ def pmc_traffic(abi_name):
 
 def gpu_clocks():
     """Current shader / memory clocks of the visible GPUs (rocm-smi, a child process), so that a
-    box-to-box spread in the bench line can be told apart from a code regression."""
+    box-to-box spread in the bench line can be told apart from a code regression. Skipped under
+    rocprofv3: its preloaded library would start in the child too (rocm-smi is a script that execs
+    its interpreter after that library has initialised the GPU)."""
     import subprocess
+    if any(k.startswith("ROCPROF") for k in os.environ):
+        return None
     try:
         r = subprocess.run(["rocm-smi", "--showclocks", "--json"], capture_output=True, text=True, timeout=20)
         d = json.loads(r.stdout)
@@ -317,7 +321,8 @@ def main():
     params = grad_vars + list(kw["embed_fn"].parameters())
     nerf.broadcast_params(params)
     zero = world > 1 and a.zero and a.mode == "train"
-    arena = nerf.GradArena(params, pad_to=world * 64 if zero else 1)
+    # defer_tables: no memset of the 64 MiB of table gradients; the owner pass overwrites them
+    arena = nerf.GradArena(params, pad_to=world * 64 if zero else 1, defer_tables=True)
     rays = (torch.from_numpy(ro).to(dev), torch.from_numpy(rd).to(dev))
     if strong:
         target = nerf.shard(torch.rand(a.rays, 3, device=dev, generator=torch.Generator(device=dev).manual_seed(0)),

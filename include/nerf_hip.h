@@ -109,7 +109,13 @@ int nerf_hash_encode_bwd_ws(const float* d_xyz, int64_t n_points,
  * log2_T, C * chunk_capacity, deterministic)); a bin call writes its ceil(n_points / C) chunks from
  * chunk_base on, and the owner call sums chunks
  * [0, n_chunks) into d_dtables (ACCUMULATED). Calls sharing a workspace must be stream-ordered and
- * use the same n_levels, log2_T, chunk_capacity and deterministic. */
+ * use the same n_levels, log2_T, chunk_capacity and deterministic.
+ * The owner's `deterministic` argument is a bit set: bit 0 = deterministic (as above), bit 1 =
+ * NERF_OWNER_OVERWRITE: the tables' prior contents are ignored and every row of all n_levels
+ * tables is STORED (its sum, or 0 where no entry lands), also when n_chunks == 0 — the result of
+ * zeroing the gradients and accumulating, bit for bit, without the memset and without the owner's
+ * row loads (the caller promises the gradients are logically zero: GradArena's deferred zero). */
+#define NERF_OWNER_OVERWRITE 2
 #ifndef NERF_HASH_CHUNK_POINTS
 #define NERF_HASH_CHUNK_POINTS 512
 #endif

@@ -178,6 +178,7 @@ static int fill_tv(TVParams& P, int n_levels, int log2_T, const int64_t* min_ver
         const int64_t n1 = cube[l] + 1;
         P.vstart[l + 1] = P.vstart[l] + n1 * n1 * n1;
     }
+
     return NERF_OK;
 }
 

@@ -37,6 +37,7 @@ struct HashGradParams {
     int slice_log2;       // owner slice = 2^slice_log2 rows (LDS: 16 B per row, 32 B deterministic)
     int owner_log2;       // owners per level = 2^owner_log2
     float* chunk_max;     // deterministic mode: [L][chunk_stride] max |entry| of each chunk, else null
+    int overwrite;        // owner pass: store every row (the gradients are logically zero), no loads
 };
 
 // QUANT: every gathered corner feature goes through the level's A-CAQ quantizer first
@@ -614,10 +615,19 @@ __global__ void __launch_bounds__(THREADS) hash_bwd_owner_kernel(HashGradParams 
         };
         for (int i = tid; i < S; i += kOwnerThreads) {
             const double vx = fixed(i, 0), vy = fixed(i, 1);
-            if (vx != 0.0 || vy != 0.0) {
+            if (hp.overwrite) {
+                dt[i] = make_float2((float)vx, (float)vy);   // == (float)(0.0 + v), and +0 where v == 0
+            } else if (vx != 0.0 || vy != 0.0) {
                 const float2 t = dt[i];
                 dt[i] = make_float2((float)((double)t.x + vx), (float)((double)t.y + vy));
             }
+        }
+        return;
+    }
+    if (hp.overwrite) {   // rows without entries become +0, as after a memset
+        for (int i = tid; i < S; i += kOwnerThreads) {
+            const double2 v = s_slice[i];
+            dt[i] = make_float2((float)v.x, (float)v.y);
         }
         return;
     }
@@ -821,10 +831,14 @@ extern "C" int nerf_tv_bwd_bin(const float* const* d_tables, int n_levels, int l
 extern "C" int nerf_hash_encode_bwd_owner(int n_levels, int log2_T, int64_t n_chunks, int64_t chunk_capacity,
                                           float* const* d_dtables, int deterministic, void* d_workspace,
                                           size_t workspace_bytes, void* stream) {
+    NERF_REQUIRE((deterministic & ~(1 | NERF_OWNER_OVERWRITE)) == 0, "hash_encode_bwd_owner: flags %d", deterministic);
+    const bool overwrite = (deterministic & NERF_OWNER_OVERWRITE) != 0;
+    deterministic &= 1;
     HashGradParams hp{};
     const int rc = bin_layout("hash_encode_bwd_owner", n_levels, log2_T, chunk_capacity, deterministic, d_workspace,
                               workspace_bytes, hp);
     if (rc) return rc;
+    hp.overwrite = overwrite ? 1 : 0;
     NERF_REQUIRE(n_chunks >= 0 && n_chunks <= chunk_capacity, "hash_encode_bwd_owner: n_chunks %lld of %lld",
                  (long long)n_chunks, (long long)chunk_capacity);
     NERF_REQUIRE(d_dtables, "hash_encode_bwd_owner: null grad tables");
@@ -832,7 +846,7 @@ extern "C" int nerf_hash_encode_bwd_owner(int n_levels, int log2_T, int64_t n_ch
         NERF_REQUIRE(d_dtables[l], "hash_encode_bwd_owner: grad table %d is null", l);
         hp.dtables[l] = d_dtables[l];
     }
-    if (n_chunks == 0) return NERF_OK;
+    if (n_chunks == 0 && !overwrite) return NERF_OK;
     hp.nchunks = (int)n_chunks;
     const dim3 grid(1u << hp.owner_log2, n_levels);
     if (deterministic)

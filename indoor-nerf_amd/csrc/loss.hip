@@ -38,20 +38,46 @@ struct LossArgs {
 __global__ void __launch_bounds__(kLossThreads) train_loss_fwd_kernel(LossArgs a) {
     __shared__ double s_red4[4][kLossThreads / 64];
     double se = 0.0, se0 = 0.0, ssp = 0.0, ssp0 = 0.0;
-    // unrolled for load ILP; each thread still adds its elements in index order
-#pragma unroll 4
-    for (int64_t i = threadIdx.x; i < a.n_rgb; i += kLossThreads) {
-        const float t = a.target[i];
-        const float d = a.rgb[i] - t;
-        se += (double)(d * d);
-        if (a.rgb0) {
-            const float d0 = a.rgb0[i] - t;
-            se0 += (double)(d0 * d0);
+    // every load of a round is issued before the first add (one memory round trip per round: the
+    // lego batch, 12,288 colour values + 4,096 sparsity values, is one round); each thread still
+    // adds its elements in index order, so the sums are those of the plain strided loops
+    constexpr int UR = 16, US = 4;
+    for (int64_t i0 = threadIdx.x, j0 = threadIdx.x; i0 < a.n_rgb || j0 < a.n_sp;
+         i0 += UR * kLossThreads, j0 += US * kLossThreads) {
+        float t[UR], r[UR], r0[UR], s[US], s0[US];
+#pragma unroll
+        for (int u = 0; u < UR; ++u) {
+            const int64_t i = i0 + (int64_t)u * kLossThreads;
+            const bool ok = i < a.n_rgb;
+            t[u] = ok ? a.target[i] : 0.f;
+            r[u] = ok ? a.rgb[i] : 0.f;
+            r0[u] = (ok && a.rgb0) ? a.rgb0[i] : 0.f;
         }
-    }
-    for (int64_t i = threadIdx.x; i < a.n_sp; i += kLossThreads) {
-        if (a.sp) ssp += (double)a.sp[i];
-        if (a.sp0) ssp0 += (double)a.sp0[i];
+#pragma unroll
+        for (int u = 0; u < US; ++u) {
+            const int64_t j = j0 + (int64_t)u * kLossThreads;
+            const bool ok = j < a.n_sp;
+            s[u] = (ok && a.sp) ? a.sp[j] : 0.f;
+            s0[u] = (ok && a.sp0) ? a.sp0[j] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < UR; ++u) {
+            if (i0 + (int64_t)u * kLossThreads < a.n_rgb) {
+                const float d = r[u] - t[u];
+                se += (double)(d * d);
+                if (a.rgb0) {
+                    const float d0 = r0[u] - t[u];
+                    se0 += (double)(d0 * d0);
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < US; ++u) {
+            if (j0 + (int64_t)u * kLossThreads < a.n_sp) {
+                if (a.sp) ssp += (double)s[u];
+                if (a.sp0) ssp0 += (double)s0[u];
+            }
+        }
     }
     // the four block sums share one barrier: wave sums, then thread 0 adds the waves' partials in
     // wave order (one barrier instead of two per sum)

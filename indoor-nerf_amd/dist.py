@@ -53,7 +53,7 @@ class GradArena:
     the buffer up to a multiple of this many elements (the sharded optimizer needs world x _ALIGN)
     — the gaps and the tail are never a gradient and stay zero."""
 
-    def __init__(self, params, pad_to=1):
+    def __init__(self, params, pad_to=1, defer_tables=False):
         # quantizer scalars (soft_bits, range_scale, v_max) never receive a gradient in the
         # reference (their uses are detached): they keep grad None, so the optimizer skips them
         self.params = [p for p in params if p.requires_grad and not getattr(p, "_nerf_no_grad", False)]
@@ -66,6 +66,16 @@ class GradArena:
         dev = self.params[0].device
         self.flat = torch.zeros(total, device=dev, dtype=torch.float32)
         self.views = [self.flat[o:o + p.numel()].view_as(p) for p, o in zip(self.params, self.offsets)]
+        # defer_tables: the hash tables' gradients (a trailing run of the arena) are not memset by
+        # zero_(); the iteration's owner pass overwrites them (hashgrid.defer_zero)
+        self.deferred, self.zero_end = [], self.flat.numel()
+        if defer_tables:
+            tail = len(self.params)
+            while tail > 0 and getattr(self.params[tail - 1], "_nerf_owner_grad", False):
+                tail -= 1
+            if tail < len(self.params):
+                self.deferred = self.views[tail:]
+                self.zero_end = self.offsets[tail]
         self.attach()
 
     def attach(self):
@@ -73,7 +83,12 @@ class GradArena:
             p.grad = v
 
     def zero_(self):
-        self.flat.zero_()
+        if self.deferred:
+            from .hashgrid import defer_zero
+            self.flat[:self.zero_end].zero_()
+            defer_zero(self.deferred)
+        else:
+            self.flat.zero_()
         self.attach()
 
     def allreduce_mean(self, group=None):

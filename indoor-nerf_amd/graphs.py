@@ -105,7 +105,7 @@ class GraphedTrainStep:
         if zero_grad is None:
             # gradients must live at fixed addresses across replays: one flat arena, zeroed in place
             from .dist import GradArena
-            arena = GradArena([p for g in optimizer.param_groups for p in g["params"]])
+            arena = GradArena([p for g in optimizer.param_groups for p in g["params"]], defer_tables=True)
             zero_grad = arena.zero_
         self.hook, self.scale_sp, self.tv_gen, self.zero_grad = grad_hook, loss_scale_sparsity, tv_generator, zero_grad
         self.post_hook = post_hook
@@ -149,15 +149,22 @@ class GraphedTrainStep:
         side = torch.cuda.Stream(device=dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         pool = torch.cuda.graph_pool_handle()
-        g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        # without a gradient hook between them (one process) the update joins the first graph: one
+        # graph launch per iteration (a second launch left the GPU idle ~9 us between them)
+        single = self.hook is None
+        g1 = torch.cuda.CUDAGraph()
+        g2 = None if single else torch.cuda.CUDAGraph()
         with torch.cuda.stream(side):
             with capturing(sc):
                 with torch.cuda.graph(g1, pool=pool, stream=side):
                     out = forward_backward(self.rays, self.target, self.kw, self.opt, self.args, global_step,
                                            H=self.H, W=self.W, K=self.K, loss_scale_sparsity=self.scale_sp,
                                            tv_generator=self.tv_gen, zero_grad=self.zero_grad, schedule=False)
-                with torch.cuda.graph(g2, pool=pool, stream=side):
-                    optimizer_update(self.opt)
+                    if single:
+                        optimizer_update(self.opt)
+                if not single:
+                    with torch.cuda.graph(g2, pool=pool, stream=side):
+                        optimizer_update(self.opt)
         torch.cuda.current_stream(dev).wait_stream(side)
         emb.current_step = step0
         self.graphs = (g1, g2)
@@ -203,7 +210,8 @@ class GraphedTrainStep:
             emb.current_step += self._n_forwards()
         if self.hook is not None:
             self.hook()
-        self.graphs[1].replay()
+        if self.graphs[1] is not None:
+            self.graphs[1].replay()
         for p in self.params:              # the replayed RAdam wrote the parameters in place
             torch.autograd.graph.increment_version(p)
         if self.post_hook is not None:

@@ -27,6 +27,38 @@ def _bbox_floats(bounding_box):
     return [float(v) for v in lo], [float(v) for v in hi]
 
 
+# Deferred zero of hash-table gradients (GradArena(defer_tables=True).zero_): instead of a 64 MiB
+# memset before the step, the iteration's binned owner pass STORES every table row
+# (NERF_OWNER_OVERWRITE: the same bits as memset + accumulate, minus the memset and the owner's row
+# loads). A deferred gradient's contents are stale until then; any other writer or reader
+# materialises the zero first (materialize_zero), and train steps do so for whatever is still
+# deferred after backward().
+_DEFERRED = {}   # data_ptr -> gradient tensor
+
+
+def defer_zero(grads):
+    for g in grads:
+        _DEFERRED[g.data_ptr()] = g
+
+
+def materialize_zero(grads=None):
+    """Zero deferred gradients now: the given ones (those of them that are deferred), or all."""
+    keys = list(_DEFERRED) if grads is None else [g.data_ptr() for g in grads if g.data_ptr() in _DEFERRED]
+    for k in keys:
+        _DEFERRED.pop(k).zero_()
+
+
+def take_deferred(grads):
+    """True (and no longer deferred) when every gradient of an owner launch is deferred: the launch
+    overwrites them. Otherwise any deferred ones among them are zeroed now and the launch adds."""
+    if grads and all(g.data_ptr() in _DEFERRED for g in grads):
+        for g in grads:
+            del _DEFERRED[g.data_ptr()]
+        return True
+    materialize_zero(grads)
+    return False
+
+
 def accumulate_grad_buffers(params):
     """The fused backward kernels ACCUMULATE straight into .grad (like a fused optimizer's bucket):
     create zero grads where they are missing and return them."""
@@ -131,8 +163,9 @@ class _PendingBins:
             return
         L, log2_T, _, det = self.tag
         with torch.cuda.stream(self.stream):
+            flags = det | (OWNER_OVERWRITE if take_deferred(self.grads) else 0)
             _lib.call("nerf_hash_encode_bwd_owner", L, log2_T, self.used, self.cap,
-                      _lib.ptr_array(self.grads, "grad_tables"), det, _lib.ptr(self.ws, "workspace", dtype=torch.uint8),
+                      _lib.ptr_array(self.grads, "grad_tables"), flags, _lib.ptr(self.ws, "workspace", dtype=torch.uint8),
                       self.ws.numel(), _lib.stream())
         cur = torch.cuda.current_stream()
         if cur != self.stream:
@@ -195,6 +228,7 @@ def bin_chunks(n_points):
 
 
 _PENDING = {}
+OWNER_OVERWRITE = 2   # include/nerf_hip.h NERF_OWNER_OVERWRITE
 
 
 def pending_bins(device):
@@ -213,6 +247,7 @@ def hash_encode_bwd(xyz, meta, dfeat, sp, sl, grad_tables, defer=None, queue=Tru
     if defer and P > 0 and int(_lib.load().nerf_hash_encode_bwd_workspace_bytes(L, log2_T, P, det)) > 0:
         pending_bins(xyz.device).add(xyz, meta, dfeat, sp, sl, grad_tables, queue=queue)
         return
+    materialize_zero(grad_tables)
     ws, nbytes = bwd_workspace(len(grad_tables), meta["log2_T"], xyz.shape[0], xyz.device)
     _lib.call("nerf_hash_encode_bwd_ws", _lib.ptr(xyz, "xyz"), xyz.shape[0], meta["bmin"], meta["bmax"],
               meta["res"], len(grad_tables), meta["log2_T"], _lib.ptr(dfeat, "grad_feat"), sp, sl,
@@ -246,6 +281,7 @@ class HashEmbedder(nn.Module):
                                          for _ in range(n_levels)])
         for emb in self.embeddings:
             nn.init.uniform_(emb.weight, a=-0.0001, b=0.0001)
+            emb.weight._nerf_owner_grad = True   # every backward into it ends in an owner pass
         # A-CAQ (hash_encoding.py:37-53): one asymmetric learned-bitwidth quantizer per level,
         # registered after the tables as in the reference (parameter order = optimizer state order)
         self.quantizers = nn.ModuleList([

@@ -68,6 +68,7 @@ class TVFn(torch.autograd.Function):
             else:
                 if det:
                     raise NotImplementedError(f"deterministic TV backward: no binned path for log2_T {ctx.log2_T}")
+                hashgrid.materialize_zero(grads)
                 _lib.call("nerf_tv_bwd", _lib.ptr_array(tables), L, ctx.log2_T, ctx.mv, ctx.dmv, ctx.cb,
                           _lib.ptr(g, "grad_loss"), _lib.ptr_array(grads, "grad_tables"), _lib.stream())
         return (None, None, None) + (None,) * len(tables)

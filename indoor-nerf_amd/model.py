@@ -15,7 +15,7 @@ from .hashgrid import HashEmbedder, SHEncoder
 from .losses import total_variation_all, train_loss
 from .optim import RAdam
 from .render import render
-from . import _lib
+from . import _lib, hashgrid
 
 DEFAULTS = dict(multires=10, i_embed=1, i_embed_views=2, multires_views=4, use_viewdirs=True, N_importance=0,
                 N_samples=64, netchunk=1024 * 64, finest_res=512, log2_hashmap_size=19, lrate=5e-4,
@@ -181,6 +181,7 @@ def forward_backward(batch_rays, target_s, render_kwargs_train, optimizer, args,
     if get("use_structural_priors") and global_step >= get("structural_loss_start_iter"):
         loss = loss + structural_loss(depth, extras, args, global_step, spatial_coords)
     loss.backward(_unit_seed(loss))
+    hashgrid.materialize_zero()   # table gradients whose deferred zero no owner pass consumed
     return loss, img_loss, psnr
 
 

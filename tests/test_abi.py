@@ -41,6 +41,8 @@ def test_error_path_reports_message(nerf):
         L.call("nerf_hash_encode_bwd_owner", 16, 19, 5, 4, None, 0, fake, need, None)
     with pytest.raises(RuntimeError, match="workspace"):
         L.call("nerf_hash_encode_bwd_owner", 16, 19, 4, 4, None, 0, fake, need - 1, None)
+    with pytest.raises(RuntimeError, match="flags 4"):   # bit 0 deterministic, bit 1 overwrite, nothing else
+        L.call("nerf_hash_encode_bwd_owner", 16, 19, 4, 4, None, 4, fake, need, None)
     with pytest.raises(RuntimeError, match="exceed the capacity"):
         L.call("nerf_hash_encode_bwd_bin", fake, 3 * C + 1, L.host_f32([0] * 3), L.host_f32([1] * 3),
                L.host_f32([16] * 16), 16, 19, fake, 32, 2, 1, 4, 0, fake, need, None)

@@ -157,6 +157,52 @@ def test_train_iteration_bitwise_reproducible(nerf, gpu):
         assert float((x - y).norm()) <= 1e-3 * float(y.norm()) + 1e-12
 
 
+def test_deferred_table_zero_bitwise(nerf, gpu):
+    """GradArena(defer_tables=True): the tables' memset is skipped and the iteration's owner pass
+    stores every row (NERF_OWNER_OVERWRITE). Deterministic mode, so the comparison is bitwise: the
+    gradients equal the memset + accumulate path's, stale table gradients do not leak in, and a
+    second backward without zeroing still accumulates."""
+    from indoor_nerf_amd import model
+    from indoor_nerf_amd.dist import GradArena
+    lo, hi = blender_bbox()
+    args = nerf.make_args(bounding_box=(torch.from_numpy(lo), torch.from_numpy(hi)), finest_res=1024, N_samples=64,
+                          N_importance=128, white_bkgd=True, tv_loss_weight=1e-6)
+    torch.manual_seed(0)
+    kw, _, _, grad_vars, opt = nerf.create_nerf(args, device=gpu)
+    kw.update(near=2.0, far=6.0, pytest=True)
+    with torch.no_grad():
+        tab = closed_form_table(scale=0.2, salt=4)
+        for i, e in enumerate(kw["embed_fn"].embeddings):
+            e.weight.copy_(torch.from_numpy(tab[i]))
+    ro, rd = synthetic_rays(2048, seed=13)
+    rays = (torch.from_numpy(ro).to(gpu), torch.from_numpy(rd).to(gpu))
+    target = torch.rand(2048, 3, device=gpu, generator=torch.Generator(device=gpu).manual_seed(4))
+    params = [p for g in opt.param_groups for p in g["params"]]
+
+    def grads(defer, passes):
+        arena = GradArena(params, defer_tables=defer)
+        arena.flat.fill_(7.0)             # stale gradients everywhere
+        assert (len(arena.deferred) == 16) == defer
+        arena.zero_()
+        for _ in range(passes):
+            model.forward_backward(rays, target, kw, opt, args, 1, tv_generator=torch.Generator().manual_seed(5),
+                                   zero_grad=lambda: None)
+        torch.cuda.synchronize()
+        return [p.grad.clone() for p in params]
+
+    nerf.set_deterministic(True)
+    try:
+        ref, got = grads(False, 1), grads(True, 1)
+        ref2, got2 = grads(False, 2), grads(True, 2)
+    finally:
+        nerf.set_deterministic(False)
+    from indoor_nerf_amd import hashgrid
+    assert not hashgrid._DEFERRED
+    for i, (x, y) in enumerate(zip(ref + ref2, got + got2)):
+        assert torch.equal(x, y), f"gradient {i % len(params)} differs ({'two passes' if i >= len(params) else 'one pass'})"
+    assert any(bool(g.any()) for g in got[-16:])
+
+
 def test_check_numerics_flags_nan_and_inf(nerf, gpu):
     t = {"rgb_map": torch.rand(4096, 3, device=gpu), "depth_map": torch.rand(4096, device=gpu),
          "acc_map": torch.rand(1000, device=gpu), "weights": torch.zeros(0, device=gpu)}
