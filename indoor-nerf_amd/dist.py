@@ -28,8 +28,8 @@ def init_process_group(backend=None):
     if backend is None:
         # NERF_DIST_BACKEND=gloo: rehearse the multi-rank path on one GPU (ranks share cuda:0)
         backend = os.environ.get("NERF_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
-    if backend == "nccl":
-        torch.cuda.set_device(local)
+    if backend == "nccl":   # ranks beyond the visible GPUs (one-GPU rehearsals) wrap around
+        torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
     dist.init_process_group(backend=backend, rank=rank, world_size=world)
     return rank, world, local
 
