@@ -8,9 +8,10 @@
 // in one thread, with the reference's op order and no contraction (-ffp-contract=off), so indices,
 // keep mask and features are bit-identical to the fp32 reference.
 //
-// Launch geometry: grid (ceil(P/256), L). Blocks are dispatched x-fastest, so at any moment the
-// whole chip works on one or two levels and each XCD's 4 MiB L2 holds the level's table lines
-// that the current point range touches (tables are 4 MiB per level at log2_T = 19).
+// Launch geometry: grid (ceil(P/128), 1 + L - G): row 0 runs the G coarse levels of its points
+// (hash_encode_fwd_pair_kernel), every other row one level. Blocks are dispatched x-fastest, so at
+// any moment the whole chip works on one or two levels and each XCD's 4 MiB L2 holds the level's
+// table lines that the current point range touches (tables are 4 MiB per level at log2_T = 19).
 #include <stdlib.h>
 
 #include <algorithm>
@@ -71,47 +72,45 @@ __device__ __forceinline__ void fwd_axes(float x, float y, float z, const HashPa
     az = xb ? a2 : o;
 }
 
-template <bool QUANT>
-__global__ void __launch_bounds__(256) hash_encode_fwd_pair_kernel(
-    const float* __restrict__ xyz, int64_t n, HashParams hp,
-    float* __restrict__ feat, int64_t sp, int64_t sl, uint8_t* __restrict__ keep,
-    const QuantRec* __restrict__ qrec) {
-#ifdef NERF_AB_FWD_POINT_MAJOR   // A/B only: all levels of a point block dispatched together
-    const int64_t t = (int64_t)blockIdx.y * blockDim.x + threadIdx.x;
-    const int lvl = blockIdx.x;
-#else
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int lvl = blockIdx.y;
-#endif
-    const int64_t p = t >> 1;
-    const int xb = (int)(t & 1);
-    const bool valid = p < n;
-    const int64_t pc = valid ? p : n - 1;             // invalid lanes mirror a valid point (no stores)
-    const float x = xyz[3 * pc + 0], y = xyz[3 * pc + 1], z = xyz[3 * pc + 2];
+// One (point, level) of a lane pair: the axes and the four gathers are issued first (fwd_gather),
+// the blend and the store follow (fwd_finish), so a thread can keep several levels' gathers in flight.
+struct FwdLvl {
+    float wx, wy, wz;
+    bool inside;
+    float2 e[4];   // corners (xb, j, k), index 2j + k
+};
+
+template <bool FAST>
+__device__ __forceinline__ void fwd_gather(float x, float y, float z, const HashParams& hp, int lvl, int xb,
+                                           FwdLvl& s) {
     AxisCell ax, ay, az;
-    if (hp.fastdiv && __ballot(!fastdiv_point_ok(x, y, z)) == 0ull)   // wave-uniform
-        fwd_axes<true>(x, y, z, hp, lvl, xb, ax, ay, az);
-    else
-        fwd_axes<false>(x, y, z, hp, lvl, xb, ax, ay, az);
+    fwd_axes<FAST>(x, y, z, hp, lvl, xb, ax, ay, az);
+    s.wx = ax.w; s.wy = ay.w; s.wz = az.w;
+    s.inside = ax.inside && ay.inside && az.inside;
     const float2* __restrict__ tab = reinterpret_cast<const float2*>(hp.tables[lvl]);
     const uint32_t bx = (uint32_t)ax.base + (uint32_t)xb, by = (uint32_t)ay.base, bz = (uint32_t)az.base;
-    float2 e[4];   // corners (xb, j, k), index 2j + k
 #pragma unroll
-    for (int c = 0; c < 4; ++c) e[c] = tab[spatial_hash3(bx, by + ((c >> 1) & 1), bz + (c & 1), hp.mask)];
+    for (int c = 0; c < 4; ++c) s.e[c] = tab[spatial_hash3(bx, by + ((c >> 1) & 1), bz + (c & 1), hp.mask)];
+}
+
+template <bool QUANT>
+__device__ __forceinline__ void fwd_finish(FwdLvl& s, int lvl, int xb, bool valid, int64_t p,
+                                           float* __restrict__ feat, int64_t sp, int64_t sl,
+                                           uint8_t* __restrict__ keep, const QuantRec* __restrict__ qrec) {
     if constexpr (QUANT) {
         const QuantRec q = qrec[lvl];
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-            e[c].x = fake_quant(e[c].x, q);
-            e[c].y = fake_quant(e[c].y, q);
+            s.e[c].x = fake_quant(s.e[c].x, q);
+            s.e[c].y = fake_quant(s.e[c].y, q);
         }
     }
-    const float wx = ax.w, wy = ay.w, wz = az.w;
+    const float wx = s.wx, wy = s.wy, wz = s.wz;
     const float fx = xb ? wx : 1.0f - wx;
     float cx[4], cy[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-        const float ax_ = e[c].x * fx, ay_ = e[c].y * fx;
+        const float ax_ = s.e[c].x * fx, ay_ = s.e[c].y * fx;
         cx[c] = ax_ + pair_swap(ax_);
         cy[c] = ay_ + pair_swap(ay_);
     }
@@ -121,9 +120,58 @@ __global__ void __launch_bounds__(256) hash_encode_fwd_pair_kernel(
     const float c0y = cy[0] * oy + cy[2] * wy, c1y = cy[1] * oy + cy[3] * wy;
     const float ox_ = c0x * oz + c1x * wz, oy_ = c0y * oz + c1y * wz;
     if (!valid) return;
-    if (lvl == 0 && keep && xb == 0) keep[p] = (ax.inside && ay.inside && az.inside) ? 1 : 0;
+    if (lvl == 0 && keep && xb == 0) keep[p] = s.inside ? 1 : 0;
     float* dst = feat + p * sp + (int64_t)lvl * sl;
     dst[xb] = xb ? oy_ : ox_;
+}
+
+// Grouped coarse levels: blockIdx.y == 0 runs levels [0, group) of its points, two levels' gathers
+// in flight at a time; the other rows run one level each (level-major: one table hot in each XCD's
+// L2). A coarse level alone is latency-bound (few, hot table lines; a single round trip per wave per
+// level): grouping the 6 coarse levels of the lego config took the forward from 121 to 107 us per
+// launch (same box; 3 or 6 levels in flight: 114 / 154 us, the registers cost occupancy).
+constexpr int kFwdGroupRound = 2;
+constexpr int kFwdGroupMax = 8;
+
+template <bool QUANT>
+__global__ void __launch_bounds__(256) hash_encode_fwd_pair_kernel(
+    const float* __restrict__ xyz, int64_t n, HashParams hp, int group,
+    float* __restrict__ feat, int64_t sp, int64_t sl, uint8_t* __restrict__ keep,
+    const QuantRec* __restrict__ qrec) {
+#ifdef NERF_AB_FWD_POINT_MAJOR   // A/B only: all levels of a point block dispatched together
+    const int64_t t = (int64_t)blockIdx.y * blockDim.x + threadIdx.x;
+    const int row = blockIdx.x;
+#else
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int row = blockIdx.y;
+#endif
+    const int64_t p = t >> 1;
+    const int xb = (int)(t & 1);
+    const bool valid = p < n;
+    const int64_t pc = valid ? p : n - 1;             // invalid lanes mirror a valid point (no stores)
+    const float x = xyz[3 * pc + 0], y = xyz[3 * pc + 1], z = xyz[3 * pc + 2];
+    const bool fast = hp.fastdiv && __ballot(!fastdiv_point_ok(x, y, z)) == 0ull;   // wave-uniform
+    if (group > 0 && row == 0) {
+        for (int l0 = 0; l0 < group; l0 += kFwdGroupRound) {
+            FwdLvl s[kFwdGroupRound];
+#pragma unroll
+            for (int g = 0; g < kFwdGroupRound; ++g) {
+                if (l0 + g < group) {
+                    if (fast) fwd_gather<true>(x, y, z, hp, l0 + g, xb, s[g]);
+                    else fwd_gather<false>(x, y, z, hp, l0 + g, xb, s[g]);
+                }
+            }
+#pragma unroll
+            for (int g = 0; g < kFwdGroupRound; ++g)
+                if (l0 + g < group) fwd_finish<QUANT>(s[g], l0 + g, xb, valid, p, feat, sp, sl, keep, qrec);
+        }
+        return;
+    }
+    const int lvl = group > 0 ? group + row - 1 : row;
+    FwdLvl s;
+    if (fast) fwd_gather<true>(x, y, z, hp, lvl, xb, s);
+    else fwd_gather<false>(x, y, z, hp, lvl, xb, s);
+    fwd_finish<QUANT>(s, lvl, xb, valid, p, feat, sp, sl, keep, qrec);
 }
 
 // Backward: dL/de_c = ((g*(1-wz or wz))*(1-wy or wy))*(1-wx or wx), the order autograd applies the
@@ -698,17 +746,29 @@ extern "C" int nerf_hash_encode_fwd_q(const float* d_xyz, int64_t n_points, cons
     hp.fastdiv = fill_cells(hp.cell, bbox_min3, bbox_max3, level_res, n_levels) ? 1u : 0u;
     hp.mask = (uint32_t)((1u << log2_T) - 1u);
     const QuantRec* q = reinterpret_cast<const QuantRec*>(d_qrec);
+    // coarse levels grouped into one grid row: the leading levels whose (res + 1)^3 vertices fit the
+    // table (no hash collisions, a small set of hot lines)
+    int group = 0;
+#ifndef NERF_AB_FWD_NO_GROUP   // A/B only: every level in its own grid row
+    while (group < std::min(n_levels, kFwdGroupMax)) {
+        const double v = (double)level_res[group] + 1.0;
+        if (v * v * v > (double)(1u << log2_T)) break;
+        ++group;
+    }
+    if (group < 2) group = 0;
+#endif
+    const int rows = group > 0 ? n_levels - group + 1 : n_levels;
 #ifdef NERF_AB_FWD_POINT_MAJOR
-    dim3 grid2(n_levels, blocks_for(2 * n_points, 256));
+    dim3 grid2(rows, blocks_for(2 * n_points, 256));
 #else
-    dim3 grid2(blocks_for(2 * n_points, 256), n_levels);
+    dim3 grid2(blocks_for(2 * n_points, 256), rows);
 #endif
     if (q)
         hipLaunchKernelGGL(hash_encode_fwd_pair_kernel<true>, grid2, dim3(256), 0, as_stream(stream), d_xyz,
-                           n_points, hp, d_feat, feat_stride_point, feat_stride_level, d_keep, q);
+                           n_points, hp, group, d_feat, feat_stride_point, feat_stride_level, d_keep, q);
     else
         hipLaunchKernelGGL(hash_encode_fwd_pair_kernel<false>, grid2, dim3(256), 0, as_stream(stream), d_xyz,
-                           n_points, hp, d_feat, feat_stride_point, feat_stride_level, d_keep, q);
+                           n_points, hp, group, d_feat, feat_stride_point, feat_stride_level, d_keep, q);
     NERF_CHECK_LAUNCH("hash_encode_fwd");
     return NERF_OK;
 }
