@@ -124,6 +124,48 @@ def test_hash_encode_edge_points_vs_c_oracle(nerf, gpu):
     np.testing.assert_array_equal(keep.cpu().numpy(), ref_keep)
 
 
+@pytest.mark.parametrize("log2_T", [12, 15])
+def test_hash_encode_small_tables_vs_oracle(nerf, gpu, oracle, log2_T):
+    """Tables smaller than the default 2^19: the forward groups the coarse levels whose (res+1)^3
+    vertices fit the table (2^15: three levels, an odd count for the two-level rounds; 2^12: none, every
+    level in its own grid row) and the binned backward runs one partial owner slice per level.
+    Features bit-exact and gradients at fp64-scatter accuracy vs the oracle (utils.py:95-117,
+    hash_encoding.py:56-107)."""
+    lo, hi = blender_bbox()
+    emb = nerf.HashEmbedder(_bbox_t(), finest_resolution=1024, log2_hashmap_size=log2_T).to(gpu)
+    g = torch.Generator().manual_seed(log2_T)
+    tabs = [torch.randn(1 << log2_T, 2, generator=g) * 0.1 for _ in range(16)]
+    with torch.no_grad():
+        for e, t in zip(emb.embeddings, tabs):
+            e.weight.copy_(t)
+    rng = np.random.RandomState(log2_T)
+    x = (lo - 0.1 + (hi - lo + 0.2) * rng.rand(65536, 3)).astype(np.float32)
+    xt = torch.from_numpy(x)
+    res = [torch.tensor(r, dtype=torch.float32) for r in emb.level_res]
+    bmin, bmax = (torch.from_numpy(v) for v in (lo, hi))
+    ref, ref_keep = oracle.hash_encode(xt, tabs, bmin, bmax, res, log2_T=log2_T)
+    feat, keep = emb(xt.to(gpu))
+    np.testing.assert_array_equal(feat.detach().cpu().numpy(), ref.numpy())
+    np.testing.assert_array_equal(keep.cpu().numpy(), ref_keep.numpy())
+    dfeat = torch.from_numpy(rng.randn(65536, 32).astype(np.float32))
+    (feat * dfeat.to(gpu)).sum().backward()
+    for lvl in (0, 3, 9, 15):
+        vmin, vmax, idx, _ = oracle.voxel_corners(xt, bmin, bmax, res[lvl], log2_T)
+        w = ((xt - vmin) / (vmax - vmin)).double()
+        wx, wy, wz = w[:, 0:1], w[:, 1:2], w[:, 2:3]
+        gl = dfeat[:, 2 * lvl:2 * lvl + 2].double()
+        contrib = []
+        for c in range(8):
+            i, j, k = (c >> 2) & 1, (c >> 1) & 1, c & 1
+            contrib.append(gl * ((wz if k else 1 - wz) * (wy if j else 1 - wy) * (wx if i else 1 - wx)))
+        contrib = torch.stack(contrib, 1).reshape(-1, 2)
+        want = torch.zeros(1 << log2_T, 2, dtype=torch.float64).index_add_(0, idx.reshape(-1), contrib)
+        scale = torch.zeros(1 << log2_T, 2, dtype=torch.float64).index_add_(0, idx.reshape(-1), contrib.abs())
+        got = emb.embeddings[lvl].weight.grad.cpu().double()
+        bad = (got - want).abs() > 2e-6 * scale + 1e-30
+        assert not bool(bad.any()), f"level {lvl}: {int(bad.sum())} rows off"
+
+
 def test_sh4_bit_exact(nerf, gpu, golden):
     g = golden("f5_sh")
     with torch.no_grad():
