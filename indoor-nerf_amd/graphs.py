@@ -3,7 +3,8 @@
 A PocketNeRF iteration (run_nerf.py:1007-1037, :1161-1162, :1289-1293) is ~40 kernel launches of
 which many are short; launched one by one from Python the GPU idles between them (the host spends
 ~0.2 ms per step in autograd and ctypes). GraphedTrainStep captures the iteration once — forward,
-losses, backward (graph 1) and the RAdam update (graph 2) — and replays it.
+losses, backward and the RAdam update: one graph on one process, two (graph 1 = forward + backward,
+graph 2 = the update) when a DP gradient hook runs between them — and replays it.
 
 What changes from step to step without changing the launch structure lives in device memory and is
 written before each replay (StepScalars): the Philox (seed, offset) of the stratified and
@@ -90,9 +91,9 @@ class StepScalars:
 
 
 class GraphedTrainStep:
-    """train_step (model.py) as two captured graphs (forward + backward, RAdam) plus the eager
-    grad hook between them and the post hook after the second (the DP collectives stay outside the
-    graphs). Call it like
+    """train_step (model.py) as captured graphs: one (forward + backward + RAdam) without a grad
+    hook; with one, two graphs (forward + backward, RAdam) and the eager grad hook between them and
+    the post hook after the second (the DP collectives stay outside the graphs). Call it like
     train_step(...) with the same arguments every iteration; it runs `warmup` eager iterations
     before the first capture (allocations, optimizer state, quantizer calibration)."""
 
