@@ -308,12 +308,42 @@ __device__ __forceinline__ void layer0(const __bf16* img, const float (&x)[16], 
     }
 }
 
-// forward chain up to h3 (and rgb when need_rgb)
+// The backward's chain wave keeps layer 0's output for its stage 6 in a per-wave global slot
+// (L2-resident: 9 KB per wave, ~9.4 MB in all) instead of recomputing it there (24 MFMAs and the
+// splits of x per tile): [wave][k][lane] float4, k = 0..7 the two h1 tiles, k = 8 the A-CAQ mask.
+constexpr int kH1SaveWords = 9;
+__device__ float4 g_h1_save[(size_t)kMlpBwdMaxBlocks * 4 * kH1SaveWords * 64];
+
+__device__ __forceinline__ void save_h1(float4* sv, const floatx16 (&h1)[2], uint32_t m1, int lane, bool quant) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+        sv[k * 64 + lane] = make_float4(h1[k >> 2][4 * (k & 3)], h1[k >> 2][4 * (k & 3) + 1],
+                                        h1[k >> 2][4 * (k & 3) + 2], h1[k >> 2][4 * (k & 3) + 3]);
+    if (quant) sv[8 * 64 + lane] = make_float4(__uint_as_float(m1), 0.f, 0.f, 0.f);
+}
+
+// L2-served loads (nt: not from this CU's L1, which may still hold the slot's previous tile)
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void load_h1(const float4* sv, floatx16 (&h1)[2], uint32_t& m1, int lane, bool quant) {
+    const f32x4* p = reinterpret_cast<const f32x4*>(sv);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const f32x4 v = __builtin_nontemporal_load(p + k * 64 + lane);
+        h1[k >> 2][4 * (k & 3)] = v.x;
+        h1[k >> 2][4 * (k & 3) + 1] = v.y;
+        h1[k >> 2][4 * (k & 3) + 2] = v.z;
+        h1[k >> 2][4 * (k & 3) + 3] = v.w;
+    }
+    m1 = quant ? __float_as_uint(__builtin_nontemporal_load(p + 8 * 64 + lane).x) : 0u;
+}
+
+// forward chain up to h3 (and rgb when need_rgb); save: the chain wave's h1 slot (backward) or null
 template <bool QUANT>
 __device__ __forceinline__ void fwd_chain(const __bf16* img, const InX6& in, ActX6& f, floatx16& rgb, int lane,
-                                          bool need_rgb, const QuantRec& aq) {
+                                          bool need_rgb, const QuantRec& aq, float4* save = nullptr) {
     const int m = lane & 31, h = lane >> 5;
     layer0<QUANT>(img, in.x, f.h1, f.m1, lane, aq);
+    if (save) save_h1(save, f.h1, f.m1, lane, QUANT);
     // L1: o = W1 h1 (rows 16..31 of the tile are never read)
     f.o = zero16();
 #pragma unroll
@@ -515,6 +545,7 @@ __device__ __forceinline__ void bwd_chain_role(const MlpArgs& a, const __bf16* i
     auto open = [&](bool act, int) { flag_wait(ack, act ? seq : seq - 1, &waited); };
 #endif
     __bf16* const stGb[2] = {stG, stG + 3 * STG_PIECE};
+    float4* const h1_slot = g_h1_save + ((size_t)blockIdx.x * 4 + p) * kH1SaveWords * 64;
     auto publish = [&]() { flag_set(ready, ++seq); };
     const int64_t n_tiles = (a.P + 31) / 32;
     for (int64_t tile = (int64_t)blk * 4 + p; tile < n_tiles; tile += (int64_t)nblk * 4) {
@@ -523,7 +554,7 @@ __device__ __forceinline__ void bwd_chain_role(const MlpArgs& a, const __bf16* i
         load_in_x6(a, tile, j, h, in);
         ActX6 f;
         floatx16 unused;
-        fwd_chain<QUANT>(imt, in, f, unused, lane, false, aq);
+        fwd_chain<QUANT>(imt, in, f, unused, lane, false, aq, h1_slot);
 
         float4 g4 = *reinterpret_cast<const float4*>(a.graw + 4u * (in.valid ? in.pt : (uint32_t)(a.P - 1)));
         if (!in.valid) g4 = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -599,20 +630,23 @@ __device__ __forceinline__ void bwd_chain_role(const MlpArgs& a, const __bf16* i
             go = mma6(tr_read(imt, IM_PIECE, IM_C0, S32, 32 * t, 0, lane), g0, go);
             go = mma6(tr_read(imt, IM_PIECE, IM_C0, S32, 32 * t + 16, 0, lane), g1, go);
         }
+        // stage 6's h1 from the slot fwd_chain filled (the wait finds nothing else outstanding here:
+        // it only orders the slot's stores before these loads)
+        floatx16 h1[2];
+        uint32_t m1;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        load_h1(h1_slot, h1, m1, lane, QUANT);
         if (a.dsh && in.valid) {
 #pragma unroll
             for (int r = 8; r < 16; ++r) a.dsh[16u * in.pt + row_of(r, h) - 16] = go[r];
         }
 
-        // stage 6 (dW1): go, h1 (recomputed from a reload of x) and layer 0's ReLU mask m1 (with QUANT:
+        // stage 6 (dW1): go, h1 (saved by fwd_chain, reloaded above) and layer 0's ReLU mask m1 (with QUANT:
         // before the activation quantizer) in the unused columns 16.. of the gradient tile.
         // The wgrad wave forms ga1 = mask(W1^T go) itself (it waits on the chain wave otherwise).
         float xr[16];
-        load_x6(a, in.pt, in.valid, h, xr, opaque_zero());
         {
-            floatx16 h1[2];
-            uint32_t m1;
-            layer0<QUANT>(imt, xr, h1, m1, lane, aq);
+            load_x6(a, in.pt, in.valid, h, xr, opaque_zero());
             const S3 GO = split_chunk(go, 0);
             open(true, 6);
 #pragma unroll
