@@ -203,6 +203,38 @@ def test_deferred_table_zero_bitwise(nerf, gpu):
     assert any(bool(g.any()) for g in got[-16:])
 
 
+def test_deferred_table_zero_other_writers(nerf, gpu):
+    """Deferred table gradients reaching a writer other than the binned owner pass are zeroed first:
+    2^20-row tables have no binned plan (the memory-side atomic path accumulates), and a backward
+    that never reaches the tables leaves them to hashgrid.materialize_zero()."""
+    from indoor_nerf_amd import hashgrid
+    from indoor_nerf_amd.dist import GradArena
+    lo, hi = blender_bbox()
+    emb = nerf.HashEmbedder((torch.from_numpy(lo), torch.from_numpy(hi)), finest_resolution=1024,
+                            log2_hashmap_size=20).to(gpu)
+    rng = np.random.RandomState(3)
+    x = torch.from_numpy((lo + (hi - lo) * rng.rand(4096, 3)).astype(np.float32)).to(gpu)
+    w = torch.from_numpy(rng.randn(4096, 32).astype(np.float32)).to(gpu)
+    params = list(emb.parameters())
+    ref_arena = GradArena(params)
+    ref_arena.zero_()
+    (emb(x)[0] * w).sum().backward()
+    ref = [p.grad.clone() for p in params]
+    arena = GradArena(params, defer_tables=True)
+    assert len(arena.deferred) == 16
+    arena.flat.fill_(7.0)
+    arena.zero_()
+    (emb(x)[0] * w).sum().backward()
+    torch.cuda.synchronize()
+    for a, b in zip(ref, params):
+        torch.testing.assert_close(b.grad, a, rtol=1e-5, atol=1e-7)
+    assert not hashgrid._DEFERRED
+    arena.flat.fill_(7.0)
+    arena.zero_()                       # no backward reaches the tables this time
+    hashgrid.materialize_zero()
+    assert all(not bool(p.grad.any()) for p in params)
+
+
 def test_check_numerics_flags_nan_and_inf(nerf, gpu):
     t = {"rgb_map": torch.rand(4096, 3, device=gpu), "depth_map": torch.rand(4096, device=gpu),
          "acc_map": torch.rand(1000, device=gpu), "weights": torch.zeros(0, device=gpu)}
