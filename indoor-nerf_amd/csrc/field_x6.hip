@@ -311,7 +311,7 @@ __device__ __forceinline__ void layer0(const __bf16* img, const float (&x)[16], 
 // The backward's chain wave keeps layer 0's output for its stage 6 in a per-wave global slot
 // (L2-resident: 9 KB per wave, ~9.4 MB in all) instead of recomputing it there (24 MFMAs and the
 // splits of x per tile): [wave][k][lane] float4, k = 0..7 the two h1 tiles, k = 8 the A-CAQ mask.
-constexpr int kH1SaveWords = 9;
+constexpr int kH1SaveWords = 11;   // + k = 9, 10: the point's SH coefficients (stage 4 stages them)
 __device__ float4 g_h1_save[(size_t)kMlpBwdMaxBlocks * 4 * kH1SaveWords * 64];
 
 __device__ __forceinline__ void save_h1(float4* sv, const floatx16 (&h1)[2], uint32_t m1, int lane, bool quant) {
@@ -337,6 +337,18 @@ __device__ __forceinline__ void load_h1(const float4* sv, floatx16 (&h1)[2], uin
     m1 = quant ? __float_as_uint(__builtin_nontemporal_load(p + 8 * 64 + lane).x) : 0u;
 }
 
+__device__ __forceinline__ void save_shv(float4* sv, const float (&shv)[8], int lane) {
+    sv[9 * 64 + lane] = make_float4(shv[0], shv[1], shv[2], shv[3]);
+    sv[10 * 64 + lane] = make_float4(shv[4], shv[5], shv[6], shv[7]);
+}
+
+__device__ __forceinline__ void load_shv(const float4* sv, float (&shv)[8], int lane) {
+    const f32x4* p = reinterpret_cast<const f32x4*>(sv);
+    const f32x4 a = __builtin_nontemporal_load(p + 9 * 64 + lane), b = __builtin_nontemporal_load(p + 10 * 64 + lane);
+    shv[0] = a.x; shv[1] = a.y; shv[2] = a.z; shv[3] = a.w;
+    shv[4] = b.x; shv[5] = b.y; shv[6] = b.z; shv[7] = b.w;
+}
+
 // forward chain up to h3 (and rgb when need_rgb); save: the chain wave's h1 slot (backward) or null
 template <bool QUANT>
 __device__ __forceinline__ void fwd_chain(const __bf16* img, const InX6& in, ActX6& f, floatx16& rgb, int lane,
@@ -360,6 +372,7 @@ __device__ __forceinline__ void fwd_chain(const __bf16* img, const InX6& in, Act
     }
     {
         const S3 SH = split_arr(in.shv);
+        if (save) save_shv(save, in.shv, lane);
 #pragma unroll
         for (int t = 0; t < 2; ++t) f.h2[t] = mma6(row_read(img, IM_C0, S32, 32 * t + m, 16 + 4 * h), SH, f.h2[t]);
     }
@@ -621,7 +634,8 @@ __device__ __forceinline__ void bwd_chain_role(const MlpArgs& a, const __bf16* i
 #pragma unroll
                 for (int r = 0; r < 8; ++r) actF[row_of(r, h) * SPF + j] = f.o[r];
                 float shv[8];
-                load_sh6(a, in.pt, in.valid, h, shv, opaque_zero());
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // orders the slot's stores (fwd_chain)
+                load_shv(h1_slot, shv, lane);                       // instead of re-evaluating the SH
                 stage_arrF(actF, shv, 16, j, h);
             }
             stage_grad(stGb[t], g0, 0, j, h);
