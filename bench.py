@@ -166,8 +166,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--rays", type=int, default=4096)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-rays", type=int, default=4096)
-    ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--cpu-rays", type=int, default=1024)
+    ap.add_argument("--cpu-warmup", type=int, default=6)
+    ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--profile-kernels", type=int, default=1, help="record HIP events per kernel in the timed region")
     ap.add_argument("--workload", default="lego", choices=sorted(WORKLOADS),
                     help="BASELINE config: lego (configs[1], the headline), fern (configs[2], LLFF NDC), "
@@ -216,19 +217,35 @@ WORKLOADS = {
 }
 
 
-def cpu_baseline(n_rays, steps):
-    """The oracle (CPU PyTorch restatement of the reference) timed on this host on the bench's own
-    batch size: one training iteration = coarse+fine render, losses incl. TV, backward, RAdam;
-    1 warm-up + `steps` timed (median), then one render-only pass (no grad) of the same rays.
-    Threads: the host's CPU share (OMP_NUM_THREADS, 16 on the GPU box) capped by the affinity mask."""
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or platform.machine()
+
+
+def cpu_threads():
+    """Threads for the CPU leg: every core of this process's affinity mask, capped by the job's CPU
+    share (OMP_NUM_THREADS: 16 per GPU on the pool's boxes, whose affinity mask shows the whole
+    machine; unset here: the mask alone)."""
+    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    share = os.environ.get("OMP_NUM_THREADS")
+    return cores, max(1, min(cores, int(share))) if share else cores
+
+
+def cpu_leg(n_rays, finest, H, warmup, timed):
+    """The oracle (CPU PyTorch restatement of the reference, oracle/nerf_oracle.py) on one bounded
+    sample: a full training iteration (coarse 64 + fine 128 render, MSE x2 + sparsity + TV, backward,
+    RAdam) on n_rays rays of the synthetic Blender rig at H x H, `warmup` iterations first (RAdam's
+    update is a no-op until N_sma >= 5 at step 6, radam.py:63-92) and the median of `timed`; then the
+    median of `timed` render-only passes (no grad) of the same rays."""
     from oracle import nerf_oracle as orc
     from indoor_nerf_amd.synthetic import blender_bbox, blender_rays
-    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
-    share = int(os.environ.get("OMP_NUM_THREADS", "16") or 16)
-    threads = max(1, min(cores, share))
-    torch.set_num_threads(threads)
     lo, hi = (torch.from_numpy(v) for v in blender_bbox())
-    res = orc.level_resolutions(16, 1024)
+    res = orc.level_resolutions(16, finest)
     g = torch.Generator().manual_seed(0)
     tabs = [((torch.rand(1 << 19, 2, generator=g) * 2 - 1) * 1e-4).requires_grad_(True) for _ in range(16)]
     cw = {k: v.requires_grad_(True) for k, v in orc.mlp_init(1).items()}
@@ -236,11 +253,11 @@ def cpu_baseline(n_rays, steps):
     opt = orc.RAdamOracle([dict(params=list(cw.values()) + list(fw.values()), lr=5e-4, betas=(0.9, 0.99), eps=1e-8,
                                 weight_decay=1e-6), dict(params=tabs, lr=5e-4, betas=(0.9, 0.99), eps=1e-15,
                                                          weight_decay=0)])
-    ro, rd = (torch.from_numpy(v) for v in blender_rays(n_rays, seed=11))
+    ro, rd = (torch.from_numpy(v) for v in blender_rays(n_rays, H=H, W=H, seed=11))
     vd = orc.viewdirs_of(rd)
     target = torch.rand(n_rays, 3, generator=g)
 
-    def step(i):
+    def step():
         out = orc.render_rays(ro, rd, vd, 2.0, 6.0, cw, fw, tabs, lo, hi, res)
         for p in list(cw.values()) + list(fw.values()) + tabs:
             p.grad = None
@@ -248,33 +265,92 @@ def cpu_baseline(n_rays, steps):
         loss = loss + 1e-10 * (out["sparsity_loss"].sum() + out["sparsity_loss0"].sum())
         tv = 0
         for lvl in range(16):
-            r, cube = orc.tv_cube(lvl, 16, 1024)
+            r, cube = orc.tv_cube(lvl, 16, finest)
             mv = torch.randint(0, r - cube, (3,), generator=g)
-            tv = tv + orc.tv_loss(tabs[lvl], lvl, mv, 16, 1024)
+            tv = tv + orc.tv_loss(tabs[lvl], lvl, mv, 16, finest)
         loss = loss + 1e-6 * tv
         loss.backward()
         opt.step()
 
-    step(0)
+    for _ in range(warmup):
+        step()
     times = []
-    for i in range(steps):
+    for _ in range(timed):
         t0 = time.perf_counter()
-        step(i + 1)
+        step()
         times.append(time.perf_counter() - t0)
     t = float(np.median(times))
+    rt = []
     with torch.no_grad():
-        t0 = time.perf_counter()
-        orc.render_rays(ro, rd, vd, 2.0, 6.0, cw, fw, tabs, lo, hi, res)
-        t_render = time.perf_counter() - t0
-    return {"value": round(n_rays / t, 2), "unit": "rays/s", "cores": threads, "kind": "port",
-            "render_only": {"value": round(n_rays / t_render, 2), "unit": "rays/s"},
-            "sample": f"the bench's batch: {n_rays} rays x (64+128) samples, finest 1024, full train iteration incl. "
-                      f"TV + RAdam; median of {steps} steps after 1 warm-up; render-only = one no-grad pass of the "
-                      f"same rays ({platform.processor() or platform.machine()}, {threads} threads)"}
+        for _ in range(timed):
+            t0 = time.perf_counter()
+            orc.render_rays(ro, rd, vd, 2.0, 6.0, cw, fw, tabs, lo, hi, res)
+            rt.append(time.perf_counter() - t0)
+    return {"value": round(n_rays / t, 2), "unit": "rays/s", "step_s": round(t, 3),
+            "render_only": {"value": round(n_rays / float(np.median(rt)), 2), "unit": "rays/s"},
+            "sample": f"{n_rays} rays of a {H}x{H} Blender rig x (64 coarse + 128 fine) samples, finest_res {finest}, "
+                      f"full train iteration incl. TV + RAdam; median of {timed} iterations after {warmup} warm-up "
+                      f"iterations (RAdam active); render-only = median of {timed} no-grad passes"}
+
+
+def cpu_baseline(n_rays, warmup, timed):
+    """SURVEY.md §8(d)'s CPU baseline on the GPU box's host cores, rank 0 at N=1 only: the lego leg
+    (configs[1]'s finest 1024 at 800x800) is `value`; the chair leg is BASELINE configs[0] (chair
+    400x400, finest_res 512, the reference's CPU path: configs/chair.txt). n_rays per iteration is
+    the configs' own N_rand (1024) so that the two legs stay within ~1 minute of CPU time; per-ray
+    work dominates the iteration (RAdam's dense pass is ~10 ms of a multi-second step), so rays/s at
+    1024 rays stands for the 4096-ray batch."""
+    cores, threads = cpu_threads()
+    torch.set_num_threads(threads)
+    lego = cpu_leg(n_rays, 1024, 800, warmup, timed)
+    chair = cpu_leg(n_rays, 512, 400, warmup, timed)
+    return {"value": lego["value"], "unit": "rays/s", "cores": threads, "kind": "port",
+            "render_only": lego["render_only"], "step_s": lego["step_s"],
+            "sample": "lego leg: " + lego["sample"],
+            "cpu": cpu_model(), "affinity_cores": cores,
+            "threads_note": "torch.set_num_threads = the job's CPU share (OMP_NUM_THREADS) within the affinity mask",
+            "chair": {**chair, "config": "BASELINE configs[0]: chair 400x400, finest_res 512 (configs/chair.txt)"}}
+
+
+def launch_ranks(a):
+    """`--gpus N` (N > 1) without torchrun's environment: start the N rank processes here (torch's
+    elastic launcher as a CHILD process, one rank per GPU, rendezvous on 127.0.0.1) and return its
+    exit status. Nothing in this process has touched the GPU (torch.cuda.device_count() does not
+    initialise it on this image). Refuses when fewer than N GPUs are visible: RCCL rejects two ranks
+    on one GPU ("Duplicate GPU detected"), and a line with fewer ranks would misreport n_gpus.
+    NERF_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs (host-staged collectives)."""
+    import socket
+    import subprocess
+    visible = torch.cuda.device_count()
+    if visible < a.gpus and os.environ.get("NERF_DIST_BACKEND") != "gloo":
+        print(f"bench.py: --gpus {a.gpus} needs {a.gpus} GPUs, {visible} visible; refusing (RCCL rejects two ranks "
+              f"on one GPU: 'Duplicate GPU detected'; NERF_DIST_BACKEND=gloo rehearses the ranks on fewer GPUs)",
+              file=sys.stderr, flush=True)
+        return 3
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd).returncode
 
 
 def main():
     a = parse()
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and a.gpus > 1:
+        sys.exit(launch_ranks(a))
+    if world_env is not None and int(world_env) != a.gpus:
+        print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world_env} (torchrun --nproc-per-node must equal --gpus)",
+              file=sys.stderr, flush=True)
+        sys.exit(2)
+    if a.gpus < 1:
+        sys.exit("bench.py: --gpus must be >= 1")
+    if a.gpus > 1 and torch.cuda.device_count() < a.gpus and os.environ.get("NERF_DIST_BACKEND") != "gloo":
+        print(f"bench.py: rank of a {a.gpus}-GPU run with {torch.cuda.device_count()} GPUs visible; refusing (RCCL "
+              f"rejects two ranks on one GPU: 'Duplicate GPU detected')", file=sys.stderr, flush=True)
+        sys.exit(3)
     import indoor_nerf_amd as nerf
     from indoor_nerf_amd import _lib
     from indoor_nerf_amd.synthetic import blender_bbox, blender_rays, llff_bbox, llff_rays
@@ -438,10 +514,11 @@ def main():
 
     value = (a.rays if strong else world * a.rays) * a.steps / elapsed
     out = {
-        "metric": "train rays/sec (4096 rays x 192 samples)" if a.mode == "train" else "render rays/sec (eval)",
+        "metric": (f"train rays/sec ({R} rays x {(ns + ni) if ni else ns} samples)" if a.mode == "train"
+                   else "render rays/sec (eval)"),
         "value": round(value, 1),
         "unit": "rays/s",
-        "n_gpus": world,
+        "n_gpus": a.gpus,
         "steps": a.steps,
         "warmup": a.warmup,
         "ms_per_step": round(1e3 * elapsed / a.steps, 3),
@@ -475,7 +552,7 @@ def main():
                                     for k, v in pj.items() if isinstance(v, dict)}
         out["psnr_vs_reference"]["source"] = "profiles/r02_psnr_vs_reference.json"
     if rank == 0 and world == 1 and not a.no_cpu_baseline and a.workload == "lego" and a.mode == "train":
-        out["cpu_baseline"] = cpu_baseline(a.cpu_rays, a.cpu_steps)
+        out["cpu_baseline"] = cpu_baseline(a.cpu_rays, a.cpu_warmup, a.cpu_steps)
     elif rank == 0:
         out["cpu_baseline"] = None
     if rank == 0:

@@ -205,9 +205,9 @@ int nerf_mlp_bwd_q(const float* d_feat, int64_t feat_stride_point, int64_t feat_
  * skipped. d_det_workspace (NULL = off; >= nerf_mlp_bwd_det_workspace_bytes()) selects the
  * DETERMINISTIC mode: every block's weight-gradient partial sum is stored and reduced over blocks in
  * a fixed order (no float atomics), so identical inputs give bit-identical gradients.
- * nerf_mlp_bwd_q and nerf_mlp_bwd_batch calls on one device must be stream-ordered: their chain
- * waves keep layer 0's activations in a device-global scratch (9 KB per wave) between two stages of
- * a tile instead of recomputing them. */
+ * Stateless: the kernels keep everything between the stages of a tile in registers and LDS, so
+ * calls on different streams of one device may run concurrently (only calls that share a
+ * d_det_workspace must be stream-ordered). */
 #define NERF_MLP_MAX_JOBS 2
 typedef struct {
     const float* feat;

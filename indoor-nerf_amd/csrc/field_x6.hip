@@ -308,54 +308,12 @@ __device__ __forceinline__ void layer0(const __bf16* img, const float (&x)[16], 
     }
 }
 
-// The backward's chain wave keeps layer 0's output for its stage 6 in a per-wave global slot
-// (L2-resident: 9 KB per wave, ~9.4 MB in all) instead of recomputing it there (24 MFMAs and the
-// splits of x per tile): [wave][k][lane] float4, k = 0..7 the two h1 tiles, k = 8 the A-CAQ mask.
-constexpr int kH1SaveWords = 11;   // + k = 9, 10: the point's SH coefficients (stage 4 stages them)
-__device__ float4 g_h1_save[(size_t)kMlpBwdMaxBlocks * 4 * kH1SaveWords * 64];
-
-__device__ __forceinline__ void save_h1(float4* sv, const floatx16 (&h1)[2], uint32_t m1, int lane, bool quant) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-        sv[k * 64 + lane] = make_float4(h1[k >> 2][4 * (k & 3)], h1[k >> 2][4 * (k & 3) + 1],
-                                        h1[k >> 2][4 * (k & 3) + 2], h1[k >> 2][4 * (k & 3) + 3]);
-    if (quant) sv[8 * 64 + lane] = make_float4(__uint_as_float(m1), 0.f, 0.f, 0.f);
-}
-
-// L2-served loads (nt: not from this CU's L1, which may still hold the slot's previous tile)
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void load_h1(const float4* sv, floatx16 (&h1)[2], uint32_t& m1, int lane, bool quant) {
-    const f32x4* p = reinterpret_cast<const f32x4*>(sv);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const f32x4 v = __builtin_nontemporal_load(p + k * 64 + lane);
-        h1[k >> 2][4 * (k & 3)] = v.x;
-        h1[k >> 2][4 * (k & 3) + 1] = v.y;
-        h1[k >> 2][4 * (k & 3) + 2] = v.z;
-        h1[k >> 2][4 * (k & 3) + 3] = v.w;
-    }
-    m1 = quant ? __float_as_uint(__builtin_nontemporal_load(p + 8 * 64 + lane).x) : 0u;
-}
-
-__device__ __forceinline__ void save_shv(float4* sv, const float (&shv)[8], int lane) {
-    sv[9 * 64 + lane] = make_float4(shv[0], shv[1], shv[2], shv[3]);
-    sv[10 * 64 + lane] = make_float4(shv[4], shv[5], shv[6], shv[7]);
-}
-
-__device__ __forceinline__ void load_shv(const float4* sv, float (&shv)[8], int lane) {
-    const f32x4* p = reinterpret_cast<const f32x4*>(sv);
-    const f32x4 a = __builtin_nontemporal_load(p + 9 * 64 + lane), b = __builtin_nontemporal_load(p + 10 * 64 + lane);
-    shv[0] = a.x; shv[1] = a.y; shv[2] = a.z; shv[3] = a.w;
-    shv[4] = b.x; shv[5] = b.y; shv[6] = b.z; shv[7] = b.w;
-}
-
-// forward chain up to h3 (and rgb when need_rgb); save: the chain wave's h1 slot (backward) or null
+// forward chain up to h3 (and rgb when need_rgb)
 template <bool QUANT>
 __device__ __forceinline__ void fwd_chain(const __bf16* img, const InX6& in, ActX6& f, floatx16& rgb, int lane,
-                                          bool need_rgb, const QuantRec& aq, float4* save = nullptr) {
+                                          bool need_rgb, const QuantRec& aq) {
     const int m = lane & 31, h = lane >> 5;
     layer0<QUANT>(img, in.x, f.h1, f.m1, lane, aq);
-    if (save) save_h1(save, f.h1, f.m1, lane, QUANT);
     // L1: o = W1 h1 (rows 16..31 of the tile are never read)
     f.o = zero16();
 #pragma unroll
@@ -372,7 +330,6 @@ __device__ __forceinline__ void fwd_chain(const __bf16* img, const InX6& in, Act
     }
     {
         const S3 SH = split_arr(in.shv);
-        if (save) save_shv(save, in.shv, lane);
 #pragma unroll
         for (int t = 0; t < 2; ++t) f.h2[t] = mma6(row_read(img, IM_C0, S32, 32 * t + m, 16 + 4 * h), SH, f.h2[t]);
     }
@@ -558,7 +515,6 @@ __device__ __forceinline__ void bwd_chain_role(const MlpArgs& a, const __bf16* i
     auto open = [&](bool act, int) { flag_wait(ack, act ? seq : seq - 1, &waited); };
 #endif
     __bf16* const stGb[2] = {stG, stG + 3 * STG_PIECE};
-    float4* const h1_slot = g_h1_save + ((size_t)blockIdx.x * 4 + p) * kH1SaveWords * 64;
     auto publish = [&]() { flag_set(ready, ++seq); };
     const int64_t n_tiles = (a.P + 31) / 32;
     for (int64_t tile = (int64_t)blk * 4 + p; tile < n_tiles; tile += (int64_t)nblk * 4) {
@@ -567,7 +523,7 @@ __device__ __forceinline__ void bwd_chain_role(const MlpArgs& a, const __bf16* i
         load_in_x6(a, tile, j, h, in);
         ActX6 f;
         floatx16 unused;
-        fwd_chain<QUANT>(imt, in, f, unused, lane, false, aq, h1_slot);
+        fwd_chain<QUANT>(imt, in, f, unused, lane, false, aq);
 
         float4 g4 = *reinterpret_cast<const float4*>(a.graw + 4u * (in.valid ? in.pt : (uint32_t)(a.P - 1)));
         if (!in.valid) g4 = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -634,8 +590,7 @@ __device__ __forceinline__ void bwd_chain_role(const MlpArgs& a, const __bf16* i
 #pragma unroll
                 for (int r = 0; r < 8; ++r) actF[row_of(r, h) * SPF + j] = f.o[r];
                 float shv[8];
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // orders the slot's stores (fwd_chain)
-                load_shv(h1_slot, shv, lane);                       // instead of re-evaluating the SH
+                load_sh6(a, in.pt, in.valid, h, shv, opaque_zero());   // re-evaluated: nothing is kept across stages
                 stage_arrF(actF, shv, 16, j, h);
             }
             stage_grad(stGb[t], g0, 0, j, h);
@@ -644,23 +599,21 @@ __device__ __forceinline__ void bwd_chain_role(const MlpArgs& a, const __bf16* i
             go = mma6(tr_read(imt, IM_PIECE, IM_C0, S32, 32 * t, 0, lane), g0, go);
             go = mma6(tr_read(imt, IM_PIECE, IM_C0, S32, 32 * t + 16, 0, lane), g1, go);
         }
-        // stage 6's h1 from the slot fwd_chain filled (the wait finds nothing else outstanding here:
-        // it only orders the slot's stores before these loads)
-        floatx16 h1[2];
-        uint32_t m1;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        load_h1(h1_slot, h1, m1, lane, QUANT);
         if (a.dsh && in.valid) {
 #pragma unroll
             for (int r = 8; r < 16; ++r) a.dsh[16u * in.pt + row_of(r, h) - 16] = go[r];
         }
 
-        // stage 6 (dW1): go, h1 (saved by fwd_chain, reloaded above) and layer 0's ReLU mask m1 (with QUANT:
-        // before the activation quantizer) in the unused columns 16.. of the gradient tile.
+        // stage 6 (dW1): go, h1 (recomputed from a reload of x: the kernel keeps no state between
+        // stages outside its registers and LDS) and layer 0's ReLU mask m1 (with QUANT: before the
+        // activation quantizer) in the unused columns 16.. of the gradient tile.
         // The wgrad wave forms ga1 = mask(W1^T go) itself (it waits on the chain wave otherwise).
         float xr[16];
+        load_x6(a, in.pt, in.valid, h, xr, opaque_zero());
         {
-            load_x6(a, in.pt, in.valid, h, xr, opaque_zero());
+            floatx16 h1[2];
+            uint32_t m1;
+            layer0<QUANT>(imt, xr, h1, m1, lane, aq);
             const S3 GO = split_chunk(go, 0);
             open(true, 6);
 #pragma unroll
@@ -815,11 +768,28 @@ __device__ __forceinline__ void bwd_wgrad_role(const MlpArgs& a, const __bf16* i
             take(); read16(o, stG + 3 * STG_PIECE, actF, lane); release();
             mma16(g.dC2, o);
         }
+        // 2 + 3: dC1 for both ga3 tiles against ONE split of h2 (per 16-point chunk c: the two h2
+        // fragments split once, both gradient tiles' fragments read), released after the last reads.
+        // Splitting h2 once instead of once per ga3 tile: 413 -> 401 us per launch (tools/mlp_ab.py).
+        // The same merge of stages 4 + 5 (dC0) is slower (the later release holds the chain wave:
+        // 414 -> 422 us), and x split once for both dW0 tiles does not move the launch.
+        seq += 1;
+        take();
 #pragma unroll
-        for (int t = 0; t < 2; ++t) {   // 2, 3: dC1
-            Ops32<2> o;   // 72 registers of operands: too many to hold beside the sums, no early release
-            take(); read32<2>(o, stG + t * 3 * STG_PIECE, actF, lane); flag_set(ack, ++seq);
-            mma32<2>(g.dC1[t], o);
+        for (int c = 0; c < 2; ++c) {
+            Raw8 hr[2];
+            S3 A[2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) hr[u] = act_read32(actF, 16 * c, 32 * u, lane);
+#pragma unroll
+            for (int t = 0; t < 2; ++t) A[t] = tr_read(stG + t * 3 * STG_PIECE, STG_PIECE, 0, S32, 16 * c, 0, lane);
+            if (c == 1) release();
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const S3 hb = split_raw(hr[u]);
+#pragma unroll
+                for (int t = 0; t < 2; ++t) g.dC1[t][u] = mma6(A[t], hb, g.dC1[t][u]);
+            }
         }
 #pragma unroll
         for (int t = 0; t < 2; ++t) {   // 4, 5: dC0

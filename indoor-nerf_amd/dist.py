@@ -225,22 +225,32 @@ class ShardedOptimizer:
             torch.autograd.graph.increment_version(p)
 
     def consolidate_state(self):
-        """Every rank's exp_avg / exp_avg_sq shards summed into full tensors on every rank (each
-        element is owned by exactly one rank; the others contribute zeros)."""
+        """COLLECTIVE: every rank must call it (model.save_checkpoint(sharded=...) does so on every
+        rank and writes on one). Every rank's exp_avg / exp_avg_sq shards are summed into full
+        tensors on every rank (each element is owned by exactly one rank; the others contribute
+        zeros) with ONE all-reduce over both moments of every parameter laid out like the gradient
+        arena, so the call count cannot differ between ranks whatever state each rank holds."""
         if self.world == 1:
             return
-        for p, r in zip(self.arena.params, self.ranges):
+        keys = ("exp_avg", "exp_avg_sq")
+        n = self.arena.flat.numel()
+        buf = torch.zeros(len(keys) * n, device=self.pflat.device, dtype=torch.float32)
+        for p, off, r in zip(self.arena.params, self.arena.offsets, self.ranges):
+            st = self.opt.state.get(p)
+            if not st or r is None:
+                continue
+            for k, key in enumerate(keys):
+                buf[k * n + off + r[0]:k * n + off + r[1]] = st[key].reshape(-1)[r[0]:r[1]]
+        h = _staged(buf)
+        dist.all_reduce(h, op=dist.ReduceOp.SUM, group=self.group)
+        if h is not buf:
+            buf.copy_(h)
+        for p, off in zip(self.arena.params, self.arena.offsets):
             st = self.opt.state.get(p)
             if not st:
                 continue
-            for key in ("exp_avg", "exp_avg_sq"):
-                t = st[key]
-                mine = torch.zeros_like(t).view(-1)
-                if r is not None:
-                    mine[r[0]:r[1]] = t.view(-1)[r[0]:r[1]]
-                h = _staged(mine)
-                dist.all_reduce(h, op=dist.ReduceOp.SUM, group=self.group)
-                t.view(-1).copy_(h.to(t.device))
+            for k, key in enumerate(keys):
+                st[key].view(-1).copy_(buf[k * n + off:k * n + off + p.numel()])
 
 
 def broadcast_params(params, src=0):

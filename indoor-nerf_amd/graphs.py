@@ -188,9 +188,10 @@ class GraphedTrainStep:
         return bool(get("use_structural_priors")) and global_step >= get("structural_loss_start_iter")
 
     def __call__(self, global_step):
-        from .model import acaq_update, lr_schedule
-        if self._priors_active(global_step) and not getattr(self.args, "fused_priors", True):
-            # the eager priors path branches on host counts and draws host permutations: not capturable
+        from .model import acaq_update, fused_priors_eligible, lr_schedule
+        if self._priors_active(global_step) and not fused_priors_eligible(self.args, self.rays[0].shape[0]):
+            # the eager priors path (args.fused_priors = False, no normals head, or more rays than the
+            # device path takes) branches on host counts and draws host permutations: not capturable
             self.graphs, self.key = None, None
             return self.eager_step(global_step)
         key = self._structure_key(global_step)

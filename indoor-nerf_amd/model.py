@@ -99,17 +99,29 @@ def create_nerf(args, device=None):
     return render_kwargs_train, render_kwargs_test, start, grad_vars, optimizer
 
 
-def save_checkpoint(path, global_step, render_kwargs_train, optimizer, sharded=None):
-    """The reference's checkpoint dict (run_nerf.py:1345-1362). With a dist.ShardedOptimizer, its
-    per-rank moment shards are first assembled into full tensors on every rank."""
+def save_checkpoint(path, global_step, render_kwargs_train, optimizer, sharded=None, write_rank=0):
+    """The reference's checkpoint dict (run_nerf.py:1345-1362), written by one process.
+
+    With a dist.ShardedOptimizer this is a COLLECTIVE call: EVERY rank must call it (the moment
+    shards are assembled into full tensors with one all-reduce first), and only rank `write_rank`
+    writes the file; a call on one rank alone would wait forever for the others. Without sharding
+    any rank may call it on its own. Returns True on the rank that wrote."""
+    rank = 0
     if sharded is not None:
+        import torch.distributed as dist
+        if sharded.world > 1 and not (dist.is_available() and dist.is_initialized()):
+            raise RuntimeError("save_checkpoint(sharded=...): torch.distributed is not initialised")
         sharded.consolidate_state()
+        rank = sharded.rank
+    if rank != write_rank:
+        return False
     fine = render_kwargs_train["network_fine"]
     torch.save({"global_step": global_step,
                 "network_fn_state_dict": render_kwargs_train["network_fn"].state_dict(),
                 "network_fine_state_dict": fine.state_dict() if fine is not None else None,
                 "embed_fn_state_dict": render_kwargs_train["embed_fn"].state_dict(),
                 "optimizer_state_dict": optimizer.state_dict()}, path)
+    return True
 
 
 def acaq_quantizers(render_kwargs_train):
@@ -198,6 +210,17 @@ def _unit_seed(loss):
     return seed
 
 
+def fused_priors_eligible(args, n_rays):
+    """True when structural_loss takes the device path (priors.fused_structural_losses): no host
+    synchronisation, so graphs.GraphedTrainStep may capture the iteration. The one test both use:
+    args.fused_priors (default True), the normals head present (predict_normals) and
+    1 <= n_rays <= PRIORS_MAX_RAYS; anything else runs the eager torch path, which branches on host
+    counts and cannot be captured."""
+    get = lambda k: getattr(args, k, DEFAULTS.get(k))  # noqa: E731
+    return (bool(getattr(args, "fused_priors", True)) and bool(get("predict_normals"))
+            and 1 <= int(n_rays) <= _lib.PRIORS_MAX_RAYS)
+
+
 def structural_loss(depth, extras, args, global_step, spatial_coords=None):
     """run_nerf.py:1068-1131: the structural-prior weights ramp from 10 % to 100 % over
     structural_loss_ramp_iters, then combine_structural_losses_v2 on the fine pass's depth and normal
@@ -217,7 +240,7 @@ def structural_loss(depth, extras, args, global_step, spatial_coords=None):
     base = {"depth_prior": get("depth_prior_weight"), "planarity": get("planarity_weight"),
             "manhattan": get("manhattan_weight"), "normal_consistency": get("normal_consistency_weight")}
     normals = extras.get("normal_map", None) if get("predict_normals") else None
-    if getattr(args, "fused_priors", True) and normals is not None and 1 <= depth.shape[0] <= _lib.PRIORS_MAX_RAYS:
+    if normals is not None and fused_priors_eligible(args, depth.shape[0]):
         sc = graphs.active()
         if sc is not None:   # captured: the ramp of the replayed step, written before every replay
             off, ptr = sc.alloc_f32(1)

@@ -259,20 +259,15 @@ def combine_structural_losses_v2(depth_pred, normals, rays_d, spatial_coords=Non
 
 
 # ---- device path: the whole combine_structural_losses_v2 in three launches (csrc/priors_fused.hip) ----
-_FUSED_WS = {}
-_FUSED_RETIRED = []   # workspaces a captured graph may still reference (never freed, see hashgrid._RETIRED)
 _CAPS = (100, 100, 50)
 
 
 def _fused_workspace(n, device):
-    need = int(_lib.load().nerf_priors_workspace_bytes(n))
-    key = str(device)
-    ws = _FUSED_WS.get(key)
-    if ws is None or ws.numel() < need:
-        if ws is not None:
-            _FUSED_RETIRED.append(ws)
-        ws = _FUSED_WS[key] = torch.empty(need, dtype=torch.uint8, device=device)
-    return ws
+    """A workspace of its own for every forward: it carries the forward's state (masks, pairs, the
+    frame) to that node's backward, so a second forward before the first backward (e.g. a logging
+    call with grad enabled) cannot overwrite it. Under a HIP-graph capture it comes from the graph's
+    private pool like every other allocation of the captured step."""
+    return torch.empty(int(_lib.load().nerf_priors_workspace_bytes(n)), dtype=torch.uint8, device=device)
 
 
 class _FusedPriorsFn(torch.autograd.Function):
@@ -285,7 +280,9 @@ class _FusedPriorsFn(torch.autograd.Function):
         d = depth.detach().float().contiguous()
         n = normals.detach().float().contiguous()
         xy = coords.detach().float().contiguous() if coords is not None else None
-        ws = _fused_workspace(N, dev)
+        ws = spec["workspace"] if spec.get("workspace") is not None else _fused_workspace(N, dev)
+        if ws.dtype != torch.uint8 or ws.numel() < int(_lib.load().nerf_priors_workspace_bytes(N)):
+            raise ValueError("fused_structural_losses: workspace must be uint8 with nerf_priors_workspace_bytes(N) bytes")
         cfg = _lib.PriorsConfig()
         w = spec["weights"]
         cfg.use_manhattan, cfg.use_planarity, cfg.use_consistency = (int(k in w) for k in
@@ -296,7 +293,9 @@ class _FusedPriorsFn(torch.autograd.Function):
         scale = spec.get("scale")
         cfg.d_scale = _lib.ptr(scale, "scale", allow_none=True)
         cfg.confidence_threshold, cfg.normal_threshold = spec["confidence"], spec["normal_threshold"]
-        keep_alive = []
+        # everything cfg points at stays referenced by ctx until the backward has read it (the ramp
+        # `scale` is often a temporary of the caller)
+        keep_alive = [] if scale is None else [scale]
         args = (_lib.ptr(d, "depth"), _lib.ptr(n, "normals"), _lib.ptr(xy, "coords", allow_none=True), N)
         wsp = (_lib.ptr(ws, "workspace", dtype=torch.uint8), ws.numel())
         if spec["replay"]:
@@ -384,12 +383,14 @@ def _replay_draws(cfg, n, xy, N, spec, keep_alive):
 
 
 def fused_structural_losses(depth_pred, normals, spatial_coords=None, weights=None, confidence_threshold=0.4,
-                            normal_threshold=0.5, scale=None, replay=False):
+                            normal_threshold=0.5, scale=None, replay=False, workspace=None):
     """combine_structural_losses_v2 on the device (csrc/priors_fused.hip): same losses, branches and
     autograd graph, no host synchronisation (capturable in a HIP graph). scale: optional device [1]
     multiplier of the weights (the train() ramp, a per-step graph slot). replay=True draws the
     reference's torch.randn/randperm/randint in its order and takes the frame's SVD from LAPACK
-    (host syncs; the golden F18 parity mode). Returns (total, parts) with parts a device [7] tensor
+    (host syncs; the golden F18 parity mode). workspace: optional uint8 device tensor of at least
+    nerf_priors_workspace_bytes(N) for this call's state (default: a fresh one per call; pass one to
+    inspect the PriorsState afterwards). Returns (total, parts) with parts a device [7] tensor
     (floor, wall, general, manhattan, planarity, consistency, total)."""
     if weights is None:
         weights = {"manhattan": 1.0, "planarity": 1.0, "normal_consistency": 0.5}
@@ -397,6 +398,6 @@ def fused_structural_losses(depth_pred, normals, spatial_coords=None, weights=No
     if not (1 <= N <= _lib.PRIORS_MAX_RAYS) or normals is None or normals.shape != (N, 3):
         raise ValueError(f"fused_structural_losses: need depth [N] and normals [N,3], 1 <= N <= {_lib.PRIORS_MAX_RAYS}")
     spec = dict(weights=weights, confidence=float(confidence_threshold), normal_threshold=float(normal_threshold),
-                scale=scale, replay=bool(replay))
+                scale=scale, replay=bool(replay), workspace=workspace)
     total = _FusedPriorsFn.apply(depth_pred, normals, spatial_coords, spec)
     return total, spec["parts"]

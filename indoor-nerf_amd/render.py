@@ -88,9 +88,27 @@ def manual_seed(seed):
     _SEED_GEN = torch.Generator().manual_seed(int(seed))
 
 
+_PYTEST_SHARD = (0, 1)
+
+
+def pytest_shard(rank, world):
+    """pytest=True draws for a data-parallel shard: every draw then takes the reference's
+    np.random.seed(0) uniforms for the GLOBAL batch (world x this rank's rays, run_nerf.py:482-486,
+    run_nerf_helpers.py:368-377) and keeps this rank's contiguous rows, so that G shards see exactly
+    the draws one process sees for the whole batch (tests/test_gpu_dist.py). (0, 1) = off."""
+    global _PYTEST_SHARD
+    if not (0 <= rank < world):
+        raise ValueError(f"pytest_shard: rank {rank} of {world}")
+    _PYTEST_SHARD = (int(rank), int(world))
+
+
 def _pytest_uniforms(shape, device):
     np.random.seed(0)
-    return torch.from_numpy(np.random.rand(*shape).astype(np.float32)).to(device)
+    rank, world = _PYTEST_SHARD
+    if world == 1:
+        return torch.from_numpy(np.random.rand(*shape).astype(np.float32)).to(device)
+    full = np.random.rand(shape[0] * world, *shape[1:]).astype(np.float32)
+    return torch.from_numpy(full[rank * shape[0]:(rank + 1) * shape[0]]).to(device)
 
 
 # ---------------------------------------------------------------- compositing

@@ -181,3 +181,61 @@ def test_sharded_optimizer_gloo(tmp_path):
         u = np.where(st >= 1 << 31, st & 0x7FFFFFFF, (~st) & 0xFFFFFFFF).astype(np.uint32).view(np.float32)
         np.testing.assert_array_equal(u, np.array([[-3.0, 2.0], [0.0, -1.0]], np.float32))
         np.testing.assert_allclose(np.load(tmp_path / f"m_{r}.npy"), [1.5])
+
+
+class _MomentShard(_SgdShard):
+    """_SgdShard with RAdam-like moments: on each rank only the rank's shard of exp_avg / exp_avg_sq
+    holds the true values (k * (index + 1)); the rest holds rank-specific garbage."""
+
+    def __init__(self, params, rank):
+        super().__init__(params)
+        self.rank = rank
+        self.state = {p: {"exp_avg": torch.full(p.shape, -100.0 - rank), "exp_avg_sq": torch.full(p.shape, 7.0 + rank)}
+                      for p in params}
+
+    def fill_shard(self):
+        for p in self.params:
+            if p in self.shard:
+                a, b, _ = self.shard[p]
+                idx = torch.arange(a, b, dtype=torch.float32) + 1
+                self.state[p]["exp_avg"].view(-1)[a:b] = idx
+                self.state[p]["exp_avg_sq"].view(-1)[a:b] = 2 * idx
+
+    def state_dict(self):
+        return {"state": {i: {k: v.clone() for k, v in self.state[p].items()} for i, p in enumerate(self.params)}}
+
+
+def _ckpt_worker(rank, world, port, out_dir):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from indoor_nerf_amd.dist import GradArena, ShardedOptimizer, init_process_group
+    from indoor_nerf_amd.model import save_checkpoint
+    init_process_group(backend="gloo")
+    g = torch.Generator().manual_seed(0)
+    params = [torch.nn.Parameter(torch.randn(n, generator=g)) for n in (300, 77, 1024, 5)]
+    opt = _MomentShard(params, rank)
+    sh = ShardedOptimizer(opt, GradArena(params, pad_to=world * 64))
+    opt.fill_shard()
+    kw = {"network_fn": torch.nn.Linear(2, 2), "network_fine": None, "embed_fn": torch.nn.Linear(3, 1)}
+    wrote = save_checkpoint(os.path.join(out_dir, "ckpt.tar"), 42, kw, opt, sharded=sh)
+    np.save(os.path.join(out_dir, f"wrote_{rank}.npy"), np.array([int(wrote)]))
+    dist.destroy_process_group()
+
+
+def test_sharded_checkpoint_collective_save(tmp_path):
+    """save_checkpoint(sharded=...) is collective: every rank calls it, the moment shards are
+    assembled with one all-reduce, and exactly one rank (0) writes the reference's dict."""
+    world = 2
+    mp.start_processes(_ckpt_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    assert [int(np.load(tmp_path / f"wrote_{r}.npy")[0]) for r in range(world)] == [1, 0]
+    ck = torch.load(tmp_path / "ckpt.tar", weights_only=True)
+    assert ck["global_step"] == 42
+    for i, n in enumerate((300, 77, 1024, 5)):
+        idx = torch.arange(n, dtype=torch.float32) + 1
+        st = ck["optimizer_state_dict"]["state"][i]
+        torch.testing.assert_close(st["exp_avg"], idx, rtol=0, atol=0)
+        torch.testing.assert_close(st["exp_avg_sq"], 2 * idx, rtol=0, atol=0)

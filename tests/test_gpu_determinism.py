@@ -125,6 +125,73 @@ def test_mlp_bwd_batch_deterministic(nerf, gpu):
         torch.testing.assert_close(x, y, rtol=1e-4, atol=1e-5 * float(y.abs().max()))
 
 
+def test_mlp_bwd_batch_concurrent_streams_bitwise(nerf, gpu):
+    """The C-ABI is stateless (SURVEY.md §8(b) Threading): two nerf_mlp_bwd_batch problems launched
+    on two streams at once — small enough (96 blocks each) that their blocks run side by side on the
+    256 CUs — give bit-identical results to the same launches run one after the other (deterministic
+    mode, one reduction workspace per stream)."""
+    from indoor_nerf_amd import _lib, field
+    torch.manual_seed(11)
+    sizes = (8192, 4096)
+    spr = (192, 64)
+    lib = _lib.load()
+
+    def problem(seed):
+        g = torch.Generator(device=gpu).manual_seed(seed)
+        nets = [nerf.NeRFSmall(2, 64, 15, 3, 64, 32, 16).to(gpu) for _ in range(2)]
+        feats = [torch.randn(16, P, 2, device=gpu, generator=g) * 0.3 for P in sizes]
+        vds = [torch.nn.functional.normalize(torch.randn(P // s, 3, device=gpu, generator=g), dim=-1)
+               for P, s in zip(sizes, spr)]
+        graws = [torch.randn(P, 4, device=gpu, generator=g) for P in sizes]
+        ws = torch.empty(int(lib.nerf_mlp_bwd_det_workspace_bytes()) // 4, device=gpu)
+        return dict(nets=nets, feats=feats, vds=vds, graws=graws, ws=ws)
+
+    def launch(pr, dfs, stream):
+        jobs = (_lib.MlpBwdJob * 2)()
+        for k, (n, P) in enumerate(zip(pr["nets"], sizes)):
+            j = jobs[k]
+            j.feat, j.feat_stride_point, j.feat_stride_level = _lib.ptr(pr["feats"][k]), 2, 2 * P
+            j.viewdirs, j.samples_per_ray, j.n_points = _lib.ptr(pr["vds"][k]), spr[k], P
+            j.weights = field._weights_struct(n.mlp_weights())
+            j.graw = _lib.ptr(pr["graws"][k])
+            j.grads = field._grads_struct(n.mlp_weights())
+            j.dfeat = _lib.ptr(dfs[k])
+        _lib.call("nerf_mlp_bwd_batch", jobs, 2, _lib.ptr(pr["ws"]), pr["ws"].numel() * 4,
+                  _lib.c_vp(stream.cuda_stream))
+
+    probs = [problem(100), problem(200)]
+
+    def run(concurrent, reps=6):
+        for pr in probs:
+            for n in pr["nets"]:
+                for p in n.parameters():
+                    p.grad = None
+        dfs = [[torch.empty(16, P, 2, device=gpu) for P in sizes] for _ in probs]
+        # .grad buffers exist before the streams fork (accumulate_grad_buffers allocates them)
+        for pr in probs:
+            for n in pr["nets"]:
+                field._grads_struct(n.mlp_weights())
+        torch.cuda.synchronize()
+        streams = [torch.cuda.Stream(device=gpu) for _ in probs]
+        for _ in range(reps):
+            if concurrent:
+                for pr, df, s in zip(probs, dfs, streams):
+                    launch(pr, df, s)
+            else:
+                for pr, df, s in zip(probs, dfs, streams):
+                    launch(pr, df, s)
+                    s.synchronize()
+        torch.cuda.synchronize()
+        return [p.grad.clone() for pr in probs for n in pr["nets"] for p in n.mlp_weights()] + \
+            [d.clone() for df in dfs for d in df]
+
+    serial = run(False)
+    for _ in range(3):
+        conc = run(True)
+        for x, y in zip(serial, conc):
+            assert torch.equal(x, y), "concurrent MLP backwards on two streams differ from serial execution"
+
+
 def test_train_iteration_bitwise_reproducible(nerf, gpu):
     from indoor_nerf_amd import model
     lo, hi = blender_bbox()

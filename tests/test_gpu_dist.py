@@ -134,3 +134,112 @@ def test_sharded_graphed_training_replicas_agree(tmp_path):
     assert all(torch.isfinite(torch.tensor(l)) for l in r0["losses"] + r1["losses"])
     for a, b in zip(r0["params"], r1["params"]):
         assert torch.equal(a, b)
+
+
+def _f10_model(nerf, dev, world):
+    """The lego configuration with F10's trained-like state (closed-form tables, the fixture's MLPs),
+    pytest draws on, the same model on every rank."""
+    import numpy as np
+    from tables import blender_bbox, closed_form_table
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    g = np.load(os.path.join(root, "tests", "golden", "f10_train.npz"))
+    lo, hi = blender_bbox()
+    args = nerf.make_args(bounding_box=(torch.from_numpy(lo), torch.from_numpy(hi)), finest_res=1024, N_samples=64,
+                          N_importance=128, white_bkgd=True, perturb=1.0, tv_loss_weight=1e-6, lrate=5e-4)
+    torch.manual_seed(0)
+    nerf.manual_seed(3)
+    kw, _, _, grad_vars, opt = nerf.create_nerf(args, device=dev)
+    kw.update(near=2.0, far=6.0, pytest=True)
+    table = closed_form_table(scale=float(g["table_scale"]), salt=3)
+    with torch.no_grad():
+        for prefix, net in (("coarse0_", kw["network_fn"]), ("fine0_", kw["network_fine"])):
+            for k, p in net.named_parameters():
+                p.copy_(torch.from_numpy(g[prefix + k.replace(".", "_")]))
+        for i, e in enumerate(kw["embed_fn"].embeddings):
+            e.weight.copy_(torch.from_numpy(table[i]))
+    params = grad_vars + list(kw["embed_fn"].parameters())
+    return args, kw, opt, params
+
+
+def _dp_worker(rank, world, port, out, R):
+    """One rank of the data-parallel equivalence test: this rank's contiguous 1/world of an R-ray
+    batch (world = 1: the whole batch in one process). (a) one iteration's gradients after the DP
+    all-reduce (mean); (b) 7 training iterations with the ZeRO-1 sharded optimizer (world > 1) or
+    plain RAdam (world = 1): the parameters."""
+    _init(rank, world, port)
+    import indoor_nerf_amd as nerf
+    from indoor_nerf_amd import render as rmod
+    from indoor_nerf_amd.model import forward_backward
+    from tables import synthetic_rays
+    dev = torch.device("cuda:0")
+    rmod.pytest_shard(rank, world)
+    ro, rd = synthetic_rays(R, seed=21)
+    target = torch.rand(R, 3, generator=torch.Generator().manual_seed(5))
+    n = R // world
+    rays = (torch.from_numpy(ro[rank * n:(rank + 1) * n]).to(dev), torch.from_numpy(rd[rank * n:(rank + 1) * n]).to(dev))
+    tgt = target[rank * n:(rank + 1) * n].to(dev)
+    res = {}
+    # (a) gradients of one iteration, all-reduced (mean over ranks)
+    args, kw, opt, params = _f10_model(nerf, dev, world)
+    arena = nerf.GradArena(params, defer_tables=True)
+    forward_backward(rays, tgt, kw, opt, args, 1, loss_scale_sparsity=float(world),
+                     tv_generator=torch.Generator().manual_seed(7), zero_grad=arena.zero_)
+    if world > 1:
+        arena.allreduce_mean()
+    torch.cuda.synchronize()
+    res["grads"] = [p.grad.detach().cpu().clone() for p in params]
+    # (b) 7 iterations
+    args, kw, opt, params = _f10_model(nerf, dev, world)
+    arena = nerf.GradArena(params, pad_to=world * 64 if world > 1 else 1, defer_tables=True)
+    hook = post = None
+    if world > 1:
+        sh = nerf.ShardedOptimizer(opt, arena)
+        hook, post = sh.reduce_grads, sh.gather_params
+    gen = torch.Generator().manual_seed(7)
+    losses = []
+    for it in range(1, 8):
+        loss, _ = nerf.train_step(rays, tgt, kw, opt, args, it, grad_hook=hook, post_hook=post,
+                                  loss_scale_sparsity=float(world), tv_generator=gen, zero_grad=arena.zero_)
+        losses.append(float(loss))
+    torch.cuda.synchronize()
+    res["params"] = [p.detach().cpu().clone() for p in params]
+    res["losses"] = losses
+    torch.save(res, os.path.join(out, f"dp{world}_{rank}.pt"))
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+def test_dp_shards_match_one_batch(tmp_path):
+    """SURVEY.md §8(e) through the HIP training step: 2 ranks x 2,048 rays (gloo, both ranks on the
+    one GPU) against 1 x 4,096 rays in one process — same weights (F10's trained-like state), the
+    same pytest draws (render.pytest_shard: each rank keeps its rows of the global batch's draws),
+    the same TV cuboids. After one iteration the all-reduced gradients match the single batch's:
+    table-gradient checksums to 1e-5 (fp32 atomics / per-rank rounding), MLP gradients to 2e-5 in
+    norm; after 7 iterations with the ZeRO-1 sharded optimizer the parameters match the single
+    process's plain RAdam within F10's bar (2e-5 relative + 1e-7 absolute)."""
+    R = 4096
+    mp.start_processes(_dp_worker, args=(1, _free_port(), str(tmp_path), R), nprocs=1, join=True,
+                       start_method="spawn")
+    mp.start_processes(_dp_worker, args=(2, _free_port(), str(tmp_path), R), nprocs=2, join=True,
+                       start_method="spawn")
+    one = torch.load(tmp_path / "dp1_0.pt", weights_only=True)
+    r0 = torch.load(tmp_path / "dp2_0.pt", weights_only=True)
+    r1 = torch.load(tmp_path / "dp2_1.pt", weights_only=True)
+    n_mlp = 10
+    for i, (a, b, c) in enumerate(zip(one["grads"], r0["grads"], r1["grads"])):
+        assert torch.equal(b, c), f"param {i}: the all-reduced gradients differ between ranks"
+        a, b = a.double(), b.double()
+        if i < n_mlp:
+            rel = float((a - b).norm() / a.norm())
+            assert rel <= 2e-5, f"MLP param {i}: DP gradient differs from the single batch by {rel:.2e} in norm"
+        else:
+            cs_a = [float((a * a).sum()), float(a.abs().sum())]
+            cs_b = [float((b * b).sum()), float(b.abs().sum())]
+            assert all(abs(x - y) <= 1e-5 * abs(x) for x, y in zip(cs_a, cs_b)), (i, cs_a, cs_b)
+            assert abs(float(a.sum()) - float(b.sum())) <= 1e-5 * cs_a[1], (i, float(a.sum()), float(b.sum()))
+    for i, (a, b, c) in enumerate(zip(one["params"], r0["params"], r1["params"])):
+        assert torch.equal(b, c), f"param {i}: replicas differ after 7 sharded steps"
+        torch.testing.assert_close(b, a, rtol=2e-5, atol=1e-7, msg=lambda m: f"param {i}: {m}")
+    # per-rank losses are those of different halves; their mean is the single batch's loss
+    for la, lb, lc in zip(one["losses"], r0["losses"], r1["losses"]):
+        assert abs(la - 0.5 * (lb + lc)) <= 1e-5 * abs(la) + 1e-7, (la, lb, lc)

@@ -174,9 +174,11 @@ def test_fused_priors_device_mode(nerf, gpu, golden):
     n = torch.from_numpy(g["a_normals"]).to(gpu).requires_grad_(True)
     xy = torch.from_numpy(g["a_coords"]).to(gpu)
     nerf.manual_seed(5)
-    t1, _ = priors.fused_structural_losses(d, n, xy)
+    from indoor_nerf_amd import _lib
+    ws = torch.empty(int(_lib.load().nerf_priors_workspace_bytes(d.shape[0])), dtype=torch.uint8, device=gpu)
+    t1, _ = priors.fused_structural_losses(d, n, xy, workspace=ws)
     t1.backward()
-    st = priors._FUSED_WS[str(gpu)][:1024].view(torch.float32).cpu()
+    st = ws[:1024].view(torch.float32).cpu()
     sti = st.view(torch.int32)
     assert int(sti[6]) == 1, "k-means ran"
     # PriorsState (csrc/priors_fused.hip): 14 ints, M, parts[7], centres[9], means[9], 6 ints, U, S, V, frame
@@ -200,6 +202,65 @@ def test_fused_priors_device_mode(nerf, gpu, golden):
     d2, n2 = d.detach().clone().requires_grad_(True), n.detach().clone().requires_grad_(True)
     t2, _ = priors.fused_structural_losses(d2, n2, xy)
     assert float(t1) == float(t2)
+
+
+@pytest.mark.gpu
+def test_fused_priors_ramp_and_state_per_call(nerf, gpu, golden):
+    """The ramp reaches the backward intact when the caller's scale tensor is a temporary (freed and
+    its memory reused before backward), and every forward keeps its own state: a second forward in
+    between (another batch, grad enabled) does not disturb the first one's backward. Gradients are
+    the ramp times F18's (the losses are linear in the weights' scale)."""
+    from indoor_nerf_amd import priors
+    g = golden("f18_priors")
+    ramp = 0.37
+    w = {"depth_prior": 1.0, "planarity": 0.5, "manhattan": 0.2, "normal_consistency": 0.1}
+    d = torch.from_numpy(g["a_depth"]).to(gpu).requires_grad_(True)
+    n = torch.from_numpy(g["a_normals"]).to(gpu).requires_grad_(True)
+    xy = torch.from_numpy(g["a_coords"]).to(gpu)
+    with replay(g, "a"):
+        total, _ = priors.fused_structural_losses(d, n, xy, w, 0.4, 0.5, scale=torch.full((1,), ramp, device=gpu),
+                                                  replay=True)
+    junk = [torch.full((1,), 123.0, device=gpu) for _ in range(64)]   # reuse of freed small blocks
+    d2 = torch.from_numpy(g["b_depth"]).to(gpu).requires_grad_(True)
+    n2 = torch.from_numpy(g["b_normals"]).to(gpu).requires_grad_(True)
+    with replay(g, "b"):
+        other, _ = priors.fused_structural_losses(d2, n2, None, w, 0.4, 0.5, replay=True)
+    total.backward()
+    del junk
+    np.testing.assert_allclose(float(total), ramp * float(g["a_total"]), rtol=1e-5)
+    for t, ref in ((d, g["a_dd"]), (n, g["a_dn"])):
+        got_g = t.grad.cpu().numpy()
+        scale = float(np.abs(ref).max()) * ramp + 1e-30
+        assert np.abs(got_g - ramp * ref).max() <= 1e-4 * scale, (np.abs(got_g - ramp * ref).max(), scale)
+    other.backward()
+    np.testing.assert_allclose(float(other), float(g["b_total"]), rtol=1e-5)
+
+
+@pytest.mark.gpu
+def test_graphed_priors_step_over_device_limit_runs_eager(nerf, gpu):
+    """More rays than the device priors take (PRIORS_MAX_RAYS): GraphedTrainStep uses the same
+    eligibility test as structural_loss and runs those iterations eagerly instead of capturing the
+    host-synchronising torch path."""
+    from indoor_nerf_amd import _lib
+    from indoor_nerf_amd.graphs import GraphedTrainStep
+    from indoor_nerf_amd.synthetic import scannet_bbox, scannet_rays
+    lo, hi = scannet_bbox()
+    R = _lib.PRIORS_MAX_RAYS + 64
+    args = nerf.make_args(bounding_box=(torch.from_numpy(lo), torch.from_numpy(hi)), finest_res=512,
+                          N_samples=32, N_importance=16, white_bkgd=False, use_structural_priors=True,
+                          structural_loss_start_iter=0, structural_loss_ramp_iters=10, tv_loss_weight=0.0)
+    torch.manual_seed(0)
+    nerf.manual_seed(11)
+    kw, _, _, _, opt = nerf.create_nerf(args, device=gpu)
+    kw.update(near=0.1, far=10.0)
+    ro, rd, _ = scannet_rays(R, seed=6)
+    rays = (torch.from_numpy(ro).to(gpu), torch.from_numpy(rd).to(gpu))
+    target = torch.rand(R, 3, device=gpu, generator=torch.Generator(device=gpu).manual_seed(1))
+    st = GraphedTrainStep(rays, target, kw, opt, args, warmup=1)
+    for it in range(1, 5):
+        loss, _ = st(it)
+        assert torch.isfinite(loss).item()
+    assert st.captures == 0 and st.graphs is None
 
 
 @pytest.mark.gpu
