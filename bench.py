@@ -36,6 +36,7 @@ X6_PEAK_TFLOPS = 2500.0 / 6
 # one or more ABI calls priced together: the hash backward is the bin pass (once per render pass)
 # plus the owner pass (once per iteration), and only their sum is a complete scatter-add.
 #   hash fwd : per point  16 levels x 8 corners x 8 B gathered + 12 B xyz + 128 B features + 1 B keep
+#   hash fwd packed (A-CAQ eval): as hash fwd with 2-B entries (two 8-bit codes)
 #   hash bwd : per point  16 x 8 x 8 B read+write of the added rows (2 x 1024) + 12 B xyz + 128 B d feat
 #   mlp fwd  : per point  9,344 MACs = 18,688 FLOP
 #   mlp bwd  : per point  2 x 18,688 FLOP (input + weight grads; the recomputed forward is not counted)
@@ -45,6 +46,9 @@ OPS = {
     "hash_bwd": dict(calls=("nerf_hash_encode_bwd_bin", "nerf_hash_encode_bwd_owner", "nerf_hash_encode_bwd_ws",
                             "nerf_hash_encode_bwd"), bound="hbm", per_unit=2 * 16 * 8 * 8 + 12 + 128, unit="point"),
     "hash_fwd": dict(calls=("nerf_hash_encode_fwd",), bound="hbm", per_unit=16 * 8 * 8 + 12 + 128 + 1, unit="point"),
+    # A-CAQ eval (int-packed tables, configs[4]): 8-bit codes = 2 B per corner entry (two features)
+    "hash_fwd_packed": dict(calls=("nerf_hash_encode_fwd_packed",), bound="hbm", per_unit=16 * 8 * 2 + 12 + 128 + 1,
+                            unit="point"),
     "mlp_bwd": dict(calls=("nerf_mlp_bwd", "nerf_mlp_bwd_batch"), bound="mfma", per_unit=2 * 18688, unit="point"),
     "mlp_fwd": dict(calls=("nerf_mlp_fwd",), bound="mfma", per_unit=18688, unit="point"),
     "composite_fwd": dict(calls=("nerf_composite_fwd",), bound="hbm", per_unit=24, unit="sample"),
@@ -62,6 +66,7 @@ STEP_RAY_BYTES = 64
 # ABI call -> the kernel symbols it launches (rocprofv3 names), to attach PMC traffic per call
 KERNEL_SYMBOLS = {
     "nerf_hash_encode_fwd": ["nerf::hash_encode_fwd_pair_kernel<false>"],
+    "nerf_hash_encode_fwd_packed": ["nerf::hash_encode_fwd_packed_kernel"],
     "nerf_hash_encode_bwd_bin": ["nerf::hash_encode_bwd_kernel<3, 512>"],
     "nerf_tv_bwd_bin": ["nerf::tv_bwd_bin_kernel<512>"],
     "nerf_hash_encode_bwd_owner": ["nerf::hash_bwd_owner_kernel<13, 1024, false>"],

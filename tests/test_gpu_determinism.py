@@ -309,7 +309,8 @@ def test_check_numerics_flags_nan_and_inf(nerf, gpu):
     t["depth_map"][4000] = float("nan")
     t["acc_map"][3] = float("inf")
     assert nerf.check_numerics(t) == ["depth_map", "acc_map"]
-    from indoor_nerf_amd import render
+    import importlib
+    render = importlib.import_module("indoor_nerf_amd.render")   # the module (the package re-exports render())
     lo, hi = blender_bbox()
     args = nerf.make_args(bounding_box=(torch.from_numpy(lo), torch.from_numpy(hi)), finest_res=1024, N_samples=64,
                           N_importance=64, white_bkgd=True)
