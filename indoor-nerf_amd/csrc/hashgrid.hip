@@ -15,6 +15,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "hash_common.h"
 
@@ -199,7 +200,14 @@ constexpr int kChunkPts = NERF_HASH_CHUNK_POINTS;   // points per chunk = thread
 constexpr int kChunkCap = kChunkPts * 8;            // entries per chunk (8 corners per point)
 constexpr int kChunkCapLog2 = kChunkPts == 256 ? 11 : kChunkPts == 512 ? 12 : 13;
 static_assert(kChunkPts == 256 || kChunkPts == 512 || kChunkPts == 1024, "chunk of 256, 512 or 1024 points");
-constexpr int kSliceLog2 = 13;            // owner slice: 2^13 rows x 16 B (fp64 pair) = 128 KiB of LDS
+#ifndef NERF_OWNER_ACC32
+#define NERF_OWNER_ACC32 0
+#endif
+#ifndef NERF_OWNER_SLICE_LOG2
+#define NERF_OWNER_SLICE_LOG2 13
+#endif
+constexpr bool kOwnerAcc32 = NERF_OWNER_ACC32 != 0;   // fp32 LDS accumulators (ds_add_f32) instead of fp64
+constexpr int kSliceLog2 = NERF_OWNER_SLICE_LOG2;     // owner slice: 2^13 rows x 16 B (fp64 pair) = 128 KiB of LDS
 constexpr int kSliceLog2Det = 12;         // deterministic: 2^12 rows x 32 B (two int64 words per feature)
 constexpr int kMaxOwnersLog2 = 7;
 constexpr int kMaxOwners = 1 << kMaxOwnersLog2;
@@ -476,24 +484,48 @@ __global__ void __launch_bounds__(THREADS) tv_bwd_bin_kernel(TVParams P, HashGra
 // hi = rint(v 2^s), lo = rint((v 2^s - hi) 2^L); the slice is summed with ds_add_u64 and the row
 // total hi 2^-s + lo 2^-(s+L) (about 2^-75 of the level's largest entry per term) is rounded to fp32
 // once. Slices are 2^12 rows (32 B of LDS per row).
+#ifdef NERF_OWNER_PROF   // diagnostic build only (tools/owner_prof.py): per-block timestamps (100 MHz real
+                        // time): start, first window scanned, entries summed, flushed
+__device__ unsigned long long owner_prof[NERF_MAX_LEVELS * kMaxOwners * 4];
+#define OWNER_T(k)                                                                                         \
+    do {                                                                                                   \
+        if (threadIdx.x == 0)                                                                              \
+            owner_prof[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 4 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define OWNER_T(k) do { } while (0)
+#endif
+
 template <int SLICE_LOG2, int THREADS, bool DET>
 __global__ void __launch_bounds__(THREADS) hash_bwd_owner_kernel(HashGradParams hp) {
+    OWNER_T(0);
     constexpr int kOwnerThreads = THREADS;
+#ifndef NERF_OWNER_BATCH
+#define NERF_OWNER_BATCH 8
+#endif
+    constexpr int NB = NERF_OWNER_BATCH;                   // steps per software-pipelined batch
     constexpr int kScanPer = 4;                            // chunks per thread in the window scan
     constexpr int kOwnerWindow = kScanPer * THREADS;       // chunks per window (the fine + coarse + TV
                                                            // chunks of a 4096-ray step fit one window)
     // fp64 accumulators: ds_add_f64 runs ~14x the rate of ds_add_f32 on gfx950 (tools/
     // lds_atomic_bench.hip: 2.24 vs 0.165 row updates per clock per CU, random rows), and the
     // slice total is rounded to fp32 once.
-    __shared__ __attribute__((aligned(16))) double2 s_slice[(DET ? 2 : 1) << SLICE_LOG2];
+    constexpr bool A32 = kOwnerAcc32 && !DET;
+    using Acc = typename std::conditional<A32, float2, double2>::type;
+    __shared__ __attribute__((aligned(16))) Acc s_slice[(DET ? 2 : 1) << SLICE_LOG2];
+    static_assert(sizeof(s_slice) <= 128 * 1024, "owner slice accumulators");
     unsigned long long* s_fix = reinterpret_cast<unsigned long long*>(s_slice);   // DET: [row][hi x, hi y, lo x, lo y]
     __shared__ uint32_t s_pre[kOwnerWindow + 1];
     __shared__ uint16_t s_beg[kOwnerWindow];
     __shared__ uint32_t s_wsum[kOwnerThreads / 64];
+#ifdef NERF_OWNER_REVERSE   // A/B: finest (heaviest) levels dispatched first
+    const int o = blockIdx.x, lvl = gridDim.y - 1 - blockIdx.y;
+#else
     const int o = blockIdx.x, lvl = blockIdx.y;
+#endif
     const int S = 1 << hp.slice_log2, n_own = 1 << hp.owner_log2;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    for (int i = tid; i < (DET ? 2 : 1) * S; i += kOwnerThreads) s_slice[i] = make_double2(0.0, 0.0);
+    for (int i = tid; i < (DET ? 2 : 1) * S; i += kOwnerThreads) s_slice[i] = Acc{0, 0};
     // DET: scale exponents (hi: 2^sh, lo: 2^(sh + L)) from the level's largest |entry| (the max of
     // the chunks' maxima; a level without entries has max 0)
     int sh = 0, sl_ = 0;
@@ -542,6 +574,7 @@ __global__ void __launch_bounds__(THREADS) hash_bwd_owner_kernel(HashGradParams 
         }
         if (nw == kOwnerWindow && tid == kOwnerThreads - 1) s_pre[nw] = ex;   // no thread holds i == nw
         __syncthreads();
+        if (w0 == 0) OWNER_T(1);
         // The window's entries split evenly across the waves; a wave walks its range 64 entries
         // (one per lane) per step. Chunk lookup is wave-cooperative, with no per-lane walk: lane l
         // holds the boundary s_pre[cw + l] of a 64-chunk window; the chunk of entry e is the last
@@ -552,7 +585,8 @@ __global__ void __launch_bounds__(THREADS) hash_bwd_owner_kernel(HashGradParams 
         const uint32_t tot = s_pre[nw];
         const uint32_t e_beg = (uint32_t)((uint64_t)tot * wave / kWaves);
         const uint32_t e_end = (uint32_t)((uint64_t)tot * (wave + 1) / kWaves);
-        const size_t region0 = ((size_t)lvl * hp.chunk_stride + w0) * kChunkCap;
+        // entry offsets fit 32 bits (make_bin_plan: < 2^32 entries), one VGPR per address
+        const uint32_t region0 = (uint32_t)(((size_t)lvl * hp.chunk_stride + w0) * kChunkCap);
         int cw = 0;
         uint32_t Bw = 0, Gw = 0, B63 = 0;   // B63: first entry beyond the window's chunks cw .. cw+62
         auto reload = [&](uint32_t E) {
@@ -568,11 +602,16 @@ __global__ void __launch_bounds__(THREADS) hash_bwd_owner_kernel(HashGradParams 
             B63 = __builtin_amdgcn_readlane(Bw, 63);
         };
         // address of entry E + lane (ok: inside [E, end of step)); returns the next step's start
-        auto step = [&](uint32_t E, size_t& addr, bool& ok) -> uint32_t {
+        auto step = [&](uint32_t E, uint32_t& addr, bool& ok) -> uint32_t {
             if (E >= e_end) { addr = region0; ok = false; return E; }
             if (E >= B63) reload(E);
             const uint32_t lim = min(min(E + 64u, B63), e_end);
             const uint32_t e = E + lane;
+#ifdef NERF_OWNER_AB_NO_LOOKUP   // diagnostic A/B only: no entry -> chunk lookup (wrong addresses)
+            ok = e < lim;
+            addr = region0 + e;
+            return lim;
+#endif
             int idx = __popcll(__ballot(Bw <= E)) - 1;
             uint64_t inner = __ballot(Bw > E && Bw < lim);
             while (inner) {
@@ -583,32 +622,37 @@ __global__ void __launch_bounds__(THREADS) hash_bwd_owner_kernel(HashGradParams 
             const uint32_t cur = (uint32_t)__builtin_amdgcn_ds_bpermute(idx << 2, (int)Bw);
             const uint32_t beg = (uint32_t)__builtin_amdgcn_ds_bpermute(idx << 2, (int)Gw);
             ok = e < lim;
-            addr = ok ? region0 + (size_t)(cw + idx) * kChunkCap + beg + (e - cur) : region0;
+            addr = ok ? region0 + (uint32_t)(cw + idx) * kChunkCap + beg + (e - cur) : region0;
             return lim;
         };
-        auto track = [&](uint32_t& E, size_t (&addr)[8], uint32_t& valid) {
+        auto track = [&](uint32_t& E, uint32_t (&addr)[NB], uint32_t& valid) {
             valid = 0;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
+            for (int j = 0; j < NB; ++j) {
                 bool ok;
                 E = step(E, addr[j], ok);
                 valid |= (ok ? 1u : 0u) << j;
             }
         };
-        auto fetch = [&](const size_t (&addr)[8], uint16_t (&h)[8], float2 (&g)[8]) {
+        auto fetch = [&](const uint32_t (&addr)[NB], uint16_t (&h)[NB], float2 (&g)[NB]) {
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
+            for (int j = 0; j < NB; ++j) {
                 // default-policy loads: the coarse pass's bins were written just before this launch and part
                 // of them is still in the Infinity Cache (nontemporal loads: 0.39 vs 0.33 ms per step)
+#ifdef NERF_OWNER_AB_NO_LOAD   // diagnostic A/B only: no entry loads (lookup + LDS sums alone)
+                h[j] = (uint16_t)((addr[j] * 2654435761u) >> 19);
+                g[j] = make_float2((float)(addr[j] & 255), 1.f);
+#else
                 h[j] = hp.bin_h[addr[j]];
                 const uint64_t gv = *reinterpret_cast<const uint64_t*>(hp.bin_g + addr[j]);   // (d feat0, d feat1)
                 g[j] = make_float2(__uint_as_float((uint32_t)gv), __uint_as_float((uint32_t)(gv >> 32)));
+#endif
             }
         };
         // software pipeline: the next batch's loads are in flight while this batch's adds run
-        size_t addr[8];
-        uint16_t h[8];
-        float2 g[8];
+        uint32_t addr[NB];
+        uint16_t h[NB];
+        float2 g[NB];
         uint32_t valid;
         uint32_t E = e_beg;
         if (E < e_end) reload(E);
@@ -617,14 +661,14 @@ __global__ void __launch_bounds__(THREADS) hash_bwd_owner_kernel(HashGradParams 
         // the loop and step() (ballots, readlane, bpermute) stay wave-uniform: exit only when no
         // lane of the wave has an entry left
         while (__ballot(valid != 0u) != 0ull) {
-            size_t addr2[8];
-            uint16_t h2[8];
-            float2 g2[8];
+            uint32_t addr2[NB];
+            uint16_t h2[NB];
+            float2 g2[NB];
             uint32_t valid2;
             track(E, addr2, valid2);
             fetch(addr2, h2, g2);
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
+            for (int j = 0; j < NB; ++j) {
                 if (valid & (1u << j)) {
                     if constexpr (DET) {
                         const double tx = ldexp((double)g[j].x, sh), ty = ldexp((double)g[j].y, sh);
@@ -637,13 +681,25 @@ __global__ void __launch_bounds__(THREADS) hash_bwd_owner_kernel(HashGradParams 
                         atomicAdd(r + 2, (unsigned long long)lx);
                         atomicAdd(r + 3, (unsigned long long)ly);
                     } else {
-                        atomicAdd(&s_slice[h[j]].x, (double)g[j].x);
-                        atomicAdd(&s_slice[h[j]].y, (double)g[j].y);
+#ifdef NERF_OWNER_AB_NO_ATOMIC   // diagnostic A/B only: plain LDS read-modify-write (racy) instead of atomics
+                        Acc t = s_slice[h[j]];
+                        t.x += g[j].x;
+                        t.y += g[j].y;
+                        s_slice[h[j]] = t;
+#else
+                        if constexpr (A32) {
+                            atomicAdd(&s_slice[h[j]].x, g[j].x);
+                            atomicAdd(&s_slice[h[j]].y, g[j].y);
+                        } else {
+                            atomicAdd(&s_slice[h[j]].x, (double)g[j].x);
+                            atomicAdd(&s_slice[h[j]].y, (double)g[j].y);
+                        }
+#endif
                     }
                 }
             }
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
+            for (int j = 0; j < NB; ++j) {
                 h[j] = h2[j];
                 g[j] = g2[j];
             }
@@ -654,6 +710,12 @@ __global__ void __launch_bounds__(THREADS) hash_bwd_owner_kernel(HashGradParams 
     // Flush: every row's table load is issued before any add (one memory round trip per block,
     // not one per row batch: a load behind the previous batch's store left 8 serial round trips).
     __syncthreads();
+    OWNER_T(2);
+#ifdef NERF_OWNER_PROF
+    struct Done {
+        __device__ ~Done() { __syncthreads(); OWNER_T(3); }
+    } done;
+#endif
     float2* dt = reinterpret_cast<float2*>(hp.dtables[lvl]) + (size_t)o * S;
     constexpr int kRows = (1 << SLICE_LOG2) / kOwnerThreads;
     if constexpr (DET) {
@@ -674,27 +736,29 @@ __global__ void __launch_bounds__(THREADS) hash_bwd_owner_kernel(HashGradParams 
     }
     if (hp.overwrite) {   // rows without entries become +0, as after a memset
         for (int i = tid; i < S; i += kOwnerThreads) {
-            const double2 v = s_slice[i];
+            const Acc v = s_slice[i];
             dt[i] = make_float2((float)v.x, (float)v.y);
         }
         return;
     }
+    // the row's prior gradient plus the slice's sum: in fp32 (A32, as the reference's accumulating
+    // .grad) or with the fp64 sum rounded once
+    auto plus = [](float t, auto v) { return A32 ? (float)(t + v) : (float)((double)t + (double)v); };
     if (S == (1 << SLICE_LOG2)) {
         float2 t[kRows];
 #pragma unroll
         for (int k = 0; k < kRows; ++k) t[k] = dt[tid + k * kOwnerThreads];
 #pragma unroll
         for (int k = 0; k < kRows; ++k) {
-            const double2 v = s_slice[tid + k * kOwnerThreads];
-            if (v.x != 0.0 || v.y != 0.0)
-                dt[tid + k * kOwnerThreads] = make_float2((float)((double)t[k].x + v.x), (float)((double)t[k].y + v.y));
+            const Acc v = s_slice[tid + k * kOwnerThreads];
+            if (v.x != 0 || v.y != 0) dt[tid + k * kOwnerThreads] = make_float2(plus(t[k].x, v.x), plus(t[k].y, v.y));
         }
     } else {   // small tables (log2_T < slice): one partial slice per level
         for (int i = tid; i < S; i += kOwnerThreads) {
-            const double2 v = s_slice[i];
-            if (v.x != 0.0 || v.y != 0.0) {
+            const Acc v = s_slice[i];
+            if (v.x != 0 || v.y != 0) {
                 const float2 t = dt[i];
-                dt[i] = make_float2((float)((double)t.x + v.x), (float)((double)t.y + v.y));
+                dt[i] = make_float2(plus(t.x, v.x), plus(t.y, v.y));
             }
         }
     }
@@ -713,6 +777,7 @@ static bool make_bin_plan(int n_levels, int log2_T, int64_t n_points, BinPlan& B
     B.owner_log2 = log2_T - B.slice_log2;
     B.nchunks = (int)((n_points + kChunkPts - 1) / kChunkPts);
     const size_t entries = (size_t)n_levels * B.nchunks * kChunkCap;
+    if (entries >= ((size_t)1 << 32)) return false;   // the owner pass indexes entries with 32 bits
     const size_t offs = (size_t)n_levels * B.nchunks * (1 << B.owner_log2);
     auto up = [](size_t v) { return (v + 255) & ~(size_t)255; };
     B.off_g = 0;
@@ -810,6 +875,12 @@ static int bin_layout(const char* who, int n_levels, int log2_T, int64_t chunk_c
 }
 
 extern "C" int nerf_hash_bwd_chunk_points(void) { return kChunkPts; }
+
+#ifdef NERF_OWNER_PROF
+extern "C" int nerf_owner_prof_read(unsigned long long* host, int n) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(owner_prof), sizeof(unsigned long long) * (size_t)n);
+}
+#endif
 
 extern "C" size_t nerf_hash_encode_bwd_workspace_bytes(int n_levels, int log2_T, int64_t n_points, int deterministic) {
     BinPlan B{};

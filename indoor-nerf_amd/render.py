@@ -29,7 +29,15 @@ _SEED_GEN = None
 
 # run_nerf.py:40 DEBUG: when True, render_rays tests every returned tensor for NaN/Inf (one fused
 # device count, csrc/checks.hip, and one host read per call) and prints the reference's message.
+# The package namespace re-exports the render() function under this module's name, so set it with
+# set_debug() (or on the module: importlib.import_module("indoor_nerf_amd.render").DEBUG).
 DEBUG = False
+
+
+def set_debug(enabled=True):
+    """run_nerf.py:40's module flag (DEBUG = True) for this package."""
+    global DEBUG
+    DEBUG = bool(enabled)
 
 
 def check_numerics(ret):

@@ -401,13 +401,29 @@ CONVERGE = dict(iters=300, R=256, every=20, lrate=5e-3, lrate_decay=500, sparsit
                 table_salt=19, seeds=(30, 31), batch_seed=20, threads=(8, 4, 6, 2, 3, 5))
 
 
-def converge_run(ref, c, threads):
+def ulp_nudge(table, seed, frac=0.01):
+    """The initial table with `frac` of its entries moved by one float32 ulp (random direction),
+    seeded: a rounding-level change of the starting state."""
+    rng = np.random.RandomState(1000 + seed)
+    mask = rng.rand(*table.shape) < frac
+    up = rng.rand(*table.shape) < 0.5
+    out = table.copy()
+    out[mask & up] = np.nextafter(table[mask & up], np.float32(np.inf))
+    out[mask & ~up] = np.nextafter(table[mask & ~up], np.float32(-np.inf))
+    return out
+
+
+def converge_run(ref, c, threads, nudge=None):
     """One reference training run of F19 with `threads` CPU threads (torch's CPU kernels split their
     reductions by thread, so two thread counts are two runs of the same algorithm whose float sums
-    differ in order: the reference's own run-to-run spread)."""
+    differ in order: the reference's own run-to-run spread). nudge: seed of a one-ulp change of 1 %
+    of the initial table entries (ulp_nudge), for runs beyond the thread-count variants."""
     torch.set_num_threads(threads)
     (ro, rd, rgb), (eo, ed, ergb), (no, nd, nrgb) = tables_convergence()
-    emb = make_embedder(ref, 1024, closed_form_table(scale=c["table_scale"], salt=c["table_salt"]))
+    table = closed_form_table(scale=c["table_scale"], salt=c["table_salt"])
+    if nudge is not None:
+        table = ulp_nudge(table, nudge)
+    emb = make_embedder(ref, 1024, table)
     coarse, fine = make_mlp(ref, c["seeds"][0]), make_mlp(ref, c["seeds"][1])
     init = {**mlp_arrays(coarse, "coarse0_"), **mlp_arrays(fine, "fine0_")}
     grad_vars = list(coarse.parameters()) + list(fine.parameters())
@@ -478,6 +494,36 @@ def gen_converge(ref, out, iters=None):
     d.update(init)
     d.update(batches=batches, eval_iters=eval_iters, config=np.array(repr(c)))
     np.savez_compressed(os.path.join(out, "f19_converge.npz"), **d)
+
+
+def gen_converge_more(ref, out, start=0, count=18, threads=2):
+    """F19b: more reference runs of F19's training (same scene, batches, MLP init, hyper-parameters),
+    each from the initial table with a seeded one-ulp change of 1 % of its entries (ulp_nudge, seeds
+    start .. start + count - 1): the thread-count variants of F19 do not vary the table-gradient
+    summation order (embedding_dense_backward sums each row in one fixed order whatever the thread
+    count), and the mid-training PSNR is sensitive to every rounding-level difference, so the
+    reference's run-to-run distribution is sampled with rounding changes of its starting state.
+    Writes f19b_converge_part{start}.npz (merge_converge_more joins the parts)."""
+    c = dict(CONVERGE)
+    d = {}
+    for k in range(start, start + count):
+        _, _, eval_iters, curves = converge_run(ref, c, threads, nudge=k)
+        d.update({f"{name}_n{k}": v for name, v in curves.items()})
+        d["eval_iters"] = eval_iters
+        np.savez_compressed(os.path.join(out, f"f19b_converge_part{start}.npz"), seeds=np.arange(start, k + 1), **d)
+
+
+def merge_converge_more(out):
+    """Join the f19b parts into f19b_converge.npz (runs keyed by their nudge seed)."""
+    parts = sorted(f for f in os.listdir(out) if f.startswith("f19b_converge_part"))
+    d, seeds = {}, []
+    for f in parts:
+        z = np.load(os.path.join(out, f))
+        seeds += [int(v) for v in z["seeds"]]
+        d.update({k: z[k] for k in z.files if k != "seeds"})
+    np.savez_compressed(os.path.join(out, "f19b_converge.npz"), seeds=np.array(sorted(seeds)), **d)
+    for f in parts:
+        os.remove(os.path.join(out, f))
 
 
 def tables_convergence():
@@ -926,4 +972,9 @@ def main(only=None):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1:])
+    if sys.argv[1:2] == ["converge_more"]:    # make_golden.py converge_more START COUNT THREADS
+        gen_converge_more(load_reference(), HERE, *(int(v) for v in sys.argv[2:5]))
+    elif sys.argv[1:2] == ["converge_merge"]:
+        merge_converge_more(HERE)
+    else:
+        main(sys.argv[1:])

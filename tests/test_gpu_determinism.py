@@ -317,10 +317,11 @@ def test_check_numerics_flags_nan_and_inf(nerf, gpu):
     kw, _, _, _, _ = nerf.create_nerf(args, device=gpu)
     kw.update(near=2.0, far=6.0)
     ro, rd = synthetic_rays(256, seed=2)
-    render.DEBUG = True
+    nerf.set_debug(True)
+    assert render.DEBUG
     try:   # the hook runs inside render_rays (run_nerf.py:545-547) and reports nothing for finite outputs
         with torch.no_grad():
             out = nerf.render(800, 800, None, rays=(torch.from_numpy(ro).to(gpu), torch.from_numpy(rd).to(gpu)), **kw)
         assert nerf.check_numerics({"rgb_map": out[0], "acc_map": out[2]}) == []
     finally:
-        render.DEBUG = False
+        nerf.set_debug(False)

@@ -41,11 +41,38 @@ class _Embed64(torch.autograd.Function):
         return None, acc.float()
 
 
-def apply_variants(variants):
+class _Embed32Shuffled(torch.autograd.Function):
+    """F.embedding whose table gradient is summed in fp32 in a seeded random order of the (point,
+    corner) contributions instead of embedding_dense_backward's fixed order (the reference runs all
+    share that order whatever their thread count)."""
+    gen = torch.Generator().manual_seed(0)
+
+    @staticmethod
+    def forward(ctx, idx, table):
+        ctx.save_for_backward(idx)
+        ctx.shape = table.shape
+        return table[idx]
+
+    @staticmethod
+    def backward(ctx, g):
+        (idx,) = ctx.saved_tensors
+        i = idx.reshape(-1)
+        perm = torch.randperm(i.numel(), generator=_Embed32Shuffled.gen)
+        acc = torch.zeros(ctx.shape, dtype=torch.float32)
+        acc.index_add_(0, i[perm], g.reshape(-1, ctx.shape[1])[perm])
+        return None, acc
+
+
+def apply_variants(variants, seed=0):
     if "gsum64" in variants:
         orc.F = type("F", (), {k: getattr(torch.nn.functional, k) for k in dir(torch.nn.functional)
                                if not k.startswith("_")})
         orc.F.embedding = staticmethod(lambda idx, table: _Embed64.apply(idx, table))
+    if "gsum32shuf" in variants:
+        _Embed32Shuffled.gen.manual_seed(seed)
+        orc.F = type("F", (), {k: getattr(torch.nn.functional, k) for k in dir(torch.nn.functional)
+                               if not k.startswith("_")})
+        orc.F.embedding = staticmethod(lambda idx, table: _Embed32Shuffled.apply(idx, table))
     if "comp64" in variants:
         base = orc.composite
 
@@ -62,10 +89,10 @@ def main():
     ap.add_argument("--stats", default="")
     ap.add_argument("--out", default="")
     ap.add_argument("--variant", default="", help="comma list: gsum64 (table gradients summed in fp64, as the "
-                    "HIP owner pass), comp64 (compositing in fp64)")
+                    "HIP owner pass), gsum32shuf (fp32 sums in a seeded random order), comp64 (compositing in fp64)")
     a = ap.parse_args()
     torch.set_num_threads(a.threads)
-    apply_variants([v for v in a.variant.split(",") if v])
+    apply_variants([v for v in a.variant.split(",") if v], seed=a.threads)
     g = np.load(os.path.join(ROOT, "tests", "golden", "f19_converge.npz"))
     import ast
     c = ast.literal_eval(str(g["config"]))
