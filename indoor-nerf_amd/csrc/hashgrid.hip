@@ -42,97 +42,11 @@ struct HashGradParams {
     int overwrite;        // owner pass: store every row (the gradients are logically zero), no loads
 };
 
-// QUANT: every gathered corner feature goes through the level's A-CAQ quantizer first
-// (hash_encoding.py:97-101: quantizers[i](voxel_embedds), elementwise on the [P,8,2] gather).
-// Lane-pair forward: lanes 2m and 2m+1 share point m of the wave and gather the x = 0 and x = 1
-// corners of its voxel. Corners (x,y,z) and (x+1,y,z) hash to h and h ^ (x ^ (x+1)), the same 64-B
-// line for 15 of 16 x, so each gather instruction touches ~32 lines instead of 64 (the vector
-// memory path processes a wave instruction's distinct lines one after another). The x blend
-// c_jk = e(0,j,k)(1-wx) + e(1,j,k)wx becomes a + partner's b (IEEE addition commutes: bit-exact).
-// value of the other lane of the pair (lanes 2m <-> 2m+1): DPP quad_perm [1,0,3,2], no LDS round
-// trip (ds_bpermute)
-__device__ __forceinline__ int pair_swap_i(int v) { return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false); }
-__device__ __forceinline__ float pair_swap(float v) { return __int_as_float(pair_swap_i(__float_as_int(v))); }
-
-// The three axes of a point for lane xb of its pair: both lanes need all three, so lane 0 computes
-// (x, y) and lane 1 (x, z) and they swap the y / z results (4 divisions per lane, not 6).
-template <bool FAST>
-__device__ __forceinline__ void fwd_axes(float x, float y, float z, const HashParams& hp, int lvl, int xb,
-                                         AxisCell& ax, AxisCell& ay, AxisCell& az) {
-    ax = axis_cell<FAST>(x, hp.bmin[0], hp.bmax[0], hp.cell[lvl][0]);
-    const AxisCell a2 = axis_cell<FAST>(xb ? z : y, xb ? hp.bmin[2] : hp.bmin[1], xb ? hp.bmax[2] : hp.bmax[1],
-                                        xb ? hp.cell[lvl][2] : hp.cell[lvl][1]);
-    const int pk = a2.base | (a2.inside ? 0x40000000 : 0);   // 0 <= base <= res < 2^30
-    const int opk = pair_swap_i(pk);
-    const float ow = pair_swap(a2.w);
-    AxisCell o;
-    o.base = opk & 0x3FFFFFFF;
-    o.inside = (opk & 0x40000000) != 0;
-    o.w = ow;
-    ay = xb ? o : a2;
-    az = xb ? a2 : o;
-}
-
-// One (point, level) of a lane pair: the axes and the four gathers are issued first (fwd_gather),
-// the blend and the store follow (fwd_finish), so a thread can keep several levels' gathers in flight.
-struct FwdLvl {
-    float wx, wy, wz;
-    bool inside;
-    float2 e[4];   // corners (xb, j, k), index 2j + k
-};
-
-template <bool FAST>
-__device__ __forceinline__ void fwd_gather(float x, float y, float z, const HashParams& hp, int lvl, int xb,
-                                           FwdLvl& s) {
-    AxisCell ax, ay, az;
-    fwd_axes<FAST>(x, y, z, hp, lvl, xb, ax, ay, az);
-    s.wx = ax.w; s.wy = ay.w; s.wz = az.w;
-    s.inside = ax.inside && ay.inside && az.inside;
-    const float2* __restrict__ tab = reinterpret_cast<const float2*>(hp.tables[lvl]);
-    const uint32_t bx = (uint32_t)ax.base + (uint32_t)xb, by = (uint32_t)ay.base, bz = (uint32_t)az.base;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) s.e[c] = tab[spatial_hash3(bx, by + ((c >> 1) & 1), bz + (c & 1), hp.mask)];
-}
-
-template <bool QUANT>
-__device__ __forceinline__ void fwd_finish(FwdLvl& s, int lvl, int xb, bool valid, int64_t p,
-                                           float* __restrict__ feat, int64_t sp, int64_t sl,
-                                           uint8_t* __restrict__ keep, const QuantRec* __restrict__ qrec) {
-    if constexpr (QUANT) {
-        const QuantRec q = qrec[lvl];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            s.e[c].x = fake_quant(s.e[c].x, q);
-            s.e[c].y = fake_quant(s.e[c].y, q);
-        }
-    }
-    const float wx = s.wx, wy = s.wy, wz = s.wz;
-    const float fx = xb ? wx : 1.0f - wx;
-    float cx[4], cy[4];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        const float ax_ = s.e[c].x * fx, ay_ = s.e[c].y * fx;
-        cx[c] = ax_ + pair_swap(ax_);
-        cy[c] = ay_ + pair_swap(ay_);
-    }
-    const float oy = 1.0f - wy, oz = 1.0f - wz;
-    // c00 = cx[0], c01 = cx[1], c10 = cx[2], c11 = cx[3]
-    const float c0x = cx[0] * oy + cx[2] * wy, c1x = cx[1] * oy + cx[3] * wy;
-    const float c0y = cy[0] * oy + cy[2] * wy, c1y = cy[1] * oy + cy[3] * wy;
-    const float ox_ = c0x * oz + c1x * wz, oy_ = c0y * oz + c1y * wz;
-    if (!valid) return;
-    if (lvl == 0 && keep && xb == 0) keep[p] = s.inside ? 1 : 0;
-    float* dst = feat + p * sp + (int64_t)lvl * sl;
-    dst[xb] = xb ? oy_ : ox_;
-}
-
 // Grouped coarse levels: blockIdx.y == 0 runs levels [0, group) of its points, two levels' gathers
 // in flight at a time; the other rows run one level each (level-major: one table hot in each XCD's
 // L2). A coarse level alone is latency-bound (few, hot table lines; a single round trip per wave per
 // level): grouping the 6 coarse levels of the lego config took the forward from 121 to 107 us per
 // launch (same box; 3 or 6 levels in flight: 114 / 154 us, the registers cost occupancy).
-constexpr int kFwdGroupRound = 2;
-constexpr int kFwdGroupMax = 8;
 
 template <bool QUANT>
 __global__ void __launch_bounds__(256) hash_encode_fwd_pair_kernel(

@@ -290,6 +290,79 @@ __global__ void __launch_bounds__(256) hash_encode_fwd_packed_kernel(
     }
 }
 
+// Lane-pair packed gather (the fp32 forward's structure, hashgrid.hip hash_encode_fwd_pair_kernel):
+// lanes 2m and 2m+1 share point m and gather the x = 0 / x = 1 corners of its voxel, so corners
+// (x, y, z) and (x+1, y, z), which hash to h and h ^ (x ^ (x+1)), leave in one instruction's line;
+// level-major grid rows (one level's packed table hot in each XCD's L2), the coarse levels whose
+// (res + 1)^3 vertices fit the table grouped into row 0, and the fast division of the voxel math.
+// The dequantized corners blend exactly as the fp32 forward (bit-identical to the one-thread path).
+template <int BITS>
+__device__ __forceinline__ float2 packed_entry(const uint8_t* base, uint32_t h, const QuantRec& q) {
+    if constexpr (BITS == 32) {
+        return reinterpret_cast<const float2*>(base)[h];
+    } else {
+        float f0, f1;
+        load_codes<BITS>(base, h, q, f0, f1);
+        return make_float2(f0, f1);
+    }
+}
+
+template <int BITS, bool FAST>
+__device__ __forceinline__ void packed_gather(float x, float y, float z, const HashParams& hp, int lvl, int xb,
+                                              const uint8_t* base, const QuantRec& q, FwdLvl& s) {
+    AxisCell ax, ay, az;
+    fwd_axes<FAST>(x, y, z, hp, lvl, xb, ax, ay, az);
+    s.wx = ax.w; s.wy = ay.w; s.wz = az.w;
+    s.inside = ax.inside && ay.inside && az.inside;
+    const uint32_t bx = (uint32_t)ax.base + (uint32_t)xb, by = (uint32_t)ay.base, bz = (uint32_t)az.base;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+        s.e[c] = packed_entry<BITS>(base, spatial_hash3(bx, by + ((c >> 1) & 1), bz + (c & 1), hp.mask), q);
+}
+
+__device__ __forceinline__ void packed_level(float x, float y, float z, const HashParams& hp, int lvl, int xb,
+                                             bool fast, int64_t T, const uint8_t* __restrict__ packed,
+                                             const QuantRec* __restrict__ qrec, FwdLvl& s) {
+    const QuantRec q = qrec[lvl];
+    const uint8_t* base = packed + (size_t)lvl * (size_t)T * 8;
+    const int w = code_width(q);   // uniform: one level per call
+#define NERF_PK(B)                                                          \
+    if (fast) packed_gather<B, true>(x, y, z, hp, lvl, xb, base, q, s);    \
+    else packed_gather<B, false>(x, y, z, hp, lvl, xb, base, q, s);
+    if (w == 4) { NERF_PK(4) } else if (w == 8) { NERF_PK(8) } else if (w == 16) { NERF_PK(16) } else { NERF_PK(32) }
+#undef NERF_PK
+}
+
+
+__global__ void __launch_bounds__(256) hash_encode_fwd_packed_pair_kernel(
+    const float* __restrict__ xyz, int64_t n, HashParams hp, int group, int64_t T, const uint8_t* __restrict__ packed,
+    const QuantRec* __restrict__ qrec, float* __restrict__ feat, int64_t sp, int64_t sl, uint8_t* __restrict__ keep) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int row = blockIdx.y;
+    const int64_t p = t >> 1;
+    const int xb = (int)(t & 1);
+    const bool valid = p < n;
+    const int64_t pc = valid ? p : n - 1;             // invalid lanes mirror a valid point (no stores)
+    const float x = xyz[3 * pc + 0], y = xyz[3 * pc + 1], z = xyz[3 * pc + 2];
+    const bool fast = hp.fastdiv && __ballot(!fastdiv_point_ok(x, y, z)) == 0ull;   // wave-uniform
+    if (group > 0 && row == 0) {
+        for (int l0 = 0; l0 < group; l0 += kFwdGroupRound) {
+            FwdLvl s[kFwdGroupRound];
+#pragma unroll
+            for (int g = 0; g < kFwdGroupRound; ++g)
+                if (l0 + g < group) packed_level(x, y, z, hp, l0 + g, xb, fast, T, packed, qrec, s[g]);
+#pragma unroll
+            for (int g = 0; g < kFwdGroupRound; ++g)
+                if (l0 + g < group) fwd_finish<false>(s[g], l0 + g, xb, valid, p, feat, sp, sl, keep, nullptr);
+        }
+        return;
+    }
+    const int lvl = group > 0 ? group + row - 1 : row;
+    FwdLvl s;
+    packed_level(x, y, z, hp, lvl, xb, fast, T, packed, qrec, s);
+    fwd_finish<false>(s, lvl, xb, valid, p, feat, sp, sl, keep, nullptr);
+}
+
 static int fill_set(QuantizerSet& s, const nerf_quantizer* qs, int n, bool need_stats) {
     NERF_REQUIRE(qs && n >= 1 && n <= NERF_MAX_QUANTIZERS, "quant: n = %d quantizers (1..%d)", n, NERF_MAX_QUANTIZERS);
     for (int i = 0; i < n; ++i) {
@@ -309,7 +382,7 @@ static int hash_params(HashParams& hp, const float* bmin, const float* bmax, con
     NERF_REQUIRE(bmin && bmax && res, "quant: null bbox / resolutions");
     for (int l = 0; l < n_levels; ++l) hp.tables[l] = tables ? tables[l] : nullptr;
     for (int a = 0; a < 3; ++a) { hp.bmin[a] = bmin[a]; hp.bmax[a] = bmax[a]; }
-    fill_cells(hp.cell, bmin, bmax, res, n_levels);
+    hp.fastdiv = fill_cells(hp.cell, bmin, bmax, res, n_levels) ? 1u : 0u;
     hp.mask = (uint32_t)((1u << log2_T) - 1u);
     return NERF_OK;
 }
@@ -417,11 +490,26 @@ extern "C" int nerf_hash_encode_fwd_packed(const float* d_xyz, int64_t n_points,
     int rc = hash_params(hp, bbox_min3, bbox_max3, level_res, n_levels, log2_T, nullptr);
     if (rc) return rc;
     if (n_points == 0) return NERF_OK;
+#ifdef NERF_AB_PACKED_ONE_THREAD   // A/B only: the one-point-per-thread packed gather
     dim3 grid(blocks_for(n_points, 256), n_levels);
     hipLaunchKernelGGL(hash_encode_fwd_packed_kernel, grid, dim3(256), 0, as_stream(stream), d_xyz, n_points, hp,
                        int64_t(1) << log2_T, reinterpret_cast<const uint8_t*>(d_packed),
                        reinterpret_cast<const QuantRec*>(d_qrec), d_feat, feat_stride_point, feat_stride_level,
                        d_keep);
+#else
+    int group = 0;   // coarse levels whose (res + 1)^3 vertices fit the table share grid row 0
+    while (group < std::min(n_levels, kFwdGroupMax)) {
+        const double v = (double)level_res[group] + 1.0;
+        if (v * v * v > (double)(1u << log2_T)) break;
+        ++group;
+    }
+    if (group < 2) group = 0;
+    const int rows = group > 0 ? n_levels - group + 1 : n_levels;
+    hipLaunchKernelGGL(hash_encode_fwd_packed_pair_kernel, dim3(blocks_for(2 * n_points, 256), rows), dim3(256), 0,
+                       as_stream(stream), d_xyz, n_points, hp, group, int64_t(1) << log2_T,
+                       reinterpret_cast<const uint8_t*>(d_packed), reinterpret_cast<const QuantRec*>(d_qrec), d_feat,
+                       feat_stride_point, feat_stride_level, d_keep);
+#endif
     NERF_CHECK_LAUNCH("hash_encode_fwd_packed");
     return NERF_OK;
 }

@@ -63,6 +63,40 @@ class _Embed32Shuffled(torch.autograd.Function):
         return None, acc
 
 
+def _split3(v):
+    """v = v0 + v1 + v2, three round-to-nearest bf16 pieces (as fp32 tensors), as csrc/field_x6.hip."""
+    v0 = v.to(torch.bfloat16).float()
+    r = v - v0
+    v1 = r.to(torch.bfloat16).float()
+    v2 = (r - v1).to(torch.bfloat16).float()
+    return v0, v1, v2
+
+
+def _mm6(a, b):
+    """a @ b as the bf16x6 MFMA products (a0b2 + a2b0 + a1b1 + a0b1 + a1b0 + a0b0, small terms first;
+    each bf16 x bf16 product is exact in fp32), fp32 accumulation."""
+    a0, a1, a2 = _split3(a)
+    b0, b1, b2 = _split3(b)
+    out = a0 @ b2
+    for x, y in ((a2, b0), (a1, b1), (a0, b1), (a1, b0), (a0, b0)):
+        out = out + x @ y
+    return out
+
+
+class _Linear6(torch.autograd.Function):
+    """x @ w.t() with the forward and both backward products in bf16x6 (the HIP MLP kernels)."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        ctx.save_for_backward(x, w)
+        return _mm6(x, w.t())
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w = ctx.saved_tensors
+        return _mm6(g, w), _mm6(g.t(), x)
+
+
 def apply_variants(variants, seed=0):
     if "gsum64" in variants:
         orc.F = type("F", (), {k: getattr(torch.nn.functional, k) for k in dir(torch.nn.functional)
@@ -73,6 +107,21 @@ def apply_variants(variants, seed=0):
         orc.F = type("F", (), {k: getattr(torch.nn.functional, k) for k in dir(torch.nn.functional)
                                if not k.startswith("_")})
         orc.F.embedding = staticmethod(lambda idx, table: _Embed32Shuffled.apply(idx, table))
+    if "mlpx6" in variants:
+        import torch.nn.functional as tf
+
+        def mlp_forward6(x, w, n_feat=32, quant=None):
+            pts, views = x[:, :n_feat], x[:, n_feat:]
+            lin = lambda a, k: _Linear6.apply(a, w[k])  # noqa: E731
+            h = tf.relu(lin(pts, "sigma_net.0.weight"))
+            o = lin(h, "sigma_net.1.weight")
+            sigma, geo = o[:, 0], o[:, 1:]
+            c = torch.cat([views, geo], -1)
+            c = tf.relu(lin(c, "color_net.0.weight"))
+            c = tf.relu(lin(c, "color_net.1.weight"))
+            rgb = lin(c, "color_net.2.weight")
+            return torch.cat([rgb, sigma[:, None]], -1)
+        orc.mlp_forward = mlp_forward6
     if "comp64" in variants:
         base = orc.composite
 
@@ -89,7 +138,8 @@ def main():
     ap.add_argument("--stats", default="")
     ap.add_argument("--out", default="")
     ap.add_argument("--variant", default="", help="comma list: gsum64 (table gradients summed in fp64, as the "
-                    "HIP owner pass), gsum32shuf (fp32 sums in a seeded random order), comp64 (compositing in fp64)")
+                    "HIP owner pass), gsum32shuf (fp32 sums in a seeded random order), comp64 (compositing in fp64), mlpx6 (MLP products as the "
+                    "bf16x6 MFMA kernels)")
     a = ap.parse_args()
     torch.set_num_threads(a.threads)
     apply_variants([v for v in a.variant.split(",") if v], seed=a.threads)
