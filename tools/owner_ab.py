@@ -44,6 +44,9 @@ def main():
     ds = [torch.randn(16, p.shape[0], 2, device=dev) for p in sets]
 
     def bins():
+        # the bucket counters start at zero (the owner pass resets them; a bins-only loop does not)
+        if hasattr(lib, "nerf_hash_bwd_workspace_init"):   # absent from libraries before the bucket layout
+            _lib.call("nerf_hash_bwd_workspace_init", _lib.ptr(ws, dtype=torch.uint8), nbytes, _lib.stream())
         base = 0
         for p, n, d in zip(sets, chunks, ds):
             _lib.call("nerf_hash_encode_bwd_bin", _lib.ptr(p), p.shape[0], meta["bmin"], meta["bmax"], meta["res"], 16, 19,
@@ -51,28 +54,25 @@ def main():
                       _lib.stream())
             base += n
 
-    bins()
-
     def owner():
         _lib.call("nerf_hash_encode_bwd_owner", 16, 19, cap, cap, gp, det, _lib.ptr(ws, dtype=torch.uint8), nbytes,
                   _lib.stream())
 
     res = {}
     for rnd in range(5):
-        for v, fn in (("bin", bins), ("owner", owner)):
-            if v == "owner":
-                bins()
-            for _ in range(2):
-                fn()
-            torch.cuda.synchronize()
+        for v in ("bin", "owner"):
             ts = []
-            for _ in range(10):
+            for k in range(12):
+                bins()   # every owner pass consumes the entries binned before it
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
-                fn()
+                (bins if v == "bin" else owner)()
                 e1.record()
+                if v == "bin":
+                    owner()
                 torch.cuda.synchronize()
-                ts.append(e0.elapsed_time(e1))
+                if k >= 2:
+                    ts.append(e0.elapsed_time(e1))
             res.setdefault(v, []).append(float(np.median(ts)))
     print(json.dumps({k: round(float(np.median(v)) * 1e3, 1) for k, v in res.items()} | {"unit": "us", "chunks": cap, "chunk_points": C, "det": det}))
 
