@@ -432,10 +432,18 @@ __global__ void __launch_bounds__(THREADS) hash_bwd_owner_kernel(HashGradParams 
     __shared__ uint32_t s_pre[kOwnerWindow + 1];
     __shared__ uint16_t s_beg[kOwnerWindow];
     __shared__ uint32_t s_wsum[kOwnerThreads / 64];
-#ifdef NERF_OWNER_REVERSE   // A/B: finest (heaviest) levels dispatched first
-    const int o = blockIdx.x, lvl = gridDim.y - 1 - blockIdx.y;
-#else
+    // Dispatch order of the levels: finest, coarsest, next finest, ... The finest levels carry the
+    // most entries (a level-15 block ~74 us, a level-0 block ~25 us, tools/owner_prof.py): dispatched
+    // level-major they start last and leave a tail of 64 long blocks on a quarter of the CUs
+    // (makespan 244 us vs 202 us of block time per CU); interleaved, light blocks fill in behind the
+    // heavy ones (235 us; owner launch 255 -> 248 us on one box, profiles/r03i_ab_owner_order.jsonl).
+    // Finest first alone is slower (273 us): the coarse pass's bins, written last, are partly still
+    // in the Infinity Cache when the early blocks read them.
+#if defined(NERF_OWNER_LEVEL_MAJOR)   // A/B only
     const int o = blockIdx.x, lvl = blockIdx.y;
+#else
+    const int o = blockIdx.x, y = blockIdx.y;
+    const int lvl = (y & 1) ? (y >> 1) : (int)gridDim.y - 1 - (y >> 1);
 #endif
     const int S = 1 << hp.slice_log2, n_own = 1 << hp.owner_log2;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
