@@ -413,11 +413,12 @@ def ulp_nudge(table, seed, frac=0.01):
     return out
 
 
-def converge_run(ref, c, threads, nudge=None):
+def converge_run(ref, c, threads, nudge=None, batch_seed=None):
     """One reference training run of F19 with `threads` CPU threads (torch's CPU kernels split their
     reductions by thread, so two thread counts are two runs of the same algorithm whose float sums
     differ in order: the reference's own run-to-run spread). nudge: seed of a one-ulp change of 1 %
-    of the initial table entries (ulp_nudge), for runs beyond the thread-count variants."""
+    of the initial table entries (ulp_nudge), for runs beyond the thread-count variants. batch_seed:
+    draw the run's ray batches with this seed instead of F19's (F19c)."""
     torch.set_num_threads(threads)
     (ro, rd, rgb), (eo, ed, ergb), (no, nd, nrgb) = tables_convergence()
     table = closed_form_table(scale=c["table_scale"], salt=c["table_salt"])
@@ -431,7 +432,7 @@ def converge_run(ref, c, threads, nudge=None):
                            {"params": list(emb.parameters()), "eps": 1e-15}], lr=c["lrate"], betas=(0.9, 0.99))
     kw = build_render_kwargs(ref, emb, coarse, fine, 64, 128, 1.0, 0.0, False)
     kw_test = dict(kw, perturb=0.0, raw_noise_std=0.0)
-    rng = np.random.RandomState(c["batch_seed"])
+    rng = np.random.RandomState(c["batch_seed"] if batch_seed is None else batch_seed)
     batches = np.stack([rng.choice(ro.shape[0], c["R"], replace=False) for _ in range(c["iters"])]).astype(np.int32)
     train_psnr, eval_psnr, novel_psnr, eval_iters = [], [], [], []
 
@@ -511,6 +512,37 @@ def gen_converge_more(ref, out, start=0, count=18, threads=2):
         d.update({f"{name}_n{k}": v for name, v in curves.items()})
         d["eval_iters"] = eval_iters
         np.savez_compressed(os.path.join(out, f"f19b_converge_part{start}.npz"), seeds=np.arange(start, k + 1), **d)
+
+
+def gen_converge_seeds(ref, out, start=0, count=3, threads=2):
+    """F19c: reference runs of F19's training whose ray batches are drawn with seeds 100 + k (k = start
+    .. start + count - 1) instead of F19's seed: different batches from the first iteration on, as
+    train()'s random batches are. RAdam makes no update before step 6 (N_sma < 5) and the per-element
+    table gradients of F19's initial state are ill-conditioned, so every run that shares F19's batches
+    (F19's thread-count runs, F19b's rounding-perturbed ones) shares one first update and one early
+    trajectory; runs over batch seeds sample the training randomness itself. The HIP test replays the
+    same seeds (numpy RandomState(seed).choice, as here). Writes f19c_converge_part{start}.npz."""
+    c = dict(CONVERGE)
+    d = {}
+    for k in range(start, start + count):
+        _, batches, eval_iters, curves = converge_run(ref, c, threads, batch_seed=100 + k)
+        d.update({f"{name}_s{100 + k}": v for name, v in curves.items()})
+        d[f"batch_sum_s{100 + k}"] = np.array(int(batches.astype(np.int64).sum()))
+        d["eval_iters"] = eval_iters
+        np.savez_compressed(os.path.join(out, f"f19c_converge_part{start}.npz"), seeds=np.arange(100 + start, 101 + k), **d)
+
+
+def merge_converge_seeds(out):
+    """Join the f19c parts into f19c_converge.npz (runs keyed by their batch seed)."""
+    parts = sorted(f for f in os.listdir(out) if f.startswith("f19c_converge_part"))
+    d, seeds = {}, []
+    for f in parts:
+        z = np.load(os.path.join(out, f))
+        seeds += [int(v) for v in z["seeds"]]
+        d.update({k: z[k] for k in z.files if k != "seeds"})
+    np.savez_compressed(os.path.join(out, "f19c_converge.npz"), seeds=np.array(sorted(seeds)), **d)
+    for f in parts:
+        os.remove(os.path.join(out, f))
 
 
 def merge_converge_more(out):
@@ -976,5 +1008,9 @@ if __name__ == "__main__":
         gen_converge_more(load_reference(), HERE, *(int(v) for v in sys.argv[2:5]))
     elif sys.argv[1:2] == ["converge_merge"]:
         merge_converge_more(HERE)
+    elif sys.argv[1:2] == ["converge_seeds"]:    # make_golden.py converge_seeds START COUNT THREADS
+        gen_converge_seeds(load_reference(), HERE, *(int(v) for v in sys.argv[2:5]))
+    elif sys.argv[1:2] == ["converge_seeds_merge"]:
+        merge_converge_seeds(HERE)
     else:
         main(sys.argv[1:])

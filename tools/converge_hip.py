@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--out", default="gpurun_out/conv/hip.npz")
     ap.add_argument("--deterministic", action="store_true")
     ap.add_argument("--stats", action="store_true")
+    ap.add_argument("--batch-seeds", default="", help="comma list: replay F19c's runs (ray batches drawn with "
+                    "numpy RandomState(seed).choice, tests/golden/make_golden.py gen_converge_seeds); --runs per seed")
     a = ap.parse_args()
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
     gpu = torch.device("cuda:0")
@@ -61,8 +63,16 @@ def main():
             out, _, _, _ = nerf.render(800, 800, None, rays=(o, d), **kw_test)
             return (-10.0 * torch.log10(((out - target) ** 2).mean())).item()
 
+    seeds = [int(v) for v in a.batch_seeds.split(",") if v] or [None]
+    plan = [(s_, k) for s_ in seeds for k in range(a.runs)]
     res = {}
-    for r in range(a.runs):
+    for r, (seed, _) in enumerate(plan):
+        if seed is not None:
+            rng = np.random.RandomState(seed)
+            bt = np.stack([rng.choice(ro.shape[0], c["R"], replace=False) for _ in range(c["iters"])])
+            batches = torch.from_numpy(bt.astype(np.int64)).to(gpu)
+            res[f"seed_{r}"] = np.array(seed)
+            res[f"batch_sum_{r}"] = np.array(int(bt.astype(np.int64).sum()))
         with torch.no_grad():
             for i, e in enumerate(emb.embeddings):
                 e.weight.copy_(torch.from_numpy(table[i]))
