@@ -75,7 +75,6 @@ KERNEL_SYMBOLS = {
     "nerf_mlp_bwd_batch": ["nerf::mlp_bwd_x6cg_kernel<false>"],
     "nerf_radam_step": ["nerf::radam_kernel"],
 }
-TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r02_traffic.json")
 
 
 def base_name(abi_name):
@@ -86,7 +85,7 @@ def base_name(abi_name):
 
 def traffic_file():
     """The newest committed PMC traffic summary (tools/profile_bench.sh), or None."""
-    for name in ("r02_traffic.json", "r01j_traffic.json"):
+    for name in ("r03_traffic.json", "r02_traffic.json", "r01j_traffic.json"):
         path = os.path.join(ROOT, "profiles", name)
         if os.path.exists(path):
             return path
@@ -504,9 +503,10 @@ def main():
                             top3=[{k: o[k] for k in ("op", "bound", "ms_per_step", "achieved", "unit", "frac")}
                                   for o in ops[:3]])
             if d["traffic"] is not None:
-                roofline["traffic_source"] = (os.path.relpath(traffic_file(), ROOT) + ": rocprofv3 FETCH_SIZE (x2, "
-                                              "gfx950 wide-read correction) + WRITE_SIZE per call, separate PMC passes "
-                                              "of this bench, x calls per iteration")
+                roofline["traffic_source"] = (os.path.relpath(traffic_file(), ROOT) + ": rocprofv3 FETCH_SIZE x2 (4/8/16-B "
+                                              "per-lane reads count half, 2-B reads are not counted: "
+                                              "profiles/r03a_pmc_calibration.json) + WRITE_SIZE per call, separate "
+                                              "PMC passes of this bench, x calls per iteration")
     step_s = elapsed / a.steps
     step_bytes = points_per_step * STEP_BYTES_PER_POINT + STEP_DENSE_BYTES + R * STEP_RAY_BYTES
     step_roofline = None
@@ -550,12 +550,15 @@ def main():
         out["deterministic"] = True
     # north star "PSNR within 0.1 dB of reference": the committed result of tests/test_gpu_converge.py
     # (the reference trained on F19 six times vs six HIP runs; late-phase mean PSNR difference per metric)
-    pv = os.path.join(ROOT, "profiles", "r02_psnr_vs_reference.json")
-    if os.path.exists(pv):
-        pj = json.load(open(pv))
-        out["psnr_vs_reference"] = {k: {"d_db": v["d_db"], "reference_db": v["reference_db"], "hip_db": v["hip_db"]}
-                                    for k, v in pj.items() if isinstance(v, dict)}
-        out["psnr_vs_reference"]["source"] = "profiles/r02_psnr_vs_reference.json"
+    for name in ("r03_psnr_vs_reference.json", "r02_psnr_vs_reference.json"):
+        pv = os.path.join(ROOT, "profiles", name)
+        if os.path.exists(pv):
+            pj = json.load(open(pv))
+            out["psnr_vs_reference"] = {k: {"d_db": v["d_db"], "reference_db": v["reference_db"], "hip_db": v["hip_db"]}
+                                        for k, v in pj.items() if isinstance(v, dict)}
+            out["psnr_vs_reference"]["source"] = "profiles/" + name + (
+                " (commit " + pj["commit"] + ")" if isinstance(pj.get("commit"), str) else "")
+            break
     if rank == 0 and world == 1 and not a.no_cpu_baseline and a.workload == "lego" and a.mode == "train":
         out["cpu_baseline"] = cpu_baseline(a.cpu_rays, a.cpu_warmup, a.cpu_steps)
     elif rank == 0:

@@ -5,7 +5,8 @@ from .dist import GradArena, ShardedOptimizer, broadcast_params, init_process_gr
 from .field import NeRFSmall, batchify, deterministic, run_network, set_deterministic
 from .hashgrid import HashEmbedder, SHEncoder, level_resolutions
 from .losses import sigma_sparsity_loss, total_variation_all, total_variation_loss, train_loss
-from .model import acaq_quantizers, acaq_update, create_nerf, make_args, save_checkpoint, train_step
+from .model import (acaq_quantizers, acaq_update, create_nerf, make_args, save_checkpoint, structural_overfit_update,
+                    train_step)
 from .optim import RAdam
 from .quantization import FakeQuantizer, LearnedBitwidthQuantizer, PassthroughQuantizer, calculate_fqr
 from .rays import RaySampler, crop_window
@@ -21,7 +22,7 @@ __all__ = ["HashEmbedder", "SHEncoder", "NeRFSmall", "RAdam", "run_network", "ba
            "to8b", "create_nerf", "make_args", "save_checkpoint", "train_step", "total_variation_loss",
            "total_variation_all", "train_loss", "sigma_sparsity_loss", "level_resolutions", "GradArena", "ShardedOptimizer", "init_process_group",
            "shard", "broadcast_params", "manual_seed", "load_library", "LearnedBitwidthQuantizer", "FakeQuantizer",
-           "PassthroughQuantizer", "calculate_fqr", "acaq_update", "acaq_quantizers", "RaySampler", "crop_window", "camera",
+           "PassthroughQuantizer", "calculate_fqr", "acaq_update", "acaq_quantizers", "structural_overfit_update", "RaySampler", "crop_window", "camera",
            "get_bbox3d_for_blenderobj", "get_bbox3d_for_llff", "render_path", "load_blender_data", "load_llff_data",
            "pose_spherical", "load_scannet_data", "ManhattanFrameEstimator", "SemanticPlaneDetector",
            "combine_structural_losses_v2", "manhattan_sdf_loss", "spatial_normal_consistency_loss",

@@ -8,6 +8,7 @@ listed in SURVEY.md §0.3 (predict_normals / use_quantization kwargs) by accepti
 import os
 from types import SimpleNamespace
 
+import numpy as np
 import torch
 
 from .field import NeRFSmall, run_network
@@ -264,6 +265,28 @@ def structural_loss(depth, extras, args, global_step, spatial_coords=None):
         print(f"  ⚠️  Structural priors V2 failed: {e}")
         return 0.0
     return total
+
+
+def structural_overfit_update(args, global_step, psnr_list):
+    """train()'s overfitting-driven reduction of the structural-prior weights (run_nerf.py:1072-1094),
+    a host-side step of the training loop: every 500 iterations from structural_loss_start_iter + 500
+    on, when more than 50 training PSNRs are recorded and the mean of the last 20 exceeds
+    args._last_test_psnr by more than args.overfitting_threshold, the four weights are multiplied by
+    0.7 (floored at args.min_structural_weight). Returns True when it reduced them. The reference
+    reads args._last_test_psnr only through hasattr and never sets it, so in its own train() this
+    never fires; a caller that records its test PSNR there gets the reduction. Under
+    graphs.GraphedTrainStep the weights are part of the launch-structure key: a reduction re-captures."""
+    get = lambda k: getattr(args, k, DEFAULTS.get(k))  # noqa: E731
+    i = global_step
+    if not (i > get("structural_loss_start_iter") + 500 and i % 500 == 0 and len(psnr_list) > 50):
+        return False
+    recent = float(np.mean(psnr_list[-20:]))
+    if not hasattr(args, "_last_test_psnr") or recent - args._last_test_psnr <= get("overfitting_threshold"):
+        return False
+    floor = get("min_structural_weight")
+    for k in ("depth_prior_weight", "planarity_weight", "manhattan_weight", "normal_consistency_weight"):
+        setattr(args, k, max(floor, get(k) * 0.7))
+    return True
 
 
 def optimizer_update(optimizer):

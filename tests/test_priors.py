@@ -292,3 +292,41 @@ def test_graphed_priors_step_matches_eager(nerf, gpu):
             assert st.captures == 1
         losses[mode] = out
     np.testing.assert_allclose(losses["graph"], losses["eager"], rtol=2e-4)
+
+
+def test_structural_overfit_update_matches_reference_loop():
+    """model.structural_overfit_update vs run_nerf.py:1072-1094 restated: fires only every 500
+    iterations after structural_loss_start_iter + 500 with > 50 recorded PSNRs and a train/test gap
+    above overfitting_threshold; multiplies the four weights by 0.7 with the min_structural_weight
+    floor; never fires without args._last_test_psnr (which the reference never sets)."""
+    import types
+
+    import indoor_nerf_amd as nerf
+
+    def reference(args, i, psnr_list):   # run_nerf.py:1073-1086
+        if i > args.structural_loss_start_iter + 500 and i % 500 == 0 and len(psnr_list) > 50:
+            recent = np.mean(psnr_list[-20:])
+            if hasattr(args, "_last_test_psnr") and recent - args._last_test_psnr > args.overfitting_threshold:
+                for k in ("depth_prior_weight", "planarity_weight", "manhattan_weight", "normal_consistency_weight"):
+                    setattr(args, k, max(args.min_structural_weight, getattr(args, k) * 0.7))
+
+    def fresh(**kw):
+        a = types.SimpleNamespace(structural_loss_start_iter=1000, overfitting_threshold=8.0, min_structural_weight=1e-4,
+                                  depth_prior_weight=0.1, planarity_weight=0.01, manhattan_weight=2e-4,
+                                  normal_consistency_weight=0.05)
+        a.__dict__.update(kw)
+        return a
+
+    rng = np.random.RandomState(3)
+    keys = ("depth_prior_weight", "planarity_weight", "manhattan_weight", "normal_consistency_weight")
+    for test_psnr in (None, 20.0, 14.0):
+        kw = {} if test_psnr is None else {"_last_test_psnr": test_psnr}
+        ours, ref = fresh(**kw), fresh(**kw)
+        psnr_list = []
+        fired = 0
+        for i in range(1, 4001):
+            psnr_list.append(float(25.0 + rng.randn()))
+            fired += nerf.structural_overfit_update(ours, i, psnr_list)
+            reference(ref, i, psnr_list)
+            assert all(getattr(ours, k) == getattr(ref, k) for k in keys), (test_psnr, i)
+        assert fired == (0 if test_psnr in (None, 20.0) else 5), fired   # i = 2000, 2500, ..., 4000

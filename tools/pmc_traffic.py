@@ -2,10 +2,13 @@
 """Per-kernel HBM-side traffic per launch from two rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE;
 separate passes, MI355X_MICROARCH.md rocprofv3 PMC slots) over the same command.
 
-rocprofv3 reports FETCH_SIZE / WRITE_SIZE in KiB per dispatch. gfx950 caveat (same guide, HBM):
-FETCH_SIZE counts a wide coalesced streaming read at half its bytes and other access widths are
-uncalibrated, so the figure is reported raw (`fetch_kib`) beside the corrected streaming estimate
-(`fetch_bytes_x2`); WRITE_SIZE is exact for 16-B streaming stores and float atomics.
+rocprofv3 reports FETCH_SIZE / WRITE_SIZE in KiB per dispatch. gfx950 correction, calibrated on this
+pool with tools/fetch_calib.hip (profiles/r03a_pmc_calibration.json: 1 GiB streamed per access width):
+FETCH_SIZE counts 4-, 8- and 16-B per-lane reads at exactly half their bytes (x2 restores them) and
+does not count 2-B per-lane reads at all; WRITE_SIZE is exact for 2-, 4-, 8- and 16-B stores. So
+`fetch_bytes_x2` is the fetched bytes of every kernel whose reads are >= 4 B per lane — all of them
+except the owner pass, whose 2-B row reads (~0.11 GB per lego step) are missing from its figure, which
+is therefore a lower bound. The raw counter is kept as `fetch_kib`.
 
 usage: pmc_traffic.py FETCH_counter_collection.csv WRITE_counter_collection.csv OUT.json
 """
