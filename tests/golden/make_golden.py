@@ -536,6 +536,10 @@ def merge_converge_seeds(out):
     """Join the f19c parts into f19c_converge.npz (runs keyed by their batch seed)."""
     parts = sorted(f for f in os.listdir(out) if f.startswith("f19c_converge_part"))
     d, seeds = {}, []
+    if os.path.exists(os.path.join(out, "f19c_converge.npz")):   # earlier merges stay
+        z = np.load(os.path.join(out, "f19c_converge.npz"))
+        seeds += [int(v) for v in z["seeds"]]
+        d.update({k: z[k] for k in z.files if k != "seeds"})
     for f in parts:
         z = np.load(os.path.join(out, f))
         seeds += [int(v) for v in z["seeds"]]

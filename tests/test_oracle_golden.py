@@ -326,3 +326,21 @@ def test_llff_bbox(golden):
     lo, hi = get_bbox3d_for_llff(g["poses"], tuple(float(v) for v in g["hwf"]), near=0.0, far=1.0)
     np.testing.assert_array_equal(lo.numpy(), g["bbox_min"])
     np.testing.assert_array_equal(hi.numpy(), g["bbox_max"])
+
+
+def test_oracle_reproduces_reference_seed_run(golden):
+    """F19d's premise (tests/golden/make_oracle_converge.py): the oracle's training run is the
+    reference's own run at the same thread count — F19c's seed-100 run (the reference, 2 threads)
+    reproduced to 1e-5 dB through its first 8 iterations, past RAdam's first update (step 6), where
+    any difference of algorithm would show (the HIP path parts from it by ~0.03 dB there)."""
+    import torch
+    from make_oracle_converge import oracle_run
+    cs = golden("f19c_converge")
+    s = int(cs["seeds"][0])
+    threads = torch.get_num_threads()
+    try:
+        r = oracle_run(s, 2, iters=8)
+    finally:
+        torch.set_num_threads(threads)
+    assert int(r["batch_sum"]) == int(cs[f"batch_sum_s{s}"])
+    np.testing.assert_allclose(r["train_psnr"], cs[f"train_psnr_s{s}"][:8], rtol=0, atol=1e-5)

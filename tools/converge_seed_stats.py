@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Paired comparison over batch seeds (F19c): per seed the reference run (tests/golden/f19c_converge.npz
 or its parts) against the mean of the HIP runs that replay the same batches (tools/converge_hip.py
---batch-seeds ...). Prints per metric the late-phase (iterations 200-300) difference per seed, their
+--batch-seeds ...). Prints per metric the late-phase (iterations 100-300) difference per seed, their
 mean D, its standard error over seeds, and per checkpoint the paired mean difference with its t value.
 With --json, writes the summary tests/test_gpu_converge.py commits as profiles/r03_psnr_vs_reference.json.
 
@@ -20,9 +20,13 @@ NAMES = ("eval_psnr", "novel_psnr", "train_psnr")
 
 
 def reference_seed_runs():
+    """F19c (the reference) and F19d (the oracle) runs keyed by batch seed."""
     files = [os.path.join(GOLD, "f19c_converge.npz")]
     if not os.path.exists(files[0]):
-        files = sorted(glob.glob(os.path.join(GOLD, "f19c_converge_part*.npz")))
+        files = []
+    files += sorted(glob.glob(os.path.join(GOLD, "f19c_converge_part*.npz")))
+    if os.path.exists(os.path.join(GOLD, "f19d_converge.npz")):
+        files.append(os.path.join(GOLD, "f19d_converge.npz"))
     out = {}
     for f in files:
         z = np.load(f)
@@ -33,9 +37,12 @@ def reference_seed_runs():
     return out
 
 
+LATE = 100   # tests/test_gpu_converge.py LATE
+
+
 def late(name, x):
-    """Late-phase mean: checkpoints at iterations 200..300 (indices 10..15), or training batches 201..300."""
-    return x[..., 200:300].mean(-1) if name == "train_psnr" else x[..., 10:16].mean(-1)
+    """Late-phase mean: checkpoints at iterations LATE..300, or training batches LATE+1..300."""
+    return x[..., LATE:].mean(-1) if name == "train_psnr" else x[..., LATE // 20:].mean(-1)
 
 
 def paired(ref, hip):
@@ -80,8 +87,8 @@ def main():
         out = {name: {"d_db": round(res[name]["D"], 4), "se_db": round(res[name]["se"], 4),
                       "reference_db": round(res[name]["reference_db"], 3), "hip_db": round(res[name]["hip_db"], 3)}
                for name in NAMES}
-        out["design"] = (f"F19c: {len(seeds)} reference runs with their own ray batches (seeds {seeds[0]}..{seeds[-1]}) "
-                         f"vs {len(next(iter(hip.values())))} HIP runs replaying each; late-phase (iterations 200-300) "
+        out["design"] = (f"F19c/F19d: {len(seeds)} reference runs with their own ray batches (seeds {seeds}) vs "
+                         f"{len(next(iter(hip.values())))} HIP runs replaying each; late-phase (iterations {LATE}-300) "
                          "mean PSNR difference averaged over seeds")
         if a.commit:
             out["commit"] = a.commit
