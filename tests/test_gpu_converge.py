@@ -67,6 +67,7 @@ def _late(name, x, every):
     return x[..., LATE // every:].mean(-1)
 
 
+@pytest.mark.timeout(900)   # ~0.4 s per HIP run: K runs x every seed, plus F19's six
 def test_convergence_psnr_within_0p1_db(nerf, gpu, golden):
     g = golden("f19_converge")
     cs = golden("f19c_converge")
@@ -130,6 +131,8 @@ def test_convergence_psnr_within_0p1_db(nerf, gpu, golden):
         assert int(bt.astype(np.int64).sum()) == int(runs[s]["batch_sum"]), f"seed {s}: batches differ"
         bt = torch.from_numpy(bt.astype(np.int64)).to(gpu)
         hip[s] = [train_run(bt) for _ in range(K)]
+        if len(hip) % 16 == 0:
+            print(f"  {len(hip)}/{len(seeds)} seeds trained", flush=True)
 
     from scipy import stats
     lines, fails = [], []
