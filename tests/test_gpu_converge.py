@@ -47,7 +47,8 @@ from tables import blender_bbox, closed_form_table, convergence_rays
 
 pytestmark = pytest.mark.gpu
 
-K = 2               # HIP runs per batch seed (the single reference run per seed dominates the variance)
+K = 1               # HIP runs per batch seed: the single reference run per seed dominates the variance, and
+                    # the suite must not fall silent for minutes (~0.4 s per HIP run)
 LATE = 100          # late phase: iterations LATE..300
 
 
@@ -67,7 +68,7 @@ def _late(name, x, every):
     return x[..., LATE // every:].mean(-1)
 
 
-@pytest.mark.timeout(900)   # ~0.4 s per HIP run: K runs x every seed, plus F19's six
+@pytest.mark.timeout(900)   # ~0.4 s per HIP run: K runs x ~150 seeds, plus F19's six
 def test_convergence_psnr_within_0p1_db(nerf, gpu, golden):
     g = golden("f19_converge")
     cs = golden("f19c_converge")
