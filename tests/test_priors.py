@@ -118,6 +118,17 @@ def test_train_step_with_structural_priors(nerf, gpu):
     torch.cuda.synchronize()
     assert st.captures == 1
     assert torch.isfinite(loss).item()
+    # the overfitting-driven weight reduction (run_nerf.py:1072-1094) changes the weights baked into the
+    # priors launches: the next steps re-capture instead of replaying the old weights
+    w0 = args.planarity_weight
+    args._last_test_psnr = -100.0
+    assert nerf.structural_overfit_update(args, 1000, [30.0] * 60)
+    assert args.planarity_weight < w0
+    for it in range(4, 7):
+        loss, psnr = st(it)
+    torch.cuda.synchronize()
+    assert st.captures == 2 and torch.isfinite(loss).item()
+    del args._last_test_psnr
     args.fused_priors = False
     loss_e, _ = st(4)
     assert st.graphs is None and torch.isfinite(loss_e).item()
