@@ -6,7 +6,7 @@ what the first update depends on, not only the values.
 
 The first-update tool's docstring follows.
 The first RAdam update of F19's training, HIP path vs the oracle (the
-reference's algorithm, pinned to the reference's own runs: tools/converge_oracle.py reproduces F19 to
+reference's algorithm, pinned to the reference's own runs: tests/diagnostics/converge_oracle.py reproduces F19 to
 1e-6 dB at a matching thread count), from the same initial state on the same batches. RAdam
 (radam.py:58-92, betas (0.9, 0.99)) makes no update while N_sma < 5, i.e. for steps 1-5; step 6 is the
 first update, and every HIP run agrees with every other one there while the first PSNR after it
@@ -15,7 +15,7 @@ update differs by more than half a full step (|dp| ~ lr: with eps 1e-15 any row 
 gradient history moves by ~lr), split by cause: exp_avg_sq zero on one side only (squares of tiny
 gradients underflowing), exp_avg sign disagreement, or neither.
 
-usage (GPU box): python tools/converge_first_update.py --steps 6 > out.json
+usage (GPU box): python tests/diagnostics/converge_first_update.py --steps 6 > out.json
 """
 import argparse
 import ast
@@ -26,7 +26,7 @@ import sys
 import numpy as np
 import torch
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
 import indoor_nerf_amd as nerf  # noqa: E402

@@ -5,7 +5,7 @@ sum is exactly zero while the fp64 sum is not (and the reverse), sign disagreeme
 update either gradient would give a row touched for the first time (eps 1e-15: any nonzero gradient
 is a full-size step, an exact zero none).
 
-usage: python tools/converge_gradsum.py --iters 40 --threads 8 [--out stats.json]
+usage: python tests/diagnostics/converge_gradsum.py --iters 40 --threads 8 [--out stats.json]
 """
 import argparse
 import ast
@@ -17,10 +17,10 @@ import sys
 import numpy as np
 import torch
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
-sys.path.insert(0, os.path.join(ROOT, "tools"))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from oracle import nerf_oracle as orc  # noqa: E402
 from tables import blender_bbox, closed_form_table, convergence_rays  # noqa: E402
 

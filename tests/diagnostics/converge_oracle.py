@@ -6,7 +6,7 @@ choice shared by the oracle and the HIP path (both restate the reference); if it
 is HIP-side numerics. Optional per-iteration diagnostics (--stats) record, per table level, the rows
 with a nonzero / exactly-zero gradient and |dp| statistics of the update.
 
-usage: python tools/converge_oracle.py --iters 120 --threads 8 [--stats out.npz]
+usage: python tests/diagnostics/converge_oracle.py --iters 120 --threads 8 [--stats out.npz]
 """
 import argparse
 import math
@@ -16,7 +16,7 @@ import sys
 import numpy as np
 import torch
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
 from oracle import nerf_oracle as orc  # noqa: E402

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Ensemble comparison for the convergence diagnostics: reference runs (F19's six thread-count runs,
-plus F19b's rounding-perturbed runs with --ref f19,f19b) against a set of runs (tools/converge_oracle.py
+plus F19b's rounding-perturbed runs with --ref f19,f19b) against a set of runs (tests/diagnostics/converge_oracle.py
 or tools/converge_hip.py outputs, or another reference set with --vs), per checkpoint: mean difference
 and its standard error; per 10-iteration window of training PSNR; and the late-phase (iterations
 200-300) means per metric.

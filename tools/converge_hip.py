@@ -1,7 +1,7 @@
 """Diagnostic (GPU box): the HIP path trained on F19's scene, initial state and batches, as
 tests/test_gpu_converge.py trains it; writes every run's per-iteration training PSNR, the
 checkpoint PSNRs and per-iteration table statistics (rows with a nonzero / exactly-zero gradient
-per level, mean / max |dp| of the update per level) to an .npz for tools/converge_oracle.py's
+per level, mean / max |dp| of the update per level) to an .npz for tests/diagnostics/converge_oracle.py's
 counterpart on CPU.
 
 usage: python tools/converge_hip.py --runs 6 --iters 120 --out gpurun_out/conv/hip.npz [--deterministic]
