@@ -353,7 +353,7 @@ extern "C" int nerf_composite_fwd(const float* d_raw, int raw_channels, const fl
     NERF_REQUIRE(n_rays >= 0 && n_samples >= 1 && n_samples <= 512, "composite_fwd: R=%lld S=%d (S must be 1..512)",
                  (long long)n_rays, n_samples);
     NERF_REQUIRE(raw_channels == 4 || raw_channels == 7, "composite_fwd: raw_channels %d", raw_channels);
-    NERF_REQUIRE(d_raw && d_z && d_rays_d && d_weights, "composite_fwd: null arg");
+    NERF_REQUIRE(n_rays == 0 || (d_raw && d_z && d_rays_d && d_weights), "composite_fwd: null arg");
     NERF_REQUIRE(!(d_normal && raw_channels != 7), "composite_fwd: normal output needs 7 raw channels");
     if (n_rays == 0) return NERF_OK;
     CompositeArgs a{};
@@ -375,7 +375,7 @@ extern "C" int nerf_composite_bwd(const float* d_raw, int raw_channels, const fl
     NERF_REQUIRE(n_rays >= 0 && n_samples >= 1 && n_samples <= 512, "composite_bwd: R=%lld S=%d (S must be 1..512)",
                  (long long)n_rays, n_samples);
     NERF_REQUIRE(raw_channels == 4 || raw_channels == 7, "composite_bwd: raw_channels %d", raw_channels);
-    NERF_REQUIRE(d_raw && d_z && d_rays_d && d_graw, "composite_bwd: null arg");
+    NERF_REQUIRE(n_rays == 0 || (d_raw && d_z && d_rays_d && d_graw), "composite_bwd: null arg");
     if (n_rays == 0) return NERF_OK;
     CompositeArgs a{};
     a.raw = d_raw; a.C = raw_channels; a.z = d_z; a.rays_d = d_rays_d; a.noise = d_noise;

@@ -28,8 +28,8 @@ static int fill_args(MlpArgs& a, const float* d_feat, int64_t sp, int64_t sl, co
                      const float* d_viewdirs, int64_t spr, const uint8_t* d_keep, int64_t n,
                      const nerf_mlp_weights* w) {
     NERF_REQUIRE(n >= 0, "mlp: n_points < 0");
-    NERF_REQUIRE(d_feat && w && w->w0 && w->w1 && w->c0 && w->c1 && w->c2, "mlp: null feature/weight pointer");
-    NERF_REQUIRE(d_viewdirs || d_sh, "mlp: need d_sh or d_viewdirs");
+    NERF_REQUIRE((n == 0 || d_feat) && w && w->w0 && w->w1 && w->c0 && w->c1 && w->c2, "mlp: null feature/weight pointer");
+    NERF_REQUIRE(n == 0 || d_viewdirs || d_sh, "mlp: need d_sh or d_viewdirs");
     NERF_REQUIRE(!d_viewdirs || spr >= 1, "mlp: samples_per_ray must be >= 1");
     a.feat = d_feat; a.sp = sp; a.sl = sl; a.sh = d_sh; a.sh_stride = sh_stride;
     a.viewdirs = d_viewdirs; a.spr = spr; a.keep = d_keep; a.P = n; a.W = *w;
@@ -41,7 +41,7 @@ static int fill_args(MlpArgs& a, const float* d_feat, int64_t sp, int64_t sl, co
 using namespace nerf;
 
 extern "C" int nerf_sh4_fwd(const float* d_dirs, int64_t n, float* d_out, void* stream) {
-    NERF_REQUIRE(n >= 0 && d_dirs && d_out, "sh4_fwd: bad args");
+    NERF_REQUIRE(n >= 0 && (n == 0 || (d_dirs && d_out)), "sh4_fwd: bad args");
     if (n == 0) return NERF_OK;
     hipLaunchKernelGGL(sh4_fwd_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, as_stream(stream), d_dirs, n, d_out);
     NERF_CHECK_LAUNCH("sh4_fwd");
@@ -57,7 +57,7 @@ extern "C" int nerf_mlp_fwd_q(const float* d_feat, int64_t feat_stride_point, in
     int rc = fill_args(a, d_feat, feat_stride_point, feat_stride_level, d_sh, sh_stride, d_viewdirs, samples_per_ray,
                        d_keep, n_points, weights);
     if (rc) return rc;
-    NERF_REQUIRE(d_raw || d_act_minmax, "mlp_fwd: null output");
+    NERF_REQUIRE(n_points == 0 || d_raw || d_act_minmax, "mlp_fwd: null output");
     if (n_points == 0) return NERF_OK;
     a.raw = d_raw;
     a.geo_out = d_geo;
@@ -85,7 +85,7 @@ extern "C" int nerf_mlp_bwd_q(const float* d_feat, int64_t feat_stride_point, in
     int rc = fill_args(a, d_feat, feat_stride_point, feat_stride_level, d_sh, sh_stride, d_viewdirs, samples_per_ray,
                        d_keep, n_points, weights);
     if (rc) return rc;
-    NERF_REQUIRE(d_graw && grads && grads->w0 && grads->w1 && grads->c0 && grads->c1 && grads->c2,
+    NERF_REQUIRE((n_points == 0 || d_graw) && grads && grads->w0 && grads->w1 && grads->c0 && grads->c1 && grads->c2,
                  "mlp_bwd: null gradient pointer");
     if (n_points == 0) return NERF_OK;
     a.graw = d_graw; a.G = *grads; a.dfeat = d_dfeat; a.dsh = d_dsh; a.dgeo = d_dgeo;
@@ -113,7 +113,7 @@ extern "C" int nerf_mlp_bwd_batch(const nerf_mlp_bwd_job* jobs, int n_jobs, floa
                            j.samples_per_ray, j.keep, j.n_points, &j.weights);
         if (rc) return rc;
         const nerf_mlp_grads& g = j.grads;
-        NERF_REQUIRE(j.graw && g.w0 && g.w1 && g.c0 && g.c1 && g.c2, "mlp_bwd_batch: job %d: null gradient pointer", k);
+        NERF_REQUIRE((j.n_points == 0 || j.graw) && g.w0 && g.w1 && g.c0 && g.c1 && g.c2, "mlp_bwd_batch: job %d: null gradient pointer", k);
         x.graw = j.graw; x.G = g; x.dfeat = j.dfeat; x.dsh = j.dsh; x.dgeo = j.dgeo;
         x.aq = reinterpret_cast<const QuantRec*>(j.act_qrec);
         if (x.P > 0) ++n;   // empty jobs launch nothing

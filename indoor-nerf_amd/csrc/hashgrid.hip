@@ -722,7 +722,7 @@ extern "C" int nerf_hash_encode_fwd_q(const float* d_xyz, int64_t n_points, cons
     NERF_REQUIRE(n_points >= 0, "hash_encode_fwd: n_points < 0");
     NERF_REQUIRE(n_levels >= 1 && n_levels <= NERF_MAX_LEVELS, "hash_encode_fwd: n_levels %d", n_levels);
     NERF_REQUIRE(log2_T >= 1 && log2_T <= 30, "hash_encode_fwd: log2_T %d", log2_T);
-    NERF_REQUIRE(d_xyz && d_feat && d_tables && level_res && bbox_min3 && bbox_max3, "hash_encode_fwd: null arg");
+    NERF_REQUIRE((n_points == 0 || (d_xyz && d_feat)) && d_tables && level_res && bbox_min3 && bbox_max3, "hash_encode_fwd: null arg");
     if (n_points == 0) return NERF_OK;
     HashParams hp{};
     for (int l = 0; l < n_levels; ++l) {
@@ -817,7 +817,7 @@ extern "C" int nerf_hash_encode_bwd_bin(const float* d_xyz, int64_t n_points, co
                                         int64_t chunk_base, int64_t chunk_capacity, int deterministic,
                                         void* d_workspace, size_t workspace_bytes, void* stream) {
     NERF_REQUIRE(n_points >= 0, "hash_encode_bwd_bin: n_points < 0");
-    NERF_REQUIRE(d_xyz && d_dfeat && level_res && bbox_min3 && bbox_max3, "hash_encode_bwd_bin: null arg");
+    NERF_REQUIRE((n_points == 0 || (d_xyz && d_dfeat)) && level_res && bbox_min3 && bbox_max3, "hash_encode_bwd_bin: null arg");
     HashGradParams hp{};
     const int rc = bin_layout("hash_encode_bwd_bin", n_levels, log2_T, chunk_capacity, deterministic, d_workspace,
                               workspace_bytes, hp);
@@ -920,7 +920,7 @@ extern "C" int nerf_hash_encode_bwd(const float* d_xyz, int64_t n_points, const 
     NERF_REQUIRE(n_points >= 0, "hash_encode_bwd: n_points < 0");
     NERF_REQUIRE(n_levels >= 1 && n_levels <= NERF_MAX_LEVELS, "hash_encode_bwd: n_levels %d", n_levels);
     NERF_REQUIRE(log2_T >= 1 && log2_T <= 30, "hash_encode_bwd: log2_T %d", log2_T);
-    NERF_REQUIRE(d_xyz && d_dfeat && d_dtables && level_res && bbox_min3 && bbox_max3, "hash_encode_bwd: null arg");
+    NERF_REQUIRE((n_points == 0 || (d_xyz && d_dfeat)) && d_dtables && level_res && bbox_min3 && bbox_max3, "hash_encode_bwd: null arg");
     if (n_points == 0) return NERF_OK;
     HashGradParams hp{};
     for (int l = 0; l < n_levels; ++l) {
@@ -944,6 +944,7 @@ extern "C" int nerf_hash_encode_bwd_ws(const float* d_xyz, int64_t n_points, con
                                        float* const* d_dtables, int deterministic, void* d_workspace,
                                        size_t workspace_bytes, void* stream) {
     NERF_REQUIRE(n_points >= 0, "hash_encode_bwd: n_points < 0");
+    if (n_points == 0) return NERF_OK;
     BinPlan B{};
     const bool binned = d_workspace != nullptr && n_levels >= 1 && n_levels <= NERF_MAX_LEVELS &&
                         make_bin_plan(n_levels, log2_T, n_points, B, deterministic != 0);

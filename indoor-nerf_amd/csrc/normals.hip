@@ -242,7 +242,7 @@ constexpr int kHeadBwdBlocks = 1024;
 
 static int fill_normal(NormalArgs& a, const float* o16, const uint8_t* keep, int64_t P, const nerf_normal_head* W) {
     NERF_REQUIRE(P >= 0, "normal_head: n_points < 0");
-    NERF_REQUIRE(o16 && W && W->n0 && W->b0 && W->n1 && W->b1, "normal_head: null argument");
+    NERF_REQUIRE((P == 0 || o16) && W && W->n0 && W->b0 && W->n1 && W->b1, "normal_head: null argument");
     a.o16 = o16;
     a.keep = keep;
     a.P = P;
@@ -259,7 +259,7 @@ extern "C" int nerf_normal_head_fwd(const float* d_o16, const float* d_raw4, con
     NormalArgs a{};
     int rc = fill_normal(a, d_o16, d_keep, n_points, head);
     if (rc) return rc;
-    NERF_REQUIRE(d_raw4 && d_raw7, "normal_head_fwd: null buffer");
+    NERF_REQUIRE(n_points == 0 || (d_raw4 && d_raw7), "normal_head_fwd: null buffer");
     if (n_points == 0) return NERF_OK;
     a.raw4 = d_raw4;
     a.raw7 = d_raw7;
@@ -279,7 +279,7 @@ extern "C" int nerf_normal_head_bwd(const float* d_o16, const uint8_t* d_keep, i
     NormalArgs a{};
     int rc = fill_normal(a, d_o16, d_keep, n_points, head);
     if (rc) return rc;
-    NERF_REQUIRE(d_graw7 && d_graw4 && d_dgeo && grads && grads->n0 && grads->b0 && grads->n1 && grads->b1,
+    NERF_REQUIRE((n_points == 0 || (d_graw7 && d_graw4 && d_dgeo)) && grads && grads->n0 && grads->b0 && grads->n1 && grads->b1,
                  "normal_head_bwd: null buffer");
     NERF_REQUIRE(d_workspace && workspace_bytes >= nerf_normal_head_bwd_workspace_bytes(),
                  "normal_head_bwd: workspace %zu B < %zu B", workspace_bytes, nerf_normal_head_bwd_workspace_bytes());

@@ -264,8 +264,8 @@ extern "C" int nerf_sample_stratified(const float* d_rays, int64_t ray_stride, i
                                       float* d_dirs, float* d_viewdirs, void* stream) {
     NERF_REQUIRE(n_rays >= 0 && n_samples >= 1, "sample_stratified: R=%lld S=%d", (long long)n_rays, n_samples);
     NERF_REQUIRE(ray_stride >= 8, "sample_stratified: ray_stride %lld < 8", (long long)ray_stride);
+    if (n_rays == 0) return NERF_OK;   // empty batches: nothing is read or written (NULL data allowed)
     NERF_REQUIRE(d_rays && d_t && d_z, "sample_stratified: null arg");
-    if (n_rays == 0) return NERF_OK;
     NERF_REQUIRE(!d_viewdirs || ray_stride > 8, "sample_stratified: viewdirs need ray_stride > 8 (got %lld)",
                  (long long)ray_stride);
     StratArgs a{d_rays, ray_stride, n_rays, n_samples, d_t, lindisp, perturb, d_u, seed, offset, d_rng, d_z, d_pts,
@@ -283,8 +283,8 @@ extern "C" int nerf_sample_pdf(const float* d_bins, int64_t bins_stride, const f
     NERF_REQUIRE(n_rays >= 0 && n_bins >= 2 && n_bins <= kMaxBins && n_importance >= 1,
                  "sample_pdf: R=%lld bins=%d N=%d (bins must be 2..%d)", (long long)n_rays, n_bins, n_importance,
                  kMaxBins);
-    NERF_REQUIRE(d_bins && d_weights && d_samples && (!det || d_t_imp), "sample_pdf: null arg");
     if (n_rays == 0) return NERF_OK;
+    NERF_REQUIRE(d_bins && d_weights && d_samples && (!det || d_t_imp), "sample_pdf: null arg");
     PdfArgs a{};
     a.bins = d_bins; a.bins_stride = bins_stride; a.w = d_weights; a.w_stride = weights_stride;
     a.R = n_rays; a.nb = n_bins; a.N = n_importance; a.det = det; a.t_imp = d_t_imp; a.u = d_u;
@@ -303,8 +303,8 @@ extern "C" int nerf_sample_fine(const float* d_rays, int64_t ray_stride, const f
                  "sample_fine: R=%lld S=%d N=%d (S in 3..%d, S+N <= %d)", (long long)n_rays, n_samples,
                  n_importance, kMaxBins, kMaxMerged);
     NERF_REQUIRE(ray_stride >= 6, "sample_fine: ray_stride %lld < 6", (long long)ray_stride);
-    NERF_REQUIRE(d_rays && d_z && d_weights && d_z_fine && (!det || d_t_imp), "sample_fine: null arg");
     if (n_rays == 0) return NERF_OK;
+    NERF_REQUIRE(d_rays && d_z && d_weights && d_z_fine && (!det || d_t_imp), "sample_fine: null arg");
     PdfArgs a{};
     a.R = n_rays; a.N = n_importance; a.det = det; a.t_imp = d_t_imp; a.u = d_u; a.seed = seed; a.offset = offset;
     a.rng = d_rng;

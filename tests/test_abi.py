@@ -58,6 +58,30 @@ def test_error_path_reports_message(nerf):
         L.call("nerf_mlp_bwd_batch", (L.MlpBwdJob * 3)(), 3, None, 0, None)
 
 
+def test_empty_batches_accept_null_data(nerf):
+    """Zero rays / points: the entries return NERF_OK before any launch and, like torch's empty
+    tensors (data_ptr 0), accept NULL per-point buffers; the same NULLs with one point are refused.
+    Host-only (no GPU call is reached)."""
+    import indoor_nerf_amd._lib as L
+    bb = (L.host_f32([0] * 3), L.host_f32([1] * 3), L.host_f32([16] * 16))
+    tabs = (ctypes.c_void_p * 16)(*([1 << 20] * 16))
+    for n, ok in ((0, True), (1, False)):
+        calls = [
+            lambda: L.call("nerf_sample_stratified", None, 11, n, 64, None, 0, 0, None, 0, 0, None, None, None, None,
+                           None, None),
+            lambda: L.call("nerf_composite_fwd", None, 4, None, None, None, n, 64, 0, *([None] * 7), None),
+            lambda: L.call("nerf_hash_encode_fwd", None, n, *bb, 16, 19, tabs, None, 2, 2, None, None),
+            lambda: L.call("nerf_hash_encode_bwd", None, n, *bb, 16, 19, None, 2, 2, tabs, None),
+            lambda: L.call("nerf_sh4_fwd", None, n, None, None),
+        ]
+        for c in calls:
+            if ok:
+                c()
+            else:
+                with pytest.raises(RuntimeError, match="null|bad args"):
+                    c()
+
+
 def _oracle_lib():
     path = os.path.join(ROOT, "oracle", "_build", "libhashgrid_ref.so")
     if not os.path.exists(path):
