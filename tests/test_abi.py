@@ -82,6 +82,18 @@ def test_empty_batches_accept_null_data(nerf):
                     c()
 
 
+def test_mlp_refuses_batches_past_32bit_indexing(nerf):
+    """The MLP kernels form 32-bit element indices: a batch whose feature / output indices would
+    pass 2^31 is refused on the host before any launch (2^27 points x 16 levels), one below is not
+    checked here (it would launch)."""
+    import indoor_nerf_amd._lib as L
+    fake = ctypes.c_void_p(1 << 20)
+    w = L.MlpWeights(*([1 << 20] * 5))
+    P = 1 << 27
+    with pytest.raises(RuntimeError, match="32-bit indexing"):
+        L.call("nerf_mlp_fwd", fake, 2, 2 * P, None, 0, fake, 192, None, P, ctypes.byref(w), fake, None, None)
+
+
 def _oracle_lib():
     path = os.path.join(ROOT, "oracle", "_build", "libhashgrid_ref.so")
     if not os.path.exists(path):
