@@ -12,6 +12,9 @@
  *   - Host arrays (level resolutions, table pointer lists, bbox) are read during the call only.
  *   - `stream` is a hipStream_t passed as void* (torch.cuda.current_stream().cuda_stream).
  *   - Return 0 on success, else a NERF_E_* code; nerf_last_error() gives the message (per thread).
+ *   - Empty batches (0 rays / points) return 0 without launching, and their per-ray / per-point
+ *     buffers may be NULL (torch's empty tensors have data_ptr 0), as the reference's torch ops
+ *     accept empty tensors; weights, tables and host arrays are still validated.
  *   - Random draws: a NULL d_u* argument means "draw in-kernel" from Philox4x32-10 keyed by
  *     (seed, offset); a non-NULL one supplies the uniforms (the reference's pytest=True path).
  *     A non-NULL d_rng (device uint64[2]) overrides (seed, offset) — used when a whole training
