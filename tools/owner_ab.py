@@ -3,7 +3,8 @@
 (4096 x 64) sets binned side by side ("bin": both bin launches), then the owner launch alone
 ("owner"), HIP-event medians. JSON out. A/B of library builds: run once per build with
 NERF_HIP_LIB=<path> (e.g. chunk sizes: tools/build_variant.py); NERF_DET=1 times the
-deterministic mode."""
+deterministic mode; NERF_FINE_S=128 sizes the fine set to the importance samples alone (DESIGN §8.5:
+what the backward and the fine gather ("fwd") would cost without the coarse points' re-encoding)."""
 import json
 import os
 import sys
@@ -31,7 +32,16 @@ def main():
     lo, hi = blender_bbox()
     emb = nerf.HashEmbedder((torch.from_numpy(lo), torch.from_numpy(hi)), finest_resolution=1024).to(dev)
     meta = emb._meta
-    sets = [ray_points(4096, 192, dev, seed=1)[0], ray_points(4096, 64, dev, seed=2)[0]]
+    s_fine = int(os.environ.get("NERF_FINE_S", "192"))
+    sets = [ray_points(4096, s_fine, dev, seed=1)[0], ray_points(4096, 64, dev, seed=2)[0]]
+    tabs = _lib.ptr_array([e.weight.detach() for e in emb.embeddings])
+    feat = torch.empty(16, sets[0].shape[0], 2, device=dev)
+    keep = torch.empty(sets[0].shape[0], dtype=torch.uint8, device=dev)
+
+    def fwd():
+        _lib.call("nerf_hash_encode_fwd", _lib.ptr(sets[0]), sets[0].shape[0], meta["bmin"], meta["bmax"], meta["res"],
+                  16, 19, tabs, _lib.ptr(feat), 2, 2 * sets[0].shape[0], _lib.ptr(keep, dtype=torch.uint8),
+                  _lib.stream())
     lib = _lib.load()
     C = int(lib.nerf_hash_bwd_chunk_points())
     chunks = [(p.shape[0] + C - 1) // C for p in sets]
@@ -60,13 +70,13 @@ def main():
 
     res = {}
     for rnd in range(5):
-        for v in ("bin", "owner"):
+        for v in ("bin", "owner", "fwd"):
             ts = []
             for k in range(12):
                 bins()   # every owner pass consumes the entries binned before it
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
-                (bins if v == "bin" else owner)()
+                {"bin": bins, "owner": owner, "fwd": fwd}[v]()
                 e1.record()
                 if v == "bin":
                     owner()
@@ -74,7 +84,8 @@ def main():
                 if k >= 2:
                     ts.append(e0.elapsed_time(e1))
             res.setdefault(v, []).append(float(np.median(ts)))
-    print(json.dumps({k: round(float(np.median(v)) * 1e3, 1) for k, v in res.items()} | {"unit": "us", "chunks": cap, "chunk_points": C, "det": det}))
+    print(json.dumps({k: round(float(np.median(v)) * 1e3, 1) for k, v in res.items()} | {"unit": "us", "chunks": cap, "chunk_points": C, "det": det,
+                      "fine_samples": s_fine}))
 
 
 if __name__ == "__main__":
