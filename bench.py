@@ -35,6 +35,9 @@ X6_PEAK_TFLOPS = 2500.0 / 6
 # Algorithmic cost per unit of each OP: bytes (HBM-bound) or FLOPs (MFMA). An op is
 # one or more ABI calls priced together: the hash backward is the bin pass (once per render pass)
 # plus the owner pass (once per iteration), and only their sum is a complete scatter-add.
+# Hash ops are priced per DISTINCT point encoded ("hash_point"): with the coarse-feature reuse (DESIGN
+# §8.5) the fine pass encodes only its importance samples, so an iteration encodes R x (64 + 128) points
+# (R x (64 + 192) without it); the MLP and compositing ops run on every point / sample of both passes.
 #   hash fwd : per point  16 levels x 8 corners x 8 B gathered + 12 B xyz + 128 B features + 1 B keep
 #   hash fwd packed (A-CAQ eval): as hash fwd with 2-B entries (two 8-bit codes)
 #   hash bwd : per point  16 x 8 x 8 B read+write of the added rows (2 x 1024) + 12 B xyz + 128 B d feat
@@ -43,12 +46,15 @@ X6_PEAK_TFLOPS = 2500.0 / 6
 #   composite: per sample 16 B raw + 4 B z + 4 B weights (fwd) / + 16 B grad (bwd)
 #   radam    : per table/MLP element 28 B (read p, g, m, v; write p, m, v)
 OPS = {
-    "hash_bwd": dict(calls=("nerf_hash_encode_bwd_bin", "nerf_hash_encode_bwd_owner", "nerf_hash_encode_bwd_ws",
-                            "nerf_hash_encode_bwd"), bound="hbm", per_unit=2 * 16 * 8 * 8 + 12 + 128, unit="point"),
-    "hash_fwd": dict(calls=("nerf_hash_encode_fwd",), bound="hbm", per_unit=16 * 8 * 8 + 12 + 128 + 1, unit="point"),
+    "hash_bwd": dict(calls=("nerf_hash_encode_bwd_bin", "nerf_hash_encode_bwd_bin_rows", "nerf_hash_encode_bwd_owner",
+                            "nerf_hash_encode_bwd_ws", "nerf_hash_encode_bwd"), bound="hbm",
+                     per_unit=2 * 16 * 8 * 8 + 12 + 128, unit="hash_point"),
+    # nerf_hash_encode_fwd_rows also copies the coarse features into the fine rows (priced as encoding)
+    "hash_fwd": dict(calls=("nerf_hash_encode_fwd", "nerf_hash_encode_fwd_rows"), bound="hbm",
+                     per_unit=16 * 8 * 8 + 12 + 128 + 1, unit="hash_point"),
     # A-CAQ eval (int-packed tables, configs[4]): 8-bit codes = 2 B per corner entry (two features)
     "hash_fwd_packed": dict(calls=("nerf_hash_encode_fwd_packed",), bound="hbm", per_unit=16 * 8 * 2 + 12 + 128 + 1,
-                            unit="point"),
+                            unit="hash_point"),
     "mlp_bwd": dict(calls=("nerf_mlp_bwd", "nerf_mlp_bwd_batch"), bound="mfma", per_unit=2 * 18688, unit="point"),
     "mlp_fwd": dict(calls=("nerf_mlp_fwd",), bound="mfma", per_unit=18688, unit="point"),
     "composite_fwd": dict(calls=("nerf_composite_fwd",), bound="hbm", per_unit=24, unit="sample"),
@@ -66,8 +72,10 @@ STEP_RAY_BYTES = 64
 # ABI call -> the kernel symbols it launches (rocprofv3 names), to attach PMC traffic per call
 KERNEL_SYMBOLS = {
     "nerf_hash_encode_fwd": ["nerf::hash_encode_fwd_pair_kernel<false>"],
-    "nerf_hash_encode_fwd_packed": ["nerf::hash_encode_fwd_packed_kernel"],
+    "nerf_hash_encode_fwd_rows": ["nerf::hash_encode_fwd_pair_kernel<false>"],
+    "nerf_hash_encode_fwd_packed": ["nerf::hash_encode_fwd_packed_pair_kernel"],
     "nerf_hash_encode_bwd_bin": ["nerf::hash_encode_bwd_kernel<3, 512>"],
+    "nerf_hash_encode_bwd_bin_rows": ["nerf::hash_encode_bwd_kernel<3, 512>"],
     "nerf_tv_bwd_bin": ["nerf::tv_bwd_bin_kernel<512>"],
     "nerf_hash_encode_bwd_owner": ["nerf::hash_bwd_owner_kernel<13, 1024, false>"],
     "nerf_mlp_fwd": ["nerf::mlp_fwd_x6_kernel<false>"],
@@ -85,7 +93,7 @@ def base_name(abi_name):
 
 def traffic_file():
     """The newest committed PMC traffic summary (tools/profile_bench.sh), or None."""
-    for name in ("r03_traffic.json", "r02_traffic.json", "r01j_traffic.json"):
+    for name in ("r04_traffic.json", "r03_traffic.json", "r02_traffic.json", "r01j_traffic.json"):
         path = os.path.join(ROOT, "profiles", name)
         if os.path.exists(path):
             return path
@@ -125,17 +133,21 @@ def gpu_clocks():
     return out or None
 
 
-def op_rooflines(kernels, steps, units, dense_elems):
+def op_rooflines(kernels, steps, units, dense_elems, hash_entries=None):
     """Per OP (OPS) per iteration: achieved = algorithmic bytes (FLOPs) of the op's units in one
     iteration / the op's summed kernel time in one iteration (HIP events), against the MI355X peak;
-    traffic = the committed PMC bytes of the op's kernels per iteration."""
+    traffic = the committed PMC bytes of the op's kernels per iteration. units: {"point", "sample",
+    "hash_point"} counts per iteration. hash_entries: entries the hash backward's bins emitted in one
+    iteration (nerf_hash_bwd_entry_count): when they are fewer than 0.1 per point-level the backward
+    did not do the priced work (the A-CAQ configuration's zero feature gradients), and the
+    op is reported without a roofline fraction."""
     out = []
     for op, d in OPS.items():
         calls = [c for c in kernels if base_name(c) in d["calls"]]
         if not calls:
             continue
         t_step = sum(kernels[c]["total_ms"] for c in calls) * 1e-3 / steps
-        n = dense_elems if d["unit"] == "element" else units
+        n = dense_elems if d["unit"] == "element" else units[d["unit"]]
         work = d["per_unit"] * n
         traffic = 0.0
         for c in calls:
@@ -158,6 +170,13 @@ def op_rooflines(kernels, steps, units, dense_elems):
                               "(csrc/field_x6.hip)"}
         r.update(ms_per_step=round(1e3 * t_step, 4), calls={c: kernels[c]["launches"] // max(1, steps) for c in calls},
                  units_per_step=n, per_unit=d["per_unit"], unit_name=d["unit"])
+        if op == "hash_bwd" and hash_entries is not None:
+            per_pl = hash_entries / max(1, n * 16)
+            r.update(entries_per_step=hash_entries, entries_per_point_level=round(per_pl, 3))
+            if per_pl < 0.1:
+                r.update(degenerate=True, achieved=None, frac=None,
+                         note="the bins emitted < 0.1 entries per point-level (zero feature gradients): the kernels "
+                              "did not do the priced work, so no roofline fraction is claimed")
         out.append(r)
     out.sort(key=lambda r: -r["ms_per_step"])
     return out
@@ -170,7 +189,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--rays", type=int, default=4096)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-rays", type=int, default=1024)
+    ap.add_argument("--cpu-rays", type=int, default=4096, help="rays of the CPU leg's timed iterations (the bench batch)")
     ap.add_argument("--cpu-warmup", type=int, default=6)
     ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--profile-kernels", type=int, default=1, help="record HIP events per kernel in the timed region")
@@ -189,6 +208,8 @@ def parse():
     ap.add_argument("--deterministic", type=int, default=0,
                     help="1: bitwise-reproducible backward (nerf.set_deterministic: fixed-point hash owner pass, "
                          "ordered MLP weight-gradient reduction)")
+    ap.add_argument("--coarse-reuse", type=int, default=1,
+                    help="1: the fine pass reuses the coarse pass's hash encoding (DESIGN §8.5); 0: re-encode (A/B)")
     ap.add_argument("--mode", default="train", choices=["train", "render"],
                     help="train: full training iteration (the metric); render: render-only (eval modules, no grad)")
     return ap.parse_args()
@@ -298,21 +319,24 @@ def cpu_leg(n_rays, finest, H, warmup, timed):
 
 
 def cpu_baseline(n_rays, warmup, timed):
-    """SURVEY.md §8(d)'s CPU baseline on the GPU box's host cores, rank 0 at N=1 only: the lego leg
-    (configs[1]'s finest 1024 at 800x800) is `value`; the chair leg is BASELINE configs[0] (chair
-    400x400, finest_res 512, the reference's CPU path: configs/chair.txt). n_rays per iteration is
-    the configs' own N_rand (1024) so that the two legs stay within ~1 minute of CPU time; per-ray
-    work dominates the iteration (RAdam's dense pass is ~10 ms of a multi-second step), so rays/s at
-    1024 rays stands for the 4096-ray batch."""
+    """SURVEY.md §8(d)'s CPU baseline on the GPU box's host cores, rank 0 at N=1 only. `value` is the
+    lego leg (configs[1]: finest 1024, 800x800) at the bench's own batch (n_rays = 4096), 2 warm-up
+    iterations and the median of 2 (RAdam's update is still off there, radam.py:63-92: a ~10 ms dense
+    pass of a ~9 s iteration). The same leg at 1024 rays with `warmup` warm-ups (RAdam active) and the
+    median of `timed` is reported beside it, so the batch-size effect is measured, and the
+    chair leg is BASELINE configs[0] (chair 400x400, finest_res 512, the reference's CPU path:
+    configs/chair.txt) at its own N_rand of 1024."""
     cores, threads = cpu_threads()
     torch.set_num_threads(threads)
-    lego = cpu_leg(n_rays, 1024, 800, warmup, timed)
-    chair = cpu_leg(n_rays, 512, 400, warmup, timed)
+    lego = cpu_leg(n_rays, 1024, 800, 2, 2)
+    lego_1k = cpu_leg(1024, 1024, 800, warmup, timed)
+    chair = cpu_leg(1024, 512, 400, warmup, timed)
     return {"value": lego["value"], "unit": "rays/s", "cores": threads, "kind": "port",
             "render_only": lego["render_only"], "step_s": lego["step_s"],
             "sample": "lego leg: " + lego["sample"],
             "cpu": cpu_model(), "affinity_cores": cores,
             "threads_note": "torch.set_num_threads = the job's CPU share (OMP_NUM_THREADS) within the affinity mask",
+            "lego_1024_rays": lego_1k,
             "chair": {**chair, "config": "BASELINE configs[0]: chair 400x400, finest_res 512 (configs/chair.txt)"}}
 
 
@@ -390,6 +414,7 @@ def main():
     nerf.manual_seed(1234 + rank)
     if a.deterministic:
         nerf.set_deterministic(True)
+    nerf.set_coarse_reuse(bool(a.coarse_reuse))
     kw, kw_test, _, grad_vars, opt = nerf.create_nerf(args, device=dev)
     for d in (kw, kw_test):
         d.update(near=wl["near"], far=wl["far"])     # train() adds the scene bounds (run_nerf.py:768-770,865-869)
@@ -492,16 +517,25 @@ def main():
     roofline, ops = None, []
     ns, ni = wl["args"]["N_samples"], wl["args"]["N_importance"]
     points_per_step = R * (ns + (ns + ni if ni else 0))
+    # distinct points the hash encoding handles: the fine pass's row-mapped gather means the reuse ran
+    reused = any(base_name(c) == "nerf_hash_encode_fwd_rows" for c in kernels)
+    units = {"point": points_per_step, "sample": points_per_step,
+             "hash_point": R * (ns + ni) if (reused and ni) else points_per_step}
+    hash_entries = None
+    if kernels and a.mode == "train":
+        from indoor_nerf_amd.hashgrid import pending_bins
+        hash_entries = pending_bins(dev).last_entry_count()
     if kernels:
-        ops = op_rooflines(kernels, a.steps, points_per_step, sum(p.numel() for p in params))
-        if ops:
+        ops = op_rooflines(kernels, a.steps, units, sum(p.numel() for p in params), hash_entries)
+        ranked = [o for o in ops if not o.get("degenerate")]
+        if ranked:
             # the dominant op: largest kernel time per iteration after grouping (hash bwd = bin + owner)
-            d = ops[0]
+            d = ranked[0]
             roofline = {k: d[k] for k in ("bound", "achieved", "peak", "unit", "frac", "traffic")}
             roofline.update(op=d["op"], ms_per_step=d["ms_per_step"], calls_per_step=d["calls"],
                             units_per_step=d["units_per_step"], per_unit=d["per_unit"], unit_name=d["unit_name"],
                             top3=[{k: o[k] for k in ("op", "bound", "ms_per_step", "achieved", "unit", "frac")}
-                                  for o in ops[:3]])
+                                  for o in ranked[:3]])
             if d["traffic"] is not None:
                 roofline["traffic_source"] = (os.path.relpath(traffic_file(), ROOT) + ": rocprofv3 FETCH_SIZE x2 (4/8/16-B "
                                               "per-lane reads count half, 2-B reads are not counted: "
@@ -538,6 +572,7 @@ def main():
                    "samples": f"{wl['args']['N_samples']}+{wl['args']['N_importance']}",
                    "parallelism": f"dp{world}" + ("-zero1" if zero else "")},
         "hip_graph": bool(gstep is not None and gstep.captures > 0),
+        "coarse_reuse": reused,
         "loss": round(float(loss), 6),
         "roofline": roofline,
         "step_roofline": step_roofline,

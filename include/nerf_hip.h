@@ -78,6 +78,21 @@ int nerf_hash_encode_fwd_q(const float* d_xyz, int64_t n_points,
                            float* d_feat, int64_t feat_stride_point, int64_t feat_stride_level,
                            uint8_t* d_keep, void* stream);
 
+/* Row-mapped forward of a render_rays fine pass with the coarse-feature reuse: the
+ * fine point set of a ray holds every coarse point bit for bit (run_nerf.py:512-516) and one embedder
+ * serves both nets (run_nerf.py:225,275). Point p of the n_points gathered ones is d_xyz row p
+ * (contiguous: the importance samples) and writes feature / keep row d_rows[p] (int32); in the same
+ * launch the n_copy coarse points' features d_copy_feat (level-major [L][n_copy][2]) and keep flags
+ * d_copy_keep are copied to rows d_copy_rows[i] of d_feat / d_keep. Copies need even, 8-B aligned
+ * feature pairs. */
+int nerf_hash_encode_fwd_rows(const float* d_xyz, const int32_t* d_rows, int64_t n_points,
+                              const float* bbox_min3, const float* bbox_max3,
+                              const float* level_res, int n_levels, int log2_T,
+                              const float* const* d_tables, const float* d_qrec,
+                              float* d_feat, int64_t feat_stride_point, int64_t feat_stride_level,
+                              uint8_t* d_keep, const float* d_copy_feat, const uint8_t* d_copy_keep,
+                              const int32_t* d_copy_rows, int64_t n_copy, void* stream);
+
 /* d_dtables: host array of n_levels device pointers; gradients are ACCUMULATED (atomic adds). */
 int nerf_hash_encode_bwd(const float* d_xyz, int64_t n_points,
                          const float* bbox_min3, const float* bbox_max3,
@@ -129,9 +144,28 @@ int nerf_hash_encode_bwd_bin(const float* d_xyz, int64_t n_points,
                              const float* d_dfeat, int64_t feat_stride_point, int64_t feat_stride_level,
                              int64_t chunk_base, int64_t chunk_capacity, int deterministic,
                              void* d_workspace, size_t workspace_bytes, void* stream);
+/* Row-mapped bin (coarse-feature reuse): point p reads d_xyz and d_dfeat at row d_rows[p] (NULL: p);
+ * with d_dfeat2 != NULL it adds d_dfeat2 at row d_rows2[p] (NULL: p; strides feat2_*) to its
+ * gradient, so a point shared by two passes is binned once with the sum of both gradients (d_dfeat
+ * may then be NULL: the point's gradient is the d_dfeat2 term alone). */
+int nerf_hash_encode_bwd_bin_rows(const float* d_xyz, const int32_t* d_rows, int64_t n_points,
+                                  const float* bbox_min3, const float* bbox_max3,
+                                  const float* level_res, int n_levels, int log2_T,
+                                  const float* d_dfeat, int64_t feat_stride_point, int64_t feat_stride_level,
+                                  const float* d_dfeat2, const int32_t* d_rows2,
+                                  int64_t feat2_stride_point, int64_t feat2_stride_level,
+                                  int64_t chunk_base, int64_t chunk_capacity, int deterministic,
+                                  void* d_workspace, size_t workspace_bytes, void* stream);
 int nerf_hash_encode_bwd_owner(int n_levels, int log2_T, int64_t n_chunks, int64_t chunk_capacity,
                                float* const* d_dtables, int deterministic, void* d_workspace,
                                size_t workspace_bytes, void* stream);
+
+/* Entries the bin launches of chunks [0, n_chunks) of a workspace emitted (sum of their segment counts:
+ * after the run merge, without zero entries), stored to d_count (device uint64). A measurement for the
+ * bench's pricing of the hash backward; same workspace rules as the owner pass. */
+int nerf_hash_bwd_entry_count(int n_levels, int log2_T, int64_t n_chunks, int64_t chunk_capacity, int deterministic,
+                              const void* d_workspace, size_t workspace_bytes, unsigned long long* d_count,
+                              void* stream);
 
 /* ---- spherical harmonics, degree 4 (SHEncoder.forward, hash_encoding.py:153-191) ---------- */
 int nerf_sh4_fwd(const float* d_dirs, int64_t n, float* d_out /* [n,16] */, void* stream);
@@ -228,6 +262,8 @@ typedef struct {
     float* dsh;
     const float* dgeo;
     const float* act_qrec;
+    const int32_t* dfeat_rows;   /* optional: point p's d feat is written to row dfeat_rows[p] of dfeat (NULL: p);
+                                    the coarse-feature reuse's importance-first order, nerf_sample_fine_rows d_perm */
 } nerf_mlp_bwd_job;
 
 size_t nerf_mlp_bwd_det_workspace_bytes(void);
@@ -309,6 +345,18 @@ int nerf_sample_fine(const float* d_rays, int64_t ray_stride, const float* d_z, 
                      int64_t n_rays, int n_samples, int n_importance, int det, const float* d_t_imp,
                      const float* d_u, uint64_t seed, uint64_t offset, const uint64_t* d_rng,
                      float* d_z_fine, float* d_pts_fine, float* d_z_std, float* d_samples, void* stream);
+/* Same, also writing the maps of the merge (NULL = skip; coarse-feature reuse):
+ * d_coarse_rows [R,S] int32 = the absolute fine row r*(S+N) + rank of coarse sample i of ray r;
+ * d_imp_rows [R,N] int32 = the fine rows of the ray's importance samples, ascending; d_imp_pts [R,N,3]
+ * their points (the same bits as d_pts_fine at those rows); d_perm [R*(S+N)] int32 = fine row ->
+ * position in the importance-first order (importance k of ray r: r*N + k; coarse i: R*N + r*S + i).
+ * Needs R*(S+N) <= INT32_MAX when a map is set. */
+int nerf_sample_fine_rows(const float* d_rays, int64_t ray_stride, const float* d_z, const float* d_weights,
+                          int64_t n_rays, int n_samples, int n_importance, int det, const float* d_t_imp,
+                          const float* d_u, uint64_t seed, uint64_t offset, const uint64_t* d_rng,
+                          float* d_z_fine, float* d_pts_fine, float* d_z_std, float* d_samples,
+                          int32_t* d_coarse_rows, int32_t* d_imp_rows, float* d_imp_pts, int32_t* d_perm,
+                          void* stream);
 
 /* ---- rays of the training batch / of a whole image (run_nerf.py:973-1004, run_nerf_helpers.py:311-320)
  * Camera: c2w = the pose [3,4] as float32 (torch.Tensor(pose)), fx = K[0][0], fy = K[1][1],

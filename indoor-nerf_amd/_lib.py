@@ -38,7 +38,7 @@ class MlpBwdJob(ctypes.Structure):
     _fields_ = [("feat", c_vp), ("feat_stride_point", c_i64), ("feat_stride_level", c_i64), ("sh", c_vp),
                 ("sh_stride", c_i64), ("viewdirs", c_vp), ("samples_per_ray", c_i64), ("keep", c_vp),
                 ("n_points", c_i64), ("weights", MlpWeights), ("graw", c_vp), ("grads", MlpGrads), ("dfeat", c_vp),
-                ("dsh", c_vp), ("dgeo", c_vp), ("act_qrec", c_vp)]
+                ("dsh", c_vp), ("dgeo", c_vp), ("act_qrec", c_vp), ("dfeat_rows", c_vp)]
 
 
 PRIORS_MAX_RAYS = 8192   # NERF_PRIORS_MAX_RAYS
@@ -93,6 +93,11 @@ SIGNATURES = {
                                  c_i64, c_int, c_vp, ctypes.c_size_t, c_vp],
     "nerf_hash_encode_bwd_owner": [c_int, c_int, c_i64, c_i64, ctypes.POINTER(c_vp), c_int, c_vp, ctypes.c_size_t,
                                    c_vp],
+    "nerf_hash_encode_fwd_rows": [c_vp, c_vp, c_i64, c_f32p, c_f32p, c_f32p, c_int, c_int, ctypes.POINTER(c_vp),
+                                  c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp],
+    "nerf_hash_encode_bwd_bin_rows": [c_vp, c_vp, c_i64, c_f32p, c_f32p, c_f32p, c_int, c_int, c_vp, c_i64, c_i64,
+                                      c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_int, c_vp, ctypes.c_size_t, c_vp],
+    "nerf_hash_bwd_entry_count": [c_int, c_int, c_i64, c_i64, c_int, c_vp, ctypes.c_size_t, c_vp, c_vp],
     "nerf_sh4_fwd": [c_vp, c_i64, c_vp, c_vp],
     "nerf_mlp_fwd": [c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, ctypes.POINTER(MlpWeights),
                      c_vp, c_vp, c_vp],
@@ -122,6 +127,8 @@ SIGNATURES = {
                         c_vp],
     "nerf_sample_fine": [c_vp, c_i64, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_vp, c_vp, c_u64, c_u64, c_vp,
                          c_vp, c_vp, c_vp, c_vp, c_vp],
+    "nerf_sample_fine_rows": [c_vp, c_i64, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_vp, c_vp, c_u64, c_u64, c_vp,
+                              c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
     "nerf_sample_rays": [ctypes.POINTER(Camera), c_int, c_int, c_int, c_int, c_int, c_int, c_i64, c_int, c_u64,
                          c_u64, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp],
     "nerf_rays_pack": [c_vp, c_vp, c_i64, ctypes.c_float, ctypes.c_float, c_int, ctypes.c_float, ctypes.c_float,

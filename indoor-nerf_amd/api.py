@@ -12,7 +12,7 @@ from .quantization import FakeQuantizer, LearnedBitwidthQuantizer, PassthroughQu
 from .rays import RaySampler, crop_window
 from .scene import get_bbox3d_for_blenderobj, get_bbox3d_for_llff
 from .render import (batchify_rays, camera, check_numerics, set_debug, get_rays, get_rays_np, img2mse, manual_seed, mse2psnr, ndc_rays, raw2outputs,
-                     render, render_path, render_rays, sample_pdf, to8b)
+                     render, render_path, render_rays, sample_pdf, set_coarse_reuse, coarse_reuse, to8b)
 from .data import load_blender_data, load_llff_data, load_scannet_data, pose_spherical
 from .priors import (ManhattanFrameEstimator, SemanticPlaneDetector, combine_structural_losses_v2, manhattan_sdf_loss,
                      spatial_normal_consistency_loss, structured_planarity_loss)
@@ -26,7 +26,8 @@ __all__ = ["HashEmbedder", "SHEncoder", "NeRFSmall", "RAdam", "run_network", "ba
            "get_bbox3d_for_blenderobj", "get_bbox3d_for_llff", "render_path", "load_blender_data", "load_llff_data",
            "pose_spherical", "load_scannet_data", "ManhattanFrameEstimator", "SemanticPlaneDetector",
            "combine_structural_losses_v2", "manhattan_sdf_loss", "spatial_normal_consistency_loss",
-           "structured_planarity_loss", "set_deterministic", "deterministic", "check_numerics", "set_debug"]
+           "structured_planarity_loss", "set_deterministic", "deterministic", "check_numerics", "set_debug",
+           "set_coarse_reuse", "coarse_reuse"]
 
 
 def load_library():

@@ -116,6 +116,7 @@ extern "C" int nerf_mlp_bwd_batch(const nerf_mlp_bwd_job* jobs, int n_jobs, floa
         NERF_REQUIRE((j.n_points == 0 || j.graw) && g.w0 && g.w1 && g.c0 && g.c1 && g.c2, "mlp_bwd_batch: job %d: null gradient pointer", k);
         x.graw = j.graw; x.G = g; x.dfeat = j.dfeat; x.dsh = j.dsh; x.dgeo = j.dgeo;
         x.aq = reinterpret_cast<const QuantRec*>(j.act_qrec);
+        x.dfeat_rows = j.dfeat_rows;
         if (x.P > 0) ++n;   // empty jobs launch nothing
     }
     if (n == 0) return NERF_OK;

@@ -32,6 +32,7 @@ struct MlpArgs {
     const float* graw;
     nerf_mlp_grads G;
     float* dfeat;
+    const int32_t* dfeat_rows;   // bwd, optional: point p's d feat goes to row dfeat_rows[p] (NULL: p)
     float* dsh;
     float* geo_out;       // fwd, optional: o = [sigma, geo 15] per point, [P,16] (normals head input)
     const float* dgeo;    // bwd, optional: upstream d o from the normals head, [P,16] (row 0 ignored)

@@ -839,7 +839,8 @@ __device__ __forceinline__ void bwd_wgrad_role(const MlpArgs& a, const __bf16* i
         const uint32_t pt = (uint32_t)(tile * 32 + j);
         if (a.dfeat && tile * 32 + j < a.P) {
             // offsets formed per tile (opaque stride): hoisted out of the loop they pin 16 registers
-            const uint32_t sl = (uint32_t)a.sl + (uint32_t)opaque_zero(), base = pt * (uint32_t)a.sp;
+            const uint32_t row = a.dfeat_rows ? (uint32_t)a.dfeat_rows[pt] : pt;
+            const uint32_t sl = (uint32_t)a.sl + (uint32_t)opaque_zero(), base = row * (uint32_t)a.sp;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int fi = row_of(r, h);

@@ -48,23 +48,65 @@ struct HashGradParams {
 // level): grouping the 6 coarse levels of the lego config took the forward from 121 to 107 us per
 // launch (same box; 3 or 6 levels in flight: 114 / 154 us, the registers cost occupancy).
 
+// Coarse-feature reuse, fused into the fine pass's forward launch: blocks past the
+// gather blocks of each grid row copy that row's level(s) of the coarse pass's features (and, in the
+// row of level 0, the keep flags) of kCopyPts points into their fine rows. The fine point set of a
+// ray holds every coarse point bit for bit (run_nerf.py:512-516 sorts cat(z_vals, z_samples); one
+// embedder serves both nets, run_nerf.py:225,275), so these rows need no gather.
+struct FwdCopy {
+    const float* src;        // coarse features, level-major [L][n][2] (ssp = 2, ssl = 2n)
+    int64_t ssp, ssl;
+    const uint8_t* skeep;
+    const int32_t* rows;     // fine row of coarse point i
+    int64_t n;
+    int gather_blocks;       // blocks [0, gather_blocks) of a grid row gather, the rest copy
+};
+constexpr int kCopyPerThread = 4;
+constexpr int kCopyPts = 256 * kCopyPerThread;
+
+__device__ __forceinline__ void fwd_copy_block(const FwdCopy& cp, int cb, int l0, int nl, float* __restrict__ feat,
+                                               int64_t sp, int64_t sl, uint8_t* __restrict__ keep) {
+    int64_t i[kCopyPerThread], r[kCopyPerThread];
+#pragma unroll
+    for (int k = 0; k < kCopyPerThread; ++k) {
+        i[k] = (int64_t)cb * kCopyPts + k * 256 + threadIdx.x;
+        r[k] = i[k] < cp.n ? (int64_t)cp.rows[i[k]] : -1;
+    }
+    for (int l = l0; l < l0 + nl; ++l) {
+        float2 v[kCopyPerThread];
+#pragma unroll
+        for (int k = 0; k < kCopyPerThread; ++k)
+            if (r[k] >= 0) v[k] = *reinterpret_cast<const float2*>(cp.src + i[k] * cp.ssp + (int64_t)l * cp.ssl);
+#pragma unroll
+        for (int k = 0; k < kCopyPerThread; ++k)
+            if (r[k] >= 0) *reinterpret_cast<float2*>(feat + r[k] * sp + (int64_t)l * sl) = v[k];
+    }
+    if (l0 == 0 && keep) {
+#pragma unroll
+        for (int k = 0; k < kCopyPerThread; ++k)
+            if (r[k] >= 0) keep[r[k]] = cp.skeep[i[k]];
+    }
+}
+
 template <bool QUANT>
 __global__ void __launch_bounds__(256) hash_encode_fwd_pair_kernel(
-    const float* __restrict__ xyz, int64_t n, HashParams hp, int group,
+    const float* __restrict__ xyz, const int32_t* __restrict__ out_rows, int64_t n, HashParams hp, int group,
     float* __restrict__ feat, int64_t sp, int64_t sl, uint8_t* __restrict__ keep,
-    const QuantRec* __restrict__ qrec) {
-#ifdef NERF_AB_FWD_POINT_MAJOR   // A/B only: all levels of a point block dispatched together
-    const int64_t t = (int64_t)blockIdx.y * blockDim.x + threadIdx.x;
-    const int row = blockIdx.x;
-#else
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const QuantRec* __restrict__ qrec, FwdCopy cp) {
     const int row = blockIdx.y;
-#endif
+    if ((int)blockIdx.x >= cp.gather_blocks) {
+        const bool grouped = group > 0 && row == 0;
+        fwd_copy_block(cp, (int)blockIdx.x - cp.gather_blocks, grouped ? 0 : (group > 0 ? group + row - 1 : row),
+                       grouped ? group : 1, feat, sp, sl, keep);
+        return;
+    }
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t p = t >> 1;
     const int xb = (int)(t & 1);
     const bool valid = p < n;
-    const int64_t pc = valid ? p : n - 1;             // invalid lanes mirror a valid point (no stores)
-    const float x = xyz[3 * pc + 0], y = xyz[3 * pc + 1], z = xyz[3 * pc + 2];
+    const int64_t pc0 = valid ? p : n - 1;            // invalid lanes mirror a valid point (no stores)
+    const float x = xyz[3 * pc0 + 0], y = xyz[3 * pc0 + 1], z = xyz[3 * pc0 + 2];
+    const int64_t pc = out_rows ? (int64_t)out_rows[pc0] : pc0;   // row of the point in feat / keep
     const bool fast = hp.fastdiv && __ballot(!fastdiv_point_ok(x, y, z)) == 0ull;   // wave-uniform
     if (group > 0 && row == 0) {
         for (int l0 = 0; l0 < group; l0 += kFwdGroupRound) {
@@ -78,7 +120,7 @@ __global__ void __launch_bounds__(256) hash_encode_fwd_pair_kernel(
             }
 #pragma unroll
             for (int g = 0; g < kFwdGroupRound; ++g)
-                if (l0 + g < group) fwd_finish<QUANT>(s[g], l0 + g, xb, valid, p, feat, sp, sl, keep, qrec);
+                if (l0 + g < group) fwd_finish<QUANT>(s[g], l0 + g, xb, valid, pc, feat, sp, sl, keep, qrec);
         }
         return;
     }
@@ -86,8 +128,9 @@ __global__ void __launch_bounds__(256) hash_encode_fwd_pair_kernel(
     FwdLvl s;
     if (fast) fwd_gather<true>(x, y, z, hp, lvl, xb, s);
     else fwd_gather<false>(x, y, z, hp, lvl, xb, s);
-    fwd_finish<QUANT>(s, lvl, xb, valid, p, feat, sp, sl, keep, qrec);
+    fwd_finish<QUANT>(s, lvl, xb, valid, pc, feat, sp, sl, keep, qrec);
 }
+
 
 // Backward: dL/de_c = ((g*(1-wz or wz))*(1-wy or wy))*(1-wx or wx), the order autograd applies the
 // three blend steps in reverse; scatter-added with fp32 atomics (no-return global_atomic_add_f32).
@@ -222,20 +265,39 @@ __device__ __forceinline__ void bin_chunk(const HashGradParams& hp, int lvl, int
     }
 }
 
+// Optional row maps of a bin launch (coarse-feature reuse): point p reads xyz and dfeat
+// at row rows[p] (NULL: p), and adds dfeat2 at row rows2[p] (NULL: p; NULL dfeat2: nothing) to its
+// gradient.
+struct BinRows {
+    const int32_t* rows;
+    const float* dfeat2;
+    const int32_t* rows2;
+    int64_t sp2, sl2;
+};
+
 // MODE 1: coalesced float atomics (no workspace); 3: binned (default).
 template <int MODE, int THREADS>
 __global__ void __launch_bounds__(THREADS) hash_encode_bwd_kernel(
     const float* __restrict__ xyz, int64_t n, HashGradParams hp,
-    const float* __restrict__ dfeat, int64_t sp, int64_t sl) {
+    const float* __restrict__ dfeat, int64_t sp, int64_t sl, BinRows br) {
     const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int lvl = blockIdx.y;
     const bool valid = p < n;
     float x = 0.f, y = 0.f, z = 0.f, gx = 0.f, gy = 0.f;
     if (valid) {
-        x = xyz[3 * p + 0]; y = xyz[3 * p + 1]; z = xyz[3 * p + 2];
-        const float* src = dfeat + p * sp + (int64_t)lvl * sl;
-        gx = src[0];
-        gy = src[1];
+        const int64_t r = br.rows ? (int64_t)br.rows[p] : p;
+        x = xyz[3 * r + 0]; y = xyz[3 * r + 1]; z = xyz[3 * r + 2];
+        if (dfeat) {
+            const float* src = dfeat + r * sp + (int64_t)lvl * sl;
+            gx = src[0];
+            gy = src[1];
+        }
+        if (br.dfeat2) {   // the same point's gradient from a second pass (coarse-feature reuse)
+            const int64_t r2 = br.rows2 ? (int64_t)br.rows2[p] : p;
+            const float2 g2 = *reinterpret_cast<const float2*>(br.dfeat2 + r2 * br.sp2 + (int64_t)lvl * br.sl2);
+            gx += g2.x;
+            gy += g2.y;
+        }
     }
     AxisCell ax, ay, az;
     if (hp.fastdiv && __ballot(valid && !fastdiv_point_ok(x, y, z)) == 0ull) {   // wave-uniform
@@ -439,12 +501,8 @@ __global__ void __launch_bounds__(THREADS) hash_bwd_owner_kernel(HashGradParams 
     // heavy ones (235 us; owner launch 255 -> 248 us on one box, profiles/r03i_ab_owner_order.jsonl).
     // Finest first alone is slower (273 us): the coarse pass's bins, written last, are partly still
     // in the Infinity Cache when the early blocks read them.
-#if defined(NERF_OWNER_LEVEL_MAJOR)   // A/B only
-    const int o = blockIdx.x, lvl = blockIdx.y;
-#else
     const int o = blockIdx.x, y = blockIdx.y;
     const int lvl = (y & 1) ? (y >> 1) : (int)gridDim.y - 1 - (y >> 1);
-#endif
     const int S = 1 << hp.slice_log2, n_own = 1 << hp.owner_log2;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     for (int i = tid; i < (DET ? 2 : 1) * S; i += kOwnerThreads) s_slice[i] = Acc{0, 0};
@@ -529,11 +587,6 @@ __global__ void __launch_bounds__(THREADS) hash_bwd_owner_kernel(HashGradParams 
             if (E >= B63) reload(E);
             const uint32_t lim = min(min(E + 64u, B63), e_end);
             const uint32_t e = E + lane;
-#ifdef NERF_OWNER_AB_NO_LOOKUP   // diagnostic A/B only: no entry -> chunk lookup (wrong addresses)
-            ok = e < lim;
-            addr = region0 + e;
-            return lim;
-#endif
             int idx = __popcll(__ballot(Bw <= E)) - 1;
             uint64_t inner = __ballot(Bw > E && Bw < lim);
             while (inner) {
@@ -561,14 +614,9 @@ __global__ void __launch_bounds__(THREADS) hash_bwd_owner_kernel(HashGradParams 
             for (int j = 0; j < NB; ++j) {
                 // default-policy loads: the coarse pass's bins were written just before this launch and part
                 // of them is still in the Infinity Cache (nontemporal loads: 0.39 vs 0.33 ms per step)
-#ifdef NERF_OWNER_AB_NO_LOAD   // diagnostic A/B only: no entry loads (lookup + LDS sums alone)
-                h[j] = (uint16_t)((addr[j] * 2654435761u) >> 19);
-                g[j] = make_float2((float)(addr[j] & 255), 1.f);
-#else
                 h[j] = hp.bin_h[addr[j]];
                 const uint64_t gv = *reinterpret_cast<const uint64_t*>(hp.bin_g + addr[j]);   // (d feat0, d feat1)
                 g[j] = make_float2(__uint_as_float((uint32_t)gv), __uint_as_float((uint32_t)(gv >> 32)));
-#endif
             }
         };
         // software pipeline: the next batch's loads are in flight while this batch's adds run
@@ -603,12 +651,6 @@ __global__ void __launch_bounds__(THREADS) hash_bwd_owner_kernel(HashGradParams 
                         atomicAdd(r + 2, (unsigned long long)lx);
                         atomicAdd(r + 3, (unsigned long long)ly);
                     } else {
-#ifdef NERF_OWNER_AB_NO_ATOMIC   // diagnostic A/B only: plain LDS read-modify-write (racy) instead of atomics
-                        Acc t = s_slice[h[j]];
-                        t.x += g[j].x;
-                        t.y += g[j].y;
-                        s_slice[h[j]] = t;
-#else
                         if constexpr (A32) {
                             atomicAdd(&s_slice[h[j]].x, g[j].x);
                             atomicAdd(&s_slice[h[j]].y, g[j].y);
@@ -616,7 +658,6 @@ __global__ void __launch_bounds__(THREADS) hash_bwd_owner_kernel(HashGradParams 
                             atomicAdd(&s_slice[h[j]].x, (double)g[j].x);
                             atomicAdd(&s_slice[h[j]].y, (double)g[j].y);
                         }
-#endif
                     }
                 }
             }
@@ -686,6 +727,29 @@ __global__ void __launch_bounds__(THREADS) hash_bwd_owner_kernel(HashGradParams 
     }
 }
 
+// Entries a step's bin launches emitted (the counts of every segment word of chunks [0, n_chunks)):
+// a measurement for bench.py's pricing of the hash backward (bins drop zero entries and merge runs).
+__global__ void __launch_bounds__(1024) bin_entry_count_kernel(const uint32_t* __restrict__ seg, int64_t n_words_per_lvl,
+                                                               int64_t stride, int n_chunks, int L,
+                                                               unsigned long long* __restrict__ count) {
+    unsigned long long part = 0;
+    const int64_t total = (int64_t)L * n_words_per_lvl * n_chunks;
+    for (int64_t i = threadIdx.x; i < total; i += blockDim.x) {
+        const int64_t row = i / n_chunks, c = i - row * n_chunks;
+        part += seg[row * stride + c] >> 16;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+    __shared__ unsigned long long s_part[16];
+    if ((threadIdx.x & 63) == 0) s_part[threadIdx.x >> 6] = part;
+    __syncthreads();
+    if (threadIdx.x == 0) {   // one block: a plain store, in a fixed order
+        unsigned long long t = 0;
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += s_part[w];
+        *count = t;
+    }
+}
+
 struct BinPlan {
     int slice_log2, owner_log2, nchunks;
     size_t off_h, off_g, off_off, off_max, total;   // byte offsets in the workspace
@@ -714,16 +778,16 @@ static bool make_bin_plan(int n_levels, int log2_T, int64_t n_points, BinPlan& B
 
 using namespace nerf;
 
-extern "C" int nerf_hash_encode_fwd_q(const float* d_xyz, int64_t n_points, const float* bbox_min3,
-                                      const float* bbox_max3, const float* level_res, int n_levels, int log2_T,
-                                      const float* const* d_tables, const float* d_qrec, float* d_feat,
-                                      int64_t feat_stride_point, int64_t feat_stride_level, uint8_t* d_keep,
-                                      void* stream) {
+static int hash_encode_fwd_impl(const float* d_xyz, const int32_t* d_rows, int64_t n_points, const float* bbox_min3,
+                                const float* bbox_max3, const float* level_res, int n_levels, int log2_T,
+                                const float* const* d_tables, const float* d_qrec, float* d_feat,
+                                int64_t feat_stride_point, int64_t feat_stride_level, uint8_t* d_keep, void* stream,
+                                FwdCopy cp = FwdCopy{}) {
     NERF_REQUIRE(n_points >= 0, "hash_encode_fwd: n_points < 0");
     NERF_REQUIRE(n_levels >= 1 && n_levels <= NERF_MAX_LEVELS, "hash_encode_fwd: n_levels %d", n_levels);
     NERF_REQUIRE(log2_T >= 1 && log2_T <= 30, "hash_encode_fwd: log2_T %d", log2_T);
     NERF_REQUIRE((n_points == 0 || (d_xyz && d_feat)) && d_tables && level_res && bbox_min3 && bbox_max3, "hash_encode_fwd: null arg");
-    if (n_points == 0) return NERF_OK;
+    if (n_points == 0 && cp.n == 0) return NERF_OK;
     HashParams hp{};
     for (int l = 0; l < n_levels; ++l) {
         NERF_REQUIRE(d_tables[l], "hash_encode_fwd: table %d is null", l);
@@ -736,28 +800,53 @@ extern "C" int nerf_hash_encode_fwd_q(const float* d_xyz, int64_t n_points, cons
     // coarse levels grouped into one grid row: the leading levels whose (res + 1)^3 vertices fit the
     // table (no hash collisions, a small set of hot lines)
     int group = 0;
-#ifndef NERF_AB_FWD_NO_GROUP   // A/B only: every level in its own grid row
     while (group < std::min(n_levels, kFwdGroupMax)) {
         const double v = (double)level_res[group] + 1.0;
         if (v * v * v > (double)(1u << log2_T)) break;
         ++group;
     }
     if (group < 2) group = 0;
-#endif
     const int rows = group > 0 ? n_levels - group + 1 : n_levels;
-#ifdef NERF_AB_FWD_POINT_MAJOR
-    dim3 grid2(rows, blocks_for(2 * n_points, 256));
-#else
-    dim3 grid2(blocks_for(2 * n_points, 256), rows);
-#endif
+    cp.gather_blocks = (int)blocks_for(2 * n_points, 256);
+    dim3 grid2(cp.gather_blocks + (unsigned)blocks_for(cp.n, kCopyPts), rows);
     if (q)
         hipLaunchKernelGGL(hash_encode_fwd_pair_kernel<true>, grid2, dim3(256), 0, as_stream(stream), d_xyz,
-                           n_points, hp, group, d_feat, feat_stride_point, feat_stride_level, d_keep, q);
+                           d_rows, n_points, hp, group, d_feat, feat_stride_point, feat_stride_level, d_keep, q, cp);
     else
         hipLaunchKernelGGL(hash_encode_fwd_pair_kernel<false>, grid2, dim3(256), 0, as_stream(stream), d_xyz,
-                           n_points, hp, group, d_feat, feat_stride_point, feat_stride_level, d_keep, q);
+                           d_rows, n_points, hp, group, d_feat, feat_stride_point, feat_stride_level, d_keep, q, cp);
     NERF_CHECK_LAUNCH("hash_encode_fwd");
     return NERF_OK;
+}
+
+extern "C" int nerf_hash_encode_fwd_q(const float* d_xyz, int64_t n_points, const float* bbox_min3,
+                                      const float* bbox_max3, const float* level_res, int n_levels, int log2_T,
+                                      const float* const* d_tables, const float* d_qrec, float* d_feat,
+                                      int64_t feat_stride_point, int64_t feat_stride_level, uint8_t* d_keep,
+                                      void* stream) {
+    return hash_encode_fwd_impl(d_xyz, nullptr, n_points, bbox_min3, bbox_max3, level_res, n_levels, log2_T, d_tables,
+                                d_qrec, d_feat, feat_stride_point, feat_stride_level, d_keep, stream);
+}
+
+extern "C" int nerf_hash_encode_fwd_rows(const float* d_xyz, const int32_t* d_rows, int64_t n_points,
+                                         const float* bbox_min3, const float* bbox_max3, const float* level_res,
+                                         int n_levels, int log2_T, const float* const* d_tables, const float* d_qrec,
+                                         float* d_feat, int64_t feat_stride_point, int64_t feat_stride_level,
+                                         uint8_t* d_keep, const float* d_copy_feat, const uint8_t* d_copy_keep,
+                                         const int32_t* d_copy_rows, int64_t n_copy, void* stream) {
+    NERF_REQUIRE(n_points >= 0 && n_copy >= 0, "hash_encode_fwd_rows: n_points %lld n_copy %lld", (long long)n_points,
+                 (long long)n_copy);
+    NERF_REQUIRE(n_points == 0 || d_rows, "hash_encode_fwd_rows: null row map");
+    NERF_REQUIRE(n_copy == 0 || (d_copy_feat && d_copy_rows && d_feat && (!d_keep || d_copy_keep)),
+                 "hash_encode_fwd_rows: null copy arg");
+    NERF_REQUIRE(n_copy == 0 || (feat_stride_point % 2 == 0 && feat_stride_level % 2 == 0 &&
+                                 ((uintptr_t)d_feat & 7) == 0 && ((uintptr_t)d_copy_feat & 7) == 0),
+                 "hash_encode_fwd_rows: copied feature pairs must be 8-B aligned");
+    NERF_REQUIRE(n_copy < ((int64_t)1 << 31) / 2, "hash_encode_fwd_rows: n_copy %lld", (long long)n_copy);
+    FwdCopy cp{};
+    cp.src = d_copy_feat; cp.ssp = 2; cp.ssl = 2 * n_copy; cp.skeep = d_copy_keep; cp.rows = d_copy_rows; cp.n = n_copy;
+    return hash_encode_fwd_impl(d_xyz, d_rows, n_points, bbox_min3, bbox_max3, level_res, n_levels, log2_T, d_tables,
+                                d_qrec, d_feat, feat_stride_point, feat_stride_level, d_keep, stream, cp);
 }
 
 extern "C" int nerf_hash_encode_fwd(const float* d_xyz, int64_t n_points, const float* bbox_min3,
@@ -811,13 +900,19 @@ extern "C" size_t nerf_hash_encode_bwd_workspace_bytes(int n_levels, int log2_T,
     return B.total;
 }
 
-extern "C" int nerf_hash_encode_bwd_bin(const float* d_xyz, int64_t n_points, const float* bbox_min3,
-                                        const float* bbox_max3, const float* level_res, int n_levels, int log2_T,
-                                        const float* d_dfeat, int64_t feat_stride_point, int64_t feat_stride_level,
-                                        int64_t chunk_base, int64_t chunk_capacity, int deterministic,
-                                        void* d_workspace, size_t workspace_bytes, void* stream) {
+extern "C" int nerf_hash_encode_bwd_bin_rows(const float* d_xyz, const int32_t* d_rows, int64_t n_points,
+                                             const float* bbox_min3, const float* bbox_max3, const float* level_res,
+                                             int n_levels, int log2_T, const float* d_dfeat, int64_t feat_stride_point,
+                                             int64_t feat_stride_level, const float* d_dfeat2, const int32_t* d_rows2,
+                                             int64_t feat2_stride_point, int64_t feat2_stride_level,
+                                             int64_t chunk_base, int64_t chunk_capacity, int deterministic,
+                                             void* d_workspace, size_t workspace_bytes, void* stream) {
     NERF_REQUIRE(n_points >= 0, "hash_encode_bwd_bin: n_points < 0");
-    NERF_REQUIRE((n_points == 0 || (d_xyz && d_dfeat)) && level_res && bbox_min3 && bbox_max3, "hash_encode_bwd_bin: null arg");
+    NERF_REQUIRE((n_points == 0 || (d_xyz && (d_dfeat || d_dfeat2))) && level_res && bbox_min3 && bbox_max3,
+                 "hash_encode_bwd_bin: null arg");
+    NERF_REQUIRE(n_points == 0 || !d_dfeat2 || (((uintptr_t)d_dfeat2 & 7) == 0 && feat2_stride_point % 2 == 0 &&
+                                                feat2_stride_level % 2 == 0),
+                 "hash_encode_bwd_bin: dfeat2 needs 8-B aligned feature pairs");
     HashGradParams hp{};
     const int rc = bin_layout("hash_encode_bwd_bin", n_levels, log2_T, chunk_capacity, deterministic, d_workspace,
                               workspace_bytes, hp);
@@ -831,10 +926,23 @@ extern "C" int nerf_hash_encode_bwd_bin(const float* d_xyz, int64_t n_points, co
     hp.fastdiv = fill_cells(hp.cell, bbox_min3, bbox_max3, level_res, n_levels) ? 1u : 0u;
     hp.chunk_base = (int)chunk_base;
     hp.nchunks = (int)(chunk_base + nch);
+    const BinRows br{d_rows, d_dfeat2, d_rows2, feat2_stride_point, feat2_stride_level};
     hipLaunchKernelGGL((hash_encode_bwd_kernel<3, kChunkPts>), dim3((unsigned)nch, n_levels), dim3(kChunkPts), 0, as_stream(stream),
-                       d_xyz, n_points, hp, d_dfeat, feat_stride_point, feat_stride_level);
+                       d_xyz, n_points, hp, d_dfeat, feat_stride_point, feat_stride_level, br);
     NERF_CHECK_LAUNCH("hash_encode_bwd_bin");
     return NERF_OK;
+}
+
+extern "C" int nerf_hash_encode_bwd_bin(const float* d_xyz, int64_t n_points, const float* bbox_min3,
+                                        const float* bbox_max3, const float* level_res, int n_levels, int log2_T,
+                                        const float* d_dfeat, int64_t feat_stride_point, int64_t feat_stride_level,
+                                        int64_t chunk_base, int64_t chunk_capacity, int deterministic,
+                                        void* d_workspace, size_t workspace_bytes, void* stream) {
+    NERF_REQUIRE(n_points == 0 || d_dfeat, "hash_encode_bwd_bin: null arg");
+    return nerf_hash_encode_bwd_bin_rows(d_xyz, nullptr, n_points, bbox_min3, bbox_max3, level_res, n_levels, log2_T,
+                                         d_dfeat, feat_stride_point, feat_stride_level, nullptr, nullptr, 0, 0,
+                                         chunk_base, chunk_capacity, deterministic, d_workspace, workspace_bytes,
+                                         stream);
 }
 
 static int64_t tv_bin_chunks(int n_levels, const int* cube) {
@@ -912,6 +1020,21 @@ extern "C" int nerf_hash_encode_bwd_owner(int n_levels, int log2_T, int64_t n_ch
     return NERF_OK;
 }
 
+extern "C" int nerf_hash_bwd_entry_count(int n_levels, int log2_T, int64_t n_chunks, int64_t chunk_capacity,
+                                         int deterministic, const void* d_workspace, size_t workspace_bytes,
+                                         unsigned long long* d_count, void* stream) {
+    HashGradParams hp{};
+    const int rc = bin_layout("hash_bwd_entry_count", n_levels, log2_T, chunk_capacity, deterministic & 1,
+                              const_cast<void*>(d_workspace), workspace_bytes, hp);
+    if (rc) return rc;
+    NERF_REQUIRE(n_chunks >= 0 && n_chunks <= chunk_capacity && d_count, "hash_bwd_entry_count: n_chunks %lld of %lld",
+                 (long long)n_chunks, (long long)chunk_capacity);
+    hipLaunchKernelGGL(bin_entry_count_kernel, dim3(1), dim3(1024), 0, as_stream(stream), hp.bin_seg,
+                       (int64_t)1 << hp.owner_log2, (int64_t)hp.chunk_stride, (int)n_chunks, n_levels, d_count);
+    NERF_CHECK_LAUNCH("hash_bwd_entry_count");
+    return NERF_OK;
+}
+
 // No workspace: coalesced memory-side float atomics (never deterministic).
 extern "C" int nerf_hash_encode_bwd(const float* d_xyz, int64_t n_points, const float* bbox_min3,
                                     const float* bbox_max3, const float* level_res, int n_levels, int log2_T,
@@ -931,7 +1054,8 @@ extern "C" int nerf_hash_encode_bwd(const float* d_xyz, int64_t n_points, const 
     hp.fastdiv = fill_cells(hp.cell, bbox_min3, bbox_max3, level_res, n_levels) ? 1u : 0u;
     hp.mask = (uint32_t)((1u << log2_T) - 1u);
     hipLaunchKernelGGL((hash_encode_bwd_kernel<1, 256>), dim3(blocks_for(n_points, 256), n_levels), dim3(256), 0,
-                       as_stream(stream), d_xyz, n_points, hp, d_dfeat, feat_stride_point, feat_stride_level);
+                       as_stream(stream), d_xyz, n_points, hp, d_dfeat, feat_stride_point, feat_stride_level,
+                       BinRows{nullptr, nullptr, nullptr, 0, 0});
     NERF_CHECK_LAUNCH("hash_encode_bwd");
     return NERF_OK;
 }
@@ -944,6 +1068,10 @@ extern "C" int nerf_hash_encode_bwd_ws(const float* d_xyz, int64_t n_points, con
                                        float* const* d_dtables, int deterministic, void* d_workspace,
                                        size_t workspace_bytes, void* stream) {
     NERF_REQUIRE(n_points >= 0, "hash_encode_bwd: n_points < 0");
+    NERF_REQUIRE(n_levels >= 1 && n_levels <= NERF_MAX_LEVELS, "hash_encode_bwd: n_levels %d", n_levels);
+    NERF_REQUIRE(log2_T >= 1 && log2_T <= 30, "hash_encode_bwd: log2_T %d", log2_T);
+    NERF_REQUIRE(d_dtables && level_res && bbox_min3 && bbox_max3, "hash_encode_bwd: null arg");
+    for (int l = 0; l < n_levels; ++l) NERF_REQUIRE(d_dtables[l], "hash_encode_bwd: grad table %d is null", l);
     if (n_points == 0) return NERF_OK;
     BinPlan B{};
     const bool binned = d_workspace != nullptr && n_levels >= 1 && n_levels <= NERF_MAX_LEVELS &&
@@ -954,7 +1082,6 @@ extern "C" int nerf_hash_encode_bwd_ws(const float* d_xyz, int64_t n_points, con
         return nerf_hash_encode_bwd(d_xyz, n_points, bbox_min3, bbox_max3, level_res, n_levels, log2_T, d_dfeat,
                                     feat_stride_point, feat_stride_level, d_dtables, stream);
     }
-    if (n_points == 0) return NERF_OK;
     const int64_t nch = (n_points + kChunkPts - 1) / kChunkPts;
     int rc = nerf_hash_encode_bwd_bin(d_xyz, n_points, bbox_min3, bbox_max3, level_res, n_levels, log2_T, d_dfeat,
                                       feat_stride_point, feat_stride_level, 0, nch, deterministic, d_workspace,

@@ -242,60 +242,12 @@ __device__ __forceinline__ void load_codes(const uint8_t* base, uint32_t h, cons
     f1 = (((float)c1 + q.qmin) - q.zp) * q.scale;
 }
 
-template <int BITS>
-__device__ __forceinline__ void gather_level(const uint8_t* base, const uint32_t (&h)[8], const QuantRec& q,
-                                             float (&e0)[8], float (&e1)[8]) {
-    if constexpr (BITS == 32) {
-        const float2* t = reinterpret_cast<const float2*>(base);
-#pragma unroll
-        for (int c = 0; c < 8; ++c) { const float2 v = t[h[c]]; e0[c] = v.x; e1[c] = v.y; }
-    } else {
-#pragma unroll
-        for (int c = 0; c < 8; ++c) load_codes<BITS>(base, h[c], q, e0[c], e1[c]);
-    }
-}
-
-__global__ void __launch_bounds__(256) hash_encode_fwd_packed_kernel(
-    const float* __restrict__ xyz, int64_t n, HashParams hp, int64_t T, const uint8_t* __restrict__ packed,
-    const QuantRec* __restrict__ qrec, float* __restrict__ feat, int64_t sp, int64_t sl, uint8_t* __restrict__ keep) {
-    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int lvl = blockIdx.y;
-    if (p >= n) return;
-    const float x = xyz[3 * p + 0], y = xyz[3 * p + 1], z = xyz[3 * p + 2];
-    const AxisCell ax = axis_cell(x, hp.bmin[0], hp.bmax[0], hp.cell[lvl][0]);
-    const AxisCell ay = axis_cell(y, hp.bmin[1], hp.bmax[1], hp.cell[lvl][1]);
-    const AxisCell az = axis_cell(z, hp.bmin[2], hp.bmax[2], hp.cell[lvl][2]);
-    if (lvl == 0 && keep) keep[p] = (ax.inside && ay.inside && az.inside) ? 1 : 0;
-    uint32_t h[8];
-#pragma unroll
-    for (int c = 0; c < 8; ++c)
-        h[c] = spatial_hash3((uint32_t)ax.base + ((c >> 2) & 1), (uint32_t)ay.base + ((c >> 1) & 1),
-                             (uint32_t)az.base + (c & 1), hp.mask);
-    const QuantRec q = qrec[lvl];
-    const uint8_t* base = packed + (size_t)lvl * (size_t)T * 8;
-    float e0[8], e1[8];
-    switch (code_width(q)) {   // uniform per block (one level per blockIdx.y)
-        case 4: gather_level<4>(base, h, q, e0, e1); break;
-        case 8: gather_level<8>(base, h, q, e0, e1); break;
-        case 16: gather_level<16>(base, h, q, e0, e1); break;
-        default: gather_level<32>(base, h, q, e0, e1); break;
-    }
-    const float f0 = trilerp(e0, ax.w, ay.w, az.w), f1 = trilerp(e1, ax.w, ay.w, az.w);
-    float* dst = feat + p * sp + (int64_t)lvl * sl;
-    if (((sp | sl) & 1) == 0) {
-        *reinterpret_cast<float2*>(dst) = make_float2(f0, f1);
-    } else {
-        dst[0] = f0;
-        dst[1] = f1;
-    }
-}
-
 // Lane-pair packed gather (the fp32 forward's structure, hashgrid.hip hash_encode_fwd_pair_kernel):
 // lanes 2m and 2m+1 share point m and gather the x = 0 / x = 1 corners of its voxel, so corners
 // (x, y, z) and (x+1, y, z), which hash to h and h ^ (x ^ (x+1)), leave in one instruction's line;
 // level-major grid rows (one level's packed table hot in each XCD's L2), the coarse levels whose
 // (res + 1)^3 vertices fit the table grouped into row 0, and the fast division of the voxel math.
-// The dequantized corners blend exactly as the fp32 forward (bit-identical to the one-thread path).
+// The dequantized corners blend exactly as the fp32 forward (bit-identical to nerf_hash_encode_fwd_q with the same eval-mode records).
 template <int BITS>
 __device__ __forceinline__ float2 packed_entry(const uint8_t* base, uint32_t h, const QuantRec& q) {
     if constexpr (BITS == 32) {
@@ -421,7 +373,7 @@ extern "C" int nerf_quant_minmax(const float* d_x, int64_t count, uint32_t* d_mi
 extern "C" int nerf_hash_gather_minmax(const float* d_xyz, int64_t n_points, const float* bbox_min3,
                                        const float* bbox_max3, const float* level_res, int n_levels, int log2_T,
                                        const float* const* d_tables, uint32_t* d_minmax, void* stream) {
-    NERF_REQUIRE(d_xyz && d_tables && d_minmax && n_points >= 0, "hash_gather_minmax: bad args");
+    NERF_REQUIRE(d_tables && d_minmax && n_points >= 0 && (n_points == 0 || d_xyz), "hash_gather_minmax: bad args");
     HashParams hp{};
     int rc = hash_params(hp, bbox_min3, bbox_max3, level_res, n_levels, log2_T, d_tables);
     if (rc) return rc;
@@ -485,18 +437,12 @@ extern "C" int nerf_hash_encode_fwd_packed(const float* d_xyz, int64_t n_points,
                                            const void* d_packed, const float* d_qrec, float* d_feat,
                                            int64_t feat_stride_point, int64_t feat_stride_level, uint8_t* d_keep,
                                            void* stream) {
-    NERF_REQUIRE(n_points >= 0 && d_xyz && d_packed && d_qrec && d_feat, "hash_encode_fwd_packed: bad args");
+    NERF_REQUIRE(n_points >= 0 && d_packed && d_qrec && (n_points == 0 || (d_xyz && d_feat)),
+                 "hash_encode_fwd_packed: bad args");
     HashParams hp{};
     int rc = hash_params(hp, bbox_min3, bbox_max3, level_res, n_levels, log2_T, nullptr);
     if (rc) return rc;
     if (n_points == 0) return NERF_OK;
-#ifdef NERF_AB_PACKED_ONE_THREAD   // A/B only: the one-point-per-thread packed gather
-    dim3 grid(blocks_for(n_points, 256), n_levels);
-    hipLaunchKernelGGL(hash_encode_fwd_packed_kernel, grid, dim3(256), 0, as_stream(stream), d_xyz, n_points, hp,
-                       int64_t(1) << log2_T, reinterpret_cast<const uint8_t*>(d_packed),
-                       reinterpret_cast<const QuantRec*>(d_qrec), d_feat, feat_stride_point, feat_stride_level,
-                       d_keep);
-#else
     int group = 0;   // coarse levels whose (res + 1)^3 vertices fit the table share grid row 0
     while (group < std::min(n_levels, kFwdGroupMax)) {
         const double v = (double)level_res[group] + 1.0;
@@ -509,7 +455,6 @@ extern "C" int nerf_hash_encode_fwd_packed(const float* d_xyz, int64_t n_points,
                        as_stream(stream), d_xyz, n_points, hp, group, int64_t(1) << log2_T,
                        reinterpret_cast<const uint8_t*>(d_packed), reinterpret_cast<const QuantRec*>(d_qrec), d_feat,
                        feat_stride_point, feat_stride_level, d_keep);
-#endif
     NERF_CHECK_LAUNCH("hash_encode_fwd_packed");
     return NERF_OK;
 }

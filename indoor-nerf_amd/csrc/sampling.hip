@@ -68,6 +68,11 @@ struct PdfArgs {
     // fine mode
     const float* rays; int64_t ray_stride; const float* z; int S;
     float* z_fine; float* pts_fine; float* z_std;
+    // optional fine-row maps (coarse-feature reuse): absolute row r*M + rank of coarse
+    // sample i ([R,S]) and of the k-th importance sample in emission order ([R,N]); the importance
+    // samples' points in that order ([R,N,3]); perm [R*M]: fine row -> its position in the
+    // importance-first order (importance k of ray r -> r*N + k, coarse i -> R*N + r*S + i)
+    int32_t* coarse_rows; int32_t* imp_rows; float* imp_pts; int32_t* perm;
 };
 
 // Build the CDF of weights (+1e-5, normalised, cumsum in fp64 as the CPU reference does) in LDS and
@@ -189,13 +194,26 @@ __global__ void __launch_bounds__(256) sample_fine_kernel(PdfArgs a) {
     }
     const float* ray = a.rays + r * a.ray_stride;
     const float ox = ray[0], oy = ray[1], oz = ray[2], dx = ray[3], dy = ray[4], dz = ray[5];
-    auto emit = [&](int rank, float v) {
+    // writes merged position `rank` of the ray, returns its absolute row r*M + rank
+    auto put = [&](int rank, float v) {
         const int64_t o = r * M + rank;
         a.z_fine[o] = v;
         if (a.pts_fine) {
             a.pts_fine[3 * o + 0] = ox + dx * v;
             a.pts_fine[3 * o + 1] = oy + dy * v;
             a.pts_fine[3 * o + 2] = oz + dz * v;
+        }
+        return o;
+    };
+    // importance sample k of the ray at fine row o: the row maps and its point (same ops as pts_fine)
+    auto imp = [&](int k, int64_t o, float v) {
+        const int64_t q = r * N + k;
+        if (a.imp_rows) a.imp_rows[q] = (int32_t)o;
+        if (a.perm) a.perm[o] = (int32_t)q;
+        if (a.imp_pts) {
+            a.imp_pts[3 * q + 0] = ox + dx * v;
+            a.imp_pts[3 * q + 1] = oy + dy * v;
+            a.imp_pts[3 * q + 2] = oz + dz * v;
         }
     };
     // torch.sort(cat(z_vals, z_samples)) (run_nerf.py:573). The stratified coarse depths are already
@@ -232,13 +250,16 @@ __global__ void __launch_bounds__(256) sample_fine_kernel(PdfArgs a) {
             const float v = all_l[i];
             int lo = 0, hi = N;
             while (lo < hi) { const int mid = (lo + hi) >> 1; if (f[mid] < v) lo = mid + 1; else hi = mid; }
-            emit(i + lo, v);
+            const int64_t o = put(i + lo, v);
+            if (a.coarse_rows) a.coarse_rows[r * S + i] = (int32_t)o;
+            if (a.perm) a.perm[o] = (int32_t)(a.R * N + r * S + i);
         }
         for (int j = lane; j < N; j += 64) {
             const float v = f[j];
             int lo = 0, hi = S;
             while (lo < hi) { const int mid = (lo + hi) >> 1; if (all_l[mid] <= v) lo = mid + 1; else hi = mid; }
-            emit(j + lo, v);
+            const int64_t o = put(j + lo, v);
+            imp(j, o, v);   // ascending along the ray
         }
         return;
     }
@@ -250,7 +271,13 @@ __global__ void __launch_bounds__(256) sample_fine_kernel(PdfArgs a) {
             const float w = all_l[i];
             rank += (w < v) || (w == v && i < e);
         }
-        emit(rank, v);
+        const int64_t o = put(rank, v);
+        if (e < S) {
+            if (a.coarse_rows) a.coarse_rows[r * S + e] = (int32_t)o;
+            if (a.perm) a.perm[o] = (int32_t)(a.R * N + r * S + e);
+        } else {
+            imp(e - S, o, v);
+        }
     }
 }
 
@@ -294,15 +321,20 @@ extern "C" int nerf_sample_pdf(const float* d_bins, int64_t bins_stride, const f
     return NERF_OK;
 }
 
-extern "C" int nerf_sample_fine(const float* d_rays, int64_t ray_stride, const float* d_z, const float* d_weights,
-                                int64_t n_rays, int n_samples, int n_importance, int det, const float* d_t_imp,
-                                const float* d_u, uint64_t seed, uint64_t offset, const uint64_t* d_rng,
-                                float* d_z_fine, float* d_pts_fine, float* d_z_std, float* d_samples, void* stream) {
+extern "C" int nerf_sample_fine_rows(const float* d_rays, int64_t ray_stride, const float* d_z, const float* d_weights,
+                                     int64_t n_rays, int n_samples, int n_importance, int det, const float* d_t_imp,
+                                     const float* d_u, uint64_t seed, uint64_t offset, const uint64_t* d_rng,
+                                     float* d_z_fine, float* d_pts_fine, float* d_z_std, float* d_samples,
+                                     int32_t* d_coarse_rows, int32_t* d_imp_rows, float* d_imp_pts, int32_t* d_perm,
+                                     void* stream) {
     NERF_REQUIRE(n_rays >= 0 && n_samples >= 3 && n_samples <= kMaxBins && n_importance >= 1 &&
                      n_samples + n_importance <= kMaxMerged,
                  "sample_fine: R=%lld S=%d N=%d (S in 3..%d, S+N <= %d)", (long long)n_rays, n_samples,
                  n_importance, kMaxBins, kMaxMerged);
     NERF_REQUIRE(ray_stride >= 6, "sample_fine: ray_stride %lld < 6", (long long)ray_stride);
+    NERF_REQUIRE((!d_coarse_rows && !d_imp_rows && !d_perm) || n_rays * (int64_t)(n_samples + n_importance) <= INT32_MAX,
+                 "sample_fine: %lld fine rows do not fit the int32 row maps",
+                 (long long)(n_rays * (int64_t)(n_samples + n_importance)));
     if (n_rays == 0) return NERF_OK;
     NERF_REQUIRE(d_rays && d_z && d_weights && d_z_fine && (!det || d_t_imp), "sample_fine: null arg");
     PdfArgs a{};
@@ -310,7 +342,17 @@ extern "C" int nerf_sample_fine(const float* d_rays, int64_t ray_stride, const f
     a.rng = d_rng;
     a.samples = d_samples; a.rays = d_rays; a.ray_stride = ray_stride; a.z = d_z; a.w = d_weights; a.S = n_samples;
     a.z_fine = d_z_fine; a.pts_fine = d_pts_fine; a.z_std = d_z_std;
+    a.coarse_rows = d_coarse_rows; a.imp_rows = d_imp_rows; a.imp_pts = d_imp_pts; a.perm = d_perm;
     hipLaunchKernelGGL(sample_fine_kernel, dim3(blocks_for(n_rays, 4)), dim3(256), 0, as_stream(stream), a);
     NERF_CHECK_LAUNCH("sample_fine");
     return NERF_OK;
+}
+
+extern "C" int nerf_sample_fine(const float* d_rays, int64_t ray_stride, const float* d_z, const float* d_weights,
+                                int64_t n_rays, int n_samples, int n_importance, int det, const float* d_t_imp,
+                                const float* d_u, uint64_t seed, uint64_t offset, const uint64_t* d_rng,
+                                float* d_z_fine, float* d_pts_fine, float* d_z_std, float* d_samples, void* stream) {
+    return nerf_sample_fine_rows(d_rays, ray_stride, d_z, d_weights, n_rays, n_samples, n_importance, det, d_t_imp,
+                                 d_u, seed, offset, d_rng, d_z_fine, d_pts_fine, d_z_std, d_samples, nullptr, nullptr,
+                                 nullptr, nullptr, stream);
 }

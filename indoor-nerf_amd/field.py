@@ -165,7 +165,7 @@ class FieldFn(torch.autograd.Function):
     """Fused run_network: pts [P,3], viewdirs [R,3] (P = R*S) -> raw [P,4] ([P,7] with normals)."""
 
     @staticmethod
-    def forward(ctx, pts, viewdirs, samples_per_ray, embedder, net, netchunk, *params):
+    def forward(ctx, pts, viewdirs, samples_per_ray, embedder, net, netchunk, reuse, *params):
         if pts.requires_grad or viewdirs.requires_grad:
             raise NotImplementedError("run_network: gradients w.r.t. positions/directions are not implemented")
         n_tab = embedder.n_levels
@@ -175,7 +175,20 @@ class FieldFn(torch.autograd.Function):
         P = pts.shape[0]
         feat = torch.empty(n_tab, P, 2, device=pts.device, dtype=torch.float32)
         keep = torch.empty(P, device=pts.device, dtype=torch.bool)
-        embedder.encode_into(pts, feat, 2, 2 * P, keep)
+        # coarse-feature reuse (render.CoarseReuse): plain fp32 tables with a binned backward
+        plain = not embedder.quantization_active() and embedder.binned_backward()
+        ctx.reuse = None
+        if reuse is not None and plain and reuse.matches(embedder, tables, P):
+            # fine pass: gather the importance samples only, copy the coarse points' features
+            embedder.encode_rows(reuse.imp_pts, reuse.imp_rows, feat, 2, 2 * P, keep,
+                                 copy=(reuse.feat, reuse.keep, reuse.coarse_rows))
+            reuse.state = "used"
+            ctx.reuse = ("fine", reuse)
+        else:
+            embedder.encode_into(pts, feat, 2, 2 * P, keep)
+            if reuse is not None and plain and reuse.state == "armed" and P == reuse.R * reuse.S:
+                reuse.record(feat, keep, pts, embedder, tables)
+                ctx.reuse = ("coarse", reuse)
         raw = torch.empty(P, 4, device=pts.device, dtype=torch.float32)
         o16 = torch.empty(P, 16, device=pts.device, dtype=torch.float32) if head else None
         # with the normals head, run_network's mask lands on n_z, not sigma (run_nerf.py:66)
@@ -206,7 +219,7 @@ class FieldFn(torch.autograd.Function):
         g = g_raw.contiguous()
         head_grads, dgeo = (None,) * ctx.n_head, None
         if head:
-            g, dgeo = _head_backward(o16, keep, head, g, ctx.needs_input_grad[6 + n_tab + 5:])
+            g, dgeo = _head_backward(o16, keep, head, g, ctx.needs_input_grad[7 + n_tab + 5:])
         need_tab = any(t.requires_grad for t in tables) and not ctx.zero_tab_grad
         need_w = any(w.requires_grad for w in weights)
         if need_w or need_tab:
@@ -216,7 +229,7 @@ class FieldFn(torch.autograd.Function):
                 _pending_field(pts.device).add(job)   # launched with the pass's other FieldFn backwards
             else:
                 _run_field_jobs([job])
-        return (None,) * (6 + n_tab + len(weights)) + tuple(head_grads)
+        return (None,) * (7 + n_tab + len(weights)) + tuple(head_grads)
 
 
 class _FieldJob:
@@ -226,6 +239,7 @@ class _FieldJob:
         self.pts, self.viewdirs, self.feat, self.keep, self.head = pts, viewdirs, feat, keep, head
         self.w0q, self.arec, self.weights, self.tables, self.g, self.dgeo = w0q, arec, weights, tables, g, dgeo
         self.spr, self.meta, self.need_w, self.need_tab = ctx.spr, ctx.embedder._meta, need_w, need_tab
+        self.reuse = ctx.reuse     # (role, render.CoarseReuse) or None
         self.stream = torch.cuda.current_stream()
 
     def mlp_job(self):
@@ -242,6 +256,8 @@ class _FieldJob:
         j.dfeat = _lib.ptr(self.dfeat, "dfeat", allow_none=True)
         j.dgeo = _lib.ptr(self.dgeo, "dgeo", allow_none=True)
         j.act_qrec = _lib.ptr(self.arec, "act_record", allow_none=True)
+        if self.need_tab and self.reuse is not None and self.reuse[0] == "fine":
+            j.dfeat_rows = _lib.ptr(self.reuse[1].perm, "perm", torch.int32)   # importance-first d feat
         return j
 
 
@@ -290,16 +306,42 @@ def _run_field_jobs(jobs):
     if tab_jobs or tv_jobs:
         dev = (tab_jobs[0].pts if tab_jobs else tv_jobs[0].g).device
         pb = pending_bins(dev)
-        pb.reserve(sum(bin_chunks(j.pts.shape[0]) for j in tab_jobs) + sum(j.n_chunks for j in tv_jobs))
+        bins = [b for j in tab_jobs for b in _bin_items(j, tab_jobs)]
+        pb.reserve(sum(bin_chunks(b["n"]) for b in bins) + sum(j.n_chunks for j in tv_jobs))
         for j in tv_jobs:
             pb.add_tv(j, queue=False)
-        for j in tab_jobs:
-            P = j.pts.shape[0]
-            hash_encode_bwd(j.pts, j.meta, j.dfeat, 2, 2 * P, accumulate_grad_buffers(j.tables), defer=True,
-                            queue=False)
+        for b in bins:
+            j = b.pop("job")
+            hash_encode_bwd(b.pop("xyz"), j.meta, b.pop("dfeat"), 2, b.pop("sl"), accumulate_grad_buffers(j.tables),
+                            defer=True, queue=False, **b)
         pb.flush()
     for j in jobs:
         j.dfeat = None
+
+
+def _bin_items(j, jobs):
+    """The bin launches of one FieldFn backward (hash_encode_bwd keyword sets). With the coarse-feature
+    reuse (render.CoarseReuse) the fine job bins its importance samples only (row map imp_rows), and
+    the fine d feat of the coarse points' rows is added to the coarse job's own (dfeat2 at coarse_rows):
+    each point shared by the two passes is binned once with the sum of both gradients. Without the
+    coarse job in this batch (its output was not differentiated), the fine job bins the coarse points
+    itself with the fine d feat alone."""
+    P = j.pts.shape[0]
+    plain = dict(job=j, xyz=j.pts, dfeat=j.dfeat, sl=2 * P, n=P)
+    if j.reuse is None or not j.reuse[1].used:
+        return [plain]
+    role, plan = j.reuse
+    partner = next((k for k in jobs if k is not j and k.reuse is not None and k.reuse[1] is plan), None)
+    n_imp = plan.R * plan.N    # the fine d feat is in importance-first order: [importance | coarse points]
+    if role == "coarse":
+        if partner is None:
+            return [plain]
+        return [dict(plain, dfeat2=partner.dfeat, dfeat2_row0=n_imp, sl2=2 * partner.pts.shape[0])]
+    out = [dict(plain, xyz=plan.imp_pts, n=n_imp)]
+    if partner is None:
+        Pc = plan.R * plan.S
+        out.append(dict(job=j, xyz=plan.pts, dfeat=None, sl=2 * Pc, n=Pc, dfeat2=j.dfeat, dfeat2_row0=n_imp, sl2=2 * P))
+    return out
 
 
 class _PendingField:
@@ -438,7 +480,8 @@ def run_network(inputs, viewdirs, fn, embed_fn, embeddirs_fn, netchunk=1024 * 64
         if embed_fn.training:
             embed_fn.current_step += 1
         R, S = inputs.shape[0], inputs.shape[1]
-        raw = FieldFn.apply(inputs.reshape(-1, 3), viewdirs, S, embed_fn, fn, netchunk,
+        reuse = getattr(inputs, "_nerf_reuse", None)     # render.CoarseReuse of this render_rays call
+        raw = FieldFn.apply(inputs.reshape(-1, 3), viewdirs, S, embed_fn, fn, netchunk, reuse,
                             *embed_fn.tables(), *fn.field_params())
         return raw.reshape(R, S, fn.raw_channels)
     inputs_flat = torch.reshape(inputs, [-1, inputs.shape[-1]])

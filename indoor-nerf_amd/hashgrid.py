@@ -170,7 +170,20 @@ class _PendingBins:
         cur = torch.cuda.current_stream()
         if cur != self.stream:
             cur.wait_stream(self.stream)
+        self.last = (self.tag, self.used, self.cap)
         self.used, self.tag, self.grads = 0, None, None
+
+    def last_entry_count(self):
+        """Entries the bins of the last owner pass's workspace emitted (nerf_hash_bwd_entry_count;
+        a host sync — measurement only, e.g. bench.py's pricing of the hash backward), or None."""
+        if getattr(self, "last", None) is None or self.ws is None:
+            return None
+        (L, log2_T, _, det), used, cap = self.last
+        out = torch.zeros(1, dtype=torch.int64, device=self.ws.device)
+        _lib.call("nerf_hash_bwd_entry_count", L, log2_T, used, cap, det,
+                  _lib.ptr(self.ws, "workspace", dtype=torch.uint8), self.ws.numel(),
+                  _lib.ptr(out, "count", dtype=torch.int64), _lib.stream())
+        return int(out.item())
 
     def reserve(self, n_chunks):
         """Size the next workspace for n_chunks chunks, so that a batch whose total is known up front
@@ -204,12 +217,22 @@ class _PendingBins:
         self.used += n_ch
         return base, det
 
-    def add(self, xyz, meta, dfeat, sp, sl, grad_tables, queue=True):
-        L, log2_T, P = len(grad_tables), meta["log2_T"], xyz.shape[0]
+    def add(self, xyz, meta, dfeat, sp, sl, grad_tables, queue=True, n=None, rows=None, dfeat2=None, rows2=None,
+            sp2=2, sl2=0, dfeat2_row0=0):
+        """Bin n points (default: every row of xyz). rows / dfeat2 / rows2: the row maps of
+        nerf_hash_encode_bwd_bin_rows (coarse-feature reuse); dfeat2_row0: dfeat2's rows start at that
+        row of the tensor."""
+        d2 = _lib.ptr(dfeat2, "grad_feat2", allow_none=True)
+        if d2 is not None:
+            d2 = _lib.c_vp(d2.value + 4 * sp2 * int(dfeat2_row0))
+        L, log2_T = len(grad_tables), meta["log2_T"]
+        P = xyz.shape[0] if n is None else n
         base, det = self._slot(L, log2_T, grad_tables, bin_chunks(P), xyz.device, queue)
-        _lib.call("nerf_hash_encode_bwd_bin", _lib.ptr(xyz, "xyz"), P, meta["bmin"], meta["bmax"], meta["res"], L,
-                  log2_T, _lib.ptr(dfeat, "grad_feat"), sp, sl, base, self.cap, det,
-                  _lib.ptr(self.ws, "workspace", dtype=torch.uint8), self.ws.numel(), _lib.stream())
+        _lib.call("nerf_hash_encode_bwd_bin_rows", _lib.ptr(xyz, "xyz"), _lib.ptr(rows, "rows", torch.int32, True), P,
+                  meta["bmin"], meta["bmax"], meta["res"], L, log2_T, _lib.ptr(dfeat, "grad_feat", allow_none=True), sp,
+                  sl, d2, _lib.ptr(rows2, "rows2", torch.int32, True), sp2,
+                  sl2, base, self.cap, det, _lib.ptr(self.ws, "workspace", dtype=torch.uint8), self.ws.numel(),
+                  _lib.stream())
 
     def add_tv(self, job, queue=True):
         """Bin a TV backward (losses.TVBinJob) into the open workspace: its gradient is summed by the
@@ -235,18 +258,22 @@ def pending_bins(device):
     return _PENDING.setdefault(str(device), _PendingBins())
 
 
-def hash_encode_bwd(xyz, meta, dfeat, sp, sl, grad_tables, defer=None, queue=True):
+def hash_encode_bwd(xyz, meta, dfeat, sp, sl, grad_tables, defer=None, queue=True, **rows):
     """Scatter-add d feat into the gradient tables (hash_encoding.py:82-107 autograd; csrc/hashgrid.hip).
     defer (default: inside an autograd backward pass) bins now and leaves the owner pass to the end
     of the pass (_PendingBins), shared with the other hash backwards of the pass; queue=False leaves
-    the owner pass to the caller (pending_bins(device).flush())."""
-    L, log2_T, P = len(grad_tables), meta["log2_T"], xyz.shape[0]
+    the owner pass to the caller (pending_bins(device).flush()). rows: n / rows / dfeat2 / rows2 / sl2
+    of _PendingBins.add (binned path only)."""
+    L, log2_T = len(grad_tables), meta["log2_T"]
+    P = xyz.shape[0] if rows.get("n") is None else rows["n"]
     if defer is None:
         defer = torch._C._current_graph_task_id() != -1
     det = int(_DET["on"])
     if defer and P > 0 and int(_lib.load().nerf_hash_encode_bwd_workspace_bytes(L, log2_T, P, det)) > 0:
-        pending_bins(xyz.device).add(xyz, meta, dfeat, sp, sl, grad_tables, queue=queue)
+        pending_bins(xyz.device).add(xyz, meta, dfeat, sp, sl, grad_tables, queue=queue, **rows)
         return
+    if any(rows.get(k) is not None for k in ("rows", "dfeat2")):
+        raise NotImplementedError("hash_encode_bwd: row maps need the binned path (log2_T <= 19, a deferred pass)")
     materialize_zero(grad_tables)
     ws, nbytes = bwd_workspace(len(grad_tables), meta["log2_T"], xyz.shape[0], xyz.device)
     _lib.call("nerf_hash_encode_bwd_ws", _lib.ptr(xyz, "xyz"), xyz.shape[0], meta["bmin"], meta["bmax"],
@@ -367,6 +394,27 @@ class HashEmbedder(nn.Module):
         _lib.call("nerf_hash_encode_fwd_q", _lib.ptr(xyz, "xyz"), P, meta["bmin"], meta["bmax"], meta["res"],
                   self.n_levels, meta["log2_T"], _lib.ptr_array(self.tables()), _lib.ptr(rec, "records", allow_none=True),
                   _lib.ptr(feat, "feat"), sp, sl, _lib.ptr(keep, "keep", dtype=torch.bool), _lib.stream())
+
+    def binned_backward(self):
+        """The binned backward exists for these tables (log2_T <= 19, plain and deterministic)."""
+        lib = _lib.load()
+        return all(int(lib.nerf_hash_encode_bwd_workspace_bytes(self.n_levels, self.log2_hashmap_size, 1, d)) > 0
+                   for d in (0, 1))
+
+    def encode_rows(self, xyz, rows, feat, sp, sl, keep, copy=None):
+        """Forward gather of the points of xyz [n, 3] into rows `rows` (int32) of feat / keep (plain
+        fp32 tables; render.CoarseReuse's importance samples); copy = (src [L, m, 2], src_keep [m],
+        src_rows [m]): in the same launch, the level-major features of m more points are copied to rows
+        src_rows (the coarse pass's features into the fine rows)."""
+        meta = self._meta
+        src, src_keep, src_rows = copy if copy is not None else (None, None, None)
+        _lib.call("nerf_hash_encode_fwd_rows", _lib.ptr(xyz.reshape(-1, 3), "xyz"), _lib.ptr(rows, "rows", torch.int32),
+                  rows.numel(), meta["bmin"], meta["bmax"], meta["res"], self.n_levels, meta["log2_T"],
+                  _lib.ptr_array(self.tables()), None, _lib.ptr(feat, "feat"), sp, sl,
+                  _lib.ptr(keep, "keep", dtype=torch.bool), _lib.ptr(src, "copy_feat", allow_none=True),
+                  _lib.ptr(src_keep, "copy_keep", dtype=torch.bool, allow_none=True),
+                  _lib.ptr(src_rows, "copy_rows", torch.int32, True), 0 if src_rows is None else src_rows.numel(),
+                  _lib.stream())
 
     def encode(self, x, layout="point"):
         return HashEncodeFn.apply(x, self, layout, *self.tables())

@@ -183,6 +183,62 @@ def raw2outputs(raw, z_vals, rays_d, raw_noise_std=0, white_bkgd=False, pytest=F
     return outs[:6]
 
 
+# ---------------------------------------------------------------- coarse-feature reuse
+
+_REUSE = {"on": True}
+
+
+def set_coarse_reuse(enabled=True):
+    """the fine pass of render_rays encodes only its importance samples and takes
+    the hash features of its coarse points from the coarse pass (on by default; off = re-encode all
+    of them, as the reference does). Features are bit-identical either way."""
+    _REUSE["on"] = bool(enabled)
+
+
+def coarse_reuse():
+    return _REUSE["on"]
+
+
+class CoarseReuse:
+    """Hand-over of one render_rays call's coarse hash encoding to its fine pass.
+
+    The reference merges the coarse depths into the fine ones (run_nerf.py:512-516: torch.sort of
+    cat([z_vals, z_samples]), then rays_o + rays_d * z) and queries both networks through ONE
+    embedder (run_nerf.py:225,275), so 64 of a ray's 192 fine points are the coarse points bit for
+    bit and, the tables being unchanged inside an iteration, so are their 16-level features.
+    render_rays attaches this object to the coarse and then the fine point tensors
+    (`pts._nerf_reuse`); field.FieldFn (the fused run_network) records the coarse features in it and
+    the fine pass gathers only its importance samples and, in the same launch, copies the coarse
+    features into their fine rows (nerf_hash_encode_fwd_rows). The fine MLP backward writes its d feat
+    in importance-first order (perm), so the fine bin reads the importance samples' rows contiguously
+    and the coarse bin adds the coarse points' fine d feat to their coarse d feat
+    (nerf_hash_encode_bwd_bin_rows): each shared point is binned once. Any other network_query_fn
+    ignores the attribute."""
+
+    def __init__(self, R, S, N):
+        self.R, self.S, self.N = R, S, N
+        self.state = "armed"          # -> "recorded" (coarse FieldFn) -> "rows" (sample_fine) -> "used"
+        self.feat = self.keep = self.pts = self.embedder = self.versions = None
+        self.coarse_rows = self.imp_rows = self.imp_pts = self.perm = None
+
+    def record(self, feat, keep, pts, embedder, tables):
+        self.feat, self.keep, self.pts, self.embedder = feat, keep, pts, embedder
+        self.versions = [t._version for t in tables]
+        self.state = "recorded"
+
+    def matches(self, embedder, tables, P):
+        return (self.state == "rows" and embedder is self.embedder and P == self.R * (self.S + self.N)
+                and [t._version for t in tables] == self.versions)
+
+    @property
+    def used(self):
+        return self.state == "used"
+
+    def release_forward(self):
+        """After the fine forward: only the row maps and the coarse points stay (the backward's)."""
+        self.feat = self.keep = self.embedder = None
+
+
 # ---------------------------------------------------------------- sampling
 
 def sample_pdf(bins, weights, N_samples, det=False, pytest=False):
@@ -224,7 +280,14 @@ def render_rays(ray_batch, network_fn, network_query_fn, N_samples, embed_fn=Non
               _lib.ptr(pts, "pts"), _lib.ptr(rays_d, "rays_d"), _lib.ptr(viewdirs, "viewdirs", allow_none=True),
               _lib.stream())
 
+    reuse = CoarseReuse(R, N_samples, N_importance) if (N_importance > 0 and _REUSE["on"] and R > 0) else None
+    if reuse is not None:
+        pts._nerf_reuse = reuse       # the fused run_network records the coarse encoding in it
     raw = network_query_fn(pts, viewdirs, network_fn)
+    if reuse is not None:
+        del pts._nerf_reuse
+        if reuse.state != "recorded" or R * (N_samples + N_importance) > 2 ** 31 - 1:
+            reuse = None
     outs = raw2outputs(raw, z, rays_d, raw_noise_std, white_bkgd, pytest=pytest, predict_normals=predict_normals)
     rgb_map, disp_map, acc_map, weights, depth_map, sparsity_loss = outs[:6]
     normal_map = outs[6] if predict_normals else None
@@ -241,14 +304,27 @@ def render_rays(ray_batch, network_fn, network_query_fn, N_samples, embed_fn=Non
         t_imp = _linspace(N_importance, dev) if det else None
         u_imp = _pytest_uniforms((R, N_importance), dev) if (pytest and not det) else None
         seed, off, rng = (0, 0, None) if (det or u_imp is not None) else _rng()
-        _lib.call("nerf_sample_fine", _lib.ptr(rays, "ray_batch"), C, _lib.ptr(z, "z"),
+        i32 = dict(device=dev, dtype=torch.int32)
+        if reuse is not None:
+            reuse.coarse_rows, reuse.imp_rows = torch.empty(R, N_samples, **i32), torch.empty(R, N_importance, **i32)
+            reuse.imp_pts, reuse.perm = torch.empty(R, N_importance, 3, **f), torch.empty(R * M, **i32)
+            reuse.state = "rows"
+        _lib.call("nerf_sample_fine_rows", _lib.ptr(rays, "ray_batch"), C, _lib.ptr(z, "z"),
                   _lib.ptr(weights.detach().contiguous(), "weights"), R, N_samples, N_importance, int(det),
                   _lib.ptr(t_imp, "t", allow_none=True), _lib.ptr(u_imp, "u", allow_none=True), seed, off, rng,
                   _lib.ptr(z_fine, "z_fine"), _lib.ptr(pts_fine, "pts_fine"), _lib.ptr(z_std, "z_std"), None,
-                  _lib.stream())
+                  _lib.ptr(None if reuse is None else reuse.coarse_rows, "coarse_rows", torch.int32, True),
+                  _lib.ptr(None if reuse is None else reuse.imp_rows, "imp_rows", torch.int32, True),
+                  _lib.ptr(None if reuse is None else reuse.imp_pts, "imp_pts", allow_none=True),
+                  _lib.ptr(None if reuse is None else reuse.perm, "perm", torch.int32, True), _lib.stream())
         z, pts = z_fine, pts_fine
         run_fn = network_fn if network_fine is None else network_fine
+        if reuse is not None:
+            pts._nerf_reuse = reuse
         raw = network_query_fn(pts, viewdirs, run_fn)
+        if reuse is not None:
+            del pts._nerf_reuse
+            reuse.release_forward()
         outs = raw2outputs(raw, z, rays_d, raw_noise_std, white_bkgd, pytest=pytest, predict_normals=predict_normals)
         rgb_map, disp_map, acc_map, weights, depth_map, sparsity_loss = outs[:6]
         normal_map = outs[6] if predict_normals else None

@@ -22,7 +22,7 @@ def test_library_exports_every_declared_symbol(nerf):
     for name in declared:
         assert hasattr(lib, name), f"libnerfhip.so does not export {name}"
     assert sorted(L.exported_symbols()) == declared, "ctypes signature table out of sync with the header"
-    assert lib.nerf_abi_version() == 3   # 3: binned TV backward, nerf_tv_fwd vertex rows
+    assert lib.nerf_abi_version() == 4   # 4: row-mapped hash fwd / bin, feature scatter, fine-row maps
 
 
 def test_error_path_reports_message(nerf):
@@ -53,7 +53,11 @@ def test_error_path_reports_message(nerf):
         L.call("nerf_hash_encode_bwd_owner", 16, 19, 4, 4, None, 1, fake, need, None)
     with pytest.raises(RuntimeError, match="deterministic"):
         L.call("nerf_hash_encode_bwd_ws", fake, 10, L.host_f32([0] * 3), L.host_f32([1] * 3), L.host_f32([16] * 16),
-               16, 19, fake, 32, 2, None, 1, None, 0, None)
+               16, 19, fake, 32, 2, (ctypes.c_void_p * 16)(*[1 << 20] * 16), 1, None, 0, None)
+    # empty batches still validate the tables and host arrays
+    with pytest.raises(RuntimeError, match="grad table 3 is null"):
+        L.call("nerf_hash_encode_bwd_ws", None, 0, L.host_f32([0] * 3), L.host_f32([1] * 3), L.host_f32([16] * 16),
+               16, 19, None, 32, 2, (ctypes.c_void_p * 16)(*([1 << 20] * 3 + [None] + [1 << 20] * 12)), 0, None, 0, None)
     with pytest.raises(RuntimeError, match="1..2"):
         L.call("nerf_mlp_bwd_batch", (L.MlpBwdJob * 3)(), 3, None, 0, None)
 

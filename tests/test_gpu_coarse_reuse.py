@@ -48,3 +48,128 @@ def test_fine_set_contains_coarse_points_bitwise(nerf, gpu):
     torch.cuda.synchronize()
     for a, b in zip(f_coarse, f_fine):   # (features [P, 32], keep mask)
         assert torch.equal(a, b)
+
+
+# ---- the reuse itself (render.CoarseReuse): the fine pass gathers its importance samples only and
+# copies the coarse features into the coarse points' fine rows; the backward bins each shared point once
+
+def _scene(nerf, gpu, R=512):
+    lo, hi = blender_bbox()
+    args = nerf.make_args(bounding_box=(torch.from_numpy(lo), torch.from_numpy(hi)), finest_res=1024, N_samples=64,
+                          N_importance=128, white_bkgd=True)
+    torch.manual_seed(0)
+    kw_train, _, _, _, _ = nerf.create_nerf(args, device=gpu)
+    with torch.no_grad():
+        g = torch.Generator().manual_seed(7)
+        for e in kw_train["embed_fn"].embeddings:
+            e.weight.copy_((torch.rand(e.weight.shape, generator=g) * 2 - 1) * 0.05)
+    kw = {k: v for k, v in kw_train.items() if k not in ("ndc", "use_viewdirs", "near", "far")}
+    ro, rd = synthetic_rays(R, seed=9)
+    ro, rd = torch.from_numpy(ro).to(gpu), torch.from_numpy(rd).to(gpu)
+    vd = rd / torch.norm(rd, dim=-1, keepdim=True)
+    rays = torch.cat([ro, rd, torch.full((R, 1), 2.0, device=gpu), torch.full((R, 1), 6.0, device=gpu), vd], -1)
+    target = torch.rand(R, 3, device=gpu, generator=torch.Generator(device=gpu).manual_seed(3))
+    return kw, rays, target
+
+
+def _params(kw):
+    return (list(kw["embed_fn"].parameters()) + list(kw["network_fn"].parameters())
+            + list(kw["network_fine"].parameters()))
+
+
+def _train_pass(nerf, kw, rays, target, reuse, parts):
+    nerf.set_coarse_reuse(reuse)
+    try:
+        for p in _params(kw):
+            p.grad = None
+        out = nerf.render_rays(rays, **kw, pytest=True)
+        loss = sum(((out[k] - target) ** 2).mean() for k in parts)
+        loss.backward()
+        torch.cuda.synchronize()
+        outs = {k: v.detach().clone() for k, v in out.items() if torch.is_tensor(v)}
+        grads = [None if p.grad is None else p.grad.detach().clone() for p in _params(kw)]
+        return outs, grads
+    finally:
+        nerf.set_coarse_reuse(True)
+
+
+@pytest.mark.parametrize("parts", [("rgb_map", "rgb0"), ("rgb_map",), ("rgb0",)],
+                         ids=["both_passes", "fine_only", "coarse_only"])
+def test_coarse_reuse_matches_reencoding(nerf, gpu, parts):
+    """Reuse on vs off on the same draws (deterministic mode, so the MLP weight gradients are summed in
+    a fixed order): every render output bit-identical; MLP gradients bit-identical; table gradients
+    within 1e-5 of the level's largest |gradient| (the shared points' fine and coarse d feat are summed
+    in fp32 before the bin instead of binned as two entries). fine_only: the coarse pass is not
+    differentiated, so the fine job bins the coarse points itself; coarse_only: no fine backward."""
+    kw, rays, target = _scene(nerf, gpu)
+    nerf.set_deterministic(True)
+    try:
+        out_a, g_a = _train_pass(nerf, kw, rays, target, True, parts)
+        out_b, g_b = _train_pass(nerf, kw, rays, target, False, parts)
+    finally:
+        nerf.set_deterministic(False)
+    assert out_a.keys() == out_b.keys()
+    for k in out_a:
+        assert torch.equal(out_a[k], out_b[k]), k
+    n_tab = kw["embed_fn"].n_levels
+    for i, (a, b) in enumerate(zip(g_a, g_b)):
+        assert (a is None) == (b is None), i
+        if a is None:
+            continue
+        if i < n_tab:
+            scale = float(b.abs().max())
+            assert float((a - b).abs().max()) <= 1e-5 * scale + 1e-30, f"table {i}"
+            assert scale > 0, f"table {i}: no gradient"
+        else:
+            assert torch.equal(a, b), f"mlp param {i - n_tab}"
+
+
+def test_coarse_reuse_is_taken(nerf, gpu):
+    """The training forward takes the reuse path: the fine FieldFn node carries a used plan, and the
+    fine hash forward gathers R*N points (nerf_hash_encode_fwd_rows), not R*(S+N)."""
+    from indoor_nerf_amd import _lib
+    kw, rays, target = _scene(nerf, gpu, R=256)
+    _lib.set_timing(True)
+    try:
+        out = nerf.render_rays(rays, **kw, pytest=True)
+        torch.cuda.synchronize()
+        names = [n for n, _, _ in _lib.timing_records()]
+    finally:
+        _lib.set_timing(False)
+    assert names.count("nerf_hash_encode_fwd_q") == 1 and names.count("nerf_hash_encode_fwd_rows") == 1
+    assert out["pts"].shape == (256, 192, 3)
+
+
+@pytest.mark.parametrize("sorted_coarse", [True, False])
+def test_fine_row_maps_partition_each_ray(nerf, gpu, sorted_coarse):
+    """nerf_sample_fine_rows: per ray, the coarse rows and the importance rows are disjoint and cover
+    the ray's S+N fine rows; z_fine at a coarse row is that coarse depth; importance rows ascend (the
+    bitonic merge) — also through the rank-sort path taken for unsorted coarse depths."""
+    from indoor_nerf_amd import _lib
+    R, S, N = 300, 64, 128
+    M = S + N
+    g = torch.Generator(device=gpu).manual_seed(5)
+    z = 2.0 + 4.0 * torch.rand(R, S, device=gpu, generator=g)
+    if sorted_coarse:
+        z = torch.sort(z, -1).values
+    w = torch.rand(R, S, device=gpu, generator=g)
+    rays = torch.rand(R, 11, device=gpu, generator=g)
+    zf, pf = torch.empty(R, M, device=gpu), torch.empty(R, M, 3, device=gpu)
+    cr = torch.empty(R, S, device=gpu, dtype=torch.int32)
+    ir = torch.empty(R, N, device=gpu, dtype=torch.int32)
+    ip = torch.empty(R, N, 3, device=gpu)
+    perm = torch.empty(R * M, device=gpu, dtype=torch.int32)
+    _lib.call("nerf_sample_fine_rows", _lib.ptr(rays), 11, _lib.ptr(z), _lib.ptr(w), R, S, N, 0, None, None, 11, 0,
+              None, _lib.ptr(zf), _lib.ptr(pf), None, None, _lib.ptr(cr, "cr", torch.int32),
+              _lib.ptr(ir, "ir", torch.int32), _lib.ptr(ip), _lib.ptr(perm, "perm", torch.int32), _lib.stream())
+    torch.cuda.synchronize()
+    base = (torch.arange(R, device=gpu) * M)[:, None]
+    allr = torch.sort(torch.cat([cr, ir], 1).long() - base, 1).values
+    assert torch.equal(allr, torch.arange(M, device=gpu).expand(R, M))
+    assert torch.equal(zf.reshape(-1)[cr.long().reshape(-1)].reshape(R, S), z)
+    assert torch.equal(pf.reshape(-1, 3)[ir.long().reshape(-1)], ip.reshape(-1, 3))   # same bits as pts_fine
+    # perm: fine row -> importance-first position (importance k of ray r: r*N + k; coarse i: R*N + r*S + i)
+    assert torch.equal(perm[ir.long().reshape(-1)].long(), torch.arange(R * N, device=gpu))
+    assert torch.equal(perm[cr.long().reshape(-1)].long(), R * N + torch.arange(R * S, device=gpu))
+    if sorted_coarse:
+        assert (ir[:, 1:] > ir[:, :-1]).all().item()
