@@ -205,6 +205,9 @@ def parse():
     ap.add_argument("--zero", type=int, default=1,
                     help="N>1: shard the optimizer (reduce-scatter -> RAdam on 1/N -> all-gather, dist.ShardedOptimizer); "
                          "0 = all-reduce + replicated RAdam")
+    ap.add_argument("--overlap", type=int, default=1,
+                    help="N>1 with --zero 1: reduce-scatter the first gradient bucket while the owner pass sums the "
+                         "second (dist.ShardedOptimizer(overlap=True)); 0 = one reduce-scatter after the backward")
     ap.add_argument("--deterministic", type=int, default=0,
                     help="1: bitwise-reproducible backward (nerf.set_deterministic: fixed-point hash owner pass, "
                          "ordered MLP weight-gradient reduction)")
@@ -426,8 +429,12 @@ def main():
     params = grad_vars + list(kw["embed_fn"].parameters())
     nerf.broadcast_params(params)
     zero = world > 1 and a.zero and a.mode == "train"
-    # defer_tables: no memset of the 64 MiB of table gradients; the owner pass overwrites them
-    arena = nerf.GradArena(params, pad_to=world * 64 if zero else 1, defer_tables=True)
+    # defer_tables: no memset of the 64 MiB of table gradients; the owner pass overwrites them.
+    # ZeRO-1 with --overlap: two gradient buckets (MLP + table levels 0..7 | levels 8..15), the first
+    # reduce-scattered while the owner pass sums the second (dist.ShardedOptimizer)
+    tabs = kw["embed_fn"].tables()
+    split = [tabs[len(tabs) // 2]] if (zero and a.overlap) else []
+    arena = nerf.GradArena(params, pad_to=world * 64 if zero else 1, defer_tables=True, bucket_starts=split)
     rays = (torch.from_numpy(ro).to(dev), torch.from_numpy(rd).to(dev))
     if strong:
         target = nerf.shard(torch.rand(a.rays, 3, device=dev, generator=torch.Generator(device=dev).manual_seed(0)),
@@ -437,7 +444,7 @@ def main():
     tv_gen = torch.Generator().manual_seed(7)       # same TV cuboids on every rank
     post = None
     if zero:
-        sharded = nerf.ShardedOptimizer(opt, arena)
+        sharded = nerf.ShardedOptimizer(opt, arena, overlap=bool(a.overlap))
         hook, post = sharded.reduce_grads, sharded.gather_params
     else:
         hook = (lambda: arena.allreduce_mean()) if world > 1 else None
@@ -570,7 +577,7 @@ def main():
         "config": {"workload": wl["desc"].format(R=R) + ("" if a.mode == "train" else " [render only]"),
                    "name": a.workload, "rays_per_gpu": R, "global_batch": R * world,
                    "samples": f"{wl['args']['N_samples']}+{wl['args']['N_importance']}",
-                   "parallelism": f"dp{world}" + ("-zero1" if zero else "")},
+                   "parallelism": f"dp{world}" + ("-zero1" if zero else "") + ("-overlap" if zero and a.overlap else "")},
         "hip_graph": bool(gstep is not None and gstep.captures > 0),
         "coarse_reuse": reused,
         "loss": round(float(loss), 6),

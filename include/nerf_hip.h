@@ -159,6 +159,12 @@ int nerf_hash_encode_bwd_bin_rows(const float* d_xyz, const int32_t* d_rows, int
 int nerf_hash_encode_bwd_owner(int n_levels, int log2_T, int64_t n_chunks, int64_t chunk_capacity,
                                float* const* d_dtables, int deterministic, void* d_workspace,
                                size_t workspace_bytes, void* stream);
+/* The owner pass of levels [level_begin, level_end) only (the same workspace and tables): a data-
+ * parallel step launches the levels of each gradient bucket separately and starts the bucket's
+ * reduce-scatter as soon as its levels are summed (dist.ShardedOptimizer buckets). */
+int nerf_hash_encode_bwd_owner_range(int n_levels, int level_begin, int level_end, int log2_T, int64_t n_chunks,
+                                     int64_t chunk_capacity, float* const* d_dtables, int deterministic,
+                                     void* d_workspace, size_t workspace_bytes, void* stream);
 
 /* Entries the bin launches of chunks [0, n_chunks) of a workspace emitted (sum of their segment counts:
  * after the run merge, without zero entries), stored to d_count (device uint64). A measurement for the

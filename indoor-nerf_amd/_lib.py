@@ -98,6 +98,8 @@ SIGNATURES = {
     "nerf_hash_encode_bwd_bin_rows": [c_vp, c_vp, c_i64, c_f32p, c_f32p, c_f32p, c_int, c_int, c_vp, c_i64, c_i64,
                                       c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_int, c_vp, ctypes.c_size_t, c_vp],
     "nerf_hash_bwd_entry_count": [c_int, c_int, c_i64, c_i64, c_int, c_vp, ctypes.c_size_t, c_vp, c_vp],
+    "nerf_hash_encode_bwd_owner_range": [c_int, c_int, c_int, c_int, c_i64, c_i64, ctypes.POINTER(c_vp), c_int, c_vp,
+                                         ctypes.c_size_t, c_vp],
     "nerf_sh4_fwd": [c_vp, c_i64, c_vp, c_vp],
     "nerf_mlp_fwd": [c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, ctypes.POINTER(MlpWeights),
                      c_vp, c_vp, c_vp],

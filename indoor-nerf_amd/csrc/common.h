@@ -145,4 +145,81 @@ __device__ __forceinline__ double wave_sum_d(double v) {
     return v;
 }
 
+// ---- fp64 wave64 scans and reductions on DPP (VALU lane moves; no LDS crossbar round trips) ----
+// A double moves as its two dwords; lanes without a source (or in masked rows) keep `old`.
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ double dpp_d(double v, double old) {
+    const uint64_t u = __double_as_longlong(v), o = __double_as_longlong(old);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)o, (int)(uint32_t)u, CTRL, ROW_MASK, 0xF, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)(o >> 32), (int)(uint32_t)(u >> 32), CTRL,
+                                                              ROW_MASK, 0xF, false);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+__device__ __forceinline__ double readlane_d(double v, int l) {
+    const uint64_t u = __double_as_longlong(v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+// Sum over the wave, returned to every lane: quad, half-row and row mirrors, then the row_bcast 15 /
+// 31 carries leave the total in lane 63, read back as a uniform value. Fixed order (deterministic).
+__device__ __forceinline__ double wave_sum_dpp(double v) {
+    v += dpp_d<0xB1>(v, 0.0);        // quad_perm [1,0,3,2]
+    v += dpp_d<0x4E>(v, 0.0);        // quad_perm [2,3,0,1]
+    v += dpp_d<0x141>(v, 0.0);       // row_half_mirror: the other quad of the 8
+    v += dpp_d<0x140>(v, 0.0);       // row_mirror: the other 8 of the row
+    v += dpp_d<0x142, 0xA>(v, 0.0);  // row_bcast:15 into rows 1, 3
+    v += dpp_d<0x143, 0xC>(v, 0.0);  // row_bcast:31 into rows 2, 3
+    return readlane_d(v, 63);
+}
+
+// Inclusive prefix sum over lanes: row_shr 1, 2, 4, 8 inside each row, then the row_bcast carries.
+__device__ __forceinline__ double wave_incl_sum_dpp(double v) {
+    v += dpp_d<0x111>(v, 0.0);
+    v += dpp_d<0x112>(v, 0.0);
+    v += dpp_d<0x114>(v, 0.0);
+    v += dpp_d<0x118>(v, 0.0);
+    v += dpp_d<0x142, 0xA>(v, 0.0);
+    v += dpp_d<0x143, 0xC>(v, 0.0);
+    return v;
+}
+
+// Exclusive product scan over lanes (lane 0 gets 1): Hillis-Steele row_shr 1, 2, 4, 8 inside each
+// row, the row_bcast 15 / 31 carries across rows, then wave_shr:1.
+__device__ __forceinline__ double wave_excl_prod_dpp(double v) {
+    v *= dpp_d<0x111>(v, 1.0);
+    v *= dpp_d<0x112>(v, 1.0);
+    v *= dpp_d<0x114>(v, 1.0);
+    v *= dpp_d<0x118>(v, 1.0);
+    v *= dpp_d<0x142, 0xA>(v, 1.0);
+    v *= dpp_d<0x143, 0xC>(v, 1.0);
+    return dpp_d<0x138>(v, 1.0);     // wave_shr:1
+}
+
+// Exclusive suffix scan of affine maps f_b(U) = X_b + P_b U over lanes (lane b gets the composition
+// of lanes b+1 .. 63 applied to U = 0, i.e. its X; lane 63 gets 0): row_shl 1, 2, 4, 8 inside each
+// row (a missing source is the identity (0, 1)), the row totals (lane 16r) read back and composed
+// across rows, then wave_shl:1.
+__device__ __forceinline__ double wave_excl_suffix_affine_dpp(double X, double P, int lane) {
+#define NERF_AFFINE_STEP(CTRL)                             {                                                          const double Xn = dpp_d<CTRL>(X, 0.0);                 const double Pn = dpp_d<CTRL>(P, 1.0);                 X = X + P * Xn;                                        P = P * Pn;                                        }
+    NERF_AFFINE_STEP(0x101)
+    NERF_AFFINE_STEP(0x102)
+    NERF_AFFINE_STEP(0x104)
+    NERF_AFFINE_STEP(0x108)
+#undef NERF_AFFINE_STEP
+    // suffix over the rows after this lane's: S3 = id, S2 = C3, S1 = C2 o C3, S0 = C1 o S1
+    const double X1 = readlane_d(X, 16), P1 = readlane_d(P, 16);
+    const double X2 = readlane_d(X, 32), P2 = readlane_d(P, 32);
+    const double X3 = readlane_d(X, 48);
+    const double S2x = X3;
+    const double S1x = X2 + P2 * S2x;
+    const double S0x = X1 + P1 * S1x;
+    const int row = lane >> 4;
+    const double Sx = row == 0 ? S0x : row == 1 ? S1x : row == 2 ? S2x : 0.0;
+    X = X + P * Sx;
+    return dpp_d<0x130>(X, 0.0);     // wave_shl:1: lane b reads lane b + 1; lane 63 keeps 0
+}
+
 }  // namespace nerf

@@ -1,8 +1,9 @@
 // Volume compositing: raw2outputs (PocketNeRF/run_nerf.py:347-411) forward and backward.
 //
 // One wavefront per ray; lane L owns the K = ceil(S/64) consecutive samples [K*L, K*L+K). The
-// transmittance T_j = prod_{k<j}(1 - alpha_k + 1e-10) is a wave-level exclusive product scan
-// (6 shuffle steps) over the lanes' local products; the backward's suffix recurrence
+// transmittance T_j = prod_{k<j}(1 - alpha_k + 1e-10) is a wave-level exclusive product scan over
+// the lanes' local products (DPP lane moves: common.h wave_excl_prod_dpp); the backward's suffix
+// recurrence
 //   U_j = sum_{k>j} gw_k alpha_k prod_{j<m<k} t_m,   dL/dalpha_j = T_j (gw_j - U_j)
 // is a wave-level suffix scan of affine maps (X, P) -> X + P*U. Scans and ray sums run in fp64:
 // the reference's CPU cumprod/cumsum accumulate in double, and the cost here is negligible.
@@ -43,17 +44,6 @@ struct RayState {
     float w[K];        // weights
 };
 
-__device__ __forceinline__ double wave_excl_prod(double v, int lane) {
-    // inclusive multiplicative scan, then shift by one lane
-    double x = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const double y = __shfl_up(x, o, 64);
-        if (lane >= o) x *= y;
-    }
-    const double ex = __shfl_up(x, 1, 64);
-    return lane == 0 ? 1.0 : ex;
-}
 
 template <int K>
 __device__ __forceinline__ void ray_forward(const CompositeArgs& a, int64_t ray, int lane, RayState<K>& st,
@@ -95,7 +85,7 @@ __device__ __forceinline__ void ray_forward(const CompositeArgs& a, int64_t ray,
             st.n[q][0] = st.n[q][1] = st.n[q][2] = 0.f;
         }
     }
-    const double pre = wave_excl_prod(lprod, lane);
+    const double pre = wave_excl_prod_dpp(lprod);
 #pragma unroll
     for (int q = 0; q < K; ++q) {
         st.T[q] = pre * Tloc[q];
@@ -110,6 +100,7 @@ struct RaySums {
 template <int K>
 __device__ __forceinline__ RaySums ray_sums(const CompositeArgs& a, const RayState<K>& st, bool need_ent) {
     double r0 = 0, r1 = 0, r2 = 0, acc = 0, dn = 0, n0 = 0, n1 = 0, n2 = 0;
+    const bool normals = a.C >= 7;   // wave-uniform
 #pragma unroll
     for (int q = 0; q < K; ++q) {
         const double w = st.w[q];
@@ -123,11 +114,11 @@ __device__ __forceinline__ RaySums ray_sums(const CompositeArgs& a, const RaySta
         n2 += (double)(st.w[q] * st.n[q][2]);
     }
     RaySums s;
-    s.rgb[0] = (float)wave_sum_d(r0);
-    s.rgb[1] = (float)wave_sum_d(r1);
-    s.rgb[2] = (float)wave_sum_d(r2);
-    s.acc = (float)wave_sum_d(acc);
-    s.depth_num = (float)wave_sum_d(dn);
+    s.rgb[0] = (float)wave_sum_dpp(r0);
+    s.rgb[1] = (float)wave_sum_dpp(r1);
+    s.rgb[2] = (float)wave_sum_dpp(r2);
+    s.acc = (float)wave_sum_dpp(acc);
+    s.depth_num = (float)wave_sum_dpp(dn);
     s.depth = s.depth_num / s.acc;
     {
         const float m = (s.depth != s.depth) ? s.depth : fmaxf(1e-10f, s.depth);   // torch.max keeps NaN
@@ -146,14 +137,17 @@ __device__ __forceinline__ RaySums ray_sums(const CompositeArgs& a, const RaySta
             const float p = st.w[q] / s.Z;
             h += (double)(logf(fminf(fmaxf(p, eps), 1.0f - eps)) * p);
         }
-        h = wave_sum_d(h);
+        h = wave_sum_dpp(h);
         const float pq = s.q / s.Z;
         h += (double)(logf(fminf(fmaxf(pq, eps), 1.0f - eps)) * pq);
         s.ent = (float)(-h);
     }
-    s.nraw[0] = (float)wave_sum_d(n0);
-    s.nraw[1] = (float)wave_sum_d(n1);
-    s.nraw[2] = (float)wave_sum_d(n2);
+    s.nraw[0] = s.nraw[1] = s.nraw[2] = 0.f;
+    if (normals) {
+        s.nraw[0] = (float)wave_sum_dpp(n0);
+        s.nraw[1] = (float)wave_sum_dpp(n1);
+        s.nraw[2] = (float)wave_sum_dpp(n2);
+    }
     s.nnorm = sqrtf(s.nraw[0] * s.nraw[0] + s.nraw[1] * s.nraw[1] + s.nraw[2] * s.nraw[2]);
     s.nden = fmaxf(s.nnorm, 1e-12f);
     return s;
@@ -192,21 +186,6 @@ __global__ void __launch_bounds__(256) composite_fwd_kernel(CompositeArgs a) {
     }
 }
 
-// suffix scan of affine maps f_b(U) = X_b + P_b*U over lanes b, b+1, ..., 63 (exclusive: lane b gets
-// the composition of lanes b+1..63 applied to U = 0, i.e. its X).
-__device__ __forceinline__ double wave_excl_suffix_affine(double X, double P, int lane) {
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const double Xn = __shfl_down(X, o, 64);
-        const double Pn = __shfl_down(P, o, 64);
-        if (lane + o < 64) {   // compose self (earlier) with the map o lanes later
-            X = X + P * Xn;
-            P = P * Pn;
-        }
-    }
-    const double ex = __shfl_down(X, 1, 64);
-    return lane == 63 ? 0.0 : ex;
-}
 
 template <int K>
 __global__ void __launch_bounds__(256) composite_bwd_kernel(CompositeArgs a) {
@@ -265,7 +244,7 @@ __global__ void __launch_bounds__(256) composite_bwd_kernel(CompositeArgs a) {
             const float dp = -ge * (logf(cp) + p * mask / cp);
             dot += (double)(dp * st.w[q]);
         }
-        dot = wave_sum_d(dot);
+        dot = wave_sum_dpp(dot);
         const float pq = s.q / s.Z;
         const float cpq = fminf(fmaxf(pq, eps), 1.0f - eps);
         const float maskq = (pq >= eps && pq <= 1.0f - eps) ? 1.f : 0.f;
@@ -307,7 +286,7 @@ __global__ void __launch_bounds__(256) composite_bwd_kernel(CompositeArgs a) {
         X = (double)gw[q] * (double)st.alpha[q] + (double)st.t[q] * X;
         P = (double)st.t[q] * P;
     }
-    double U = wave_excl_suffix_affine(X, P, lane);   // U at this lane's last sample
+    double U = wave_excl_suffix_affine_dpp(X, P, lane);   // U at this lane's last sample
     float* out = a.graw;
 #pragma unroll
     for (int q = K - 1; q >= 0; --q) {

@@ -64,14 +64,18 @@ __device__ __forceinline__ void split2(float a, float b, uint32_t& p0, uint32_t&
     p2 = pk_bf16(sa, sb);
 }
 
-// ReLU as one integer op per element (a negative float is a negative int; +0/-0 -> +0): a float
-// max compiles to two v_max_f32 per element on MFMA results (a canonicalising max first).
+// ReLU as ONE integer op per element, v_max_i32(bits, 0): a negative float (and -0, and a negative
+// NaN) is a negative int and becomes +0, a positive one keeps its bits. A float max compiles to two
+// v_max_f32 per element on MFMA results (a canonicalising max first), the shift-and-mask form to two.
 __device__ __forceinline__ void relu16i(floatx16& v) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int i = __float_as_int(v[r]);
-        v[r] = __int_as_float(i & ~(i >> 31));
-    }
+    for (int r = 0; r < 16; ++r) v[r] = __int_as_float(max(__float_as_int(v[r]), 0));
+}
+
+// bit k of m |= (v > 0) for a ReLU output v >= 0 (its bits are nonzero iff v > 0): v_min_u32 +
+// v_lshl_or_b32, two ops instead of compare, select and or
+__device__ __forceinline__ uint32_t relu_bit(uint32_t m, float v, int k) {
+    return m | (min(__float_as_uint(v), 1u) << k);
 }
 
 __device__ __forceinline__ S3 split8(float v0, float v1, float v2, float v3, float v4, float v5, float v6, float v7) {
@@ -285,27 +289,33 @@ struct ActX6 {
 };
 
 // layer 0: h1 = relu(W0 x) (A-CAQ: Q(relu(.)), m1 = its ReLU mask); lane = point j, half h
+// (on the pieces of x, split by the caller: the backward stages them for dW0 as well)
 template <bool QUANT>
-__device__ __forceinline__ void layer0(const __bf16* img, const float (&x)[16], floatx16 (&h1)[2], uint32_t& m1,
-                                       int lane, const QuantRec& aq) {
+__device__ __forceinline__ void layer0_split(const __bf16* img, const S3 (&xb)[2], floatx16 (&h1)[2], uint32_t& m1,
+                                             int lane, const QuantRec& aq) {
     const int m = lane & 31, h = lane >> 5;
     h1[0] = h1[1] = zero16();
 #pragma unroll
-    for (int c = 0; c < 2; ++c) {
-        const S3 xb = split_arr(x + 8 * c);
+    for (int c = 0; c < 2; ++c)
 #pragma unroll
-        for (int t = 0; t < 2; ++t) h1[t] = mma6(row_read(img, IM_W0, S32, 32 * t + m, 16 * c + 4 * h), xb, h1[t]);
-    }
+        for (int t = 0; t < 2; ++t) h1[t] = mma6(row_read(img, IM_W0, S32, 32 * t + m, 16 * c + 4 * h), xb[c], h1[t]);
     m1 = 0;
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
         relu16i(h1[t]);
         if constexpr (QUANT) {
 #pragma unroll
-            for (int r = 0; r < 16; ++r) m1 |= (h1[t][r] > 0.f ? 1u : 0u) << (16 * t + r);
+            for (int r = 0; r < 16; ++r) m1 = relu_bit(m1, h1[t][r], 16 * t + r);
             fake_quant16(h1[t], aq);
         }
     }
+}
+
+template <bool QUANT>
+__device__ __forceinline__ void layer0(const __bf16* img, const float (&x)[16], floatx16 (&h1)[2], uint32_t& m1,
+                                       int lane, const QuantRec& aq) {
+    const S3 xb[2] = {split_arr(x), split_arr(x + 8)};
+    layer0_split<QUANT>(img, xb, h1, m1, lane, aq);
 }
 
 // forward chain up to h3 (and rgb when need_rgb)
@@ -608,12 +618,18 @@ __device__ __forceinline__ void bwd_chain_role(const MlpArgs& a, const __bf16* i
         // stages outside its registers and LDS) and layer 0's ReLU mask m1 (with QUANT: before the
         // activation quantizer) in the unused columns 16.. of the gradient tile.
         // The wgrad wave forms ga1 = mask(W1^T go) itself (it waits on the chain wave otherwise).
-        float xr[16];
-        load_x6(a, in.pt, in.valid, h, xr, opaque_zero());
+        // x's bf16 pieces are kept for stage 7 (staged split: the wgrad wave does not split x).
+        S3 xb[2];
+        {
+            float xr[16];
+            load_x6(a, in.pt, in.valid, h, xr, opaque_zero());
+            xb[0] = split_arr(xr);
+            xb[1] = split_arr(xr + 8);
+        }
         {
             floatx16 h1[2];
             uint32_t m1;
-            layer0<QUANT>(imt, xr, h1, m1, lane, aq);
+            layer0_split<QUANT>(imt, xb, h1, m1, lane, aq);
             const S3 GO = split_chunk(go, 0);
             open(true, 6);
 #pragma unroll
@@ -624,15 +640,15 @@ __device__ __forceinline__ void bwd_chain_role(const MlpArgs& a, const __bf16* i
 #pragma unroll
                 for (int t = 0; t < 2; ++t)
 #pragma unroll
-                    for (int r = 0; r < 16; ++r) m1 |= (h1[t][r] > 0.f ? 1u : 0u) << (16 * t + r);
+                    for (int r = 0; r < 16; ++r) m1 = relu_bit(m1, h1[t][r], 16 * t + r);
             }
             *reinterpret_cast<uint32_t*>(stGb[0] + j * S32 + 16 + 2 * h) = m1;
             publish();
         }
-        // stage 7 (dW0): x
+        // stage 7 (dW0): x, as its bf16 pieces in a [32 points][S32] image in the activation buffer
         open(true, 7);
-        stage_arrF(actF, xr, 0, j, h);
-        stage_arrF(actF, xr + 8, 16, j, h);
+        stage(stA, STG_PIECE, S32, xb[0], 0, 0, j, h);
+        stage(stA, STG_PIECE, S32, xb[1], 0, 1, j, h);
         publish();
     }
 #ifdef NERF_X6CG_PROF
@@ -825,14 +841,17 @@ __device__ __forceinline__ void bwd_wgrad_role(const MlpArgs& a, const __bf16* i
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
-            Ops32<1> o;
-            S3 gb[2];
+            S3 A[2], X[2], gb[2];
             const __bf16* sg = stG + (1 - t) * 3 * STG_PIECE;
-            read32<1>(o, sg, actF, lane);
 #pragma unroll
-            for (int c = 0; c < 2; ++c) gb[c] = row_read_st(sg, STG_PIECE, S32, j, 16 * c + 4 * h);
+            for (int c = 0; c < 2; ++c) {
+                A[c] = tr_read(sg, STG_PIECE, 0, S32, 16 * c, 0, lane);
+                X[c] = tr_read(stA, STG_PIECE, 0, S32, 16 * c, 0, lane);   // x pieces (k = point)
+                gb[c] = row_read_st(sg, STG_PIECE, S32, j, 16 * c + 4 * h);
+            }
             if (t == 1) flag_set(ack, ++seq);
-            mma32<1>(g.dW0[t], o);
+#pragma unroll
+            for (int c = 0; c < 2; ++c) g.dW0[t][0] = mma6(A[c], X[c], g.dW0[t][0]);
 #pragma unroll
             for (int c = 0; c < 2; ++c) gx = mma6(tr_read(img, IM_PIECE, IM_W0, S32, 32 * t + 16 * c, 0, lane), gb[c], gx);
         }

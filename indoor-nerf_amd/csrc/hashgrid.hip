@@ -40,6 +40,7 @@ struct HashGradParams {
     int owner_log2;       // owners per level = 2^owner_log2
     float* chunk_max;     // deterministic mode: [L][chunk_stride] max |entry| of each chunk, else null
     int overwrite;        // owner pass: store every row (the gradients are logically zero), no loads
+    int level0;           // owner pass: first level of the launch's level range (grid rows = its levels)
 };
 
 // Grouped coarse levels: blockIdx.y == 0 runs levels [0, group) of its points, two levels' gathers
@@ -502,7 +503,7 @@ __global__ void __launch_bounds__(THREADS) hash_bwd_owner_kernel(HashGradParams 
     // Finest first alone is slower (273 us): the coarse pass's bins, written last, are partly still
     // in the Infinity Cache when the early blocks read them.
     const int o = blockIdx.x, y = blockIdx.y;
-    const int lvl = (y & 1) ? (y >> 1) : (int)gridDim.y - 1 - (y >> 1);
+    const int lvl = hp.level0 + ((y & 1) ? (y >> 1) : (int)gridDim.y - 1 - (y >> 1));
     const int S = 1 << hp.slice_log2, n_own = 1 << hp.owner_log2;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     for (int i = tid; i < (DET ? 2 : 1) * S; i += kOwnerThreads) s_slice[i] = Acc{0, 0};
@@ -989,10 +990,13 @@ extern "C" int nerf_tv_bwd_bin(const float* const* d_tables, int n_levels, int l
     return NERF_OK;
 }
 
-extern "C" int nerf_hash_encode_bwd_owner(int n_levels, int log2_T, int64_t n_chunks, int64_t chunk_capacity,
-                                          float* const* d_dtables, int deterministic, void* d_workspace,
-                                          size_t workspace_bytes, void* stream) {
+extern "C" int nerf_hash_encode_bwd_owner_range(int n_levels, int level_begin, int level_end, int log2_T,
+                                                int64_t n_chunks, int64_t chunk_capacity, float* const* d_dtables,
+                                                int deterministic, void* d_workspace, size_t workspace_bytes,
+                                                void* stream) {
     NERF_REQUIRE((deterministic & ~(1 | NERF_OWNER_OVERWRITE)) == 0, "hash_encode_bwd_owner: flags %d", deterministic);
+    NERF_REQUIRE(0 <= level_begin && level_begin <= level_end && level_end <= n_levels,
+                 "hash_encode_bwd_owner: level range [%d, %d) of %d", level_begin, level_end, n_levels);
     const bool overwrite = (deterministic & NERF_OWNER_OVERWRITE) != 0;
     deterministic &= 1;
     HashGradParams hp{};
@@ -1007,9 +1011,10 @@ extern "C" int nerf_hash_encode_bwd_owner(int n_levels, int log2_T, int64_t n_ch
         NERF_REQUIRE(d_dtables[l], "hash_encode_bwd_owner: grad table %d is null", l);
         hp.dtables[l] = d_dtables[l];
     }
-    if (n_chunks == 0 && !overwrite) return NERF_OK;
+    if ((n_chunks == 0 && !overwrite) || level_end == level_begin) return NERF_OK;
     hp.nchunks = (int)n_chunks;
-    const dim3 grid(1u << hp.owner_log2, n_levels);
+    hp.level0 = level_begin;
+    const dim3 grid(1u << hp.owner_log2, level_end - level_begin);
     if (deterministic)
         hipLaunchKernelGGL((hash_bwd_owner_kernel<kSliceLog2Det, 1024, true>), grid, dim3(1024), 0, as_stream(stream),
                            hp);
@@ -1033,6 +1038,13 @@ extern "C" int nerf_hash_bwd_entry_count(int n_levels, int log2_T, int64_t n_chu
                        (int64_t)1 << hp.owner_log2, (int64_t)hp.chunk_stride, (int)n_chunks, n_levels, d_count);
     NERF_CHECK_LAUNCH("hash_bwd_entry_count");
     return NERF_OK;
+}
+
+extern "C" int nerf_hash_encode_bwd_owner(int n_levels, int log2_T, int64_t n_chunks, int64_t chunk_capacity,
+                                          float* const* d_dtables, int deterministic, void* d_workspace,
+                                          size_t workspace_bytes, void* stream) {
+    return nerf_hash_encode_bwd_owner_range(n_levels, 0, n_levels, log2_T, n_chunks, chunk_capacity, d_dtables,
+                                            deterministic, d_workspace, workspace_bytes, stream);
 }
 
 // No workspace: coalesced memory-side float atomics (never deterministic).

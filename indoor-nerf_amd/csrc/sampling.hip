@@ -83,7 +83,7 @@ __device__ __forceinline__ void build_cdf(int nb, WAt w_at, float* cdf_l, int la
     // sum of (w + 1e-5)
     double part = 0.0;
     for (int i = lane; i < nw; i += 64) part += (double)(w_at(i) + 1e-5f);
-    const float wsum = (float)wave_sum_d(part);
+    const float wsum = (float)wave_sum_dpp(part);
     // contiguous chunk per lane for the prefix sum
     const int per = (nw + 63) / 64;
     const int i0 = lane * per;
@@ -92,12 +92,7 @@ __device__ __forceinline__ void build_cdf(int nb, WAt w_at, float* cdf_l, int la
         const int i = i0 + k;
         if (i < nw) loc += (double)((w_at(i) + 1e-5f) / wsum);
     }
-    double incl = loc;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const double y = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += y;
-    }
+    const double incl = wave_incl_sum_dpp(loc);
     double run = incl - loc;
     for (int k = 0; k < per; ++k) {
         const int i = i0 + k;
@@ -183,13 +178,13 @@ __global__ void __launch_bounds__(256) sample_fine_kernel(PdfArgs a) {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     if (a.z_std) {
-        const double mean = wave_sum_d(sum) / (double)N;
+        const double mean = wave_sum_dpp(sum) / (double)N;
         double ss = 0.0;
         for (int k = lane; k < N; k += 64) {
             const double d = (double)all_l[S + k] - mean;
             ss += d * d;
         }
-        ss = wave_sum_d(ss);
+        ss = wave_sum_dpp(ss);
         if (lane == 0) a.z_std[r] = (float)sqrt(ss / (double)N);
     }
     const float* ray = a.rays + r * a.ray_stride;

@@ -53,16 +53,24 @@ class GradArena:
     the buffer up to a multiple of this many elements (the sharded optimizer needs world x _ALIGN)
     — the gaps and the tail are never a gradient and stay zero."""
 
-    def __init__(self, params, pad_to=1, defer_tables=False):
+    def __init__(self, params, pad_to=1, defer_tables=False, bucket_starts=()):
         # quantizer scalars (soft_bits, range_scale, v_max) never receive a gradient in the
         # reference (their uses are detached): they keep grad None, so the optimizer skips them
         self.params = [p for p in params if p.requires_grad and not getattr(p, "_nerf_no_grad", False)]
-        self.offsets, off = [], 0
+        # buckets: contiguous element ranges, each a multiple of pad_to long, split before the
+        # parameters in bucket_starts (dist.ShardedOptimizer reduces them one by one)
+        starts = {id(p) for p in bucket_starts}
+        self.offsets, off, b0, self.buckets = [], 0, 0, []
         for p in self.params:
+            if id(p) in starts and off > b0:
+                off = -(-off // pad_to) * pad_to
+                self.buckets.append((b0, off))
+                b0 = off
             self.offsets.append(off)
             off += -(-p.numel() // _ALIGN) * _ALIGN
         self.numel = off
         total = -(-self.numel // pad_to) * pad_to
+        self.buckets.append((b0, total))
         dev = self.params[0].device
         self.flat = torch.zeros(total, device=dev, dtype=torch.float32)
         self.views = [self.flat[o:o + p.numel()].view_as(p) for p, o in zip(self.params, self.offsets)]
@@ -112,6 +120,27 @@ def _staged(t):
     return t.cpu() if (t.is_cuda and dist.get_backend() == "gloo") else t
 
 
+def _reduce_scatter(out, inp, group=None):
+    """dist.reduce_scatter_tensor (sum) for every backend: 'nccl' (RCCL) on the device tensors, gloo
+    (tests, one-GPU rehearsals) on host copies — the same call and the same shard indexing."""
+    if dist.get_backend(group) == "gloo" and (out.is_cuda or inp.is_cuda):
+        h = torch.empty(out.shape, dtype=out.dtype)
+        dist.reduce_scatter_tensor(h, inp.cpu(), op=dist.ReduceOp.SUM, group=group)
+        out.copy_(h)
+    else:
+        dist.reduce_scatter_tensor(out, inp, op=dist.ReduceOp.SUM, group=group)
+
+
+def _all_gather(out, inp, group=None):
+    """dist.all_gather_into_tensor for every backend (gloo on host copies); inp may be a view of out."""
+    if dist.get_backend(group) == "gloo" and (out.is_cuda or inp.is_cuda):
+        h = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_gather_into_tensor(h, inp.cpu(), group=group)
+        out.copy_(h)
+    else:
+        dist.all_gather_into_tensor(out, inp, group=group)
+
+
 def _capturing(t):
     return t.is_cuda and torch.cuda.is_current_stream_capturing()
 
@@ -159,7 +188,8 @@ class ShardedOptimizer:
     """Optimizer-state sharding for data parallelism (ZeRO stage 1).
 
     The parameters become views of one flat fp32 buffer laid out like the GradArena, padded to a
-    multiple of world x _ALIGN, and rank r owns the contiguous range [r N/G, (r+1) N/G) of it.
+    multiple of world x _ALIGN, and in each of the arena's buckets (one, or the split made with
+    GradArena(bucket_starts=...)) rank r owns the contiguous r-th 1/G of the bucket.
     Per iteration, instead of an all-reduce of the gradients and a dense RAdam pass over all 16.8 M
     elements on every rank:
       reduce_grads()   reduce-scatter (sum) of the gradient buffer into this rank's shard, x 1/G
@@ -168,14 +198,20 @@ class ShardedOptimizer:
     The collective bytes equal one all-reduce; the dense optimizer traffic drops by G. Elementwise
     RAdam on a shard is bit-identical to RAdam on the whole tensor (tests/test_gpu_dist.py).
     Exp_avg / exp_avg_sq are valid on the rank's own shard only; consolidate_state() assembles
-    them for a checkpoint (model.save_checkpoint)."""
+    them for a checkpoint (model.save_checkpoint).
 
-    def __init__(self, optimizer, arena, group=None):
+    overlap (with buckets): the step's hash-table owner pass is held back (hashgrid.hold_owner, set
+    by model.train_step / graphs.GraphedTrainStep for this hook) and reduce_grads() runs it bucket by
+    bucket — the levels of bucket 0, then those of bucket 1, ... — starting each bucket's
+    reduce-scatter on a side stream as soon as its levels are summed, so the collective of the first
+    buckets runs under the owner pass of the later ones."""
+
+    def __init__(self, optimizer, arena, group=None, overlap=False):
         self.opt, self.arena, self.group = optimizer, arena, group
         self.world = dist.get_world_size(group) if (dist.is_available() and dist.is_initialized()) else 1
         self.rank = dist.get_rank(group) if self.world > 1 else 0
         n_flat = arena.flat.numel()
-        if n_flat % (self.world * _ALIGN):
+        if any((e - s) % (self.world * _ALIGN) for s, e in arena.buckets):
             raise ValueError("ShardedOptimizer: build the GradArena with pad_to=world*64")
         dev = arena.flat.device
         # parameters as views of one flat buffer (same layout as the gradients)
@@ -186,41 +222,81 @@ class ShardedOptimizer:
                 view.copy_(p.data)
                 p.data = view
         arena.attach()
-        self.count = n_flat // self.world
-        self.lo, self.hi = self.rank * self.count, (self.rank + 1) * self.count
+        # per bucket (s, e): this rank owns [own_lo, own_hi), stored at gshard[g0, g0 + n/G)
+        self.pieces, g0 = [], 0
+        for s, e in arena.buckets:
+            n = (e - s) // self.world
+            self.pieces.append((s + self.rank * n, s + (self.rank + 1) * n, g0))
+            g0 += n
+        self.count = g0
         self.gshard = torch.zeros(self.count, device=dev, dtype=torch.float32)
-        ranges = shard_ranges(arena.offsets, [p.numel() for p in arena.params], self.lo, self.hi)
-        shard = {}
-        for p, off, r in zip(arena.params, arena.offsets, ranges):
-            if r is not None:
-                a, b = r
-                shard[p] = (a, b, self.gshard[off + a - self.lo:off + b - self.lo])
-        self.ranges = ranges
+        shard, self.ranges = {}, []
+        for p, off in zip(arena.params, arena.offsets):
+            r = None
+            for lo, hi, gp in self.pieces:
+                a, b = max(lo, off), min(hi, off + p.numel())
+                if b > a:
+                    r = (a - off, b - off)
+                    shard[p] = (a - off, b - off, self.gshard[gp + a - lo:gp + b - lo])
+            self.ranges.append(r)
         optimizer.set_shard(shard if self.world > 1 else None)
+        self.overlap = bool(overlap) and len(arena.buckets) > 1 and dev.type == "cuda"
+        self.side = torch.cuda.Stream(device=dev) if self.overlap else None
+        self._levels = None
+
+    def _level_ranges(self, held):
+        """Per bucket, the level range [lb, le) of the held owner pass whose tables lie in it."""
+        if self._levels is None or self._levels[0] is not held:
+            base = self.arena.flat.data_ptr()
+            bucket_of = []
+            for g in held.grads:
+                off = (g.data_ptr() - base) // 4
+                bucket_of.append(next(k for k, (s, e) in enumerate(self.arena.buckets) if s <= off < e))
+            if bucket_of != sorted(bucket_of):
+                raise RuntimeError("ShardedOptimizer(overlap): table levels must lie in bucket order")
+            ranges = [(bucket_of.index(k) if k in bucket_of else 0, len(bucket_of) - bucket_of[::-1].index(k)
+                       if k in bucket_of else 0) for k in range(len(self.arena.buckets))]
+            self._levels = (held, ranges)
+        return self._levels[1]
 
     def reduce_grads(self):
-        """Reduce-scatter of the gradient arena: this rank's shard of the mean gradient."""
+        """Reduce-scatter of each gradient bucket: this rank's shard of the mean gradient. The same
+        collective on every backend (RCCL on the device buffers; gloo on host copies of them). With
+        overlap and a held owner pass: every bucket's levels are summed and recorded first, then each
+        bucket's reduce-scatter waits on the side stream for its own levels only."""
+        from .hashgrid import pending_bins
+        held = pending_bins(self.arena.flat.device).take_held() if self.overlap else None
         if self.world == 1:
+            if held is not None:
+                held.run(0, held.L)
             return
-        flat = self.arena.flat
-        if dist.get_backend(self.group) == "gloo":      # no reduce-scatter in gloo: all-reduce + slice
-            h = flat.cpu()
-            dist.all_reduce(h, op=dist.ReduceOp.SUM, group=self.group)
-            self.gshard.copy_(h[self.lo:self.hi].to(self.gshard.device))
-        else:
-            dist.reduce_scatter_tensor(self.gshard, flat, op=dist.ReduceOp.SUM, group=self.group)
-        self.gshard.mul_(1.0 / self.world)
+        flat, events = self.arena.flat, []
+        if held is not None:
+            for lb, le in self._level_ranges(held):
+                held.run(lb, le)
+                ev = torch.cuda.Event()
+                ev.record()
+                events.append(ev)
+        for k, ((s, e), (lo, hi, g0)) in enumerate(zip(self.arena.buckets, self.pieces)):
+            out = self.gshard[g0:g0 + hi - lo]
+            if events:
+                self.side.wait_event(events[k])
+                with torch.cuda.stream(self.side):
+                    _reduce_scatter(out, flat[s:e], self.group)
+                    out.mul_(1.0 / self.world)
+            else:
+                _reduce_scatter(out, flat[s:e], self.group)
+                out.mul_(1.0 / self.world)
+        if events:
+            torch.cuda.current_stream(flat.device).wait_stream(self.side)
 
     def gather_params(self):
-        """All-gather of the updated parameter shards (in place: the shard is a view of the output)."""
+        """All-gather of each bucket's updated parameter shards (in place: the shard is a view of the
+        output)."""
         if self.world == 1:
             return
-        if dist.get_backend(self.group) == "gloo":
-            parts = [torch.empty(self.count) for _ in range(self.world)]
-            dist.all_gather(parts, self.pflat[self.lo:self.hi].cpu(), group=self.group)
-            self.pflat.copy_(torch.cat(parts).to(self.pflat.device))
-        else:
-            dist.all_gather_into_tensor(self.pflat, self.pflat[self.lo:self.hi], group=self.group)
+        for (s, e), (lo, hi, _) in zip(self.arena.buckets, self.pieces):
+            _all_gather(self.pflat[s:e], self.pflat[lo:hi], self.group)
         for p in self.arena.params:       # the collective wrote the parameters in place
             torch.autograd.graph.increment_version(p)
 

@@ -138,8 +138,8 @@ class GraphedTrainStep:
         return (tv_w > 0, quant, priors)
 
     def _capture(self, global_step):
-        from . import _lib
-        from .model import forward_backward, optimizer_update
+        from . import _lib, hashgrid
+        from .model import forward_backward, holds_owner, optimizer_update
         if _lib.timing_enabled():
             raise RuntimeError("GraphedTrainStep: kernel timing is on; torch on ROCm cannot capture timing "
                                "events (time eager_step() instead)")
@@ -155,7 +155,9 @@ class GraphedTrainStep:
         single = self.hook is None
         g1 = torch.cuda.CUDAGraph()
         g2 = None if single else torch.cuda.CUDAGraph()
-        with torch.cuda.stream(side):
+        # with an overlapping DP hook the owner pass stays out of graph 1: the hook runs it by level range
+        # beside the bucket reduce-scatters (dist.ShardedOptimizer(overlap=True))
+        with torch.cuda.stream(side), hashgrid.hold_owner(dev, holds_owner(self.hook)):
             with capturing(sc):
                 with torch.cuda.graph(g1, pool=pool, stream=side):
                     out = forward_backward(self.rays, self.target, self.kw, self.opt, self.args, global_step,

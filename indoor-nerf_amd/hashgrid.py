@@ -157,21 +157,30 @@ class _PendingBins:
     def __init__(self):
         self.ws, self.cap, self.used, self.peak = None, 0, 0, 0
         self.tag = self.grads = self.stream = None
+        self.hold = False     # hold_owner(): the pass's owner launch is left to the caller (HeldOwner)
+        self.held = None
 
     def flush(self):
         if self.used == 0:
             return
         L, log2_T, _, det = self.tag
+        flags = det | (OWNER_OVERWRITE if take_deferred(self.grads) else 0)
+        held = HeldOwner(L, log2_T, self.used, self.cap, self.grads, flags, self.ws)
+        self.last = (self.tag, self.used, self.cap)
+        self.used, self.tag, self.grads = 0, None, None
+        if self.hold:
+            self.held = held
+            return
         with torch.cuda.stream(self.stream):
-            flags = det | (OWNER_OVERWRITE if take_deferred(self.grads) else 0)
-            _lib.call("nerf_hash_encode_bwd_owner", L, log2_T, self.used, self.cap,
-                      _lib.ptr_array(self.grads, "grad_tables"), flags, _lib.ptr(self.ws, "workspace", dtype=torch.uint8),
-                      self.ws.numel(), _lib.stream())
+            held.run(0, L)
         cur = torch.cuda.current_stream()
         if cur != self.stream:
             cur.wait_stream(self.stream)
-        self.last = (self.tag, self.used, self.cap)
-        self.used, self.tag, self.grads = 0, None, None
+
+    def take_held(self):
+        """The owner pass held back by hold_owner() (HeldOwner), or None. It stays valid for replays of a
+        captured step (same workspace, tables and chunk counts)."""
+        return self.held
 
     def last_entry_count(self):
         """Entries the bins of the last owner pass's workspace emitted (nerf_hash_bwd_entry_count;
@@ -242,6 +251,43 @@ class _PendingBins:
         _lib.call("nerf_tv_bwd_bin", _lib.ptr_array(job.tables), L, job.log2_T, job.mv, job.dmv, job.cb,
                   _lib.ptr(job.g, "grad_loss"), _lib.ptr(job.verts, "tv_verts", allow_none=True), base, self.cap, det,
                   _lib.ptr(self.ws, "workspace", dtype=torch.uint8), self.ws.numel(), _lib.stream())
+
+
+class HeldOwner:
+    """An owner pass of a binned backward, launched by the caller, level range by level range
+    (nerf_hash_encode_bwd_owner_range): a data-parallel step starts the reduce-scatter of each gradient
+    bucket once its levels are summed (dist.ShardedOptimizer). `flags` (deterministic, overwrite) were
+    fixed when the pass was held."""
+
+    def __init__(self, L, log2_T, used, cap, grads, flags, ws):
+        self.L, self.log2_T, self.used, self.cap, self.grads = L, log2_T, used, cap, list(grads)
+        self.flags, self.ws = flags, ws
+
+    def run(self, level_begin, level_end):
+        """Launch the levels [level_begin, level_end) on the CURRENT stream (the caller's: after a replayed
+        graph the capture stream is not ordered behind the replay)."""
+        _lib.call("nerf_hash_encode_bwd_owner_range", self.L, level_begin, level_end, self.log2_T, self.used,
+                  self.cap, _lib.ptr_array(self.grads, "grad_tables"), self.flags,
+                  _lib.ptr(self.ws, "workspace", dtype=torch.uint8), self.ws.numel(), _lib.stream())
+
+
+class hold_owner:
+    """Context manager: inside it, the binned backwards' owner passes are not launched at the end of
+    the autograd pass but held (pending_bins(device).take_held()) for the caller to run by level range.
+    Only the caller that runs them may use it (dist.ShardedOptimizer.reduce_grads does)."""
+
+    def __init__(self, device, enabled=True):
+        self.pb, self.enabled = pending_bins(device), bool(enabled)
+
+    def __enter__(self):
+        self.prev, self.pb.hold = self.pb.hold, self.enabled or self.pb.hold
+        if self.enabled:
+            self.pb.held = None
+        return self.pb
+
+    def __exit__(self, *exc):
+        self.pb.hold = self.prev
+        return False
 
 
 def bin_chunks(n_points):

@@ -304,6 +304,12 @@ def lr_schedule(optimizer, args, global_step):
         g["lr"] = new_lrate
 
 
+def holds_owner(grad_hook):
+    """True when grad_hook runs the step's held owner pass itself (dist.ShardedOptimizer.reduce_grads
+    with overlap: the owner pass is launched bucket by bucket beside the reduce-scatters)."""
+    return bool(getattr(getattr(grad_hook, "__self__", None), "overlap", False))
+
+
 def train_step(batch_rays, target_s, render_kwargs_train, optimizer, args, global_step, H=0, W=0, K=None,
                grad_hook=None, loss_scale_sparsity=1.0, tv_generator=None, zero_grad=None, spatial_coords=None,
                post_hook=None):
@@ -312,10 +318,11 @@ def train_step(batch_rays, target_s, render_kwargs_train, optimizer, args, globa
     RAdam step, [post_hook, e.g. the sharded optimizer's parameter all-gather], A-CAQ bit widths,
     lr decay (:1182-1250, :1289-1293). Returns (loss, psnr) as device tensors (no host sync).
     graphs.GraphedTrainStep replays the same iteration from HIP graphs."""
-    loss, img_loss, psnr = forward_backward(batch_rays, target_s, render_kwargs_train, optimizer, args, global_step,
-                                            H=H, W=W, K=K, loss_scale_sparsity=loss_scale_sparsity,
-                                            tv_generator=tv_generator, zero_grad=zero_grad,
-                                            spatial_coords=spatial_coords)
+    with hashgrid.hold_owner(target_s.device, holds_owner(grad_hook)):
+        loss, img_loss, psnr = forward_backward(batch_rays, target_s, render_kwargs_train, optimizer, args,
+                                                global_step, H=H, W=W, K=K, loss_scale_sparsity=loss_scale_sparsity,
+                                                tv_generator=tv_generator, zero_grad=zero_grad,
+                                                spatial_coords=spatial_coords)
     if grad_hook is not None:
         grad_hook()
     optimizer_update(optimizer)

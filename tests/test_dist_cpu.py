@@ -5,6 +5,7 @@ import os
 import socket
 
 import numpy as np
+import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -119,7 +120,7 @@ class _SgdShard:
                     p.view(-1)[a:b].sub_(0.5 * g)
 
 
-def _zero_worker(rank, world, port, out_dir):
+def _zero_worker(rank, world, port, out_dir, buckets=False):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path.insert(0, root)
@@ -131,7 +132,9 @@ def _zero_worker(rank, world, port, out_dir):
     g = torch.Generator().manual_seed(0)
     params = [torch.nn.Parameter(torch.randn(n, generator=g)) for n in (300, 77, 1024, 5)]
     opt = _SgdShard(params)
-    arena = GradArena(params, pad_to=world * 64)
+    # buckets: the arena split before the third parameter (dist.ShardedOptimizer's per-bucket shards)
+    arena = GradArena(params, pad_to=world * 64, bucket_starts=[params[2]] if buckets else ())
+    assert len(arena.buckets) == (2 if buckets else 1)
     sh = ShardedOptimizer(opt, arena)
     for step in range(3):
         arena.zero_()
@@ -158,9 +161,12 @@ def _zero_worker(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
-def test_sharded_optimizer_gloo(tmp_path):
+@pytest.mark.parametrize("buckets", [False, True], ids=["one_bucket", "two_buckets"])
+def test_sharded_optimizer_gloo(tmp_path, buckets):
+    """reduce_scatter_tensor / all_gather_into_tensor (the production collectives, every backend) over
+    one bucket or two: the replicas agree and equal one process's update with the mean gradient."""
     world = 2
-    mp.start_processes(_zero_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+    mp.start_processes(_zero_worker, args=(world, _free_port(), str(tmp_path), buckets), nprocs=world, join=True,
                        start_method="spawn")
     p0, p1 = np.load(tmp_path / "p_0.npy"), np.load(tmp_path / "p_1.npy")
     np.testing.assert_array_equal(p0, p1)
@@ -205,7 +211,7 @@ class _MomentShard(_SgdShard):
         return {"state": {i: {k: v.clone() for k, v in self.state[p].items()} for i, p in enumerate(self.params)}}
 
 
-def _ckpt_worker(rank, world, port, out_dir):
+def _ckpt_worker(rank, world, port, out_dir, buckets=True):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path.insert(0, root)
@@ -217,7 +223,7 @@ def _ckpt_worker(rank, world, port, out_dir):
     g = torch.Generator().manual_seed(0)
     params = [torch.nn.Parameter(torch.randn(n, generator=g)) for n in (300, 77, 1024, 5)]
     opt = _MomentShard(params, rank)
-    sh = ShardedOptimizer(opt, GradArena(params, pad_to=world * 64))
+    sh = ShardedOptimizer(opt, GradArena(params, pad_to=world * 64, bucket_starts=[params[2]] if buckets else ()))
     opt.fill_shard()
     kw = {"network_fn": torch.nn.Linear(2, 2), "network_fine": None, "embed_fn": torch.nn.Linear(3, 1)}
     wrote = save_checkpoint(os.path.join(out_dir, "ckpt.tar"), 42, kw, opt, sharded=sh)

@@ -91,7 +91,7 @@ def test_sharded_radam_bit_identical(tmp_path):
     assert not torch.equal(r0["shard"][0], mlp0[0].detach())
 
 
-def _train_worker(rank, world, port, out):
+def _train_worker(rank, world, port, out, overlap=False):
     _init(rank, world, port)
     import indoor_nerf_amd as nerf
     from indoor_nerf_amd.graphs import GraphedTrainStep
@@ -106,8 +106,10 @@ def _train_worker(rank, world, port, out):
     kw.update(near=2.0, far=6.0)
     params = grad_vars + list(kw["embed_fn"].parameters())
     nerf.broadcast_params(params)
-    arena = nerf.GradArena(params, pad_to=world * 64)
-    sh = nerf.ShardedOptimizer(opt, arena)
+    tabs = kw["embed_fn"].tables()
+    arena = nerf.GradArena(params, pad_to=world * 64, defer_tables=overlap,
+                           bucket_starts=[tabs[len(tabs) // 2]] if overlap else ())
+    sh = nerf.ShardedOptimizer(opt, arena, overlap=overlap)
     ro, rd = synthetic_rays(512, seed=50 + rank)
     rays = (torch.from_numpy(ro).to(dev), torch.from_numpy(rd).to(dev))
     target = torch.rand(512, 3, device=dev, generator=torch.Generator(device=dev).manual_seed(rank))
@@ -124,9 +126,13 @@ def _train_worker(rank, world, port, out):
     torch.distributed.destroy_process_group()
 
 
-def test_sharded_graphed_training_replicas_agree(tmp_path):
+@pytest.mark.parametrize("overlap", [False, True], ids=["zero1", "zero1_overlap"])
+def test_sharded_graphed_training_replicas_agree(tmp_path, overlap):
+    """Graph 1 (forward + backward; with overlap, without the owner pass, which the hook runs by
+    level range beside the bucket reduce-scatters), the hook, graph 2 (RAdam on the shard), the
+    all-gather: replicas stay bit-identical over 6 iterations and the loss is finite."""
     world = 2
-    mp.start_processes(_train_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+    mp.start_processes(_train_worker, args=(world, _free_port(), str(tmp_path), overlap), nprocs=world, join=True,
                        start_method="spawn")
     r0 = torch.load(tmp_path / "train_0.pt", weights_only=True)
     r1 = torch.load(tmp_path / "train_1.pt", weights_only=True)
@@ -161,7 +167,7 @@ def _f10_model(nerf, dev, world):
     return args, kw, opt, params
 
 
-def _dp_worker(rank, world, port, out, R):
+def _dp_worker(rank, world, port, out, R, overlap=False):
     """One rank of the data-parallel equivalence test: this rank's contiguous 1/world of an R-ray
     batch (world = 1: the whole batch in one process). (a) one iteration's gradients after the DP
     all-reduce (mean); (b) 7 training iterations with the ZeRO-1 sharded optimizer (world > 1) or
@@ -191,10 +197,14 @@ def _dp_worker(rank, world, port, out, R):
     res["grads"] = [p.grad.detach().cpu().clone() for p in params]
     # (b) 7 iterations
     args, kw, opt, params = _f10_model(nerf, dev, world)
-    arena = nerf.GradArena(params, pad_to=world * 64 if world > 1 else 1, defer_tables=True)
+    tabs = kw["embed_fn"].tables()
+    arena = nerf.GradArena(params, pad_to=world * 64 if world > 1 else 1, defer_tables=True,
+                           bucket_starts=[tabs[len(tabs) // 2]] if overlap else ())
     hook = post = None
     if world > 1:
-        sh = nerf.ShardedOptimizer(opt, arena)
+        # overlap: the owner pass held and run bucket by bucket beside the two reduce-scatters
+        sh = nerf.ShardedOptimizer(opt, arena, overlap=overlap)
+        assert sh.overlap == overlap
         hook, post = sh.reduce_grads, sh.gather_params
     gen = torch.Generator().manual_seed(7)
     res["params0"] = [p.detach().cpu().clone() for p in params]
@@ -206,12 +216,13 @@ def _dp_worker(rank, world, port, out, R):
     torch.cuda.synchronize()
     res["params"] = [p.detach().cpu().clone() for p in params]
     res["losses"] = losses
-    torch.save(res, os.path.join(out, f"dp{world}_{rank}.pt"))
+    torch.save(res, os.path.join(out, f"dp{world}{'o' if overlap else ''}_{rank}.pt"))
     if world > 1:
         torch.distributed.destroy_process_group()
 
 
-def test_dp_shards_match_one_batch(tmp_path):
+@pytest.mark.parametrize("overlap", [False, True], ids=["zero1", "zero1_overlap"])
+def test_dp_shards_match_one_batch(tmp_path, overlap):
     """SURVEY.md §8(e) through the HIP training step: 2 ranks x 2,048 rays (gloo, both ranks on the
     one GPU) against 1 x 4,096 rays in one process — same weights (F10's trained-like state), the
     same pytest draws (render.pytest_shard: each rank keeps its rows of the global batch's draws),
@@ -224,11 +235,12 @@ def test_dp_shards_match_one_batch(tmp_path):
     R = 4096
     mp.start_processes(_dp_worker, args=(1, _free_port(), str(tmp_path), R), nprocs=1, join=True,
                        start_method="spawn")
-    mp.start_processes(_dp_worker, args=(2, _free_port(), str(tmp_path), R), nprocs=2, join=True,
+    mp.start_processes(_dp_worker, args=(2, _free_port(), str(tmp_path), R, overlap), nprocs=2, join=True,
                        start_method="spawn")
+    tag = "dp2o" if overlap else "dp2"
     one = torch.load(tmp_path / "dp1_0.pt", weights_only=True)
-    r0 = torch.load(tmp_path / "dp2_0.pt", weights_only=True)
-    r1 = torch.load(tmp_path / "dp2_1.pt", weights_only=True)
+    r0 = torch.load(tmp_path / f"{tag}_0.pt", weights_only=True)
+    r1 = torch.load(tmp_path / f"{tag}_1.pt", weights_only=True)
     n_mlp = 10
     for i, (a, b, c) in enumerate(zip(one["grads"], r0["grads"], r1["grads"])):
         assert torch.equal(b, c), f"param {i}: the all-reduced gradients differ between ranks"
