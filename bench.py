@@ -37,7 +37,9 @@ X6_PEAK_TFLOPS = 2500.0 / 6
 # plus the owner pass (once per iteration), and only their sum is a complete scatter-add.
 # Hash ops are priced per DISTINCT point encoded ("hash_point"): with the coarse-feature reuse (DESIGN
 # §8.5) the fine pass encodes only its importance samples, so an iteration encodes R x (64 + 128) points
-# (R x (64 + 192) without it); the MLP and compositing ops run on every point / sample of both passes.
+# (R x (64 + 192) without it); the MLP forward and compositing ops run on every point / sample of both
+# passes. The backward ops are priced by the points they walk ("bwd_point", "bwd_hash_point"): with
+# the active-point backward (field.set_active_points) only the samples with a nonzero raw gradient.
 #   hash fwd : per point  16 levels x 8 corners x 8 B gathered + 12 B xyz + 128 B features + 1 B keep
 #   hash fwd packed (A-CAQ eval): as hash fwd with 2-B entries (two 8-bit codes)
 #   hash bwd : per point  16 x 8 x 8 B read+write of the added rows (2 x 1024) + 12 B xyz + 128 B d feat
@@ -48,14 +50,14 @@ X6_PEAK_TFLOPS = 2500.0 / 6
 OPS = {
     "hash_bwd": dict(calls=("nerf_hash_encode_bwd_bin", "nerf_hash_encode_bwd_bin_rows", "nerf_hash_encode_bwd_owner",
                             "nerf_hash_encode_bwd_ws", "nerf_hash_encode_bwd"), bound="hbm",
-                     per_unit=2 * 16 * 8 * 8 + 12 + 128, unit="hash_point"),
+                     per_unit=2 * 16 * 8 * 8 + 12 + 128, unit="bwd_hash_point"),
     # nerf_hash_encode_fwd_rows also copies the coarse features into the fine rows (priced as encoding)
     "hash_fwd": dict(calls=("nerf_hash_encode_fwd", "nerf_hash_encode_fwd_rows"), bound="hbm",
                      per_unit=16 * 8 * 8 + 12 + 128 + 1, unit="hash_point"),
     # A-CAQ eval (int-packed tables, configs[4]): 8-bit codes = 2 B per corner entry (two features)
     "hash_fwd_packed": dict(calls=("nerf_hash_encode_fwd_packed",), bound="hbm", per_unit=16 * 8 * 2 + 12 + 128 + 1,
                             unit="hash_point"),
-    "mlp_bwd": dict(calls=("nerf_mlp_bwd", "nerf_mlp_bwd_batch"), bound="mfma", per_unit=2 * 18688, unit="point"),
+    "mlp_bwd": dict(calls=("nerf_mlp_bwd", "nerf_mlp_bwd_batch"), bound="mfma", per_unit=2 * 18688, unit="bwd_point"),
     "mlp_fwd": dict(calls=("nerf_mlp_fwd",), bound="mfma", per_unit=18688, unit="point"),
     "composite_fwd": dict(calls=("nerf_composite_fwd",), bound="hbm", per_unit=24, unit="sample"),
     "composite_bwd": dict(calls=("nerf_composite_bwd",), bound="hbm", per_unit=40, unit="sample"),
@@ -211,6 +213,9 @@ def parse():
     ap.add_argument("--deterministic", type=int, default=0,
                     help="1: bitwise-reproducible backward (nerf.set_deterministic: fixed-point hash owner pass, "
                          "ordered MLP weight-gradient reduction)")
+    ap.add_argument("--active-points", type=int, default=1,
+                    help="1: the field backward walks only the samples with a nonzero raw gradient "
+                         "(field.set_active_points); 0: every sample (A/B)")
     ap.add_argument("--coarse-reuse", type=int, default=1,
                     help="1: the fine pass reuses the coarse pass's hash encoding (DESIGN §8.5); 0: re-encode (A/B)")
     ap.add_argument("--mode", default="train", choices=["train", "render"],
@@ -418,6 +423,7 @@ def main():
     if a.deterministic:
         nerf.set_deterministic(True)
     nerf.set_coarse_reuse(bool(a.coarse_reuse))
+    nerf.set_active_points(bool(a.active_points))
     kw, kw_test, _, grad_vars, opt = nerf.create_nerf(args, device=dev)
     for d in (kw, kw_test):
         d.update(near=wl["near"], far=wl["far"])     # train() adds the scene bounds (run_nerf.py:768-770,865-869)
@@ -528,10 +534,17 @@ def main():
     reused = any(base_name(c) == "nerf_hash_encode_fwd_rows" for c in kernels)
     units = {"point": points_per_step, "sample": points_per_step,
              "hash_point": R * (ns + ni) if (reused and ni) else points_per_step}
-    hash_entries = None
+    units["bwd_point"], units["bwd_hash_point"] = units["point"], units["hash_point"]
+    hash_entries = active = None
     if kernels and a.mode == "train":
+        from indoor_nerf_amd.field import last_active_units
         from indoor_nerf_amd.hashgrid import pending_bins
         hash_entries = pending_bins(dev).last_entry_count()
+        active = last_active_units()
+        if active is not None:
+            # the backward walks the active points only (field.set_active_points): price the work it did
+            units["bwd_point"] = active["mlp_points"]
+            units["bwd_hash_point"] = active["hash_points"]
     if kernels:
         ops = op_rooflines(kernels, a.steps, units, sum(p.numel() for p in params), hash_entries)
         ranked = [o for o in ops if not o.get("degenerate")]
@@ -580,6 +593,9 @@ def main():
                    "parallelism": f"dp{world}" + ("-zero1" if zero else "") + ("-overlap" if zero and a.overlap else "")},
         "hip_graph": bool(gstep is not None and gstep.captures > 0),
         "coarse_reuse": reused,
+        "active_points": None if active is None else {"fraction": round(active["fraction"], 4),
+                                                      "mlp_bwd_points": active["mlp_points"],
+                                                      "hash_bwd_points": active["hash_points"]},
         "loss": round(float(loss), 6),
         "roofline": roofline,
         "step_roofline": step_roofline,
@@ -592,12 +608,17 @@ def main():
         out["deterministic"] = True
     # north star "PSNR within 0.1 dB of reference": the committed result of tests/test_gpu_converge.py
     # (the reference trained on F19 six times vs six HIP runs; late-phase mean PSNR difference per metric)
-    for name in ("r03_psnr_vs_reference.json", "r02_psnr_vs_reference.json"):
+    for name in ("r04_psnr_vs_reference.json", "r03_psnr_vs_reference.json", "r02_psnr_vs_reference.json"):
         pv = os.path.join(ROOT, "profiles", name)
         if os.path.exists(pv):
             pj = json.load(open(pv))
             out["psnr_vs_reference"] = {k: {"d_db": v["d_db"], "reference_db": v["reference_db"], "hip_db": v["hip_db"]}
-                                        for k, v in pj.items() if isinstance(v, dict)}
+                                        for k, v in pj.items() if isinstance(v, dict) and "d_db" in v}
+            if isinstance(pj.get("design"), str):
+                out["psnr_vs_reference"]["runs"] = pj["design"]
+            if isinstance(pj.get("all_seeds"), dict):
+                out["psnr_vs_reference"]["with_oracle_runs"] = {
+                    k: v["d_db"] for k, v in pj["all_seeds"].items() if isinstance(v, dict)}
             out["psnr_vs_reference"]["source"] = "profiles/" + name + (
                 " (commit " + pj["commit"] + ")" if isinstance(pj.get("commit"), str) else "")
             break

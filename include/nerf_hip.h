@@ -147,8 +147,10 @@ int nerf_hash_encode_bwd_bin(const float* d_xyz, int64_t n_points,
 /* Row-mapped bin (coarse-feature reuse): point p reads d_xyz and d_dfeat at row d_rows[p] (NULL: p);
  * with d_dfeat2 != NULL it adds d_dfeat2 at row d_rows2[p] (NULL: p; strides feat2_*) to its
  * gradient, so a point shared by two passes is binned once with the sum of both gradients (d_dfeat
- * may then be NULL: the point's gradient is the d_dfeat2 term alone). */
-int nerf_hash_encode_bwd_bin_rows(const float* d_xyz, const int32_t* d_rows, int64_t n_points,
+ * may then be NULL: the point's gradient is the d_dfeat2 term alone). d_count (device int, NULL = all
+ * n_points): only points p < *d_count are binned (d_rows = an active-point list of nerf_active_rows);
+ * the launch covers the chunks of n_points, those past the count get empty segments. */
+int nerf_hash_encode_bwd_bin_rows(const float* d_xyz, const int32_t* d_rows, const int32_t* d_count, int64_t n_points,
                                   const float* bbox_min3, const float* bbox_max3,
                                   const float* level_res, int n_levels, int log2_T,
                                   const float* d_dfeat, int64_t feat_stride_point, int64_t feat_stride_level,
@@ -172,6 +174,22 @@ int nerf_hash_encode_bwd_owner_range(int n_levels, int level_begin, int level_en
 int nerf_hash_bwd_entry_count(int n_levels, int log2_T, int64_t n_chunks, int64_t chunk_capacity, int deterministic,
                               const void* d_workspace, size_t workspace_bytes, unsigned long long* d_count,
                               void* stream);
+
+/* ---- active points of a field backward -----------------------------------------------------------
+ * raw2outputs' autograd (run_nerf.py:364-386) gives every sample with relu(sigma + noise) = 0 an all-
+ * zero raw-gradient row, and NeRFSmall's backward is linear in it: such points add nothing to the MLP
+ * weight gradients or the hash-table gradients. nerf_active_rows lists, in ascending order, the rows p
+ * of d_graw [P,4] (or of d_dgeo [P,16], rows 1..15, when given) that are not all zero: d_rows [P] and
+ * d_counts[0]; with d_perm [P], the positions d_perm[p] < n_first of the active rows also go to
+ * d_first [n_first] / d_counts[1]. d_zero_feat (optional, level-major, n_levels x 2 floats per row at
+ * stride zero_stride_level): the rows d_perm[p] (or p) >= n_first of the INACTIVE points are zeroed
+ * (feature-gradient rows a bin reads but the active-point backward does not write). Two launches, no
+ * host sync; the workspace is nerf_active_rows_workspace_bytes(P). */
+size_t nerf_active_rows_workspace_bytes(int64_t n_points);
+int nerf_active_rows(const float* d_graw, const float* d_dgeo, int64_t n_points, const int32_t* d_perm,
+                     int64_t n_first, int32_t* d_rows, int32_t* d_first, int32_t* d_counts,
+                     float* d_zero_feat, int64_t zero_stride_level, int n_levels, void* d_workspace,
+                     size_t workspace_bytes, void* stream);
 
 /* ---- spherical harmonics, degree 4 (SHEncoder.forward, hash_encoding.py:153-191) ---------- */
 int nerf_sh4_fwd(const float* d_dirs, int64_t n, float* d_out /* [n,16] */, void* stream);
@@ -270,6 +288,9 @@ typedef struct {
     const float* act_qrec;
     const int32_t* dfeat_rows;   /* optional: point p's d feat is written to row dfeat_rows[p] of dfeat (NULL: p);
                                     the coarse-feature reuse's importance-first order, nerf_sample_fine_rows d_perm */
+    const int32_t* rows;         /* optional (with d_count): walk only the points rows[0 .. *d_count) — the active
+                                    points of nerf_active_rows; the other points' d feat / d sh are not written */
+    const int32_t* d_count;      /* device int: the number of rows */
 } nerf_mlp_bwd_job;
 
 size_t nerf_mlp_bwd_det_workspace_bytes(void);

@@ -38,7 +38,8 @@ class MlpBwdJob(ctypes.Structure):
     _fields_ = [("feat", c_vp), ("feat_stride_point", c_i64), ("feat_stride_level", c_i64), ("sh", c_vp),
                 ("sh_stride", c_i64), ("viewdirs", c_vp), ("samples_per_ray", c_i64), ("keep", c_vp),
                 ("n_points", c_i64), ("weights", MlpWeights), ("graw", c_vp), ("grads", MlpGrads), ("dfeat", c_vp),
-                ("dsh", c_vp), ("dgeo", c_vp), ("act_qrec", c_vp), ("dfeat_rows", c_vp)]
+                ("dsh", c_vp), ("dgeo", c_vp), ("act_qrec", c_vp), ("dfeat_rows", c_vp),
+                ("rows", c_vp), ("d_count", c_vp)]
 
 
 PRIORS_MAX_RAYS = 8192   # NERF_PRIORS_MAX_RAYS
@@ -95,8 +96,10 @@ SIGNATURES = {
                                    c_vp],
     "nerf_hash_encode_fwd_rows": [c_vp, c_vp, c_i64, c_f32p, c_f32p, c_f32p, c_int, c_int, ctypes.POINTER(c_vp),
                                   c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp],
-    "nerf_hash_encode_bwd_bin_rows": [c_vp, c_vp, c_i64, c_f32p, c_f32p, c_f32p, c_int, c_int, c_vp, c_i64, c_i64,
-                                      c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_int, c_vp, ctypes.c_size_t, c_vp],
+    "nerf_hash_encode_bwd_bin_rows": [c_vp, c_vp, c_vp, c_i64, c_f32p, c_f32p, c_f32p, c_int, c_int, c_vp, c_i64,
+                                      c_i64, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_int, c_vp, ctypes.c_size_t, c_vp],
+    "nerf_active_rows": [c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_vp, ctypes.c_size_t,
+                         c_vp],
     "nerf_hash_bwd_entry_count": [c_int, c_int, c_i64, c_i64, c_int, c_vp, ctypes.c_size_t, c_vp, c_vp],
     "nerf_hash_encode_bwd_owner_range": [c_int, c_int, c_int, c_int, c_i64, c_i64, ctypes.POINTER(c_vp), c_int, c_vp,
                                          ctypes.c_size_t, c_vp],
@@ -188,6 +191,8 @@ def load():
     lib.nerf_priors_workspace_bytes.argtypes = [c_i64]
     lib.nerf_mlp_bwd_det_workspace_bytes.restype = ctypes.c_size_t
     lib.nerf_mlp_bwd_det_workspace_bytes.argtypes = []
+    lib.nerf_active_rows_workspace_bytes.restype = ctypes.c_size_t
+    lib.nerf_active_rows_workspace_bytes.argtypes = [c_i64]
     lib.nerf_quant_packed_bytes.restype = ctypes.c_size_t
     lib.nerf_quant_packed_bytes.argtypes = [c_int, c_int]
     for name, argtypes in SIGNATURES.items():
@@ -202,7 +207,7 @@ def exported_symbols():
     return ["nerf_last_error", "nerf_abi_version", "nerf_hash_bwd_chunk_points", "nerf_tv_bwd_bin_chunks",
             "nerf_hash_encode_bwd_workspace_bytes",
             "nerf_quant_packed_bytes", "nerf_mlp_bwd_det_workspace_bytes", "nerf_priors_workspace_bytes",
-            "nerf_normal_head_bwd_workspace_bytes"] + list(SIGNATURES)
+            "nerf_normal_head_bwd_workspace_bytes", "nerf_active_rows_workspace_bytes"] + list(SIGNATURES)
 
 
 _TIMING = None   # when a list: (name, start_event, end_event) per launch, recorded on the current stream

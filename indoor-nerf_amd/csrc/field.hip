@@ -117,6 +117,9 @@ extern "C" int nerf_mlp_bwd_batch(const nerf_mlp_bwd_job* jobs, int n_jobs, floa
         x.graw = j.graw; x.G = g; x.dfeat = j.dfeat; x.dsh = j.dsh; x.dgeo = j.dgeo;
         x.aq = reinterpret_cast<const QuantRec*>(j.act_qrec);
         x.dfeat_rows = j.dfeat_rows;
+        NERF_REQUIRE(!j.rows == !j.d_count, "mlp_bwd_batch: job %d: rows and d_count go together", k);
+        x.rows = j.rows;
+        x.count = j.d_count;
         if (x.P > 0) ++n;   // empty jobs launch nothing
     }
     if (n == 0) return NERF_OK;

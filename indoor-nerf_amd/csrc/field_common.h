@@ -33,6 +33,8 @@ struct MlpArgs {
     nerf_mlp_grads G;
     float* dfeat;
     const int32_t* dfeat_rows;   // bwd, optional: point p's d feat goes to row dfeat_rows[p] (NULL: p)
+    const int32_t* rows;         // bwd, optional: walk only the points rows[0 .. *count) (active points)
+    const int32_t* count;
     float* dsh;
     float* geo_out;       // fwd, optional: o = [sigma, geo 15] per point, [P,16] (normals head input)
     const float* dgeo;    // bwd, optional: upstream d o from the normals head, [P,16] (row 0 ignored)

@@ -280,6 +280,28 @@ __device__ __forceinline__ void load_in_x6(const MlpArgs& a, int64_t tile, int j
     load_sh6(a, in.pt, in.valid, h, in.shv, 0);
 }
 
+// Backward tiles over the active points only (a.rows, MlpArgs): tile slot idx is point rows[idx]; the
+// number of points is read on the device (graph-capturable: the list is built in the same stream).
+__device__ __forceinline__ int64_t bwd_points(const MlpArgs& a) {
+    return a.rows ? (int64_t)*a.count : a.P;
+}
+
+__device__ __forceinline__ void bwd_point(const MlpArgs& a, int64_t n, int64_t tile, int j, uint32_t& pt, bool& valid) {
+    const int64_t idx = tile * 32 + j;
+    valid = idx < n;
+    if (a.rows) {
+        pt = (uint32_t)a.rows[valid ? idx : n - 1];
+    } else {
+        pt = (uint32_t)idx;
+    }
+}
+
+__device__ __forceinline__ void load_in_x6_bwd(const MlpArgs& a, int64_t n, int64_t tile, int j, int h, InX6& in) {
+    bwd_point(a, n, tile, j, in.pt, in.valid);
+    load_x6(a, in.pt, in.valid, h, in.x, 0);
+    load_sh6(a, in.pt, in.valid, h, in.shv, 0);
+}
+
 struct ActX6 {
     floatx16 h1[2];
     floatx16 o;
@@ -526,11 +548,12 @@ __device__ __forceinline__ void bwd_chain_role(const MlpArgs& a, const __bf16* i
 #endif
     __bf16* const stGb[2] = {stG, stG + 3 * STG_PIECE};
     auto publish = [&]() { flag_set(ready, ++seq); };
-    const int64_t n_tiles = (a.P + 31) / 32;
+    const int64_t n_pts = bwd_points(a);
+    const int64_t n_tiles = (n_pts + 31) / 32;
     for (int64_t tile = (int64_t)blk * 4 + p; tile < n_tiles; tile += (int64_t)nblk * 4) {
         const __bf16* imt = img + opaque_zero();
         InX6 in;
-        load_in_x6(a, tile, j, h, in);
+        load_in_x6_bwd(a, n_pts, tile, j, h, in);
         ActX6 f;
         floatx16 unused;
         fwd_chain<QUANT>(imt, in, f, unused, lane, false, aq);
@@ -777,7 +800,8 @@ __device__ __forceinline__ void bwd_wgrad_role(const MlpArgs& a, const __bf16* i
 #endif
     auto take = [&]() { flag_wait(ready, seq + 1, &waited); };
     auto release = [&]() { flag_set_now(ack, ++seq); };
-    const int64_t n_tiles = (a.P + 31) / 32;
+    const int64_t n_pts = bwd_points(a);
+    const int64_t n_tiles = (n_pts + 31) / 32;
     for (int64_t tile = (int64_t)blk * 4 + p; tile < n_tiles; tile += (int64_t)nblk * 4) {
         {   // 1: dC2
             Ops16 o;
@@ -855,8 +879,10 @@ __device__ __forceinline__ void bwd_wgrad_role(const MlpArgs& a, const __bf16* i
 #pragma unroll
             for (int c = 0; c < 2; ++c) gx = mma6(tr_read(img, IM_PIECE, IM_W0, S32, 32 * t + 16 * c, 0, lane), gb[c], gx);
         }
-        const uint32_t pt = (uint32_t)(tile * 32 + j);
-        if (a.dfeat && tile * 32 + j < a.P) {
+        uint32_t pt;
+        bool pvalid;
+        bwd_point(a, n_pts, tile, j, pt, pvalid);
+        if (a.dfeat && pvalid) {
             // offsets formed per tile (opaque stride): hoisted out of the loop they pin 16 registers
             const uint32_t row = a.dfeat_rows ? (uint32_t)a.dfeat_rows[pt] : pt;
             const uint32_t sl = (uint32_t)a.sl + (uint32_t)opaque_zero(), base = row * (uint32_t)a.sp;

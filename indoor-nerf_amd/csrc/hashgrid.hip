@@ -274,6 +274,7 @@ struct BinRows {
     const float* dfeat2;
     const int32_t* rows2;
     int64_t sp2, sl2;
+    const int32_t* count;   // optional device int: only points p < *count are binned (an active-point list)
 };
 
 // MODE 1: coalesced float atomics (no workspace); 3: binned (default).
@@ -283,6 +284,17 @@ __global__ void __launch_bounds__(THREADS) hash_encode_bwd_kernel(
     const float* __restrict__ dfeat, int64_t sp, int64_t sl, BinRows br) {
     const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int lvl = blockIdx.y;
+    if (br.count) n = min(n, (int64_t)*br.count);
+    if constexpr (MODE == 3) {
+        if ((int64_t)blockIdx.x * blockDim.x >= n) {   // a chunk past the active points: empty segments
+            const int chunk = hp.chunk_base + (int)blockIdx.x;
+            const int n_own = 1 << hp.owner_log2;
+            for (int o = threadIdx.x; o < n_own; o += blockDim.x)
+                hp.bin_seg[((size_t)lvl * n_own + o) * hp.chunk_stride + chunk] = 0u;
+            if (hp.chunk_max && threadIdx.x == 0) hp.chunk_max[(size_t)lvl * hp.chunk_stride + chunk] = 0.f;
+            return;
+        }
+    }
     const bool valid = p < n;
     float x = 0.f, y = 0.f, z = 0.f, gx = 0.f, gy = 0.f;
     if (valid) {
@@ -901,7 +913,8 @@ extern "C" size_t nerf_hash_encode_bwd_workspace_bytes(int n_levels, int log2_T,
     return B.total;
 }
 
-extern "C" int nerf_hash_encode_bwd_bin_rows(const float* d_xyz, const int32_t* d_rows, int64_t n_points,
+extern "C" int nerf_hash_encode_bwd_bin_rows(const float* d_xyz, const int32_t* d_rows, const int32_t* d_count,
+                                             int64_t n_points,
                                              const float* bbox_min3, const float* bbox_max3, const float* level_res,
                                              int n_levels, int log2_T, const float* d_dfeat, int64_t feat_stride_point,
                                              int64_t feat_stride_level, const float* d_dfeat2, const int32_t* d_rows2,
@@ -927,7 +940,7 @@ extern "C" int nerf_hash_encode_bwd_bin_rows(const float* d_xyz, const int32_t* 
     hp.fastdiv = fill_cells(hp.cell, bbox_min3, bbox_max3, level_res, n_levels) ? 1u : 0u;
     hp.chunk_base = (int)chunk_base;
     hp.nchunks = (int)(chunk_base + nch);
-    const BinRows br{d_rows, d_dfeat2, d_rows2, feat2_stride_point, feat2_stride_level};
+    const BinRows br{d_rows, d_dfeat2, d_rows2, feat2_stride_point, feat2_stride_level, d_count};
     hipLaunchKernelGGL((hash_encode_bwd_kernel<3, kChunkPts>), dim3((unsigned)nch, n_levels), dim3(kChunkPts), 0, as_stream(stream),
                        d_xyz, n_points, hp, d_dfeat, feat_stride_point, feat_stride_level, br);
     NERF_CHECK_LAUNCH("hash_encode_bwd_bin");
@@ -940,7 +953,8 @@ extern "C" int nerf_hash_encode_bwd_bin(const float* d_xyz, int64_t n_points, co
                                         int64_t chunk_base, int64_t chunk_capacity, int deterministic,
                                         void* d_workspace, size_t workspace_bytes, void* stream) {
     NERF_REQUIRE(n_points == 0 || d_dfeat, "hash_encode_bwd_bin: null arg");
-    return nerf_hash_encode_bwd_bin_rows(d_xyz, nullptr, n_points, bbox_min3, bbox_max3, level_res, n_levels, log2_T,
+    return nerf_hash_encode_bwd_bin_rows(d_xyz, nullptr, nullptr, n_points, bbox_min3, bbox_max3, level_res, n_levels,
+                                         log2_T,
                                          d_dfeat, feat_stride_point, feat_stride_level, nullptr, nullptr, 0, 0,
                                          chunk_base, chunk_capacity, deterministic, d_workspace, workspace_bytes,
                                          stream);
@@ -1067,7 +1081,7 @@ extern "C" int nerf_hash_encode_bwd(const float* d_xyz, int64_t n_points, const 
     hp.mask = (uint32_t)((1u << log2_T) - 1u);
     hipLaunchKernelGGL((hash_encode_bwd_kernel<1, 256>), dim3(blocks_for(n_points, 256), n_levels), dim3(256), 0,
                        as_stream(stream), d_xyz, n_points, hp, d_dfeat, feat_stride_point, feat_stride_level,
-                       BinRows{nullptr, nullptr, nullptr, 0, 0});
+                       BinRows{nullptr, nullptr, nullptr, 0, 0, nullptr});
     NERF_CHECK_LAUNCH("hash_encode_bwd");
     return NERF_OK;
 }

@@ -242,9 +242,11 @@ class _FieldJob:
         self.reuse = ctx.reuse     # (role, render.CoarseReuse) or None
         self.stream = torch.cuda.current_stream()
 
+    def alloc(self):
+        self.dfeat = torch.empty_like(self.feat) if self.need_tab else None
+
     def mlp_job(self):
         P = self.pts.shape[0]
-        self.dfeat = torch.empty_like(self.feat) if self.need_tab else None
         j = _lib.MlpBwdJob()
         j.feat, j.feat_stride_point, j.feat_stride_level = _lib.ptr(self.feat, "feat"), 2, 2 * P
         j.viewdirs, j.samples_per_ray = _lib.ptr(self.viewdirs, "viewdirs"), self.spr
@@ -258,10 +260,76 @@ class _FieldJob:
         j.act_qrec = _lib.ptr(self.arec, "act_record", allow_none=True)
         if self.need_tab and self.reuse is not None and self.reuse[0] == "fine":
             j.dfeat_rows = _lib.ptr(self.reuse[1].perm, "perm", torch.int32)   # importance-first d feat
+        if getattr(self, "act", None) is not None:
+            j.rows = _lib.ptr(self.act[0], "active_rows", torch.int32)
+            j.d_count = self.count_ptr(0)
         return j
+
+    def find_active(self, jobs):
+        """The active points of this backward (nerf_active_rows: rows whose upstream gradient is not all
+        zero), before its MLP backward: self.act = (rows, first, counts) and j.rows / j.d_count of the
+        MLP job. Feature-gradient rows that a bin reads but the active-point backward does not write are
+        zeroed here: the coarse points' rows of a reuse pair (the merged coarse bin walks every coarse
+        point)."""
+        P = self.pts.shape[0]
+        self.act = None
+        if not _ACTIVE["on"] or P == 0:
+            return
+        role, plan = self.reuse if (self.reuse is not None and self.reuse[1].used) else (None, None)
+        partner = None if plan is None else next(
+            (k for k in jobs if k is not self and k.reuse is not None and k.reuse[1] is plan), None)
+        dev = self.pts.device
+        i32 = dict(device=dev, dtype=torch.int32)
+        rows, counts = torch.empty(P, **i32), torch.empty(2, **i32)
+        first = perm = zero = None
+        n_first = 0
+        if self.need_tab and role == "fine":
+            perm, n_first = plan.perm, plan.R * plan.N
+            first, zero = torch.empty(n_first, **i32), self.dfeat
+        elif self.need_tab and role == "coarse" and partner is not None and partner.need_tab:
+            zero = self.dfeat
+        ws = torch.empty(int(_lib.load().nerf_active_rows_workspace_bytes(P)) // 4, **i32)
+        _lib.call("nerf_active_rows", _lib.ptr(self.g, "grad_raw"), _lib.ptr(self.dgeo, "dgeo", allow_none=True), P,
+                  _lib.ptr(perm, "perm", torch.int32, True), n_first, _lib.ptr(rows, "rows", torch.int32),
+                  _lib.ptr(first, "first", torch.int32, True), _lib.ptr(counts, "counts", torch.int32),
+                  _lib.ptr(zero, "zero_feat", allow_none=True), 2 * P, len(self.tables),
+                  _lib.ptr(ws, "workspace", torch.int32), ws.numel() * 4, _lib.stream())
+        self.act = (rows, first, counts)
+        # the points the bins walk: a reuse pair's coarse bin walks every coarse point (zeroed rows), the
+        # fine one the active importance samples; otherwise the active rows
+        binned = "all" if (role == "coarse" and zero is not None) else ("first" if first is not None else "rows")
+        _LAST_ACTIVE.append((counts, P, binned))
+
+    def count_ptr(self, k):
+        """Device pointer of counts[k] of the active lists."""
+        return _lib.c_vp(self.act[2].data_ptr() + 4 * k)
 
 
 _DETERMINISTIC = {"on": False, "ws": {}}
+_ACTIVE = {"on": True}
+_LAST_ACTIVE = []    # (device counts, points) of the last field backward's jobs (bench.py reports them)
+
+
+def last_active_units():
+    """Of the last field backward (a host sync; None without active lists): the fraction of its points
+    that were active, the points its MLP backward walked and the points its hash bins walked."""
+    if not _LAST_ACTIVE:
+        return None
+    mlp = sum(int(c[0]) for c, _, _ in _LAST_ACTIVE)
+    binned = sum(P if b == "all" else int(c[1]) if b == "first" else int(c[0]) for c, P, b in _LAST_ACTIVE)
+    return {"fraction": mlp / max(1, sum(P for _, P, _ in _LAST_ACTIVE)), "mlp_points": mlp, "hash_points": binned}
+
+
+def set_active_points(enabled=True):
+    """Walk only the active points in the field backward (nerf_active_rows): the MLP backward and the
+    hash bins skip the samples whose raw gradient is all zero (relu(sigma + noise) = 0: no alpha, no
+    weight, no sigma gradient, run_nerf.py:364-386), whose terms in every gradient sum are exactly 0.
+    Off: every point is walked (A/B)."""
+    _ACTIVE["on"] = bool(enabled)
+
+
+def active_points():
+    return _ACTIVE["on"]
 
 
 def set_deterministic(enabled=True):
@@ -297,6 +365,11 @@ def _run_field_jobs(jobs):
     jobs = [j for j in jobs if isinstance(j, _FieldJob)]
     if jobs:
         ws = _det_workspace(jobs[0].pts.device)
+        for j in jobs:
+            j.alloc()
+        _LAST_ACTIVE.clear()
+        for j in jobs:
+            j.find_active(jobs)
         for k in range(0, len(jobs), _lib.MLP_MAX_JOBS):
             part = jobs[k:k + _lib.MLP_MAX_JOBS]
             arr = (_lib.MlpBwdJob * len(part))(*[j.mlp_job() for j in part])
@@ -328,16 +401,23 @@ def _bin_items(j, jobs):
     itself with the fine d feat alone."""
     P = j.pts.shape[0]
     plain = dict(job=j, xyz=j.pts, dfeat=j.dfeat, sl=2 * P, n=P)
+    act = getattr(j, "act", None)
+    # with active lists: the bin walks the active rows only (count on the device)
+    listed = dict(plain, rows=act[0], count=j.count_ptr(0)) if act is not None else plain
     if j.reuse is None or not j.reuse[1].used:
-        return [plain]
+        return [listed]
     role, plan = j.reuse
     partner = next((k for k in jobs if k is not j and k.reuse is not None and k.reuse[1] is plan), None)
     n_imp = plan.R * plan.N    # the fine d feat is in importance-first order: [importance | coarse points]
     if role == "coarse":
         if partner is None:
-            return [plain]
+            return [listed]
+        # every coarse point: its inactive rows were zeroed (find_active), and so were the fine ones
         return [dict(plain, dfeat2=partner.dfeat, dfeat2_row0=n_imp, sl2=2 * partner.pts.shape[0])]
-    out = [dict(plain, xyz=plan.imp_pts, n=n_imp)]
+    if act is not None:   # the active importance samples (positions in the importance-first order)
+        out = [dict(plain, xyz=plan.imp_pts, n=n_imp, rows=act[1], count=j.count_ptr(1))]
+    else:
+        out = [dict(plain, xyz=plan.imp_pts, n=n_imp)]
     if partner is None:
         Pc = plan.R * plan.S
         out.append(dict(job=j, xyz=plan.pts, dfeat=None, sl=2 * Pc, n=Pc, dfeat2=j.dfeat, dfeat2_row0=n_imp, sl2=2 * P))

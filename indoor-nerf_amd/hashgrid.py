@@ -227,17 +227,18 @@ class _PendingBins:
         return base, det
 
     def add(self, xyz, meta, dfeat, sp, sl, grad_tables, queue=True, n=None, rows=None, dfeat2=None, rows2=None,
-            sp2=2, sl2=0, dfeat2_row0=0):
+            sp2=2, sl2=0, dfeat2_row0=0, count=None):
         """Bin n points (default: every row of xyz). rows / dfeat2 / rows2: the row maps of
         nerf_hash_encode_bwd_bin_rows (coarse-feature reuse); dfeat2_row0: dfeat2's rows start at that
-        row of the tensor."""
+        row of the tensor; count: device pointer of the number of listed rows (active points)."""
         d2 = _lib.ptr(dfeat2, "grad_feat2", allow_none=True)
         if d2 is not None:
             d2 = _lib.c_vp(d2.value + 4 * sp2 * int(dfeat2_row0))
         L, log2_T = len(grad_tables), meta["log2_T"]
         P = xyz.shape[0] if n is None else n
         base, det = self._slot(L, log2_T, grad_tables, bin_chunks(P), xyz.device, queue)
-        _lib.call("nerf_hash_encode_bwd_bin_rows", _lib.ptr(xyz, "xyz"), _lib.ptr(rows, "rows", torch.int32, True), P,
+        _lib.call("nerf_hash_encode_bwd_bin_rows", _lib.ptr(xyz, "xyz"), _lib.ptr(rows, "rows", torch.int32, True), count,
+                  P,
                   meta["bmin"], meta["bmax"], meta["res"], L, log2_T, _lib.ptr(dfeat, "grad_feat", allow_none=True), sp,
                   sl, d2, _lib.ptr(rows2, "rows2", torch.int32, True), sp2,
                   sl2, base, self.cap, det, _lib.ptr(self.ws, "workspace", dtype=torch.uint8), self.ws.numel(),
@@ -318,7 +319,7 @@ def hash_encode_bwd(xyz, meta, dfeat, sp, sl, grad_tables, defer=None, queue=Tru
     if defer and P > 0 and int(_lib.load().nerf_hash_encode_bwd_workspace_bytes(L, log2_T, P, det)) > 0:
         pending_bins(xyz.device).add(xyz, meta, dfeat, sp, sl, grad_tables, queue=queue, **rows)
         return
-    if any(rows.get(k) is not None for k in ("rows", "dfeat2")):
+    if any(rows.get(k) is not None for k in ("rows", "dfeat2", "count")):
         raise NotImplementedError("hash_encode_bwd: row maps need the binned path (log2_T <= 19, a deferred pass)")
     materialize_zero(grad_tables)
     ws, nbytes = bwd_workspace(len(grad_tables), meta["log2_T"], xyz.shape[0], xyz.device)

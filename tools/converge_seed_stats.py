@@ -20,7 +20,7 @@ NAMES = ("eval_psnr", "novel_psnr", "train_psnr")
 
 
 def reference_seed_runs():
-    """F19c (the reference) and F19d (the oracle) runs keyed by batch seed."""
+    """F19c (the reference) and F19d (the oracle) runs keyed by batch seed; run["source"] says which."""
     files = [os.path.join(GOLD, "f19c_converge.npz")]
     if not os.path.exists(files[0]):
         files = []
@@ -34,6 +34,7 @@ def reference_seed_runs():
             s = int(s)
             out[s] = {k: z[f"{k}_s{s}"] for k in NAMES}
             out[s]["batch_sum"] = int(z[f"batch_sum_s{s}"])
+            out[s]["source"] = "oracle" if "f19d" in os.path.basename(f) else "reference"
     return out
 
 
@@ -84,12 +85,19 @@ def main():
         t = dk.mean(0) / np.maximum(dk.std(0, ddof=1) / np.sqrt(len(seeds)), 1e-12)
         print(name, "per checkpoint D(t):", " ".join(f"{20 * i}:{m:+.3f}({x:+.1f})" for i, (m, x) in enumerate(zip(dk.mean(0), t))))
     if a.json:
-        out = {name: {"d_db": round(res[name]["D"], 4), "se_db": round(res[name]["se"], 4),
-                      "reference_db": round(res[name]["reference_db"], 3), "hip_db": round(res[name]["hip_db"], 3)}
-               for name in NAMES}
-        out["design"] = (f"F19c/F19d: {len(seeds)} reference runs with their own ray batches (seeds {seeds}) vs "
-                         f"{len(next(iter(hip.values())))} HIP runs replaying each; late-phase (iterations {LATE}-300) "
-                         "mean PSNR difference averaged over seeds")
+        # top level: the reference's own runs (F19c) only; all_seeds adds the oracle's F19d runs
+        rref = paired({s: v for s, v in ref.items() if v["source"] == "reference"}, hip)
+        summ = lambda r: {name: {"d_db": round(r[name]["D"], 4), "se_db": round(r[name]["se"], 4),  # noqa: E731
+                                 "reference_db": round(r[name]["reference_db"], 3), "hip_db": round(r[name]["hip_db"], 3)}
+                          for name in NAMES}
+        out = summ(rref)
+        out["all_seeds"] = summ(res)
+        out["all_seeds"]["note"] = (f"{len(seeds)} seeds: {len(rref['seeds'])} reference runs (F19c) + "
+                                    f"{len(seeds) - len(rref['seeds'])} ORACLE runs (F19d, oracle/nerf_oracle.py on the "
+                                    "GPU box's CPU cores, pinned to the reference by tests/test_oracle_golden.py)")
+        out["design"] = (f"F19c: {len(rref['seeds'])} runs of the REFERENCE with their own ray batches (seeds "
+                         f"{rref['seeds']}) vs {len(next(iter(hip.values())))} HIP runs replaying each; late-phase "
+                         f"(iterations {LATE}-300) mean PSNR difference averaged over seeds")
         if a.commit:
             out["commit"] = a.commit
         json.dump(out, open(a.json, "w"), indent=1)
