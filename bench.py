@@ -213,9 +213,10 @@ def parse():
     ap.add_argument("--deterministic", type=int, default=0,
                     help="1: bitwise-reproducible backward (nerf.set_deterministic: fixed-point hash owner pass, "
                          "ordered MLP weight-gradient reduction)")
-    ap.add_argument("--active-points", type=int, default=1,
+    ap.add_argument("--active-points", type=int, default=0,
                     help="1: the field backward walks only the samples with a nonzero raw gradient "
-                         "(field.set_active_points); 0: every sample (A/B)")
+                         "(field.set_active_points; pays on sparse scenes, not on this synthetic workload); "
+                         "0: every sample")
     ap.add_argument("--coarse-reuse", type=int, default=1,
                     help="1: the fine pass reuses the coarse pass's hash encoding (DESIGN §8.5); 0: re-encode (A/B)")
     ap.add_argument("--mode", default="train", choices=["train", "render"],
@@ -557,8 +558,9 @@ def main():
                             top3=[{k: o[k] for k in ("op", "bound", "ms_per_step", "achieved", "unit", "frac")}
                                   for o in ranked[:3]])
             if d["traffic"] is not None:
-                roofline["traffic_source"] = (os.path.relpath(traffic_file(), ROOT) + ": rocprofv3 FETCH_SIZE x2 (4/8/16-B "
-                                              "per-lane reads count half, 2-B reads are not counted: "
+                roofline["traffic_source"] = (os.path.relpath(traffic_file(), ROOT) + ": rocprofv3 FETCH_SIZE x the "
+                                              "calibrated factor per access pattern (x2 for 4/8/16-B per-lane reads; "
+                                              "x1.56 for the owner pass's 8-B + 2-B entries: "
                                               "profiles/r03a_pmc_calibration.json) + WRITE_SIZE per call, separate "
                                               "PMC passes of this bench, x calls per iteration")
     step_s = elapsed / a.steps

@@ -84,7 +84,7 @@ def _grads(nerf, kw, rays, target, active, reuse, parts):
         torch.cuda.synchronize()
         return [None if p.grad is None else p.grad.detach().clone() for p in _params(kw)]
     finally:
-        nerf.set_active_points(True)
+        nerf.set_active_points(False)
         nerf.set_coarse_reuse(True)
 
 
