@@ -49,7 +49,8 @@ X6_PEAK_TFLOPS = 2500.0 / 6
 #   radam    : per table/MLP element 28 B (read p, g, m, v; write p, m, v)
 OPS = {
     "hash_bwd": dict(calls=("nerf_hash_encode_bwd_bin", "nerf_hash_encode_bwd_bin_rows", "nerf_hash_encode_bwd_owner",
-                            "nerf_hash_encode_bwd_ws", "nerf_hash_encode_bwd"), bound="hbm",
+                            "nerf_hash_encode_bwd_owner_range", "nerf_hash_encode_bwd_ws", "nerf_hash_encode_bwd"),
+                     bound="hbm",
                      per_unit=2 * 16 * 8 * 8 + 12 + 128, unit="bwd_hash_point"),
     # nerf_hash_encode_fwd_rows also copies the coarse features into the fine rows (priced as encoding)
     "hash_fwd": dict(calls=("nerf_hash_encode_fwd", "nerf_hash_encode_fwd_rows"), bound="hbm",
@@ -80,6 +81,7 @@ KERNEL_SYMBOLS = {
     "nerf_hash_encode_bwd_bin_rows": ["nerf::hash_encode_bwd_kernel<3, 512>"],
     "nerf_tv_bwd_bin": ["nerf::tv_bwd_bin_kernel<512>"],
     "nerf_hash_encode_bwd_owner": ["nerf::hash_bwd_owner_kernel<13, 1024, false>"],
+    "nerf_hash_encode_bwd_owner_range": ["nerf::hash_bwd_owner_kernel<13, 1024, false>"],
     "nerf_mlp_fwd": ["nerf::mlp_fwd_x6_kernel<false>"],
     "nerf_mlp_bwd": ["nerf::mlp_bwd_x6cg_kernel<false>"],
     "nerf_mlp_bwd_batch": ["nerf::mlp_bwd_x6cg_kernel<false>"],
