@@ -52,8 +52,7 @@ OPS = {
                             "nerf_hash_encode_bwd_owner_range", "nerf_hash_encode_bwd_ws", "nerf_hash_encode_bwd"),
                      bound="hbm",
                      per_unit=2 * 16 * 8 * 8 + 12 + 128, unit="bwd_hash_point"),
-    # nerf_hash_encode_fwd_rows also copies the coarse features into the fine rows (priced as encoding)
-    "hash_fwd": dict(calls=("nerf_hash_encode_fwd", "nerf_hash_encode_fwd_rows"), bound="hbm",
+    "hash_fwd": dict(calls=("nerf_hash_encode_fwd",), bound="hbm",
                      per_unit=16 * 8 * 8 + 12 + 128 + 1, unit="hash_point"),
     # A-CAQ eval (int-packed tables, configs[4]): 8-bit codes = 2 B per corner entry (two features)
     "hash_fwd_packed": dict(calls=("nerf_hash_encode_fwd_packed",), bound="hbm", per_unit=16 * 8 * 2 + 12 + 128 + 1,
@@ -75,7 +74,6 @@ STEP_RAY_BYTES = 64
 # ABI call -> the kernel symbols it launches (rocprofv3 names), to attach PMC traffic per call
 KERNEL_SYMBOLS = {
     "nerf_hash_encode_fwd": ["nerf::hash_encode_fwd_pair_kernel<false>"],
-    "nerf_hash_encode_fwd_rows": ["nerf::hash_encode_fwd_pair_kernel<false>"],
     "nerf_hash_encode_fwd_packed": ["nerf::hash_encode_fwd_packed_pair_kernel"],
     "nerf_hash_encode_bwd_bin": ["nerf::hash_encode_bwd_kernel<3, 512>"],
     "nerf_hash_encode_bwd_bin_rows": ["nerf::hash_encode_bwd_kernel<3, 512>"],
@@ -90,9 +88,12 @@ KERNEL_SYMBOLS = {
 
 
 def base_name(abi_name):
-    """nerf_mlp_fwd_q -> nerf_mlp_fwd: the _q entry points are the same kernels with optional
-    A-CAQ records (NULL on the unquantized path)."""
-    return abi_name[:-2] if abi_name.endswith("_q") else abi_name
+    """nerf_mlp_fwd_q / nerf_mlp_fwd_ord -> nerf_mlp_fwd: the _q entry points are the same kernels with
+    optional A-CAQ records (NULL on the unquantized path), _ord with an optional point order."""
+    for suffix in ("_q", "_ord"):
+        if abi_name.endswith(suffix):
+            return abi_name[:-len(suffix)]
+    return abi_name
 
 
 def traffic_file():
@@ -533,8 +534,9 @@ def main():
     roofline, ops = None, []
     ns, ni = wl["args"]["N_samples"], wl["args"]["N_importance"]
     points_per_step = R * (ns + (ns + ni if ni else 0))
-    # distinct points the hash encoding handles: the fine pass's row-mapped gather means the reuse ran
-    reused = any(base_name(c) == "nerf_hash_encode_fwd_rows" for c in kernels)
+    # distinct points the hash encoding handles: fewer when the fine pass reused the coarse features
+    from indoor_nerf_amd.render import last_reuse_used
+    reused = bool(kernels) and last_reuse_used()
     units = {"point": points_per_step, "sample": points_per_step,
              "hash_point": R * (ns + ni) if (reused and ni) else points_per_step}
     units["bwd_point"], units["bwd_hash_point"] = units["point"], units["hash_point"]

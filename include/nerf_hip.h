@@ -78,21 +78,6 @@ int nerf_hash_encode_fwd_q(const float* d_xyz, int64_t n_points,
                            float* d_feat, int64_t feat_stride_point, int64_t feat_stride_level,
                            uint8_t* d_keep, void* stream);
 
-/* Row-mapped forward of a render_rays fine pass with the coarse-feature reuse: the
- * fine point set of a ray holds every coarse point bit for bit (run_nerf.py:512-516) and one embedder
- * serves both nets (run_nerf.py:225,275). Point p of the n_points gathered ones is d_xyz row p
- * (contiguous: the importance samples) and writes feature / keep row d_rows[p] (int32); in the same
- * launch the n_copy coarse points' features d_copy_feat (level-major [L][n_copy][2]) and keep flags
- * d_copy_keep are copied to rows d_copy_rows[i] of d_feat / d_keep. Copies need even, 8-B aligned
- * feature pairs. */
-int nerf_hash_encode_fwd_rows(const float* d_xyz, const int32_t* d_rows, int64_t n_points,
-                              const float* bbox_min3, const float* bbox_max3,
-                              const float* level_res, int n_levels, int log2_T,
-                              const float* const* d_tables, const float* d_qrec,
-                              float* d_feat, int64_t feat_stride_point, int64_t feat_stride_level,
-                              uint8_t* d_keep, const float* d_copy_feat, const uint8_t* d_copy_keep,
-                              const int32_t* d_copy_rows, int64_t n_copy, void* stream);
-
 /* d_dtables: host array of n_levels device pointers; gradients are ACCUMULATED (atomic adds). */
 int nerf_hash_encode_bwd(const float* d_xyz, int64_t n_points,
                          const float* bbox_min3, const float* bbox_max3,
@@ -178,16 +163,16 @@ int nerf_hash_bwd_entry_count(int n_levels, int log2_T, int64_t n_chunks, int64_
 /* ---- active points of a field backward -----------------------------------------------------------
  * raw2outputs' autograd (run_nerf.py:364-386) gives every sample with relu(sigma + noise) = 0 an all-
  * zero raw-gradient row, and NeRFSmall's backward is linear in it: such points add nothing to the MLP
- * weight gradients or the hash-table gradients. nerf_active_rows lists, in ascending order, the rows p
- * of d_graw [P,4] (or of d_dgeo [P,16], rows 1..15, when given) that are not all zero: d_rows [P] and
- * d_counts[0]; with d_perm [P], the positions d_perm[p] < n_first of the active rows also go to
- * d_first [n_first] / d_counts[1]. d_zero_feat (optional, level-major, n_levels x 2 floats per row at
- * stride zero_stride_level): the rows d_perm[p] (or p) >= n_first of the INACTIVE points are zeroed
- * (feature-gradient rows a bin reads but the active-point backward does not write). Two launches, no
- * host sync; the workspace is nerf_active_rows_workspace_bytes(P). */
+ * weight gradients or the hash-table gradients. nerf_active_rows lists, in ascending order, the points
+ * p whose row d_graw_rows[p] (NULL: p) of d_graw [P,4] (or of d_dgeo [P,16], rows 1..15, when given)
+ * is not all zero: d_rows [P], d_counts[0]; d_counts[1] = how many of them are < n_first (the list's
+ * prefix). d_zero_feat (optional, level-major, n_levels x 2 floats per row at stride
+ * zero_stride_level): rows p >= n_first of the INACTIVE points are zeroed (feature-gradient rows a bin
+ * reads but the active-point backward does not write). Two launches, no host sync; the workspace is
+ * nerf_active_rows_workspace_bytes(P). */
 size_t nerf_active_rows_workspace_bytes(int64_t n_points);
-int nerf_active_rows(const float* d_graw, const float* d_dgeo, int64_t n_points, const int32_t* d_perm,
-                     int64_t n_first, int32_t* d_rows, int32_t* d_first, int32_t* d_counts,
+int nerf_active_rows(const float* d_graw, const float* d_dgeo, int64_t n_points, const int32_t* d_graw_rows,
+                     int64_t n_first, int32_t* d_rows, int32_t* d_counts,
                      float* d_zero_feat, int64_t zero_stride_level, int n_levels, void* d_workspace,
                      size_t workspace_bytes, void* stream);
 
@@ -252,6 +237,26 @@ int nerf_mlp_fwd_q(const float* d_feat, int64_t feat_stride_point, int64_t feat_
                    const uint8_t* d_keep, int64_t n_points,
                    const nerf_mlp_weights* weights, float* d_raw, float* d_geo,
                    const float* d_act_qrec, uint32_t* d_act_minmax, int64_t act_calib_points, void* stream);
+/* Point order of a fine pass with the coarse-feature reuse: the features are in the
+ * importance-first order of the reuse (rows [0, seg_split): importance sample k of ray r at r*N + k;
+ * then coarse sample i of ray r at seg_split + r*S + i) while raw / geo (fwd) and graw / dgeo / dsh
+ * (bwd) stay in the merged order render_rays composites (run_nerf.py:512-516). Point p's row there is
+ * io_rows[p] (NULL: p; nerf_sample_fine_rows' d_imp_rows followed by its d_coarse_rows); its view
+ * direction is ray p / samples_per_ray below seg_split and (p - seg_split) / spr2 from there on. */
+typedef struct {
+    const int32_t* io_rows;
+    int64_t seg_split;
+    int64_t spr2;
+} nerf_point_order;
+
+/* nerf_mlp_fwd_q in a point order (NULL order: the identity, seg_split = n_points). */
+int nerf_mlp_fwd_ord(const float* d_feat, int64_t feat_stride_point, int64_t feat_stride_level,
+                     const float* d_sh, int64_t sh_stride,
+                     const float* d_viewdirs, int64_t samples_per_ray,
+                     const uint8_t* d_keep, int64_t n_points,
+                     const nerf_mlp_weights* weights, float* d_raw, float* d_geo,
+                     const float* d_act_qrec, uint32_t* d_act_minmax, int64_t act_calib_points,
+                     const nerf_point_order* order, void* stream);
 int nerf_mlp_bwd_q(const float* d_feat, int64_t feat_stride_point, int64_t feat_stride_level,
                    const float* d_sh, int64_t sh_stride,
                    const float* d_viewdirs, int64_t samples_per_ray,
@@ -286,8 +291,8 @@ typedef struct {
     float* dsh;
     const float* dgeo;
     const float* act_qrec;
-    const int32_t* dfeat_rows;   /* optional: point p's d feat is written to row dfeat_rows[p] of dfeat (NULL: p);
-                                    the coarse-feature reuse's importance-first order, nerf_sample_fine_rows d_perm */
+    nerf_point_order order;      /* spr2 == 0 (zero-filled): one segment, rows io_rows (NULL: the identity) */
+    int64_t dfeat_stride_point, dfeat_stride_level;   /* 0: the feature strides */
     const int32_t* rows;         /* optional (with d_count): walk only the points rows[0 .. *d_count) — the active
                                     points of nerf_active_rows; the other points' d feat / d sh are not written */
     const int32_t* d_count;      /* device int: the number of rows */

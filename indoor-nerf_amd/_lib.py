@@ -33,13 +33,18 @@ MLP_MAX_JOBS = 2   # NERF_MLP_MAX_JOBS
 MAX_CHECK = 32     # NERF_MAX_CHECK
 
 
+class PointOrder(ctypes.Structure):
+    """nerf_point_order (include/nerf_hip.h)."""
+    _fields_ = [("io_rows", c_vp), ("seg_split", c_i64), ("spr2", c_i64)]
+
+
 class MlpBwdJob(ctypes.Structure):
     """nerf_mlp_bwd_job (include/nerf_hip.h): the arguments of nerf_mlp_bwd_q for one net."""
     _fields_ = [("feat", c_vp), ("feat_stride_point", c_i64), ("feat_stride_level", c_i64), ("sh", c_vp),
                 ("sh_stride", c_i64), ("viewdirs", c_vp), ("samples_per_ray", c_i64), ("keep", c_vp),
                 ("n_points", c_i64), ("weights", MlpWeights), ("graw", c_vp), ("grads", MlpGrads), ("dfeat", c_vp),
-                ("dsh", c_vp), ("dgeo", c_vp), ("act_qrec", c_vp), ("dfeat_rows", c_vp),
-                ("rows", c_vp), ("d_count", c_vp)]
+                ("dsh", c_vp), ("dgeo", c_vp), ("act_qrec", c_vp), ("order", PointOrder),
+                ("dfeat_stride_point", c_i64), ("dfeat_stride_level", c_i64), ("rows", c_vp), ("d_count", c_vp)]
 
 
 PRIORS_MAX_RAYS = 8192   # NERF_PRIORS_MAX_RAYS
@@ -94,12 +99,9 @@ SIGNATURES = {
                                  c_i64, c_int, c_vp, ctypes.c_size_t, c_vp],
     "nerf_hash_encode_bwd_owner": [c_int, c_int, c_i64, c_i64, ctypes.POINTER(c_vp), c_int, c_vp, ctypes.c_size_t,
                                    c_vp],
-    "nerf_hash_encode_fwd_rows": [c_vp, c_vp, c_i64, c_f32p, c_f32p, c_f32p, c_int, c_int, ctypes.POINTER(c_vp),
-                                  c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp],
     "nerf_hash_encode_bwd_bin_rows": [c_vp, c_vp, c_vp, c_i64, c_f32p, c_f32p, c_f32p, c_int, c_int, c_vp, c_i64,
                                       c_i64, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_int, c_vp, ctypes.c_size_t, c_vp],
-    "nerf_active_rows": [c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_vp, ctypes.c_size_t,
-                         c_vp],
+    "nerf_active_rows": [c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_int, c_vp, ctypes.c_size_t, c_vp],
     "nerf_hash_bwd_entry_count": [c_int, c_int, c_i64, c_i64, c_int, c_vp, ctypes.c_size_t, c_vp, c_vp],
     "nerf_hash_encode_bwd_owner_range": [c_int, c_int, c_int, c_int, c_i64, c_i64, ctypes.POINTER(c_vp), c_int, c_vp,
                                          ctypes.c_size_t, c_vp],
@@ -110,6 +112,8 @@ SIGNATURES = {
                      c_vp, ctypes.POINTER(MlpGrads), c_vp, c_vp, c_vp, c_vp],
     "nerf_mlp_fwd_q": [c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, ctypes.POINTER(MlpWeights),
                        c_vp, c_vp, c_vp, c_vp, c_i64, c_vp],
+    "nerf_mlp_fwd_ord": [c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, ctypes.POINTER(MlpWeights),
+                         c_vp, c_vp, c_vp, c_vp, c_i64, ctypes.POINTER(PointOrder), c_vp],
     "nerf_mlp_bwd_q": [c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, ctypes.POINTER(MlpWeights),
                        c_vp, ctypes.POINTER(MlpGrads), c_vp, c_vp, c_vp, c_vp, c_vp],
     "nerf_count_nonfinite": [ctypes.POINTER(c_vp), ctypes.POINTER(c_i64), c_int, c_vp, c_vp],
@@ -262,6 +266,14 @@ def ptr(t, name="tensor", dtype=torch.float32, allow_none=False):
     if not t.is_contiguous():
         raise ValueError(f"{name}: tensor must be contiguous")
     return c_vp(t.data_ptr())
+
+
+def ptr_at(t, elems, name="tensor", dtype=torch.float32):
+    """ptr(t) advanced by `elems` elements (a row offset inside a contiguous buffer)."""
+    p = ptr(t, name, dtype)
+    if not 0 <= elems <= t.numel():
+        raise ValueError(f"{name}: offset {elems} outside {t.numel()} elements")
+    return c_vp((p.value or 0) + elems * t.element_size())
 
 
 def host_f32(values):

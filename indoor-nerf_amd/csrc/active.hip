@@ -8,7 +8,7 @@
 // without the zero terms.
 //
 // Stable compaction in two launches: (1) per block of kBlockPts points, the number of active points
-// (and of active ones among the first n_first positions of a permutation, below); (2) each block sums
+// (and of active ones among the first n_first points); (2) each block sums
 // the counts of the blocks before it and writes its active indices in ascending order (wave ballots,
 // an LDS scan over the block's waves). Ascending order keeps the samples of a ray adjacent, which the
 // hash bins' run merge relies on, and makes the lists (and so every sum over them) deterministic.
@@ -24,18 +24,18 @@ struct ActiveArgs {
     const float* graw;      // [P, 4]
     const float* dgeo;      // optional [P, 16] (normals head: rows 1..15 are the upstream d geo)
     int64_t P;
-    const int32_t* perm;    // optional [P]: position of row p in another order (importance-first)
-    int64_t n_first;        // positions < n_first are counted in the second list
-    int32_t* rows;          // out [P]: active rows, ascending
-    int32_t* first;         // optional out [n_first]: active positions < n_first, ascending
-    int32_t* counts;        // out [2]: number of rows, of first
+    const int32_t* graw_rows;   // optional [P]: row of point p in graw / dgeo (the reuse's point order)
+    int64_t n_first;        // active points < n_first are counted apart (the list's prefix)
+    int32_t* rows;          // out [P]: active points, ascending
+    int32_t* counts;        // out [2]: number of active points, of those < n_first
     int32_t* block_counts;  // workspace [2][n_blocks]
     // optional: zero the feature-gradient rows the backward will not write but a bin will read —
-    // row perm[p] (or p) of an INACTIVE point p, when that row is >= n_first (all rows without perm)
+    // row p >= n_first of an INACTIVE point p
     float* zero; int64_t zero_sl; int n_levels;
 };
 
 __device__ __forceinline__ bool row_active(const ActiveArgs& a, int64_t p) {
+    if (a.graw_rows) p = a.graw_rows[p];
     const float4 g = *reinterpret_cast<const float4*>(a.graw + 4 * p);
     bool on = g.x != 0.f || g.y != 0.f || g.z != 0.f || g.w != 0.f;
     if (a.dgeo && !on) {
@@ -59,7 +59,7 @@ __global__ void __launch_bounds__(kActThreads) active_count_kernel(ActiveArgs a)
         const int64_t p = base + k * kActThreads + threadIdx.x;
         if (p < a.P && row_active(a, p)) {
             ++n0;
-            if (a.first && a.perm[p] < a.n_first) ++n1;
+            if (p < a.n_first) ++n1;
         }
     }
 #pragma unroll
@@ -104,22 +104,17 @@ __global__ void __launch_bounds__(kActThreads) active_scatter_kernel(ActiveArgs 
     for (int k = 0; k < kActPer; ++k) {
         const int64_t p = pbase + k * kActThreads + threadIdx.x;
         const bool on = p < a.P && row_active(a, p);
-        if (a.zero && p < a.P && !on) {
-            const int64_t r = a.perm ? (int64_t)a.perm[p] : p;
-            if (!a.perm || r >= a.n_first)
-                for (int l = 0; l < a.n_levels; ++l)
-                    *reinterpret_cast<float2*>(a.zero + 2 * r + l * a.zero_sl) = make_float2(0.f, 0.f);
-        }
-        const int32_t pos = (on && a.first) ? a.perm[p] : 0;
-        const bool on1 = on && a.first && pos < a.n_first;
+        if (a.zero && p < a.P && !on && p >= a.n_first)
+            for (int l = 0; l < a.n_levels; ++l)
+                *reinterpret_cast<float2*>(a.zero + 2 * p + l * a.zero_sl) = make_float2(0.f, 0.f);
+        const bool on1 = on && p < a.n_first;
         const uint64_t m0 = __ballot(on), m1 = __ballot(on1);
         const uint64_t below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
         if (lane == 0) { s_cnt[0][w] = __popcll(m0); s_cnt[1][w] = __popcll(m1); }
         __syncthreads();
-        int w0 = base0, w1 = base1;
-        for (int i = 0; i < w; ++i) { w0 += s_cnt[0][i]; w1 += s_cnt[1][i]; }
+        int w0 = base0;
+        for (int i = 0; i < w; ++i) w0 += s_cnt[0][i];
         if (on) a.rows[w0 + __popcll(m0 & below)] = (int32_t)p;
-        if (on1) a.first[w1 + __popcll(m1 & below)] = pos;
         for (int i = 0; i < kActThreads / 64; ++i) { base0 += s_cnt[0][i]; base1 += s_cnt[1][i]; }
         __syncthreads();
     }
@@ -138,15 +133,15 @@ extern "C" size_t nerf_active_rows_workspace_bytes(int64_t n_points) {
     return (size_t)2 * (size_t)std::max<int64_t>(1, (n_points + kBlockPts - 1) / kBlockPts) * sizeof(int32_t);
 }
 
-extern "C" int nerf_active_rows(const float* d_graw, const float* d_dgeo, int64_t n_points, const int32_t* d_perm,
-                                int64_t n_first, int32_t* d_rows, int32_t* d_first, int32_t* d_counts,
+extern "C" int nerf_active_rows(const float* d_graw, const float* d_dgeo, int64_t n_points,
+                                const int32_t* d_graw_rows, int64_t n_first, int32_t* d_rows, int32_t* d_counts,
                                 float* d_zero_feat, int64_t zero_stride_level, int n_levels, void* d_workspace,
                                 size_t workspace_bytes, void* stream) {
     NERF_REQUIRE(n_points >= 0 && n_points <= INT32_MAX, "active_rows: n_points %lld", (long long)n_points);
     NERF_REQUIRE(d_counts && d_workspace && workspace_bytes >= nerf_active_rows_workspace_bytes(n_points),
                  "active_rows: null counts / workspace, or workspace %zu B < %zu B", workspace_bytes,
                  nerf_active_rows_workspace_bytes(n_points));
-    NERF_REQUIRE(!d_first || (d_perm && n_first >= 0), "active_rows: the second list needs perm and n_first");
+    NERF_REQUIRE(n_first >= 0, "active_rows: n_first %lld", (long long)n_first);
     NERF_REQUIRE(!d_zero_feat || (n_levels >= 1 && n_levels <= NERF_MAX_LEVELS && zero_stride_level % 2 == 0 &&
                                   ((uintptr_t)d_zero_feat & 7) == 0),
                  "active_rows: zeroed feature rows need 1..16 levels and 8-B aligned pairs");
@@ -160,7 +155,7 @@ extern "C" int nerf_active_rows(const float* d_graw, const float* d_dgeo, int64_
     NERF_REQUIRE(d_graw && d_rows, "active_rows: null arg");
     NERF_REQUIRE(((uintptr_t)d_graw & 15) == 0 && (!d_dgeo || ((uintptr_t)d_dgeo & 15) == 0),
                  "active_rows: graw / dgeo rows must be 16-B aligned");
-    ActiveArgs a{d_graw, d_dgeo, n_points, d_perm, n_first, d_rows, d_first, d_counts,
+    ActiveArgs a{d_graw, d_dgeo, n_points, d_graw_rows, n_first, d_rows, d_counts,
                  static_cast<int32_t*>(d_workspace), d_zero_feat, zero_stride_level, n_levels};
     const unsigned nb = blocks_for(n_points, kBlockPts);
     hipLaunchKernelGGL(active_count_kernel, dim3(nb), dim3(kActThreads), 0, as_stream(stream), a);

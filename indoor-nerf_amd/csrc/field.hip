@@ -33,6 +33,20 @@ static int fill_args(MlpArgs& a, const float* d_feat, int64_t sp, int64_t sl, co
     NERF_REQUIRE(!d_viewdirs || spr >= 1, "mlp: samples_per_ray must be >= 1");
     a.feat = d_feat; a.sp = sp; a.sl = sl; a.sh = d_sh; a.sh_stride = sh_stride;
     a.viewdirs = d_viewdirs; a.spr = spr; a.keep = d_keep; a.P = n; a.W = *w;
+    a.dsp = sp; a.dsl = sl;
+    a.io_rows = nullptr; a.seg_split = n; a.spr2 = 1;
+    return NERF_OK;
+}
+
+static int fill_order(MlpArgs& a, const nerf_point_order* o) {
+    if (!o) return NERF_OK;
+    a.io_rows = o->io_rows;
+    if (o->spr2 == 0) return NERF_OK;   // one segment (a zero-filled order)
+    NERF_REQUIRE(o->seg_split >= 0 && o->seg_split <= a.P && o->spr2 >= 1,
+                 "mlp: point order: seg_split %lld of %lld points, spr2 %lld", (long long)o->seg_split,
+                 (long long)a.P, (long long)o->spr2);
+    a.seg_split = o->seg_split;
+    a.spr2 = o->spr2;
     return NERF_OK;
 }
 
@@ -48,14 +62,16 @@ extern "C" int nerf_sh4_fwd(const float* d_dirs, int64_t n, float* d_out, void* 
     return NERF_OK;
 }
 
-extern "C" int nerf_mlp_fwd_q(const float* d_feat, int64_t feat_stride_point, int64_t feat_stride_level,
-                              const float* d_sh, int64_t sh_stride, const float* d_viewdirs, int64_t samples_per_ray,
-                              const uint8_t* d_keep, int64_t n_points, const nerf_mlp_weights* weights, float* d_raw,
-                              float* d_geo, const float* d_act_qrec, uint32_t* d_act_minmax, int64_t act_calib_points,
-                              void* stream) {
+extern "C" int nerf_mlp_fwd_ord(const float* d_feat, int64_t feat_stride_point, int64_t feat_stride_level,
+                                const float* d_sh, int64_t sh_stride, const float* d_viewdirs, int64_t samples_per_ray,
+                                const uint8_t* d_keep, int64_t n_points, const nerf_mlp_weights* weights, float* d_raw,
+                                float* d_geo, const float* d_act_qrec, uint32_t* d_act_minmax,
+                                int64_t act_calib_points, const nerf_point_order* order, void* stream) {
     MlpArgs a{};
     int rc = fill_args(a, d_feat, feat_stride_point, feat_stride_level, d_sh, sh_stride, d_viewdirs, samples_per_ray,
                        d_keep, n_points, weights);
+    if (rc) return rc;
+    rc = fill_order(a, order);
     if (rc) return rc;
     NERF_REQUIRE(n_points == 0 || d_raw || d_act_minmax, "mlp_fwd: null output");
     if (n_points == 0) return NERF_OK;
@@ -66,6 +82,16 @@ extern "C" int nerf_mlp_fwd_q(const float* d_feat, int64_t feat_stride_point, in
     a.calib_points = act_calib_points;
     // the calibration-only launch (d_act_minmax) computes layer 0 and its statistics, nothing else
     return a.act_minmax ? launch_mlp_act_minmax_x6(a, as_stream(stream)) : launch_mlp_fwd_x6(a, as_stream(stream));
+}
+
+extern "C" int nerf_mlp_fwd_q(const float* d_feat, int64_t feat_stride_point, int64_t feat_stride_level,
+                              const float* d_sh, int64_t sh_stride, const float* d_viewdirs, int64_t samples_per_ray,
+                              const uint8_t* d_keep, int64_t n_points, const nerf_mlp_weights* weights, float* d_raw,
+                              float* d_geo, const float* d_act_qrec, uint32_t* d_act_minmax, int64_t act_calib_points,
+                              void* stream) {
+    return nerf_mlp_fwd_ord(d_feat, feat_stride_point, feat_stride_level, d_sh, sh_stride, d_viewdirs, samples_per_ray,
+                            d_keep, n_points, weights, d_raw, d_geo, d_act_qrec, d_act_minmax, act_calib_points, nullptr,
+                            stream);
 }
 
 extern "C" int nerf_mlp_fwd(const float* d_feat, int64_t feat_stride_point, int64_t feat_stride_level,
@@ -116,7 +142,12 @@ extern "C" int nerf_mlp_bwd_batch(const nerf_mlp_bwd_job* jobs, int n_jobs, floa
         NERF_REQUIRE((j.n_points == 0 || j.graw) && g.w0 && g.w1 && g.c0 && g.c1 && g.c2, "mlp_bwd_batch: job %d: null gradient pointer", k);
         x.graw = j.graw; x.G = g; x.dfeat = j.dfeat; x.dsh = j.dsh; x.dgeo = j.dgeo;
         x.aq = reinterpret_cast<const QuantRec*>(j.act_qrec);
-        x.dfeat_rows = j.dfeat_rows;
+        rc = fill_order(x, &j.order);
+        if (rc) return rc;
+        if (j.dfeat_stride_level) {
+            x.dsp = j.dfeat_stride_point;
+            x.dsl = j.dfeat_stride_level;
+        }
         NERF_REQUIRE(!j.rows == !j.d_count, "mlp_bwd_batch: job %d: rows and d_count go together", k);
         x.rows = j.rows;
         x.count = j.d_count;

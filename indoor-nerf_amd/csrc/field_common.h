@@ -32,7 +32,11 @@ struct MlpArgs {
     const float* graw;
     nerf_mlp_grads G;
     float* dfeat;
-    const int32_t* dfeat_rows;   // bwd, optional: point p's d feat goes to row dfeat_rows[p] (NULL: p)
+    int64_t dsp, dsl;            // bwd: d feat strides (fill_args: the feature strides)
+    // point order (nerf_point_order): point p's row in raw / geo / graw / dgeo / dsh is io_rows[p] (NULL:
+    // p); its ray is p / spr below seg_split, (p - seg_split) / spr2 from there on
+    const int32_t* io_rows;
+    int64_t seg_split, spr2;
     const int32_t* rows;         // bwd, optional: walk only the points rows[0 .. *count) (active points)
     const int32_t* count;
     float* dsh;

@@ -258,7 +258,8 @@ __device__ __forceinline__ void load_sh6(const MlpArgs& a, uint32_t pt, bool val
     float o[16];
     const uint32_t pc = valid ? pt : (uint32_t)(a.P - 1);
     if (a.viewdirs) {
-        const uint32_t ray = pc / (uint32_t)a.spr * 3u + zero;
+        const uint32_t ray = (pc < (uint32_t)a.seg_split ? pc / (uint32_t)a.spr
+                                                         : (pc - (uint32_t)a.seg_split) / (uint32_t)a.spr2) * 3u + zero;
         sh4_eval(a.viewdirs[ray], a.viewdirs[ray + 1], a.viewdirs[ray + 2], o);
     } else {
 #pragma unroll
@@ -278,6 +279,11 @@ __device__ __forceinline__ void load_in_x6(const MlpArgs& a, int64_t tile, int j
     in.valid = tile * 32 + j < a.P;
     load_x6(a, in.pt, in.valid, h, in.x, 0);
     load_sh6(a, in.pt, in.valid, h, in.shv, 0);
+}
+
+// Row of point pt in raw / geo / graw / dgeo / dsh (MlpArgs point order)
+__device__ __forceinline__ uint32_t io_row(const MlpArgs& a, uint32_t pt) {
+    return a.io_rows ? (uint32_t)a.io_rows[pt] : pt;
 }
 
 // Backward tiles over the active points only (a.rows, MlpArgs): tile slot idx is point rows[idx]; the
@@ -407,13 +413,14 @@ __global__ void __launch_bounds__(512, 2) mlp_fwd_x6_kernel(MlpArgs a) {
         ActX6 f;
         floatx16 rgb;
         fwd_chain<QUANT>(img + opaque_zero(), in, f, rgb, lane, true, aq);
+        const uint32_t orow = in.valid ? io_row(a, in.pt) : 0u;
         if (h == 0 && in.valid) {
             const bool keep = a.keep ? a.keep[in.pt] != 0 : true;
-            *reinterpret_cast<float4*>(a.raw + 4u * in.pt) = make_float4(rgb[0], rgb[1], rgb[2], keep ? f.o[0] : 0.f);
+            *reinterpret_cast<float4*>(a.raw + 4u * orow) = make_float4(rgb[0], rgb[1], rgb[2], keep ? f.o[0] : 0.f);
         }
         if (a.geo_out && in.valid) {
 #pragma unroll
-            for (int r = 0; r < 8; ++r) a.geo_out[16u * in.pt + row_of(r, h)] = f.o[r];
+            for (int r = 0; r < 8; ++r) a.geo_out[16u * orow + row_of(r, h)] = f.o[r];
         }
     }
 }
@@ -558,7 +565,8 @@ __device__ __forceinline__ void bwd_chain_role(const MlpArgs& a, const __bf16* i
         floatx16 unused;
         fwd_chain<QUANT>(imt, in, f, unused, lane, false, aq);
 
-        float4 g4 = *reinterpret_cast<const float4*>(a.graw + 4u * (in.valid ? in.pt : (uint32_t)(a.P - 1)));
+        const uint32_t orow = io_row(a, in.valid ? in.pt : (uint32_t)(a.P - 1));
+        float4 g4 = *reinterpret_cast<const float4*>(a.graw + 4u * orow);
         if (!in.valid) g4 = make_float4(0.f, 0.f, 0.f, 0.f);
         const bool keep = in.valid && (a.keep ? a.keep[in.pt] != 0 : true);
         const float gsig = keep ? g4.w : 0.f;
@@ -612,7 +620,7 @@ __device__ __forceinline__ void bwd_chain_role(const MlpArgs& a, const __bf16* i
 #pragma unroll
             for (int r = 0; r < 8; ++r) {
                 const int row = row_of(r, h);
-                if (row >= 1) go[r] = a.dgeo[16u * in.pt + row];
+                if (row >= 1) go[r] = a.dgeo[16u * orow + row];
             }
         }
 #pragma unroll
@@ -634,7 +642,7 @@ __device__ __forceinline__ void bwd_chain_role(const MlpArgs& a, const __bf16* i
         }
         if (a.dsh && in.valid) {
 #pragma unroll
-            for (int r = 8; r < 16; ++r) a.dsh[16u * in.pt + row_of(r, h) - 16] = go[r];
+            for (int r = 8; r < 16; ++r) a.dsh[16u * orow + row_of(r, h) - 16] = go[r];
         }
 
         // stage 6 (dW1): go, h1 (recomputed from a reload of x: the kernel keeps no state between
@@ -884,8 +892,7 @@ __device__ __forceinline__ void bwd_wgrad_role(const MlpArgs& a, const __bf16* i
         bwd_point(a, n_pts, tile, j, pt, pvalid);
         if (a.dfeat && pvalid) {
             // offsets formed per tile (opaque stride): hoisted out of the loop they pin 16 registers
-            const uint32_t row = a.dfeat_rows ? (uint32_t)a.dfeat_rows[pt] : pt;
-            const uint32_t sl = (uint32_t)a.sl + (uint32_t)opaque_zero(), base = row * (uint32_t)a.sp;
+            const uint32_t sl = (uint32_t)a.dsl + (uint32_t)opaque_zero(), base = pt * (uint32_t)a.dsp;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int fi = row_of(r, h);
@@ -1012,7 +1019,8 @@ __global__ void __launch_bounds__(256) mlp_wgrad_reduce_kernel(const float* __re
 // every element index the kernels form (feat, sh, raw/graw, geo/dgeo/dsh, dfeat) stays below 2^31
 static bool fits_u32(const MlpArgs& a) {
     const int64_t lim = (int64_t)1 << 31;
-    return a.P * a.sp + 16 * a.sl < lim && a.P * a.sh_stride + 16 < lim && 16 * (a.P + 32) < lim;
+    return a.P * a.sp + 16 * a.sl < lim && a.P * a.dsp + 16 * a.dsl < lim && a.P * a.sh_stride + 16 < lim &&
+           16 * (a.P + 32) < lim;
 }
 
 int launch_mlp_fwd_x6(const MlpArgs& a, hipStream_t stream) {

@@ -49,65 +49,18 @@ struct HashGradParams {
 // level): grouping the 6 coarse levels of the lego config took the forward from 121 to 107 us per
 // launch (same box; 3 or 6 levels in flight: 114 / 154 us, the registers cost occupancy).
 
-// Coarse-feature reuse, fused into the fine pass's forward launch: blocks past the
-// gather blocks of each grid row copy that row's level(s) of the coarse pass's features (and, in the
-// row of level 0, the keep flags) of kCopyPts points into their fine rows. The fine point set of a
-// ray holds every coarse point bit for bit (run_nerf.py:512-516 sorts cat(z_vals, z_samples); one
-// embedder serves both nets, run_nerf.py:225,275), so these rows need no gather.
-struct FwdCopy {
-    const float* src;        // coarse features, level-major [L][n][2] (ssp = 2, ssl = 2n)
-    int64_t ssp, ssl;
-    const uint8_t* skeep;
-    const int32_t* rows;     // fine row of coarse point i
-    int64_t n;
-    int gather_blocks;       // blocks [0, gather_blocks) of a grid row gather, the rest copy
-};
-constexpr int kCopyPerThread = 4;
-constexpr int kCopyPts = 256 * kCopyPerThread;
-
-__device__ __forceinline__ void fwd_copy_block(const FwdCopy& cp, int cb, int l0, int nl, float* __restrict__ feat,
-                                               int64_t sp, int64_t sl, uint8_t* __restrict__ keep) {
-    int64_t i[kCopyPerThread], r[kCopyPerThread];
-#pragma unroll
-    for (int k = 0; k < kCopyPerThread; ++k) {
-        i[k] = (int64_t)cb * kCopyPts + k * 256 + threadIdx.x;
-        r[k] = i[k] < cp.n ? (int64_t)cp.rows[i[k]] : -1;
-    }
-    for (int l = l0; l < l0 + nl; ++l) {
-        float2 v[kCopyPerThread];
-#pragma unroll
-        for (int k = 0; k < kCopyPerThread; ++k)
-            if (r[k] >= 0) v[k] = *reinterpret_cast<const float2*>(cp.src + i[k] * cp.ssp + (int64_t)l * cp.ssl);
-#pragma unroll
-        for (int k = 0; k < kCopyPerThread; ++k)
-            if (r[k] >= 0) *reinterpret_cast<float2*>(feat + r[k] * sp + (int64_t)l * sl) = v[k];
-    }
-    if (l0 == 0 && keep) {
-#pragma unroll
-        for (int k = 0; k < kCopyPerThread; ++k)
-            if (r[k] >= 0) keep[r[k]] = cp.skeep[i[k]];
-    }
-}
-
 template <bool QUANT>
 __global__ void __launch_bounds__(256) hash_encode_fwd_pair_kernel(
-    const float* __restrict__ xyz, const int32_t* __restrict__ out_rows, int64_t n, HashParams hp, int group,
+    const float* __restrict__ xyz, int64_t n, HashParams hp, int group,
     float* __restrict__ feat, int64_t sp, int64_t sl, uint8_t* __restrict__ keep,
-    const QuantRec* __restrict__ qrec, FwdCopy cp) {
+    const QuantRec* __restrict__ qrec) {
     const int row = blockIdx.y;
-    if ((int)blockIdx.x >= cp.gather_blocks) {
-        const bool grouped = group > 0 && row == 0;
-        fwd_copy_block(cp, (int)blockIdx.x - cp.gather_blocks, grouped ? 0 : (group > 0 ? group + row - 1 : row),
-                       grouped ? group : 1, feat, sp, sl, keep);
-        return;
-    }
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t p = t >> 1;
     const int xb = (int)(t & 1);
     const bool valid = p < n;
-    const int64_t pc0 = valid ? p : n - 1;            // invalid lanes mirror a valid point (no stores)
-    const float x = xyz[3 * pc0 + 0], y = xyz[3 * pc0 + 1], z = xyz[3 * pc0 + 2];
-    const int64_t pc = out_rows ? (int64_t)out_rows[pc0] : pc0;   // row of the point in feat / keep
+    const int64_t pc = valid ? p : n - 1;             // invalid lanes mirror a valid point (no stores)
+    const float x = xyz[3 * pc + 0], y = xyz[3 * pc + 1], z = xyz[3 * pc + 2];
     const bool fast = hp.fastdiv && __ballot(!fastdiv_point_ok(x, y, z)) == 0ull;   // wave-uniform
     if (group > 0 && row == 0) {
         for (int l0 = 0; l0 < group; l0 += kFwdGroupRound) {
@@ -791,16 +744,16 @@ static bool make_bin_plan(int n_levels, int log2_T, int64_t n_points, BinPlan& B
 
 using namespace nerf;
 
-static int hash_encode_fwd_impl(const float* d_xyz, const int32_t* d_rows, int64_t n_points, const float* bbox_min3,
-                                const float* bbox_max3, const float* level_res, int n_levels, int log2_T,
-                                const float* const* d_tables, const float* d_qrec, float* d_feat,
-                                int64_t feat_stride_point, int64_t feat_stride_level, uint8_t* d_keep, void* stream,
-                                FwdCopy cp = FwdCopy{}) {
+extern "C" int nerf_hash_encode_fwd_q(const float* d_xyz, int64_t n_points, const float* bbox_min3,
+                                      const float* bbox_max3, const float* level_res, int n_levels, int log2_T,
+                                      const float* const* d_tables, const float* d_qrec, float* d_feat,
+                                      int64_t feat_stride_point, int64_t feat_stride_level, uint8_t* d_keep,
+                                      void* stream) {
     NERF_REQUIRE(n_points >= 0, "hash_encode_fwd: n_points < 0");
     NERF_REQUIRE(n_levels >= 1 && n_levels <= NERF_MAX_LEVELS, "hash_encode_fwd: n_levels %d", n_levels);
     NERF_REQUIRE(log2_T >= 1 && log2_T <= 30, "hash_encode_fwd: log2_T %d", log2_T);
     NERF_REQUIRE((n_points == 0 || (d_xyz && d_feat)) && d_tables && level_res && bbox_min3 && bbox_max3, "hash_encode_fwd: null arg");
-    if (n_points == 0 && cp.n == 0) return NERF_OK;
+    if (n_points == 0) return NERF_OK;
     HashParams hp{};
     for (int l = 0; l < n_levels; ++l) {
         NERF_REQUIRE(d_tables[l], "hash_encode_fwd: table %d is null", l);
@@ -820,46 +773,15 @@ static int hash_encode_fwd_impl(const float* d_xyz, const int32_t* d_rows, int64
     }
     if (group < 2) group = 0;
     const int rows = group > 0 ? n_levels - group + 1 : n_levels;
-    cp.gather_blocks = (int)blocks_for(2 * n_points, 256);
-    dim3 grid2(cp.gather_blocks + (unsigned)blocks_for(cp.n, kCopyPts), rows);
+    dim3 grid2((unsigned)blocks_for(2 * n_points, 256), rows);
     if (q)
         hipLaunchKernelGGL(hash_encode_fwd_pair_kernel<true>, grid2, dim3(256), 0, as_stream(stream), d_xyz,
-                           d_rows, n_points, hp, group, d_feat, feat_stride_point, feat_stride_level, d_keep, q, cp);
+                           n_points, hp, group, d_feat, feat_stride_point, feat_stride_level, d_keep, q);
     else
         hipLaunchKernelGGL(hash_encode_fwd_pair_kernel<false>, grid2, dim3(256), 0, as_stream(stream), d_xyz,
-                           d_rows, n_points, hp, group, d_feat, feat_stride_point, feat_stride_level, d_keep, q, cp);
+                           n_points, hp, group, d_feat, feat_stride_point, feat_stride_level, d_keep, q);
     NERF_CHECK_LAUNCH("hash_encode_fwd");
     return NERF_OK;
-}
-
-extern "C" int nerf_hash_encode_fwd_q(const float* d_xyz, int64_t n_points, const float* bbox_min3,
-                                      const float* bbox_max3, const float* level_res, int n_levels, int log2_T,
-                                      const float* const* d_tables, const float* d_qrec, float* d_feat,
-                                      int64_t feat_stride_point, int64_t feat_stride_level, uint8_t* d_keep,
-                                      void* stream) {
-    return hash_encode_fwd_impl(d_xyz, nullptr, n_points, bbox_min3, bbox_max3, level_res, n_levels, log2_T, d_tables,
-                                d_qrec, d_feat, feat_stride_point, feat_stride_level, d_keep, stream);
-}
-
-extern "C" int nerf_hash_encode_fwd_rows(const float* d_xyz, const int32_t* d_rows, int64_t n_points,
-                                         const float* bbox_min3, const float* bbox_max3, const float* level_res,
-                                         int n_levels, int log2_T, const float* const* d_tables, const float* d_qrec,
-                                         float* d_feat, int64_t feat_stride_point, int64_t feat_stride_level,
-                                         uint8_t* d_keep, const float* d_copy_feat, const uint8_t* d_copy_keep,
-                                         const int32_t* d_copy_rows, int64_t n_copy, void* stream) {
-    NERF_REQUIRE(n_points >= 0 && n_copy >= 0, "hash_encode_fwd_rows: n_points %lld n_copy %lld", (long long)n_points,
-                 (long long)n_copy);
-    NERF_REQUIRE(n_points == 0 || d_rows, "hash_encode_fwd_rows: null row map");
-    NERF_REQUIRE(n_copy == 0 || (d_copy_feat && d_copy_rows && d_feat && (!d_keep || d_copy_keep)),
-                 "hash_encode_fwd_rows: null copy arg");
-    NERF_REQUIRE(n_copy == 0 || (feat_stride_point % 2 == 0 && feat_stride_level % 2 == 0 &&
-                                 ((uintptr_t)d_feat & 7) == 0 && ((uintptr_t)d_copy_feat & 7) == 0),
-                 "hash_encode_fwd_rows: copied feature pairs must be 8-B aligned");
-    NERF_REQUIRE(n_copy < ((int64_t)1 << 31) / 2, "hash_encode_fwd_rows: n_copy %lld", (long long)n_copy);
-    FwdCopy cp{};
-    cp.src = d_copy_feat; cp.ssp = 2; cp.ssl = 2 * n_copy; cp.skeep = d_copy_keep; cp.rows = d_copy_rows; cp.n = n_copy;
-    return hash_encode_fwd_impl(d_xyz, d_rows, n_points, bbox_min3, bbox_max3, level_res, n_levels, log2_T, d_tables,
-                                d_qrec, d_feat, feat_stride_point, feat_stride_level, d_keep, stream, cp);
 }
 
 extern "C" int nerf_hash_encode_fwd(const float* d_xyz, int64_t n_points, const float* bbox_min3,

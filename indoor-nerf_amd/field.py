@@ -161,6 +161,14 @@ def _scratch_grads(weights):
     return g
 
 
+def _point_order(order):
+    """nerf_point_order of (io_rows, seg_split, spr2), or None (the identity)."""
+    if order is None:
+        return None
+    rows, split, spr2 = order
+    return _lib.PointOrder(_lib.ptr(rows, "io_rows", torch.int32).value, split, spr2)
+
+
 class FieldFn(torch.autograd.Function):
     """Fused run_network: pts [P,3], viewdirs [R,3] (P = R*S) -> raw [P,4] ([P,7] with normals)."""
 
@@ -173,38 +181,52 @@ class FieldFn(torch.autograd.Function):
         pts = pts.contiguous()
         viewdirs = viewdirs.contiguous()
         P = pts.shape[0]
-        feat = torch.empty(n_tab, P, 2, device=pts.device, dtype=torch.float32)
-        keep = torch.empty(P, device=pts.device, dtype=torch.bool)
-        # coarse-feature reuse (render.CoarseReuse, DESIGN §8.5): plain fp32 tables with a binned backward
-        plain = not embedder.quantization_active() and embedder.binned_backward()
-        ctx.reuse = None
-        if reuse is not None and plain and reuse.matches(embedder, tables, P):
-            # fine pass: gather the importance samples only, copy the coarse points' features
-            embedder.encode_rows(reuse.imp_pts, reuse.imp_rows, feat, 2, 2 * P, keep,
-                                 copy=(reuse.feat, reuse.keep, reuse.coarse_rows))
-            reuse.state = "used"
-            ctx.reuse = ("fine", reuse)
-        else:
-            embedder.encode_into(pts, feat, 2, 2 * P, keep)
-            if reuse is not None and plain and reuse.state == "armed" and P == reuse.R * reuse.S:
-                reuse.record(feat, keep, pts, embedder, tables)
-                ctx.reuse = ("coarse", reuse)
-        raw = torch.empty(P, 4, device=pts.device, dtype=torch.float32)
-        o16 = torch.empty(P, 16, device=pts.device, dtype=torch.float32) if head else None
-        # with the normals head, run_network's mask lands on n_z, not sigma (run_nerf.py:66)
-        keep_arg = None if head else _lib.ptr(keep, "keep", dtype=torch.bool)
-        feat_args = (_lib.ptr(feat, "feat"), 2, 2 * P, None, 0, _lib.ptr(viewdirs, "viewdirs"), samples_per_ray,
-                     keep_arg)
+        dev = pts.device
         # the activation quantizer calibrates on the first netchunk points (run_nerf.py:43-50, :64)
         n_calib = P if netchunk is None else min(P, netchunk)
+        # coarse-feature reuse (render.CoarseReuse, DESIGN §8.5): plain fp32 tables with a binned backward
+        plain = not embedder.quantization_active() and embedder.binned_backward()
+        ctx.reuse = order = None
+        spr = samples_per_ray
+        if (reuse is not None and plain and reuse.matches(embedder, tables, P)
+                and (not net.use_quantization or n_calib >= P)):   # calibration over all points: any order
+            # fine pass: the importance samples are gathered into the head rows of the reuse buffer, whose
+            # tail holds the coarse pass's features; the MLP walks that importance-first order
+            feat, keep, row0 = reuse.feat, reuse.keep, 0
+            embedder.encode_into(reuse.imp_pts.view(-1, 3), feat, 2, 2 * P, keep)
+            order = (reuse.inv, reuse.R * reuse.N, reuse.S)
+            spr = reuse.N
+            reuse.state = "used"
+            ctx.reuse = ("fine", reuse)
+        elif reuse is not None and plain and reuse.state == "armed" and P == reuse.R * reuse.S:
+            feat, keep, row0 = reuse.alloc(n_tab, dev)      # coarse pass: the tail rows of the reuse buffer
+            embedder.encode_into(pts, feat, 2, 2 * feat.shape[1], keep, row0=row0)
+            reuse.record(pts, embedder, tables)
+            ctx.reuse = ("coarse", reuse)
+        else:
+            feat = torch.empty(n_tab, P, 2, device=dev, dtype=torch.float32)
+            keep, row0 = torch.empty(P, device=dev, dtype=torch.bool), 0
+            embedder.encode_into(pts, feat, 2, 2 * P, keep)
+        sl = 2 * feat.shape[1]
+        keep = keep[row0:row0 + P]                   # the MLP's keep flags, in its point order
+        raw = torch.empty(P, 4, device=dev, dtype=torch.float32)
+        o16 = torch.empty(P, 16, device=dev, dtype=torch.float32) if head else None
+        # with the normals head, run_network's mask lands on n_z, not sigma (run_nerf.py:66); the head
+        # runs in the merged order of raw / geo
+        keep_arg = None if head else _lib.ptr(keep, "keep", dtype=torch.bool)
+        if head and order is not None:
+            keep = torch.empty_like(keep).index_put_((order[0].long(),), keep)
+        feat_args = (_lib.ptr_at(feat, 2 * row0, "feat"), 2, sl, None, 0, _lib.ptr(viewdirs, "viewdirs"), spr,
+                     keep_arg)
         w0q, arec = net.quant_state(lambda w0q: _act_calibration(feat_args, P, weights, w0q, n_calib))
-        _lib.call("nerf_mlp_fwd_q", *feat_args, P, _weights_struct(weights, w0q), _lib.ptr(raw, "raw"),
+        _lib.call("nerf_mlp_fwd_ord", *feat_args, P, _weights_struct(weights, w0q), _lib.ptr(raw, "raw"),
                   _lib.ptr(o16, "geo", allow_none=True), _lib.ptr(arec, "act_record", allow_none=True), None, 0,
-                  _lib.stream())
+                  _point_order(order), _lib.stream())
         if head:
             raw = _head_forward(o16, raw, keep, head)
         ctx.save_for_backward(pts, viewdirs, feat, keep, o16, w0q, arec, *params)
-        ctx.spr, ctx.embedder, ctx.n_tab, ctx.n_head = samples_per_ray, embedder, n_tab, len(head)
+        ctx.spr, ctx.embedder, ctx.n_tab, ctx.n_head = spr, embedder, n_tab, len(head)
+        ctx.frow0, ctx.order = row0, order
         ctx.eval_quant = net.use_quantization and not net.training
         ctx.zero_tab_grad = embedder.quantization_active() and not embedder.training
         return raw
@@ -240,15 +262,21 @@ class _FieldJob:
         self.w0q, self.arec, self.weights, self.tables, self.g, self.dgeo = w0q, arec, weights, tables, g, dgeo
         self.spr, self.meta, self.need_w, self.need_tab = ctx.spr, ctx.embedder._meta, need_w, need_tab
         self.reuse = ctx.reuse     # (role, render.CoarseReuse) or None
+        self.frow0, self.order = ctx.frow0, ctx.order   # feature rows from frow0 of feat; the MLP's point order
         self.stream = torch.cuda.current_stream()
 
     def alloc(self):
-        self.dfeat = torch.empty_like(self.feat) if self.need_tab else None
+        P = self.pts.shape[0]
+        self.dfeat = torch.empty(self.feat.shape[0], P, 2, device=self.feat.device) if self.need_tab else None
 
     def mlp_job(self):
         P = self.pts.shape[0]
         j = _lib.MlpBwdJob()
-        j.feat, j.feat_stride_point, j.feat_stride_level = _lib.ptr(self.feat, "feat"), 2, 2 * P
+        j.feat = _lib.ptr_at(self.feat, 2 * self.frow0, "feat")
+        j.feat_stride_point, j.feat_stride_level = 2, 2 * self.feat.shape[1]
+        j.dfeat_stride_point, j.dfeat_stride_level = 2, 2 * P
+        if self.order is not None:
+            j.order = _point_order(self.order)
         j.viewdirs, j.samples_per_ray = _lib.ptr(self.viewdirs, "viewdirs"), self.spr
         j.keep = None if self.head else _lib.ptr(self.keep, "keep", dtype=torch.bool)
         j.n_points = P
@@ -258,19 +286,18 @@ class _FieldJob:
         j.dfeat = _lib.ptr(self.dfeat, "dfeat", allow_none=True)
         j.dgeo = _lib.ptr(self.dgeo, "dgeo", allow_none=True)
         j.act_qrec = _lib.ptr(self.arec, "act_record", allow_none=True)
-        if self.need_tab and self.reuse is not None and self.reuse[0] == "fine":
-            j.dfeat_rows = _lib.ptr(self.reuse[1].perm, "perm", torch.int32)   # importance-first d feat
         if getattr(self, "act", None) is not None:
             j.rows = _lib.ptr(self.act[0], "active_rows", torch.int32)
             j.d_count = self.count_ptr(0)
         return j
 
     def find_active(self, jobs):
-        """The active points of this backward (nerf_active_rows: rows whose upstream gradient is not all
-        zero), before its MLP backward: self.act = (rows, first, counts) and j.rows / j.d_count of the
-        MLP job. Feature-gradient rows that a bin reads but the active-point backward does not write are
-        zeroed here: the coarse points' rows of a reuse pair (the merged coarse bin walks every coarse
-        point)."""
+        """The active points of this backward (nerf_active_rows: points whose upstream gradient row is not
+        all zero), in the MLP's point order, before its MLP backward: self.act = (rows, counts) and
+        j.rows / j.d_count of the MLP job (counts[1]: the active importance samples of a reuse fine pass,
+        the list's prefix). Feature-gradient rows that a bin reads but the active-point backward does not
+        write are zeroed here: the coarse points' rows of a reuse pair (the merged coarse bin walks every
+        coarse point)."""
         P = self.pts.shape[0]
         self.act = None
         if not _ACTIVE["on"] or P == 0:
@@ -281,28 +308,27 @@ class _FieldJob:
         dev = self.pts.device
         i32 = dict(device=dev, dtype=torch.int32)
         rows, counts = torch.empty(P, **i32), torch.empty(2, **i32)
-        first = perm = zero = None
+        graw_rows = zero = None
         n_first = 0
-        if self.need_tab and role == "fine":
-            perm, n_first = plan.perm, plan.R * plan.N
-            first, zero = torch.empty(n_first, **i32), self.dfeat
+        if role == "fine":   # the MLP walks the importance-first order; graw / dgeo are in the merged one
+            graw_rows, n_first = self.order[0], plan.R * plan.N
+            zero = self.dfeat if self.need_tab else None
         elif self.need_tab and role == "coarse" and partner is not None and partner.need_tab:
             zero = self.dfeat
         ws = torch.empty(int(_lib.load().nerf_active_rows_workspace_bytes(P)) // 4, **i32)
         _lib.call("nerf_active_rows", _lib.ptr(self.g, "grad_raw"), _lib.ptr(self.dgeo, "dgeo", allow_none=True), P,
-                  _lib.ptr(perm, "perm", torch.int32, True), n_first, _lib.ptr(rows, "rows", torch.int32),
-                  _lib.ptr(first, "first", torch.int32, True), _lib.ptr(counts, "counts", torch.int32),
-                  _lib.ptr(zero, "zero_feat", allow_none=True), 2 * P, len(self.tables),
-                  _lib.ptr(ws, "workspace", torch.int32), ws.numel() * 4, _lib.stream())
-        self.act = (rows, first, counts)
+                  _lib.ptr(graw_rows, "graw_rows", torch.int32, True), n_first, _lib.ptr(rows, "rows", torch.int32),
+                  _lib.ptr(counts, "counts", torch.int32), _lib.ptr(zero, "zero_feat", allow_none=True), 2 * P,
+                  len(self.tables), _lib.ptr(ws, "workspace", torch.int32), ws.numel() * 4, _lib.stream())
+        self.act = (rows, counts)
         # the points the bins walk: a reuse pair's coarse bin walks every coarse point (zeroed rows), the
         # fine one the active importance samples; otherwise the active rows
-        binned = "all" if (role == "coarse" and zero is not None) else ("first" if first is not None else "rows")
+        binned = "all" if (role == "coarse" and zero is not None) else ("first" if role == "fine" else "rows")
         _LAST_ACTIVE.append((counts, P, binned))
 
     def count_ptr(self, k):
         """Device pointer of counts[k] of the active lists."""
-        return _lib.c_vp(self.act[2].data_ptr() + 4 * k)
+        return _lib.c_vp(self.act[1].data_ptr() + 4 * k)
 
 
 _DETERMINISTIC = {"on": False, "ws": {}}
@@ -396,8 +422,9 @@ def _run_field_jobs(jobs):
 
 def _bin_items(j, jobs):
     """The bin launches of one FieldFn backward (hash_encode_bwd keyword sets). With the coarse-feature
-    reuse (render.CoarseReuse) the fine job bins its importance samples only (row map imp_rows), and
-    the fine d feat of the coarse points' rows is added to the coarse job's own (dfeat2 at coarse_rows):
+    reuse (render.CoarseReuse) the fine job bins its importance samples only (the head rows of its
+    importance-first d feat), and the fine d feat of the coarse points (its tail rows) is added to the
+    coarse job's own (dfeat2):
     each point shared by the two passes is binned once with the sum of both gradients. Without the
     coarse job in this batch (its output was not differentiated), the fine job bins the coarse points
     itself with the fine d feat alone."""
@@ -416,8 +443,8 @@ def _bin_items(j, jobs):
             return [listed]
         # every coarse point: its inactive rows were zeroed (find_active), and so were the fine ones
         return [dict(plain, dfeat2=partner.dfeat, dfeat2_row0=n_imp, sl2=2 * partner.pts.shape[0])]
-    if act is not None:   # the active importance samples (positions in the importance-first order)
-        out = [dict(plain, xyz=plan.imp_pts, n=n_imp, rows=act[1], count=j.count_ptr(1))]
+    if act is not None:   # the active importance samples: the prefix of the active list
+        out = [dict(plain, xyz=plan.imp_pts, n=n_imp, rows=act[0], count=j.count_ptr(1))]
     else:
         out = [dict(plain, xyz=plan.imp_pts, n=n_imp)]
     if partner is None:

@@ -425,43 +425,32 @@ class HashEmbedder(nn.Module):
         st["key"] = key
         return st["buf"], rec
 
-    def encode_into(self, xyz, feat, sp, sl, keep):
+    def encode_into(self, xyz, feat, sp, sl, keep, row0=0):
         """Forward gather into caller-allocated feat/keep on the path this forward needs: plain,
-        fake-quantized (training / STE) or int-packed (eval-mode quantizers)."""
+        fake-quantized (training / STE) or int-packed (eval-mode quantizers). row0: the points land in
+        rows row0 .. row0 + n of feat (level-major, point stride sp, level stride sl) and keep."""
         meta = self._meta
         P = xyz.shape[0]
+        if P > 0 and ((row0 + P - 1) * sp + (self.n_levels - 1) * sl + 2 > feat.numel() or row0 + P > keep.numel()):
+            raise ValueError("encode_into: rows out of the feature / keep buffers")
+        fp = _lib.ptr_at(feat, sp * row0, "feat")
+        kp = _lib.ptr_at(keep, row0, "keep", dtype=torch.bool)
         if self.quantization_active() and not self.training:
             buf, rec = self.packed_tables()
             _lib.call("nerf_hash_encode_fwd_packed", _lib.ptr(xyz, "xyz"), P, meta["bmin"], meta["bmax"], meta["res"],
                       self.n_levels, meta["log2_T"], _lib.ptr(buf, "packed", dtype=torch.uint8),
-                      _lib.ptr(rec, "records"), _lib.ptr(feat, "feat"), sp, sl,
-                      _lib.ptr(keep, "keep", dtype=torch.bool), _lib.stream())
+                      _lib.ptr(rec, "records"), fp, sp, sl, kp, _lib.stream())
             return
         rec = self.level_records(xyz) if self.quantization_active() else None
         _lib.call("nerf_hash_encode_fwd_q", _lib.ptr(xyz, "xyz"), P, meta["bmin"], meta["bmax"], meta["res"],
                   self.n_levels, meta["log2_T"], _lib.ptr_array(self.tables()), _lib.ptr(rec, "records", allow_none=True),
-                  _lib.ptr(feat, "feat"), sp, sl, _lib.ptr(keep, "keep", dtype=torch.bool), _lib.stream())
+                  fp, sp, sl, kp, _lib.stream())
 
     def binned_backward(self):
         """The binned backward exists for these tables (log2_T <= 19, plain and deterministic)."""
         lib = _lib.load()
         return all(int(lib.nerf_hash_encode_bwd_workspace_bytes(self.n_levels, self.log2_hashmap_size, 1, d)) > 0
                    for d in (0, 1))
-
-    def encode_rows(self, xyz, rows, feat, sp, sl, keep, copy=None):
-        """Forward gather of the points of xyz [n, 3] into rows `rows` (int32) of feat / keep (plain
-        fp32 tables; render.CoarseReuse's importance samples); copy = (src [L, m, 2], src_keep [m],
-        src_rows [m]): in the same launch, the level-major features of m more points are copied to rows
-        src_rows (the coarse pass's features into the fine rows)."""
-        meta = self._meta
-        src, src_keep, src_rows = copy if copy is not None else (None, None, None)
-        _lib.call("nerf_hash_encode_fwd_rows", _lib.ptr(xyz.reshape(-1, 3), "xyz"), _lib.ptr(rows, "rows", torch.int32),
-                  rows.numel(), meta["bmin"], meta["bmax"], meta["res"], self.n_levels, meta["log2_T"],
-                  _lib.ptr_array(self.tables()), None, _lib.ptr(feat, "feat"), sp, sl,
-                  _lib.ptr(keep, "keep", dtype=torch.bool), _lib.ptr(src, "copy_feat", allow_none=True),
-                  _lib.ptr(src_keep, "copy_keep", dtype=torch.bool, allow_none=True),
-                  _lib.ptr(src_rows, "copy_rows", torch.int32, True), 0 if src_rows is None else src_rows.numel(),
-                  _lib.stream())
 
     def encode(self, x, layout="point"):
         return HashEncodeFn.apply(x, self, layout, *self.tables())

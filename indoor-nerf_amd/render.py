@@ -199,6 +199,11 @@ def coarse_reuse():
     return _REUSE["on"]
 
 
+def last_reuse_used():
+    """Whether the last render_rays call's fine pass took the coarse features (bench.py's pricing)."""
+    return _REUSE.get("last", False)
+
+
 class CoarseReuse:
     """Hand-over of one render_rays call's coarse hash encoding to its fine pass.
 
@@ -207,22 +212,31 @@ class CoarseReuse:
     embedder (run_nerf.py:225,275), so 64 of a ray's 192 fine points are the coarse points bit for
     bit and, the tables being unchanged inside an iteration, so are their 16-level features.
     render_rays attaches this object to the coarse and then the fine point tensors
-    (`pts._nerf_reuse`); field.FieldFn (the fused run_network) records the coarse features in it and
-    the fine pass gathers only its importance samples and, in the same launch, copies the coarse
-    features into their fine rows (nerf_hash_encode_fwd_rows). The fine MLP backward writes its d feat
-    in importance-first order (perm), so the fine bin reads the importance samples' rows contiguously
-    and the coarse bin adds the coarse points' fine d feat to their coarse d feat
-    (nerf_hash_encode_bwd_bin_rows): each shared point is binned once. Any other network_query_fn
-    ignores the attribute."""
+    (`pts._nerf_reuse`); field.FieldFn (the fused run_network) encodes the coarse points into the tail
+    rows of one feature buffer [L, R*(S+N), 2] laid out in importance-first order (importance sample k
+    of ray r at row r*N + k, then coarse sample i at R*N + r*S + i), and the fine pass gathers only its
+    importance samples, into the head rows: no copy, no scattered writes. The fine MLP walks that order
+    (nerf_point_order: raw / geo / graw / dgeo stay in the merged order at rows inv, = the sampler's
+    importance rows then its coarse rows), so its d feat is importance-first too: the fine bin reads
+    the importance samples' rows contiguously and the coarse bin adds the coarse points' fine d feat
+    (the tail rows) to their coarse d feat (nerf_hash_encode_bwd_bin_rows): each shared point is binned
+    once. Any other network_query_fn ignores the attribute."""
 
     def __init__(self, R, S, N):
         self.R, self.S, self.N = R, S, N
         self.state = "armed"          # -> "recorded" (coarse FieldFn) -> "rows" (sample_fine) -> "used"
         self.feat = self.keep = self.pts = self.embedder = self.versions = None
-        self.coarse_rows = self.imp_rows = self.imp_pts = self.perm = None
+        self.inv = self.imp_pts = None
 
-    def record(self, feat, keep, pts, embedder, tables):
-        self.feat, self.keep, self.pts, self.embedder = feat, keep, pts, embedder
+    def alloc(self, n_levels, device):
+        """The shared feature / keep buffers; returns them and the coarse pass's first row."""
+        P = self.R * (self.S + self.N)
+        self.feat = torch.empty(n_levels, P, 2, device=device, dtype=torch.float32)
+        self.keep = torch.empty(P, device=device, dtype=torch.bool)
+        return self.feat, self.keep, self.R * self.N
+
+    def record(self, pts, embedder, tables):
+        self.pts, self.embedder = pts, embedder
         self.versions = [t._version for t in tables]
         self.state = "recorded"
 
@@ -306,17 +320,17 @@ def render_rays(ray_batch, network_fn, network_query_fn, N_samples, embed_fn=Non
         seed, off, rng = (0, 0, None) if (det or u_imp is not None) else _rng()
         i32 = dict(device=dev, dtype=torch.int32)
         if reuse is not None:
-            reuse.coarse_rows, reuse.imp_rows = torch.empty(R, N_samples, **i32), torch.empty(R, N_importance, **i32)
-            reuse.imp_pts, reuse.perm = torch.empty(R, N_importance, 3, **f), torch.empty(R * M, **i32)
+            # inv = [importance rows | coarse rows]: the merged row of each importance-first position
+            reuse.inv, reuse.imp_pts = torch.empty(R * M, **i32), torch.empty(R, N_importance, 3, **f)
             reuse.state = "rows"
+        inv = None if reuse is None else reuse.inv
         _lib.call("nerf_sample_fine_rows", _lib.ptr(rays, "ray_batch"), C, _lib.ptr(z, "z"),
                   _lib.ptr(weights.detach().contiguous(), "weights"), R, N_samples, N_importance, int(det),
                   _lib.ptr(t_imp, "t", allow_none=True), _lib.ptr(u_imp, "u", allow_none=True), seed, off, rng,
                   _lib.ptr(z_fine, "z_fine"), _lib.ptr(pts_fine, "pts_fine"), _lib.ptr(z_std, "z_std"), None,
-                  _lib.ptr(None if reuse is None else reuse.coarse_rows, "coarse_rows", torch.int32, True),
-                  _lib.ptr(None if reuse is None else reuse.imp_rows, "imp_rows", torch.int32, True),
-                  _lib.ptr(None if reuse is None else reuse.imp_pts, "imp_pts", allow_none=True),
-                  _lib.ptr(None if reuse is None else reuse.perm, "perm", torch.int32, True), _lib.stream())
+                  None if inv is None else _lib.ptr_at(inv, R * N_importance, "coarse_rows", torch.int32),
+                  _lib.ptr(inv, "imp_rows", torch.int32, True),
+                  _lib.ptr(None if reuse is None else reuse.imp_pts, "imp_pts", allow_none=True), None, _lib.stream())
         z, pts = z_fine, pts_fine
         run_fn = network_fn if network_fine is None else network_fine
         if reuse is not None:
@@ -325,6 +339,7 @@ def render_rays(ray_batch, network_fn, network_query_fn, N_samples, embed_fn=Non
         if reuse is not None:
             del pts._nerf_reuse
             reuse.release_forward()
+        _REUSE["last"] = reuse is not None and reuse.used
         outs = raw2outputs(raw, z, rays_d, raw_noise_std, white_bkgd, pytest=pytest, predict_normals=predict_normals)
         rgb_map, disp_map, acc_map, weights, depth_map, sparsity_loss = outs[:6]
         normal_map = outs[6] if predict_normals else None

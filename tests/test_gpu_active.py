@@ -11,41 +11,39 @@ pytestmark = pytest.mark.gpu
 
 
 def test_active_rows_kernel(nerf, gpu):
-    """nerf_active_rows against torch: the nonzero rows in ascending order, the importance-first
-    positions of the active rows below n_first, and the zeroed rows of the inactive points."""
+    """nerf_active_rows against torch: the points whose graw row (through the row map, the reuse's
+    point order) is nonzero, ascending; how many of them are below n_first; the zeroed rows of the
+    inactive points at or above n_first. Also without a row map."""
     from indoor_nerf_amd import _lib
     g = torch.Generator(device=gpu).manual_seed(1)
+    i32 = torch.int32
     for P in (1, 63, 4096, 4097, 100_003):
-        graw = torch.randn(P, 4, device=gpu, generator=g)
-        graw[torch.rand(P, device=gpu, generator=g) < 0.4] = 0.0
-        graw[torch.rand(P, device=gpu, generator=g) < 0.05, 1:] = 0.0   # partly zero rows stay active
-        perm = torch.randperm(P, device=gpu, generator=g).to(torch.int32)
-        n_first = P // 3
-        L = 16
-        zero = torch.full((L, P, 2), 7.0, device=gpu)
-        rows = torch.full((P,), -1, device=gpu, dtype=torch.int32)
-        first = torch.full((max(n_first, 1),), -1, device=gpu, dtype=torch.int32)
-        counts = torch.zeros(2, device=gpu, dtype=torch.int32)
-        ws = torch.empty(int(_lib.load().nerf_active_rows_workspace_bytes(P)) // 4, device=gpu, dtype=torch.int32)
-        i32 = torch.int32
-        _lib.call("nerf_active_rows", _lib.ptr(graw), None, P, _lib.ptr(perm, "perm", i32), n_first,
-                  _lib.ptr(rows, "rows", i32), _lib.ptr(first, "first", i32), _lib.ptr(counts, "counts", i32),
-                  _lib.ptr(zero), 2 * P, L, _lib.ptr(ws, "ws", i32), ws.numel() * 4, _lib.stream())
-        torch.cuda.synchronize()
-        on = (graw != 0).any(-1)
-        want = torch.nonzero(on).flatten().to(i32)
-        assert int(counts[0]) == want.numel()
-        assert torch.equal(rows[:want.numel()], want)
-        pos = perm[want]
-        want1 = pos[pos < n_first]
-        assert int(counts[1]) == want1.numel()
-        assert torch.equal(first[:want1.numel()], want1)
-        # zeroed: rows perm[p] >= n_first of the inactive points; every other row untouched
-        zrow = perm[~on].long()
-        zrow = zrow[zrow >= n_first]
-        expect = torch.full((L, P, 2), 7.0, device=gpu)
-        expect[:, zrow, :] = 0.0
-        assert torch.equal(zero, expect)
+        for mapped in (True, False):
+            graw = torch.randn(P, 4, device=gpu, generator=g)
+            graw[torch.rand(P, device=gpu, generator=g) < 0.4] = 0.0
+            graw[torch.rand(P, device=gpu, generator=g) < 0.05, 1:] = 0.0   # partly zero rows stay active
+            gmap = torch.randperm(P, device=gpu, generator=g).to(i32) if mapped else None
+            n_first = P // 3
+            L = 16
+            zero = torch.full((L, P, 2), 7.0, device=gpu)
+            rows = torch.full((P,), -1, device=gpu, dtype=i32)
+            counts = torch.zeros(2, device=gpu, dtype=i32)
+            ws = torch.empty(int(_lib.load().nerf_active_rows_workspace_bytes(P)) // 4, device=gpu, dtype=i32)
+            _lib.call("nerf_active_rows", _lib.ptr(graw), None, P, _lib.ptr(gmap, "graw_rows", i32, True), n_first,
+                      _lib.ptr(rows, "rows", i32), _lib.ptr(counts, "counts", i32),
+                      _lib.ptr(zero), 2 * P, L, _lib.ptr(ws, "ws", i32), ws.numel() * 4, _lib.stream())
+            torch.cuda.synchronize()
+            on = (graw[gmap.long()] if mapped else graw).ne(0).any(-1)
+            want = torch.nonzero(on).flatten().to(i32)
+            assert int(counts[0]) == want.numel()
+            assert torch.equal(rows[:want.numel()], want)
+            assert int(counts[1]) == int((want < n_first).sum())
+            # zeroed: rows p >= n_first of the inactive points; every other row untouched
+            zrow = torch.nonzero(~on).flatten()
+            zrow = zrow[zrow >= n_first]
+            expect = torch.full((L, P, 2), 7.0, device=gpu)
+            expect[:, zrow, :] = 0.0
+            assert torch.equal(zero, expect)
 
 
 def _scene(nerf, gpu, R=512):
