@@ -839,11 +839,26 @@ __device__ __forceinline__ void bwd_wgrad_role(const MlpArgs& a, const __bf16* i
                 for (int t = 0; t < 2; ++t) g.dC1[t][u] = mma6(A[t], hb, g.dC1[t][u]);
             }
         }
+        {   // 4, 5: dC0 for both ga2 tiles against ONE split of [o ; sh] (staged once, at stage 4)
+            S3 B[2], A[2];
+            take();
 #pragma unroll
-        for (int t = 0; t < 2; ++t) {   // 4, 5: dC0
-            Ops32<1> o;
-            take(); read32<1>(o, stG + t * 3 * STG_PIECE, actF, lane); release();
-            mma32<1>(g.dC0[t], o);
+            for (int c = 0; c < 2; ++c) A[c] = tr_read(stG, STG_PIECE, 0, S32, 16 * c, 0, lane);
+            Raw8 br[2];
+#pragma unroll
+            for (int c = 0; c < 2; ++c) br[c] = act_read32(actF, 16 * c, 0, lane);
+            release();
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                B[c] = split_raw(br[c]);
+                g.dC0[0][0] = mma6(A[c], B[c], g.dC0[0][0]);
+            }
+            take();
+#pragma unroll
+            for (int c = 0; c < 2; ++c) A[c] = tr_read(stG + 3 * STG_PIECE, STG_PIECE, 0, S32, 16 * c, 0, lane);
+            release();
+#pragma unroll
+            for (int c = 0; c < 2; ++c) g.dC0[1][0] = mma6(A[c], B[c], g.dC0[1][0]);
         }
         // 6: dW1, and ga1 = W1^T go masked by layer 0's ReLU (go read in the B layout: lane = point).
         // From here until stage 7 is released both gradient buffers are this wave's (the chain wave
