@@ -97,8 +97,11 @@ struct RaySums {
     float rgb[3], acc, depth_num, depth, disp, wsum, q, Z, ent, nraw[3], nden, nnorm;
 };
 
+// need_rgb / need_depth (wave-uniform): the backward needs neither the colour sums nor, without a
+// depth or disparity gradient, the depth numerator — each skipped sum is one fp64 wave reduction
 template <int K>
-__device__ __forceinline__ RaySums ray_sums(const CompositeArgs& a, const RayState<K>& st, bool need_ent) {
+__device__ __forceinline__ RaySums ray_sums(const CompositeArgs& a, const RayState<K>& st, bool need_ent,
+                                           bool need_rgb = true, bool need_depth = true) {
     double r0 = 0, r1 = 0, r2 = 0, acc = 0, dn = 0, n0 = 0, n1 = 0, n2 = 0;
     const bool normals = a.C >= 7;   // wave-uniform
 #pragma unroll
@@ -114,11 +117,14 @@ __device__ __forceinline__ RaySums ray_sums(const CompositeArgs& a, const RaySta
         n2 += (double)(st.w[q] * st.n[q][2]);
     }
     RaySums s;
-    s.rgb[0] = (float)wave_sum_dpp(r0);
-    s.rgb[1] = (float)wave_sum_dpp(r1);
-    s.rgb[2] = (float)wave_sum_dpp(r2);
+    s.rgb[0] = s.rgb[1] = s.rgb[2] = 0.f;
+    if (need_rgb) {
+        s.rgb[0] = (float)wave_sum_dpp(r0);
+        s.rgb[1] = (float)wave_sum_dpp(r1);
+        s.rgb[2] = (float)wave_sum_dpp(r2);
+    }
     s.acc = (float)wave_sum_dpp(acc);
-    s.depth_num = (float)wave_sum_dpp(dn);
+    s.depth_num = need_depth ? (float)wave_sum_dpp(dn) : 0.f;
     s.depth = s.depth_num / s.acc;
     {
         const float m = (s.depth != s.depth) ? s.depth : fmaxf(1e-10f, s.depth);   // torch.max keeps NaN
@@ -196,7 +202,7 @@ __global__ void __launch_bounds__(256) composite_bwd_kernel(CompositeArgs a) {
     float norm_d;
     ray_forward<K>(a, ray, lane, st, norm_d);
     const bool need_ent = a.g_ent != nullptr && a.g_ent[ray] != 0.f;
-    const RaySums s = ray_sums<K>(a, st, false);
+    const RaySums s = ray_sums<K>(a, st, false, false, a.g_depth != nullptr || a.g_disp != nullptr);
 
     // ---- per-ray upstream gradients
     float gr[3] = {0.f, 0.f, 0.f};
@@ -233,6 +239,7 @@ __global__ void __launch_bounds__(256) composite_bwd_kernel(CompositeArgs a) {
     const float eps = 1.1920928955078125e-07f;
     float gent_w_common = 0.f;     // added to every w_j: gZ + g_Wsum
     float ge = 0.f;
+    float dpk[K];                  // d entropy / d p_j of this lane's samples (used twice)
     if (need_ent) {
         ge = a.g_ent[ray];
         double dot = 0;   // sum_i dp_i * probs_i
@@ -241,8 +248,8 @@ __global__ void __launch_bounds__(256) composite_bwd_kernel(CompositeArgs a) {
             const float p = st.w[q] / s.Z;
             const float cp = fminf(fmaxf(p, eps), 1.0f - eps);
             const float mask = (p >= eps && p <= 1.0f - eps) ? 1.f : 0.f;
-            const float dp = -ge * (logf(cp) + p * mask / cp);
-            dot += (double)(dp * st.w[q]);
+            dpk[q] = -ge * (logf(cp) + p * mask / cp);
+            dot += (double)(dpk[q] * st.w[q]);
         }
         dot = wave_sum_dpp(dot);
         const float pq = s.q / s.Z;
@@ -267,13 +274,7 @@ __global__ void __launch_bounds__(256) composite_bwd_kernel(CompositeArgs a) {
             g += g_acc;
             if (a.g_w) g += a.g_w[ray * a.S + j];
             if (use_depth) g += gN * st.z[q] + gA;
-            if (need_ent) {
-                const float p = st.w[q] / s.Z;
-                const float cp = fminf(fmaxf(p, eps), 1.0f - eps);
-                const float mask = (p >= eps && p <= 1.0f - eps) ? 1.f : 0.f;
-                const float dp = -ge * (logf(cp) + p * mask / cp);
-                g += dp / s.Z + gent_w_common;
-            }
+            if (need_ent) g += dpk[q] / s.Z + gent_w_common;
             if (a.C >= 7) g += gnr[0] * st.n[q][0] + gnr[1] * st.n[q][1] + gnr[2] * st.n[q][2];
         }
         gw[q] = g;

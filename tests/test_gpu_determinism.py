@@ -140,7 +140,9 @@ def test_mlp_bwd_batch_concurrent_streams_bitwise(nerf, gpu):
         g = torch.Generator(device=gpu).manual_seed(seed)
         nets = [nerf.NeRFSmall(2, 64, 15, 3, 64, 32, 16).to(gpu) for _ in range(2)]
         feats = [torch.randn(16, P, 2, device=gpu, generator=g) * 0.3 for P in sizes]
-        vds = [torch.nn.functional.normalize(torch.randn(P // s, 3, device=gpu, generator=g), dim=-1)
+        # ceil(P / spr) rays: 8192 points at 192 samples per ray end in a partial 43rd ray (a floor
+        # here left its points reading past the view directions: garbage, and once a fault)
+        vds = [torch.nn.functional.normalize(torch.randn(-(-P // s), 3, device=gpu, generator=g), dim=-1)
                for P, s in zip(sizes, spr)]
         graws = [torch.randn(P, 4, device=gpu, generator=g) for P in sizes]
         ws = torch.empty(int(lib.nerf_mlp_bwd_det_workspace_bytes()) // 4, device=gpu)
