@@ -79,10 +79,10 @@ __global__ void __launch_bounds__(kLossThreads) train_loss_fwd_kernel(LossArgs a
             }
         }
     }
-    // the four block sums share one barrier: wave sums, then thread 0 adds the waves' partials in
+    // the four block sums share one barrier: wave sums (DPP lane moves), then thread 0 adds the waves' partials in
     // wave order (one barrier instead of two per sum)
     {
-        const double w0 = wave_sum_d(se), w1 = wave_sum_d(se0), w2 = wave_sum_d(ssp), w3 = wave_sum_d(ssp0);
+        const double w0 = wave_sum_dpp(se), w1 = wave_sum_dpp(se0), w2 = wave_sum_dpp(ssp), w3 = wave_sum_dpp(ssp0);
         const int w = threadIdx.x >> 6;
         if ((threadIdx.x & 63) == 0) { s_red4[0][w] = w0; s_red4[1][w] = w1; s_red4[2][w] = w2; s_red4[3][w] = w3; }
         __syncthreads();

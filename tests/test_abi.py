@@ -77,6 +77,10 @@ def test_empty_batches_accept_null_data(nerf):
             lambda: L.call("nerf_hash_encode_fwd", None, n, *bb, 16, 19, tabs, None, 2, 2, None, None),
             lambda: L.call("nerf_hash_encode_bwd", None, n, *bb, 16, 19, None, 2, 2, tabs, None),
             lambda: L.call("nerf_sh4_fwd", None, n, None, None),
+            # A-CAQ: eval-mode int-packed gather and the calibration's corner min/max
+            lambda: L.call("nerf_hash_encode_fwd_packed", None, n, *bb, 16, 19, ctypes.c_void_p(1 << 20),
+                           ctypes.c_void_p(1 << 20), None, 2, 2, None, None),
+            lambda: L.call("nerf_hash_gather_minmax", None, n, *bb, 16, 19, tabs, ctypes.c_void_p(1 << 20), None),
         ]
         for c in calls:
             if ok:
