@@ -536,7 +536,7 @@ def main():
     points_per_step = R * (ns + (ns + ni if ni else 0))
     # distinct points the hash encoding handles: fewer when the fine pass reused the coarse features
     from indoor_nerf_amd.render import last_reuse_used
-    reused = bool(kernels) and last_reuse_used()
+    reused = last_reuse_used()
     units = {"point": points_per_step, "sample": points_per_step,
              "hash_point": R * (ns + ni) if (reused and ni) else points_per_step}
     units["bwd_point"], units["bwd_hash_point"] = units["point"], units["hash_point"]

@@ -218,7 +218,7 @@ __global__ void __launch_bounds__(256) sample_fine_kernel(PdfArgs a) {
     // on how ties are ordered, so this equals the rank sort below, which remains for unsorted coarse
     // depths (callers passing their own z).
     bool coarse_sorted = true;
-    for (int i = lane; i + 1 < S; i += 64) coarse_sorted &= !(zr[i + 1] < zr[i]);
+    for (int i = lane; i + 1 < S; i += 64) coarse_sorted &= !(all_l[i + 1] < all_l[i]);   // the LDS copy: no reload
     int P2 = 1;
     while (P2 < N) P2 <<= 1;
     if (__ballot(!coarse_sorted) == 0ull && S + P2 <= kMaxMerged) {
