@@ -85,6 +85,12 @@ KERNEL_SYMBOLS = {
     "nerf_mlp_bwd_batch": ["nerf::mlp_bwd_x6cg_kernel<false>"],
     "nerf_radam_step": ["nerf::radam_kernel"],
 }
+# calls whose every launch runs ONE of the listed kernels (the coarse pass's K = 1 and the fine pass's
+# K = 3 compositing, one launch each per iteration): per-call traffic = the mean over the kernels
+KERNEL_VARIANTS = {
+    "nerf_composite_fwd": ["nerf::composite_fwd_kernel<1>", "nerf::composite_fwd_kernel<3>"],
+    "nerf_composite_bwd": ["nerf::composite_bwd_kernel<1>", "nerf::composite_bwd_kernel<3>"],
+}
 
 
 def base_name(abi_name):
@@ -110,11 +116,14 @@ def pmc_traffic(abi_name):
     FETCH_SIZE and WRITE_SIZE in separate rocprofv3 passes of this bench), or None."""
     abi_name = base_name(abi_name)
     path = traffic_file()
-    if path is None or abi_name not in KERNEL_SYMBOLS:
+    if path is None or (abi_name not in KERNEL_SYMBOLS and abi_name not in KERNEL_VARIANTS):
         return None
     t = json.load(open(path))
-    parts = [t.get(k, {}).get("traffic_bytes") for k in KERNEL_SYMBOLS[abi_name]]
-    return None if any(p is None for p in parts) else float(sum(parts))
+    syms = KERNEL_SYMBOLS.get(abi_name) or KERNEL_VARIANTS[abi_name]
+    parts = [t.get(k, {}).get("traffic_bytes") for k in syms]
+    if any(p is None for p in parts):
+        return None
+    return float(sum(parts)) / (len(parts) if abi_name in KERNEL_VARIANTS else 1)
 
 
 def gpu_clocks():
