@@ -49,7 +49,8 @@ X6_PEAK_TFLOPS = 2500.0 / 6
 #   radam    : per table/MLP element 28 B (read p, g, m, v; write p, m, v)
 OPS = {
     "hash_bwd": dict(calls=("nerf_hash_encode_bwd_bin", "nerf_hash_encode_bwd_bin_rows", "nerf_hash_encode_bwd_owner",
-                            "nerf_hash_encode_bwd_owner_range", "nerf_hash_encode_bwd_ws", "nerf_hash_encode_bwd"),
+                            "nerf_hash_encode_bwd_owner_range", "nerf_hash_encode_bwd_owner_step",
+                            "nerf_hash_encode_bwd_ws", "nerf_hash_encode_bwd"),
                      bound="hbm",
                      per_unit=2 * 16 * 8 * 8 + 12 + 128, unit="bwd_hash_point"),
     "hash_fwd": dict(calls=("nerf_hash_encode_fwd",), bound="hbm",
@@ -80,6 +81,7 @@ KERNEL_SYMBOLS = {
     "nerf_tv_bwd_bin": ["nerf::tv_bwd_bin_kernel<512>"],
     "nerf_hash_encode_bwd_owner": ["nerf::hash_bwd_owner_kernel<13, 1024, false>"],
     "nerf_hash_encode_bwd_owner_range": ["nerf::hash_bwd_owner_kernel<13, 1024, false>"],
+    "nerf_hash_encode_bwd_owner_step": ["nerf::hash_bwd_owner_kernel<13, 1024, false>"],
     "nerf_mlp_fwd": ["nerf::mlp_fwd_x6_kernel<false>"],
     "nerf_mlp_bwd": ["nerf::mlp_bwd_x6cg_kernel<false>"],
     "nerf_mlp_bwd_batch": ["nerf::mlp_bwd_x6cg_kernel<false>"],
@@ -147,22 +149,25 @@ def gpu_clocks():
     return out or None
 
 
-def op_rooflines(kernels, steps, units, dense_elems, hash_entries=None):
+def op_rooflines(kernels, steps, units, dense_elems, hash_entries=None, fused_elems=0):
     """Per OP (OPS) per iteration: achieved = algorithmic bytes (FLOPs) of the op's units in one
     iteration / the op's summed kernel time in one iteration (HIP events), against the MI355X peak;
     traffic = the committed PMC bytes of the op's kernels per iteration. units: {"point", "sample",
     "hash_point"} counts per iteration. hash_entries: entries the hash backward's bins emitted in one
     iteration (nerf_hash_bwd_entry_count): when they are fewer than 0.1 per point-level the backward
     did not do the priced work (the A-CAQ configuration's zero feature gradients), and the
-    op is reported without a roofline fraction."""
+    op is reported without a roofline fraction. fused_elems: table elements whose RAdam step ran inside
+    the owner pass (hashgrid.fused_table_step): priced in hash_bwd at 24 B each (parameter and both
+    moments read and written; the gradient is stored once either way and not read back), and out of
+    radam's elements."""
     out = []
     for op, d in OPS.items():
         calls = [c for c in kernels if base_name(c) in d["calls"]]
         if not calls:
             continue
         t_step = sum(kernels[c]["total_ms"] for c in calls) * 1e-3 / steps
-        n = dense_elems if d["unit"] == "element" else units[d["unit"]]
-        work = d["per_unit"] * n
+        n = dense_elems - fused_elems if d["unit"] == "element" else units[d["unit"]]
+        work = d["per_unit"] * n + (24 * fused_elems if op == "hash_bwd" else 0)
         traffic = 0.0
         for c in calls:
             tc = pmc_traffic(c)
@@ -184,6 +189,8 @@ def op_rooflines(kernels, steps, units, dense_elems, hash_entries=None):
                               "(csrc/field_x6.hip)"}
         r.update(ms_per_step=round(1e3 * t_step, 4), calls={c: kernels[c]["launches"] // max(1, steps) for c in calls},
                  units_per_step=n, per_unit=d["per_unit"], unit_name=d["unit"])
+        if op == "hash_bwd" and fused_elems:
+            r["fused_table_step_bytes"] = 24 * fused_elems
         if op == "hash_bwd" and hash_entries is not None:
             per_pl = hash_entries / max(1, n * 16)
             r.update(entries_per_step=hash_entries, entries_per_point_level=round(per_pl, 3))
@@ -219,6 +226,8 @@ def parse():
     ap.add_argument("--zero", type=int, default=1,
                     help="N>1: shard the optimizer (reduce-scatter -> RAdam on 1/N -> all-gather, dist.ShardedOptimizer); "
                          "0 = all-reduce + replicated RAdam")
+    ap.add_argument("--fused-table-step", type=int, default=0,
+                    help="1: the tables' RAdam step runs inside the owner pass (one process; hashgrid.fused_table_step)")
     ap.add_argument("--overlap", type=int, default=1,
                     help="N>1 with --zero 1: reduce-scatter the first gradient bucket while the owner pass sums the "
                          "second (dist.ShardedOptimizer(overlap=True)); 0 = one reduce-scatter after the backward")
@@ -436,6 +445,7 @@ def main():
     if a.deterministic:
         nerf.set_deterministic(True)
     nerf.set_coarse_reuse(bool(a.coarse_reuse))
+    nerf.set_fused_table_step(bool(a.fused_table_step))
     nerf.set_active_points(bool(a.active_points))
     kw, kw_test, _, grad_vars, opt = nerf.create_nerf(args, device=dev)
     for d in (kw, kw_test):
@@ -545,6 +555,8 @@ def main():
     points_per_step = R * (ns + (ns + ni if ni else 0))
     # distinct points the hash encoding handles: fewer when the fine pass reused the coarse features
     from indoor_nerf_amd.render import last_reuse_used
+    from indoor_nerf_amd.hashgrid import last_fused_table_step
+    fused_step = last_fused_table_step()
     reused = last_reuse_used()
     units = {"point": points_per_step, "sample": points_per_step,
              "hash_point": R * (ns + ni) if (reused and ni) else points_per_step}
@@ -560,7 +572,9 @@ def main():
             units["bwd_point"] = active["mlp_points"]
             units["bwd_hash_point"] = active["hash_points"]
     if kernels:
-        ops = op_rooflines(kernels, a.steps, units, sum(p.numel() for p in params), hash_entries)
+        from indoor_nerf_amd.hashgrid import last_fused_table_step
+        fused_elems = sum(t.numel() for t in kw["embed_fn"].tables()) if last_fused_table_step() else 0
+        ops = op_rooflines(kernels, a.steps, units, sum(p.numel() for p in params), hash_entries, fused_elems)
         ranked = [o for o in ops if not o.get("degenerate")]
         if ranked:
             # the dominant op: largest kernel time per iteration after grouping (hash bwd = bin + owner)
@@ -608,6 +622,7 @@ def main():
                    "parallelism": f"dp{world}" + ("-zero1" if zero else "") + ("-overlap" if zero and a.overlap else "")},
         "hip_graph": bool(gstep is not None and gstep.captures > 0),
         "coarse_reuse": reused,
+        "fused_table_step": fused_step,
         "active_points": None if active is None else {"fraction": round(active["fraction"], 4),
                                                       "mlp_bwd_points": active["mlp_points"],
                                                       "hash_bwd_points": active["hash_points"]},

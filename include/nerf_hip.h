@@ -153,6 +153,28 @@ int nerf_hash_encode_bwd_owner_range(int n_levels, int level_begin, int level_en
                                      int64_t chunk_capacity, float* const* d_dtables, int deterministic,
                                      void* d_workspace, size_t workspace_bytes, void* stream);
 
+/* The owner pass of levels [level_begin, level_end) with the tables' optimizer step fused into it: after
+ * a block stores its slice's gradient rows (NERF_OWNER_OVERWRITE required: the stored row is then the
+ * whole gradient of the step), it applies RAdam to those rows of d_params[l] / d_exp_avg[l] /
+ * d_exp_avg_sq[l] — the elementwise update of nerf_radam_step, bit for bit, with the segment scalars
+ * below (or, with d_coef, (decay_coef, step_coef, mode) read from device memory: graph replays). The
+ * gradients stay stored (optimizer.step() leaves .grad in place). One launch instead of the owner pass
+ * plus the tables' share of nerf_radam_step (16.8 M of its 16.8 M elements at the lego config): the
+ * gradient is not read back, and the parameter rows stream while the owner blocks sum. NULL step: the
+ * plain owner pass. */
+typedef struct {
+    float* const* d_params;       /* host arrays of n_levels device pointers, [2^log2_T][2] fp32 each */
+    float* const* d_exp_avg;
+    float* const* d_exp_avg_sq;
+    float beta1, beta2, one_minus_beta1, one_minus_beta2, eps, decay_coef, step_coef;
+    int mode;                     /* 0: moments only, 1: SGD-like, 2: adaptive (radam.py:49-79) */
+    const float* d_coef;          /* optional device float[4]: (decay_coef, step_coef, mode, unused) */
+} nerf_radam_table_step;
+int nerf_hash_encode_bwd_owner_step(int n_levels, int level_begin, int level_end, int log2_T, int64_t n_chunks,
+                                    int64_t chunk_capacity, float* const* d_dtables, int deterministic,
+                                    void* d_workspace, size_t workspace_bytes, const nerf_radam_table_step* step,
+                                    void* stream);
+
 /* Entries the bin launches of chunks [0, n_chunks) of a workspace emitted (sum of their segment counts:
  * after the run merge, without zero entries), stored to d_count (device uint64). A measurement for the
  * bench's pricing of the hash backward; same workspace rules as the owner pass. */

@@ -75,6 +75,16 @@ class RAdamSegment(ctypes.Structure):
                 ("mode", c_int)]
 
 
+class RAdamTableStep(ctypes.Structure):
+    """nerf_radam_table_step (include/nerf_hip.h): the tables' optimizer step fused into the owner pass."""
+    _fields_ = [("d_params", ctypes.POINTER(c_vp)), ("d_exp_avg", ctypes.POINTER(c_vp)),
+                ("d_exp_avg_sq", ctypes.POINTER(c_vp)),
+                ("beta1", ctypes.c_float), ("beta2", ctypes.c_float),
+                ("one_minus_beta1", ctypes.c_float), ("one_minus_beta2", ctypes.c_float),
+                ("eps", ctypes.c_float), ("decay_coef", ctypes.c_float), ("step_coef", ctypes.c_float),
+                ("mode", c_int), ("d_coef", c_vp)]
+
+
 class Quantizer(ctypes.Structure):
     _fields_ = [("soft_bits", c_vp), ("range_scale", c_vp), ("v_max", c_vp), ("running_min", c_vp),
                 ("running_max", c_vp), ("min_bits", ctypes.c_float), ("max_bits", ctypes.c_float)]
@@ -103,6 +113,8 @@ SIGNATURES = {
                                       c_i64, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_int, c_vp, ctypes.c_size_t, c_vp],
     "nerf_active_rows": [c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_int, c_vp, ctypes.c_size_t, c_vp],
     "nerf_hash_bwd_entry_count": [c_int, c_int, c_i64, c_i64, c_int, c_vp, ctypes.c_size_t, c_vp, c_vp],
+    "nerf_hash_encode_bwd_owner_step": [c_int, c_int, c_int, c_int, c_i64, c_i64, ctypes.POINTER(c_vp), c_int, c_vp,
+                                        ctypes.c_size_t, ctypes.POINTER(RAdamTableStep), c_vp],
     "nerf_hash_encode_bwd_owner_range": [c_int, c_int, c_int, c_int, c_i64, c_i64, ctypes.POINTER(c_vp), c_int, c_vp,
                                          ctypes.c_size_t, c_vp],
     "nerf_sh4_fwd": [c_vp, c_i64, c_vp, c_vp],

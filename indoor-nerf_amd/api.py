@@ -3,7 +3,7 @@ run_nerf_helpers.py, hash_encoding.py, radam.py, loss.py) backed by libnerfhip."
 from . import _lib
 from .dist import GradArena, ShardedOptimizer, broadcast_params, init_process_group, shard
 from .field import NeRFSmall, active_points, batchify, deterministic, run_network, set_active_points, set_deterministic
-from .hashgrid import HashEmbedder, SHEncoder, level_resolutions
+from .hashgrid import HashEmbedder, SHEncoder, fused_table_step_enabled, level_resolutions, set_fused_table_step
 from .losses import sigma_sparsity_loss, total_variation_all, total_variation_loss, train_loss
 from .model import (acaq_quantizers, acaq_update, create_nerf, make_args, save_checkpoint, structural_overfit_update,
                     train_step)
@@ -27,7 +27,8 @@ __all__ = ["HashEmbedder", "SHEncoder", "NeRFSmall", "RAdam", "run_network", "ba
            "pose_spherical", "load_scannet_data", "ManhattanFrameEstimator", "SemanticPlaneDetector",
            "combine_structural_losses_v2", "manhattan_sdf_loss", "spatial_normal_consistency_loss",
            "structured_planarity_loss", "set_deterministic", "deterministic", "check_numerics", "set_debug",
-           "set_coarse_reuse", "coarse_reuse", "set_active_points", "active_points"]
+           "set_coarse_reuse", "coarse_reuse", "set_active_points", "active_points", "set_fused_table_step",
+           "fused_table_step_enabled"]
 
 
 def load_library():

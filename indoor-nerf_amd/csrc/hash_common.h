@@ -5,6 +5,22 @@
 
 namespace nerf {
 
+// RAdam's elementwise update (radam.py:49-79), in the reference's op order (compiled with
+// -ffp-contract=off); shared by the fused optimizer launch (optim.hip) and the owner pass's fused table
+// step (hashgrid.hip), which therefore update a table element bit for bit alike:
+//   v = v*b2 + ((1-b2)*g)*g            exp_avg_sq.mul_(beta2).addcmul_(1 - beta2, grad, grad)
+//   m = m*b1 + (1-b1)*g                exp_avg.mul_(beta1).add_(1 - beta1, grad)
+//   p = p + (-wd*lr)*p                 weight decay (when wd != 0)
+//   p = p + ((-step*lr)*m)/(sqrt(v)+eps)   addcdiv_ (mode 2), or p + (-step*lr)*m (mode 1)
+__device__ __forceinline__ void radam_elem(const nerf_radam_segment& s, float& p, float g, float& m, float& v) {
+    v = v * s.beta2 + (s.one_minus_beta2 * g) * g;
+    m = m * s.beta1 + s.one_minus_beta1 * g;
+    if (s.mode == 0) return;
+    if (s.decay_coef != 0.f) p = p + s.decay_coef * p;
+    if (s.mode == 2) p = p + (s.step_coef * m) / (sqrtf(v) + s.eps);
+    else p = p + s.step_coef * m;
+}
+
 struct HashParams {
     const float* tables[NERF_MAX_LEVELS];
     float cell[NERF_MAX_LEVELS][3];   // grid_size = (box_max - box_min) / res, fp32 on the host

@@ -41,7 +41,49 @@ struct HashGradParams {
     float* chunk_max;     // deterministic mode: [L][chunk_stride] max |entry| of each chunk, else null
     int overwrite;        // owner pass: store every row (the gradients are logically zero), no loads
     int level0;           // owner pass: first level of the launch's level range (grid rows = its levels)
+    // owner pass, optional: the optimizer step of the tables fused into the flush (overwrite mode):
+    // each row's gradient, once stored, updates the row's parameters and moments (radam_elem)
+    float* st_p[NERF_MAX_LEVELS];
+    float* st_m[NERF_MAX_LEVELS];
+    float* st_v[NERF_MAX_LEVELS];
+    nerf_radam_segment st;   // scalars (pointers unused)
+    const float* st_coef;    // optional device (decay_coef, step_coef, mode, -): graph replays
+    int st_on;
 };
+
+// The fused table step of an owner block: rows [0, S) of the slice at `row0` of level lvl; g(i) gives
+// row i's gradient (as just stored). All loads of a batch of rows are issued before the first update.
+template <int THREADS, int ROWS, typename G>
+__device__ __forceinline__ void owner_table_step(const HashGradParams& hp, int lvl, size_t row0, int S, G g) {
+    nerf_radam_segment s = hp.st;
+    if (hp.st_coef) {
+        s.decay_coef = hp.st_coef[0];
+        s.step_coef = hp.st_coef[1];
+        s.mode = (int)hp.st_coef[2];
+    }
+    float2* P = reinterpret_cast<float2*>(hp.st_p[lvl]) + row0;
+    float2* M = reinterpret_cast<float2*>(hp.st_m[lvl]) + row0;
+    float2* V = reinterpret_cast<float2*>(hp.st_v[lvl]) + row0;
+    for (int b = threadIdx.x; b < S; b += ROWS * THREADS) {
+        float2 p[ROWS], m[ROWS], v[ROWS];
+#pragma unroll
+        for (int k = 0; k < ROWS; ++k) {
+            const int i = b + k * THREADS;
+            if (i < S) { p[k] = P[i]; m[k] = M[i]; v[k] = V[i]; }
+        }
+#pragma unroll
+        for (int k = 0; k < ROWS; ++k) {
+            const int i = b + k * THREADS;
+            if (i >= S) continue;
+            const float2 gi = g(i);
+            radam_elem(s, p[k].x, gi.x, m[k].x, v[k].x);
+            radam_elem(s, p[k].y, gi.y, m[k].y, v[k].y);
+            M[i] = m[k];
+            V[i] = v[k];
+            if (s.mode != 0) P[i] = p[k];
+        }
+    }
+}
 
 // Grouped coarse levels: blockIdx.y == 0 runs levels [0, group) of its points, two levels' gathers
 // in flight at a time; the other rows run one level each (level-major: one table hot in each XCD's
@@ -661,6 +703,10 @@ __global__ void __launch_bounds__(THREADS) hash_bwd_owner_kernel(HashGradParams 
                 dt[i] = make_float2((float)((double)t.x + vx), (float)((double)t.y + vy));
             }
         }
+        if (hp.st_on)   // overwrite mode (the entry point checks): the gradient is the row's stored value
+            owner_table_step<kOwnerThreads, kRows>(hp, lvl, (size_t)o * S, S, [&](int i) {
+                return make_float2((float)fixed(i, 0), (float)fixed(i, 1));
+            });
         return;
     }
     if (hp.overwrite) {   // rows without entries become +0, as after a memset
@@ -668,6 +714,11 @@ __global__ void __launch_bounds__(THREADS) hash_bwd_owner_kernel(HashGradParams 
             const Acc v = s_slice[i];
             dt[i] = make_float2((float)v.x, (float)v.y);
         }
+        if (hp.st_on)
+            owner_table_step<kOwnerThreads, kRows>(hp, lvl, (size_t)o * S, S, [&](int i) {
+                const Acc v = s_slice[i];
+                return make_float2((float)v.x, (float)v.y);
+            });
         return;
     }
     // the row's prior gradient plus the slice's sum: in fp32 (A32, as the reference's accumulating
@@ -926,10 +977,10 @@ extern "C" int nerf_tv_bwd_bin(const float* const* d_tables, int n_levels, int l
     return NERF_OK;
 }
 
-extern "C" int nerf_hash_encode_bwd_owner_range(int n_levels, int level_begin, int level_end, int log2_T,
-                                                int64_t n_chunks, int64_t chunk_capacity, float* const* d_dtables,
-                                                int deterministic, void* d_workspace, size_t workspace_bytes,
-                                                void* stream) {
+extern "C" int nerf_hash_encode_bwd_owner_step(int n_levels, int level_begin, int level_end, int log2_T,
+                                               int64_t n_chunks, int64_t chunk_capacity, float* const* d_dtables,
+                                               int deterministic, void* d_workspace, size_t workspace_bytes,
+                                               const nerf_radam_table_step* step, void* stream) {
     NERF_REQUIRE((deterministic & ~(1 | NERF_OWNER_OVERWRITE)) == 0, "hash_encode_bwd_owner: flags %d", deterministic);
     NERF_REQUIRE(0 <= level_begin && level_begin <= level_end && level_end <= n_levels,
                  "hash_encode_bwd_owner: level range [%d, %d) of %d", level_begin, level_end, n_levels);
@@ -942,6 +993,27 @@ extern "C" int nerf_hash_encode_bwd_owner_range(int n_levels, int level_begin, i
     hp.overwrite = overwrite ? 1 : 0;
     NERF_REQUIRE(n_chunks >= 0 && n_chunks <= chunk_capacity, "hash_encode_bwd_owner: n_chunks %lld of %lld",
                  (long long)n_chunks, (long long)chunk_capacity);
+    if (step) {
+        NERF_REQUIRE(overwrite, "hash_encode_bwd_owner: the fused table step needs NERF_OWNER_OVERWRITE (the "
+                                "stored row is the whole gradient)");
+        NERF_REQUIRE(step->d_params && step->d_exp_avg && step->d_exp_avg_sq && step->mode >= 0 && step->mode <= 2,
+                     "hash_encode_bwd_owner: bad table step");
+        for (int l = level_begin; l < level_end; ++l) {
+            NERF_REQUIRE(step->d_params[l] && step->d_exp_avg[l] && step->d_exp_avg_sq[l] &&
+                             (((uintptr_t)step->d_params[l] | (uintptr_t)step->d_exp_avg[l] |
+                               (uintptr_t)step->d_exp_avg_sq[l]) & 7) == 0,
+                         "hash_encode_bwd_owner: table step level %d: null or unaligned tensor", l);
+            hp.st_p[l] = step->d_params[l];
+            hp.st_m[l] = step->d_exp_avg[l];
+            hp.st_v[l] = step->d_exp_avg_sq[l];
+        }
+        hp.st.beta1 = step->beta1; hp.st.beta2 = step->beta2;
+        hp.st.one_minus_beta1 = step->one_minus_beta1; hp.st.one_minus_beta2 = step->one_minus_beta2;
+        hp.st.eps = step->eps; hp.st.decay_coef = step->decay_coef; hp.st.step_coef = step->step_coef;
+        hp.st.mode = step->mode;
+        hp.st_coef = step->d_coef;
+        hp.st_on = 1;
+    }
     NERF_REQUIRE(d_dtables, "hash_encode_bwd_owner: null grad tables");
     for (int l = 0; l < n_levels; ++l) {
         NERF_REQUIRE(d_dtables[l], "hash_encode_bwd_owner: grad table %d is null", l);
@@ -959,6 +1031,14 @@ extern "C" int nerf_hash_encode_bwd_owner_range(int n_levels, int level_begin, i
                            hp);
     NERF_CHECK_LAUNCH("hash_encode_bwd_owner");
     return NERF_OK;
+}
+
+extern "C" int nerf_hash_encode_bwd_owner_range(int n_levels, int level_begin, int level_end, int log2_T,
+                                                int64_t n_chunks, int64_t chunk_capacity, float* const* d_dtables,
+                                                int deterministic, void* d_workspace, size_t workspace_bytes,
+                                                void* stream) {
+    return nerf_hash_encode_bwd_owner_step(n_levels, level_begin, level_end, log2_T, n_chunks, chunk_capacity,
+                                           d_dtables, deterministic, d_workspace, workspace_bytes, nullptr, stream);
 }
 
 extern "C" int nerf_hash_bwd_entry_count(int n_levels, int log2_T, int64_t n_chunks, int64_t chunk_capacity,

@@ -157,7 +157,8 @@ class GraphedTrainStep:
         g2 = None if single else torch.cuda.CUDAGraph()
         # with an overlapping DP hook the owner pass stays out of graph 1: the hook runs it by level range
         # beside the bucket reduce-scatters (dist.ShardedOptimizer(overlap=True))
-        with torch.cuda.stream(side), hashgrid.hold_owner(dev, holds_owner(self.hook)):
+        with torch.cuda.stream(side), hashgrid.hold_owner(dev, holds_owner(self.hook)), \
+                hashgrid.fused_table_step(dev, self.opt, emb.tables(), enabled=self.hook is None):
             with capturing(sc):
                 with torch.cuda.graph(g1, pool=pool, stream=side):
                     out = forward_backward(self.rays, self.target, self.kw, self.opt, self.args, global_step,

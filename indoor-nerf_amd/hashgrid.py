@@ -159,13 +159,21 @@ class _PendingBins:
         self.tag = self.grads = self.stream = None
         self.hold = False     # hold_owner(): the pass's owner launch is left to the caller (HeldOwner)
         self.held = None
+        self.step_plan = None  # fused_table_step(): (optimizer, tables) whose step the owner pass runs
 
     def flush(self):
         if self.used == 0:
             return
         L, log2_T, _, det = self.tag
         flags = det | (OWNER_OVERWRITE if take_deferred(self.grads) else 0)
-        held = HeldOwner(L, log2_T, self.used, self.cap, self.grads, flags, self.ws)
+        step = None
+        plan = self.step_plan
+        if (plan is not None and not self.hold and (flags & OWNER_OVERWRITE)
+                and [g.data_ptr() for g in self.grads] == [p.grad.data_ptr() for p in plan[1]]):
+            self.step_plan = None          # one owner pass per plan
+            step = plan[0].table_step(plan[1])
+        _FUSED_STEP["last"] = step is not None
+        held = HeldOwner(L, log2_T, self.used, self.cap, self.grads, flags, self.ws, step)
         self.last = (self.tag, self.used, self.cap)
         self.used, self.tag, self.grads = 0, None, None
         if self.hold:
@@ -260,16 +268,17 @@ class HeldOwner:
     bucket once its levels are summed (dist.ShardedOptimizer). `flags` (deterministic, overwrite) were
     fixed when the pass was held."""
 
-    def __init__(self, L, log2_T, used, cap, grads, flags, ws):
+    def __init__(self, L, log2_T, used, cap, grads, flags, ws, step=None):
         self.L, self.log2_T, self.used, self.cap, self.grads = L, log2_T, used, cap, list(grads)
-        self.flags, self.ws = flags, ws
+        self.flags, self.ws, self.step = flags, ws, step
 
     def run(self, level_begin, level_end):
         """Launch the levels [level_begin, level_end) on the CURRENT stream (the caller's: after a replayed
-        graph the capture stream is not ordered behind the replay)."""
-        _lib.call("nerf_hash_encode_bwd_owner_range", self.L, level_begin, level_end, self.log2_T, self.used,
+        graph the capture stream is not ordered behind the replay); with a fused table step
+        (fused_table_step) the tables' optimizer update runs in the same launch."""
+        _lib.call("nerf_hash_encode_bwd_owner_step", self.L, level_begin, level_end, self.log2_T, self.used,
                   self.cap, _lib.ptr_array(self.grads, "grad_tables"), self.flags,
-                  _lib.ptr(self.ws, "workspace", dtype=torch.uint8), self.ws.numel(), _lib.stream())
+                  _lib.ptr(self.ws, "workspace", dtype=torch.uint8), self.ws.numel(), self.step, _lib.stream())
 
 
 class hold_owner:
@@ -288,6 +297,46 @@ class hold_owner:
 
     def __exit__(self, *exc):
         self.pb.hold = self.prev
+        return False
+
+
+_FUSED_STEP = {"on": False}
+
+
+def set_fused_table_step(enabled=True):
+    """Fuse the hash tables' RAdam step into the iteration's owner pass (nerf_hash_encode_bwd_owner_step;
+    on by default): model.train_step / graphs.GraphedTrainStep without a gradient hook (one process)
+    and with the deferred table-gradient zero. Bit-identical to the owner pass + the optimizer's own
+    launch; off = the two launches."""
+    _FUSED_STEP["on"] = bool(enabled)
+
+
+def fused_table_step_enabled():
+    return _FUSED_STEP["on"]
+
+
+def last_fused_table_step():
+    """Whether the last owner pass launched (or captured) ran the tables' optimizer step (bench.py)."""
+    return _FUSED_STEP.get("last", False)
+
+
+class fused_table_step:
+    """Context manager around an iteration's forward + backward: the owner pass of the tables' binned
+    backward also applies `optimizer`'s step to them (RAdam.table_step), and optimizer.step() then
+    skips them. Inactive (a no-op) when disabled, when the optimizer has no table_step, or when the
+    pass is held for a gradient hook (data parallel: the gradients are reduced first)."""
+
+    def __init__(self, device, optimizer, tables, enabled=True):
+        self.pb = pending_bins(device)
+        self.plan = ((optimizer, list(tables)) if (enabled and _FUSED_STEP["on"] and tables
+                                                     and hasattr(optimizer, "table_step")) else None)
+
+    def __enter__(self):
+        self.pb.step_plan = self.plan
+        return self
+
+    def __exit__(self, *exc):
+        self.pb.step_plan = None
         return False
 
 

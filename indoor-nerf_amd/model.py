@@ -318,7 +318,9 @@ def train_step(batch_rays, target_s, render_kwargs_train, optimizer, args, globa
     RAdam step, [post_hook, e.g. the sharded optimizer's parameter all-gather], A-CAQ bit widths,
     lr decay (:1182-1250, :1289-1293). Returns (loss, psnr) as device tensors (no host sync).
     graphs.GraphedTrainStep replays the same iteration from HIP graphs."""
-    with hashgrid.hold_owner(target_s.device, holds_owner(grad_hook)):
+    with hashgrid.hold_owner(target_s.device, holds_owner(grad_hook)), \
+            hashgrid.fused_table_step(target_s.device, optimizer, render_kwargs_train["embed_fn"].tables(),
+                                      enabled=grad_hook is None):
         loss, img_loss, psnr = forward_backward(batch_rays, target_s, render_kwargs_train, optimizer, args,
                                                 global_step, H=H, W=W, K=K, loss_scale_sparsity=loss_scale_sparsity,
                                                 tv_generator=tv_generator, zero_grad=zero_grad,

@@ -33,6 +33,7 @@ class RAdam(Optimizer):
                         buffer=[[None, None, None] for _ in range(10)])
         super().__init__(params, defaults)
         self.shard = None
+        self._fused = set()    # ids of the parameters whose step of this iteration the owner pass ran
 
     def set_shard(self, shard):
         """Data-parallel optimizer sharding (dist.ShardedOptimizer): `shard` maps a parameter to the
@@ -122,6 +123,57 @@ class RAdam(Optimizer):
                     state["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
                 yield group, p
 
+    def table_step(self, tables):
+        """The hash tables' step of this iteration as a nerf_radam_table_step for the owner pass
+        (hashgrid.fused_table_step), or None when it cannot be fused: the tables must share one
+        parameter group and one step count, without data-parallel sharding. Eager: the scalars of the
+        coming step (state['step'] advances in step(), which then skips the tables); under a HIP-graph
+        capture: a device slot that a filler refreshes before every replay (and advances the count)."""
+        from . import graphs
+        if self.shard is not None or not tables:
+            return None
+        group = next((g for g in self.param_groups if any(q is tables[0] for q in g["params"])), None)
+        if group is None or any(not any(q is p for q in group["params"]) for p in tables):
+            return None
+        for p in tables:
+            if p.grad is None or p.dtype != torch.float32 or not p.is_contiguous():
+                return None
+            state = self.state[p]
+            if len(state) == 0:
+                state["step"] = 0
+                state["exp_avg"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+                state["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+        if len({self.state[p]["step"] for p in tables}) != 1:
+            return None
+        beta1, beta2 = group["betas"]
+        s = _lib.RAdamTableStep()
+        keep = [_lib.ptr_array(list(tables), "tables"),
+                _lib.ptr_array([self.state[p]["exp_avg"] for p in tables], "exp_avg"),
+                _lib.ptr_array([self.state[p]["exp_avg_sq"] for p in tables], "exp_avg_sq")]
+        s.d_params, s.d_exp_avg, s.d_exp_avg_sq = keep
+        s.beta1, s.beta2, s.one_minus_beta1, s.one_minus_beta2 = beta1, beta2, 1 - beta1, 1 - beta2
+        s.eps = group["eps"]
+        sc = graphs.active()
+        if sc is None:
+            n_sma, step_size = self._scalars(group, self.state[tables[0]]["step"] + 1)
+            mode = 2 if n_sma >= 5 else (1 if step_size > 0 else 0)
+            s.decay_coef, s.step_coef = self._coefs(group, mode, step_size)
+            s.mode, s.d_coef = mode, None
+        else:
+            off, dptr = sc.alloc_f32(4)
+            s.decay_coef = s.step_coef = 0.0
+            s.mode, s.d_coef = 2, dptr
+
+            def fill(hi, hf, off=off, group=group, tables=tuple(tables)):
+                for p in tables:
+                    mode, step_size = self._advance(group, p)
+                dc, stc = self._coefs(group, mode, step_size)
+                hf[off:off + 4] = (dc, stc, float(mode), 0.0)
+            sc.add_filler(fill)
+        self._fused = {id(p) for p in tables}
+        s._keep = keep      # the pointer arrays live as long as the struct
+        return s
+
     @torch.no_grad()
     def step(self, closure=None):
         loss = None
@@ -134,7 +186,12 @@ class RAdam(Optimizer):
             self._capture_step(sc)
             return loss
         segs, updated = [], []
+        fused, self._fused = self._fused, set()
         for group, p in self._params():
+            if id(p) in fused:     # updated by the owner pass (table_step): the step count only
+                self._advance(group, p)
+                torch.autograd.graph.increment_version(p)
+                continue
             mode, step_size = self._advance(group, p)
             rng = self._range(p)
             if rng is None:
@@ -155,7 +212,8 @@ class RAdam(Optimizer):
         """Captured in a HIP graph (graphs.GraphedTrainStep): the launch reads (decay_coef,
         step_coef, mode) of each tensor from device slots that a filler computes before every
         replay with the same host algebra (state['step'] advances there, not at capture)."""
-        every = list(self._params())
+        fused, self._fused = self._fused, set()
+        every = [(g, p) for g, p in self._params() if id(p) not in fused]   # the owner pass's (table_step)
         pairs = [(g, p) for g, p in every if self._range(p) is not None]
         others = [(g, p) for g, p in every if self._range(p) is None]
         if others:
