@@ -93,9 +93,10 @@ def _train_pass(nerf, kw, rays, target, reuse, parts):
         nerf.set_coarse_reuse(True)
 
 
+@pytest.mark.parametrize("R", [512, 4096])
 @pytest.mark.parametrize("parts", [("rgb_map", "rgb0"), ("rgb_map",), ("rgb0",)],
                          ids=["both_passes", "fine_only", "coarse_only"])
-def test_coarse_reuse_matches_reencoding(nerf, gpu, parts):
+def test_coarse_reuse_matches_reencoding(nerf, gpu, parts, R):
     """Reuse on vs off on the same draws (deterministic mode, so the MLP weight gradients are summed in
     a fixed order): every render output bit-identical; MLP gradients within 1e-6 in norm (the fine
     net's points are walked in the reuse's importance-first order, so its tiles hold other points and
@@ -103,7 +104,7 @@ def test_coarse_reuse_matches_reencoding(nerf, gpu, parts):
     within 1e-5 of the level's largest |gradient| (the shared points' fine and coarse d feat are summed
     in fp32 before the bin instead of binned as two entries). fine_only: the coarse pass is not
     differentiated, so the fine job bins the coarse points itself; coarse_only: no fine backward."""
-    kw, rays, target = _scene(nerf, gpu)
+    kw, rays, target = _scene(nerf, gpu, R=R)     # 4096: the bench's batch (786,432 fine points)
     nerf.set_deterministic(True)
     try:
         out_a, g_a = _train_pass(nerf, kw, rays, target, True, parts)

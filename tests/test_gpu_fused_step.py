@@ -33,6 +33,7 @@ def _run(nerf, gpu, fused, graphed, steps, R=1024):
     arena = nerf.GradArena(params, defer_tables=True)     # the owner pass stores the tables' gradients
     nerf.manual_seed(99)
     tv_gen = torch.Generator().manual_seed(7)
+    prev = hashgrid.fused_table_step_enabled()
     hashgrid.set_fused_table_step(fused)
     try:
         if graphed:
@@ -44,7 +45,7 @@ def _run(nerf, gpu, fused, graphed, steps, R=1024):
                 nerf.train_step(rays, target, kw, opt, args, it, tv_generator=tv_gen, zero_grad=arena.zero_)
         torch.cuda.synchronize()
     finally:
-        hashgrid.set_fused_table_step(True)
+        hashgrid.set_fused_table_step(prev)
     tabs = kw["embed_fn"].tables()
     state = [(opt.state[p]["step"], opt.state[p]["exp_avg"].clone(), opt.state[p]["exp_avg_sq"].clone()) for p in tabs]
     return [p.detach().clone() for p in params], [p.grad.clone() for p in tabs], state, p0
