@@ -223,23 +223,61 @@ __global__ void __launch_bounds__(256) sample_fine_kernel(PdfArgs a) {
     while (P2 < N) P2 <<= 1;
     if (__ballot(!coarse_sorted) == 0ull && S + P2 <= kMaxMerged) {
         float* f = all_l + S;
-        for (int i = N + lane; i < P2; i += 64) f[i] = INFINITY;
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        for (int k = 2; k <= P2; k <<= 1) {
-            for (int j = k >> 1; j > 0; j >>= 1) {
-                for (int i = lane; i < P2; i += 64) {
-                    const int l = i ^ j;
-                    if (l > i) {
-                        const float x = f[i], y = f[l];
-                        const bool up = (i & k) == 0;
-                        if (up ? (y < x) : (x < y)) { f[i] = y; f[l] = x; }
+        if (P2 <= 128) {
+            // in registers: element e = lane + 64 h (h < P2 / 64; below 64 elements the lanes past P2 hold
+            // +inf); partners across lanes through __shfl_xor, across h in the lane itself. Lower index of
+            // a pair keeps the min in an ascending block, the max in a descending one (== the swap below)
+            float v[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int e = lane + 64 * h;
+                v[h] = e < N ? f[e] : INFINITY;
+            }
+            const int H = P2 > 64 ? 2 : 1;
+            for (int k = 2; k <= P2; k <<= 1) {
+                for (int j = k >> 1; j > 0; j >>= 1) {
+                    if (j == 64) {   // k == 128: the whole run ascends; lower = h 0
+                        const float a = fminf(v[0], v[1]), b = fmaxf(v[0], v[1]);
+                        v[0] = a;
+                        v[1] = b;
+                        continue;
+                    }
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        if (h >= H) break;
+                        const int e = lane + 64 * h;
+                        const float y = __shfl_xor(v[h], j, 64);
+                        const bool lower = (lane & j) == 0, up = (e & k) == 0;
+                        v[h] = (lower == up) ? fminf(v[h], y) : fmaxf(v[h], y);
                     }
                 }
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            }
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+                if (h < H && lane + 64 * h < P2) f[lane + 64 * h] = v[h];
+        } else {
+            for (int i = N + lane; i < P2; i += 64) f[i] = INFINITY;
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            for (int k = 2; k <= P2; k <<= 1) {
+                for (int j = k >> 1; j > 0; j >>= 1) {
+                    for (int i = lane; i < P2; i += 64) {
+                        const int l = i ^ j;
+                        if (l > i) {
+                            const float x = f[i], y = f[l];
+                            const bool up = (i & k) == 0;
+                            if (up ? (y < x) : (x < y)) { f[i] = y; f[l] = x; }
+                        }
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                }
             }
         }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         // coarse i: i + #{fine < v}; fine j: j + #{coarse <= v}
         for (int i = lane; i < S; i += 64) {
             const float v = all_l[i];
