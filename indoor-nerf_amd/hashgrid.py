@@ -161,14 +161,17 @@ class _PendingBins:
         self.held = None
         self.step_plan = None  # fused_table_step(): (optimizer, tables) whose step the owner pass runs
 
-    def flush(self):
+    def flush(self, final=True):
+        """Launch (or hold) the owner pass of the open workspace. final=False: an early flush that makes
+        room for more bins of the same pass (_slot) — its gradients are partial, so it never runs a fused
+        table step."""
         if self.used == 0:
             return
         L, log2_T, _, det = self.tag
         flags = det | (OWNER_OVERWRITE if take_deferred(self.grads) else 0)
         step = None
         plan = self.step_plan
-        if (plan is not None and not self.hold and (flags & OWNER_OVERWRITE)
+        if (plan is not None and final and not self.hold and (flags & OWNER_OVERWRITE)
                 and [g.data_ptr() for g in self.grads] == [p.grad.data_ptr() for p in plan[1]]):
             self.step_plan = None          # one owner pass per plan
             step = plan[0].table_step(plan[1])
@@ -217,7 +220,7 @@ class _PendingBins:
         total = (self.used if self.tag == tag else 0) + n_ch
         self.peak = max(self.peak, total)     # the next pass sizes its workspace for this
         if self.used and (self.tag != tag or total > self.cap):
-            self.flush()
+            self.flush(final=False)
         if self.used == 0:
             cap = max(self.peak, n_ch)
             C = int(lib.nerf_hash_bwd_chunk_points())
