@@ -472,15 +472,6 @@ int nerf_tv_fwd(const float* const* d_tables, int n_levels, int log2_T, const in
                 const int64_t* d_min_vertex, const int* cube, float* d_loss,
                 float* d_verts /* optional out: float2[sum_l (cube_l+1)^3], the vertices' table rows */,
                 void* stream);
-/* Same, STORING d_loss[l] (no zeroed accumulator needed): with a workspace of
- * nerf_tv_fwd_workspace_bytes(n_levels) bytes whose arrival counters are zero (zero-fill it once; every
- * call leaves them zero again), each level's last block sums the blocks' partial sums in block order —
- * the same value on every run. Calls sharing a workspace must be stream-ordered. NULL workspace:
- * nerf_tv_fwd. */
-size_t nerf_tv_fwd_workspace_bytes(int n_levels);
-int nerf_tv_fwd_ws(const float* const* d_tables, int n_levels, int log2_T, const int64_t* min_vertex,
-                   const int64_t* d_min_vertex, const int* cube, float* d_loss, float* d_verts,
-                   void* d_workspace, size_t workspace_bytes, void* stream);
 int nerf_tv_bwd(const float* const* d_tables, int n_levels, int log2_T, const int64_t* min_vertex,
                 const int64_t* d_min_vertex, const int* cube, const float* d_scale /* device [n_levels] */,
                 float* const* d_dtables, void* stream);

@@ -156,8 +156,6 @@ SIGNATURES = {
                        c_int, c_vp, c_vp],
     "nerf_radam_step": [ctypes.POINTER(RAdamSegment), c_int, c_vp, c_vp],
     "nerf_nearest_pixel": [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp],
-    "nerf_tv_fwd_ws": [ctypes.POINTER(c_vp), c_int, c_int, ctypes.POINTER(c_i64), c_vp, ctypes.POINTER(c_int), c_vp,
-                       c_vp, c_vp, ctypes.c_size_t, c_vp],
     "nerf_tv_fwd": [ctypes.POINTER(c_vp), c_int, c_int, ctypes.POINTER(c_i64), c_vp, ctypes.POINTER(c_int), c_vp,
                     c_vp, c_vp],
     "nerf_tv_bwd": [ctypes.POINTER(c_vp), c_int, c_int, ctypes.POINTER(c_i64), c_vp, ctypes.POINTER(c_int), c_vp,
@@ -199,8 +197,6 @@ def load():
     lib.nerf_abi_version.argtypes = []
     lib.nerf_hash_bwd_chunk_points.restype = c_int
     lib.nerf_hash_bwd_chunk_points.argtypes = []
-    lib.nerf_tv_fwd_workspace_bytes.restype = ctypes.c_size_t
-    lib.nerf_tv_fwd_workspace_bytes.argtypes = [c_int]
     lib.nerf_tv_bwd_bin_chunks.restype = c_i64
     lib.nerf_tv_bwd_bin_chunks.argtypes = [c_int, ctypes.POINTER(c_int)]
     lib.nerf_hash_encode_bwd_workspace_bytes.restype = ctypes.c_size_t
@@ -225,7 +221,7 @@ def load():
 
 def exported_symbols():
     return ["nerf_last_error", "nerf_abi_version", "nerf_hash_bwd_chunk_points", "nerf_tv_bwd_bin_chunks",
-            "nerf_tv_fwd_workspace_bytes",
+
             "nerf_hash_encode_bwd_workspace_bytes",
             "nerf_quant_packed_bytes", "nerf_mlp_bwd_det_workspace_bytes", "nerf_priors_workspace_bytes",
             "nerf_normal_head_bwd_workspace_bytes", "nerf_active_rows_workspace_bytes"] + list(SIGNATURES)

@@ -241,8 +241,6 @@ struct TVParams {
     const int64_t* dmv;   // optional device [L][3] cuboid corners (graph replays draw new ones)
     const float* scale;   // bwd: device [L] upstream gradient per level
     float* loss;          // fwd: device [L]
-    float* partials;      // fwd, optional: [L][gridDim.x] block sums; the level's last block STORES loss[l]
-    int* counters;        // ... with these [L] arrival counters (zero on entry, reset to zero on exit)
     float2* verts;        // optional: the cuboid vertices' table rows, level l at verts + vstart[l]
                           // (written by tv_fwd, read by tv_bwd_bin in place of the hashed gathers)
 };

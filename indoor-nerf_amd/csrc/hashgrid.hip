@@ -51,10 +51,13 @@ struct HashGradParams {
     int st_on;
 };
 
-// The fused table step of an owner block: rows [0, S) of the slice at `row0` of level lvl; g(i) gives
-// row i's gradient (as just stored). All loads of a batch of rows are issued before the first update.
+// The flush of an owner block with the fused table step: rows [0, S) of the slice at `row0` of level lvl;
+// g(i) gives row i's gradient, which is stored to dt[i] (overwrite mode) and then updates the row's
+// parameters and moments. A batch's parameter / moment loads are issued before its first gradient, so
+// they are in flight while the gradients are formed and stored.
 template <int THREADS, int ROWS, typename G>
-__device__ __forceinline__ void owner_table_step(const HashGradParams& hp, int lvl, size_t row0, int S, G g) {
+__device__ __forceinline__ void owner_table_step(const HashGradParams& hp, int lvl, size_t row0, int S, float2* dt,
+                                                 G g) {
     nerf_radam_segment s = hp.st;
     if (hp.st_coef) {
         s.decay_coef = hp.st_coef[0];
@@ -76,6 +79,7 @@ __device__ __forceinline__ void owner_table_step(const HashGradParams& hp, int l
             const int i = b + k * THREADS;
             if (i >= S) continue;
             const float2 gi = g(i);
+            dt[i] = gi;
             radam_elem(s, p[k].x, gi.x, m[k].x, v[k].x);
             radam_elem(s, p[k].y, gi.y, m[k].y, v[k].y);
             M[i] = m[k];
@@ -676,7 +680,24 @@ __global__ void __launch_bounds__(THREADS) hash_bwd_owner_kernel(HashGradParams 
             }
             valid = valid2;
         }
-        __syncthreads();   // s_pre / s_beg reused by the next window
+        if (w0 + kOwnerWindow < hp.nchunks) __syncthreads();   // s_pre / s_beg reused by the next window
+    }
+    // fused table step, full slices (the lego hot path): the last window's barrier is the flush barrier
+    // below, and a thread done with its entries issues its rows' parameter / moment loads before it
+    // waits there for the block's slower waves
+    // (half of a thread's rows here, the other half at the flush: all of them would spill)
+    constexpr int kRowsP = (1 << SLICE_LOG2) / THREADS, kHalf = kRowsP / 2;
+    const bool pre = !DET && hp.st_on && hp.overwrite && S == (1 << SLICE_LOG2);
+    float2 pp[kRowsP], pm[kRowsP], pv[kRowsP];
+    const size_t prow0 = (size_t)o * S;
+    auto pload = [&](int k) {
+        pp[k] = reinterpret_cast<const float2*>(hp.st_p[lvl])[prow0 + tid + k * THREADS];
+        pm[k] = reinterpret_cast<const float2*>(hp.st_m[lvl])[prow0 + tid + k * THREADS];
+        pv[k] = reinterpret_cast<const float2*>(hp.st_v[lvl])[prow0 + tid + k * THREADS];
+    };
+    if (pre) {
+#pragma unroll
+        for (int k = 0; k < kHalf; ++k) pload(k);
     }
     // Flush: every row's table load is issued before any add (one memory round trip per block,
     // not one per row batch: a load behind the previous batch's store left 8 serial round trips).
@@ -694,6 +715,12 @@ __global__ void __launch_bounds__(THREADS) hash_bwd_owner_kernel(HashGradParams 
             const long long hi = (long long)s_fix[4 * row + f], lo = (long long)s_fix[4 * row + 2 + f];
             return ldexp((double)hi, -sh) + ldexp((double)lo, -sl_);
         };
+        if (hp.st_on) {   // overwrite mode (the entry point checks): the stored row is the step's gradient
+            owner_table_step<kOwnerThreads, kRows>(hp, lvl, (size_t)o * S, S, dt, [&](int i) {
+                return make_float2((float)fixed(i, 0), (float)fixed(i, 1));
+            });
+            return;
+        }
         for (int i = tid; i < S; i += kOwnerThreads) {
             const double vx = fixed(i, 0), vy = fixed(i, 1);
             if (hp.overwrite) {
@@ -703,22 +730,46 @@ __global__ void __launch_bounds__(THREADS) hash_bwd_owner_kernel(HashGradParams 
                 dt[i] = make_float2((float)((double)t.x + vx), (float)((double)t.y + vy));
             }
         }
-        if (hp.st_on)   // overwrite mode (the entry point checks): the gradient is the row's stored value
-            owner_table_step<kOwnerThreads, kRows>(hp, lvl, (size_t)o * S, S, [&](int i) {
-                return make_float2((float)fixed(i, 0), (float)fixed(i, 1));
-            });
         return;
     }
     if (hp.overwrite) {   // rows without entries become +0, as after a memset
+        if (pre) {
+            nerf_radam_segment s = hp.st;
+            if (hp.st_coef) {
+                s.decay_coef = hp.st_coef[0];
+                s.step_coef = hp.st_coef[1];
+                s.mode = (int)hp.st_coef[2];
+            }
+            float2* P = reinterpret_cast<float2*>(hp.st_p[lvl]) + (size_t)o * S;
+            float2* M = reinterpret_cast<float2*>(hp.st_m[lvl]) + (size_t)o * S;
+            float2* V = reinterpret_cast<float2*>(hp.st_v[lvl]) + (size_t)o * S;
+#pragma unroll
+            for (int k = kHalf; k < kRowsP; ++k) pload(k);
+#pragma unroll
+            for (int k = 0; k < kRowsP; ++k) {
+                const int i = tid + k * kOwnerThreads;
+                const Acc v = s_slice[i];
+                const float2 g = make_float2((float)v.x, (float)v.y);
+                dt[i] = g;
+                radam_elem(s, pp[k].x, g.x, pm[k].x, pv[k].x);
+                radam_elem(s, pp[k].y, g.y, pm[k].y, pv[k].y);
+                M[i] = pm[k];
+                V[i] = pv[k];
+                if (s.mode != 0) P[i] = pp[k];
+            }
+            return;
+        }
+        if (hp.st_on) {
+            owner_table_step<kOwnerThreads, kRows>(hp, lvl, (size_t)o * S, S, dt, [&](int i) {
+                const Acc v = s_slice[i];
+                return make_float2((float)v.x, (float)v.y);
+            });
+            return;
+        }
         for (int i = tid; i < S; i += kOwnerThreads) {
             const Acc v = s_slice[i];
             dt[i] = make_float2((float)v.x, (float)v.y);
         }
-        if (hp.st_on)
-            owner_table_step<kOwnerThreads, kRows>(hp, lvl, (size_t)o * S, S, [&](int i) {
-                const Acc v = s_slice[i];
-                return make_float2((float)v.x, (float)v.y);
-            });
         return;
     }
     // the row's prior gradient plus the slice's sum: in fp32 (A32, as the reference's accumulating

@@ -109,22 +109,7 @@ __global__ void __launch_bounds__(256) tv_fwd_kernel(TVParams P) {
     __syncthreads();
     if (threadIdx.x == 0) {
         const float t = (s_part[0] + s_part[1]) + (s_part[2] + s_part[3]);
-        if (!P.partials) {
-            if (t != 0.f) atomicAdd(P.loss + l, t);
-            return;
-        }
-        // block sum stored, then the arrival count (release: the store is visible first); the level's
-        // last block (acquire) sums the partials in block order and stores the loss: no zeroed
-        // accumulator, and the same sum on every run
-        P.partials[l * gridDim.x + blockIdx.x] = t;
-        const int n = __hip_atomic_fetch_add(P.counters + l, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-        if (n == (int)gridDim.x - 1) {
-            float s = 0.f;
-            for (unsigned b = 0; b < gridDim.x; ++b)
-                s += __hip_atomic_load(P.partials + l * gridDim.x + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            P.loss[l] = s;
-            __hip_atomic_store(P.counters + l, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        if (t != 0.f) atomicAdd(P.loss + l, t);
     }
 }
 
@@ -203,17 +188,9 @@ extern "C" int nerf_radam_step(const nerf_radam_segment* segs, int n_segs, const
     return NERF_OK;
 }
 
-extern "C" size_t nerf_tv_fwd_workspace_bytes(int n_levels) {
-    if (n_levels < 1 || n_levels > NERF_MAX_LEVELS) return 0;
-    return (size_t)n_levels * (kTVBlocks * sizeof(float) + sizeof(int));
-}
-
-extern "C" int nerf_tv_fwd_ws(const float* const* d_tables, int n_levels, int log2_T, const int64_t* min_vertex,
-                              const int64_t* d_min_vertex, const int* cube, float* d_loss, float* d_verts,
-                              void* d_workspace, size_t workspace_bytes, void* stream) {
-    NERF_REQUIRE(!d_workspace || workspace_bytes >= nerf_tv_fwd_workspace_bytes(n_levels),
-                 "tv_fwd: workspace %zu B < %zu B", workspace_bytes, nerf_tv_fwd_workspace_bytes(n_levels));
-    NERF_REQUIRE(((uintptr_t)d_workspace & 3) == 0, "tv_fwd: workspace must be 4-B aligned");
+extern "C" int nerf_tv_fwd(const float* const* d_tables, int n_levels, int log2_T, const int64_t* min_vertex,
+                           const int64_t* d_min_vertex, const int* cube, float* d_loss, float* d_verts,
+                           void* stream) {
     TVParams P{};
     int rc = fill_tv(P, n_levels, log2_T, min_vertex, d_min_vertex, cube);
     if (rc) return rc;
@@ -224,20 +201,9 @@ extern "C" int nerf_tv_fwd_ws(const float* const* d_tables, int n_levels, int lo
     }
     P.loss = d_loss;
     P.verts = reinterpret_cast<float2*>(d_verts);
-    if (d_workspace) {
-        P.partials = static_cast<float*>(d_workspace);
-        P.counters = reinterpret_cast<int*>(P.partials + (size_t)n_levels * kTVBlocks);
-    }
     hipLaunchKernelGGL(tv_fwd_kernel, dim3(kTVBlocks, n_levels), dim3(256), 0, as_stream(stream), P);
     NERF_CHECK_LAUNCH("tv_fwd");
     return NERF_OK;
-}
-
-extern "C" int nerf_tv_fwd(const float* const* d_tables, int n_levels, int log2_T, const int64_t* min_vertex,
-                           const int64_t* d_min_vertex, const int* cube, float* d_loss, float* d_verts,
-                           void* stream) {
-    return nerf_tv_fwd_ws(d_tables, n_levels, log2_T, min_vertex, d_min_vertex, cube, d_loss, d_verts, nullptr, 0,
-                          stream);
 }
 
 extern "C" int nerf_tv_bwd(const float* const* d_tables, int n_levels, int log2_T, const int64_t* min_vertex,

@@ -24,23 +24,6 @@ def tv_cube(level, min_resolution, max_resolution, n_levels):
     return res, cube
 
 
-_TV_WS = {}
-
-
-def _tv_workspace(device, L):
-    """nerf_tv_fwd_ws's workspace (block sums + arrival counters, zero-filled once; every launch leaves
-    the counters zero), per device; None when it would first be allocated inside a HIP-graph capture
-    (its zero fill would be captured and replayed every step)."""
-    key = (str(device), L)
-    ws = _TV_WS.get(key)
-    if ws is None:
-        if torch.cuda.is_current_stream_capturing():
-            return None
-        n = int(_lib.load().nerf_tv_fwd_workspace_bytes(L)) // 4
-        ws = _TV_WS[key] = torch.zeros(n, device=device, dtype=torch.int32)
-    return ws
-
-
 class TVFn(torch.autograd.Function):
     """min_vertex: host [L,3] cuboid corners, or an int device address of [L,3] int64 slots that a
     captured step refreshes before every replay (graphs.StepScalars)."""
@@ -55,14 +38,9 @@ class TVFn(torch.autograd.Function):
         dev = tables[0].device
         # the cuboid vertices' rows, gathered once here: the backward's stencil reads them densely
         verts = torch.empty(2 * sum((int(c) + 1) ** 3 for c in cubes), device=dev, dtype=torch.float32)
-        ws = _tv_workspace(dev, L)
-        if ws is None:   # first use inside a graph capture: the zeroed accumulator of nerf_tv_fwd
-            loss = torch.zeros(L, device=dev, dtype=torch.float32)
-        else:            # the kernel stores every level's loss: no zero fill per step
-            loss = torch.empty(L, device=dev, dtype=torch.float32)
-        _lib.call("nerf_tv_fwd_ws", _lib.ptr_array(tables), L, log2_T, mv, dmv, cb, _lib.ptr(loss, "loss"),
-                  _lib.ptr(verts, "tv_verts"), None if ws is None else _lib.ptr(ws, "tv_workspace", torch.int32),
-                  0 if ws is None else ws.numel() * 4, _lib.stream())
+        loss = torch.zeros(L, device=dev, dtype=torch.float32)
+        _lib.call("nerf_tv_fwd", _lib.ptr_array(tables), L, log2_T, mv, dmv, cb, _lib.ptr(loss, "loss"),
+                  _lib.ptr(verts, "tv_verts"), _lib.stream())
         ctx.save_for_backward(*tables)
         ctx.mv, ctx.dmv, ctx.cb, ctx.log2_T, ctx.verts = mv, dmv, cb, log2_T, verts
         return loss
