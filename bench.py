@@ -226,7 +226,7 @@ def parse():
     ap.add_argument("--zero", type=int, default=1,
                     help="N>1: shard the optimizer (reduce-scatter -> RAdam on 1/N -> all-gather, dist.ShardedOptimizer); "
                          "0 = all-reduce + replicated RAdam")
-    ap.add_argument("--fused-table-step", type=int, default=0,
+    ap.add_argument("--fused-table-step", type=int, default=1,
                     help="1: the tables' RAdam step runs inside the owner pass (one process; hashgrid.fused_table_step)")
     ap.add_argument("--overlap", type=int, default=1,
                     help="N>1 with --zero 1: reduce-scatter the first gradient bucket while the owner pass sums the "

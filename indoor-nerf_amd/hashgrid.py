@@ -303,7 +303,7 @@ class hold_owner:
         return False
 
 
-_FUSED_STEP = {"on": False}
+_FUSED_STEP = {"on": True}
 
 
 def set_fused_table_step(enabled=True):
