@@ -60,8 +60,12 @@ OPS = {
                             unit="hash_point"),
     "mlp_bwd": dict(calls=("nerf_mlp_bwd", "nerf_mlp_bwd_batch"), bound="mfma", per_unit=2 * 18688, unit="bwd_point"),
     "mlp_fwd": dict(calls=("nerf_mlp_fwd",), bound="mfma", per_unit=18688, unit="point"),
-    "composite_fwd": dict(calls=("nerf_composite_fwd",), bound="hbm", per_unit=24, unit="sample"),
-    "composite_bwd": dict(calls=("nerf_composite_bwd",), bound="hbm", per_unit=40, unit="sample"),
+    # the coarse pass's compositing runs in the sampler's launch (nerf_composite_sample_fine): its time
+    # is the op's, the sampler's bytes are not priced (a lower bound on the op's fraction)
+    "composite_fwd": dict(calls=("nerf_composite_fwd", "nerf_composite_sample_fine"), bound="hbm", per_unit=24,
+                          unit="sample"),
+    "composite_bwd": dict(calls=("nerf_composite_bwd", "nerf_composite_bwd_batch"), bound="hbm", per_unit=40,
+                          unit="sample"),
     "radam": dict(calls=("nerf_radam_step",), bound="hbm", per_unit=28, unit="element"),
 }
 # algorithmic HBM bytes of one whole iteration per ray at 64 + 128 samples
@@ -86,9 +90,12 @@ KERNEL_SYMBOLS = {
     "nerf_mlp_bwd": ["nerf::mlp_bwd_x6cg_kernel<false>"],
     "nerf_mlp_bwd_batch": ["nerf::mlp_bwd_x6cg_kernel<false>"],
     "nerf_radam_step": ["nerf::radam_kernel"],
+    "nerf_composite_sample_fine": ["nerf::composite_sample_fine_kernel<1>"],
+    "nerf_composite_bwd_batch": ["nerf::composite_bwd_pair_kernel<3, 1>"],
 }
 # calls whose every launch runs ONE of the listed kernels (the coarse pass's K = 1 and the fine pass's
-# K = 3 compositing, one launch each per iteration): per-call traffic = the mean over the kernels
+# K = 3 compositing, one launch each per iteration, with the fused sampler and the batched backward
+# off): per-call traffic = the mean over the kernels
 KERNEL_VARIANTS = {
     "nerf_composite_fwd": ["nerf::composite_fwd_kernel<1>", "nerf::composite_fwd_kernel<3>"],
     "nerf_composite_bwd": ["nerf::composite_bwd_kernel<1>", "nerf::composite_bwd_kernel<3>"],
@@ -228,6 +235,11 @@ def parse():
                          "0 = all-reduce + replicated RAdam")
     ap.add_argument("--fused-table-step", type=int, default=1,
                     help="1: the tables' RAdam step runs inside the owner pass (one process; hashgrid.fused_table_step)")
+    ap.add_argument("--fused-sampler", type=int, default=1,
+                    help="1: the coarse compositing and the hierarchical sampler in one launch "
+                         "(render.set_fused_coarse_sampler)")
+    ap.add_argument("--batched-composite", type=int, default=1,
+                    help="1: the fine and coarse compositing backwards in one launch (render.set_batched_composite_bwd)")
     ap.add_argument("--overlap", type=int, default=1,
                     help="N>1 with --zero 1: reduce-scatter the first gradient bucket while the owner pass sums the "
                          "second (dist.ShardedOptimizer(overlap=True)); 0 = one reduce-scatter after the backward")
@@ -446,6 +458,8 @@ def main():
         nerf.set_deterministic(True)
     nerf.set_coarse_reuse(bool(a.coarse_reuse))
     nerf.set_fused_table_step(bool(a.fused_table_step))
+    nerf.set_fused_coarse_sampler(bool(a.fused_sampler))
+    nerf.set_batched_composite_bwd(bool(a.batched_composite))
     nerf.set_active_points(bool(a.active_points))
     kw, kw_test, _, grad_vars, opt = nerf.create_nerf(args, device=dev)
     for d in (kw, kw_test):
@@ -572,6 +586,12 @@ def main():
             units["bwd_point"] = active["mlp_points"]
             units["bwd_hash_point"] = active["hash_points"]
     if kernels:
+        # with the fused sampler only the fine pass calls nerf_composite_fwd: its own K kernel
+        if a.fused_sampler and ni:
+            KERNEL_VARIANTS["nerf_composite_fwd"] = [f"nerf::composite_fwd_kernel<{(ns + ni + 63) // 64}>"]
+        if a.batched_composite and ni:
+            KERNEL_SYMBOLS["nerf_composite_bwd_batch"] = [
+                f"nerf::composite_bwd_pair_kernel<{(ns + ni + 63) // 64}, {(ns + 63) // 64}>"]
         from indoor_nerf_amd.hashgrid import last_fused_table_step
         fused_elems = sum(t.numel() for t in kw["embed_fn"].tables()) if last_fused_table_step() else 0
         ops = op_rooflines(kernels, a.steps, units, sum(p.numel() for p in params), hash_entries, fused_elems)
@@ -623,6 +643,8 @@ def main():
         "hip_graph": bool(gstep is not None and gstep.captures > 0),
         "coarse_reuse": reused,
         "fused_table_step": fused_step,
+        "fused_coarse_sampler": bool(a.fused_sampler and ni),
+        "batched_composite_bwd": bool(a.batched_composite and ni),
         "active_points": None if active is None else {"fraction": round(active["fraction"], 4),
                                                       "mlp_bwd_points": active["mlp_points"],
                                                       "hash_bwd_points": active["hash_points"]},

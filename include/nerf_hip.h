@@ -371,6 +371,20 @@ int nerf_composite_bwd(const float* d_raw, int raw_channels, const float* d_z, c
                        const float* d_g_weights, const float* d_g_depth, const float* d_g_entropy,
                        const float* d_g_normal, float* d_graw, void* stream);
 
+/* Several compositing backwards in one call (the fine and the coarse pass of a training iteration):
+ * each job's fields as the nerf_composite_bwd arguments of the same name. Two jobs with
+ * ceil(S/64) in {(1,1),(2,1),(3,1),(4,1),(2,2),(3,2),(4,2),(3,3)} (either order) run as ONE launch;
+ * otherwise one launch per job. Every job is validated before anything is launched; results are
+ * bit-identical to nerf_composite_bwd per job. */
+typedef struct nerf_composite_bwd_job {
+    const float* raw; int raw_channels; const float* z; const float* rays_d; const float* noise;
+    int64_t n_rays; int n_samples; int white_bkgd;
+    const float* g_rgb; const float* g_disp; const float* g_acc; const float* g_weights; const float* g_depth;
+    const float* g_entropy; const float* g_normal;
+    float* graw;
+} nerf_composite_bwd_job;
+int nerf_composite_bwd_batch(const nerf_composite_bwd_job* jobs, int n_jobs, void* stream);
+
 /* ---- ray sampling (render_rays, run_nerf.py:460-490) --------------------------------------
  * d_rays: packed ray batch [R, ray_stride] = [o(3), d(3), near, far, (viewdir(3))] as render()
  * builds it (run_nerf.py:134-140). d_t: [S] = torch.linspace(0,1,S) values. perturb != 0 jitters
@@ -411,6 +425,20 @@ int nerf_sample_fine_rows(const float* d_rays, int64_t ray_stride, const float* 
                           float* d_z_fine, float* d_pts_fine, float* d_z_std, float* d_samples,
                           int32_t* d_coarse_rows, int32_t* d_imp_rows, float* d_imp_pts, int32_t* d_perm,
                           void* stream);
+
+/* The coarse pass of render_rays in one launch: nerf_composite_fwd (arguments as there; d_z, d_weights
+ * and n_rays / n_samples are shared with the sampler) followed by nerf_sample_fine_rows on its weights
+ * (the remaining arguments as there). Bit-identical to the two calls, which it makes itself when
+ * n_samples > 128 (the fused launch holds the weights of a ray in LDS, one wave per ray). */
+int nerf_composite_sample_fine(const float* d_raw, int raw_channels, const float* d_z, const float* d_rays_d,
+                               const float* d_noise, int64_t n_rays, int n_samples, int white_bkgd,
+                               float* d_rgb, float* d_disp, float* d_acc, float* d_weights, float* d_depth,
+                               float* d_entropy, float* d_normal,
+                               const float* d_rays, int64_t ray_stride, int n_importance, int det,
+                               const float* d_t_imp, const float* d_u, uint64_t seed, uint64_t offset,
+                               const uint64_t* d_rng, float* d_z_fine, float* d_pts_fine, float* d_z_std,
+                               float* d_samples, int32_t* d_coarse_rows, int32_t* d_imp_rows, float* d_imp_pts,
+                               int32_t* d_perm, void* stream);
 
 /* ---- rays of the training batch / of a whole image (run_nerf.py:973-1004, run_nerf_helpers.py:311-320)
  * Camera: c2w = the pose [3,4] as float32 (torch.Tensor(pose)), fx = K[0][0], fy = K[1][1],

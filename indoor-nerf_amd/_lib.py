@@ -50,6 +50,13 @@ class MlpBwdJob(ctypes.Structure):
 PRIORS_MAX_RAYS = 8192   # NERF_PRIORS_MAX_RAYS
 
 
+class CompositeBwdJob(ctypes.Structure):
+    _fields_ = [("raw", c_vp), ("raw_channels", c_int), ("z", c_vp), ("rays_d", c_vp), ("noise", c_vp),
+                ("n_rays", c_i64), ("n_samples", c_int), ("white_bkgd", c_int),
+                ("g_rgb", c_vp), ("g_disp", c_vp), ("g_acc", c_vp), ("g_weights", c_vp), ("g_depth", c_vp),
+                ("g_entropy", c_vp), ("g_normal", c_vp), ("graw", c_vp)]
+
+
 class PriorsConfig(ctypes.Structure):
     """nerf_priors_config (include/nerf_hip.h)."""
     _fields_ = [("use_manhattan", c_int), ("use_planarity", c_int), ("use_consistency", c_int),
@@ -142,6 +149,11 @@ SIGNATURES = {
                            c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
     "nerf_composite_bwd": [c_vp, c_int, c_vp, c_vp, c_vp, c_i64, c_int, c_int,
                            c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
+    "nerf_composite_bwd_batch": [ctypes.POINTER(CompositeBwdJob), c_int, c_vp],
+    "nerf_composite_sample_fine": [c_vp, c_int, c_vp, c_vp, c_vp, c_i64, c_int, c_int,
+                                   c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                   c_vp, c_i64, c_int, c_int, c_vp, c_vp, c_u64, c_u64, c_vp,
+                                   c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
     "nerf_sample_stratified": [c_vp, c_i64, c_i64, c_int, c_vp, c_int, c_int, c_vp, c_u64, c_u64, c_vp, c_vp, c_vp,
                                c_vp, c_vp, c_vp],
     "nerf_sample_pdf": [c_vp, c_i64, c_vp, c_i64, c_i64, c_int, c_int, c_int, c_vp, c_vp, c_u64, c_u64, c_vp, c_vp,

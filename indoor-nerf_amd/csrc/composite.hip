@@ -1,203 +1,24 @@
 // Volume compositing: raw2outputs (PocketNeRF/run_nerf.py:347-411) forward and backward.
 //
-// One wavefront per ray; lane L owns the K = ceil(S/64) consecutive samples [K*L, K*L+K). The
-// transmittance T_j = prod_{k<j}(1 - alpha_k + 1e-10) is a wave-level exclusive product scan over
-// the lanes' local products (DPP lane moves: common.h wave_excl_prod_dpp); the backward's suffix
-// recurrence
+// One wavefront per ray (composite_common.h). The backward's suffix recurrence
 //   U_j = sum_{k>j} gw_k alpha_k prod_{j<m<k} t_m,   dL/dalpha_j = T_j (gw_j - U_j)
-// is a wave-level suffix scan of affine maps (X, P) -> X + P*U. Scans and ray sums run in fp64:
-// the reference's CPU cumprod/cumsum accumulate in double, and the cost here is negligible.
-// Quirks kept: last delta = 1e10, +1e-10 inside the product, NaN depth when sum(w) == 0,
-// disp = 1/max(1e-10, depth) (NaN propagates), Categorical entropy over [w, max(1-sum w, 1e-6)].
-#include "common.h"
+// is a wave-level suffix scan of affine maps (X, P) -> X + P*U in fp64.
+#include "composite_common.h"
 
 namespace nerf {
-
-struct CompositeArgs {
-    const float* raw; int C;
-    const float* z;
-    const float* rays_d;
-    const float* noise;
-    int64_t R; int S; int white;
-    // forward outputs
-    float* rgb; float* disp; float* acc; float* weights; float* depth; float* entropy; float* normal;
-    // backward inputs/outputs
-    const float* g_rgb; const float* g_disp; const float* g_acc; const float* g_w;
-    const float* g_depth; const float* g_ent; const float* g_normal;
-    float* graw;
-};
-
-__device__ __forceinline__ float sigmoidf(float x) { return 1.0f / (1.0f + expf(-x)); }
-
-// Per-sample forward quantities.
-template <int K>
-struct RayState {
-    float c[K][3];     // sigmoid(rgb_raw)
-    float n[K][3];     // normals (C == 7)
-    float s[K];        // sigma + noise
-    float delta[K];    // dists * |d|
-    float e[K];        // exp(-relu(s) * delta)
-    float alpha[K];
-    float t[K];        // 1 - alpha + 1e-10
-    float z[K];
-    double T[K];       // transmittance (exclusive product)
-    float w[K];        // weights
-};
-
-
-template <int K>
-__device__ __forceinline__ void ray_forward(const CompositeArgs& a, int64_t ray, int lane, RayState<K>& st,
-                                            float& norm_d) {
-    const float dx = a.rays_d[3 * ray + 0], dy = a.rays_d[3 * ray + 1], dz = a.rays_d[3 * ray + 2];
-    norm_d = sqrtf(dx * dx + dy * dy + dz * dz);
-    const float* zr = a.z + ray * a.S;
-    double lprod = 1.0;
-    double Tloc[K];
-#pragma unroll
-    for (int q = 0; q < K; ++q) {
-        const int j = lane * K + q;
-        Tloc[q] = lprod;
-        if (j < a.S) {
-            const float* r = a.raw + (ray * a.S + j) * a.C;
-            const float zj = zr[j];
-            st.z[q] = zj;
-            const float dist = (j + 1 < a.S) ? (zr[j + 1] - zj) : 1e10f;
-            st.delta[q] = dist * norm_d;
-            st.c[q][0] = sigmoidf(r[0]);
-            st.c[q][1] = sigmoidf(r[1]);
-            st.c[q][2] = sigmoidf(r[2]);
-            float sg = r[3];
-            if (a.noise) sg = sg + a.noise[ray * a.S + j];
-            st.s[q] = sg;
-            const float relu_s = sg > 0.f ? sg : 0.f;
-            st.e[q] = expf(-relu_s * st.delta[q]);
-            st.alpha[q] = 1.0f - st.e[q];
-            st.t[q] = (1.0f - st.alpha[q]) + 1e-10f;
-            if (a.C >= 7) {
-                st.n[q][0] = r[4]; st.n[q][1] = r[5]; st.n[q][2] = r[6];
-            } else {
-                st.n[q][0] = st.n[q][1] = st.n[q][2] = 0.f;
-            }
-            lprod *= (double)st.t[q];
-        } else {
-            st.z[q] = 0.f; st.delta[q] = 0.f; st.s[q] = 0.f; st.e[q] = 1.f; st.alpha[q] = 0.f; st.t[q] = 1.f;
-            st.c[q][0] = st.c[q][1] = st.c[q][2] = 0.f;
-            st.n[q][0] = st.n[q][1] = st.n[q][2] = 0.f;
-        }
-    }
-    const double pre = wave_excl_prod_dpp(lprod);
-#pragma unroll
-    for (int q = 0; q < K; ++q) {
-        st.T[q] = pre * Tloc[q];
-        st.w[q] = st.alpha[q] * (float)st.T[q];
-    }
-}
-
-struct RaySums {
-    float rgb[3], acc, depth_num, depth, disp, wsum, q, Z, ent, nraw[3], nden, nnorm;
-};
-
-// need_rgb / need_depth (wave-uniform): the backward needs neither the colour sums nor, without a
-// depth or disparity gradient, the depth numerator — each skipped sum is one fp64 wave reduction
-template <int K>
-__device__ __forceinline__ RaySums ray_sums(const CompositeArgs& a, const RayState<K>& st, bool need_ent,
-                                           bool need_rgb = true, bool need_depth = true) {
-    double r0 = 0, r1 = 0, r2 = 0, acc = 0, dn = 0, n0 = 0, n1 = 0, n2 = 0;
-    const bool normals = a.C >= 7;   // wave-uniform
-#pragma unroll
-    for (int q = 0; q < K; ++q) {
-        const double w = st.w[q];
-        r0 += (double)(st.w[q] * st.c[q][0]);
-        r1 += (double)(st.w[q] * st.c[q][1]);
-        r2 += (double)(st.w[q] * st.c[q][2]);
-        acc += w;
-        dn += (double)(st.w[q] * st.z[q]);
-        n0 += (double)(st.w[q] * st.n[q][0]);
-        n1 += (double)(st.w[q] * st.n[q][1]);
-        n2 += (double)(st.w[q] * st.n[q][2]);
-    }
-    RaySums s;
-    s.rgb[0] = s.rgb[1] = s.rgb[2] = 0.f;
-    if (need_rgb) {
-        s.rgb[0] = (float)wave_sum_dpp(r0);
-        s.rgb[1] = (float)wave_sum_dpp(r1);
-        s.rgb[2] = (float)wave_sum_dpp(r2);
-    }
-    s.acc = (float)wave_sum_dpp(acc);
-    s.depth_num = need_depth ? (float)wave_sum_dpp(dn) : 0.f;
-    s.depth = s.depth_num / s.acc;
-    {
-        const float m = (s.depth != s.depth) ? s.depth : fmaxf(1e-10f, s.depth);   // torch.max keeps NaN
-        s.disp = 1.0f / m;
-    }
-    s.wsum = s.acc;
-    s.q = fmaxf(1.0f - s.wsum, 1e-6f);
-    if (!(1.0f - s.wsum == 1.0f - s.wsum)) s.q = 1.0f - s.wsum;   // NaN stays NaN under clamp
-    s.Z = (float)((double)s.acc + (double)s.q);
-    s.ent = 0.f;
-    if (need_ent) {
-        const float eps = 1.1920928955078125e-07f;
-        double h = 0;
-#pragma unroll
-        for (int q = 0; q < K; ++q) {
-            const float p = st.w[q] / s.Z;
-            h += (double)(logf(fminf(fmaxf(p, eps), 1.0f - eps)) * p);
-        }
-        h = wave_sum_dpp(h);
-        const float pq = s.q / s.Z;
-        h += (double)(logf(fminf(fmaxf(pq, eps), 1.0f - eps)) * pq);
-        s.ent = (float)(-h);
-    }
-    s.nraw[0] = s.nraw[1] = s.nraw[2] = 0.f;
-    if (normals) {
-        s.nraw[0] = (float)wave_sum_dpp(n0);
-        s.nraw[1] = (float)wave_sum_dpp(n1);
-        s.nraw[2] = (float)wave_sum_dpp(n2);
-    }
-    s.nnorm = sqrtf(s.nraw[0] * s.nraw[0] + s.nraw[1] * s.nraw[1] + s.nraw[2] * s.nraw[2]);
-    s.nden = fmaxf(s.nnorm, 1e-12f);
-    return s;
-}
 
 template <int K>
 __global__ void __launch_bounds__(256) composite_fwd_kernel(CompositeArgs a) {
     const int lane = threadIdx.x & 63;
     const int64_t ray = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (ray >= a.R) return;   // wave-uniform
-    RayState<K> st;
-    float norm_d;
-    ray_forward<K>(a, ray, lane, st, norm_d);
-    const RaySums s = ray_sums<K>(a, st, a.entropy != nullptr);
-#pragma unroll
-    for (int q = 0; q < K; ++q) {
-        const int j = lane * K + q;
-        if (j < a.S) a.weights[ray * a.S + j] = st.w[q];
-    }
-    if (lane == 0) {
-        float rgb0 = s.rgb[0], rgb1 = s.rgb[1], rgb2 = s.rgb[2];
-        if (a.white) {
-            const float bg = 1.0f - s.acc;
-            rgb0 = rgb0 + bg; rgb1 = rgb1 + bg; rgb2 = rgb2 + bg;
-        }
-        if (a.rgb) { a.rgb[3 * ray] = rgb0; a.rgb[3 * ray + 1] = rgb1; a.rgb[3 * ray + 2] = rgb2; }
-        if (a.acc) a.acc[ray] = s.acc;
-        if (a.depth) a.depth[ray] = s.depth;
-        if (a.disp) a.disp[ray] = s.disp;
-        if (a.entropy) a.entropy[ray] = s.ent;
-        if (a.normal) {
-            a.normal[3 * ray + 0] = s.nraw[0] / s.nden;
-            a.normal[3 * ray + 1] = s.nraw[1] / s.nden;
-            a.normal[3 * ray + 2] = s.nraw[2] / s.nden;
-        }
-    }
+    composite_fwd_ray<K>(a, ray, lane, nullptr);
 }
 
 
+// The backward of one ray (the wave's).
 template <int K>
-__global__ void __launch_bounds__(256) composite_bwd_kernel(CompositeArgs a) {
-    const int lane = threadIdx.x & 63;
-    const int64_t ray = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (ray >= a.R) return;
+__device__ __forceinline__ void composite_bwd_ray(const CompositeArgs& a, int64_t ray, int lane) {
     RayState<K> st;
     float norm_d;
     ray_forward<K>(a, ray, lane, st, norm_d);
@@ -310,6 +131,28 @@ __global__ void __launch_bounds__(256) composite_bwd_kernel(CompositeArgs a) {
     }
 }
 
+template <int K>
+__global__ void __launch_bounds__(256) composite_bwd_kernel(CompositeArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int64_t ray = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (ray >= a.R) return;   // wave-uniform
+    composite_bwd_ray<K>(a, ray, lane);
+}
+
+// Two compositing backwards in one launch (the fine and the coarse pass of a training iteration):
+// blocks [0, split) take a0's rays, the rest a1's; each wave runs the single-job code above.
+template <int K0, int K1>
+__global__ void __launch_bounds__(256) composite_bwd_pair_kernel(CompositeArgs a0, CompositeArgs a1, unsigned split) {
+    const int lane = threadIdx.x & 63;
+    if (blockIdx.x < split) {
+        const int64_t ray = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+        if (ray < a0.R) composite_bwd_ray<K0>(a0, ray, lane);
+    } else {
+        const int64_t ray = (int64_t)(blockIdx.x - split) * 4 + (threadIdx.x >> 6);
+        if (ray < a1.R) composite_bwd_ray<K1>(a1, ray, lane);
+    }
+}
+
 }  // namespace nerf
 
 using namespace nerf;
@@ -347,23 +190,81 @@ extern "C" int nerf_composite_fwd(const float* d_raw, int raw_channels, const fl
     return NERF_OK;
 }
 
+static int composite_bwd_args(const nerf_composite_bwd_job& j, CompositeArgs& a) {
+    NERF_REQUIRE(j.n_rays >= 0 && j.n_samples >= 1 && j.n_samples <= 512,
+                 "composite_bwd: R=%lld S=%d (S must be 1..512)", (long long)j.n_rays, j.n_samples);
+    NERF_REQUIRE(j.raw_channels == 4 || j.raw_channels == 7, "composite_bwd: raw_channels %d", j.raw_channels);
+    NERF_REQUIRE(j.n_rays == 0 || (j.raw && j.z && j.rays_d && j.graw), "composite_bwd: null arg");
+    a = CompositeArgs{};
+    a.raw = j.raw; a.C = j.raw_channels; a.z = j.z; a.rays_d = j.rays_d; a.noise = j.noise;
+    a.R = j.n_rays; a.S = j.n_samples; a.white = j.white_bkgd;
+    a.g_rgb = j.g_rgb; a.g_disp = j.g_disp; a.g_acc = j.g_acc; a.g_w = j.g_weights; a.g_depth = j.g_depth;
+    a.g_ent = j.g_entropy; a.g_normal = j.g_normal; a.graw = j.graw;
+    return NERF_OK;
+}
+
+static void composite_bwd_launch(const CompositeArgs& a, hipStream_t stream) {
+    NERF_COMPOSITE_DISPATCH(composite_bwd_kernel, a.S, dim3(blocks_for(a.R, 4)), stream, a);
+}
+
 extern "C" int nerf_composite_bwd(const float* d_raw, int raw_channels, const float* d_z, const float* d_rays_d,
                                   const float* d_noise, int64_t n_rays, int n_samples, int white_bkgd,
                                   const float* d_g_rgb, const float* d_g_disp, const float* d_g_acc,
                                   const float* d_g_weights, const float* d_g_depth, const float* d_g_entropy,
                                   const float* d_g_normal, float* d_graw, void* stream) {
-    NERF_REQUIRE(n_rays >= 0 && n_samples >= 1 && n_samples <= 512, "composite_bwd: R=%lld S=%d (S must be 1..512)",
-                 (long long)n_rays, n_samples);
-    NERF_REQUIRE(raw_channels == 4 || raw_channels == 7, "composite_bwd: raw_channels %d", raw_channels);
-    NERF_REQUIRE(n_rays == 0 || (d_raw && d_z && d_rays_d && d_graw), "composite_bwd: null arg");
+    const nerf_composite_bwd_job j{d_raw, raw_channels, d_z, d_rays_d, d_noise, n_rays, n_samples, white_bkgd,
+                                   d_g_rgb, d_g_disp, d_g_acc, d_g_weights, d_g_depth, d_g_entropy, d_g_normal,
+                                   d_graw};
+    CompositeArgs a;
+    const int rc = composite_bwd_args(j, a);
+    if (rc != NERF_OK) return rc;
     if (n_rays == 0) return NERF_OK;
-    CompositeArgs a{};
-    a.raw = d_raw; a.C = raw_channels; a.z = d_z; a.rays_d = d_rays_d; a.noise = d_noise;
-    a.R = n_rays; a.S = n_samples; a.white = white_bkgd;
-    a.g_rgb = d_g_rgb; a.g_disp = d_g_disp; a.g_acc = d_g_acc; a.g_w = d_g_weights; a.g_depth = d_g_depth;
-    a.g_ent = d_g_entropy; a.g_normal = d_g_normal; a.graw = d_graw;
-    dim3 grid(blocks_for(n_rays, 4));
-    NERF_COMPOSITE_DISPATCH(composite_bwd_kernel, n_samples, grid, as_stream(stream), a);
+    composite_bwd_launch(a, as_stream(stream));
     NERF_CHECK_LAUNCH("composite_bwd");
     return NERF_OK;
 }
+
+#define NERF_PAIR(K0, K1) \
+    case 10 * K0 + K1: hipLaunchKernelGGL((composite_bwd_pair_kernel<K0, K1>), grid, dim3(256), 0, st, a0, a1, split); break;
+
+extern "C" int nerf_composite_bwd_batch(const nerf_composite_bwd_job* jobs, int n_jobs, void* stream) {
+    NERF_REQUIRE(n_jobs >= 0 && (n_jobs == 0 || jobs), "composite_bwd_batch: %d jobs", n_jobs);
+    CompositeArgs args[2];
+    int live = 0;
+    for (int i = 0; i < n_jobs; ++i) {   // every job validated before anything is launched
+        CompositeArgs a;
+        const int rc = composite_bwd_args(jobs[i], a);
+        if (rc != NERF_OK) return rc;
+    }
+    hipStream_t st = as_stream(stream);
+    for (int i = 0; i < n_jobs; ++i) {
+        CompositeArgs a;
+        composite_bwd_args(jobs[i], a);
+        if (a.R == 0) continue;
+        if (live == 2) {   // more than two: the rest one launch each
+            composite_bwd_launch(a, st);
+            continue;
+        }
+        args[live++] = a;
+    }
+    if (live == 2) {
+        // the heavier job's blocks first (the launch's tail is the lighter job's short waves)
+        if (pick_k(args[1].S) > pick_k(args[0].S)) std::swap(args[0], args[1]);
+        const CompositeArgs& a0 = args[0];
+        const CompositeArgs& a1 = args[1];
+        const unsigned split = blocks_for(a0.R, 4);
+        const dim3 grid(split + blocks_for(a1.R, 4));
+        switch (10 * pick_k(a0.S) + pick_k(a1.S)) {
+            NERF_PAIR(1, 1) NERF_PAIR(2, 1) NERF_PAIR(3, 1) NERF_PAIR(4, 1) NERF_PAIR(2, 2) NERF_PAIR(3, 2)
+            NERF_PAIR(4, 2) NERF_PAIR(3, 3)
+            default:
+                composite_bwd_launch(a0, st);
+                composite_bwd_launch(a1, st);
+        }
+    } else if (live == 1) {
+        composite_bwd_launch(args[0], st);
+    }
+    NERF_CHECK_LAUNCH("composite_bwd_batch");
+    return NERF_OK;
+}
+#undef NERF_PAIR

@@ -1,6 +1,6 @@
 // Ray sampling of render_rays: stratified depths (PocketNeRF/run_nerf.py:466-490) and the
 // hierarchical step (run_nerf.py:508-513 + sample_pdf, run_nerf_helpers.py:354-397 + z_std :541).
-#include "common.h"
+#include "composite_common.h"
 
 namespace nerf {
 
@@ -146,26 +146,19 @@ __global__ void __launch_bounds__(256) sample_pdf_kernel(PdfArgs a) {
         a.samples[r * a.N + k] = invert_cdf(cdf_l, bins_l, a.nb, draw_u(a, r, k));
 }
 
-// Fine-pass sampler: z_mid bins, weights[...,1:-1], importance samples, rank-sort merge, points.
-__global__ void __launch_bounds__(256) sample_fine_kernel(PdfArgs a) {
-    __shared__ float s_cdf[4][kMaxBins];
-    __shared__ float s_bins[4][kMaxBins];
-    __shared__ float s_all[4][kMaxMerged];
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int64_t r = (int64_t)blockIdx.x * 4 + wv;
-    if (r >= a.R) return;
+// Fine-pass sampler of ray r (the wave's): z_mid bins, weights[...,1:-1], importance samples,
+// rank-sort merge, points. w_at(i) gives coarse weight i; cdf_l / bins_l / all_l are the wave's LDS rows.
+template <typename WAt>
+__device__ __forceinline__ void sample_fine_ray(const PdfArgs& a, int64_t r, int lane, WAt w_at, float* cdf_l,
+                                                float* bins_l, float* all_l) {
     const int S = a.S, N = a.N, M = S + N, nb = S - 1;
-    float* cdf_l = s_cdf[wv];
-    float* bins_l = s_bins[wv];
-    float* all_l = s_all[wv];
     const float* zr = a.z + r * S;
-    const float* wr = a.w + r * S;
     for (int i = lane; i < S; i += 64) {
         const float zi = zr[i];
         all_l[i] = zi;
         if (i + 1 < S) bins_l[i] = 0.5f * (zr[i + 1] + zi);      // .5 * (z[1:] + z[:-1])
     }
-    build_cdf(nb, [&](int i) { return wr[i + 1]; }, cdf_l, lane);   // weights[..., 1:-1]
+    build_cdf(nb, [&](int i) { return w_at(i + 1); }, cdf_l, lane);   // weights[..., 1:-1]
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     double sum = 0.0;
@@ -314,6 +307,36 @@ __global__ void __launch_bounds__(256) sample_fine_kernel(PdfArgs a) {
     }
 }
 
+__global__ void __launch_bounds__(256) sample_fine_kernel(PdfArgs a) {
+    __shared__ float s_cdf[4][kMaxBins];
+    __shared__ float s_bins[4][kMaxBins];
+    __shared__ float s_all[4][kMaxMerged];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t r = (int64_t)blockIdx.x * 4 + wv;
+    if (r >= a.R) return;
+    const float* wr = a.w + r * a.S;
+    sample_fine_ray(a, r, lane, [&](int i) { return wr[i]; }, s_cdf[wv], s_bins[wv], s_all[wv]);
+}
+
+// The coarse pass's compositing (composite_common.h) and the hierarchical sampler in one launch: the
+// wave composites its ray, keeps the weights in LDS (they also go to c.weights) and samples from
+// them — the same values the separate launches pass through HBM, so every output is bit-identical.
+template <int K>
+__global__ void __launch_bounds__(256) composite_sample_fine_kernel(CompositeArgs c, PdfArgs a) {
+    __shared__ float s_cdf[4][kMaxBins];
+    __shared__ float s_bins[4][kMaxBins];
+    __shared__ float s_all[4][kMaxMerged];
+    __shared__ float s_w[4][64 * K];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t r = (int64_t)blockIdx.x * 4 + wv;
+    if (r >= a.R) return;   // wave-uniform
+    float* w_l = s_w[wv];
+    composite_fwd_ray<K>(c, r, lane, w_l);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    sample_fine_ray(a, r, lane, [&](int i) { return w_l[i]; }, s_cdf[wv], s_bins[wv], s_all[wv]);
+}
+
 }  // namespace nerf
 
 using namespace nerf;
@@ -378,6 +401,53 @@ extern "C" int nerf_sample_fine_rows(const float* d_rays, int64_t ray_stride, co
     a.coarse_rows = d_coarse_rows; a.imp_rows = d_imp_rows; a.imp_pts = d_imp_pts; a.perm = d_perm;
     hipLaunchKernelGGL(sample_fine_kernel, dim3(blocks_for(n_rays, 4)), dim3(256), 0, as_stream(stream), a);
     NERF_CHECK_LAUNCH("sample_fine");
+    return NERF_OK;
+}
+
+extern "C" int nerf_composite_sample_fine(
+    const float* d_raw, int raw_channels, const float* d_z, const float* d_rays_d, const float* d_noise, int64_t n_rays,
+    int n_samples, int white_bkgd, float* d_rgb, float* d_disp, float* d_acc, float* d_weights, float* d_depth,
+    float* d_entropy, float* d_normal, const float* d_rays, int64_t ray_stride, int n_importance, int det,
+    const float* d_t_imp, const float* d_u, uint64_t seed, uint64_t offset, const uint64_t* d_rng, float* d_z_fine,
+    float* d_pts_fine, float* d_z_std, float* d_samples, int32_t* d_coarse_rows, int32_t* d_imp_rows,
+    float* d_imp_pts, int32_t* d_perm, void* stream) {
+    const int K = (n_samples + 63) / 64;
+    if (n_rays == 0 || K > 2 || n_samples < 3 || n_samples > kMaxBins) {
+        // the two launches (their own checks and messages); one launch covers K = 1, 2
+        int rc = nerf_composite_fwd(d_raw, raw_channels, d_z, d_rays_d, d_noise, n_rays, n_samples, white_bkgd, d_rgb,
+                                    d_disp, d_acc, d_weights, d_depth, d_entropy, d_normal, stream);
+        if (rc != NERF_OK) return rc;
+        return nerf_sample_fine_rows(d_rays, ray_stride, d_z, d_weights, n_rays, n_samples, n_importance, det, d_t_imp,
+                                     d_u, seed, offset, d_rng, d_z_fine, d_pts_fine, d_z_std, d_samples, d_coarse_rows,
+                                     d_imp_rows, d_imp_pts, d_perm, stream);
+    }
+    NERF_REQUIRE(raw_channels == 4 || raw_channels == 7, "composite_sample_fine: raw_channels %d", raw_channels);
+    NERF_REQUIRE(d_raw && d_z && d_rays_d && d_weights, "composite_sample_fine: null compositing arg");
+    NERF_REQUIRE(!(d_normal && raw_channels != 7), "composite_sample_fine: normal output needs 7 raw channels");
+    NERF_REQUIRE(n_importance >= 1 && n_samples + n_importance <= kMaxMerged,
+                 "composite_sample_fine: S=%d N=%d (S+N <= %d)", n_samples, n_importance, kMaxMerged);
+    NERF_REQUIRE(ray_stride >= 6, "composite_sample_fine: ray_stride %lld < 6", (long long)ray_stride);
+    NERF_REQUIRE((!d_coarse_rows && !d_imp_rows && !d_perm) || n_rays * (int64_t)(n_samples + n_importance) <= INT32_MAX,
+                 "composite_sample_fine: %lld fine rows do not fit the int32 row maps",
+                 (long long)(n_rays * (int64_t)(n_samples + n_importance)));
+    NERF_REQUIRE(d_rays && d_z_fine && (!det || d_t_imp), "composite_sample_fine: null sampling arg");
+    CompositeArgs c{};
+    c.raw = d_raw; c.C = raw_channels; c.z = d_z; c.rays_d = d_rays_d; c.noise = d_noise;
+    c.R = n_rays; c.S = n_samples; c.white = white_bkgd;
+    c.rgb = d_rgb; c.disp = d_disp; c.acc = d_acc; c.weights = d_weights; c.depth = d_depth;
+    c.entropy = d_entropy; c.normal = d_normal;
+    PdfArgs a{};
+    a.R = n_rays; a.N = n_importance; a.det = det; a.t_imp = d_t_imp; a.u = d_u; a.seed = seed; a.offset = offset;
+    a.rng = d_rng;
+    a.samples = d_samples; a.rays = d_rays; a.ray_stride = ray_stride; a.z = d_z; a.w = d_weights; a.S = n_samples;
+    a.z_fine = d_z_fine; a.pts_fine = d_pts_fine; a.z_std = d_z_std;
+    a.coarse_rows = d_coarse_rows; a.imp_rows = d_imp_rows; a.imp_pts = d_imp_pts; a.perm = d_perm;
+    const dim3 grid(blocks_for(n_rays, 4));
+    if (K == 1)
+        hipLaunchKernelGGL(composite_sample_fine_kernel<1>, grid, dim3(256), 0, as_stream(stream), c, a);
+    else
+        hipLaunchKernelGGL(composite_sample_fine_kernel<2>, grid, dim3(256), 0, as_stream(stream), c, a);
+    NERF_CHECK_LAUNCH("composite_sample_fine");
     return NERF_OK;
 }
 

@@ -389,7 +389,9 @@ def _det_workspace(device):
 def _run_field_jobs(jobs):
     """MLP backwards of up to two nets per launch (nerf_mlp_bwd_batch), then the hash backwards (and
     the pass's TV backwards, losses.TVBinJob) binned side by side and summed by one owner pass."""
-    tv_jobs = [j for j in jobs if not isinstance(j, _FieldJob)]
+    from .render import CompositeJob, run_composite_jobs
+    run_composite_jobs([j for j in jobs if isinstance(j, CompositeJob)])    # the fields' raw gradients
+    tv_jobs = [j for j in jobs if not isinstance(j, (_FieldJob, CompositeJob))]
     jobs = [j for j in jobs if isinstance(j, _FieldJob)]
     if jobs:
         ws = _det_workspace(jobs[0].pts.device)
@@ -467,6 +469,15 @@ class _PendingField:
         if not self.jobs:
             torch.autograd.Variable._execution_engine.queue_callback(self.flush)
         self.jobs.append(job)
+
+    def flush_composites(self):
+        """Launch the queued compositing backwards now (render._RawGuardFn)."""
+        from .render import CompositeJob, run_composite_jobs
+        comp = [j for j in self.jobs if isinstance(j, CompositeJob)]
+        if comp:
+            self.jobs = [j for j in self.jobs if not isinstance(j, CompositeJob)]
+            with torch.cuda.stream(comp[0].stream):
+                run_composite_jobs(comp)
 
     def flush(self):
         jobs, self.jobs = self.jobs, []
@@ -592,7 +603,11 @@ def run_network(inputs, viewdirs, fn, embed_fn, embeddirs_fn, netchunk=1024 * 64
         reuse = getattr(inputs, "_nerf_reuse", None)     # render.CoarseReuse of this render_rays call
         raw = FieldFn.apply(inputs.reshape(-1, 3), viewdirs, S, embed_fn, fn, netchunk, reuse,
                             *embed_fn.tables(), *fn.field_params())
-        return raw.reshape(R, S, fn.raw_channels)
+        out = raw.reshape(R, S, fn.raw_channels)
+        # without a normals head FieldFn's backward only queues its job: raw2outputs may then defer the
+        # compositing backward too (render.CompositeJob)
+        out._nerf_field_raw = fn.raw_channels == 4
+        return out
     inputs_flat = torch.reshape(inputs, [-1, inputs.shape[-1]])
     embedded, keep_mask = embed_fn(inputs_flat)
     if viewdirs is not None:

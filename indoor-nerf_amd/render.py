@@ -123,7 +123,7 @@ def _pytest_uniforms(shape, device):
 
 class CompositeFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, raw, z, rays_d, noise, white_bkgd):
+    def forward(ctx, raw, z, rays_d, noise, white_bkgd, sampler=None, defer=False):
         if z.requires_grad or rays_d.requires_grad:
             raise NotImplementedError("raw2outputs: gradients w.r.t. z_vals / rays_d are not implemented "
                                       "(the reference detaches both)")
@@ -137,12 +137,16 @@ class CompositeFn(torch.autograd.Function):
         rgb, disp, acc = torch.empty(R, 3, **f), torch.empty(R, **f), torch.empty(R, **f)
         weights, depth, ent = torch.empty(R, S, **f), torch.empty(R, **f), torch.empty(R, **f)
         normal = torch.empty(R, 3, **f) if C == 7 else None
-        _lib.call("nerf_composite_fwd", _lib.ptr(raw, "raw"), C, _lib.ptr(z, "z_vals"), _lib.ptr(rays_d, "rays_d"),
-                  _lib.ptr(noise, "noise", allow_none=True), R, S, int(bool(white_bkgd)), _lib.ptr(rgb, "rgb"),
-                  _lib.ptr(disp, "disp"), _lib.ptr(acc, "acc"), _lib.ptr(weights, "weights"), _lib.ptr(depth, "depth"),
-                  _lib.ptr(ent, "entropy"), _lib.ptr(normal, "normal", allow_none=True), _lib.stream())
+        cargs = (_lib.ptr(raw, "raw"), C, _lib.ptr(z, "z_vals"), _lib.ptr(rays_d, "rays_d"),
+                 _lib.ptr(noise, "noise", allow_none=True), R, S, int(bool(white_bkgd)), _lib.ptr(rgb, "rgb"),
+                 _lib.ptr(disp, "disp"), _lib.ptr(acc, "acc"), _lib.ptr(weights, "weights"), _lib.ptr(depth, "depth"),
+                 _lib.ptr(ent, "entropy"), _lib.ptr(normal, "normal", allow_none=True))
+        if sampler is None:
+            _lib.call("nerf_composite_fwd", *cargs, _lib.stream())
+        else:   # the coarse pass: the hierarchical sampler on these weights in the same launch
+            _lib.call("nerf_composite_sample_fine", *cargs, *sampler, _lib.stream())
         ctx.save_for_backward(raw, z, rays_d, noise)
-        ctx.white = int(bool(white_bkgd))
+        ctx.white, ctx.defer = int(bool(white_bkgd)), defer
         outs = (rgb, disp, acc, weights, depth, ent)
         return outs + ((normal,) if normal is not None else ())
 
@@ -153,15 +157,88 @@ class CompositeFn(torch.autograd.Function):
         names = ["g_rgb", "g_disp", "g_acc", "g_weights", "g_depth", "g_entropy", "g_normal"]
         gs = [None if g is None else g.contiguous().float() for g in grads] + [None] * (7 - len(grads))
         graw = torch.empty_like(raw)
-        _lib.call("nerf_composite_bwd", _lib.ptr(raw, "raw"), C, _lib.ptr(z, "z_vals"), _lib.ptr(rays_d, "rays_d"),
-                  _lib.ptr(noise, "noise", allow_none=True), R, S, ctx.white,
-                  *[_lib.ptr(g, n, allow_none=True) for g, n in zip(gs, names)], _lib.ptr(graw, "grad_raw"),
+        job = _lib.CompositeBwdJob(_lib.ptr(raw, "raw"), C, _lib.ptr(z, "z_vals"), _lib.ptr(rays_d, "rays_d"),
+                                   _lib.ptr(noise, "noise", allow_none=True), R, S, ctx.white,
+                                   *[_lib.ptr(g, n, allow_none=True) for g, n in zip(gs, names)],
+                                   _lib.ptr(graw, "grad_raw"))
+        task = torch._C._current_graph_task_id()
+        if ctx.defer and _DEFER["on"] and task != -1 and task != _DEFER["off_task"]:
+            # graw is read only by the field's (deferred) backward: launched with the pass's other
+            # compositing backward as the pass's final callback (field._PendingField)
+            from .field import _pending_field
+            _pending_field(raw.device).add(CompositeJob(job, (raw, z, rays_d, noise, gs, graw)))
+        else:
+            _lib.call("nerf_composite_bwd_batch", (_lib.CompositeBwdJob * 1)(job), 1, _lib.stream())
+        return graw, None, None, None, None, None, None
+
+
+class CompositeJob:
+    """A compositing backward awaiting its launch (nerf_composite_bwd_batch: the fine and the coarse
+    pass's in one launch); `refs` keeps its inputs and output alive until then."""
+
+    def __init__(self, job, refs):
+        self.job, self.refs = job, refs
+        self.stream = torch.cuda.current_stream()
+
+
+def run_composite_jobs(jobs):
+    if jobs:
+        _lib.call("nerf_composite_bwd_batch", (_lib.CompositeBwdJob * len(jobs))(*[j.job for j in jobs]), len(jobs),
                   _lib.stream())
-        return graw, None, None, None, None
 
 
-def raw2outputs(raw, z_vals, rays_d, raw_noise_std=0, white_bkgd=False, pytest=False, predict_normals=False):
-    """run_nerf.py:347-411 -> (rgb_map, disp_map, acc_map, weights, depth_map, sparsity_loss[, normal_map])."""
+_DEFER = {"on": True, "off_task": None}
+
+
+def set_batched_composite_bwd(enabled=True):
+    """Defer the compositing backward of a field's raw output to the pass's final callback, where the
+    fine and the coarse pass's run as one launch (on by default). Taken only for raw straight from the
+    fused field without a normals head (the field's own backward is deferred too, so nothing else reads
+    the raw gradient before the launch); a render_rays raw output that is itself differentiated
+    (retraw) flushes the deferred launch first (_RawGuardFn)."""
+    _DEFER["on"] = bool(enabled)
+
+
+def batched_composite_bwd():
+    return _DEFER["on"]
+
+
+class _RawGuardFn(torch.autograd.Function):
+    """render_rays' raw output (retraw) when the compositing backward of the same raw may be deferred:
+    identity forward; a gradient through it (a loss on raw itself) launches any deferred compositing
+    backward at once and turns deferral off for the rest of the pass, so autograd's sum of the two
+    raw gradients reads a written buffer."""
+
+    @staticmethod
+    def forward(ctx, raw):
+        return raw.view_as(raw)
+
+    @staticmethod
+    def backward(ctx, g):
+        _DEFER["off_task"] = torch._C._current_graph_task_id()
+        from .field import _pending_field
+        _pending_field(g.device).flush_composites()
+        return g
+
+
+_FUSED_SAMPLER = {"on": True}
+
+
+def set_fused_coarse_sampler(enabled=True):
+    """render_rays' coarse compositing and hierarchical sampler in one launch (nerf_composite_sample_fine,
+    on by default; bit-identical to nerf_composite_fwd + nerf_sample_fine_rows)."""
+    _FUSED_SAMPLER["on"] = bool(enabled)
+
+
+def fused_coarse_sampler():
+    return _FUSED_SAMPLER["on"]
+
+
+def raw2outputs(raw, z_vals, rays_d, raw_noise_std=0, white_bkgd=False, pytest=False, predict_normals=False,
+                _sampler=None, _defer=False):
+    """run_nerf.py:347-411 -> (rgb_map, disp_map, acc_map, weights, depth_map, sparsity_loss[, normal_map]).
+    Internal (render_rays): _sampler = its nerf_sample_fine_rows arguments after d_weights' group;
+    _defer = raw reaches nothing but this call and render_rays' guarded raw output."""
     R, S = raw.shape[0], raw.shape[1]
     noise = None
     if raw_noise_std > 0.:
@@ -173,7 +250,8 @@ def raw2outputs(raw, z_vals, rays_d, raw_noise_std=0, white_bkgd=False, pytest=F
         raise ValueError(f"raw2outputs: raw must have 4 or 7 channels, got {raw.shape[-1]}")
     if not predict_normals and raw.shape[-1] == 7:
         raw = raw[..., :4]      # the reference reads channels 0..3 only
-    outs = CompositeFn.apply(raw.float(), z_vals, rays_d, noise, white_bkgd)
+    defer = _defer and bool(getattr(raw, "_nerf_field_raw", False)) and raw.dtype == torch.float32
+    outs = CompositeFn.apply(raw.float(), z_vals, rays_d, noise, white_bkgd, _sampler, defer)
     if predict_normals:
         if raw.shape[-1] == 4:
             # the reference slices raw[..., 4:7] of a 4-channel raw (the coarse net has no normals
@@ -302,14 +380,8 @@ def render_rays(ray_batch, network_fn, network_query_fn, N_samples, embed_fn=Non
         del pts._nerf_reuse
         if reuse.state != "recorded" or R * (N_samples + N_importance) > 2 ** 31 - 1:
             reuse = None
-    outs = raw2outputs(raw, z, rays_d, raw_noise_std, white_bkgd, pytest=pytest, predict_normals=predict_normals)
-    rgb_map, disp_map, acc_map, weights, depth_map, sparsity_loss = outs[:6]
-    normal_map = outs[6] if predict_normals else None
-
     ret = {}
     if N_importance > 0:
-        rgb_map_0, depth_map_0, acc_map_0, sparsity_loss_0, normal_map_0 = (rgb_map, depth_map, acc_map,
-                                                                             sparsity_loss, normal_map)
         det = perturb == 0.
         M = N_samples + N_importance
         z_fine = torch.empty(R, M, **f)
@@ -324,13 +396,21 @@ def render_rays(ray_batch, network_fn, network_query_fn, N_samples, embed_fn=Non
             reuse.inv, reuse.imp_pts = torch.empty(R * M, **i32), torch.empty(R, N_importance, 3, **f)
             reuse.state = "rows"
         inv = None if reuse is None else reuse.inv
-        _lib.call("nerf_sample_fine_rows", _lib.ptr(rays, "ray_batch"), C, _lib.ptr(z, "z"),
-                  _lib.ptr(weights.detach().contiguous(), "weights"), R, N_samples, N_importance, int(det),
-                  _lib.ptr(t_imp, "t", allow_none=True), _lib.ptr(u_imp, "u", allow_none=True), seed, off, rng,
-                  _lib.ptr(z_fine, "z_fine"), _lib.ptr(pts_fine, "pts_fine"), _lib.ptr(z_std, "z_std"), None,
-                  None if inv is None else _lib.ptr_at(inv, R * N_importance, "coarse_rows", torch.int32),
-                  _lib.ptr(inv, "imp_rows", torch.int32, True),
-                  _lib.ptr(None if reuse is None else reuse.imp_pts, "imp_pts", allow_none=True), None, _lib.stream())
+        # nerf_sample_fine_rows' arguments after (d_z, d_weights, n_rays, n_samples)
+        samp = (N_importance, int(det), _lib.ptr(t_imp, "t", allow_none=True), _lib.ptr(u_imp, "u", allow_none=True),
+                seed, off, rng, _lib.ptr(z_fine, "z_fine"), _lib.ptr(pts_fine, "pts_fine"), _lib.ptr(z_std, "z_std"),
+                None, None if inv is None else _lib.ptr_at(inv, R * N_importance, "coarse_rows", torch.int32),
+                _lib.ptr(inv, "imp_rows", torch.int32, True),
+                _lib.ptr(None if reuse is None else reuse.imp_pts, "imp_pts", allow_none=True), None)
+        fused = _FUSED_SAMPLER["on"]
+        outs = raw2outputs(raw, z, rays_d, raw_noise_std, white_bkgd, pytest=pytest, predict_normals=predict_normals,
+                           _sampler=(_lib.ptr(rays, "ray_batch"), C) + samp if fused else None, _defer=True)
+        weights = outs[3]
+        if not fused:
+            _lib.call("nerf_sample_fine_rows", _lib.ptr(rays, "ray_batch"), C, _lib.ptr(z, "z"),
+                      _lib.ptr(weights.detach().contiguous(), "weights"), R, N_samples, *samp, _lib.stream())
+        rgb_map_0, _, acc_map_0, _, depth_map_0, sparsity_loss_0 = outs[:6]
+        normal_map_0 = outs[6] if predict_normals else None
         z, pts = z_fine, pts_fine
         run_fn = network_fn if network_fine is None else network_fine
         if reuse is not None:
@@ -340,19 +420,25 @@ def render_rays(ray_batch, network_fn, network_query_fn, N_samples, embed_fn=Non
             del pts._nerf_reuse
             reuse.release_forward()
         _REUSE["last"] = reuse is not None and reuse.used
-        outs = raw2outputs(raw, z, rays_d, raw_noise_std, white_bkgd, pytest=pytest, predict_normals=predict_normals)
+        outs = raw2outputs(raw, z, rays_d, raw_noise_std, white_bkgd, pytest=pytest, predict_normals=predict_normals,
+                           _defer=True)
         rgb_map, disp_map, acc_map, weights, depth_map, sparsity_loss = outs[:6]
         normal_map = outs[6] if predict_normals else None
         ret.update(rgb0=rgb_map_0, depth0=depth_map_0, acc0=acc_map_0, sparsity_loss0=sparsity_loss_0, z_std=z_std)
         if predict_normals:
             ret["normal0"] = normal_map_0
+    else:
+        outs = raw2outputs(raw, z, rays_d, raw_noise_std, white_bkgd, pytest=pytest, predict_normals=predict_normals,
+                           _defer=True)
+        rgb_map, disp_map, acc_map, weights, depth_map, sparsity_loss = outs[:6]
+        normal_map = outs[6] if predict_normals else None
 
     ret.update(rgb_map=rgb_map, depth_map=depth_map, acc_map=acc_map, sparsity_loss=sparsity_loss, pts=pts,
                rays_d=rays_d)
     if predict_normals:
         ret["normal_map"] = normal_map
     if retraw:
-        ret["raw"] = raw
+        ret["raw"] = _RawGuardFn.apply(raw) if getattr(raw, "_nerf_field_raw", False) else raw
     if DEBUG:
         check_numerics(ret)
     return ret
