@@ -240,6 +240,12 @@ def parse():
                          "(render.set_fused_coarse_sampler)")
     ap.add_argument("--batched-composite", type=int, default=1,
                     help="1: the fine and coarse compositing backwards in one launch (render.set_batched_composite_bwd)")
+    ap.add_argument("--sh-rows", type=int, default=1,
+                    help="1: per-ray SH4 rows written by the stratified sampler, loaded by the MLP kernels "
+                         "(render.set_sh_rows)")
+    ap.add_argument("--fold-fills", type=int, default=1,
+                    help="1: the step's gradient and TV-accumulator zero fills run inside render()'s first launch "
+                         "(_lib.set_fold_fills)")
     ap.add_argument("--overlap", type=int, default=1,
                     help="N>1 with --zero 1: reduce-scatter the first gradient bucket while the owner pass sums the "
                          "second (dist.ShardedOptimizer(overlap=True)); 0 = one reduce-scatter after the backward")
@@ -461,6 +467,8 @@ def main():
     nerf.set_fused_coarse_sampler(bool(a.fused_sampler))
     nerf.set_batched_composite_bwd(bool(a.batched_composite))
     nerf.set_active_points(bool(a.active_points))
+    _lib.set_fold_fills(bool(a.fold_fills))
+    nerf.set_sh_rows(bool(a.sh_rows))
     kw, kw_test, _, grad_vars, opt = nerf.create_nerf(args, device=dev)
     for d in (kw, kw_test):
         d.update(near=wl["near"], far=wl["far"])     # train() adds the scene bounds (run_nerf.py:768-770,865-869)

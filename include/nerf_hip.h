@@ -208,7 +208,9 @@ int nerf_sh4_fwd(const float* d_dirs, int64_t n, float* d_out /* [n,16] */, void
  * c1 [64,64], c2 [3,64] (create_nerf's NeRFSmall(num_layers=2, num_layers_color=3)).
  * Input point p: hash features x[p][k] = d_feat[p*feat_stride_point + (k/2)*feat_stride_level + k%2]
  * (k < 32); view encoding: if d_viewdirs != NULL, SH4 of d_viewdirs[p / samples_per_ray] is
- * computed in-kernel, else sh[p][k] = d_sh[p*sh_stride + k] (k < 16).
+ * computed in-kernel, else sh[p][k] = d_sh[p*sh_stride + k] (k < 16) — or, with sh_stride == 0, the
+ * per-RAY rows sh[p][k] = d_sh[16*(p / samples_per_ray) + k] (16-B aligned; the point order's two
+ * segments as for d_viewdirs), e.g. nerf_sample_stratified_sh's d_sh.
  * d_keep may be NULL (keep all). Output d_raw [P,4] = [rgb_raw(3), sigma_raw].
  */
 typedef struct {
@@ -398,6 +400,14 @@ int nerf_sample_stratified(const float* d_rays, int64_t ray_stride, int64_t n_ra
                            float* d_viewdirs /* optional [R,3]: the last 3 ray columns (stride > 8) */,
                            void* stream);
 
+/* Same, also writing d_sh [R,16] = SH4 of each ray's view direction (the last 3 columns; needs
+ * ray_stride > 8; hash_encoding.py:153-191): the per-ray rows the MLP entries take with sh_stride 0. */
+int nerf_sample_stratified_sh(const float* d_rays, int64_t ray_stride, int64_t n_rays, int n_samples,
+                              const float* d_t, int lindisp, int perturb, const float* d_u,
+                              uint64_t seed, uint64_t offset, const uint64_t* d_rng,
+                              float* d_z, float* d_pts, float* d_dirs, float* d_viewdirs, float* d_sh,
+                              void* stream);
+
 /* sample_pdf (run_nerf_helpers.py:354-397) on bins [R,n_bins], weights [R,n_bins-1];
  * det: u = d_t_imp (torch.linspace(0,1,N) values, [N]); else u = d_u [R,N] or Philox. */
 int nerf_sample_pdf(const float* d_bins, int64_t bins_stride, const float* d_weights, int64_t weights_stride,
@@ -466,6 +476,13 @@ int nerf_sample_rays(const nerf_camera* cam, int H, int W, int crop_r0, int crop
  * (8 floats without viewdirs). d_rays_o/d [n,3]; d_out [n, 11 | 8]. */
 int nerf_rays_pack(const float* d_rays_o, const float* d_rays_d, int64_t n_rays, float near, float far,
                    int ndc, float ndc_coef_w, float ndc_coef_h, int use_viewdirs, float* d_out, void* stream);
+/* Same, also storing 0.0f over up to NERF_MAX_ZERO_RANGES float ranges in the same launch: a training
+ * step's gradient / loss-accumulator zero fills, folded into its first launch (_lib.defer_fill_zero). */
+#define NERF_MAX_ZERO_RANGES 4
+typedef struct nerf_zero_range { float* ptr; int64_t n; } nerf_zero_range;
+int nerf_rays_pack_z(const float* d_rays_o, const float* d_rays_d, int64_t n_rays, float near, float far,
+                     int ndc, float ndc_coef_w, float ndc_coef_h, int use_viewdirs, float* d_out,
+                     const nerf_zero_range* zeros, int n_zeros, void* stream);
 
 /* ---- RAdam (PocketNeRF/radam.py:28-94), one launch over up to 32 tensor segments ----------
  * Per segment: p, g, m (exp_avg), v (exp_avg_sq) of n elements. The host evaluates the scalar

@@ -57,6 +57,13 @@ class CompositeBwdJob(ctypes.Structure):
                 ("g_entropy", c_vp), ("g_normal", c_vp), ("graw", c_vp)]
 
 
+class ZeroRange(ctypes.Structure):
+    _fields_ = [("ptr", c_vp), ("n", c_i64)]
+
+
+MAX_ZERO_RANGES = 4
+
+
 class PriorsConfig(ctypes.Structure):
     """nerf_priors_config (include/nerf_hip.h)."""
     _fields_ = [("use_manhattan", c_int), ("use_planarity", c_int), ("use_consistency", c_int),
@@ -156,6 +163,8 @@ SIGNATURES = {
                                    c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
     "nerf_sample_stratified": [c_vp, c_i64, c_i64, c_int, c_vp, c_int, c_int, c_vp, c_u64, c_u64, c_vp, c_vp, c_vp,
                                c_vp, c_vp, c_vp],
+    "nerf_sample_stratified_sh": [c_vp, c_i64, c_i64, c_int, c_vp, c_int, c_int, c_vp, c_u64, c_u64, c_vp, c_vp, c_vp,
+                                  c_vp, c_vp, c_vp, c_vp],
     "nerf_sample_pdf": [c_vp, c_i64, c_vp, c_i64, c_i64, c_int, c_int, c_int, c_vp, c_vp, c_u64, c_u64, c_vp, c_vp,
                         c_vp],
     "nerf_sample_fine": [c_vp, c_i64, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_vp, c_vp, c_u64, c_u64, c_vp,
@@ -164,6 +173,8 @@ SIGNATURES = {
                               c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
     "nerf_sample_rays": [ctypes.POINTER(Camera), c_int, c_int, c_int, c_int, c_int, c_int, c_i64, c_int, c_u64,
                          c_u64, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp],
+    "nerf_rays_pack_z": [c_vp, c_vp, c_i64, ctypes.c_float, ctypes.c_float, c_int, ctypes.c_float, ctypes.c_float,
+                         c_int, c_vp, ctypes.POINTER(ZeroRange), c_int, c_vp],
     "nerf_rays_pack": [c_vp, c_vp, c_i64, ctypes.c_float, ctypes.c_float, c_int, ctypes.c_float, ctypes.c_float,
                        c_int, c_vp, c_vp],
     "nerf_radam_step": [ctypes.POINTER(RAdamSegment), c_int, c_vp, c_vp],
@@ -276,6 +287,53 @@ def call(name, *args):
 
 def stream():
     return c_vp(torch.cuda.current_stream().cuda_stream)
+
+
+# Zero fills folded into a later launch (nerf_rays_pack_z: render()'s first kernel): a training step
+# registers its MLP-gradient zero and its TV loss accumulator here before render(), and whoever needs
+# one of them zero before that launch took it calls flush_zero_fills first.
+_ZERO_FILLS = []
+_FOLD_FILLS = {"on": True}
+
+
+def set_fold_fills(enabled=True):
+    """Fold deferrable zero fills into render()'s first launch (default); off = fill at once."""
+    _FOLD_FILLS["on"] = bool(enabled)
+
+
+def defer_fill_zero(t):
+    """Zero the contiguous float32 CUDA tensor `t` in the next nerf_rays_pack_z launch (or at
+    flush_zero_fills, whichever comes first)."""
+    if not (_FOLD_FILLS["on"] and t.is_cuda and t.dtype == torch.float32 and t.is_contiguous()):
+        t.zero_()
+        return
+    _ZERO_FILLS.append(t)
+
+
+def take_zero_fills():
+    """Up to MAX_ZERO_RANGES pending fills as a ZeroRange array (ctypes) + count; they are done by the
+    caller's launch."""
+    taken = _ZERO_FILLS[:MAX_ZERO_RANGES]
+    del _ZERO_FILLS[:MAX_ZERO_RANGES]
+    arr = (ZeroRange * max(1, len(taken)))(*[ZeroRange(t.data_ptr(), t.numel()) for t in taken])
+    return arr, len(taken), taken
+
+
+def flush_zero_fills(tensors=None):
+    """Zero pending fills now: those overlapping the given tensors, or all."""
+    global _ZERO_FILLS
+    if tensors is None:
+        todo, _ZERO_FILLS = _ZERO_FILLS, []
+    else:
+        spans = [(t.data_ptr(), t.data_ptr() + t.numel() * t.element_size()) for t in tensors]
+
+        def hit(z):
+            a, b = z.data_ptr(), z.data_ptr() + z.numel() * 4
+            return any(a < e and s < b for s, e in spans)
+        todo = [z for z in _ZERO_FILLS if hit(z)]
+        _ZERO_FILLS = [z for z in _ZERO_FILLS if not hit(z)]
+    for z in todo:
+        z.zero_()
 
 
 def ptr(t, name="tensor", dtype=torch.float32, allow_none=False):

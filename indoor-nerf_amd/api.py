@@ -14,7 +14,7 @@ from .scene import get_bbox3d_for_blenderobj, get_bbox3d_for_llff
 from .render import (batchify_rays, camera, check_numerics, set_debug, get_rays, get_rays_np, img2mse, manual_seed, mse2psnr, ndc_rays, raw2outputs,
                      render, render_path, render_rays, sample_pdf, set_coarse_reuse, coarse_reuse, to8b,
                      set_fused_coarse_sampler, fused_coarse_sampler, set_batched_composite_bwd,
-                     batched_composite_bwd)
+                     batched_composite_bwd, set_sh_rows, sh_rows)
 from .data import load_blender_data, load_llff_data, load_scannet_data, pose_spherical
 from .priors import (ManhattanFrameEstimator, SemanticPlaneDetector, combine_structural_losses_v2, manhattan_sdf_loss,
                      spatial_normal_consistency_loss, structured_planarity_loss)
@@ -30,7 +30,7 @@ __all__ = ["HashEmbedder", "SHEncoder", "NeRFSmall", "RAdam", "run_network", "ba
            "combine_structural_losses_v2", "manhattan_sdf_loss", "spatial_normal_consistency_loss",
            "structured_planarity_loss", "set_deterministic", "deterministic", "check_numerics", "set_debug",
            "set_coarse_reuse", "coarse_reuse", "set_fused_coarse_sampler", "fused_coarse_sampler",
-           "set_batched_composite_bwd", "batched_composite_bwd", "set_active_points", "active_points", "set_fused_table_step",
+           "set_batched_composite_bwd", "batched_composite_bwd", "set_sh_rows", "sh_rows", "set_active_points", "active_points", "set_fused_table_step",
            "fused_table_step_enabled"]
 
 

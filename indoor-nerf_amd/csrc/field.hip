@@ -31,6 +31,8 @@ static int fill_args(MlpArgs& a, const float* d_feat, int64_t sp, int64_t sl, co
     NERF_REQUIRE((n == 0 || d_feat) && w && w->w0 && w->w1 && w->c0 && w->c1 && w->c2, "mlp: null feature/weight pointer");
     NERF_REQUIRE(n == 0 || d_viewdirs || d_sh, "mlp: need d_sh or d_viewdirs");
     NERF_REQUIRE(!d_viewdirs || spr >= 1, "mlp: samples_per_ray must be >= 1");
+    NERF_REQUIRE(d_viewdirs || sh_stride != 0 || spr >= 1, "mlp: per-ray SH rows need samples_per_ray >= 1");
+    NERF_REQUIRE(d_viewdirs || sh_stride != 0 || ((uintptr_t)d_sh & 15) == 0, "mlp: per-ray SH rows must be 16-B aligned");
     a.feat = d_feat; a.sp = sp; a.sl = sl; a.sh = d_sh; a.sh_stride = sh_stride;
     a.viewdirs = d_viewdirs; a.spr = spr; a.keep = d_keep; a.P = n; a.W = *w;
     a.dsp = sp; a.dsl = sl;

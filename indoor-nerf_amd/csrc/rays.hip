@@ -95,11 +95,11 @@ struct PackArgs {
     float cw, ch;          // float32(-1/(W/(2 focal))), float32(-1/(H/(2 focal)))
     float* out;
     int stride;            // 8 or 11
+    nerf_zero_range zero[NERF_MAX_ZERO_RANGES];   // fills folded into this launch (render's first)
+    int n_zero;
 };
 
-__global__ void __launch_bounds__(256) rays_pack_kernel(PackArgs a) {
-    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= a.n) return;
+__device__ __forceinline__ void pack_ray(const PackArgs& a, int64_t r) {
     float ox = a.o[3 * r], oy = a.o[3 * r + 1], oz = a.o[3 * r + 2];
     float dx = a.d[3 * r], dy = a.d[3 * r + 1], dz = a.d[3 * r + 2];
     float* dst = a.out + r * a.stride;
@@ -123,6 +123,16 @@ __global__ void __launch_bounds__(256) rays_pack_kernel(PackArgs a) {
     dst[3] = dx; dst[4] = dy; dst[5] = dz;
     dst[6] = a.near;
     dst[7] = a.far;
+}
+
+__global__ void __launch_bounds__(256) rays_pack_kernel(PackArgs a) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < a.n) pack_ray(a, t);
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int k = 0; k < a.n_zero; ++k) {
+        float* z = a.zero[k].ptr;
+        for (int64_t i = t; i < a.zero[k].n; i += stride) z[i] = 0.0f;
+    }
 }
 
 static uint32_t splitmix(uint64_t& s) {
@@ -163,14 +173,32 @@ extern "C" int nerf_sample_rays(const nerf_camera* cam, int H, int W, int crop_r
     return NERF_OK;
 }
 
+extern "C" int nerf_rays_pack_z(const float* d_rays_o, const float* d_rays_d, int64_t n_rays, float near, float far,
+                                int ndc, float ndc_coef_w, float ndc_coef_h, int use_viewdirs, float* d_out,
+                                const nerf_zero_range* zeros, int n_zeros, void* stream) {
+    NERF_REQUIRE(n_rays >= 0 && (n_rays == 0 || (d_rays_o && d_rays_d && d_out)), "rays_pack: bad args");
+    NERF_REQUIRE(n_zeros >= 0 && n_zeros <= NERF_MAX_ZERO_RANGES && (n_zeros == 0 || zeros),
+                 "rays_pack: %d zero ranges (at most %d)", n_zeros, NERF_MAX_ZERO_RANGES);
+    PackArgs a{d_rays_o, d_rays_d, n_rays, near, far, ndc ? 1 : 0, use_viewdirs ? 1 : 0, ndc_coef_w, ndc_coef_h,
+               d_out, use_viewdirs ? 11 : 8, {}, 0};
+    int64_t most = 0;
+    for (int k = 0; k < n_zeros; ++k) {
+        NERF_REQUIRE(zeros[k].n >= 0 && (zeros[k].n == 0 || zeros[k].ptr), "rays_pack: zero range %d", k);
+        if (zeros[k].n == 0) continue;
+        a.zero[a.n_zero++] = zeros[k];
+        most = std::max(most, zeros[k].n);
+    }
+    if (n_rays == 0 && a.n_zero == 0) return NERF_OK;
+    // the rays' threads, or enough for 16 values each of the largest range (at most 1024 blocks)
+    const unsigned blocks = std::max(blocks_for(n_rays, 256), std::min(1024u, blocks_for(most, 256 * 16)));
+    hipLaunchKernelGGL(rays_pack_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), a);
+    NERF_CHECK_LAUNCH("rays_pack");
+    return NERF_OK;
+}
+
 extern "C" int nerf_rays_pack(const float* d_rays_o, const float* d_rays_d, int64_t n_rays, float near, float far,
                               int ndc, float ndc_coef_w, float ndc_coef_h, int use_viewdirs, float* d_out,
                               void* stream) {
-    NERF_REQUIRE(n_rays >= 0 && (n_rays == 0 || (d_rays_o && d_rays_d && d_out)), "rays_pack: bad args");
-    if (n_rays == 0) return NERF_OK;
-    PackArgs a{d_rays_o, d_rays_d, n_rays, near, far, ndc ? 1 : 0, use_viewdirs ? 1 : 0, ndc_coef_w, ndc_coef_h,
-               d_out, use_viewdirs ? 11 : 8};
-    hipLaunchKernelGGL(rays_pack_kernel, dim3(blocks_for(n_rays, 256)), dim3(256), 0, as_stream(stream), a);
-    NERF_CHECK_LAUNCH("rays_pack");
-    return NERF_OK;
+    return nerf_rays_pack_z(d_rays_o, d_rays_d, n_rays, near, far, ndc, ndc_coef_w, ndc_coef_h, use_viewdirs, d_out,
+                            nullptr, 0, stream);
 }

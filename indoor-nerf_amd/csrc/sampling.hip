@@ -1,6 +1,7 @@
 // Ray sampling of render_rays: stratified depths (PocketNeRF/run_nerf.py:466-490) and the
 // hierarchical step (run_nerf.py:508-513 + sample_pdf, run_nerf_helpers.py:354-397 + z_std :541).
 #include "composite_common.h"
+#include "field_common.h"
 
 namespace nerf {
 
@@ -11,6 +12,7 @@ struct StratArgs {
     float* z; float* pts;
     float* dirs;       // optional [R,3]: the rays' directions (columns 3..5), contiguous
     float* viewdirs;   // optional [R,3]: the rays' view directions (the last three columns)
+    float* sh;         // optional [R,16]: SH4 of the view directions (field_common.h sh4_eval)
 };
 
 __device__ __forceinline__ float base_depth(float near, float far, float t, int lindisp) {
@@ -44,6 +46,16 @@ __global__ void __launch_bounds__(256) sample_stratified_kernel(StratArgs a) {
         if (a.viewdirs) {
             const float* v = ray + a.stride - 3;
             a.viewdirs[3 * r + 0] = v[0]; a.viewdirs[3 * r + 1] = v[1]; a.viewdirs[3 * r + 2] = v[2];
+        }
+        if (a.sh) {
+            const float* v = ray + a.stride - 3;
+            float o[16];
+            sh4_eval(v[0], v[1], v[2], o);
+            float4* dst = reinterpret_cast<float4*>(a.sh + 16 * r);
+            dst[0] = make_float4(o[0], o[1], o[2], o[3]);
+            dst[1] = make_float4(o[4], o[5], o[6], o[7]);
+            dst[2] = make_float4(o[8], o[9], o[10], o[11]);
+            dst[3] = make_float4(o[12], o[13], o[14], o[15]);
         }
     }
     if (a.pts) {
@@ -345,14 +357,24 @@ extern "C" int nerf_sample_stratified(const float* d_rays, int64_t ray_stride, i
                                       const float* d_t, int lindisp, int perturb, const float* d_u, uint64_t seed,
                                       uint64_t offset, const uint64_t* d_rng, float* d_z, float* d_pts,
                                       float* d_dirs, float* d_viewdirs, void* stream) {
+    return nerf_sample_stratified_sh(d_rays, ray_stride, n_rays, n_samples, d_t, lindisp, perturb, d_u, seed, offset,
+                                     d_rng, d_z, d_pts, d_dirs, d_viewdirs, nullptr, stream);
+}
+
+extern "C" int nerf_sample_stratified_sh(const float* d_rays, int64_t ray_stride, int64_t n_rays, int n_samples,
+                                         const float* d_t, int lindisp, int perturb, const float* d_u, uint64_t seed,
+                                         uint64_t offset, const uint64_t* d_rng, float* d_z, float* d_pts,
+                                         float* d_dirs, float* d_viewdirs, float* d_sh, void* stream) {
     NERF_REQUIRE(n_rays >= 0 && n_samples >= 1, "sample_stratified: R=%lld S=%d", (long long)n_rays, n_samples);
     NERF_REQUIRE(ray_stride >= 8, "sample_stratified: ray_stride %lld < 8", (long long)ray_stride);
     if (n_rays == 0) return NERF_OK;   // empty batches: nothing is read or written (NULL data allowed)
     NERF_REQUIRE(d_rays && d_t && d_z, "sample_stratified: null arg");
     NERF_REQUIRE(!d_viewdirs || ray_stride > 8, "sample_stratified: viewdirs need ray_stride > 8 (got %lld)",
                  (long long)ray_stride);
+    NERF_REQUIRE(!d_sh || (ray_stride > 8 && ((uintptr_t)d_sh & 15) == 0),
+                 "sample_stratified: SH rows need ray_stride > 8 and 16-B alignment");
     StratArgs a{d_rays, ray_stride, n_rays, n_samples, d_t, lindisp, perturb, d_u, seed, offset, d_rng, d_z, d_pts,
-                d_dirs, d_viewdirs};
+                d_dirs, d_viewdirs, d_sh};
     hipLaunchKernelGGL(sample_stratified_kernel, dim3(blocks_for(n_rays * n_samples, 256)), dim3(256), 0,
                        as_stream(stream), a);
     NERF_CHECK_LAUNCH("sample_stratified");

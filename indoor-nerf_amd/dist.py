@@ -13,6 +13,8 @@ import os
 import torch
 import torch.distributed as dist
 
+from . import _lib
+
 
 def env_rank_world():
     return int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1)), int(os.environ.get("LOCAL_RANK", 0))
@@ -92,8 +94,10 @@ class GradArena:
 
     def zero_(self):
         if self.deferred:
+            # deferred zero: the tables' by the iteration's owner pass (it stores every row), the dense
+            # rest by render()'s first launch (_lib.defer_fill_zero) or before the backward at the latest
             from .hashgrid import defer_zero
-            self.flat[:self.zero_end].zero_()
+            _lib.defer_fill_zero(self.flat[:self.zero_end])
             defer_zero(self.deferred)
         else:
             self.flat.zero_()

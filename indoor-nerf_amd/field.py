@@ -179,6 +179,7 @@ class FieldFn(torch.autograd.Function):
         n_tab = embedder.n_levels
         tables, weights, head = params[:n_tab], params[n_tab:n_tab + 5], params[n_tab + 5:]
         pts = pts.contiguous()
+        sh_rays = getattr(viewdirs, "_nerf_sh", None)   # render_rays' per-ray SH4 rows (sh_stride 0)
         viewdirs = viewdirs.contiguous()
         P = pts.shape[0]
         dev = pts.device
@@ -216,8 +217,11 @@ class FieldFn(torch.autograd.Function):
         keep_arg = None if head else _lib.ptr(keep, "keep", dtype=torch.bool)
         if head and order is not None:
             keep = torch.empty_like(keep).index_put_((order[0].long(),), keep)
-        feat_args = (_lib.ptr_at(feat, 2 * row0, "feat"), 2, sl, None, 0, _lib.ptr(viewdirs, "viewdirs"), spr,
-                     keep_arg)
+        if sh_rays is not None:
+            view_args = (_lib.ptr(sh_rays, "sh_rows"), 0, None)
+        else:
+            view_args = (None, 0, _lib.ptr(viewdirs, "viewdirs"))
+        feat_args = (_lib.ptr_at(feat, 2 * row0, "feat"), 2, sl, *view_args, spr, keep_arg)
         w0q, arec = net.quant_state(lambda w0q: _act_calibration(feat_args, P, weights, w0q, n_calib))
         _lib.call("nerf_mlp_fwd_ord", *feat_args, P, _weights_struct(weights, w0q), _lib.ptr(raw, "raw"),
                   _lib.ptr(o16, "geo", allow_none=True), _lib.ptr(arec, "act_record", allow_none=True), None, 0,
@@ -226,6 +230,7 @@ class FieldFn(torch.autograd.Function):
             raw = _head_forward(o16, raw, keep, head)
         ctx.save_for_backward(pts, viewdirs, feat, keep, o16, w0q, arec, *params)
         ctx.spr, ctx.embedder, ctx.n_tab, ctx.n_head = spr, embedder, n_tab, len(head)
+        ctx.sh_rays = sh_rays
         ctx.frow0, ctx.order = row0, order
         ctx.eval_quant = net.use_quantization and not net.training
         ctx.zero_tab_grad = embedder.quantization_active() and not embedder.training
@@ -261,6 +266,7 @@ class _FieldJob:
         self.pts, self.viewdirs, self.feat, self.keep, self.head = pts, viewdirs, feat, keep, head
         self.w0q, self.arec, self.weights, self.tables, self.g, self.dgeo = w0q, arec, weights, tables, g, dgeo
         self.spr, self.meta, self.need_w, self.need_tab = ctx.spr, ctx.embedder._meta, need_w, need_tab
+        self.sh_rays = ctx.sh_rays
         self.reuse = ctx.reuse     # (role, render.CoarseReuse) or None
         self.frow0, self.order = ctx.frow0, ctx.order   # feature rows from frow0 of feat; the MLP's point order
         self.stream = torch.cuda.current_stream()
@@ -277,7 +283,11 @@ class _FieldJob:
         j.dfeat_stride_point, j.dfeat_stride_level = 2, 2 * P
         if self.order is not None:
             j.order = _point_order(self.order)
-        j.viewdirs, j.samples_per_ray = _lib.ptr(self.viewdirs, "viewdirs"), self.spr
+        if self.sh_rays is not None:   # per-ray SH rows (sh_stride 0)
+            j.sh, j.sh_stride, j.viewdirs = _lib.ptr(self.sh_rays, "sh_rows"), 0, None
+        else:
+            j.viewdirs = _lib.ptr(self.viewdirs, "viewdirs")
+        j.samples_per_ray = self.spr
         j.keep = None if self.head else _lib.ptr(self.keep, "keep", dtype=torch.bool)
         j.n_points = P
         j.weights = _weights_struct(self.weights, self.w0q)

@@ -42,7 +42,9 @@ def defer_zero(grads):
 
 
 def materialize_zero(grads=None):
-    """Zero deferred gradients now: the given ones (those of them that are deferred), or all."""
+    """Zero deferred gradients now: the given ones (those of them that are deferred), or all (and every
+    pending dense fill, _lib.defer_fill_zero)."""
+    _lib.flush_zero_fills(grads)
     keys = list(_DEFERRED) if grads is None else [g.data_ptr() for g in grads if g.data_ptr() in _DEFERRED]
     for k in keys:
         _DEFERRED.pop(k).zero_()

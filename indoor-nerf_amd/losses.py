@@ -28,7 +28,7 @@ class TVFn(torch.autograd.Function):
     """min_vertex: host [L,3] cuboid corners, or an int device address of [L,3] int64 slots that a
     captured step refreshes before every replay (graphs.StepScalars)."""
     @staticmethod
-    def forward(ctx, min_vertex, cubes, log2_T, *tables):
+    def forward(ctx, min_vertex, cubes, log2_T, out, *tables):
         L = len(tables)
         if isinstance(min_vertex, int):
             mv, dmv = None, _lib.c_vp(min_vertex)
@@ -38,7 +38,11 @@ class TVFn(torch.autograd.Function):
         dev = tables[0].device
         # the cuboid vertices' rows, gathered once here: the backward's stencil reads them densely
         verts = torch.empty(2 * sum((int(c) + 1) ** 3 for c in cubes), device=dev, dtype=torch.float32)
-        loss = torch.zeros(L, device=dev, dtype=torch.float32)
+        if out is None:
+            loss = torch.zeros(L, device=dev, dtype=torch.float32)
+        else:   # a zeroed accumulator (tv_accumulator: its fill rides along in render()'s first launch)
+            _lib.flush_zero_fills([out])
+            loss = out
         _lib.call("nerf_tv_fwd", _lib.ptr_array(tables), L, log2_T, mv, dmv, cb, _lib.ptr(loss, "loss"),
                   _lib.ptr(verts, "tv_verts"), _lib.stream())
         ctx.save_for_backward(*tables)
@@ -72,7 +76,7 @@ class TVFn(torch.autograd.Function):
                 hashgrid.materialize_zero(grads)
                 _lib.call("nerf_tv_bwd", _lib.ptr_array(tables), L, ctx.log2_T, ctx.mv, ctx.dmv, ctx.cb,
                           _lib.ptr(g, "grad_loss"), _lib.ptr_array(grads, "grad_tables"), _lib.stream())
-        return (None, None, None) + (None,) * len(tables)
+        return (None, None, None, None) + (None,) * len(tables)
 
 
 class TVBinJob:
@@ -96,8 +100,17 @@ def draw_min_vertices(embedder, generator=None):
     return torch.stack(mvs), cubes
 
 
-def total_variation_all(embedder, min_vertex=None, generator=None):
-    """Per-level TV losses [L] of all levels of `embedder` (sum them for the reference's TV_loss)."""
+def tv_accumulator(embedder):
+    """The [L] loss accumulator of a later total_variation_all(..., out=), its zero fill deferred to the
+    next render()'s first launch (_lib.defer_fill_zero): a training step allocates it before render."""
+    acc = torch.empty(embedder.n_levels, device=embedder.tables()[0].device, dtype=torch.float32)
+    _lib.defer_fill_zero(acc)
+    return acc
+
+
+def total_variation_all(embedder, min_vertex=None, generator=None, out=None):
+    """Per-level TV losses [L] of all levels of `embedder` (sum them for the reference's TV_loss).
+    out: an accumulator from tv_accumulator (None: a fresh zeroed one)."""
     from . import graphs
     sc = graphs.active()
     if sc is not None and min_vertex is None:
@@ -110,13 +123,13 @@ def total_variation_all(embedder, min_vertex=None, generator=None):
             hi[off:off + 3 * L] = mv.reshape(-1).numpy()
         sc.add_filler(fill)
         cubes = [tv_cube(l, embedder.base_resolution, embedder.finest_resolution, L)[1] for l in range(L)]
-        return TVFn.apply(ptr, cubes, embedder.log2_hashmap_size, *embedder.tables())
+        return TVFn.apply(ptr, cubes, embedder.log2_hashmap_size, out, *embedder.tables())
     if min_vertex is None:
         min_vertex, cubes = draw_min_vertices(embedder, generator)
     else:
         cubes = [tv_cube(l, embedder.base_resolution, embedder.finest_resolution, embedder.n_levels)[1]
                  for l in range(embedder.n_levels)]
-    return TVFn.apply(torch.as_tensor(min_vertex), cubes, embedder.log2_hashmap_size, *embedder.tables())
+    return TVFn.apply(torch.as_tensor(min_vertex), cubes, embedder.log2_hashmap_size, out, *embedder.tables())
 
 
 def total_variation_loss(embeddings, min_resolution, max_resolution, level, log2_hashmap_size, n_levels=16,
@@ -125,7 +138,7 @@ def total_variation_loss(embeddings, min_resolution, max_resolution, level, log2
     res, cube = tv_cube(level, min_resolution, max_resolution, n_levels)
     if min_vertex is None:
         min_vertex = torch.randint(0, res - cube, (3,))
-    return TVFn.apply(torch.as_tensor(min_vertex).reshape(1, 3), [cube], log2_hashmap_size, embeddings.weight)[0]
+    return TVFn.apply(torch.as_tensor(min_vertex).reshape(1, 3), [cube], log2_hashmap_size, None, embeddings.weight)[0]
 
 
 class TrainLossFn(torch.autograd.Function):

@@ -13,7 +13,7 @@ import torch
 
 from .field import NeRFSmall, run_network
 from .hashgrid import HashEmbedder, SHEncoder
-from .losses import total_variation_all, train_loss
+from .losses import total_variation_all, train_loss, tv_accumulator
 from .optim import RAdam
 from .render import render
 from . import _lib, hashgrid
@@ -177,15 +177,20 @@ def forward_backward(batch_rays, target_s, render_kwargs_train, optimizer, args,
     """render (coarse+fine), zero grads, img/img0 MSE + sparsity + TV (run_nerf.py:1007-1037),
     backward. Returns (loss, img_loss, psnr) device tensors (no host sync)."""
     get = lambda k: getattr(args, k, DEFAULTS.get(k))  # noqa: E731
-    rgb, depth, acc, extras = render(H, W, K, chunk=get("chunk"), rays=batch_rays, retraw=True,
-                                     **render_kwargs_train)
+    # the gradient zero and the TV loss accumulator first: a GradArena(defer_tables=True) zero and the
+    # accumulator's fill are then stores in render()'s first launch (_lib.defer_fill_zero), not fills.
+    # Equivalent to the reference's render -> zero_grad order: the forward touches no gradient
     if zero_grad is None:
         optimizer.zero_grad()
     else:
         zero_grad()
-    # run_nerf.py:1011-1037 (img2mse x2, sparsity, TV, mse2psnr) fused into one launch (csrc/loss.hip)
     tv_w = get("tv_loss_weight")
-    tv = total_variation_all(render_kwargs_train["embed_fn"], generator=tv_generator) if tv_w > 0 else None
+    tv_acc = tv_accumulator(render_kwargs_train["embed_fn"]) if tv_w > 0 else None
+    rgb, depth, acc, extras = render(H, W, K, chunk=get("chunk"), rays=batch_rays, retraw=True,
+                                     **render_kwargs_train)
+    # run_nerf.py:1011-1037 (img2mse x2, sparsity, TV, mse2psnr) fused into one launch (csrc/loss.hip)
+    tv = (total_variation_all(render_kwargs_train["embed_fn"], generator=tv_generator, out=tv_acc)
+          if tv_w > 0 else None)
     loss, img_loss, psnr = train_loss(rgb, extras.get("rgb0"), target_s, extras.get("sparsity_loss"),
                                       extras.get("sparsity_loss0"), tv, get("sparse_loss_weight") * loss_scale_sparsity,
                                       tv_w if tv_w > 0 else 0.0)
@@ -193,6 +198,7 @@ def forward_backward(batch_rays, target_s, render_kwargs_train, optimizer, args,
         args.tv_loss_weight = 0.0
     if get("use_structural_priors") and global_step >= get("structural_loss_start_iter"):
         loss = loss + structural_loss(depth, extras, args, global_step, spatial_coords)
+    _lib.flush_zero_fills()       # fills no launch took (render() without rays to pack)
     loss.backward(_unit_seed(loss))
     hashgrid.materialize_zero()   # table gradients whose deferred zero no owner pass consumed
     return loss, img_loss, psnr

@@ -222,6 +222,17 @@ class _RawGuardFn(torch.autograd.Function):
 
 
 _FUSED_SAMPLER = {"on": True}
+_SH_ROWS = {"on": True}
+
+
+def set_sh_rows(enabled=True):
+    """render_rays writes each ray's SH4 view encoding once (nerf_sample_stratified_sh) and the fused
+    field's MLP kernels load it instead of evaluating SH per point (on by default; bit-identical)."""
+    _SH_ROWS["on"] = bool(enabled)
+
+
+def sh_rows():
+    return _SH_ROWS["on"]
 
 
 def set_fused_coarse_sampler(enabled=True):
@@ -367,10 +378,16 @@ def render_rays(ray_batch, network_fn, network_query_fn, N_samples, embed_fn=Non
     pts = torch.empty(R, N_samples, 3, **f)
     u = _pytest_uniforms((R, N_samples), dev) if (perturb > 0. and pytest) else None
     seed, off, rng = (0, 0, None) if (u is not None or not perturb > 0.) else _rng()
-    _lib.call("nerf_sample_stratified", _lib.ptr(rays, "ray_batch"), C, R, N_samples, _lib.ptr(_linspace(N_samples, dev)),
-              int(bool(lindisp)), int(perturb > 0.), _lib.ptr(u, "u", allow_none=True), seed, off, rng, _lib.ptr(z, "z"),
-              _lib.ptr(pts, "pts"), _lib.ptr(rays_d, "rays_d"), _lib.ptr(viewdirs, "viewdirs", allow_none=True),
+    # the view directions' SH4 rows, once per ray (the fused field reads them instead of evaluating
+    # SH per point, field.FieldFn): attached to the viewdirs tensor the field receives
+    sh_rays = torch.empty(R, 16, **f) if (viewdirs is not None and _SH_ROWS["on"]) else None
+    _lib.call("nerf_sample_stratified_sh", _lib.ptr(rays, "ray_batch"), C, R, N_samples,
+              _lib.ptr(_linspace(N_samples, dev)), int(bool(lindisp)), int(perturb > 0.), _lib.ptr(u, "u", allow_none=True),
+              seed, off, rng, _lib.ptr(z, "z"), _lib.ptr(pts, "pts"), _lib.ptr(rays_d, "rays_d"),
+              _lib.ptr(viewdirs, "viewdirs", allow_none=True), _lib.ptr(sh_rays, "sh_rows", allow_none=True),
               _lib.stream())
+    if sh_rays is not None:
+        viewdirs._nerf_sh = sh_rays
 
     reuse = CoarseReuse(R, N_samples, N_importance) if (N_importance > 0 and _REUSE["on"] and R > 0) else None
     if reuse is not None:
@@ -514,8 +531,10 @@ def _pack_rays(H, W, K, rays_o, rays_d, near, far, ndc, use_viewdirs):
         # -1./(W/(2.*focal)) is a python double in the reference; torch rounds it to float32
         cw = float(np.float32(-1. / (W / (2. * float(focal)))))
         ch = float(np.float32(-1. / (H / (2. * float(focal)))))
-    _lib.call("nerf_rays_pack", _lib.ptr(o, "rays_o"), _lib.ptr(d, "rays_d"), n, float(near), float(far), int(bool(ndc)),
-              cw, ch, int(bool(use_viewdirs)), _lib.ptr(out, "rays"), _lib.stream())
+    zeros, nz, keep = _lib.take_zero_fills()     # a training step's zero fills ride along (_lib.defer_fill_zero)
+    _lib.call("nerf_rays_pack_z", _lib.ptr(o, "rays_o"), _lib.ptr(d, "rays_d"), n, float(near), float(far),
+              int(bool(ndc)), cw, ch, int(bool(use_viewdirs)), _lib.ptr(out, "rays"), zeros, nz, _lib.stream())
+    del keep
     return out
 
 
