@@ -37,6 +37,8 @@ static int fill_args(MlpArgs& a, const float* d_feat, int64_t sp, int64_t sl, co
     a.viewdirs = d_viewdirs; a.spr = spr; a.keep = d_keep; a.P = n; a.W = *w;
     a.dsp = sp; a.dsl = sl;
     a.io_rows = nullptr; a.seg_split = n; a.spr2 = 1;
+    ray_div_magic(spr, a.rd_m1, a.rd_s1);
+    ray_div_magic(1, a.rd_m2, a.rd_s2);
     return NERF_OK;
 }
 
@@ -49,6 +51,7 @@ static int fill_order(MlpArgs& a, const nerf_point_order* o) {
                  (long long)a.P, (long long)o->spr2);
     a.seg_split = o->seg_split;
     a.spr2 = o->spr2;
+    ray_div_magic(a.spr2, a.rd_m2, a.rd_s2);
     return NERF_OK;
 }
 

@@ -259,8 +259,7 @@ __device__ __forceinline__ void load_sh6(const MlpArgs& a, uint32_t pt, bool val
     const uint32_t pc = valid ? pt : (uint32_t)(a.P - 1);
     if (!a.viewdirs && a.sh_stride == 0) {
         // per-ray SH rows (written by the stratified sampler): two 16-B loads, no evaluation
-        const uint32_t ray = (pc < (uint32_t)a.seg_split ? pc / (uint32_t)a.spr
-                                                         : (pc - (uint32_t)a.seg_split) / (uint32_t)a.spr2) * 16u + zero;
+        const uint32_t ray = ray_of(a, pc) * 16u + zero;
         const float4 u = *reinterpret_cast<const float4*>(a.sh + ray + 4 * h);
         const float4 v = *reinterpret_cast<const float4*>(a.sh + ray + 8 + 4 * h);
         shv[0] = valid ? u.x : 0.f; shv[1] = valid ? u.y : 0.f; shv[2] = valid ? u.z : 0.f; shv[3] = valid ? u.w : 0.f;
