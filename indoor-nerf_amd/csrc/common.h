@@ -35,6 +35,21 @@ inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s);
 
 constexpr int kWave = 64;
 
+// n / d for 0 <= n < 2^31 as mulhi(n, m) >> s (Granlund-Montgomery: l = ceil(log2 d),
+// m = ceil(2^(31+l) / d) < 2^32, s = l - 1; m = 0 encodes d = 1): a runtime-invariant divisor costs
+// two VALU ops instead of the ~15 of an integer division (v_rcp_iflag + correction steps)
+__device__ __forceinline__ uint32_t udiv_magic(uint32_t n, uint32_t m, int s) {
+    return m ? (__umulhi(n, m) >> s) : n;
+}
+
+inline void ray_div_magic(int64_t d, uint32_t& m, int& s) {
+    if (d <= 1) { m = 0; s = 0; return; }
+    int l = 0;
+    while ((int64_t(1) << l) < d) ++l;
+    m = (uint32_t)(((uint64_t(1) << (31 + l)) + (uint64_t)d - 1) / (uint64_t)d);
+    s = l - 1;
+}
+
 inline unsigned blocks_for(int64_t n, int threads) {
     return (unsigned)((n + threads - 1) / threads);
 }

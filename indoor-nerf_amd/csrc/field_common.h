@@ -80,22 +80,10 @@ __device__ __forceinline__ void sh4_eval(float x, float y, float z, float* o) {
     o[15] = (-0.5900435899266435f * x) * (xx - 3.0f * yy);
 }
 
-__device__ __forceinline__ uint32_t udiv_magic(uint32_t n, uint32_t m, int s) {
-    return m ? (__umulhi(n, m) >> s) : n;
-}
-
 // The ray of point pc (the point order's two segments, MlpArgs)
 __device__ __forceinline__ uint32_t ray_of(const MlpArgs& a, uint32_t pc) {
     return pc < (uint32_t)a.seg_split ? udiv_magic(pc, a.rd_m1, a.rd_s1)
                                       : udiv_magic(pc - (uint32_t)a.seg_split, a.rd_m2, a.rd_s2);
-}
-
-inline void ray_div_magic(int64_t d, uint32_t& m, int& s) {
-    if (d <= 1) { m = 0; s = 0; return; }
-    int l = 0;
-    while ((int64_t(1) << l) < d) ++l;
-    m = (uint32_t)(((uint64_t(1) << (31 + l)) + (uint64_t)d - 1) / (uint64_t)d);
-    s = l - 1;
 }
 
 __device__ __forceinline__ floatx16 zero16() {
