@@ -209,8 +209,10 @@ int nerf_sh4_fwd(const float* d_dirs, int64_t n, float* d_out /* [n,16] */, void
  * Input point p: hash features x[p][k] = d_feat[p*feat_stride_point + (k/2)*feat_stride_level + k%2]
  * (k < 32); view encoding: if d_viewdirs != NULL, SH4 of d_viewdirs[p / samples_per_ray] is
  * computed in-kernel, else sh[p][k] = d_sh[p*sh_stride + k] (k < 16) — or, with sh_stride == 0, the
- * per-RAY rows sh[p][k] = d_sh[16*(p / samples_per_ray) + k] (16-B aligned; the point order's two
- * segments as for d_viewdirs), e.g. nerf_sample_stratified_sh's d_sh.
+ * per-RAY records of 40 floats: sh[p][k] = d_sh[40*(p / samples_per_ray) + k], followed by the three
+ * exact bf16 pieces of the 16 values (piece q of k at bf16 index 32 + 16q + k of the record) that
+ * the MLP kernels use as the pre-split matrix operand (16-B aligned; the point order's two segments
+ * as for d_viewdirs), i.e. nerf_sample_stratified_sh's d_sh.
  * d_keep may be NULL (keep all). Output d_raw [P,4] = [rgb_raw(3), sigma_raw].
  */
 typedef struct {
@@ -400,8 +402,9 @@ int nerf_sample_stratified(const float* d_rays, int64_t ray_stride, int64_t n_ra
                            float* d_viewdirs /* optional [R,3]: the last 3 ray columns (stride > 8) */,
                            void* stream);
 
-/* Same, also writing d_sh [R,16] = SH4 of each ray's view direction (the last 3 columns; needs
- * ray_stride > 8; hash_encoding.py:153-191): the per-ray rows the MLP entries take with sh_stride 0. */
+/* Same, also writing d_sh [R,40] = per ray SH4 of its view direction (the last 3 columns; needs
+ * ray_stride > 8; hash_encoding.py:153-191), 16 fp32 values and their three bf16 pieces: the per-ray
+ * records the MLP entries take with sh_stride 0. */
 int nerf_sample_stratified_sh(const float* d_rays, int64_t ray_stride, int64_t n_rays, int n_samples,
                               const float* d_t, int lindisp, int perturb, const float* d_u,
                               uint64_t seed, uint64_t offset, const uint64_t* d_rng,

@@ -80,6 +80,10 @@ __device__ __forceinline__ void sh4_eval(float x, float y, float z, float* o) {
     o[15] = (-0.5900435899266435f * x) * (xx - 3.0f * yy);
 }
 
+// Per-ray SH record (sh_stride 0, nerf_sample_stratified_sh): 16 fp32 coefficients, then the three
+// exact bf16 pieces (v0 = bf16(v), v1 = bf16(v - v0), v2 = bf16(v - v0 - v1)) of each, 160 B
+constexpr int kShRecord = 40;   // floats
+
 // The ray of point pc (the point order's two segments, MlpArgs)
 __device__ __forceinline__ uint32_t ray_of(const MlpArgs& a, uint32_t pc) {
     return pc < (uint32_t)a.seg_split ? udiv_magic(pc, a.rd_m1, a.rd_s1)

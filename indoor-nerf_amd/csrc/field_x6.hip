@@ -228,10 +228,10 @@ __device__ __forceinline__ int opaque_zero() {
 }
 
 // ---- per-tile inputs ---------------------------------------------------------------------------
-// x[8c + i] = feature 16c + 4h + (i&3) + 8(i>>2); shv[i] = SH 4h + (i&3) + 8(i>>2)
+// x[8c + i] = feature 16c + 4h + (i&3) + 8(i>>2); SH = the three bf16 pieces of SH 4h + (i&3) + 8(i>>2)
 struct InX6 {
     float x[16];
-    float shv[8];
+    S3 SH;
     uint32_t pt;    // 32-bit indexing (launch_* checks the sizes): one VGPR per address, saddr forms
     bool valid;
 };
@@ -259,7 +259,7 @@ __device__ __forceinline__ void load_sh6(const MlpArgs& a, uint32_t pt, bool val
     const uint32_t pc = valid ? pt : (uint32_t)(a.P - 1);
     if (!a.viewdirs && a.sh_stride == 0) {
         // per-ray SH rows (written by the stratified sampler): two 16-B loads, no evaluation
-        const uint32_t ray = ray_of(a, pc) * 16u + zero;
+        const uint32_t ray = ray_of(a, pc) * (uint32_t)kShRecord + zero;
         const float4 u = *reinterpret_cast<const float4*>(a.sh + ray + 4 * h);
         const float4 v = *reinterpret_cast<const float4*>(a.sh + ray + 8 + 4 * h);
         shv[0] = valid ? u.x : 0.f; shv[1] = valid ? u.y : 0.f; shv[2] = valid ? u.z : 0.f; shv[3] = valid ? u.w : 0.f;
@@ -283,11 +283,31 @@ __device__ __forceinline__ void load_sh6(const MlpArgs& a, uint32_t pt, bool val
     }
 }
 
+// The C0 operand of the point's SH: from the per-ray records' pre-split pieces (kShRecord layout:
+// 16 fp32 coefficients, then pieces 0, 1, 2 of the 16 as bf16; two 8-B loads per piece), else split here
+__device__ __forceinline__ S3 load_sh_split(const MlpArgs& a, uint32_t pt, bool valid, int h) {
+    if (!a.viewdirs && a.sh_stride == 0) {
+        const uint32_t pc = valid ? pt : (uint32_t)(a.P - 1);
+        const uint16_t* rec = reinterpret_cast<const uint16_t*>(a.sh + ray_of(a, pc) * (uint32_t)kShRecord) + 32;
+        S3 s;
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            const u32x2 g0 = *reinterpret_cast<const u32x2*>(rec + 16 * q + 4 * h);
+            const u32x2 g1 = *reinterpret_cast<const u32x2*>(rec + 16 * q + 8 + 4 * h);
+            s.p[q] = valid ? u32x4{g0.x, g0.y, g1.x, g1.y} : u32x4{0u, 0u, 0u, 0u};
+        }
+        return s;
+    }
+    float shv[8];
+    load_sh6(a, pt, valid, h, shv, 0);
+    return split_arr(shv);
+}
+
 __device__ __forceinline__ void load_in_x6(const MlpArgs& a, int64_t tile, int j, int h, InX6& in) {
     in.pt = (uint32_t)(tile * 32 + j);
     in.valid = tile * 32 + j < a.P;
     load_x6(a, in.pt, in.valid, h, in.x, 0);
-    load_sh6(a, in.pt, in.valid, h, in.shv, 0);
+    in.SH = load_sh_split(a, in.pt, in.valid, h);
 }
 
 // Row of point pt in raw / geo / graw / dgeo / dsh (MlpArgs point order)
@@ -314,7 +334,7 @@ __device__ __forceinline__ void bwd_point(const MlpArgs& a, int64_t n, int64_t t
 __device__ __forceinline__ void load_in_x6_bwd(const MlpArgs& a, int64_t n, int64_t tile, int j, int h, InX6& in) {
     bwd_point(a, n, tile, j, in.pt, in.valid);
     load_x6(a, in.pt, in.valid, h, in.x, 0);
-    load_sh6(a, in.pt, in.valid, h, in.shv, 0);
+    in.SH = load_sh_split(a, in.pt, in.valid, h);
 }
 
 struct ActX6 {
@@ -376,9 +396,8 @@ __device__ __forceinline__ void fwd_chain(const __bf16* img, const InX6& in, Act
         for (int t = 0; t < 2; ++t) f.h2[t] = mma6(row_read(img, IM_C0, S32, 32 * t + m, 4 * h), O0, f.h2[t]);
     }
     {
-        const S3 SH = split_arr(in.shv);
 #pragma unroll
-        for (int t = 0; t < 2; ++t) f.h2[t] = mma6(row_read(img, IM_C0, S32, 32 * t + m, 16 + 4 * h), SH, f.h2[t]);
+        for (int t = 0; t < 2; ++t) f.h2[t] = mma6(row_read(img, IM_C0, S32, 32 * t + m, 16 + 4 * h), in.SH, f.h2[t]);
     }
     relu16i(f.h2[0]); relu16i(f.h2[1]);
     // C1: h3 = relu(C1 h2)

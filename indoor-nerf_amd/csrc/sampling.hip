@@ -51,11 +51,21 @@ __global__ void __launch_bounds__(256) sample_stratified_kernel(StratArgs a) {
             const float* v = ray + a.stride - 3;
             float o[16];
             sh4_eval(v[0], v[1], v[2], o);
-            float4* dst = reinterpret_cast<float4*>(a.sh + 16 * r);
+            float4* dst = reinterpret_cast<float4*>(a.sh + kShRecord * r);
             dst[0] = make_float4(o[0], o[1], o[2], o[3]);
             dst[1] = make_float4(o[4], o[5], o[6], o[7]);
             dst[2] = make_float4(o[8], o[9], o[10], o[11]);
             dst[3] = make_float4(o[12], o[13], o[14], o[15]);
+            __bf16* pc = reinterpret_cast<__bf16*>(a.sh + kShRecord * r + 16);   // the MLP's pre-split operand
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                const __bf16 p0 = (__bf16)o[k];
+                const float r1 = o[k] - (float)p0;
+                const __bf16 p1 = (__bf16)r1;
+                pc[k] = p0;
+                pc[16 + k] = p1;
+                pc[32 + k] = (__bf16)(r1 - (float)p1);
+            }
         }
     }
     if (a.pts) {

@@ -380,7 +380,8 @@ def render_rays(ray_batch, network_fn, network_query_fn, N_samples, embed_fn=Non
     seed, off, rng = (0, 0, None) if (u is not None or not perturb > 0.) else _rng()
     # the view directions' SH4 rows, once per ray (the fused field reads them instead of evaluating
     # SH per point, field.FieldFn): attached to the viewdirs tensor the field receives
-    sh_rays = torch.empty(R, 16, **f) if (viewdirs is not None and _SH_ROWS["on"]) else None
+    # [R, 40]: 16 fp32 coefficients + their three bf16 pieces (the MLP's pre-split C0 operand)
+    sh_rays = torch.empty(R, 40, **f) if (viewdirs is not None and _SH_ROWS["on"]) else None
     _lib.call("nerf_sample_stratified_sh", _lib.ptr(rays, "ray_batch"), C, R, N_samples,
               _lib.ptr(_linspace(N_samples, dev)), int(bool(lindisp)), int(perturb > 0.), _lib.ptr(u, "u", allow_none=True),
               seed, off, rng, _lib.ptr(z, "z"), _lib.ptr(pts, "pts"), _lib.ptr(rays_d, "rays_d"),

@@ -1,7 +1,8 @@
-"""Per-ray SH4 rows (nerf_sample_stratified_sh writes SH4 of each ray's view direction once; the MLP
-kernels take them with sh_stride 0 instead of evaluating SH per point, render.set_sh_rows) against the
-in-kernel evaluation: the same sh4_eval on the same floats, so the MLP outputs and every gradient are
-bit-identical — at the ABI (forward and backward, two-segment point order) and through render_rays."""
+"""Per-ray SH4 records (nerf_sample_stratified_sh writes SH4 of each ray's view direction once, with its
+three exact bf16 pieces; the MLP kernels take them with sh_stride 0 instead of evaluating and splitting
+SH per point, render.set_sh_rows) against the in-kernel evaluation: the same sh4_eval on the same
+floats and the same split, so the MLP outputs and every gradient are bit-identical — at the ABI
+(forward and backward, two-segment point order) and through render_rays."""
 import pytest
 import torch
 
@@ -21,13 +22,18 @@ def test_mlp_per_ray_sh_rows_bitwise(nerf, gpu):
     rays[:, 8:] = torch.nn.functional.normalize(torch.randn(R, 3, device=gpu, generator=g), dim=-1)
     t = torch.linspace(0, 1, S, device=gpu)
     z, pts = torch.empty(R, S, device=gpu), torch.empty(R, S, 3, device=gpu)
-    vd, sh = torch.empty(R, 3, device=gpu), torch.empty(R, 16, device=gpu)
+    vd, sh = torch.empty(R, 3, device=gpu), torch.empty(R, 40, device=gpu)
     _lib.call("nerf_sample_stratified_sh", _lib.ptr(rays), 11, R, S, _lib.ptr(t), 0, 0, None, 0, 0, None, _lib.ptr(z),
               _lib.ptr(pts), None, _lib.ptr(vd), _lib.ptr(sh), _lib.stream())
     ref = torch.empty(R, 16, device=gpu)
     _lib.call("nerf_sh4_fwd", _lib.ptr(vd), R, _lib.ptr(ref), _lib.stream())
     torch.cuda.synchronize()
-    assert torch.equal(sh, ref)
+    assert torch.equal(sh[:, :16], ref)
+    # the record's bf16 pieces: exact (v0 + v1 + v2 == v) and each the RNE bf16 of the remainder
+    pcs = sh[:, 16:].contiguous().view(torch.bfloat16).float().reshape(R, 3, 16)
+    assert torch.equal(pcs[:, 0], ref.bfloat16().float())
+    assert torch.equal(pcs[:, 1], (ref - pcs[:, 0]).bfloat16().float())
+    assert torch.equal((pcs[:, 0] + pcs[:, 1]) + pcs[:, 2], ref)
     # the reuse's two-segment point order: importance rows (N per ray) then coarse rows (S per ray)
     ranks = torch.argsort(torch.rand(R, M, device=gpu, generator=g), -1) + (torch.arange(R, device=gpu) * M)[:, None]
     inv = torch.cat([ranks[:, :N].reshape(-1), ranks[:, N:].reshape(-1)]).to(torch.int32)
