@@ -40,3 +40,17 @@ def test_kernel_variants_traffic_is_the_mean(tmp_path, monkeypatch):
     assert bench.pmc_traffic("nerf_composite_fwd") == 2000.0      # x 2 launches per step = both kernels
     assert bench.pmc_traffic("nerf_composite_bwd") is None         # kernels missing from the summary
     assert bench.base_name("nerf_mlp_fwd_ord") == bench.base_name("nerf_mlp_fwd_q") == "nerf_mlp_fwd"
+
+
+def test_merged_compositing_calls_are_priced():
+    """The coarse compositing inside the sampler launch and the batched backward count toward the
+    compositing ops (their time is the op's; the sampler's bytes are not priced)."""
+    units = {"point": 1_048_576, "sample": 1_048_576, "hash_point": 786_432, "bwd_point": 1_048_576,
+             "bwd_hash_point": 786_432}
+    k = _kernels(nerf_composite_fwd=(1, 0.0104), nerf_composite_sample_fine=(1, 0.0216),
+                 nerf_composite_bwd_batch=(1, 0.0171))
+    ops = {o["op"]: o for o in bench.op_rooflines(k, 1, units, 0)}
+    assert ops["composite_fwd"]["calls"] == {"nerf_composite_fwd": 1, "nerf_composite_sample_fine": 1}
+    assert abs(ops["composite_fwd"]["ms_per_step"] - 0.032) < 1e-9
+    assert ops["composite_bwd"]["calls"] == {"nerf_composite_bwd_batch": 1}
+    assert ops["composite_bwd"]["algorithmic_bytes"] == 40 * units["sample"]
