@@ -48,7 +48,8 @@ X6_PEAK_TFLOPS = 2500.0 / 6
 #   composite: per sample 16 B raw + 4 B z + 4 B weights (fwd) / + 16 B grad (bwd)
 #   radam    : per table/MLP element 28 B (read p, g, m, v; write p, m, v)
 OPS = {
-    "hash_bwd": dict(calls=("nerf_hash_encode_bwd_bin", "nerf_hash_encode_bwd_bin_rows", "nerf_hash_encode_bwd_owner",
+    "hash_bwd": dict(calls=("nerf_hash_encode_bwd_bin", "nerf_hash_encode_bwd_bin_rows", "nerf_hash_encode_bwd_bin_batch",
+                            "nerf_hash_encode_bwd_owner",
                             "nerf_hash_encode_bwd_owner_range", "nerf_hash_encode_bwd_owner_step",
                             "nerf_hash_encode_bwd_ws", "nerf_hash_encode_bwd"),
                      bound="hbm",
@@ -82,6 +83,7 @@ KERNEL_SYMBOLS = {
     "nerf_hash_encode_fwd_packed": ["nerf::hash_encode_fwd_packed_pair_kernel"],
     "nerf_hash_encode_bwd_bin": ["nerf::hash_encode_bwd_kernel<3, 512>"],
     "nerf_hash_encode_bwd_bin_rows": ["nerf::hash_encode_bwd_kernel<3, 512>"],
+    "nerf_hash_encode_bwd_bin_batch": ["nerf::hash_encode_bwd_pair_kernel<512>"],
     "nerf_tv_bwd_bin": ["nerf::tv_bwd_bin_kernel<512>"],
     "nerf_hash_encode_bwd_owner": ["nerf::hash_bwd_owner_kernel<13, 1024, false>"],
     "nerf_hash_encode_bwd_owner_range": ["nerf::hash_bwd_owner_kernel<13, 1024, false>"],
@@ -240,6 +242,8 @@ def parse():
                          "(render.set_fused_coarse_sampler)")
     ap.add_argument("--batched-composite", type=int, default=1,
                     help="1: the fine and coarse compositing backwards in one launch (render.set_batched_composite_bwd)")
+    ap.add_argument("--bin-batch", type=int, default=1,
+                    help="1: the pass's hash bins as one launch (field.set_bin_batch)")
     ap.add_argument("--sh-rows", type=int, default=1,
                     help="1: per-ray SH4 rows written by the stratified sampler, loaded by the MLP kernels "
                          "(render.set_sh_rows)")
@@ -469,6 +473,8 @@ def main():
     nerf.set_active_points(bool(a.active_points))
     _lib.set_fold_fills(bool(a.fold_fills))
     nerf.set_sh_rows(bool(a.sh_rows))
+    from indoor_nerf_amd import field as _field
+    _field.set_bin_batch(bool(a.bin_batch))
     kw, kw_test, _, grad_vars, opt = nerf.create_nerf(args, device=dev)
     for d in (kw, kw_test):
         d.update(near=wl["near"], far=wl["far"])     # train() adds the scene bounds (run_nerf.py:768-770,865-869)

@@ -143,6 +143,22 @@ int nerf_hash_encode_bwd_bin_rows(const float* d_xyz, const int32_t* d_rows, con
                                   int64_t feat2_stride_point, int64_t feat2_stride_level,
                                   int64_t chunk_base, int64_t chunk_capacity, int deterministic,
                                   void* d_workspace, size_t workspace_bytes, void* stream);
+
+/* Several bin launches of one workspace as ONE call (the fine and the coarse pass of an iteration): each
+ * job's fields as the nerf_hash_encode_bwd_bin_rows arguments of the same name; the shared arguments
+ * (box, levels, workspace) as there. Two non-empty jobs run as one launch (no drain / ramp between
+ * them), more as one launch per further pair. Every job is validated before anything is launched;
+ * the workspace contents are those of the separate calls. */
+typedef struct nerf_bin_job {
+    const float* xyz; const int32_t* rows; const int32_t* count; int64_t n_points;
+    const float* dfeat; int64_t feat_stride_point, feat_stride_level;
+    const float* dfeat2; const int32_t* rows2; int64_t feat2_stride_point, feat2_stride_level;
+    int64_t chunk_base;
+} nerf_bin_job;
+int nerf_hash_encode_bwd_bin_batch(const nerf_bin_job* jobs, int n_jobs, const float* bbox_min3,
+                                   const float* bbox_max3, const float* level_res, int n_levels, int log2_T,
+                                   int64_t chunk_capacity, int deterministic, void* d_workspace,
+                                   size_t workspace_bytes, void* stream);
 int nerf_hash_encode_bwd_owner(int n_levels, int log2_T, int64_t n_chunks, int64_t chunk_capacity,
                                float* const* d_dtables, int deterministic, void* d_workspace,
                                size_t workspace_bytes, void* stream);

@@ -57,6 +57,13 @@ class CompositeBwdJob(ctypes.Structure):
                 ("g_entropy", c_vp), ("g_normal", c_vp), ("graw", c_vp)]
 
 
+class BinJob(ctypes.Structure):
+    """nerf_bin_job (include/nerf_hip.h)."""
+    _fields_ = [("xyz", c_vp), ("rows", c_vp), ("count", c_vp), ("n_points", c_i64), ("dfeat", c_vp),
+                ("feat_stride_point", c_i64), ("feat_stride_level", c_i64), ("dfeat2", c_vp), ("rows2", c_vp),
+                ("feat2_stride_point", c_i64), ("feat2_stride_level", c_i64), ("chunk_base", c_i64)]
+
+
 class ZeroRange(ctypes.Structure):
     _fields_ = [("ptr", c_vp), ("n", c_i64)]
 
@@ -123,6 +130,8 @@ SIGNATURES = {
                                  c_i64, c_int, c_vp, ctypes.c_size_t, c_vp],
     "nerf_hash_encode_bwd_owner": [c_int, c_int, c_i64, c_i64, ctypes.POINTER(c_vp), c_int, c_vp, ctypes.c_size_t,
                                    c_vp],
+    "nerf_hash_encode_bwd_bin_batch": [ctypes.POINTER(BinJob), c_int, c_f32p, c_f32p, c_f32p, c_int, c_int, c_i64,
+                                       c_int, c_vp, ctypes.c_size_t, c_vp],
     "nerf_hash_encode_bwd_bin_rows": [c_vp, c_vp, c_vp, c_i64, c_f32p, c_f32p, c_f32p, c_int, c_int, c_vp, c_i64,
                                       c_i64, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_int, c_vp, ctypes.c_size_t, c_vp],
     "nerf_active_rows": [c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_int, c_vp, ctypes.c_size_t, c_vp],

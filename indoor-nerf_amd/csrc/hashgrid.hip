@@ -276,17 +276,18 @@ struct BinRows {
     const int32_t* count;   // optional device int: only points p < *count are binned (an active-point list)
 };
 
-// MODE 1: coalesced float atomics (no workspace); 3: binned (default).
+// MODE 1: coalesced float atomics (no workspace); 3: binned (default). blk: the block's chunk within the
+// launch's points (blockIdx.x, or its offset in a two-job launch).
 template <int MODE, int THREADS>
-__global__ void __launch_bounds__(THREADS) hash_encode_bwd_kernel(
-    const float* __restrict__ xyz, int64_t n, HashGradParams hp,
-    const float* __restrict__ dfeat, int64_t sp, int64_t sl, BinRows br) {
-    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void bwd_bin_block(const float* __restrict__ xyz, int64_t n, const HashGradParams& hp,
+                                              const float* __restrict__ dfeat, int64_t sp, int64_t sl,
+                                              const BinRows& br, int blk) {
+    const int64_t p = (int64_t)blk * blockDim.x + threadIdx.x;
     const int lvl = blockIdx.y;
     if (br.count) n = min(n, (int64_t)*br.count);
     if constexpr (MODE == 3) {
-        if ((int64_t)blockIdx.x * blockDim.x >= n) {   // a chunk past the active points: empty segments
-            const int chunk = hp.chunk_base + (int)blockIdx.x;
+        if ((int64_t)blk * blockDim.x >= n) {   // a chunk past the active points: empty segments
+            const int chunk = hp.chunk_base + blk;
             const int n_own = 1 << hp.owner_log2;
             for (int o = threadIdx.x; o < n_own; o += blockDim.x)
                 hp.bin_seg[((size_t)lvl * n_own + o) * hp.chunk_stride + chunk] = 0u;
@@ -374,7 +375,7 @@ __global__ void __launch_bounds__(THREADS) hash_encode_bwd_kernel(
             ey[e] = cgy[c];
             on[e] = emit && (ex[e] != 0.f || ey[e] != 0.f);
         }
-        bin_chunk<THREADS, 8, true>(hp, lvl, hp.chunk_base + (int)blockIdx.x, hh, ex, ey, on);
+        bin_chunk<THREADS, 8, true>(hp, lvl, hp.chunk_base + blk, hh, ex, ey, on);
     } else {
         __shared__ float s_val[4][64][17];
         __shared__ uint32_t s_h[4][64][9];
@@ -399,6 +400,30 @@ __global__ void __launch_bounds__(THREADS) hash_encode_bwd_kernel(
             if (h != kSkip && v != 0.f) atomic_add_f32(tab + 2 * h + f, v);
         }
     }
+}
+
+template <int MODE, int THREADS>
+__global__ void __launch_bounds__(THREADS) hash_encode_bwd_kernel(
+    const float* __restrict__ xyz, int64_t n, HashGradParams hp,
+    const float* __restrict__ dfeat, int64_t sp, int64_t sl, BinRows br) {
+    bwd_bin_block<MODE, THREADS>(xyz, n, hp, dfeat, sp, sl, br, (int)blockIdx.x);
+}
+
+// Two bin jobs in one launch (the fine and the coarse pass of an iteration, side by side in one
+// workspace): blocks [0, split) bin job a's chunks, the rest job b's — no drain / ramp between them.
+struct BinJob {
+    const float* xyz;
+    int64_t n;
+    HashGradParams hp;
+    const float* dfeat;
+    int64_t sp, sl;
+    BinRows br;
+};
+
+template <int THREADS>
+__global__ void __launch_bounds__(THREADS) hash_encode_bwd_pair_kernel(BinJob a, BinJob b, unsigned split) {
+    if (blockIdx.x < split) bwd_bin_block<3, THREADS>(a.xyz, a.n, a.hp, a.dfeat, a.sp, a.sl, a.br, (int)blockIdx.x);
+    else bwd_bin_block<3, THREADS>(b.xyz, b.n, b.hp, b.dfeat, b.sp, b.sl, b.br, (int)(blockIdx.x - split));
 }
 
 // TV backward (loss.py:11-43 autograd) into the binned workspace, summed by the same owner pass as
@@ -945,28 +970,67 @@ extern "C" int nerf_hash_encode_bwd_bin_rows(const float* d_xyz, const int32_t* 
                                              int64_t feat2_stride_point, int64_t feat2_stride_level,
                                              int64_t chunk_base, int64_t chunk_capacity, int deterministic,
                                              void* d_workspace, size_t workspace_bytes, void* stream) {
-    NERF_REQUIRE(n_points >= 0, "hash_encode_bwd_bin: n_points < 0");
-    NERF_REQUIRE((n_points == 0 || (d_xyz && (d_dfeat || d_dfeat2))) && level_res && bbox_min3 && bbox_max3,
+    const nerf_bin_job j{d_xyz, d_rows, d_count, n_points, d_dfeat, feat_stride_point, feat_stride_level, d_dfeat2,
+                         d_rows2, feat2_stride_point, feat2_stride_level, chunk_base};
+    return nerf_hash_encode_bwd_bin_batch(&j, 1, bbox_min3, bbox_max3, level_res, n_levels, log2_T, chunk_capacity,
+                                          deterministic, d_workspace, workspace_bytes, stream);
+}
+
+static int bin_job(const nerf_bin_job& j, const float* bbox_min3, const float* bbox_max3, const float* level_res,
+                   int n_levels, int log2_T, int64_t chunk_capacity, int deterministic, void* d_workspace,
+                   size_t workspace_bytes, BinJob& out, int64_t& nch) {
+    NERF_REQUIRE(j.n_points >= 0, "hash_encode_bwd_bin: n_points < 0");
+    NERF_REQUIRE((j.n_points == 0 || (j.xyz && (j.dfeat || j.dfeat2))) && level_res && bbox_min3 && bbox_max3,
                  "hash_encode_bwd_bin: null arg");
-    NERF_REQUIRE(n_points == 0 || !d_dfeat2 || (((uintptr_t)d_dfeat2 & 7) == 0 && feat2_stride_point % 2 == 0 &&
-                                                feat2_stride_level % 2 == 0),
+    NERF_REQUIRE(j.n_points == 0 || !j.dfeat2 || (((uintptr_t)j.dfeat2 & 7) == 0 && j.feat2_stride_point % 2 == 0 &&
+                                                  j.feat2_stride_level % 2 == 0),
                  "hash_encode_bwd_bin: dfeat2 needs 8-B aligned feature pairs");
     HashGradParams hp{};
     const int rc = bin_layout("hash_encode_bwd_bin", n_levels, log2_T, chunk_capacity, deterministic, d_workspace,
                               workspace_bytes, hp);
     if (rc) return rc;
-    const int64_t nch = (n_points + kChunkPts - 1) / kChunkPts;
-    NERF_REQUIRE(chunk_base >= 0 && chunk_base + nch <= chunk_capacity,
-                 "hash_encode_bwd_bin: chunks [%lld, %lld) exceed the capacity %lld", (long long)chunk_base,
-                 (long long)(chunk_base + nch), (long long)chunk_capacity);
-    if (n_points == 0) return NERF_OK;
+    nch = (j.n_points + kChunkPts - 1) / kChunkPts;
+    NERF_REQUIRE(j.chunk_base >= 0 && j.chunk_base + nch <= chunk_capacity,
+                 "hash_encode_bwd_bin: chunks [%lld, %lld) exceed the capacity %lld", (long long)j.chunk_base,
+                 (long long)(j.chunk_base + nch), (long long)chunk_capacity);
     for (int a = 0; a < 3; ++a) { hp.bmin[a] = bbox_min3[a]; hp.bmax[a] = bbox_max3[a]; }
     hp.fastdiv = fill_cells(hp.cell, bbox_min3, bbox_max3, level_res, n_levels) ? 1u : 0u;
-    hp.chunk_base = (int)chunk_base;
-    hp.nchunks = (int)(chunk_base + nch);
-    const BinRows br{d_rows, d_dfeat2, d_rows2, feat2_stride_point, feat2_stride_level, d_count};
-    hipLaunchKernelGGL((hash_encode_bwd_kernel<3, kChunkPts>), dim3((unsigned)nch, n_levels), dim3(kChunkPts), 0, as_stream(stream),
-                       d_xyz, n_points, hp, d_dfeat, feat_stride_point, feat_stride_level, br);
+    hp.chunk_base = (int)j.chunk_base;
+    hp.nchunks = (int)(j.chunk_base + nch);
+    out = BinJob{j.xyz, j.n_points, hp, j.dfeat, j.feat_stride_point, j.feat_stride_level,
+                 BinRows{j.rows, j.dfeat2, j.rows2, j.feat2_stride_point, j.feat2_stride_level, j.count}};
+    return NERF_OK;
+}
+
+extern "C" int nerf_hash_encode_bwd_bin_batch(const nerf_bin_job* jobs, int n_jobs, const float* bbox_min3,
+                                              const float* bbox_max3, const float* level_res, int n_levels,
+                                              int log2_T, int64_t chunk_capacity, int deterministic,
+                                              void* d_workspace, size_t workspace_bytes, void* stream) {
+    NERF_REQUIRE(n_jobs >= 0 && n_jobs <= 8 && (n_jobs == 0 || jobs), "hash_encode_bwd_bin_batch: %d jobs", n_jobs);
+    BinJob bj[8];
+    int64_t nch[8];
+    for (int i = 0; i < n_jobs; ++i) {   // every job validated before anything is launched
+        const int rc = bin_job(jobs[i], bbox_min3, bbox_max3, level_res, n_levels, log2_T, chunk_capacity,
+                               deterministic, d_workspace, workspace_bytes, bj[i], nch[i]);
+        if (rc) return rc;
+    }
+    hipStream_t st = as_stream(stream);
+    int i = 0;
+    while (i < n_jobs) {
+        if (jobs[i].n_points == 0) { ++i; continue; }
+        int k = i + 1;
+        while (k < n_jobs && jobs[k].n_points == 0) ++k;
+        if (k < n_jobs) {   // two jobs: one launch
+            hipLaunchKernelGGL((hash_encode_bwd_pair_kernel<kChunkPts>), dim3((unsigned)(nch[i] + nch[k]), n_levels),
+                               dim3(kChunkPts), 0, st, bj[i], bj[k], (unsigned)nch[i]);
+            i = k + 1;
+        } else {
+            const BinJob& b = bj[i];
+            hipLaunchKernelGGL((hash_encode_bwd_kernel<3, kChunkPts>), dim3((unsigned)nch[i], n_levels), dim3(kChunkPts),
+                               0, st, b.xyz, b.n, b.hp, b.dfeat, b.sp, b.sl, b.br);
+            i = k;
+        }
+    }
     NERF_CHECK_LAUNCH("hash_encode_bwd_bin");
     return NERF_OK;
 }

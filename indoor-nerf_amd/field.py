@@ -342,6 +342,13 @@ class _FieldJob:
 
 
 _DETERMINISTIC = {"on": False, "ws": {}}
+_BIN_BATCH = {"on": True}
+
+
+def set_bin_batch(enabled=True):
+    """The hash bins of a backward pass (fine + coarse) as one launch (nerf_hash_encode_bwd_bin_batch;
+    default on, the same workspace contents as one launch each)."""
+    _BIN_BATCH["on"] = bool(enabled)
 _ACTIVE = {"on": False}
 _LAST_ACTIVE = []    # (device counts, points) of the last field backward's jobs (bench.py reports them)
 
@@ -423,10 +430,16 @@ def _run_field_jobs(jobs):
         pb.reserve(sum(bin_chunks(b["n"]) for b in bins) + sum(j.n_chunks for j in tv_jobs))
         for j in tv_jobs:
             pb.add_tv(j, queue=False)
-        for b in bins:
-            j = b.pop("job")
-            hash_encode_bwd(b.pop("xyz"), j.meta, b.pop("dfeat"), 2, b.pop("sl"), accumulate_grad_buffers(j.tables),
-                            defer=True, queue=False, **b)
+        if _BIN_BATCH["on"]:
+            pb.begin_batch()  # the pass's hash bins as one launch (nerf_hash_encode_bwd_bin_batch)
+        try:
+            for b in bins:
+                j = b.pop("job")
+                hash_encode_bwd(b.pop("xyz"), j.meta, b.pop("dfeat"), 2, b.pop("sl"), accumulate_grad_buffers(j.tables),
+                                defer=True, queue=False, **b)
+        finally:
+            if _BIN_BATCH["on"]:
+                pb.end_batch()
         pb.flush()
     for j in jobs:
         j.dfeat = None

@@ -162,11 +162,14 @@ class _PendingBins:
         self.hold = False     # hold_owner(): the pass's owner launch is left to the caller (HeldOwner)
         self.held = None
         self.step_plan = None  # fused_table_step(): (optimizer, tables) whose step the owner pass runs
+        self.batch = None      # begin_batch(): bin launches collected for one nerf_hash_encode_bwd_bin_batch
 
     def flush(self, final=True):
         """Launch (or hold) the owner pass of the open workspace. final=False: an early flush that makes
         room for more bins of the same pass (_slot) — its gradients are partial, so it never runs a fused
         table step."""
+        if self.batch:
+            self._drain_batch()           # collected bins of this workspace run before its owner pass
         if self.used == 0:
             return
         L, log2_T, _, det = self.tag
@@ -250,12 +253,37 @@ class _PendingBins:
         L, log2_T = len(grad_tables), meta["log2_T"]
         P = xyz.shape[0] if n is None else n
         base, det = self._slot(L, log2_T, grad_tables, bin_chunks(P), xyz.device, queue)
-        _lib.call("nerf_hash_encode_bwd_bin_rows", _lib.ptr(xyz, "xyz"), _lib.ptr(rows, "rows", torch.int32, True), count,
-                  P,
-                  meta["bmin"], meta["bmax"], meta["res"], L, log2_T, _lib.ptr(dfeat, "grad_feat", allow_none=True), sp,
-                  sl, d2, _lib.ptr(rows2, "rows2", torch.int32, True), sp2,
-                  sl2, base, self.cap, det, _lib.ptr(self.ws, "workspace", dtype=torch.uint8), self.ws.numel(),
-                  _lib.stream())
+        job = _lib.BinJob(_lib.ptr(xyz, "xyz"), _lib.ptr(rows, "rows", torch.int32, True), count, P,
+                          _lib.ptr(dfeat, "grad_feat", allow_none=True), sp, sl, d2,
+                          _lib.ptr(rows2, "rows2", torch.int32, True), sp2, sl2, base)
+        common = (meta["bmin"], meta["bmax"], meta["res"], L, log2_T)
+        if self.batch is not None:
+            key = (id(self.ws), self.cap, det, L, log2_T, id(meta["bmin"]), id(meta["bmax"]), id(meta["res"]))
+            if self.batch and self.batch[0][1] != key:
+                self._drain_batch()
+            self.batch.append((job, key, common, det, (xyz, rows, dfeat, dfeat2, rows2)))
+            return
+        self._launch_bins([job], common, det)
+
+    def _launch_bins(self, jobs, common, det):
+        _lib.call("nerf_hash_encode_bwd_bin_batch", (_lib.BinJob * len(jobs))(*jobs), len(jobs), *common, self.cap, det,
+                  _lib.ptr(self.ws, "workspace", dtype=torch.uint8), self.ws.numel(), _lib.stream())
+
+    def begin_batch(self):
+        """Collect the following add() calls of one workspace into one nerf_hash_encode_bwd_bin_batch
+        (end_batch; the fine and the coarse bins of an iteration then run as one launch)."""
+        self.batch = []
+
+    def _drain_batch(self):
+        """Launch the collected bins (they target the open workspace) and keep collecting."""
+        if self.batch:
+            _, _, common, det, _ = self.batch[0]
+            self._launch_bins([b[0] for b in self.batch], common, det)
+            self.batch = []
+
+    def end_batch(self):
+        self._drain_batch()
+        self.batch = None
 
     def add_tv(self, job, queue=True):
         """Bin a TV backward (losses.TVBinJob) into the open workspace: its gradient is summed by the
