@@ -7,8 +7,9 @@
  *
  * Conventions
  *   - Every pointer argument named d_* is DEVICE memory, caller-owned, contiguous, float32 unless
- *     typed otherwise; outputs are caller-allocated. The library allocates nothing and keeps no
- *     state between calls (reentrant; safe under stream capture).
+ *     typed otherwise; outputs are caller-allocated. The library allocates nothing (except
+ *     nerf_host_ring_alloc's host ring) and keeps no state between calls (reentrant; safe under
+ *     stream capture).
  *   - Host arrays (level resolutions, table pointer lists, bbox) are read during the call only.
  *   - `stream` is a hipStream_t passed as void* (torch.cuda.current_stream().cuda_stream).
  *   - Return 0 on success, else a NERF_E_* code; nerf_last_error() gives the message (per thread).
@@ -527,6 +528,21 @@ typedef struct {
 } nerf_radam_segment;
 
 int nerf_radam_step(const nerf_radam_segment* segs, int n_segs, const float* d_coef, void* stream);
+
+/* ---- per-step scalars of a captured training step (graphs.StepScalars) ------------------------
+ * The one exception to "the library allocates nothing": nerf_host_ring_alloc returns n_bytes of
+ * pinned, device-mapped, coherent host memory (hipHostMalloc Mapped|Coherent); free it with
+ * nerf_host_ring_free after the last replay that reads it has completed.
+ * nerf_scalars_fetch (one block, the first launch of a captured step) copies slot
+ * (d_ctl[0] mod n_slots) of that ring (n_slots x slot_bytes) into d_dst and advances d_ctl[0]; only
+ * the 4-byte words [0, d_ctl[1]) and [d_ctl[2], d_ctl[2] + d_ctl[3]) are copied. d_ctl: device
+ * int64[4]. done_offset >= 0: the int64 at that byte offset of the ring (past the slots) receives
+ * the new d_ctl[0] once the slot is read, so the host knows which slots it may rewrite. Replaces the
+ * host->device copy and event queued before every replay (graphs.py StepScalars.upload). */
+int nerf_host_ring_alloc(int64_t n_bytes, void** host);
+int nerf_host_ring_free(void* host);
+int nerf_scalars_fetch(const void* host_ring, int64_t slot_bytes, int n_slots, int64_t done_offset, int64_t* d_ctl,
+                       void* d_dst, void* stream);
 
 /* ---- total-variation loss on one hashed cuboid per level (loss.py:11-43) ------------------
  * min_vertex: host int64[n_levels][3] (the reference draws it with torch.randint);

@@ -187,6 +187,9 @@ SIGNATURES = {
     "nerf_rays_pack": [c_vp, c_vp, c_i64, ctypes.c_float, ctypes.c_float, c_int, ctypes.c_float, ctypes.c_float,
                        c_int, c_vp, c_vp],
     "nerf_radam_step": [ctypes.POINTER(RAdamSegment), c_int, c_vp, c_vp],
+    "nerf_host_ring_alloc": [c_i64, ctypes.POINTER(c_vp)],
+    "nerf_host_ring_free": [c_vp],
+    "nerf_scalars_fetch": [c_vp, c_i64, c_int, c_i64, c_vp, c_vp, c_vp],
     "nerf_nearest_pixel": [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp],
     "nerf_tv_fwd": [ctypes.POINTER(c_vp), c_int, c_int, ctypes.POINTER(c_i64), c_vp, ctypes.POINTER(c_int), c_vp,
                     c_vp, c_vp],

@@ -11,12 +11,13 @@ written before each replay (StepScalars): the Philox (seed, offset) of the strat
 importance sampling kernels, the TV cuboid corners (drawn on the host with the same generator as
 the eager path), and RAdam's per-step scalars (step count, N_sma, step size, lr decay). Those are
 computed by the same host code as the eager path ("fillers" registered while capturing), written
-into a pinned ring buffer and copied asynchronously ahead of the replay.
+into a ring of mapped host memory and fetched by the replay's own first launch.
 
 The launch structure itself depends on host state that changes rarely: the TV term switches off
 after iteration 1000 (run_nerf.py:1036-1037) and A-CAQ quantization switches on after the
 embedder's warm-up; GraphedTrainStep re-captures when that key changes.
 """
+import time
 from contextlib import contextmanager
 
 import torch
@@ -40,22 +41,48 @@ def capturing(scalars):
 
 
 class StepScalars:
-    """Device-resident per-step scalars of a captured step (int64 and float32 slots)."""
+    """Device-resident per-step scalars of a captured step (int64 and float32 slots).
+
+    The host writes each replay's values into the next slot of a ring of mapped host memory
+    (nerf_host_ring_alloc); the captured step's first launch (nerf_scalars_fetch) copies that slot
+    into the device slots, picking it with a device counter the launch advances, and publishes how
+    many replays have fetched into the ring, so the host rewrites a slot only after its last reader
+    without an event. Nothing is queued between two replays; the pinned copy + event it replaces
+    cost 8 us per step (profiles/r04zf_ab_upload.jsonl)."""
 
     def __init__(self, device, n_i64=1024, n_f32=1024, ring=4):
-        # one byte buffer per side ([int64 slots | float32 slots]), so an upload is ONE copy
-        nb = 8 * n_i64 + 4 * n_f32
-        self.dev = torch.zeros(nb, dtype=torch.uint8, device=device)
+        import ctypes
+        import numpy as np
+        from . import _lib
+        self.n_i64, self.nb = n_i64, 8 * n_i64 + 4 * n_f32
+        # [int64 slots | float32 slots] on the device; the ring holds `ring` copies of that layout
+        self.dev = torch.zeros(self.nb, dtype=torch.uint8, device=device)
         self.dev_i = self.dev[:8 * n_i64].view(torch.int64)
         self.dev_f = self.dev[8 * n_i64:].view(torch.float32)
-        self.pinned_bytes = [torch.zeros(nb, dtype=torch.uint8).pin_memory() for _ in range(ring)]
-        self.pinned = [(b[:8 * n_i64].view(torch.int64), b[8 * n_i64:].view(torch.float32))
-                       for b in self.pinned_bytes]
-        self.events = [None] * ring
-        self.k = 0
+        self.ctl = torch.zeros(4, dtype=torch.int64, device=device)   # replays, words A, start B, words B
+        h = ctypes.c_void_p()
+        self.done_off = ring * self.nb           # int64 after the slots: fetches completed (device-written)
+        _lib.call("nerf_host_ring_alloc", self.done_off + 64, ctypes.byref(h))
+        self._ring = h.value
+        buf = np.ctypeslib.as_array((ctypes.c_uint8 * (self.done_off + 64)).from_address(self._ring))
+        self.pinned = [(buf[k * self.nb:k * self.nb + 8 * n_i64].view(np.int64),
+                        buf[k * self.nb + 8 * n_i64:(k + 1) * self.nb].view(np.float32)) for k in range(ring)]
+        self.done = buf[self.done_off:self.done_off + 8].view(np.int64)
+        self.done[0] = 0
+        self.issued = 0    # uploads so far = index of the replay the next upload prepares
         self.step = 0      # the global step of the replay being prepared (fillers may read it)
         self.ni = self.nf = 0
         self.fillers = []
+
+    def __del__(self):
+        ring, self._ring = getattr(self, "_ring", None), None
+        if ring:
+            from . import _lib
+            try:
+                torch.cuda.synchronize(self.dev.device)     # no replay still reads the ring
+                _lib.call("nerf_host_ring_free", ring)
+            except Exception:      # interpreter shutdown: the process's mappings go with it
+                pass
 
     def alloc_i64(self, n):
         if self.ni + n > self.dev_i.numel():
@@ -73,21 +100,33 @@ class StepScalars:
         """fn(host_int64_numpy, host_float32_numpy) writes this step's values into its slots."""
         self.fillers.append(fn)
 
+    def capture_fetch(self):
+        """The fetch launch: first in the captured step, on the capture stream."""
+        from . import _lib
+        _lib.call("nerf_scalars_fetch", self._ring, self.nb, len(self.pinned), self.done_off,
+                  _lib.ptr(self.ctl, "ctl", torch.int64), self.dev.data_ptr(), _lib.stream())
+
+    def seal(self):
+        """After the capture: the words the fetch copies (the slots the capture allocated)."""
+        self.ctl.copy_(torch.tensor([0, 2 * self.ni, 2 * self.n_i64, self.nf], dtype=torch.int64))
+        torch.cuda.synchronize(self.dev.device)
+        self.done[0] = 0
+        self.issued = 0
+
     def upload(self):
-        """Run every filler into the next pinned ring slot and copy it to the device (async,
-        stream-ordered before the replay that reads it)."""
-        k = self.k
-        self.k = (k + 1) % len(self.pinned)
-        if self.events[k] is not None:
-            self.events[k].synchronize()          # the copy that last read this slot has completed
-        hi, hf = self.pinned[k]
-        ni, nf = hi.numpy(), hf.numpy()
+        """Run every filler into the ring slot the next replay fetches (call once before each replay)."""
+        n, R = self.issued, len(self.pinned)
+        if int(self.done[0]) < n - R + 1:        # replay n - R has not fetched this slot yet
+            deadline = time.monotonic() + 60.0
+            while int(self.done[0]) < n - R + 1:
+                if time.monotonic() > deadline:
+                    raise RuntimeError(f"StepScalars: replay {n - R} never fetched its scalars (each upload() "
+                                       "must be followed by one replay of the captured step)")
+                time.sleep(0)
+        hi, hf = self.pinned[n % R]
         for fn in self.fillers:
-            fn(ni, nf)
-        self.dev.copy_(self.pinned_bytes[k], non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record()
-        self.events[k] = ev
+            fn(hi, hf)
+        self.issued = n + 1
 
 
 class GraphedTrainStep:
@@ -161,6 +200,7 @@ class GraphedTrainStep:
                 hashgrid.fused_table_step(dev, self.opt, emb.tables(), enabled=self.hook is None):
             with capturing(sc):
                 with torch.cuda.graph(g1, pool=pool, stream=side):
+                    sc.capture_fetch()
                     out = forward_backward(self.rays, self.target, self.kw, self.opt, self.args, global_step,
                                            H=self.H, W=self.W, K=self.K, loss_scale_sparsity=self.scale_sp,
                                            tv_generator=self.tv_gen, zero_grad=self.zero_grad, schedule=False)
@@ -170,6 +210,7 @@ class GraphedTrainStep:
                     with torch.cuda.graph(g2, pool=pool, stream=side):
                         optimizer_update(self.opt)
         torch.cuda.current_stream(dev).wait_stream(side)
+        sc.seal()
         emb.current_step = step0
         self.graphs = (g1, g2)
         self.out = out
