@@ -1,3 +1,7 @@
+# Round 4's A/B of the captured step's scalar upload (profiles/r04zc_diag_constant_jitter.jsonl,
+# profiles/r04zf_ab_upload.jsonl). The NERF_DIAG_UPLOAD modes it selects (copy / event / spin / none)
+# were a temporary switch in graphs.StepScalars, removed once "spin" (the in-graph fetch) was adopted:
+# re-running it needs that switch patched back in. usage: bash tools/gpu_ab_upload.sh OUT
 set -o pipefail
 out=${1:-r04ze}
 mkdir -p gpurun_out/$out
