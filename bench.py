@@ -262,6 +262,10 @@ def parse():
                          "0: every sample")
     ap.add_argument("--coarse-reuse", type=int, default=1,
                     help="1: the fine pass reuses the coarse pass's hash encoding (DESIGN §8.5); 0: re-encode (A/B)")
+    ap.add_argument("--fresh-rays", type=int, default=1,
+                    help="also time the step with a new ray batch every iteration (train()'s no_batching draw: "
+                         "one random view, N_rand random pixels; blender-rig workloads, graph mode): "
+                         "fresh_rays_ms_per_step in the line")
     ap.add_argument("--mode", default="train", choices=["train", "render"],
                     help="train: full training iteration (the metric); render: render-only (eval modules, no grad)")
     return ap.parse_args()
@@ -292,6 +296,27 @@ WORKLOADS = {
                  desc="lego + A-CAQ train step: {R} rays/GPU x (64 + 128) samples, 8-bit learned-bitwidth quantizers "
                       "on the 16 levels, W0 and the hidden activation (past warm-up, calibrated)"),
 }
+
+
+PRODUCT_TREE = ("indoor-nerf_amd", "include")
+
+
+def product_tree_sha():
+    """sha256 over the product's sources (indoor-nerf_amd/*.py, csrc/*, include/*.h), path-sorted:
+    identifies the tree a committed result (profiles/*_psnr_vs_reference.json) was produced by. Works
+    without git (the GPU box receives the tree without .git)."""
+    import hashlib
+    h = hashlib.sha256()
+    files = []
+    for top in PRODUCT_TREE:
+        for dp, dns, fns in os.walk(os.path.join(ROOT, top)):
+            dns[:] = sorted(d for d in dns if d != "__pycache__")
+            files += [os.path.join(dp, f) for f in fns if f.endswith((".py", ".hip", ".h", ".cpp"))]
+    for f in sorted(files):
+        h.update(os.path.relpath(f, ROOT).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
 
 
 def cpu_model():
@@ -372,15 +397,14 @@ def cpu_leg(n_rays, finest, H, warmup, timed):
 
 def cpu_baseline(n_rays, warmup, timed):
     """SURVEY.md §8(d)'s CPU baseline on the GPU box's host cores, rank 0 at N=1 only. `value` is the
-    lego leg (configs[1]: finest 1024, 800x800) at the bench's own batch (n_rays = 4096), 2 warm-up
-    iterations and the median of 2 (RAdam's update is still off there, radam.py:63-92: a ~10 ms dense
-    pass of a ~9 s iteration). The same leg at 1024 rays with `warmup` warm-ups (RAdam active) and the
-    median of `timed` is reported beside it, so the batch-size effect is measured, and the
-    chair leg is BASELINE configs[0] (chair 400x400, finest_res 512, the reference's CPU path:
-    configs/chair.txt) at its own N_rand of 1024."""
+    lego leg (configs[1]: finest 1024, 800x800) at the bench's own batch (n_rays = 4096), `warmup`
+    (6) warm-up iterations, so RAdam's update is active (radam.py:63-92: N_sma >= 5 from step 6), and
+    the median of `timed` (3). The same leg at 1024 rays is reported beside it, so the batch-size
+    effect is measured, and the chair leg is BASELINE configs[0] (chair 400x400,
+    finest_res 512, the reference's CPU path: configs/chair.txt) at its own N_rand of 1024."""
     cores, threads = cpu_threads()
     torch.set_num_threads(threads)
-    lego = cpu_leg(n_rays, 1024, 800, 2, 2)
+    lego = cpu_leg(n_rays, 1024, 800, warmup, timed)
     lego_1k = cpu_leg(1024, 1024, 800, warmup, timed)
     chair = cpu_leg(1024, 512, 400, warmup, timed)
     return {"value": lego["value"], "unit": "rays/s", "cores": threads, "kind": "port",
@@ -390,6 +414,55 @@ def cpu_baseline(n_rays, warmup, timed):
             "threads_note": "torch.set_num_threads = the job's CPU share (OMP_NUM_THREADS) within the affinity mask",
             "lego_1024_rays": lego_1k,
             "chair": {**chair, "config": "BASELINE configs[0]: chair 400x400, finest_res 512 (configs/chair.txt)"}}
+
+
+def fresh_rays_leg(a, kw, opt, args, arena, hook, post, world, dev, it, rank):
+    """The same training step with a NEW ray batch every iteration, as train() draws it for the lego
+    config (configs/lego.txt: no_batching = True; run_nerf.py:975-1004): one of the rig's 100 training
+    views (np.random.choice) and N_rand = R distinct pixels of it (rays.RaySampler: the image set and
+    the cameras resident in HBM, one nerf_sample_rays_sel launch inside the captured step reading the
+    replay's (image, seed, offset) slot). Past the precrop phase (precrop_iters = 500 of 8,001
+    iterations): the whole 800 x 800 image. Synthetic images (no dataset on the box): U[0,1) colours.
+    Returns (ms per step over a.steps timed steps after a.warmup, the next iteration index)."""
+    from indoor_nerf_amd import RaySampler
+    from indoor_nerf_amd.graphs import GraphedTrainStep
+    from indoor_nerf_amd.synthetic import CAMERA_ANGLE_X, pose_spherical
+    H = W = 800
+    n_img = 100
+    focal = 0.5 * W / np.tan(0.5 * CAMERA_ANGLE_X)
+    K = np.array([[focal, 0, 0.5 * W], [0, focal, 0.5 * H], [0, 0, 1]])
+    poses = np.stack([pose_spherical(t, -30.0, 4.0311) for t in np.linspace(-180, 180, n_img + 1)[:-1]])
+    g = torch.Generator(device=dev).manual_seed(1000 + rank)
+    images = torch.rand(n_img, H, W, 3, device=dev, generator=g)
+    R = a.rays if a.scaling == "weak" else a.rays // world
+    np.random.seed(2000 + rank)            # the image draw (np.random.choice, as train())
+    sampler = RaySampler(images, poses, H, W, K, np.arange(n_img), R, precrop_iters=0, device=dev)
+    del images
+    rays = (torch.empty(R, 3, device=dev), torch.empty(R, 3, device=dev))
+    target = torch.empty(R, 3, device=dev)
+    tv_gen = torch.Generator().manual_seed(8)
+    st = GraphedTrainStep(rays, target, kw, opt, args, H=H, W=W, grad_hook=hook, loss_scale_sparsity=float(world),
+                          tv_generator=tv_gen, zero_grad=arena.zero_, post_hook=post, sampler=sampler)
+    for _ in range(a.warmup):
+        st(it)
+        it += 1
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        st(it)
+        it += 1
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return 1e3 * elapsed / a.steps, it, bool(st.captures > 0)
 
 
 def launch_ranks(a):
@@ -624,6 +697,17 @@ def main():
                                               "x1.56 for the owner pass's 8-B + 2-B entries: "
                                               "profiles/r03a_pmc_calibration.json) + WRITE_SIZE per call, separate "
                                               "PMC passes of this bench, x calls per iteration")
+    fresh = None
+    if a.fresh_rays and gstep is not None and wl["rays"] == "blender":
+        fresh_ms, it, fresh_graphed = fresh_rays_leg(a, kw, opt, args, arena, hook, post, world, dev, it, rank)
+        fresh = {"ms_per_step": round(fresh_ms, 3),
+                 "value": round((a.rays if strong else world * a.rays) / (fresh_ms * 1e-3), 1), "unit": "rays/s",
+                 "hip_graph": fresh_graphed,
+                 "batch": "a new batch every iteration as train() draws it for configs/lego.txt (no_batching): one "
+                          "of 100 lego-rig views at random, R distinct random pixels of the whole 800x800 image "
+                          "(past precrop), drawn on the device inside the captured step (nerf_sample_rays_sel); "
+                          "synthetic U[0,1) images",
+                 "vs_fixed_batch_ms": round(fresh_ms - 1e3 * elapsed / a.steps, 3)}
     step_s = elapsed / a.steps
     step_bytes = points_per_step * STEP_BYTES_PER_POINT + STEP_DENSE_BYTES + R * STEP_RAY_BYTES
     step_roofline = None
@@ -663,6 +747,8 @@ def main():
                                                       "mlp_bwd_points": active["mlp_points"],
                                                       "hash_bwd_points": active["hash_points"]},
         "loss": round(float(loss), 6),
+        "fresh_rays_ms_per_step": None if fresh is None else fresh["ms_per_step"],
+        "fresh_rays": fresh,
         "roofline": roofline,
         "step_roofline": step_roofline,
         "ops": ops,
@@ -687,6 +773,10 @@ def main():
                     k: v["d_db"] for k, v in pj["all_seeds"].items() if isinstance(v, dict)}
             out["psnr_vs_reference"]["source"] = "profiles/" + name + (
                 " (commit " + pj["commit"] + ")" if isinstance(pj.get("commit"), str) else "")
+            # stale: the file was produced by another product tree than the one benched here (or does not
+            # say which); tests/test_gpu_converge.py re-checks the bar at every GPU test run
+            out["psnr_vs_reference"]["tree_sha"] = pj.get("tree_sha")
+            out["psnr_vs_reference"]["stale"] = pj.get("tree_sha") != product_tree_sha()
             break
     if rank == 0 and world == 1 and not a.no_cpu_baseline and a.workload == "lego" and a.mode == "train":
         out["cpu_baseline"] = cpu_baseline(a.cpu_rays, a.cpu_warmup, a.cpu_steps)

@@ -489,6 +489,16 @@ int nerf_sample_rays(const nerf_camera* cam, int H, int W, int crop_r0, int crop
                      int64_t n_rays, int random, uint64_t seed, uint64_t offset,
                      const float* d_image, int channels, float* d_rays_o, float* d_rays_d, float* d_target,
                      int32_t* d_coords, void* stream);
+/* nerf_sample_rays (random = 1) with the image chosen on the device: d_sel = {image index, seed,
+ * offset} (device int64[3], read by the launch — a captured training step's per-replay slots: train()
+ * draws a new image and pixel batch every iteration, run_nerf.py:975-1004); d_cams [n_images]
+ * nerf_camera and d_images [n_images, H, W, channels] float32 (may be NULL if d_target is NULL)
+ * resident on the device; the image index is taken mod n_images. Bit-identical to nerf_sample_rays
+ * with that image's camera and image, the same seed and offset. */
+int nerf_sample_rays_sel(const nerf_camera* d_cams, const float* d_images, int64_t n_images, int H, int W,
+                         int channels, int crop_r0, int crop_c0, int crop_h, int crop_w, int64_t n_rays,
+                         const int64_t* d_sel, float* d_rays_o, float* d_rays_d, float* d_target,
+                         int32_t* d_coords, void* stream);
 
 /* render()'s ray batch (run_nerf.py:115-140): viewdir = d/|d| of the world direction, optional
  * ndc_rays with near plane 1 (run_nerf_helpers.py:333-350; ndc_coef_w/h = float32 of
@@ -537,8 +547,11 @@ int nerf_radam_step(const nerf_radam_segment* segs, int n_segs, const float* d_c
  * (d_ctl[0] mod n_slots) of that ring (n_slots x slot_bytes) into d_dst and advances d_ctl[0]; only
  * the 4-byte words [0, d_ctl[1]) and [d_ctl[2], d_ctl[2] + d_ctl[3]) are copied. d_ctl: device
  * int64[4]. done_offset >= 0: the int64 at that byte offset of the ring (past the slots) receives
- * the new d_ctl[0] once the slot is read, so the host knows which slots it may rewrite. Replaces the
- * host->device copy and event queued before every replay (graphs.py StepScalars.upload). */
+ * the new d_ctl[0] once the slot is read, so the host knows which slots it may rewrite; the last 8
+ * bytes of every slot then hold the index (int64) of the replay the host wrote the slot for, and a
+ * fetch that finds another index than its d_ctl[0] stores d_ctl[0] + 1 into the int64 at
+ * done_offset + 8 (sticky: only while that word is 0; the ring holds done_offset + 16 bytes or more).
+ * Replaces the host->device copy and event queued before every replay (graphs.py StepScalars.upload). */
 int nerf_host_ring_alloc(int64_t n_bytes, void** host);
 int nerf_host_ring_free(void* host);
 int nerf_scalars_fetch(const void* host_ring, int64_t slot_bytes, int n_slots, int64_t done_offset, int64_t* d_ctl,

@@ -4,6 +4,7 @@ The product path has no fallback: if the library is missing, cannot be loaded, o
 contiguous float32 CUDA tensor, the call raises. Kernel errors raise RuntimeError with the
 library's message (nerf_last_error).
 """
+import contextlib
 import ctypes
 import os
 
@@ -182,6 +183,8 @@ SIGNATURES = {
                               c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
     "nerf_sample_rays": [ctypes.POINTER(Camera), c_int, c_int, c_int, c_int, c_int, c_int, c_i64, c_int, c_u64,
                          c_u64, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp],
+    "nerf_sample_rays_sel": [c_vp, c_vp, c_i64, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_i64, c_vp, c_vp,
+                             c_vp, c_vp, c_vp, c_vp],
     "nerf_rays_pack_z": [c_vp, c_vp, c_i64, ctypes.c_float, ctypes.c_float, c_int, ctypes.c_float, ctypes.c_float,
                          c_int, c_vp, ctypes.POINTER(ZeroRange), c_int, c_vp],
     "nerf_rays_pack": [c_vp, c_vp, c_i64, ctypes.c_float, ctypes.c_float, c_int, ctypes.c_float, ctypes.c_float,
@@ -302,10 +305,14 @@ def stream():
 
 
 # Zero fills folded into a later launch (nerf_rays_pack_z: render()'s first kernel): a training step
-# registers its MLP-gradient zero and its TV loss accumulator here before render(), and whoever needs
-# one of them zero before that launch took it calls flush_zero_fills first.
-_ZERO_FILLS = []
+# (model.forward_backward, inside zero_deferral()) registers its MLP-gradient zero and its TV loss
+# accumulator here before render(), and whoever needs one of them zero before that launch took it
+# calls flush_zero_fills first. Pending fills are kept per device: a render() on one device takes only
+# that device's ranges. Outside a training step's scope every fill is done at once, so public callers
+# (GradArena.zero_() followed by a read of p.grad, or a backward of their own) never see stale values.
+_ZERO_FILLS = {}   # device index -> [tensor]
 _FOLD_FILLS = {"on": True}
+_DEFER_SCOPE = [0]
 
 
 def set_fold_fills(enabled=True):
@@ -313,37 +320,57 @@ def set_fold_fills(enabled=True):
     _FOLD_FILLS["on"] = bool(enabled)
 
 
+@contextlib.contextmanager
+def zero_deferral():
+    """Scope of one training iteration (model.forward_backward): zero fills and the tables' deferred
+    gradient zero may wait for the launches that consume them."""
+    _DEFER_SCOPE[0] += 1
+    try:
+        yield
+    finally:
+        _DEFER_SCOPE[0] -= 1
+
+
+def zero_deferral_active():
+    return _DEFER_SCOPE[0] > 0
+
+
 def defer_fill_zero(t):
-    """Zero the contiguous float32 CUDA tensor `t` in the next nerf_rays_pack_z launch (or at
-    flush_zero_fills, whichever comes first)."""
-    if not (_FOLD_FILLS["on"] and t.is_cuda and t.dtype == torch.float32 and t.is_contiguous()):
+    """Zero the contiguous float32 CUDA tensor `t` in the next nerf_rays_pack_z launch on its device (or
+    at flush_zero_fills, whichever comes first); at once outside zero_deferral()."""
+    if not (_FOLD_FILLS["on"] and _DEFER_SCOPE[0] > 0 and t.is_cuda and t.dtype == torch.float32
+            and t.is_contiguous()):
         t.zero_()
         return
-    _ZERO_FILLS.append(t)
+    _ZERO_FILLS.setdefault(t.device.index, []).append(t)
 
 
-def take_zero_fills():
-    """Up to MAX_ZERO_RANGES pending fills as a ZeroRange array (ctypes) + count; they are done by the
-    caller's launch."""
-    taken = _ZERO_FILLS[:MAX_ZERO_RANGES]
-    del _ZERO_FILLS[:MAX_ZERO_RANGES]
+def take_zero_fills(device):
+    """Up to MAX_ZERO_RANGES pending fills of `device` as a ZeroRange array (ctypes) + count; they are
+    done by the caller's launch."""
+    pending = _ZERO_FILLS.get(torch.device(device).index, [])
+    taken = pending[:MAX_ZERO_RANGES]
+    del pending[:MAX_ZERO_RANGES]
     arr = (ZeroRange * max(1, len(taken)))(*[ZeroRange(t.data_ptr(), t.numel()) for t in taken])
     return arr, len(taken), taken
 
 
 def flush_zero_fills(tensors=None):
-    """Zero pending fills now: those overlapping the given tensors, or all."""
-    global _ZERO_FILLS
+    """Zero pending fills now: those overlapping the given tensors, or all (every device)."""
+    todo = []
     if tensors is None:
-        todo, _ZERO_FILLS = _ZERO_FILLS, []
+        for pending in _ZERO_FILLS.values():
+            todo += pending
+            pending.clear()
     else:
-        spans = [(t.data_ptr(), t.data_ptr() + t.numel() * t.element_size()) for t in tensors]
+        spans = [(t.device.index, t.data_ptr(), t.data_ptr() + t.numel() * t.element_size()) for t in tensors]
 
         def hit(z):
             a, b = z.data_ptr(), z.data_ptr() + z.numel() * 4
-            return any(a < e and s < b for s, e in spans)
-        todo = [z for z in _ZERO_FILLS if hit(z)]
-        _ZERO_FILLS = [z for z in _ZERO_FILLS if not hit(z)]
+            return any(d == z.device.index and a < e and s < b for d, s, e in spans)
+        for pending in _ZERO_FILLS.values():
+            todo += [z for z in pending if hit(z)]
+            pending[:] = [z for z in pending if not hit(z)]
     for z in todo:
         z.zero_()
 

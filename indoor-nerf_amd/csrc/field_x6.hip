@@ -204,6 +204,18 @@ __device__ __forceinline__ S3 tr_read(const __bf16* img, int piece, int base, in
     return s;
 }
 
+// tr_read for a row-stacked A operand (stride S32 images): lanes m < 16 (16-lane groups 0 and 2)
+// take columns 0..15 of the block starting at element base_lo, lanes m >= 16 (groups 1 and 3) the
+// same columns of the block at base_hi, k over the block's 16 rows (one piece each)
+__device__ __forceinline__ u32x4 tr_read_pair(const __bf16* img, int base_lo, int base_hi, int lane) {
+    const int g = lane >> 4, il = lane & 15, q = il >> 2, p = il & 3, h = g >> 1;
+    const int oa = ((g & 1) ? base_hi : base_lo) + (4 * h + q) * S32 + 4 * p;
+    const bf16x4 ta = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(img + oa));
+    const bf16x4 tb = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(img + oa + 8 * S32));
+    const u32x2 a = __builtin_bit_cast(u32x2, ta), b = __builtin_bit_cast(u32x2, tb);
+    return u32x4{a.x, a.y, b.x, b.y};
+}
+
 // Stage chunk c of a 32-row tile (lane = point j) into a [32 points][S] staging image at
 // columns col_t + 16c + 4h + (i&3) + 8(i>>2).
 __device__ __forceinline__ void stage(__bf16* st, int piece, int S, const S3& s, int col_t, int c, int j, int h) {
@@ -375,19 +387,55 @@ __device__ __forceinline__ void layer0(const __bf16* img, const float (&x)[16], 
     layer0_split<QUANT>(img, xb, h1, m1, lane, aq);
 }
 
-// forward chain up to h3 (and rgb when need_rgb)
+// One weight piece per row half of a 32-row A operand: lane m reads the row starting at element
+// row_lo (m < 16) or row_hi (m >= 16), columns col0 + (i&3) + 8(i>>2)
+__device__ __forceinline__ u32x4 row_read_pair(const __bf16* img, int row_lo, int row_hi, int m, int col0) {
+    const int o0 = (m < 16 ? row_lo : row_hi) + col0;
+    const u32x2 a = *reinterpret_cast<const u32x2*>(img + o0);
+    const u32x2 b = *reinterpret_cast<const u32x2*>(img + o0 + 8);
+    return u32x4{a.x, a.y, b.x, b.y};
+}
+
+// A 16-row layer (W1: o = W1 h1) on 32x32x16 tiles with the two row halves carrying different weight
+// pieces: A01 = [a0 ; a1] and A2z = [a2 ; 0], so four MFMAs per k-chunk form the six x6 terms (and
+// a1 b2): rows r and r + 16 of the accumulator hold the two partial sums (the caller adds them).
+// The half-empty tile took six MFMAs per k-chunk.
+__device__ __forceinline__ floatx16 mma4_rows16(const u32x4& A01, const u32x4& A2z, const S3& B, floatx16 c) {
+    c = X6_MFMA(A2z, B.p[0], c);   // a2 b0 | 0
+    c = X6_MFMA(A01, B.p[2], c);   // a0 b2 | a1 b2
+    c = X6_MFMA(A01, B.p[1], c);   // a0 b1 | a1 b1
+    c = X6_MFMA(A01, B.p[0], c);   // a0 b0 | a1 b0
+    return c;
+}
+
+// rows 0..15 of a row-stacked accumulator: registers r and r + 8 of a lane hold rows R and R + 16
+__device__ __forceinline__ floatx16 fold_rows16(const floatx16& acc) {
+    floatx16 o = zero16();
+#pragma unroll
+    for (int r = 0; r < 8; ++r) o[r] = acc[r] + acc[r + 8];
+    return o;
+}
+
+// forward chain up to h3 (the output layer C2 is the caller's: forward kernel rgb_c2)
 template <bool QUANT>
-__device__ __forceinline__ void fwd_chain(const __bf16* img, const InX6& in, ActX6& f, floatx16& rgb, int lane,
-                                          bool need_rgb, const QuantRec& aq) {
+__device__ __forceinline__ void fwd_chain(const __bf16* img, const InX6& in, ActX6& f, int lane, const QuantRec& aq) {
     const int m = lane & 31, h = lane >> 5;
     layer0<QUANT>(img, in.x, f.h1, f.m1, lane, aq);
-    // L1: o = W1 h1 (rows 16..31 of the tile are never read)
-    f.o = zero16();
+    // L1: o = W1 h1, row-stacked pieces; the zero half reads rows of C2's zero padding (rows 3..15)
+    {
+        floatx16 acc = zero16();
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+        for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int c = 0; c < 2; ++c)
-            f.o = mma6(row_read(img, IM_W1, S64, m & 15, 32 * t + 16 * c + 4 * h), split_chunk(f.h1[t], c), f.o);
+            for (int c = 0; c < 2; ++c) {
+                const int col0 = 32 * t + 16 * c + 4 * h;
+                const int r = IM_W1 + (m & 15) * S64;
+                const u32x4 A01 = row_read_pair(img, r, IM_PIECE + r, m, col0);
+                const u32x4 A2z = row_read_pair(img, 2 * IM_PIECE + r, IM_C2 + 8 * S64, m, col0);
+                acc = mma4_rows16(A01, A2z, split_chunk(f.h1[t], c), acc);
+            }
+        f.o = fold_rows16(acc);
+    }
     // C0: h2 = relu(C0' [o rows 0..15 ; sh])
     f.h2[0] = f.h2[1] = zero16();
     {
@@ -412,14 +460,56 @@ __device__ __forceinline__ void fwd_chain(const __bf16* img, const InX6& in, Act
                 f.h3[to] = mma6(row_read(img, IM_C1, S64, 32 * to + m, 32 * t + 16 * c + 4 * h), hb, f.h3[to]);
         }
     relu16i(f.h3[0]); relu16i(f.h3[1]);
-    if (!need_rgb) return;
-    // C2: rgb = C2 h3 (rows 0..2 used)
-    rgb = zero16();
+}
+
+// Output layer rgb = C2 h3 (3 rows) in exact fp32 VALU: on 32-row tiles it used 3 of 32 rows and
+// needed the h3 split (24 MFMAs + 176 VALU per tile). Lane (j, h) holds h3 at neurons
+// 32t + row_of(r, h): it forms the three partial dot products over those 32 neurons (fp32 FMA chains,
+// weights from an fp32 LDS image [h][o][32]: ds_read_b128 broadcasts), and two v_permlane32_swap
+// exchanges add the lane halves' partials. Every lane ends with all three outputs of its point.
+constexpr int C2F_FLOATS = 2 * 3 * 32;
+
+__device__ inline void fill_c2f(float* c2f, const nerf_mlp_weights& W) {
+    for (int idx = threadIdx.x; idx < C2F_FLOATS; idx += blockDim.x) {
+        const int hh = idx / 96, o = (idx / 32) % 3, k = idx & 31;
+        c2f[idx] = W.c2[o * 64 + 32 * (k >> 4) + row_of(k & 15, hh)];
+    }
+}
+
+__device__ __forceinline__ float swap_half_sum(float lo, float hi, float& other) {
+    // lanes 32..63 of `lo` trade places with lanes 0..31 of `hi`: afterwards lanes 0..31 hold
+    // (lo_lo, lo_hi) and lanes 32..63 (hi_lo, hi_hi), so one add gives lo's half sum in the lower
+    // lanes and hi's in the upper lanes
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(lo), __float_as_uint(hi), false, false);
+    other = __uint_as_float(r[1]);
+    return __uint_as_float(r[0]);
+}
+
+__device__ __forceinline__ void rgb_c2(const float* c2f, const floatx16 (&h3)[2], int h, float (&rgb)[3]) {
+    const float4* w4 = reinterpret_cast<const float4*>(c2f + 96 * h);
+    float p[3];
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int o = 0; o < 3; ++o) {
+        float acc = 0.f;
 #pragma unroll
-        for (int c = 0; c < 2; ++c)
-            rgb = mma6(row_read(img, IM_C2, S64, m & 15, 32 * t + 16 * c + 4 * h), split_chunk(f.h3[t], c), rgb);
+        for (int q = 0; q < 8; ++q) {
+            const float4 w = w4[8 * o + q];
+            const int k = 4 * q;
+            acc = __builtin_fmaf(w.x, h3[k >> 4][k & 15], acc);
+            acc = __builtin_fmaf(w.y, h3[(k + 1) >> 4][(k + 1) & 15], acc);
+            acc = __builtin_fmaf(w.z, h3[(k + 2) >> 4][(k + 2) & 15], acc);
+            acc = __builtin_fmaf(w.w, h3[(k + 3) >> 4][(k + 3) & 15], acc);
+        }
+        p[o] = acc;
+    }
+    float b, d;
+    const float a = swap_half_sum(p[0], p[1], b);
+    const float s01 = a + b;                       // lanes 0..31: rgb0, lanes 32..63: rgb1
+    const float c = swap_half_sum(p[2], p[2], d);
+    rgb[2] = c + d;                                // every lane
+    float e;
+    rgb[0] = swap_half_sum(s01, s01, e);           // the lower lanes' value, in every lane
+    rgb[1] = e;
 }
 
 // ================================================================ forward kernel
@@ -428,7 +518,9 @@ template <bool QUANT>
 // waves per SIMD (105 VGPRs) instead of 2 with 256-thread blocks
 __global__ void __launch_bounds__(512, 2) mlp_fwd_x6_kernel(MlpArgs a) {
     __shared__ __attribute__((aligned(16))) __bf16 img[3 * IM_PIECE];
+    __shared__ __attribute__((aligned(16))) float c2f[C2F_FLOATS];
     fill_images(img, a.W);
+    fill_c2f(c2f, a.W);
     __syncthreads();
     const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
     QuantRec aq{};
@@ -439,8 +531,10 @@ __global__ void __launch_bounds__(512, 2) mlp_fwd_x6_kernel(MlpArgs a) {
         InX6 in;
         load_in_x6(a, tile, j, h, in);
         ActX6 f;
-        floatx16 rgb;
-        fwd_chain<QUANT>(img + opaque_zero(), in, f, rgb, lane, true, aq);
+        const int z = opaque_zero();
+        fwd_chain<QUANT>(img + z, in, f, lane, aq);
+        float rgb[3];
+        rgb_c2(c2f + z, f.h3, h, rgb);
         const uint32_t orow = in.valid ? io_row(a, in.pt) : 0u;
         if (h == 0 && in.valid) {
             const bool keep = a.keep ? a.keep[in.pt] != 0 : true;
@@ -545,6 +639,10 @@ constexpr int ACTF_FLOATS = 64 * SPF;                     // 9,216 B
 // per wave pair: the activation image and TWO gradient buffers (stage k uses buffer k & 1)
 constexpr int ST_CG = 2 * ACTF_FLOATS + 6 * STG_PIECE;    // bf16 elements (23,040 B)
 constexpr int X6_CG_LDS = IM_BYTES + 4 * ST_CG * 2;       // 158,976 B
+// and behind it a zero block of 16 rows x S32 (1,152 B): the zero half of row-stacked transposed
+// A operands (tr_read_pair)
+constexpr int X6_ZBLK = X6_CG_LDS / 2;                    // element offset from the image
+constexpr int X6_ZBLK_ELEMS = 16 * S32;
 
 __device__ __forceinline__ void stage_tileF(float* actF, const floatx16& v, int row0, int j, int h) {
 #pragma unroll
@@ -590,8 +688,7 @@ __device__ __forceinline__ void bwd_chain_role(const MlpArgs& a, const __bf16* i
         InX6 in;
         load_in_x6_bwd(a, n_pts, tile, j, h, in);
         ActX6 f;
-        floatx16 unused;
-        fwd_chain<QUANT>(imt, in, f, unused, lane, false, aq);
+        fwd_chain<QUANT>(imt, in, f, lane, aq);
 
         const uint32_t orow = io_row(a, in.valid ? in.pt : (uint32_t)(a.P - 1));
         float4 g4 = *reinterpret_cast<const float4*>(a.graw + 4u * orow);
@@ -651,6 +748,9 @@ __device__ __forceinline__ void bwd_chain_role(const MlpArgs& a, const __bf16* i
                 if (row >= 1) go[r] = a.dgeo[16u * orow + row];
             }
         }
+        // without an SH gradient only rows 0..15 of go (sigma, geo) are live: their A operand C0'^T
+        // is row-stacked as in fwd_chain's W1 layer (four MFMAs per k-chunk instead of six)
+        const bool stack = a.dsh == nullptr;
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
             const S3 g0 = split_chunk(ga2[t], 0), g1 = split_chunk(ga2[t], 1);
@@ -665,9 +765,20 @@ __device__ __forceinline__ void bwd_chain_role(const MlpArgs& a, const __bf16* i
             stage_grad(stGb[t], g0, 0, j, h);
             stage_grad(stGb[t], g1, 1, j, h);
             publish();
-            go = mma6(tr_read(imt, IM_PIECE, IM_C0, S32, 32 * t, 0, lane), g0, go);
-            go = mma6(tr_read(imt, IM_PIECE, IM_C0, S32, 32 * t + 16, 0, lane), g1, go);
+            if (stack) {
+#pragma unroll
+                for (int c = 0; c < 2; ++c) {
+                    const int row0 = IM_C0 + (32 * t + 16 * c) * S32;
+                    const u32x4 A01 = tr_read_pair(imt, row0, IM_PIECE + row0, lane);
+                    const u32x4 A2z = tr_read_pair(imt, 2 * IM_PIECE + row0, X6_ZBLK, lane);
+                    go = mma4_rows16(A01, A2z, c ? g1 : g0, go);
+                }
+            } else {
+                go = mma6(tr_read(imt, IM_PIECE, IM_C0, S32, 32 * t, 0, lane), g0, go);
+                go = mma6(tr_read(imt, IM_PIECE, IM_C0, S32, 32 * t + 16, 0, lane), g1, go);
+            }
         }
+        if (stack) go = fold_rows16(go);
         if (a.dsh && in.valid) {
 #pragma unroll
             for (int r = 8; r < 16; ++r) a.dsh[16u * orow + row_of(r, h) - 16] = go[r];
@@ -962,7 +1073,7 @@ struct MlpBwdJobs {
 
 template <bool QUANT>
 __global__ void __launch_bounds__(512, 1) mlp_bwd_x6cg_kernel(MlpBwdJobs jobs) {
-    __shared__ __attribute__((aligned(16))) __bf16 lds[X6_CG_LDS / 2];
+    __shared__ __attribute__((aligned(16))) __bf16 lds[X6_CG_LDS / 2 + X6_ZBLK_ELEMS];
     __shared__ int flags[8];   // ready[0..3], ack[0..3]
     const bool second = (int)blockIdx.x >= jobs.split;
     const MlpArgs& a = second ? jobs.a[1] : jobs.a[0];
@@ -974,6 +1085,7 @@ __global__ void __launch_bounds__(512, 1) mlp_bwd_x6cg_kernel(MlpBwdJobs jobs) {
     __bf16* stA = lds + 3 * IM_PIECE + p * ST_CG;   // fp32 activation image (actF)
     __bf16* stG = stA + 2 * ACTF_FLOATS;
     fill_images(img, a.W);
+    for (int i = threadIdx.x; i < X6_ZBLK_ELEMS / 2; i += blockDim.x) reinterpret_cast<uint32_t*>(img + X6_ZBLK)[i] = 0u;
     if (threadIdx.x < 8) flags[threadIdx.x] = 0;
     __syncthreads();
 

@@ -135,16 +135,90 @@ __global__ void __launch_bounds__(256) rays_pack_kernel(PackArgs a) {
     }
 }
 
-static uint32_t splitmix(uint64_t& s) {
+__host__ __device__ __forceinline__ uint32_t splitmix(uint64_t& s) {
     uint64_t z = (s += 0x9E3779B97F4A7C15ull);
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
     return (uint32_t)((z ^ (z >> 31)) >> 16);
 }
 
+// nerf_sample_rays with the image, its camera and the draw's (seed, offset) chosen on the device:
+// sel = {image index, seed, offset} (int64, e.g. a captured step's per-replay slots), so one
+// captured launch draws a new batch every replay. Same keys, permutation and ray arithmetic as the
+// host-argument launch (bit-identical for the same image, seed and offset).
+__global__ void __launch_bounds__(256) sample_rays_sel_kernel(const nerf_camera* __restrict__ cams,
+                                                              const float* __restrict__ images, int64_t n_images,
+                                                              int64_t image_elems, int W_img, int r0, int c0, int cw,
+                                                              int64_t n_cells, int64_t n_rays, int half_bits,
+                                                              const int64_t* __restrict__ sel, int channels,
+                                                              float* __restrict__ rays_o, float* __restrict__ rays_d,
+                                                              float* __restrict__ target, int32_t* __restrict__ coords) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n_rays) return;
+    int64_t img = sel[0] % n_images;
+    if (img < 0) img += n_images;
+    uint64_t s = (uint64_t)sel[1] ^ ((uint64_t)sel[2] * 0xD1B54A32D192ED03ull);
+    const uint32_t k0 = splitmix(s), k1 = splitmix(s), k2 = splitmix(s), k3 = splitmix(s);
+    const nerf_camera& cm = cams[img];
+    Cam c;
+#pragma unroll
+    for (int k = 0; k < 12; ++k) c.c2w[k] = cm.c2w[k];
+    c.fx = cm.fx; c.fy = cm.fy; c.cx = cm.cx; c.cy = cm.cy;
+    // one body with the host-argument kernel: a thread of a one-ray grid at ray t
+    const uint32_t key[4] = {k0, k1, k2, k3};
+    uint32_t x = (uint32_t)t;
+    do {
+        x = feistel_perm(x, half_bits, key);
+    } while ((int64_t)x >= n_cells);
+    const int64_t cell = x;
+    const int row = r0 + (int)(cell / cw), col = c0 + (int)(cell % cw);
+    const float i = (float)col, j = (float)row;
+    const float d0 = (i - c.cx) / c.fx;
+    const float d1 = -(j - c.cy) / c.fy;
+    const float d2 = -1.0f;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const float p0 = d0 * c.c2w[4 * a + 0], p1 = d1 * c.c2w[4 * a + 1], p2 = d2 * c.c2w[4 * a + 2];
+        rays_d[3 * t + a] = (p0 + p1) + p2;
+        rays_o[3 * t + a] = c.c2w[4 * a + 3];
+    }
+    if (target) {
+        const float* px = images + img * image_elems + ((int64_t)row * W_img + col) * channels;
+#pragma unroll
+        for (int a = 0; a < 3; ++a) target[3 * t + a] = px[a];
+    }
+    if (coords) {
+        coords[2 * t] = row;
+        coords[2 * t + 1] = col;
+    }
+}
+
 }  // namespace nerf
 
 using namespace nerf;
+
+extern "C" int nerf_sample_rays_sel(const nerf_camera* d_cams, const float* d_images, int64_t n_images, int H, int W,
+                                    int channels, int crop_r0, int crop_c0, int crop_h, int crop_w, int64_t n_rays,
+                                    const int64_t* d_sel, float* d_rays_o, float* d_rays_d, float* d_target,
+                                    int32_t* d_coords, void* stream) {
+    NERF_REQUIRE(d_cams && d_sel && d_rays_o && d_rays_d && n_images > 0, "sample_rays_sel: null argument");
+    NERF_REQUIRE(H > 0 && W > 0 && crop_r0 >= 0 && crop_c0 >= 0 && crop_h > 0 && crop_w > 0 &&
+                 crop_r0 + crop_h <= H && crop_c0 + crop_w <= W, "sample_rays_sel: crop window outside the %dx%d image",
+                 H, W);
+    const int64_t n_cells = (int64_t)crop_h * crop_w;
+    NERF_REQUIRE(n_rays >= 0 && n_rays <= n_cells, "sample_rays_sel: %lld rays from %lld pixels (no replacement)",
+                 (long long)n_rays, (long long)n_cells);
+    NERF_REQUIRE(n_cells <= (int64_t(1) << 30), "sample_rays_sel: crop window too large");
+    NERF_REQUIRE(!d_target || (d_images && channels >= 3), "sample_rays_sel: target needs images with >= 3 channels");
+    if (n_rays == 0) return NERF_OK;
+    int bits = 2;
+    while ((int64_t(1) << bits) < n_cells) bits += 2;
+    hipLaunchKernelGGL(sample_rays_sel_kernel, dim3(blocks_for(n_rays, 256)), dim3(256), 0, as_stream(stream), d_cams,
+                       d_images, n_images, (int64_t)H * W * channels, W, crop_r0, crop_c0, crop_w, n_cells, n_rays,
+                       bits / 2, d_sel, channels, d_rays_o, d_rays_d, d_target, d_coords);
+    NERF_CHECK_LAUNCH("sample_rays_sel");
+    return NERF_OK;
+}
 
 extern "C" int nerf_sample_rays(const nerf_camera* cam, int H, int W, int crop_r0, int crop_c0, int crop_h,
                                 int crop_w, int64_t n_rays, int random, uint64_t seed, uint64_t offset,

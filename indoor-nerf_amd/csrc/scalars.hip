@@ -13,11 +13,21 @@ namespace nerf {
 // load's value was stored before the barrier): the host reuses a slot only after the fetch that read
 // it, with no event between replays. A relaxed store: a release at system scope compiles to a
 // write-back of the whole L2 (the previous step's dirty lines) before it.
+// With `done`, the last 8 bytes of a slot carry the index of the replay the host wrote it for: a slot
+// whose tag is not this fetch's count (the host's and the device's counts have parted, e.g. an
+// upload without its replay) sets the sticky error word behind `done` to count + 1, which the host
+// checks at its next upload — the step would otherwise run on another step's seeds and coefficients.
 __global__ void __launch_bounds__(256) scalars_fetch_kernel(const uint32_t* ring, int64_t slot_words, int n_slots,
                                                            int64_t* ctl, uint32_t* dst, int64_t* done) {
     const int64_t c = ctl[0];
     const int64_t na = ctl[1], b0 = ctl[2], nb = ctl[3];
     const uint32_t* src = ring + (c % n_slots) * slot_words;
+    if (done && threadIdx.x == 0) {
+        const int64_t tag = __hip_atomic_load(reinterpret_cast<const int64_t*>(src + slot_words - 2), __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_SYSTEM);
+        if (tag != c && __hip_atomic_load(done + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0)
+            __hip_atomic_store(done + 1, c + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     for (int64_t i = threadIdx.x; i < na + nb; i += blockDim.x) {
         const int64_t w = i < na ? i : b0 + (i - na);
         // system scope: the host wrote the slot after this ring was last read; no cached copy is used
@@ -55,8 +65,9 @@ extern "C" int nerf_scalars_fetch(const void* host_ring, int64_t slot_bytes, int
     NERF_REQUIRE(host_ring && d_ctl && d_dst && n_slots >= 1 && slot_bytes > 0 && slot_bytes % 4 == 0,
                  "scalars_fetch: ring %p ctl %p dst %p slots %d slot_bytes %lld", host_ring, (void*)d_ctl, d_dst,
                  n_slots, (long long)slot_bytes);
-    NERF_REQUIRE(done_offset < 0 || (done_offset >= n_slots * slot_bytes && done_offset % 8 == 0),
-                 "scalars_fetch: done_offset %lld overlaps the slots or is unaligned", (long long)done_offset);
+    NERF_REQUIRE(done_offset < 0 || (done_offset >= n_slots * slot_bytes && done_offset % 8 == 0 && slot_bytes % 8 == 0),
+                 "scalars_fetch: done_offset %lld overlaps the slots or is unaligned (slot_bytes %lld)",
+                 (long long)done_offset, (long long)slot_bytes);
     void* dev_ring = nullptr;
     const hipError_t e = hipHostGetDevicePointer(&dev_ring, const_cast<void*>(host_ring), 0);
     NERF_REQUIRE(e == hipSuccess, "scalars_fetch: ring is not mapped host memory (%s)", hipGetErrorString(e));

@@ -93,13 +93,19 @@ class GradArena:
             p.grad = v
 
     def zero_(self):
-        if self.deferred:
-            # deferred zero: the tables' by the iteration's owner pass (it stores every row), the dense
-            # rest by render()'s first launch (_lib.defer_fill_zero) or before the backward at the latest
+        if self.deferred and _lib.zero_deferral_active():
+            # inside a training iteration (model.forward_backward): the tables' zero by the iteration's
+            # owner pass (it stores every row), the dense rest by render()'s first launch
+            # (_lib.defer_fill_zero) or before the backward at the latest
             from .hashgrid import defer_zero
             _lib.defer_fill_zero(self.flat[:self.zero_end])
             defer_zero(self.deferred)
         else:
+            # anywhere else the gradients read zero when zero_() returns
+            if self.deferred:
+                from .hashgrid import forget_deferred
+                forget_deferred(self.deferred)
+            _lib.flush_zero_fills([self.flat])
             self.flat.zero_()
         self.attach()
 

@@ -54,6 +54,8 @@ class StepScalars:
         import ctypes
         import numpy as np
         from . import _lib
+        if n_f32 % 2:
+            raise ValueError("StepScalars: n_f32 must be even (the slot's last 8 bytes hold its replay tag)")
         self.n_i64, self.nb = n_i64, 8 * n_i64 + 4 * n_f32
         # [int64 slots | float32 slots] on the device; the ring holds `ring` copies of that layout
         self.dev = torch.zeros(self.nb, dtype=torch.uint8, device=device)
@@ -69,20 +71,30 @@ class StepScalars:
                         buf[k * self.nb + 8 * n_i64:(k + 1) * self.nb].view(np.float32)) for k in range(ring)]
         self.done = buf[self.done_off:self.done_off + 8].view(np.int64)
         self.done[0] = 0
+        # the fetch's sticky error word: replay index + 1 of a fetch whose slot carried another tag
+        self.err = buf[self.done_off + 8:self.done_off + 16].view(np.int64)
+        self.err[0] = 0
+        # the last 8 bytes of each slot: the index of the replay the slot was written for
+        self.tags = [buf[(k + 1) * self.nb - 8:(k + 1) * self.nb].view(np.int64) for k in range(ring)]
         self.issued = 0    # uploads so far = index of the replay the next upload prepares
         self.step = 0      # the global step of the replay being prepared (fillers may read it)
         self.ni = self.nf = 0
         self.fillers = []
 
-    def __del__(self):
+    def close(self):
+        """Free the ring now (outside any capture): after a synchronize no replay still reads it."""
         ring, self._ring = getattr(self, "_ring", None), None
         if ring:
             from . import _lib
-            try:
-                torch.cuda.synchronize(self.dev.device)     # no replay still reads the ring
-                _lib.call("nerf_host_ring_free", ring)
-            except Exception:      # interpreter shutdown: the process's mappings go with it
-                pass
+            torch.cuda.synchronize(self.dev.device)
+            _lib.call("nerf_host_ring_free", ring)
+
+    def __del__(self):
+        # fallback only (GraphedTrainStep closes the ring it replaces)
+        try:
+            self.close()
+        except Exception:      # interpreter shutdown: the process's mappings go with it
+            pass
 
     def alloc_i64(self, n):
         if self.ni + n > self.dev_i.numel():
@@ -91,7 +103,7 @@ class StepScalars:
         return off, self.dev_i.data_ptr() + 8 * off
 
     def alloc_f32(self, n):
-        if self.nf + n > self.dev_f.numel():
+        if self.nf + n > self.dev_f.numel() - 2:     # the last two words: the slot's replay tag
             raise RuntimeError("StepScalars: float32 slots exhausted")
         off, self.nf = self.nf, self.nf + n
         return off, self.dev_f.data_ptr() + 4 * off
@@ -111,10 +123,20 @@ class StepScalars:
         self.ctl.copy_(torch.tensor([0, 2 * self.ni, 2 * self.n_i64, self.nf], dtype=torch.int64))
         torch.cuda.synchronize(self.dev.device)
         self.done[0] = 0
+        self.err[0] = 0
         self.issued = 0
+
+    def check(self):
+        """Raise if a replay fetched a slot written for another replay (the fetch kernel's tag check)."""
+        e = int(self.err[0])
+        if e:
+            raise RuntimeError(f"StepScalars: replay {e - 1} fetched a ring slot written for another replay: the "
+                               "uploads and the replays of the captured step have parted (each upload() must be "
+                               "followed by exactly one replay); re-seal() before replaying again")
 
     def upload(self):
         """Run every filler into the ring slot the next replay fetches (call once before each replay)."""
+        self.check()
         n, R = self.issued, len(self.pinned)
         if int(self.done[0]) < n - R + 1:        # replay n - R has not fetched this slot yet
             deadline = time.monotonic() + 60.0
@@ -126,6 +148,7 @@ class StepScalars:
         hi, hf = self.pinned[n % R]
         for fn in self.fillers:
             fn(hi, hf)
+        self.tags[n % R][0] = n
         self.issued = n + 1
 
 
@@ -138,8 +161,11 @@ class GraphedTrainStep:
 
     def __init__(self, batch_rays, target_s, render_kwargs_train, optimizer, args, H=0, W=0, K=None,
                  grad_hook=None, loss_scale_sparsity=1.0, tv_generator=None, zero_grad=None, warmup=2,
-                 post_hook=None):
+                 post_hook=None, sampler=None):
         self.rays, self.target = batch_rays, target_s
+        # sampler (rays.RaySampler): every iteration draws a new batch into batch_rays / target_s first
+        # (train()'s no_batching path, run_nerf.py:975-1004), inside the captured step
+        self.sampler = sampler
         self.kw, self.opt, self.args = render_kwargs_train, optimizer, args
         self.H, self.W, self.K = H, W, K
         if zero_grad is None:
@@ -174,7 +200,8 @@ class GraphedTrainStep:
             priors = (get("depth_prior_weight"), get("planarity_weight"), get("manhattan_weight"),
                       get("normal_consistency_weight"), get("structural_loss_start_iter"),
                       get("structural_loss_ramp_iters"))
-        return (tv_w > 0, quant, priors)
+        crop = self.sampler.crop_key(global_step) if self.sampler is not None else None
+        return (tv_w > 0, quant, priors, crop)
 
     def _capture(self, global_step):
         from . import _lib, hashgrid
@@ -201,6 +228,8 @@ class GraphedTrainStep:
             with capturing(sc):
                 with torch.cuda.graph(g1, pool=pool, stream=side):
                     sc.capture_fetch()
+                    if self.sampler is not None:
+                        self.sampler.fill(global_step, self.rays[0], self.rays[1], self.target)
                     out = forward_backward(self.rays, self.target, self.kw, self.opt, self.args, global_step,
                                            H=self.H, W=self.W, K=self.K, loss_scale_sparsity=self.scale_sp,
                                            tv_generator=self.tv_gen, zero_grad=self.zero_grad, schedule=False)
@@ -212,9 +241,12 @@ class GraphedTrainStep:
         torch.cuda.current_stream(dev).wait_stream(side)
         sc.seal()
         emb.current_step = step0
+        old = getattr(self, "scalars", None)
         self.graphs = (g1, g2)
         self.out = out
         self.scalars = sc
+        if old is not None:
+            old.close()     # the replaced graph's ring (its graph is gone: no replay can read it)
         self.params = [p for g in self.opt.param_groups for p in g["params"] if p.grad is not None]
         self.captures += 1
 
@@ -222,6 +254,8 @@ class GraphedTrainStep:
         """The same iteration launched eagerly (same arguments, host state and gradient arena),
         e.g. to time its kernels with HIP events, which cannot be captured."""
         from .model import train_step
+        if self.sampler is not None:
+            self.sampler.fill(global_step, self.rays[0], self.rays[1], self.target)
         return train_step(self.rays, self.target, self.kw, self.opt, self.args, global_step, H=self.H, W=self.W,
                           K=self.K, grad_hook=self.hook, loss_scale_sparsity=self.scale_sp,
                           tv_generator=self.tv_gen, zero_grad=self.zero_grad, post_hook=self.post_hook)
@@ -249,8 +283,14 @@ class GraphedTrainStep:
         if self.graphs is None:
             self._capture(global_step)
         self.scalars.step = global_step
-        self.scalars.upload()
-        self.graphs[0].replay()
+        try:
+            self.scalars.upload()
+            self.graphs[0].replay()
+        except BaseException:
+            # an upload without its replay (or the reverse) would pair every later replay with another
+            # step's slot: re-synchronise the host's and the device's replay counts
+            self.scalars.seal()
+            raise
         emb = self.kw["embed_fn"]
         if emb.training:
             emb.current_step += self._n_forwards()

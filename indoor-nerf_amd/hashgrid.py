@@ -50,6 +50,12 @@ def materialize_zero(grads=None):
         _DEFERRED.pop(k).zero_()
 
 
+def forget_deferred(grads):
+    """Drop pending deferred zeros of these gradients (their owner zeroed them itself)."""
+    for g in grads:
+        _DEFERRED.pop(g.data_ptr(), None)
+
+
 def take_deferred(grads):
     """True (and no longer deferred) when every gradient of an owner launch is deferred: the launch
     overwrites them. Otherwise any deferred ones among them are zeroed now and the launch adds."""

@@ -176,6 +176,13 @@ def forward_backward(batch_rays, target_s, render_kwargs_train, optimizer, args,
                      loss_scale_sparsity=1.0, tv_generator=None, zero_grad=None, schedule=True, spatial_coords=None):
     """render (coarse+fine), zero grads, img/img0 MSE + sparsity + TV (run_nerf.py:1007-1037),
     backward. Returns (loss, img_loss, psnr) device tensors (no host sync)."""
+    with _lib.zero_deferral():
+        return _forward_backward(batch_rays, target_s, render_kwargs_train, optimizer, args, global_step, H, W, K,
+                                 loss_scale_sparsity, tv_generator, zero_grad, schedule, spatial_coords)
+
+
+def _forward_backward(batch_rays, target_s, render_kwargs_train, optimizer, args, global_step, H, W, K,
+                      loss_scale_sparsity, tv_generator, zero_grad, schedule, spatial_coords):
     get = lambda k: getattr(args, k, DEFAULTS.get(k))  # noqa: E731
     # the gradient zero and the TV loss accumulator first: a GradArena(defer_tables=True) zero and the
     # accumulator's fill are then stores in render()'s first launch (_lib.defer_fill_zero), not fills.
@@ -250,10 +257,12 @@ def structural_loss(depth, extras, args, global_step, spatial_coords=None):
     if normals is not None and fused_priors_eligible(args, depth.shape[0]):
         sc = graphs.active()
         if sc is not None:   # captured: the ramp of the replayed step, written before every replay
+            import weakref
             off, ptr = sc.alloc_f32(1)
+            sc_ref = weakref.ref(sc)   # no StepScalars <-> filler cycle: the ring is freed with its graph
 
             def fill(hi, hf, off=off):
-                hf[off] = ramp_of(sc.step)
+                hf[off] = ramp_of(sc_ref().step)
             sc.add_filler(fill)
             scale = sc.dev_f[off:off + 1]
         else:

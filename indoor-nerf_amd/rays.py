@@ -41,6 +41,7 @@ class RaySampler:
         self.precrop_iters, self.precrop_frac = precrop_iters, precrop_frac
         self.device = device
         self._cams = {}
+        self._d_cams = None
 
     def _camera(self, img_i):
         if img_i not in self._cams:
@@ -63,3 +64,54 @@ class RaySampler:
                   _lib.ptr(target, "target"), _lib.ptr(coords, "coords", dtype=torch.int32, allow_none=True),
                   _lib.stream())
         return (rays, target, coords) if return_coords else (rays, target)
+
+    def crop_key(self, i):
+        """The launch structure of iteration i's draw (the precrop window is on or off): part of a
+        captured step's re-capture key (graphs.GraphedTrainStep)."""
+        return crop_window(self.H, self.W, i, self.precrop_iters, self.precrop_frac)
+
+    def _device_cams(self):
+        """Every image's nerf_camera, resident on the device (nerf_sample_rays_sel picks one)."""
+        if self._d_cams is None:
+            n = self.images.shape[0]
+            arr = (_lib.Camera * n)(*[self._camera(k) for k in range(n)])
+            raw = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
+            self._d_cams = raw.to(self.device)
+        return self._d_cams
+
+    def fill(self, i, rays_o, rays_d, target):
+        """Iteration i's batch into the caller's buffers (rays_o, rays_d [N_rand, 3], target
+        [N_rand, 3]): the image with np.random.choice(i_train) and the pixels from a fresh seed, as
+        sample() draws them. While a training step is captured (graphs.GraphedTrainStep(sampler=...))
+        the (image, seed, offset) triple is a per-replay slot (graphs.StepScalars) that the captured
+        nerf_sample_rays_sel launch reads, so every replay trains on a new batch (run_nerf.py:975-1004);
+        the draws happen in the same order as eagerly, so the replayed batches equal the eager ones."""
+        import weakref
+        from . import graphs
+        r0, c0, h, w = crop_window(self.H, self.W, i, self.precrop_iters, self.precrop_frac)
+        n = self.N_rand
+        for t, name in ((rays_o, "rays_o"), (rays_d, "rays_d"), (target, "target")):
+            if tuple(t.shape) != (n, 3):
+                raise ValueError(f"RaySampler.fill: {name} must be [{n}, 3], got {tuple(t.shape)}")
+        sc = graphs.active()
+        C = int(self.images.shape[-1])
+        if sc is None:
+            img_i = int(np.random.choice(self.i_train))
+            s0, s1 = _draw_seed()
+            img = self.images[img_i]
+            _lib.call("nerf_sample_rays", self._camera(img_i), self.H, self.W, r0, c0, h, w, n, 1, s0, s1 + int(i),
+                      _lib.ptr(img, "image"), C, _lib.ptr(rays_o, "rays_o"), _lib.ptr(rays_d, "rays_d"),
+                      _lib.ptr(target, "target"), None, _lib.stream())
+            return
+        off, ptr = sc.alloc_i64(3)
+        sc_ref = weakref.ref(sc)
+
+        def fill(hi, hf, off=off):
+            img_i = int(np.random.choice(self.i_train))
+            s0, s1 = _draw_seed()
+            hi[off], hi[off + 1], hi[off + 2] = img_i, s0, s1 + int(sc_ref().step)
+        sc.add_filler(fill)
+        _lib.call("nerf_sample_rays_sel", _lib.ptr(self._device_cams(), "cams", dtype=torch.uint8),
+                  _lib.ptr(self.images, "images"), int(self.images.shape[0]), self.H, self.W, C, r0, c0, h, w, n,
+                  _lib.c_vp(ptr), _lib.ptr(rays_o, "rays_o"), _lib.ptr(rays_d, "rays_d"), _lib.ptr(target, "target"),
+                  None, _lib.stream())

@@ -532,7 +532,7 @@ def _pack_rays(H, W, K, rays_o, rays_d, near, far, ndc, use_viewdirs):
         # -1./(W/(2.*focal)) is a python double in the reference; torch rounds it to float32
         cw = float(np.float32(-1. / (W / (2. * float(focal)))))
         ch = float(np.float32(-1. / (H / (2. * float(focal)))))
-    zeros, nz, keep = _lib.take_zero_fills()     # a training step's zero fills ride along (_lib.defer_fill_zero)
+    zeros, nz, keep = _lib.take_zero_fills(d.device)   # a training step's zero fills ride along (_lib.defer_fill_zero)
     _lib.call("nerf_rays_pack_z", _lib.ptr(o, "rays_o"), _lib.ptr(d, "rays_d"), n, float(near), float(far),
               int(bool(ndc)), cw, ch, int(bool(use_viewdirs)), _lib.ptr(out, "rays"), zeros, nz, _lib.stream())
     del keep

@@ -252,10 +252,9 @@ def test_deferred_table_zero_bitwise(nerf, gpu):
         arena = GradArena(params, defer_tables=defer)
         arena.flat.fill_(7.0)             # stale gradients everywhere
         assert (len(arena.deferred) == 16) == defer
-        arena.zero_()
-        for _ in range(passes):
+        for k in range(passes):           # the zero inside the first iteration's scope (_lib.zero_deferral)
             model.forward_backward(rays, target, kw, opt, args, 1, tv_generator=torch.Generator().manual_seed(5),
-                                   zero_grad=lambda: None)
+                                   zero_grad=arena.zero_ if k == 0 else (lambda: None))
         torch.cuda.synchronize()
         return [p.grad.clone() for p in params]
 
@@ -289,18 +288,48 @@ def test_deferred_table_zero_other_writers(nerf, gpu):
     ref_arena.zero_()
     (emb(x)[0] * w).sum().backward()
     ref = [p.grad.clone() for p in params]
+    from indoor_nerf_amd import _lib
     arena = GradArena(params, defer_tables=True)
     assert len(arena.deferred) == 16
     arena.flat.fill_(7.0)
-    arena.zero_()
+    with _lib.zero_deferral():          # as inside a training iteration
+        arena.zero_()
+    assert len(hashgrid._DEFERRED) == 16
     (emb(x)[0] * w).sum().backward()
     torch.cuda.synchronize()
     for a, b in zip(ref, params):
         torch.testing.assert_close(b.grad, a, rtol=1e-5, atol=1e-7)
     assert not hashgrid._DEFERRED
     arena.flat.fill_(7.0)
-    arena.zero_()                       # no backward reaches the tables this time
+    with _lib.zero_deferral():
+        arena.zero_()                   # no backward reaches the tables this time
     hashgrid.materialize_zero()
+    assert all(not bool(p.grad.any()) for p in params)
+
+
+def test_arena_zero_outside_a_step_is_immediate(nerf, gpu):
+    """GradArena(defer_tables=True).zero_() called by user code (outside model.forward_backward's
+    zero_deferral scope) leaves no fill pending: the gradients read zero as soon as it returns, and no
+    later launch on any device takes their ranges."""
+    from indoor_nerf_amd import _lib, hashgrid
+    from indoor_nerf_amd.dist import GradArena
+    lo, hi = blender_bbox()
+    emb = nerf.HashEmbedder((torch.from_numpy(lo), torch.from_numpy(hi)), finest_resolution=1024).to(gpu)
+    net = nerf.NeRFSmall(2, 64, 15, 3, 64, 32, 16).to(gpu)
+    params = list(net.parameters()) + list(emb.parameters())
+    arena = GradArena(params, defer_tables=True)
+    assert len(arena.deferred) == 16 and arena.zero_end > 0
+    arena.flat.fill_(7.0)
+    arena.zero_()
+    assert not any(_lib._ZERO_FILLS.values()) and not hashgrid._DEFERRED
+    assert all(not bool(p.grad.any()) for p in params)
+    # inside a step's scope the same call defers: the dense part waits for render()'s first launch
+    arena.flat.fill_(7.0)
+    with _lib.zero_deferral():
+        arena.zero_()
+    assert sum(len(v) for v in _lib._ZERO_FILLS.values()) == 1 and len(hashgrid._DEFERRED) == 16
+    hashgrid.materialize_zero()
+    assert not any(_lib._ZERO_FILLS.values()) and not hashgrid._DEFERRED
     assert all(not bool(p.grad.any()) for p in params)
 
 

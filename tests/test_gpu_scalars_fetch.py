@@ -23,9 +23,12 @@ def test_fetch_cycles_the_ring(gpu):
         done[0] = 0
         dst = torch.full((slot_bytes // 4,), 0xDEAD, dtype=torch.int32, device=gpu)
         ctl = torch.tensor([0, 5, 40, 3], dtype=torch.int64, device=gpu)   # words [0,5) and [40,43)
+        err = buf[done_off + 8:done_off + 16].view(np.int64)
+        err[0] = 0
         for n in range(7):
             k = n % n_slots
             words[k] = np.arange(slot_bytes // 4, dtype=np.uint32) + 1000 * (n + 1)
+            words[k][-2:].view(np.int64)[0] = n         # the slot's replay tag
             _lib.call("nerf_scalars_fetch", h.value, slot_bytes, n_slots, done_off, _lib.ptr(ctl, "ctl", torch.int64),
                       dst.data_ptr(), _lib.stream())
             torch.cuda.synchronize()
@@ -36,8 +39,50 @@ def test_fetch_cycles_the_ring(gpu):
             np.testing.assert_array_equal(got, want)
             assert int(ctl[0]) == n + 1 and int(done[0]) == n + 1
             assert int(ctl[1]) == 5 and int(ctl[2]) == 40 and int(ctl[3]) == 3
+            assert int(err[0]) == 0
+        # a slot written for another replay: flagged (sticky, the first mismatch's count + 1), copied anyway
+        for n in (7, 8):
+            k = n % n_slots
+            words[k][-2:].view(np.int64)[0] = n + 3
+            _lib.call("nerf_scalars_fetch", h.value, slot_bytes, n_slots, done_off, _lib.ptr(ctl, "ctl", torch.int64),
+                      dst.data_ptr(), _lib.stream())
+            torch.cuda.synchronize()
+            assert int(err[0]) == 8 and int(done[0]) == n + 1
         with pytest.raises(RuntimeError):    # done word inside the slots
             _lib.call("nerf_scalars_fetch", h.value, slot_bytes, n_slots, 8, _lib.ptr(ctl, "ctl", torch.int64),
                       dst.data_ptr(), _lib.stream())
     finally:
         _lib.call("nerf_host_ring_free", h.value)
+
+
+def test_step_scalars_detects_parted_counts(gpu):
+    """graphs.StepScalars: an upload() without its replay parts the host's slot index from the device
+    count; the next replay's fetch flags it and the following upload() raises instead of training on
+    another step's scalars. seal() re-synchronises."""
+    from indoor_nerf_amd import _lib
+    from indoor_nerf_amd.graphs import StepScalars
+    sc = StepScalars(gpu, n_i64=8, n_f32=8, ring=2)
+    off, dptr = sc.alloc_i64(1)
+    sc.add_filler(lambda hi, hf: hi.__setitem__(off, 100 + sc.issued))
+    g = torch.cuda.CUDAGraph()
+    side = torch.cuda.Stream(device=gpu)
+    with torch.cuda.stream(side), torch.cuda.graph(g, stream=side):
+        sc.capture_fetch()
+    torch.cuda.current_stream(gpu).wait_stream(side)
+    sc.seal()
+    for n in range(3):
+        sc.upload()
+        g.replay()
+        torch.cuda.synchronize()
+        assert int(sc.dev_i[off]) == 100 + n
+    sc.upload()            # ... and no replay: the counts part
+    sc.upload()
+    g.replay()             # fetches slot 3 % 2, written for replay 4
+    torch.cuda.synchronize()
+    with pytest.raises(RuntimeError, match="parted"):
+        sc.upload()
+    sc.seal()
+    sc.upload()
+    g.replay()
+    torch.cuda.synchronize()
+    assert int(sc.dev_i[off]) == 100 and int(sc.err[0]) == 0

@@ -11,6 +11,7 @@ import argparse
 import glob
 import json
 import os
+import sys
 
 import numpy as np
 
@@ -100,6 +101,9 @@ def main():
                          f"(iterations {LATE}-300) mean PSNR difference averaged over seeds")
         if a.commit:
             out["commit"] = a.commit
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        from bench import product_tree_sha
+        out["tree_sha"] = product_tree_sha()    # bench.py marks the result stale once the tree moves on
         json.dump(out, open(a.json, "w"), indent=1)
 
 

@@ -4,6 +4,7 @@
 checksum of every output (dfeat of both nets, the ten weight gradients) so that builds can be told to
 compute the same thing. A/B of library builds: run once per build with NERF_HIP_LIB=<path>
 (tools/build_variant.py). JSON out."""
+import ctypes
 import json
 import os
 import sys
@@ -62,21 +63,38 @@ def main():
     torch.cuda.synchronize()
     check = {"dfeat_f": float(kf["dfeat"].double().abs().sum()), "dfeat_c": float(kc["dfeat"].double().abs().sum()),
              "grads": [float(t.double().sum()) for k in (kf, kc) for t in k["grads"]]}
-    ts = []
-    for rnd in range(5):
-        for _ in range(3):
-            run()
-        torch.cuda.synchronize()
-        for _ in range(20):
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            run()
-            e1.record()
+    def timed(fn):
+        ts = []
+        for rnd in range(5):
+            for _ in range(3):
+                fn()
             torch.cuda.synchronize()
-            ts.append(e0.elapsed_time(e1))
-    print(json.dumps({"lib": os.environ.get("NERF_HIP_LIB", "default"), "us_median": round(float(np.median(ts)) * 1e3, 1),
-                      "us_min": round(float(np.min(ts)) * 1e3, 1), "det": det, "check": check}))
+            for _ in range(20):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                fn()
+                e1.record()
+                torch.cuda.synchronize()
+                ts.append(e0.elapsed_time(e1))
+        return ts
 
+    # forward of the fine net (the lego step's larger MLP forward launch)
+    raw = torch.empty(kf["feat"].shape[1], 4, device=dev)
+    w = jf.weights
+
+    def fwd():
+        _lib.call("nerf_mlp_fwd", _lib.ptr(kf["feat"]), 2, 2 * raw.shape[0], None, 0, _lib.ptr(kf["vd"]), 192,
+                  _lib.ptr(kf["keep"], dtype=torch.bool), raw.shape[0], ctypes.byref(w), _lib.ptr(raw), None,
+                  _lib.stream())
+
+    fwd()
+    torch.cuda.synchronize()
+    check["raw"] = float(raw.double().abs().sum())
+    ts = timed(run)
+    tf = timed(fwd)
+    print(json.dumps({"lib": os.environ.get("NERF_HIP_LIB", "default"), "us_median": round(float(np.median(ts)) * 1e3, 1),
+                      "us_min": round(float(np.min(ts)) * 1e3, 1), "fwd_us_median": round(float(np.median(tf)) * 1e3, 1),
+                      "fwd_us_min": round(float(np.min(tf)) * 1e3, 1), "det": det, "check": check}))
 
 if __name__ == "__main__":
     main()
