@@ -111,6 +111,24 @@ __device__ __forceinline__ float dpp_move(float v) {
 // of the classic DPP scan, each applied only where the source lane lies in the same run. STEPS: the
 // intra-row distances 1 .. 2^(STEPS-1) are applied (enough when every run is shorter than 2^STEPS
 // lanes); CROSS: the carries across rows.
+// Step-major: each step runs over all N values before the next, so a DPP read never follows the
+// VALU write of its source register within the 2-wait-state hazard window (value-major order put
+// an s_nop in front of nearly every DPP step).
+template <int N, int CTRL, int ROW_MASK>
+__device__ __forceinline__ void seg_scan_step(float (&v)[N], bool take) {
+    float t[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        if constexpr (ROW_MASK == 0xF) {
+            t[i] = v[i] + dpp_move<CTRL, ROW_MASK>(v[i]);
+        } else {   // masked-out rows never take the step: their lanes' t may be anything (mov_dpp: old undef)
+            t[i] = v[i] + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v[i]), CTRL, ROW_MASK, 0xF, false));
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] = take ? t[i] : v[i];   // a select, not a branch
+}
+
 template <int N, int STEPS, bool CROSS>
 __device__ __forceinline__ void wave_segmented_scan_steps(float (&v)[N], int lane, int start) {
     const int r16 = lane & 15, row = lane >> 4, span = lane - start;
@@ -120,18 +138,13 @@ __device__ __forceinline__ void wave_segmented_scan_steps(float (&v)[N], int lan
     const bool t8 = r16 >= 8 && span >= 8;
     const bool tb15 = (row & 1) && start <= 16 * row - 1;
     const bool tb31 = row >= 2 && start <= 31;
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-        float x = v[i], t;
-        t = dpp_move<0x111, 0xF>(x); if (t1) x += t;
-        if constexpr (STEPS >= 2) { t = dpp_move<0x112, 0xF>(x); if (t2) x += t; }
-        if constexpr (STEPS >= 3) { t = dpp_move<0x114, 0xF>(x); if (t4) x += t; }
-        if constexpr (STEPS >= 4) { t = dpp_move<0x118, 0xF>(x); if (t8) x += t; }
-        if constexpr (CROSS) {
-            t = dpp_move<0x142, 0xA>(x); if (tb15) x += t;
-            t = dpp_move<0x143, 0xC>(x); if (tb31) x += t;
-        }
-        v[i] = x;
+    seg_scan_step<N, 0x111, 0xF>(v, t1);
+    if constexpr (STEPS >= 2) seg_scan_step<N, 0x112, 0xF>(v, t2);
+    if constexpr (STEPS >= 3) seg_scan_step<N, 0x114, 0xF>(v, t4);
+    if constexpr (STEPS >= 4) seg_scan_step<N, 0x118, 0xF>(v, t8);
+    if constexpr (CROSS) {
+        seg_scan_step<N, 0x142, 0xA>(v, tb15);
+        seg_scan_step<N, 0x143, 0xC>(v, tb31);
     }
 }
 

@@ -256,12 +256,14 @@ __device__ __forceinline__ void load_x6(const MlpArgs& a, uint32_t pt, bool vali
 #pragma unroll
             for (int e = 0; e < 2; ++e) {
                 const int level = 8 * c + 4 * q + 2 * h + e;   // features 2 level, 2 level + 1
-                // branch-free: a tail lane loads the last point and zeroes it (no basic-block split,
-                // so the scheduler keeps one region for the whole tile)
+                // branch-free: a tail lane computes on the last point's features. Its column of every
+                // tile is its own (Y = W X mixes no columns), the forward stores nothing for it, and in
+                // the backward its upstream gradient is zero, so every weight-gradient term it forms is
+                // 0 x (finite) — no zeroing of the inputs (28 selects per tile) is needed
                 const uint32_t pc = valid ? pt : (uint32_t)(a.P - 1);
                 const float2 v = *reinterpret_cast<const float2*>(a.feat + (uint32_t)(pc * (uint32_t)a.sp + level * (uint32_t)a.sl + zero));
-                x[8 * c + 4 * q + 2 * e] = valid ? v.x : 0.f;
-                x[8 * c + 4 * q + 2 * e + 1] = valid ? v.y : 0.f;
+                x[8 * c + 4 * q + 2 * e] = v.x;
+                x[8 * c + 4 * q + 2 * e + 1] = v.y;
             }
 }
 
@@ -274,8 +276,8 @@ __device__ __forceinline__ void load_sh6(const MlpArgs& a, uint32_t pt, bool val
         const uint32_t ray = ray_of(a, pc) * (uint32_t)kShRecord + zero;
         const float4 u = *reinterpret_cast<const float4*>(a.sh + ray + 4 * h);
         const float4 v = *reinterpret_cast<const float4*>(a.sh + ray + 8 + 4 * h);
-        shv[0] = valid ? u.x : 0.f; shv[1] = valid ? u.y : 0.f; shv[2] = valid ? u.z : 0.f; shv[3] = valid ? u.w : 0.f;
-        shv[4] = valid ? v.x : 0.f; shv[5] = valid ? v.y : 0.f; shv[6] = valid ? v.z : 0.f; shv[7] = valid ? v.w : 0.f;
+        shv[0] = u.x; shv[1] = u.y; shv[2] = u.z; shv[3] = u.w;   // tail lanes: the last point's (load_x6)
+        shv[4] = v.x; shv[5] = v.y; shv[6] = v.z; shv[7] = v.w;
         return;
     }
     if (a.viewdirs) {
@@ -286,8 +288,6 @@ __device__ __forceinline__ void load_sh6(const MlpArgs& a, uint32_t pt, bool val
 #pragma unroll
         for (int k = 0; k < 16; ++k) o[k] = a.sh[(uint32_t)(pc * (uint32_t)a.sh_stride + k + zero)];
     }
-#pragma unroll
-    for (int k = 0; k < 16; ++k) o[k] = valid ? o[k] : 0.f;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {   // static indices + one select (a dynamic o[4h + k] is a 16-way select chain)
         const int k = (i & 3) + 8 * (i >> 2);
@@ -306,7 +306,7 @@ __device__ __forceinline__ S3 load_sh_split(const MlpArgs& a, uint32_t pt, bool 
         for (int q = 0; q < 3; ++q) {
             const u32x2 g0 = *reinterpret_cast<const u32x2*>(rec + 16 * q + 4 * h);
             const u32x2 g1 = *reinterpret_cast<const u32x2*>(rec + 16 * q + 8 + 4 * h);
-            s.p[q] = valid ? u32x4{g0.x, g0.y, g1.x, g1.y} : u32x4{0u, 0u, 0u, 0u};
+            s.p[q] = u32x4{g0.x, g0.y, g1.x, g1.y};   // tail lanes: the last point's (load_x6)
         }
         return s;
     }
@@ -784,9 +784,9 @@ __device__ __forceinline__ void bwd_chain_role(const MlpArgs& a, const __bf16* i
             for (int r = 8; r < 16; ++r) a.dsh[16u * orow + row_of(r, h) - 16] = go[r];
         }
 
-        // stage 6 (dW1): go, h1 (recomputed from a reload of x: the kernel keeps no state between
-        // stages outside its registers and LDS) and layer 0's ReLU mask m1 (with QUANT: before the
-        // activation quantizer) in the unused columns 16.. of the gradient tile.
+        // stage 6 (dW1): go, h1 (held in registers since the forward recompute; with QUANT recomputed
+        // from a reload of x) and layer 0's ReLU mask m1 (with QUANT: before the activation quantizer)
+        // in the unused columns 16.. of the gradient tile.
         // The wgrad wave forms ga1 = mask(W1^T go) itself (it waits on the chain wave otherwise).
         // x's bf16 pieces are kept for stage 7 (staged split: the wgrad wave does not split x).
         S3 xb[2];
@@ -799,7 +799,13 @@ __device__ __forceinline__ void bwd_chain_role(const MlpArgs& a, const __bf16* i
         {
             floatx16 h1[2];
             uint32_t m1;
-            layer0_split<QUANT>(imt, xb, h1, m1, lane, aq);
+            if constexpr (QUANT) {
+                layer0_split<QUANT>(imt, xb, h1, m1, lane, aq);   // kept live, the quantizer state spills
+            } else {
+                h1[0] = f.h1[0];   // layer 0's output of the forward recompute, live since (24 MFMAs and
+                h1[1] = f.h1[1];   // the ReLUs fewer than recomputing it here; no spills without QUANT)
+                m1 = 0;
+            }
             const S3 GO = split_chunk(go, 0);
             open(true, 6);
 #pragma unroll

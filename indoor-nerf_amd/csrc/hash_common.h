@@ -24,6 +24,7 @@ __device__ __forceinline__ void radam_elem(const nerf_radam_segment& s, float& p
 struct HashParams {
     const float* tables[NERF_MAX_LEVELS];
     float cell[NERF_MAX_LEVELS][3];   // grid_size = (box_max - box_min) / res, fp32 on the host
+    float rcell[NERF_MAX_LEVELS][3];  // RN(1 / grid_size) (fill_cells): div_rn<true>'s reciprocal of the cell
     float bmin[3];
     float bmax[3];
     uint32_t mask;
@@ -50,6 +51,17 @@ __device__ __forceinline__ float div_rn(float n, float d) {
     }
 }
 
+// div_rn<true> with the reciprocal given: r = RN(1 / d), computed once per launch on the host for a
+// uniform divisor (the cell size of a level and axis). Quotient then two residual corrections: with
+// r correctly rounded and no operand or residual leaving the normal range (the FAST conditions), the
+// last correction returns RN(n / d) (Markstein's correction theorem); the refined hardware
+// reciprocal this replaces (v_rcp_f32 + two FMAs per axis) is no closer to 1 / d than r.
+__device__ __forceinline__ float div_rn_recip(float n, float d, float r) {
+    float q = n * r;
+    q = fmaf(fmaf(-d, q, n), r, q);
+    return fmaf(fmaf(-d, q, n), r, q);
+}
+
 // A point admits the fast division when every |coordinate| is in [2^-72, 2^40] (NaN/Inf fail):
 // then x - vmin and clamp(x) - lo are 0 or >= 2^-95 in magnitude (vmin = base * cell + lo is 0
 // or >= 2^-63 given fill_cells' bounds on lo and cell) and both quotients stay normal.
@@ -66,23 +78,45 @@ struct AxisCell {
     bool inside;   // x == max(min(x, bmax), bmin)
 };
 
+// FAST (finite coordinates, fastdiv_point_ok): the clamp as one v_med3_f32 (the median of x, lo, hi
+// IS clamp(x, lo, hi) for lo <= hi; a zero's sign it may pick differently cannot move the floor) and
+// the cell division with the host's reciprocal rcell.
 template <bool FAST = false>
-__device__ __forceinline__ AxisCell axis_cell(float x, float lo, float hi, float cell) {
+__device__ __forceinline__ AxisCell axis_cell(float x, float lo, float hi, float cell, float rcell = 0.f) {
     AxisCell a;
     a.inside = (x == fmaxf(fminf(x, hi), lo));
-    float xc = fminf(fmaxf(x, lo), hi);                   // torch.clamp(min=lo, max=hi)
-    a.base = (int)floorf(div_rn<FAST>(xc - lo, cell));    // floor(...).int()
+    if constexpr (FAST) {
+        const float xc = __builtin_amdgcn_fmed3f(x, lo, hi);
+        a.base = (int)floorf(div_rn_recip(xc - lo, cell, rcell));
+    } else {
+        float xc = fminf(fmaxf(x, lo), hi);                   // torch.clamp(min=lo, max=hi)
+        a.base = (int)floorf(div_rn<false>(xc - lo, cell));   // floor(...).int()
+    }
     float vmin = (float)a.base * cell + lo;               // bottom_left_idx*grid_size + box_min
     float vmax = vmin + cell;                             // + 1.0*grid_size
     a.w = div_rn<FAST>(x - vmin, vmax - vmin);
     return a;
 }
 
+// RN(1 / c) for a positive normal float c: the double quotient rounded to float, then the float
+// neighbour whose error is smaller, if any (the error 1 - c r is exact in double: c r has <= 48
+// significant bits), so a double rounding of 1 / c cannot leave it off by one.
+static float recip_rn(float c) {
+    float r = (float)(1.0 / (double)c);
+    auto err = [c](float q) { const double e = 1.0 - (double)c * (double)q; return e < 0 ? -e : e; };
+    for (const float q : {nextafterf(r, 0.f), nextafterf(r, 1e30f)}) {
+        const double eq = err(q), er = err(r);
+        if (eq < er || (eq == er && (__builtin_bit_cast(uint32_t, q) & 1u) == 0u)) r = q;
+    }
+    return r;
+}
+
 // grid_size = (box_max - box_min) / resolution (utils.py:106): the same two fp32 operations,
 // correctly rounded, on the host once per launch instead of per point. Returns whether the box and
 // the cells admit div_rn<true>: |box bounds| 0 or in [2^-40, 2^40], cells in [2^-40, 2^40] and at
 // least 2^-16 of the largest |bound| (so vmax - vmin stays within 2^-7 of the cell).
-static bool fill_cells(float (*cell)[3], const float* bmin, const float* bmax, const float* res, int n_levels) {
+static bool fill_cells(float (*cell)[3], float (*rcell)[3], const float* bmin, const float* bmax, const float* res,
+                       int n_levels) {
     bool ok = true;
     float big = 0.f;
     for (int a = 0; a < 3; ++a)
@@ -96,6 +130,7 @@ static bool fill_cells(float (*cell)[3], const float* bmin, const float* bmax, c
             const volatile float d = bmax[a] - bmin[a];
             cell[l][a] = d / res[l];
             const float c = cell[l][a];
+            rcell[l][a] = recip_rn(c);
             ok = ok && c >= 0x1p-40f && c <= 0x1p40f && c >= big * 0x1p-16f;
         }
     return ok;
@@ -161,9 +196,10 @@ __device__ __forceinline__ float pair_swap(float v) { return __int_as_float(pair
 template <bool FAST>
 __device__ __forceinline__ void fwd_axes(float x, float y, float z, const HashParams& hp, int lvl, int xb,
                                          AxisCell& ax, AxisCell& ay, AxisCell& az) {
-    ax = axis_cell<FAST>(x, hp.bmin[0], hp.bmax[0], hp.cell[lvl][0]);
+    ax = axis_cell<FAST>(x, hp.bmin[0], hp.bmax[0], hp.cell[lvl][0], hp.rcell[lvl][0]);
     const AxisCell a2 = axis_cell<FAST>(xb ? z : y, xb ? hp.bmin[2] : hp.bmin[1], xb ? hp.bmax[2] : hp.bmax[1],
-                                        xb ? hp.cell[lvl][2] : hp.cell[lvl][1]);
+                                        xb ? hp.cell[lvl][2] : hp.cell[lvl][1],
+                                        xb ? hp.rcell[lvl][2] : hp.rcell[lvl][1]);
     const int pk = a2.base | (a2.inside ? 0x40000000 : 0);   // 0 <= base <= res < 2^30
     const int opk = pair_swap_i(pk);
     const float ow = pair_swap(a2.w);

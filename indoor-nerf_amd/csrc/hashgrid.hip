@@ -24,6 +24,7 @@ namespace nerf {
 struct HashGradParams {
     float* dtables[NERF_MAX_LEVELS];
     float cell[NERF_MAX_LEVELS][3];
+    float rcell[NERF_MAX_LEVELS][3];   // RN(1 / cell): div_rn_recip (hash_common.h)
     float bmin[3];
     float bmax[3];
     uint32_t mask;
@@ -314,9 +315,9 @@ __device__ __forceinline__ void bwd_bin_block(const float* __restrict__ xyz, int
     }
     AxisCell ax, ay, az;
     if (hp.fastdiv && __ballot(valid && !fastdiv_point_ok(x, y, z)) == 0ull) {   // wave-uniform
-        ax = axis_cell<true>(x, hp.bmin[0], hp.bmax[0], hp.cell[lvl][0]);
-        ay = axis_cell<true>(y, hp.bmin[1], hp.bmax[1], hp.cell[lvl][1]);
-        az = axis_cell<true>(z, hp.bmin[2], hp.bmax[2], hp.cell[lvl][2]);
+        ax = axis_cell<true>(x, hp.bmin[0], hp.bmax[0], hp.cell[lvl][0], hp.rcell[lvl][0]);
+        ay = axis_cell<true>(y, hp.bmin[1], hp.bmax[1], hp.cell[lvl][1], hp.rcell[lvl][1]);
+        az = axis_cell<true>(z, hp.bmin[2], hp.bmax[2], hp.cell[lvl][2], hp.rcell[lvl][2]);
     } else {
         ax = axis_cell(x, hp.bmin[0], hp.bmax[0], hp.cell[lvl][0]);
         ay = axis_cell(y, hp.bmin[1], hp.bmax[1], hp.cell[lvl][1]);
@@ -887,7 +888,7 @@ extern "C" int nerf_hash_encode_fwd_q(const float* d_xyz, int64_t n_points, cons
         hp.tables[l] = d_tables[l];
     }
     for (int a = 0; a < 3; ++a) { hp.bmin[a] = bbox_min3[a]; hp.bmax[a] = bbox_max3[a]; }
-    hp.fastdiv = fill_cells(hp.cell, bbox_min3, bbox_max3, level_res, n_levels) ? 1u : 0u;
+    hp.fastdiv = fill_cells(hp.cell, hp.rcell, bbox_min3, bbox_max3, level_res, n_levels) ? 1u : 0u;
     hp.mask = (uint32_t)((1u << log2_T) - 1u);
     const QuantRec* q = reinterpret_cast<const QuantRec*>(d_qrec);
     // coarse levels grouped into one grid row: the leading levels whose (res + 1)^3 vertices fit the
@@ -994,7 +995,7 @@ static int bin_job(const nerf_bin_job& j, const float* bbox_min3, const float* b
                  "hash_encode_bwd_bin: chunks [%lld, %lld) exceed the capacity %lld", (long long)j.chunk_base,
                  (long long)(j.chunk_base + nch), (long long)chunk_capacity);
     for (int a = 0; a < 3; ++a) { hp.bmin[a] = bbox_min3[a]; hp.bmax[a] = bbox_max3[a]; }
-    hp.fastdiv = fill_cells(hp.cell, bbox_min3, bbox_max3, level_res, n_levels) ? 1u : 0u;
+    hp.fastdiv = fill_cells(hp.cell, hp.rcell, bbox_min3, bbox_max3, level_res, n_levels) ? 1u : 0u;
     hp.chunk_base = (int)j.chunk_base;
     hp.nchunks = (int)(j.chunk_base + nch);
     out = BinJob{j.xyz, j.n_points, hp, j.dfeat, j.feat_stride_point, j.feat_stride_level,
@@ -1194,7 +1195,7 @@ extern "C" int nerf_hash_encode_bwd(const float* d_xyz, int64_t n_points, const 
         hp.dtables[l] = d_dtables[l];
     }
     for (int a = 0; a < 3; ++a) { hp.bmin[a] = bbox_min3[a]; hp.bmax[a] = bbox_max3[a]; }
-    hp.fastdiv = fill_cells(hp.cell, bbox_min3, bbox_max3, level_res, n_levels) ? 1u : 0u;
+    hp.fastdiv = fill_cells(hp.cell, hp.rcell, bbox_min3, bbox_max3, level_res, n_levels) ? 1u : 0u;
     hp.mask = (uint32_t)((1u << log2_T) - 1u);
     hipLaunchKernelGGL((hash_encode_bwd_kernel<1, 256>), dim3(blocks_for(n_points, 256), n_levels), dim3(256), 0,
                        as_stream(stream), d_xyz, n_points, hp, d_dfeat, feat_stride_point, feat_stride_level,

@@ -334,7 +334,7 @@ static int hash_params(HashParams& hp, const float* bmin, const float* bmax, con
     NERF_REQUIRE(bmin && bmax && res, "quant: null bbox / resolutions");
     for (int l = 0; l < n_levels; ++l) hp.tables[l] = tables ? tables[l] : nullptr;
     for (int a = 0; a < 3; ++a) { hp.bmin[a] = bmin[a]; hp.bmax[a] = bmax[a]; }
-    hp.fastdiv = fill_cells(hp.cell, bmin, bmax, res, n_levels) ? 1u : 0u;
+    hp.fastdiv = fill_cells(hp.cell, hp.rcell, bmin, bmax, res, n_levels) ? 1u : 0u;
     hp.mask = (uint32_t)((1u << log2_T) - 1u);
     return NERF_OK;
 }

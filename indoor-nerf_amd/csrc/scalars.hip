@@ -14,9 +14,9 @@ namespace nerf {
 // it, with no event between replays. A relaxed store: a release at system scope compiles to a
 // write-back of the whole L2 (the previous step's dirty lines) before it.
 // With `done`, the last 8 bytes of a slot carry the index of the replay the host wrote it for: a slot
-// whose tag is not this fetch's count (the host's and the device's counts have parted, e.g. an
-// upload without its replay) sets the sticky error word behind `done` to count + 1, which the host
-// checks at its next upload — the step would otherwise run on another step's seeds and coefficients.
+// whose tag is not this fetch's count (a replay without its upload: the slot still holds an earlier
+// replay's scalars) sets the sticky error word behind `done` to count + 1, which the host checks at
+// its next upload — the step would otherwise run on another step's seeds and coefficients.
 __global__ void __launch_bounds__(256) scalars_fetch_kernel(const uint32_t* ring, int64_t slot_words, int n_slots,
                                                            int64_t* ctl, uint32_t* dst, int64_t* done) {
     const int64_t c = ctl[0];

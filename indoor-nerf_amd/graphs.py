@@ -131,8 +131,9 @@ class StepScalars:
         e = int(self.err[0])
         if e:
             raise RuntimeError(f"StepScalars: replay {e - 1} fetched a ring slot written for another replay: the "
-                               "uploads and the replays of the captured step have parted (each upload() must be "
-                               "followed by exactly one replay); re-seal() before replaying again")
+                               "uploads and the replays of the captured step have parted (a replay without its "
+                               "upload(); each upload() must be followed by exactly one replay); re-seal() before "
+                               "replaying again")
 
     def upload(self):
         """Run every filler into the ring slot the next replay fetches (call once before each replay)."""

@@ -42,6 +42,7 @@ class RaySampler:
         self.device = device
         self._cams = {}
         self._d_cams = None
+        self._device_cams()     # every camera resident now: a captured step reads them (fill)
 
     def _camera(self, img_i):
         if img_i not in self._cams:

@@ -94,14 +94,15 @@ def test_fused_table_step_is_taken(nerf, gpu):
     assert names.count("nerf_hash_encode_bwd_owner_step") == 2 and names.count("nerf_radam_step") == 2
 
 
-def _unfused_reference(nerf, opt, tables, pre, step):
+def _unfused_reference(nerf, opt, tables, pre, step, lr):
     """RAdam's own launch (nerf_radam_step) applied to the pre-step clones `pre` = [(p, m, v)] with the
-    gradient rows the fused owner pass stored in the tables' .grad, at optimizer step `step`."""
+    gradient rows the fused owner pass stored in the tables' .grad, at optimizer step `step` and the
+    learning rate of that step (train_step's lr_schedule has moved the group's lr on since)."""
     from indoor_nerf_amd import _lib
     group = next(g for g in opt.param_groups if any(q is tables[0] for q in g["params"]))
     n_sma, step_size = opt._scalars(group, step)
     mode = 2 if n_sma >= 5 else (1 if step_size > 0 else 0)
-    dc, stc = opt._coefs(group, mode, step_size)
+    dc, stc = opt._coefs({**group, "lr": lr}, mode, step_size)
     beta1, beta2 = group["betas"]
     segs = []
     for t, (cp, cm, cv) in zip(tables, pre):
@@ -156,6 +157,7 @@ def test_fused_table_step_default_mode_matches_radam_launch(nerf, gpu, graphed, 
         for it in range(1, 10):
             torch.cuda.synchronize()
             pre = None
+            lr = next(g for g in opt.param_groups if any(q is tabs[0] for q in g["params"]))["lr"]
             if it >= 2:   # state exists from the first step on
                 pre = [(p.detach().clone(), opt.state[p]["exp_avg"].clone(), opt.state[p]["exp_avg_sq"].clone())
                        for p in tabs]
@@ -167,7 +169,7 @@ def test_fused_table_step_default_mode_matches_radam_launch(nerf, gpu, graphed, 
             if pre is None:
                 continue
             assert hashgrid.last_fused_table_step() or graphed
-            modes.add(_unfused_reference(nerf, opt, tabs, pre, opt.state[tabs[0]]["step"]))
+            modes.add(_unfused_reference(nerf, opt, tabs, pre, opt.state[tabs[0]]["step"], lr))
             for lvl, (p, (cp, cm, cv)) in enumerate(zip(tabs, pre)):
                 assert torch.equal(p.detach(), cp), f"iteration {it} level {lvl}: parameters"
                 assert torch.equal(opt.state[p]["exp_avg"], cm), f"iteration {it} level {lvl}: exp_avg"

@@ -56,10 +56,10 @@ def test_fetch_cycles_the_ring(gpu):
 
 
 def test_step_scalars_detects_parted_counts(gpu):
-    """graphs.StepScalars: an upload() without its replay parts the host's slot index from the device
-    count; the next replay's fetch flags it and the following upload() raises instead of training on
-    another step's scalars. seal() re-synchronises."""
-    from indoor_nerf_amd import _lib
+    """graphs.StepScalars: a replay without its upload() fetches a slot written for an earlier replay
+    (its tag is that replay's index, not the device count): the fetch flags it and the next upload()
+    raises instead of training on another step's scalars. seal() re-synchronises. (An upload without
+    its replay can only come from an exception between the two; GraphedTrainStep re-seals then.)"""
     from indoor_nerf_amd.graphs import StepScalars
     sc = StepScalars(gpu, n_i64=8, n_f32=8, ring=2)
     off, dptr = sc.alloc_i64(1)
@@ -75,10 +75,10 @@ def test_step_scalars_detects_parted_counts(gpu):
         g.replay()
         torch.cuda.synchronize()
         assert int(sc.dev_i[off]) == 100 + n
-    sc.upload()            # ... and no replay: the counts part
-    sc.upload()
-    g.replay()             # fetches slot 3 % 2, written for replay 4
+    assert int(sc.err[0]) == 0
+    g.replay()             # no upload: replay 3 fetches slot 1, written for replay 1
     torch.cuda.synchronize()
+    assert int(sc.err[0]) == 4
     with pytest.raises(RuntimeError, match="parted"):
         sc.upload()
     sc.seal()
