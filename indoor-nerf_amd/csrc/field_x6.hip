@@ -350,6 +350,7 @@ __device__ __forceinline__ void load_in_x6_bwd(const MlpArgs& a, int64_t n, int6
 }
 
 struct ActX6 {
+    S3 xb[2];       // x's pieces (layer 0's B operand)
     floatx16 h1[2];
     floatx16 o;
     floatx16 h2[2];
@@ -420,7 +421,9 @@ __device__ __forceinline__ floatx16 fold_rows16(const floatx16& acc) {
 template <bool QUANT>
 __device__ __forceinline__ void fwd_chain(const __bf16* img, const InX6& in, ActX6& f, int lane, const QuantRec& aq) {
     const int m = lane & 31, h = lane >> 5;
-    layer0<QUANT>(img, in.x, f.h1, f.m1, lane, aq);
+    f.xb[0] = split_arr(in.x);
+    f.xb[1] = split_arr(in.x + 8);
+    layer0_split<QUANT>(img, f.xb, f.h1, f.m1, lane, aq);
     // L1: o = W1 h1, row-stacked pieces; the zero half reads rows of C2's zero padding (rows 3..15)
     {
         floatx16 acc = zero16();
@@ -785,17 +788,13 @@ __device__ __forceinline__ void bwd_chain_role(const MlpArgs& a, const __bf16* i
         }
 
         // stage 6 (dW1): go, h1 (held in registers since the forward recompute; with QUANT recomputed
-        // from a reload of x) and layer 0's ReLU mask m1 (with QUANT: before the activation quantizer)
+        // from x's pieces) and layer 0's ReLU mask m1 (with QUANT: before the activation quantizer)
         // in the unused columns 16.. of the gradient tile.
         // The wgrad wave forms ga1 = mask(W1^T go) itself (it waits on the chain wave otherwise).
-        // x's bf16 pieces are kept for stage 7 (staged split: the wgrad wave does not split x).
-        S3 xb[2];
-        {
-            float xr[16];
-            load_x6(a, in.pt, in.valid, h, xr, opaque_zero());
-            xb[0] = split_arr(xr);
-            xb[1] = split_arr(xr + 8);
-        }
+        // x's bf16 pieces, split once by fwd_chain and held since, are staged at stage 7 (the wgrad
+        // wave does not split x; no reload of the features: 4 B/lane of spills, MLP backward 380 ->
+        // 375 us per launch, profiles/r05d_ab_bench.jsonl)
+        S3 xb[2] = {f.xb[0], f.xb[1]};
         {
             floatx16 h1[2];
             uint32_t m1;

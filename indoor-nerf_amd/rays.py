@@ -31,7 +31,10 @@ class RaySampler:
 
     def __init__(self, images, poses, H, W, K, i_train, N_rand, precrop_iters=0, precrop_frac=0.5, device=None):
         device = torch.device(device or "cuda")
-        self.images = torch.as_tensor(np.asarray(images), dtype=torch.float32).to(device).contiguous()
+        if torch.is_tensor(images):    # e.g. already resident on the device
+            self.images = images.to(device=device, dtype=torch.float32).contiguous()
+        else:
+            self.images = torch.as_tensor(np.asarray(images), dtype=torch.float32).to(device).contiguous()
         if self.images.dim() != 4 or self.images.shape[-1] < 3:
             raise ValueError("RaySampler: images must be [N, H, W, C>=3]")
         self.poses = np.asarray(poses, dtype=np.float32)[:, :3, :4]
