@@ -546,6 +546,12 @@ __global__ void __launch_bounds__(THREADS) hash_bwd_owner_kernel(HashGradParams 
     const int S = 1 << hp.slice_log2, n_own = 1 << hp.owner_log2;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     for (int i = tid; i < (DET ? 2 : 1) * S; i += kOwnerThreads) s_slice[i] = Acc{0, 0};
+    // the two features' sums as separate arrays: an 8-B add to row h of one array lands on banks
+    // (2h, 2h + 1) mod 64, all 32 bank pairs, where the interleaved (x, y) rows put every x add on
+    // banks 4h, 4h + 1 (16 pairs) and doubled the conflicts of the random-row scatter
+    using Sc = typename std::conditional<A32, float, double>::type;
+    Sc* const s_ax = reinterpret_cast<Sc*>(s_slice);
+    Sc* const s_ay = s_ax + S;
     // DET: scale exponents (hi: 2^sh, lo: 2^(sh + L)) from the level's largest |entry| (the max of
     // the chunks' maxima; a level without entries has max 0)
     int sh = 0, sl_ = 0;
@@ -691,13 +697,8 @@ __global__ void __launch_bounds__(THREADS) hash_bwd_owner_kernel(HashGradParams 
                         atomicAdd(r + 2, (unsigned long long)lx);
                         atomicAdd(r + 3, (unsigned long long)ly);
                     } else {
-                        if constexpr (A32) {
-                            atomicAdd(&s_slice[h[j]].x, g[j].x);
-                            atomicAdd(&s_slice[h[j]].y, g[j].y);
-                        } else {
-                            atomicAdd(&s_slice[h[j]].x, (double)g[j].x);
-                            atomicAdd(&s_slice[h[j]].y, (double)g[j].y);
-                        }
+                        atomicAdd(&s_ax[h[j]], (Sc)g[j].x);
+                        atomicAdd(&s_ay[h[j]], (Sc)g[j].y);
                     }
                 }
             }
@@ -776,7 +777,7 @@ __global__ void __launch_bounds__(THREADS) hash_bwd_owner_kernel(HashGradParams 
 #pragma unroll
             for (int k = 0; k < kRowsP; ++k) {
                 const int i = tid + k * kOwnerThreads;
-                const Acc v = s_slice[i];
+                const Acc v{s_ax[i], s_ay[i]};
                 const float2 g = make_float2((float)v.x, (float)v.y);
                 dt[i] = g;
                 radam_elem(s, pp[k].x, g.x, pm[k].x, pv[k].x);
@@ -789,13 +790,13 @@ __global__ void __launch_bounds__(THREADS) hash_bwd_owner_kernel(HashGradParams 
         }
         if (hp.st_on) {
             owner_table_step<kOwnerThreads, kRows>(hp, lvl, (size_t)o * S, S, dt, [&](int i) {
-                const Acc v = s_slice[i];
+                const Acc v{s_ax[i], s_ay[i]};
                 return make_float2((float)v.x, (float)v.y);
             });
             return;
         }
         for (int i = tid; i < S; i += kOwnerThreads) {
-            const Acc v = s_slice[i];
+            const Acc v{s_ax[i], s_ay[i]};
             dt[i] = make_float2((float)v.x, (float)v.y);
         }
         return;
@@ -809,12 +810,12 @@ __global__ void __launch_bounds__(THREADS) hash_bwd_owner_kernel(HashGradParams 
         for (int k = 0; k < kRows; ++k) t[k] = dt[tid + k * kOwnerThreads];
 #pragma unroll
         for (int k = 0; k < kRows; ++k) {
-            const Acc v = s_slice[tid + k * kOwnerThreads];
+            const Acc v{s_ax[tid + k * kOwnerThreads], s_ay[tid + k * kOwnerThreads]};
             if (v.x != 0 || v.y != 0) dt[tid + k * kOwnerThreads] = make_float2(plus(t[k].x, v.x), plus(t[k].y, v.y));
         }
     } else {   // small tables (log2_T < slice): one partial slice per level
         for (int i = tid; i < S; i += kOwnerThreads) {
-            const Acc v = s_slice[i];
+            const Acc v{s_ax[i], s_ay[i]};
             if (v.x != 0 || v.y != 0) {
                 const float2 t = dt[i];
                 dt[i] = make_float2(plus(t.x, v.x), plus(t.y, v.y));
