@@ -530,7 +530,9 @@ __global__ void __launch_bounds__(THREADS) hash_bwd_owner_kernel(HashGradParams 
     using Acc = typename std::conditional<A32, float2, double2>::type;
     __shared__ __attribute__((aligned(16))) Acc s_slice[(DET ? 2 : 1) << SLICE_LOG2];
     static_assert(sizeof(s_slice) <= 128 * 1024, "owner slice accumulators");
-    unsigned long long* s_fix = reinterpret_cast<unsigned long long*>(s_slice);   // DET: [row][hi x, hi y, lo x, lo y]
+    // DET: four fixed-point word arrays [hi x | hi y | lo x | lo y][S] (8-B row stride per array: random
+    // rows spread over all 32 bank pairs; one [row][4] record put every add on 8 of them)
+    unsigned long long* s_fix = reinterpret_cast<unsigned long long*>(s_slice);
     __shared__ uint32_t s_pre[kOwnerWindow + 1];
     __shared__ uint16_t s_beg[kOwnerWindow];
     __shared__ uint32_t s_wsum[kOwnerThreads / 64];
@@ -691,11 +693,11 @@ __global__ void __launch_bounds__(THREADS) hash_bwd_owner_kernel(HashGradParams 
                         const double hx = rint(tx), hy = rint(ty);
                         const long long lx = (long long)rint(ldexp(tx - hx, sl_ - sh));
                         const long long ly = (long long)rint(ldexp(ty - hy, sl_ - sh));
-                        unsigned long long* r = s_fix + 4 * h[j];
-                        atomicAdd(r + 0, (unsigned long long)(long long)hx);
-                        atomicAdd(r + 1, (unsigned long long)(long long)hy);
-                        atomicAdd(r + 2, (unsigned long long)lx);
-                        atomicAdd(r + 3, (unsigned long long)ly);
+                        unsigned long long* r = s_fix + h[j];
+                        atomicAdd(r, (unsigned long long)(long long)hx);
+                        atomicAdd(r + S, (unsigned long long)(long long)hy);
+                        atomicAdd(r + 2 * S, (unsigned long long)lx);
+                        atomicAdd(r + 3 * S, (unsigned long long)ly);
                     } else {
                         atomicAdd(&s_ax[h[j]], (Sc)g[j].x);
                         atomicAdd(&s_ay[h[j]], (Sc)g[j].y);
@@ -741,7 +743,7 @@ __global__ void __launch_bounds__(THREADS) hash_bwd_owner_kernel(HashGradParams 
     constexpr int kRows = (1 << SLICE_LOG2) / kOwnerThreads;
     if constexpr (DET) {
         auto fixed = [&](int row, int f) {
-            const long long hi = (long long)s_fix[4 * row + f], lo = (long long)s_fix[4 * row + 2 + f];
+            const long long hi = (long long)s_fix[f * S + row], lo = (long long)s_fix[(2 + f) * S + row];
             return ldexp((double)hi, -sh) + ldexp((double)lo, -sl_);
         };
         if (hp.st_on) {   // overwrite mode (the entry point checks): the stored row is the step's gradient
