@@ -760,7 +760,7 @@ def main():
         out["deterministic"] = True
     # north star "PSNR within 0.1 dB of reference": the committed result of tests/test_gpu_converge.py
     # (the reference trained on F19 six times vs six HIP runs; late-phase mean PSNR difference per metric)
-    for name in ("r04_psnr_vs_reference.json", "r03_psnr_vs_reference.json", "r02_psnr_vs_reference.json"):
+    for name in ("r05_psnr_vs_reference.json", "r04_psnr_vs_reference.json", "r03_psnr_vs_reference.json", "r02_psnr_vs_reference.json"):
         pv = os.path.join(ROOT, "profiles", name)
         if os.path.exists(pv):
             pj = json.load(open(pv))
