@@ -622,6 +622,8 @@ def main():
     for _ in range(a.steps):
         loss, psnr = step(it)
         it += 1
+    if zero:
+        sharded.wait_params()      # the last step's gated all-gather is part of the timed work
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()

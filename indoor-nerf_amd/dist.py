@@ -151,6 +151,32 @@ def _all_gather(out, inp, group=None):
         dist.all_gather_into_tensor(out, inp, group=group)
 
 
+def _all_gather_begin(out, inp, group, stream):
+    """Start dist.all_gather_into_tensor on `stream` (the caller's side stream) and return
+    (event, finish): `event` completes with the gathered `out` once finish() (None on device backends)
+    has run on the host. RCCL: the collective is enqueued on the stream, the event recorded behind it.
+    gloo (one-GPU rehearsals, tests): the shard goes to the host, the collective runs asynchronously in
+    gloo's thread, and finish() waits for it and copies the result back on the stream — so the GPU
+    runs the caller's next launches while the collective is in flight, as it would beside RCCL."""
+    ev = torch.cuda.Event()
+    if dist.get_backend(group) == "gloo" and (out.is_cuda or inp.is_cuda):
+        with torch.cuda.stream(stream):
+            h_in = inp.cpu()
+        h = torch.empty(out.shape, dtype=out.dtype)
+        work = dist.all_gather_into_tensor(h, h_in, group=group, async_op=True)
+
+        def finish():
+            work.wait()
+            with torch.cuda.stream(stream):
+                out.copy_(h)
+                ev.record(stream)
+        return ev, finish
+    with torch.cuda.stream(stream):
+        dist.all_gather_into_tensor(out, inp, group=group)
+        ev.record(stream)
+    return ev, None
+
+
 def _capturing(t):
     return t.is_cuda and torch.cuda.is_current_stream_capturing()
 
@@ -214,9 +240,16 @@ class ShardedOptimizer:
     by model.train_step / graphs.GraphedTrainStep for this hook) and reduce_grads() runs it bucket by
     bucket — the levels of bucket 0, then those of bucket 1, ... — starting each bucket's
     reduce-scatter on a side stream as soon as its levels are summed, so the collective of the first
-    buckets runs under the owner pass of the later ones."""
+    buckets runs under the owner pass of the later ones.
+    overlap_gather (default: overlap): gather_params() all-gathers the first bucket in stream order and
+    every later bucket that holds only hash-table levels on the side stream, registering a gate
+    (hashgrid.gate_tables) at the bucket's first level: the next iteration's hash forward launches
+    the levels below it while the collective runs and waits only before the gated levels; any other
+    reader of the tables (TV, A-CAQ calibration, the packed eval tables, reduce_grads,
+    consolidate_state, wait_params) joins the gates first. Parameters of a gated bucket read through
+    another path after gather_params() (e.g. a direct copy of the tensors) need wait_params() first."""
 
-    def __init__(self, optimizer, arena, group=None, overlap=False):
+    def __init__(self, optimizer, arena, group=None, overlap=False, overlap_gather=None):
         self.opt, self.arena, self.group = optimizer, arena, group
         self.world = dist.get_world_size(group) if (dist.is_available() and dist.is_initialized()) else 1
         self.rank = dist.get_rank(group) if self.world > 1 else 0
@@ -253,6 +286,32 @@ class ShardedOptimizer:
         self.overlap = bool(overlap) and len(arena.buckets) > 1 and dev.type == "cuda"
         self.side = torch.cuda.Stream(device=dev) if self.overlap else None
         self._levels = None
+        og = self.overlap if overlap_gather is None else (bool(overlap_gather) and self.overlap)
+        self._gates = self._gate_levels() if og else {}
+
+    def _gate_levels(self):
+        """{bucket index: first table level} for the buckets after the first that hold only hash-table
+        levels (HashEmbedder tags each table with ._nerf_level), in ascending level order; the
+        first bucket that breaks this ends the list (it and the later ones are gathered in order)."""
+        out, last = {}, -1
+        for k, (s, e) in enumerate(self.arena.buckets):
+            if k == 0:
+                continue
+            held = [p for p, off in zip(self.arena.params, self.arena.offsets) if s <= off < e]
+            lv = [getattr(p, "_nerf_level", None) for p in held]
+            if not held or None in lv or min(lv) <= last:
+                break
+            out[k], last = min(lv), max(lv)
+        return out
+
+    def gate_levels(self):
+        """The table levels at which gather_params() leaves a gate for the next forward (ascending)."""
+        return sorted(self._gates.values())
+
+    def wait_params(self):
+        """Make the current stream wait for the side-stream all-gathers of the last gather_params()."""
+        from .hashgrid import join_tables
+        join_tables(self.pflat.device)
 
     def _level_ranges(self, held):
         """Per bucket, the level range [lb, le) of the held owner pass whose tables lie in it."""
@@ -275,6 +334,7 @@ class ShardedOptimizer:
         overlap and a held owner pass: every bucket's levels are summed and recorded first, then each
         bucket's reduce-scatter waits on the side stream for its own levels only."""
         from .hashgrid import pending_bins
+        self.wait_params()      # the last all-gather wrote the parameter shards the update reads
         held = pending_bins(self.arena.flat.device).take_held() if self.overlap else None
         if self.world == 1:
             if held is not None:
@@ -302,11 +362,23 @@ class ShardedOptimizer:
 
     def gather_params(self):
         """All-gather of each bucket's updated parameter shards (in place: the shard is a view of the
-        output)."""
+        output); with overlap_gather the table-only buckets after the first on the side stream,
+        behind gates the next forward joins (class docstring)."""
         if self.world == 1:
             return
-        for (s, e), (lo, hi, _) in zip(self.arena.buckets, self.pieces):
-            _all_gather(self.pflat[s:e], self.pflat[lo:hi], self.group)
+        from .hashgrid import TableGate, gate_tables
+        dev = self.pflat.device
+        self.wait_params()
+        gates = []
+        for k, ((s, e), (lo, hi, _)) in enumerate(zip(self.arena.buckets, self.pieces)):
+            if k not in self._gates:
+                _all_gather(self.pflat[s:e], self.pflat[lo:hi], self.group)
+                continue
+            if not gates:
+                self.side.wait_stream(torch.cuda.current_stream(dev))   # the update wrote the shards
+            ev, finish = _all_gather_begin(self.pflat[s:e], self.pflat[lo:hi], self.group, self.side)
+            gates.append(TableGate(self._gates[k], ev, finish))
+        gate_tables(dev, gates)
         for p in self.arena.params:       # the collective wrote the parameters in place
             torch.autograd.graph.increment_version(p)
 
@@ -318,6 +390,7 @@ class ShardedOptimizer:
         arena, so the call count cannot differ between ranks whatever state each rank holds."""
         if self.world == 1:
             return
+        self.wait_params()
         keys = ("exp_avg", "exp_avg_sq")
         n = self.arena.flat.numel()
         buf = torch.zeros(len(keys) * n, device=self.pflat.device, dtype=torch.float32)

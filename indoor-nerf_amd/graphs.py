@@ -153,6 +153,48 @@ class StepScalars:
         self.issued = n + 1
 
 
+class _Segments:
+    """Capture of one graph as a list of graphs cut at chosen points (split()): each segment is its own
+    CUDAGraph on the same memory pool and capture stream, replayed in order with host work (event
+    waits) between them. Used for graph 1 of a step whose hash forward is gated by a pending
+    parameter all-gather (dist.ShardedOptimizer.gather_params): the segment boundary sits where the
+    eager forward would wait (hashgrid.split_next_forward)."""
+
+    def __init__(self, pool, stream):
+        self.pool, self.stream, self.graphs, self.cuts = pool, stream, [], []
+
+    def _begin(self):
+        g = torch.cuda.CUDAGraph()
+        g.capture_begin(self.pool, capture_error_mode="global")
+        self.graphs.append(g)
+
+    def split(self, level):
+        self.graphs[-1].capture_end()
+        self.cuts.append(int(level))
+        self._begin()
+
+    def __enter__(self):
+        torch.cuda.synchronize()
+        self._ctx = torch.cuda.stream(self.stream)
+        self._ctx.__enter__()
+        self._begin()
+        return self
+
+    def __exit__(self, *exc):
+        try:
+            self.graphs[-1].capture_end()
+        finally:
+            self._ctx.__exit__(*exc)
+        return False
+
+
+def gate_levels(post_hook):
+    """The table levels at which a post hook (dist.ShardedOptimizer.gather_params) leaves gates for the
+    next forward; [] for any other hook."""
+    fn = getattr(getattr(post_hook, "__self__", None), "gate_levels", None)
+    return list(fn()) if callable(fn) else []
+
+
 class GraphedTrainStep:
     """train_step (model.py) as captured graphs: one (forward + backward + RAdam) without a grad
     hook; with one, two graphs (forward + backward, RAdam) and the eager grad hook between them and
@@ -211,6 +253,7 @@ class GraphedTrainStep:
             raise RuntimeError("GraphedTrainStep: kernel timing is on; torch on ROCm cannot capture timing "
                                "events (time eager_step() instead)")
         dev = self.target.device
+        hashgrid.join_tables(dev)          # the previous step's parameter all-gather, if still pending
         sc = StepScalars(dev)
         emb = self.kw["embed_fn"]
         step0 = emb.current_step           # the captured (not executed) forwards must not count
@@ -220,22 +263,28 @@ class GraphedTrainStep:
         # without a gradient hook between them (one process) the update joins the first graph: one
         # graph launch per iteration (a second launch left the GPU idle ~9 us between them)
         single = self.hook is None
-        g1 = torch.cuda.CUDAGraph()
         g2 = None if single else torch.cuda.CUDAGraph()
         # with an overlapping DP hook the owner pass stays out of graph 1: the hook runs it by level range
         # beside the bucket reduce-scatters (dist.ShardedOptimizer(overlap=True))
         with torch.cuda.stream(side), hashgrid.hold_owner(dev, holds_owner(self.hook)), \
                 hashgrid.fused_table_step(dev, self.opt, emb.tables(), enabled=self.hook is None):
             with capturing(sc):
-                with torch.cuda.graph(g1, pool=pool, stream=side):
-                    sc.capture_fetch()
-                    if self.sampler is not None:
-                        self.sampler.fill(global_step, self.rays[0], self.rays[1], self.target)
-                    out = forward_backward(self.rays, self.target, self.kw, self.opt, self.args, global_step,
-                                           H=self.H, W=self.W, K=self.K, loss_scale_sparsity=self.scale_sp,
-                                           tv_generator=self.tv_gen, zero_grad=self.zero_grad, schedule=False)
-                    if single:
-                        optimizer_update(self.opt)
+                # with a gated parameter all-gather behind the post hook, graph 1 is cut into segments
+                # where the hash forward would wait for it (replayed with the waits between them)
+                seg = _Segments(pool, side)
+                try:
+                    with seg:
+                        hashgrid.split_next_forward(dev, gate_levels(self.post_hook), seg.split)
+                        sc.capture_fetch()
+                        if self.sampler is not None:
+                            self.sampler.fill(global_step, self.rays[0], self.rays[1], self.target)
+                        out = forward_backward(self.rays, self.target, self.kw, self.opt, self.args, global_step,
+                                               H=self.H, W=self.W, K=self.K, loss_scale_sparsity=self.scale_sp,
+                                               tv_generator=self.tv_gen, zero_grad=self.zero_grad, schedule=False)
+                        if single:
+                            optimizer_update(self.opt)
+                finally:
+                    hashgrid.split_next_forward(dev, None, None)
                 if not single:
                     with torch.cuda.graph(g2, pool=pool, stream=side):
                         optimizer_update(self.opt)
@@ -243,7 +292,8 @@ class GraphedTrainStep:
         sc.seal()
         emb.current_step = step0
         old = getattr(self, "scalars", None)
-        self.graphs = (g1, g2)
+        self.graphs = (seg.graphs, g2)
+        self.cuts = seg.cuts
         self.out = out
         self.scalars = sc
         if old is not None:
@@ -260,6 +310,21 @@ class GraphedTrainStep:
         return train_step(self.rays, self.target, self.kw, self.opt, self.args, global_step, H=self.H, W=self.W,
                           K=self.K, grad_hook=self.hook, loss_scale_sparsity=self.scale_sp,
                           tv_generator=self.tv_gen, zero_grad=self.zero_grad, post_hook=self.post_hook)
+
+    def _replay_forward(self):
+        """Graph 1's segments in order; before each, the pending table gates (the last post hook's
+        side-stream all-gathers) of the levels it reads: segment k reads levels below the next cut,
+        the last one everything."""
+        from . import hashgrid
+        dev = self.target.device
+        segs, gates = self.graphs[0], hashgrid.take_gates(self.target.device)
+        ends = list(self.cuts) + [float("inf")]
+        stream = torch.cuda.current_stream(dev)
+        for k, g in enumerate(segs):
+            for gate in [x for x in gates if x.level < ends[k]]:
+                gates.remove(gate)
+                gate.join(stream)
+            g.replay()
 
     def _priors_active(self, global_step):
         from .model import DEFAULTS
@@ -286,7 +351,7 @@ class GraphedTrainStep:
         self.scalars.step = global_step
         try:
             self.scalars.upload()
-            self.graphs[0].replay()
+            self._replay_forward()
         except BaseException:
             # an upload without its replay (or the reverse) would pair every later replay with another
             # step's slot: re-synchronise the host's and the device's replay counts

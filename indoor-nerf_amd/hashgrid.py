@@ -67,6 +67,58 @@ def take_deferred(grads):
     return False
 
 
+# Parameter-gather gates (dist.ShardedOptimizer(overlap=True).gather_params): the
+# all-gather of each table bucket after the first runs on a side stream and is joined only where the
+# next iteration first reads those levels. The hash forward launches the levels below a gate, joins
+# it, then launches the levels from it on (encode_into); any other reader of the tables joins every
+# pending gate first (join_tables). Under graph capture the gated forward is cut into graph segments
+# at the same levels instead (split_next_forward), and the replay joins the gates between the segments.
+class TableGate:
+    """Levels [level, L) of a device's tables are being written by a side-stream collective: join()
+    runs `finish` on the host once (the gloo rehearsal's wait + host->device copy; None on RCCL) and
+    makes `stream` wait for `event`."""
+
+    def __init__(self, level, event, finish=None):
+        self.level, self.event, self.finish = int(level), event, finish
+
+    def join(self, stream):
+        if self.finish is not None:
+            f, self.finish = self.finish, None
+            f()
+        stream.wait_event(self.event)
+
+
+_GATES = {}    # str(device) -> [TableGate], ascending levels
+_SPLITS = {}   # str(device) -> (levels, callback): the next hash forward is cut into graph segments
+
+
+def gate_tables(device, gates):
+    """Register the pending table gates of `device` (an older set is joined first)."""
+    join_tables(device)
+    if gates:
+        _GATES[str(device)] = sorted(gates, key=lambda g: g.level)
+
+
+def join_tables(device):
+    """Make the current stream wait for every pending table gate of `device` (no-op without one)."""
+    for g in _GATES.pop(str(device), ()):
+        g.join(torch.cuda.current_stream(device))
+
+
+def take_gates(device):
+    """Remove and return the pending gates of `device` (the caller joins them)."""
+    return _GATES.pop(str(device), [])
+
+
+def split_next_forward(device, levels, split):
+    """During a graph capture: cut the next hash forward on `device` before each of `levels`, calling
+    split(level) there (graphs.GraphedTrainStep ends one graph segment and begins the next)."""
+    if levels:
+        _SPLITS[str(device)] = (sorted(int(v) for v in levels), split)
+    else:
+        _SPLITS.pop(str(device), None)
+
+
 def accumulate_grad_buffers(params):
     """The fused backward kernels ACCUMULATE straight into .grad (like a fused optimizer's bucket):
     create zero grads where they are missing and return them."""
@@ -441,9 +493,10 @@ class HashEmbedder(nn.Module):
         res, self.b = level_resolutions(self.base_resolution, self.finest_resolution, n_levels)
         self.embeddings = nn.ModuleList([nn.Embedding(2 ** log2_hashmap_size, n_features_per_level)
                                          for _ in range(n_levels)])
-        for emb in self.embeddings:
+        for i, emb in enumerate(self.embeddings):
             nn.init.uniform_(emb.weight, a=-0.0001, b=0.0001)
             emb.weight._nerf_owner_grad = True   # every backward into it ends in an owner pass
+            emb.weight._nerf_level = i           # dist.ShardedOptimizer's gather gates name levels
         # A-CAQ (hash_encoding.py:37-53): one asymmetric learned-bitwidth quantizer per level,
         # registered after the tables as in the reference (parameter order = optimizer state order)
         self.quantizers = nn.ModuleList([
@@ -472,6 +525,7 @@ class HashEmbedder(nn.Module):
         if self.training:
             todo = [i for i, q in enumerate(qs) if not q.calibrated]
             if todo:
+                join_tables(xyz.device)
                 xyz = xyz.contiguous()
                 st = new_stats(len(qs), xyz.device)
                 meta = self._meta
@@ -500,6 +554,7 @@ class HashEmbedder(nn.Module):
         tabs = self.tables()
         key = tuple((t.data_ptr(), t._version) for t in tabs)
         n, dev = self.n_levels, tabs[0].device
+        join_tables(dev)
         st = self._packed
         if st is None or st["buf"].device != dev:
             nbytes = int(_lib.load().nerf_quant_packed_bytes(n, self.log2_hashmap_size))
@@ -523,6 +578,12 @@ class HashEmbedder(nn.Module):
             raise ValueError("encode_into: rows out of the feature / keep buffers")
         fp = _lib.ptr_at(feat, sp * row0, "feat")
         kp = _lib.ptr_at(keep, row0, "keep", dtype=torch.bool)
+        key, L = str(xyz.device), self.n_levels
+        plain = not self.quantization_active()
+        gates = _GATES.pop(key, []) if plain else []
+        plan = _SPLITS.pop(key, None) if plain else None
+        if not plain:
+            join_tables(xyz.device)
         if self.quantization_active() and not self.training:
             buf, rec = self.packed_tables()
             _lib.call("nerf_hash_encode_fwd_packed", _lib.ptr(xyz, "xyz"), P, meta["bmin"], meta["bmax"], meta["res"],
@@ -530,9 +591,39 @@ class HashEmbedder(nn.Module):
                       _lib.ptr(rec, "records"), fp, sp, sl, kp, _lib.stream())
             return
         rec = self.level_records(xyz) if self.quantization_active() else None
-        _lib.call("nerf_hash_encode_fwd_q", _lib.ptr(xyz, "xyz"), P, meta["bmin"], meta["bmax"], meta["res"],
-                  self.n_levels, meta["log2_T"], _lib.ptr_array(self.tables()), _lib.ptr(rec, "records", allow_none=True),
-                  fp, sp, sl, kp, _lib.stream())
+        if not gates and plan is None:
+            _lib.call("nerf_hash_encode_fwd_q", _lib.ptr(xyz, "xyz"), P, meta["bmin"], meta["bmax"], meta["res"],
+                      self.n_levels, meta["log2_T"], _lib.ptr_array(self.tables()),
+                      _lib.ptr(rec, "records", allow_none=True), fp, sp, sl, kp, _lib.stream())
+            return
+        # gated (a pending parameter all-gather of the upper levels) or cut for a graph capture: the
+        # levels below each cut first, then the wait / the segment boundary, then the next range.
+        # Levels are independent (the keep flags come with level 0), so the features are the same bits.
+        stream = torch.cuda.current_stream(xyz.device)
+        cuts = [g.level for g in gates] if gates else plan[0]
+        bounds = sorted({0, L} | {min(max(c, 0), L) for c in cuts})
+        tabs = self.tables()
+        for lb, le in zip(bounds[:-1], bounds[1:]):
+            for g in [g for g in gates if g.level <= lb]:
+                gates.remove(g)
+                g.join(stream)
+            if plan is not None and lb in plan[0] and lb > 0:
+                plan[1](lb)
+            res = self._level_slice(lb, le)
+            _lib.call("nerf_hash_encode_fwd_q", _lib.ptr(xyz, "xyz"), P, meta["bmin"], meta["bmax"], res, le - lb,
+                      meta["log2_T"], _lib.ptr_array(tabs[lb:le]), None,
+                      _lib.ptr_at(feat, sp * row0 + sl * lb, "feat"), sp, sl, kp if lb == 0 else None, _lib.stream())
+        for g in gates:           # cuts at or past the last level: nothing here reads them
+            g.join(stream)
+
+    def _level_slice(self, lb, le):
+        """Host resolutions of levels [lb, le) (the whole-grid array for [0, L))."""
+        if (lb, le) == (0, self.n_levels):
+            return self._meta["res"]
+        cache = self._meta.setdefault("res_slices", {})
+        if (lb, le) not in cache:
+            cache[(lb, le)] = _lib.host_f32(self.level_res[lb:le])
+        return cache[(lb, le)]
 
     def binned_backward(self):
         """The binned backward exists for these tables (log2_T <= 19, plain and deterministic)."""

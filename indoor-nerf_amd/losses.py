@@ -43,6 +43,7 @@ class TVFn(torch.autograd.Function):
         else:   # a zeroed accumulator (tv_accumulator: its fill rides along in render()'s first launch)
             _lib.flush_zero_fills([out])
             loss = out
+        hashgrid.join_tables(dev)     # a pending parameter all-gather of the upper levels (dist.py)
         _lib.call("nerf_tv_fwd", _lib.ptr_array(tables), L, log2_T, mv, dmv, cb, _lib.ptr(loss, "loss"),
                   _lib.ptr(verts, "tv_verts"), _lib.stream())
         ctx.save_for_backward(*tables)

@@ -245,3 +245,49 @@ def test_sharded_checkpoint_collective_save(tmp_path):
         st = ck["optimizer_state_dict"]["state"][i]
         torch.testing.assert_close(st["exp_avg"], idx, rtol=0, atol=0)
         torch.testing.assert_close(st["exp_avg_sq"], 2 * idx, rtol=0, atol=0)
+
+
+def test_gather_gate_levels_from_buckets():
+    """ShardedOptimizer's gated all-gather plan: the buckets after the first that hold only
+    hash-table levels (._nerf_level, set by HashEmbedder), in ascending level order, each gated at its
+    first level; a bucket with any other parameter ends the plan. No gates without overlap / on CPU."""
+    from indoor_nerf_amd.dist import GradArena, ShardedOptimizer
+
+    def make(starts):
+        mlp = [torch.nn.Parameter(torch.zeros(n)) for n in (300, 77)]
+        tabs = [torch.nn.Parameter(torch.zeros(1 << 10, 2)) for _ in range(4)]
+        for i, t in enumerate(tabs):
+            t._nerf_level = i
+        params = mlp + tabs
+        sh = ShardedOptimizer(_SgdShard(params), GradArena(params, pad_to=64, bucket_starts=starts(mlp, tabs)))
+        return sh
+
+    sh = make(lambda m, t: [t[2]])
+    assert sh.gate_levels() == [] and sh._gates == {}       # overlap needs CUDA buckets
+    assert sh._gate_levels() == {1: 2}
+    assert make(lambda m, t: [t[1], t[3]])._gate_levels() == {1: 1, 2: 3}
+    assert make(lambda m, t: [m[1]])._gate_levels() == {}     # bucket 1 holds an MLP tensor
+    assert make(lambda m, t: [])._gate_levels() == {}
+
+
+def test_table_gate_join_order():
+    """hashgrid's gate registry: join() runs the host finish once, then the stream wait; gate_tables
+    joins an older set first; take_gates hands the set over."""
+    from indoor_nerf_amd import hashgrid
+
+    class _Stream:
+        def __init__(self):
+            self.waited = []
+
+        def wait_event(self, ev):
+            self.waited.append(ev)
+
+    calls = []
+    s = _Stream()
+    g = hashgrid.TableGate(8, "ev8", finish=lambda: calls.append("finish"))
+    g.join(s)
+    g.join(s)
+    assert calls == ["finish"] and s.waited == ["ev8", "ev8"]
+    hashgrid.gate_tables("cpu:test", [hashgrid.TableGate(12, "b"), hashgrid.TableGate(4, "a")])
+    got = hashgrid.take_gates("cpu:test")
+    assert [x.level for x in got] == [4, 12] and hashgrid.take_gates("cpu:test") == []

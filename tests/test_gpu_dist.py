@@ -120,6 +120,7 @@ def _train_worker(rank, world, port, out, overlap=False):
     for it in range(1, 7):
         loss, _ = st(it)
         losses.append(float(loss))
+    sh.wait_params()       # with overlap the last all-gather of the table levels 8-15 is still gated
     torch.cuda.synchronize()
     torch.save({"params": [p.detach().cpu() for p in params], "losses": losses, "captures": st.captures},
                os.path.join(out, f"train_{rank}.pt"))
@@ -140,6 +141,74 @@ def test_sharded_graphed_training_replicas_agree(tmp_path, overlap):
     assert all(torch.isfinite(torch.tensor(l)) for l in r0["losses"] + r1["losses"])
     for a, b in zip(r0["params"], r1["params"]):
         assert torch.equal(a, b)
+
+
+def _gather_worker(rank, world, port, out):
+    """ZeRO-1 with two buckets (MLP + levels 0-7 | levels 8-15), deterministic mode, 5 iterations, four
+    ways: eager / graphed x all-gather in stream order (overlap_gather=False) / gated (the levels 8-15
+    bucket all-gathered on the side stream, joined by the next forward between its level ranges)."""
+    _init(rank, world, port)
+    import indoor_nerf_amd as nerf
+    from indoor_nerf_amd import hashgrid
+    from indoor_nerf_amd.graphs import GraphedTrainStep
+    from tables import blender_bbox, synthetic_rays
+    nerf.set_deterministic(True)
+    dev = torch.device("cuda:0")
+    lo, hi = blender_bbox()
+    res = {}
+    for graphed in (False, True):
+        for gated in (False, True):
+            args = nerf.make_args(bounding_box=(torch.from_numpy(lo), torch.from_numpy(hi)), finest_res=1024,
+                                  N_samples=64, N_importance=128, white_bkgd=True, perturb=1.0, tv_loss_weight=1e-6)
+            torch.manual_seed(rank)
+            nerf.manual_seed(77 + rank)
+            kw, _, _, grad_vars, opt = nerf.create_nerf(args, device=dev)
+            kw.update(near=2.0, far=6.0)
+            params = grad_vars + list(kw["embed_fn"].parameters())
+            nerf.broadcast_params(params)
+            tabs = kw["embed_fn"].tables()
+            arena = nerf.GradArena(params, pad_to=world * 64, defer_tables=True, bucket_starts=[tabs[8]])
+            sh = nerf.ShardedOptimizer(opt, arena, overlap=True, overlap_gather=gated)
+            assert sh.gate_levels() == ([8] if gated else [])
+            ro, rd = synthetic_rays(512, seed=50 + rank)
+            rays = (torch.from_numpy(ro).to(dev), torch.from_numpy(rd).to(dev))
+            target = torch.rand(512, 3, device=dev, generator=torch.Generator(device=dev).manual_seed(rank))
+            common = dict(grad_hook=sh.reduce_grads, post_hook=sh.gather_params, loss_scale_sparsity=float(world),
+                          tv_generator=torch.Generator().manual_seed(7), zero_grad=arena.zero_)
+            st = GraphedTrainStep(rays, target, kw, opt, args, **common) if graphed else None
+            losses, pending = [], 0
+            for it in range(1, 6):
+                loss, _ = st(it) if graphed else nerf.train_step(rays, target, kw, opt, args, it, **common)
+                losses.append(float(loss))
+                pending += len(hashgrid._GATES.get(str(dev), []))
+            sh.wait_params()
+            torch.cuda.synchronize()
+            res[(graphed, gated)] = {"params": [p.detach().cpu() for p in params], "losses": losses,
+                                     "pending": pending, "cuts": list(st.cuts) if graphed else None,
+                                     "segments": len(st.graphs[0]) if graphed else None}
+    torch.save({f"{int(g)}{int(o)}": v for (g, o), v in res.items()}, os.path.join(out, f"gather_{rank}.pt"))
+    torch.distributed.destroy_process_group()
+
+
+def test_param_gather_overlap_bit_identical(tmp_path):
+    """The gated parameter all-gather (dist.ShardedOptimizer(overlap=True)) against the same
+    collective in stream order, eager and graphed: parameters and losses bit-identical after 5
+    iterations, replicas bit-identical; every gated step left its gate for the next forward, and the
+    captured graph 1 is cut into two segments at level 8."""
+    world = 2
+    mp.start_processes(_gather_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    r = [torch.load(tmp_path / f"gather_{k}.pt", weights_only=True) for k in range(world)]
+    for mode in ("0", "1"):
+        serial, gated = r[0][mode + "0"], r[0][mode + "1"]
+        assert serial["pending"] == 0 and gated["pending"] == 5
+        assert serial["losses"] == gated["losses"]
+        for a, b in zip(serial["params"], gated["params"]):
+            assert torch.equal(a, b)
+        for a, b in zip(gated["params"], r[1][mode + "1"]["params"]):
+            assert torch.equal(a, b)
+    assert r[0]["11"]["cuts"] == [8] and r[0]["11"]["segments"] == 2
+    assert r[0]["10"]["cuts"] == [] and r[0]["10"]["segments"] == 1
 
 
 def _f10_model(nerf, dev, world):
@@ -215,6 +284,8 @@ def _dp_worker(rank, world, port, out, R, overlap=False, det=False):
         loss, _ = nerf.train_step(rays, tgt, kw, opt, args, it, grad_hook=hook, post_hook=post,
                                   loss_scale_sparsity=float(world), tv_generator=gen, zero_grad=arena.zero_)
         losses.append(float(loss))
+    if world > 1:
+        sh.wait_params()   # the last gated all-gather (overlap)
     torch.cuda.synchronize()
     res["params"] = [p.detach().cpu().clone() for p in params]
     res["losses"] = losses

@@ -12,7 +12,11 @@ reduce-scatter (the side stream it is issued on), plus host times; per rank, the
 (us from the step's first stamp) go to OUT.json (rank r writes OUT.json.r<r>). With gloo the
 collective itself runs on the host between a device->host and a host->device copy on the side stream,
 so what the trace shows is the side stream's bucket-0 span running while the main stream still
-executes the owner blocks of bucket 1's levels — the RCCL collective would sit in the same place."""
+executes the owner blocks of bucket 1's levels — the RCCL collective would sit in the same place.
+The gated parameter all-gather (ShardedOptimizer.gather_params with overlap): the bucket of levels
+8-15 starts on the side stream at the end of step i (gloo: asynchronously in gloo's thread), and step
+i + 1's hash forward launches levels 0-7, joins the gate (host wait for gloo + the copy back on the side
+stream + the main stream's event wait), then launches levels 8-15; the last two steps are written."""
 import json
 import os
 import sys
@@ -60,6 +64,28 @@ def main():
         stamp(f"reduce-scatter bucket {n} end", s)
         return r
 
+    orig_ag, orig_join, orig_slice = ndist._all_gather_begin, hashgrid.TableGate.join, hashgrid.HashEmbedder._level_slice
+
+    def ag(o, i, group, stream):
+        stamp("all-gather gated bucket start (side stream)", stream)
+        ev, finish = orig_ag(o, i, group, stream)
+
+        def fin():
+            if finish is not None:
+                finish()
+            stamp("all-gather gated bucket end (side stream)", stream)
+        return ev, fin
+
+    def join(self, stream):
+        stamp(f"gate level {self.level}: join (host) ", stream)
+        orig_join(self, stream)
+        stamp(f"gate level {self.level}: main stream past the wait", stream)
+
+    def level_slice(self, lb, le):
+        stamp(f"hash forward levels [{lb},{le}) launch")
+        return orig_slice(self, lb, le)
+
+    ndist._all_gather_begin, hashgrid.TableGate.join, hashgrid.HashEmbedder._level_slice = ag, join, level_slice
     nerf.train_step, hashgrid.HeldOwner.run, ndist._reduce_scatter = train_step, run, rs
     import bench
     bench.main()
@@ -69,8 +95,13 @@ def main():
     ref, h0 = last[0][1], last[0][2]
     spans = [{"event": n, "gpu_us": round(1e3 * ref.elapsed_time(ev), 1), "host_us": round(1e6 * (h - h0), 1)}
              for n, ev, h in last]
+    two = STEPS[-2] + STEPS[-1]
+    ref2, h2 = two[0][1], two[0][2]
+    spans2 = [{"event": n, "gpu_us": round(1e3 * ref2.elapsed_time(ev), 1), "host_us": round(1e6 * (h - h2), 1)}
+              for n, ev, h in two]
     with open(f"{out}.r{rank}", "w") as f:
-        json.dump({"rank": rank, "steps_recorded": len(STEPS), "last_step": spans}, f, indent=1)
+        json.dump({"rank": rank, "steps_recorded": len(STEPS), "last_step": spans, "last_two_steps": spans2},
+                  f, indent=1)
 
 
 if __name__ == "__main__":
