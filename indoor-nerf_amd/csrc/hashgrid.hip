@@ -8,8 +8,8 @@
 // in one thread, with the reference's op order and no contraction (-ffp-contract=off), so indices,
 // keep mask and features are bit-identical to the fp32 reference.
 //
-// Launch geometry: grid (ceil(P/128), 1 + L - G): row 0 runs the G coarse levels of its points
-// (hash_encode_fwd_pair_kernel), every other row one level. Blocks are dispatched x-fastest, so at
+// Launch geometry: rows of blocks in one grid dimension: row 0 runs the G coarse levels of its points
+// (hash_encode_fwd_pair_kernel), every other row one level. Blocks are dispatched in order, so at
 // any moment the whole chip works on one or two levels and each XCD's 4 MiB L2 holds the level's
 // table lines that the current point range touches (tables are 4 MiB per level at log2_T = 19).
 #include <stdlib.h>
@@ -96,20 +96,54 @@ __device__ __forceinline__ void owner_table_step(const HashGradParams& hp, int l
 // level): grouping the 6 coarse levels of the lego config took the forward from 121 to 107 us per
 // launch (same box; 3 or 6 levels in flight: 114 / 154 us, the registers cost occupancy).
 
+#ifdef NERF_FWD_PROF   // diagnostic build only (tools/fwd_prof.py): per-block start / end (100 MHz real
+                       // time) and the XCC / hardware ids of the block's first wave
+constexpr int kFwdProfBlocks = 65536;
+__device__ unsigned long long fwd_prof[kFwdProfBlocks * 3];
+#endif
+
+// Points per thread on the single-level rows (the grouped row keeps one: its levels are its
+// memory-level parallelism). Two points (p and p + 128 of the block's 256) put 8 gathers in flight
+// per thread instead of 4: per-block timelines (tools/fwd_prof.py, profiles/r05p_fwd_prof_pts*.json)
+// show each level row running as ~1.5 waves of latency-bound blocks; 92.6 -> 88.2 us per launch in
+// the bench, bit-identical (profiles/r05p_ab_fwd_row_pts2.jsonl)
+#ifndef NERF_FWD_ROW_PTS
+#define NERF_FWD_ROW_PTS 2
+#endif
+constexpr int kFwdRowPts = NERF_FWD_ROW_PTS;
+
+// Grid: one dimension, rows in order — blocks [0, gx0) the grouped row (128 points each), then gx1
+// blocks (128 kFwdRowPts points each) per single-level row (group == 0: gx1 per level from block 0).
 template <bool QUANT>
 __global__ void __launch_bounds__(256) hash_encode_fwd_pair_kernel(
-    const float* __restrict__ xyz, int64_t n, HashParams hp, int group,
+    const float* __restrict__ xyz, int64_t n, HashParams hp, int group, unsigned gx0, unsigned gx1,
     float* __restrict__ feat, int64_t sp, int64_t sl, uint8_t* __restrict__ keep,
     const QuantRec* __restrict__ qrec) {
-    const int row = blockIdx.y;
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t p = t >> 1;
-    const int xb = (int)(t & 1);
-    const bool valid = p < n;
-    const int64_t pc = valid ? p : n - 1;             // invalid lanes mirror a valid point (no stores)
-    const float x = xyz[3 * pc + 0], y = xyz[3 * pc + 1], z = xyz[3 * pc + 2];
-    const bool fast = hp.fastdiv && __ballot(!fastdiv_point_ok(x, y, z)) == 0ull;   // wave-uniform
-    if (group > 0 && row == 0) {
+#ifdef NERF_FWD_PROF
+    const size_t prof_blk = blockIdx.x;
+    if (threadIdx.x == 0 && prof_blk < kFwdProfBlocks) {
+        fwd_prof[prof_blk * 3 + 0] = __builtin_amdgcn_s_memrealtime();
+        // XCC_ID (hwreg 20, 4 bits) << 32 | HW_ID (hwreg 4: wave, SIMD, CU, SE ids)
+        const unsigned xcc = __builtin_amdgcn_s_getreg(20 | (3 << 11));
+        const unsigned hw = __builtin_amdgcn_s_getreg(4 | (31 << 11));
+        fwd_prof[prof_blk * 3 + 2] = ((unsigned long long)xcc << 32) | hw;
+    }
+    struct Done {
+        size_t b;
+        __device__ ~Done() {
+            __syncthreads();
+            if (threadIdx.x == 0 && b < kFwdProfBlocks) fwd_prof[b * 3 + 1] = __builtin_amdgcn_s_memrealtime();
+        }
+    } done{prof_blk};
+#endif
+    const unsigned b = blockIdx.x;
+    const int xb = (int)(threadIdx.x & 1);
+    if (group > 0 && b < gx0) {
+        const int64_t p = ((int64_t)b * blockDim.x + threadIdx.x) >> 1;
+        const bool valid = p < n;
+        const int64_t pc = valid ? p : n - 1;         // invalid lanes mirror a valid point (no stores)
+        const float x = xyz[3 * pc + 0], y = xyz[3 * pc + 1], z = xyz[3 * pc + 2];
+        const bool fast = hp.fastdiv && __ballot(!fastdiv_point_ok(x, y, z)) == 0ull;   // wave-uniform
         for (int l0 = 0; l0 < group; l0 += kFwdGroupRound) {
             FwdLvl s[kFwdGroupRound];
 #pragma unroll
@@ -125,11 +159,30 @@ __global__ void __launch_bounds__(256) hash_encode_fwd_pair_kernel(
         }
         return;
     }
-    const int lvl = group > 0 ? group + row - 1 : row;
-    FwdLvl s;
-    if (fast) fwd_gather<true>(x, y, z, hp, lvl, xb, s);
-    else fwd_gather<false>(x, y, z, hp, lvl, xb, s);
-    fwd_finish<QUANT>(s, lvl, xb, valid, pc, feat, sp, sl, keep, qrec);
+    const unsigned r = group > 0 ? b - gx0 : b;
+    const int lvl = (group > 0 ? group : 0) + (int)(r / gx1);
+    const int64_t p0 = (int64_t)(r % gx1) * (128 * kFwdRowPts) + (threadIdx.x >> 1);
+    int64_t pc[kFwdRowPts];
+    bool valid[kFwdRowPts];
+    float x[kFwdRowPts], y[kFwdRowPts], z[kFwdRowPts];
+    bool ok = true;
+#pragma unroll
+    for (int k = 0; k < kFwdRowPts; ++k) {
+        const int64_t p = p0 + 128 * k;
+        valid[k] = p < n;
+        pc[k] = valid[k] ? p : n - 1;
+        x[k] = xyz[3 * pc[k] + 0]; y[k] = xyz[3 * pc[k] + 1]; z[k] = xyz[3 * pc[k] + 2];
+        ok = ok && fastdiv_point_ok(x[k], y[k], z[k]);
+    }
+    const bool fast = hp.fastdiv && __ballot(!ok) == 0ull;
+    FwdLvl s[kFwdRowPts];
+#pragma unroll
+    for (int k = 0; k < kFwdRowPts; ++k) {
+        if (fast) fwd_gather<true>(x[k], y[k], z[k], hp, lvl, xb, s[k]);
+        else fwd_gather<false>(x[k], y[k], z[k], hp, lvl, xb, s[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < kFwdRowPts; ++k) fwd_finish<QUANT>(s[k], lvl, xb, valid[k], pc[k], feat, sp, sl, keep, qrec);
 }
 
 
@@ -905,14 +958,17 @@ extern "C" int nerf_hash_encode_fwd_q(const float* d_xyz, int64_t n_points, cons
         ++group;
     }
     if (group < 2) group = 0;
-    const int rows = group > 0 ? n_levels - group + 1 : n_levels;
-    dim3 grid2((unsigned)blocks_for(2 * n_points, 256), rows);
+    const unsigned gx0 = group > 0 ? (unsigned)blocks_for(2 * n_points, 256) : 0u;
+    const unsigned gx1 = (unsigned)blocks_for(2 * n_points, 256 * kFwdRowPts);
+    const size_t nblk = (size_t)gx0 + (size_t)gx1 * (size_t)(n_levels - (group > 0 ? group : 0));
+    NERF_REQUIRE(nblk < (1ull << 31), "hash_encode_fwd: %lld points", (long long)n_points);
+    const dim3 grid((unsigned)nblk);
     if (q)
-        hipLaunchKernelGGL(hash_encode_fwd_pair_kernel<true>, grid2, dim3(256), 0, as_stream(stream), d_xyz,
-                           n_points, hp, group, d_feat, feat_stride_point, feat_stride_level, d_keep, q);
+        hipLaunchKernelGGL(hash_encode_fwd_pair_kernel<true>, grid, dim3(256), 0, as_stream(stream), d_xyz,
+                           n_points, hp, group, gx0, gx1, d_feat, feat_stride_point, feat_stride_level, d_keep, q);
     else
-        hipLaunchKernelGGL(hash_encode_fwd_pair_kernel<false>, grid2, dim3(256), 0, as_stream(stream), d_xyz,
-                           n_points, hp, group, d_feat, feat_stride_point, feat_stride_level, d_keep, q);
+        hipLaunchKernelGGL(hash_encode_fwd_pair_kernel<false>, grid, dim3(256), 0, as_stream(stream), d_xyz,
+                           n_points, hp, group, gx0, gx1, d_feat, feat_stride_point, feat_stride_level, d_keep, q);
     NERF_CHECK_LAUNCH("hash_encode_fwd");
     return NERF_OK;
 }
@@ -954,6 +1010,12 @@ static int bin_layout(const char* who, int n_levels, int log2_T, int64_t chunk_c
 }
 
 extern "C" int nerf_hash_bwd_chunk_points(void) { return kChunkPts; }
+
+#ifdef NERF_FWD_PROF
+extern "C" int nerf_fwd_prof_read(unsigned long long* host, int n) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(fwd_prof), sizeof(unsigned long long) * (size_t)n);
+}
+#endif
 
 #ifdef NERF_OWNER_PROF
 extern "C" int nerf_owner_prof_read(unsigned long long* host, int n) {
