@@ -219,6 +219,10 @@ static_assert(kChunkPts == 256 || kChunkPts == 512 || kChunkPts == 1024, "chunk 
 #endif
 constexpr bool kOwnerAcc32 = NERF_OWNER_ACC32 != 0;   // fp32 LDS accumulators (ds_add_f32) instead of fp64
 constexpr int kSliceLog2 = NERF_OWNER_SLICE_LOG2;     // owner slice: 2^13 rows x 16 B (fp64 pair) = 128 KiB of LDS
+#ifndef NERF_OWNER_THREADS
+#define NERF_OWNER_THREADS 1024
+#endif
+constexpr int kOwnerThreadsDefault = NERF_OWNER_THREADS;
 constexpr int kSliceLog2Det = 12;         // deterministic: 2^12 rows x 32 B (two int64 words per feature)
 constexpr int kMaxOwnersLog2 = 7;
 constexpr int kMaxOwners = 1 << kMaxOwnersLog2;
@@ -545,7 +549,9 @@ __global__ void __launch_bounds__(THREADS) tv_bwd_bin_kernel(TVParams P, HashGra
 // lane, all lanes busy whatever the segment lengths.
 // SLICE_LOG2 / THREADS: 2^13-row slices with one 1024-thread block per CU (128 KiB of LDS); 2^12-row
 // slices with two 512-thread blocks per CU measured slower (0.41 vs 0.34 ms per backward: the
-// doubled per-owner segment scans outweigh the overlap).
+// doubled per-owner segment scans outweigh the overlap); again in round 5 with the fused table step
+// in the flush (one block's flush beside the other's sums): owner 256.5 -> 269.4 us, bins +3 us
+// (-DNERF_OWNER_SLICE_LOG2=12 -DNERF_OWNER_THREADS=512, profiles/r05r_ab_owner_slice12_rejected.jsonl).
 //
 // DET (deterministic mode): integer accumulation is associative, so the sums do not depend on the
 // order in which waves add entries. Each entry v becomes two int64 fixed-point words at the level's
@@ -1210,8 +1216,8 @@ extern "C" int nerf_hash_encode_bwd_owner_step(int n_levels, int level_begin, in
         hipLaunchKernelGGL((hash_bwd_owner_kernel<kSliceLog2Det, 1024, true>), grid, dim3(1024), 0, as_stream(stream),
                            hp);
     else
-        hipLaunchKernelGGL((hash_bwd_owner_kernel<kSliceLog2, 1024, false>), grid, dim3(1024), 0, as_stream(stream),
-                           hp);
+        hipLaunchKernelGGL((hash_bwd_owner_kernel<kSliceLog2, kOwnerThreadsDefault, false>), grid,
+                           dim3(kOwnerThreadsDefault), 0, as_stream(stream), hp);
     NERF_CHECK_LAUNCH("hash_encode_bwd_owner");
     return NERF_OK;
 }
