@@ -223,6 +223,10 @@ constexpr int kSliceLog2 = NERF_OWNER_SLICE_LOG2;     // owner slice: 2^13 rows 
 #define NERF_OWNER_THREADS 1024
 #endif
 constexpr int kOwnerThreadsDefault = NERF_OWNER_THREADS;
+#ifndef NERF_BIN_NT_STORES
+#define NERF_BIN_NT_STORES 1
+#endif
+
 constexpr int kSliceLog2Det = 12;         // deterministic: 2^12 rows x 32 B (two int64 words per feature)
 constexpr int kMaxOwnersLog2 = 7;
 constexpr int kMaxOwners = 1 << kMaxOwnersLog2;
@@ -318,10 +322,21 @@ __device__ __forceinline__ void bin_chunk(const HashGradParams& hp, int lvl, int
     const uint32_t total = s_start[n_own];
     const size_t base = ((size_t)lvl * hp.chunk_stride + chunk) * kChunkCap;
     // two entries per lane: rows as one dword, (d feat) x 2 as one dwordx4; a trailing odd
-    // slot carries stale LDS bytes that no owner reads (owners read < count per segment)
+    // slot carries stale LDS bytes that no owner reads (owners read < count per segment).
+    // Nontemporal stores: the ~0.5 GB of entries a step writes would otherwise stream through the
+    // 256 MB Infinity Cache and evict the tables and moments (192 MB) the fused table step and the
+    // next forward read: owner 258 -> 239 us, step 1.332 -> 1.311 ms on one box
+    // (profiles/r05t_ab_bin_nt_stores.jsonl). Nontemporal entry LOADS in the owner on top: owner
+    // 236 -> 280 us; nontemporal gradient-row stores in the fused step: +-0 (r05u) — both rejected.
     for (uint32_t i = 2 * threadIdx.x; i < total; i += 2 * THREADS) {
+#if NERF_BIN_NT_STORES
+        __builtin_nontemporal_store(*reinterpret_cast<const uint32_t*>(&s_eh[i]), reinterpret_cast<uint32_t*>(hp.bin_h + base + i));
+        typedef float nt_f4 __attribute__((ext_vector_type(4)));
+        __builtin_nontemporal_store(*reinterpret_cast<const nt_f4*>(&s_eg[i]), reinterpret_cast<nt_f4*>(hp.bin_g + base + i));
+#else
         *reinterpret_cast<uint32_t*>(hp.bin_h + base + i) = *reinterpret_cast<const uint32_t*>(&s_eh[i]);
         *reinterpret_cast<float4*>(hp.bin_g + base + i) = *reinterpret_cast<const float4*>(&s_eg[i]);
+#endif
     }
 }
 
