@@ -248,6 +248,18 @@ struct InX6 {
     bool valid;
 };
 
+// NT: nontemporal loads (the backward's re-read of the features, the last use of the ~100 MB a
+// step's hash forward writes: they no longer displace the tables and moments in the Infinity Cache;
+// with the bins' d feat loads the same way, bins 202 -> 177 us and step 1.216 -> 1.187 ms on one box,
+// profiles/r05v_ab_nt_feature_loads.jsonl)
+#ifndef NERF_X6_BWD_NT_FEAT
+#define NERF_X6_BWD_NT_FEAT 1
+#endif
+#ifndef NERF_X6_NT_DFEAT
+#define NERF_X6_NT_DFEAT 0
+#endif
+typedef float f32x2_nt __attribute__((ext_vector_type(2)));
+template <bool NT = false>
 __device__ __forceinline__ void load_x6(const MlpArgs& a, uint32_t pt, bool valid, int h, float (&x)[16], int zero) {
 #pragma unroll
     for (int c = 0; c < 2; ++c)
@@ -261,9 +273,16 @@ __device__ __forceinline__ void load_x6(const MlpArgs& a, uint32_t pt, bool vali
                 // the backward its upstream gradient is zero, so every weight-gradient term it forms is
                 // 0 x (finite) — no zeroing of the inputs (28 selects per tile) is needed
                 const uint32_t pc = valid ? pt : (uint32_t)(a.P - 1);
-                const float2 v = *reinterpret_cast<const float2*>(a.feat + (uint32_t)(pc * (uint32_t)a.sp + level * (uint32_t)a.sl + zero));
-                x[8 * c + 4 * q + 2 * e] = v.x;
-                x[8 * c + 4 * q + 2 * e + 1] = v.y;
+                const float* src = a.feat + (uint32_t)(pc * (uint32_t)a.sp + level * (uint32_t)a.sl + zero);
+                if constexpr (NT) {
+                    const f32x2_nt v = __builtin_nontemporal_load(reinterpret_cast<const f32x2_nt*>(src));
+                    x[8 * c + 4 * q + 2 * e] = v.x;
+                    x[8 * c + 4 * q + 2 * e + 1] = v.y;
+                } else {
+                    const float2 v = *reinterpret_cast<const float2*>(src);
+                    x[8 * c + 4 * q + 2 * e] = v.x;
+                    x[8 * c + 4 * q + 2 * e + 1] = v.y;
+                }
             }
 }
 
@@ -318,7 +337,7 @@ __device__ __forceinline__ S3 load_sh_split(const MlpArgs& a, uint32_t pt, bool 
 __device__ __forceinline__ void load_in_x6(const MlpArgs& a, int64_t tile, int j, int h, InX6& in) {
     in.pt = (uint32_t)(tile * 32 + j);
     in.valid = tile * 32 + j < a.P;
-    load_x6(a, in.pt, in.valid, h, in.x, 0);
+    load_x6(a, in.pt, in.valid, h, in.x, 0);   // (nontemporal here too: bins +3 us, r05w — rejected)
     in.SH = load_sh_split(a, in.pt, in.valid, h);
 }
 
@@ -345,7 +364,7 @@ __device__ __forceinline__ void bwd_point(const MlpArgs& a, int64_t n, int64_t t
 
 __device__ __forceinline__ void load_in_x6_bwd(const MlpArgs& a, int64_t n, int64_t tile, int j, int h, InX6& in) {
     bwd_point(a, n, tile, j, in.pt, in.valid);
-    load_x6(a, in.pt, in.valid, h, in.x, 0);
+    load_x6<NERF_X6_BWD_NT_FEAT != 0>(a, in.pt, in.valid, h, in.x, 0);
     in.SH = load_sh_split(a, in.pt, in.valid, h);
 }
 
@@ -1055,7 +1074,11 @@ __device__ __forceinline__ void bwd_wgrad_role(const MlpArgs& a, const __bf16* i
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int fi = row_of(r, h);
+#if NERF_X6_NT_DFEAT
+                __builtin_nontemporal_store(gx[r], &a.dfeat[base + (fi >> 1) * sl + (fi & 1)]);
+#else
                 a.dfeat[base + (fi >> 1) * sl + (fi & 1)] = gx[r];
+#endif
             }
         }
     }

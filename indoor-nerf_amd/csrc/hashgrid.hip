@@ -227,6 +227,7 @@ constexpr int kOwnerThreadsDefault = NERF_OWNER_THREADS;
 #define NERF_BIN_NT_STORES 1
 #endif
 
+
 constexpr int kSliceLog2Det = 12;         // deterministic: 2^12 rows x 32 B (two int64 words per feature)
 constexpr int kMaxOwnersLog2 = 7;
 constexpr int kMaxOwners = 1 << kMaxOwnersLog2;
@@ -375,16 +376,19 @@ __device__ __forceinline__ void bwd_bin_block(const float* __restrict__ xyz, int
     if (valid) {
         const int64_t r = br.rows ? (int64_t)br.rows[p] : p;
         x = xyz[3 * r + 0]; y = xyz[3 * r + 1]; z = xyz[3 * r + 2];
+        // d feat is read once: nontemporal loads keep it from displacing the tables and moments in the
+        // Infinity Cache (with the MLP backward's feature loads: bins 202 -> 177 us per step,
+        // profiles/r05v_ab_nt_feature_loads.jsonl)
         if (dfeat) {
             const float* src = dfeat + r * sp + (int64_t)lvl * sl;
-            gx = src[0];
-            gy = src[1];
+            gx = __builtin_nontemporal_load(src);
+            gy = __builtin_nontemporal_load(src + 1);
         }
         if (br.dfeat2) {   // the same point's gradient from a second pass (coarse-feature reuse)
             const int64_t r2 = br.rows2 ? (int64_t)br.rows2[p] : p;
-            const float2 g2 = *reinterpret_cast<const float2*>(br.dfeat2 + r2 * br.sp2 + (int64_t)lvl * br.sl2);
-            gx += g2.x;
-            gy += g2.y;
+            const float* s2 = br.dfeat2 + r2 * br.sp2 + (int64_t)lvl * br.sl2;
+            gx += __builtin_nontemporal_load(s2);
+            gy += __builtin_nontemporal_load(s2 + 1);
         }
     }
     AxisCell ax, ay, az;
