@@ -188,6 +188,21 @@ class _Segments:
         return False
 
 
+class SegmentedGraph:
+    """Graph 1 of a step as its captured segments (_Segments); replay() replays them in order on the
+    current stream (GraphedTrainStep._replay_forward joins pending table gates between them)."""
+
+    def __init__(self, graphs, cuts):
+        self.segments, self.cuts = list(graphs), list(cuts)
+
+    def replay(self):
+        for g in self.segments:
+            g.replay()
+
+    def __len__(self):
+        return len(self.segments)
+
+
 def gate_levels(post_hook):
     """The table levels at which a post hook (dist.ShardedOptimizer.gather_params) leaves gates for the
     next forward; [] for any other hook."""
@@ -292,7 +307,7 @@ class GraphedTrainStep:
         sc.seal()
         emb.current_step = step0
         old = getattr(self, "scalars", None)
-        self.graphs = (seg.graphs, g2)
+        self.graphs = (SegmentedGraph(seg.graphs, seg.cuts), g2)
         self.cuts = seg.cuts
         self.out = out
         self.scalars = sc
@@ -317,7 +332,7 @@ class GraphedTrainStep:
         the last one everything."""
         from . import hashgrid
         dev = self.target.device
-        segs, gates = self.graphs[0], hashgrid.take_gates(self.target.device)
+        segs, gates = self.graphs[0].segments, hashgrid.take_gates(self.target.device)
         ends = list(self.cuts) + [float("inf")]
         stream = torch.cuda.current_stream(dev)
         for k, g in enumerate(segs):

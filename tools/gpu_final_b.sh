@@ -1,12 +1,11 @@
-# Final GPU pass of a round: GPU suite, smoke(), the default bench line (with the CPU baseline), the
+# Final GPU pass, measurement half (the suite, smoke() and the convergence replays run in
+# tools/gpu_milestone_a.sh): the default bench line (with the CPU baseline and the fresh-ray leg), the
 # other workloads and the deterministic lego line, rocprofv3 kernel stats + PMC traffic + SQ counters.
-# usage: bash tools/gpu_final.sh TAG   (outputs under gpurun_out/TAG/, prof_TAG/, sq_TAG/)
+# usage: bash tools/gpu_final_b.sh TAG   (outputs under gpurun_out/TAG/, prof_TAG/, sq_TAG/)
 set -o pipefail
 TAG=${1:-final}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > $OUT/gpu_tests.log 2>&1 || exit 1
-timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $OUT/smoke.log 2>&1 || exit 2
 timeout -k 10 700 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err || exit 3
 for wl in fern acaq scannet; do
   timeout -k 10 200 python -u bench.py --workload $wl --no-cpu-baseline > $OUT/bench_$wl.json 2> $OUT/bench_$wl.err || exit 4
