@@ -115,7 +115,7 @@ def base_name(abi_name):
 
 def traffic_file():
     """The newest committed PMC traffic summary (tools/profile_bench.sh), or None."""
-    for name in ("r04_traffic.json", "r03_traffic.json", "r02_traffic.json", "r01j_traffic.json"):
+    for name in ("r05_traffic.json", "r04_traffic.json", "r03_traffic.json", "r02_traffic.json", "r01j_traffic.json"):
         path = os.path.join(ROOT, "profiles", name)
         if os.path.exists(path):
             return path
