@@ -454,6 +454,9 @@ def fresh_rays_leg(a, kw, opt, args, arena, hook, post, world, dev, it, rank):
     for _ in range(a.steps):
         st(it)
         it += 1
+    wait = getattr(getattr(post, "__self__", None), "wait_params", None)
+    if wait is not None:
+        wait()                             # the last step's gated all-gather (ZeRO-1 with overlap)
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()

@@ -153,6 +153,12 @@ class StepScalars:
         self.issued = n + 1
 
 
+# "thread_local": only the capturing thread's unsafe calls (allocations, synchronisations) invalidate the
+# capture. With the nccl (RCCL) process group a watchdog thread queries its collectives' events while
+# a step is captured; the process-wide "global" mode would count those queries against the capture.
+CAPTURE_MODE = "thread_local"
+
+
 class _Segments:
     """Capture of one graph as a list of graphs cut at chosen points (split()): each segment is its own
     CUDAGraph on the same memory pool and capture stream, replayed in order with host work (event
@@ -165,7 +171,7 @@ class _Segments:
 
     def _begin(self):
         g = torch.cuda.CUDAGraph()
-        g.capture_begin(self.pool, capture_error_mode="global")
+        g.capture_begin(self.pool, capture_error_mode=CAPTURE_MODE)
         self.graphs.append(g)
 
     def split(self, level):
@@ -301,7 +307,7 @@ class GraphedTrainStep:
                 finally:
                     hashgrid.split_next_forward(dev, None, None)
                 if not single:
-                    with torch.cuda.graph(g2, pool=pool, stream=side):
+                    with torch.cuda.graph(g2, pool=pool, stream=side, capture_error_mode=CAPTURE_MODE):
                         optimizer_update(self.opt)
         torch.cuda.current_stream(dev).wait_stream(side)
         sc.seal()
