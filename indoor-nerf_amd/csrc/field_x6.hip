@@ -139,22 +139,36 @@ __device__ __forceinline__ float image_value(int idx, const nerf_mlp_weights& W)
     return (k >> 6) < 3 ? W.c2[k] : 0.f;
 }
 
+// Every block's prologue. The loads of a round (kFillRound per thread) are issued before the first
+// split / store: one memory round trip per round instead of one per element (a thread of a 512-wide
+// block has 20 elements; one at a time, their L2 latencies were serial).
+constexpr int kFillRound = 10;
 __device__ inline void fill_images(__bf16* img, const nerf_mlp_weights& W) {
-    for (int idx = threadIdx.x; idx < L_END; idx += blockDim.x) {
-        int off;
-        if (idx < L_W1) off = IM_W0 + (idx >> 5) * S32 + (idx & 31);
-        else if (idx < L_C0) { const int k = idx - L_W1; off = IM_W1 + (k >> 6) * S64 + (k & 63); }
-        else if (idx < L_C1) { const int k = idx - L_C0; off = IM_C0 + (k >> 5) * S32 + (k & 31); }
-        else if (idx < L_C2) { const int k = idx - L_C1; off = IM_C1 + (k >> 6) * S64 + (k & 63); }
-        else { const int k = idx - L_C2; off = IM_C2 + (k >> 6) * S64 + (k & 63); }
-        const float v = image_value(idx, W);
-        const __bf16 a0 = (__bf16)v;
-        const float r1 = v - (float)a0;
-        const __bf16 a1 = (__bf16)r1;
-        const __bf16 a2 = (__bf16)(r1 - (float)a1);
-        img[off] = a0;
-        img[IM_PIECE + off] = a1;
-        img[2 * IM_PIECE + off] = a2;
+    for (int base = threadIdx.x; base < L_END; base += kFillRound * blockDim.x) {
+        float v[kFillRound];
+#pragma unroll
+        for (int u = 0; u < kFillRound; ++u) {
+            const int idx = base + u * (int)blockDim.x;
+            v[u] = idx < L_END ? image_value(idx, W) : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < kFillRound; ++u) {
+            const int idx = base + u * (int)blockDim.x;
+            if (idx >= L_END) continue;
+            int off;
+            if (idx < L_W1) off = IM_W0 + (idx >> 5) * S32 + (idx & 31);
+            else if (idx < L_C0) { const int k = idx - L_W1; off = IM_W1 + (k >> 6) * S64 + (k & 63); }
+            else if (idx < L_C1) { const int k = idx - L_C0; off = IM_C0 + (k >> 5) * S32 + (k & 31); }
+            else if (idx < L_C2) { const int k = idx - L_C1; off = IM_C1 + (k >> 6) * S64 + (k & 63); }
+            else { const int k = idx - L_C2; off = IM_C2 + (k >> 6) * S64 + (k & 63); }
+            const __bf16 a0 = (__bf16)v[u];
+            const float r1 = v[u] - (float)a0;
+            const __bf16 a1 = (__bf16)r1;
+            const __bf16 a2 = (__bf16)(r1 - (float)a1);
+            img[off] = a0;
+            img[IM_PIECE + off] = a1;
+            img[2 * IM_PIECE + off] = a2;
+        }
     }
 }
 

@@ -228,6 +228,7 @@ constexpr int kOwnerThreadsDefault = NERF_OWNER_THREADS;
 #endif
 
 
+
 constexpr int kSliceLog2Det = 12;         // deterministic: 2^12 rows x 32 B (two int64 words per feature)
 constexpr int kMaxOwnersLog2 = 7;
 constexpr int kMaxOwners = 1 << kMaxOwnersLog2;
@@ -620,7 +621,9 @@ __global__ void __launch_bounds__(THREADS) hash_bwd_owner_kernel(HashGradParams 
     // (makespan 244 us vs 202 us of block time per CU); interleaved, light blocks fill in behind the
     // heavy ones (235 us; owner launch 255 -> 248 us on one box, profiles/r03i_ab_owner_order.jsonl).
     // Finest first alone is slower (273 us): the coarse pass's bins, written last, are partly still
-    // in the Infinity Cache when the early blocks read them.
+    // in the Infinity Cache when the early blocks read them. Re-measured in round 5 with the entries
+    // stored nontemporally (no bins in the Infinity Cache) as a longest-first order: 234.7 -> 249.9 us
+    // (profiles/r05ac_ab_fill_prologue_owner_lpt.jsonl) — the interleaving stays.
     const int o = blockIdx.x, y = blockIdx.y;
     const int lvl = hp.level0 + ((y & 1) ? (y >> 1) : (int)gridDim.y - 1 - (y >> 1));
     const int S = 1 << hp.slice_log2, n_own = 1 << hp.owner_log2;

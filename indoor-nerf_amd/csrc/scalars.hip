@@ -23,10 +23,11 @@ __global__ void __launch_bounds__(256) scalars_fetch_kernel(const uint32_t* ring
     const int64_t na = ctl[1], b0 = ctl[2], nb = ctl[3];
     const uint32_t* src = ring + (c % n_slots) * slot_words;
     if (done && threadIdx.x == 0) {
+        // both host words in one round trip (the error word is read whether or not the tag matches)
         const int64_t tag = __hip_atomic_load(reinterpret_cast<const int64_t*>(src + slot_words - 2), __ATOMIC_RELAXED,
                                               __HIP_MEMORY_SCOPE_SYSTEM);
-        if (tag != c && __hip_atomic_load(done + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0)
-            __hip_atomic_store(done + 1, c + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        const int64_t err = __hip_atomic_load(done + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (tag != c && err == 0) __hip_atomic_store(done + 1, c + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     for (int64_t i = threadIdx.x; i < na + nb; i += blockDim.x) {
         const int64_t w = i < na ? i : b0 + (i - na);
