@@ -269,6 +269,9 @@ struct InX6 {
 #ifndef NERF_X6_BWD_NT_FEAT
 #define NERF_X6_BWD_NT_FEAT 1
 #endif
+#ifndef NERF_X6_BWD_PREFETCH
+#define NERF_X6_BWD_PREFETCH 1
+#endif
 typedef float f32x2_nt __attribute__((ext_vector_type(2)));
 template <bool NT = false>
 __device__ __forceinline__ void load_x6(const MlpArgs& a, uint32_t pt, bool valid, int h, float (&x)[16], int zero) {
@@ -716,10 +719,20 @@ __device__ __forceinline__ void bwd_chain_role(const MlpArgs& a, const __bf16* i
     auto publish = [&]() { flag_set(ready, ++seq); };
     const int64_t n_pts = bwd_points(a);
     const int64_t n_tiles = (n_pts + 31) / 32;
+#if NERF_X6_BWD_PREFETCH
+    // the next tile's inputs are loaded after stage 5 (the forward state is dead by then) and are in
+    // flight during stages 6 and 7 instead of stalling the next tile's forward recompute
+    InX6 in_next;
+    if ((int64_t)blk * 4 + p < n_tiles) load_in_x6_bwd(a, n_pts, (int64_t)blk * 4 + p, j, h, in_next);
+#endif
     for (int64_t tile = (int64_t)blk * 4 + p; tile < n_tiles; tile += (int64_t)nblk * 4) {
         const __bf16* imt = img + opaque_zero();
+#if NERF_X6_BWD_PREFETCH
+        InX6 in = in_next;
+#else
         InX6 in;
         load_in_x6_bwd(a, n_pts, tile, j, h, in);
+#endif
         ActX6 f;
         fwd_chain<QUANT>(imt, in, f, lane, aq);
 
@@ -817,6 +830,9 @@ __device__ __forceinline__ void bwd_chain_role(const MlpArgs& a, const __bf16* i
             for (int r = 8; r < 16; ++r) a.dsh[16u * orow + row_of(r, h) - 16] = go[r];
         }
 
+#if NERF_X6_BWD_PREFETCH
+        if (tile + (int64_t)nblk * 4 < n_tiles) load_in_x6_bwd(a, n_pts, tile + (int64_t)nblk * 4, j, h, in_next);
+#endif
         // stage 6 (dW1): go, h1 (held in registers since the forward recompute; with QUANT recomputed
         // from x's pieces) and layer 0's ReLU mask m1 (with QUANT: before the activation quantizer)
         // in the unused columns 16.. of the gradient tile.
