@@ -599,6 +599,8 @@ __global__ void __launch_bounds__(THREADS) hash_bwd_owner_kernel(HashGradParams 
 #define NERF_OWNER_BATCH 8
 #endif
     constexpr int NB = NERF_OWNER_BATCH;                   // steps per software-pipelined batch
+                                                           // (12: owner 234 -> 241 us; 16: 271 us with
+                                                           // spills; profiles/r05af_ab_owner_batch_rejected.jsonl)
     constexpr int kScanPer = 4;                            // chunks per thread in the window scan
     constexpr int kOwnerWindow = kScanPer * THREADS;       // chunks per window (the fine + coarse + TV
                                                            // chunks of a 4096-ray step fit one window)
