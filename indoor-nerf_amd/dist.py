@@ -165,7 +165,7 @@ def _all_gather_begin(out, inp, group, stream):
         h = torch.empty(out.shape, dtype=out.dtype)
         work = dist.all_gather_into_tensor(h, h_in, group=group, async_op=True)
 
-        def finish():
+        def finish(keep=(h_in, h)):   # the collective's host buffers live until it has completed
             work.wait()
             with torch.cuda.stream(stream):
                 out.copy_(h)
