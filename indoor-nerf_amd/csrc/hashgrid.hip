@@ -56,6 +56,15 @@ struct HashGradParams {
 // g(i) gives row i's gradient, which is stored to dt[i] (overwrite mode) and then updates the row's
 // parameters and moments. A batch's parameter / moment loads are issued before its first gradient, so
 // they are in flight while the gradients are formed and stored.
+// A row that never received a gradient (its moments are +0) and gets none now: without weight decay
+// RAdam leaves its parameter and moments bit for bit as they are (+0 * beta + (+0 * g) * g = +0, and
+// p + (c * +0) / (sqrt(+0) + eps) = p), so only its gradient row is stored. Most rows of the coarse
+// levels' 2^19-row tables are never hashed to: the table step skips their 24 B of writes.
+__device__ __forceinline__ bool radam_idle(const nerf_radam_segment& s, float2 g, float2 m, float2 v) {
+    return s.decay_coef == 0.f && (__float_as_uint(g.x) | __float_as_uint(g.y) | __float_as_uint(m.x) |
+                                   __float_as_uint(m.y) | __float_as_uint(v.x) | __float_as_uint(v.y)) == 0u;
+}
+
 template <int THREADS, int ROWS, typename G>
 __device__ __forceinline__ void owner_table_step(const HashGradParams& hp, int lvl, size_t row0, int S, float2* dt,
                                                  G g) {
@@ -81,6 +90,7 @@ __device__ __forceinline__ void owner_table_step(const HashGradParams& hp, int l
             if (i >= S) continue;
             const float2 gi = g(i);
             dt[i] = gi;
+            if (radam_idle(s, gi, m[k], v[k])) continue;
             radam_elem(s, p[k].x, gi.x, m[k].x, v[k].x);
             radam_elem(s, p[k].y, gi.y, m[k].y, v[k].y);
             M[i] = m[k];
@@ -865,6 +875,7 @@ __global__ void __launch_bounds__(THREADS) hash_bwd_owner_kernel(HashGradParams 
                 const Acc v{s_ax[i], s_ay[i]};
                 const float2 g = make_float2((float)v.x, (float)v.y);
                 dt[i] = g;
+                if (radam_idle(s, g, pm[k], pv[k])) continue;
                 radam_elem(s, pp[k].x, g.x, pm[k].x, pv[k].x);
                 radam_elem(s, pp[k].y, g.y, pm[k].y, pv[k].y);
                 M[i] = pm[k];
