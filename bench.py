@@ -215,8 +215,11 @@ def op_rooflines(kernels, steps, units, dense_elems, hash_entries=None, fused_el
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=8)
+    # steady state: after the warm-up's capture and the barrier, the replayed step settles over ~20
+    # iterations (1.217 / 1.214 ms averaged over 20 timed steps after 8 warm-ups vs 1.192 / 1.195 ms
+    # over 60 after 40 and 1.191 / 1.195 ms over 100 after 8, same box, profiles/r05ap_bench_warmup_length.jsonl)
+    ap.add_argument("--steps", type=int, default=60)
+    ap.add_argument("--warmup", type=int, default=40)
     ap.add_argument("--rays", type=int, default=4096)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-rays", type=int, default=4096, help="rays of the CPU leg's timed iterations (the bench batch)")
