@@ -1,0 +1,78 @@
+#!/usr/bin/env python3
+"""Where the deterministic two-rank rehearsal stops being reproducible (tools/det_repro.py found its
+one-iteration all-reduced table gradients differ run to run): part (a) of tests/test_gpu_dist.py's
+_dp_worker only, deterministic mode, each rank's gradients saved BEFORE and AFTER the gloo all-reduce;
+two runs with both ranks computing at once on the one GPU and two with the ranks taking turns
+(barrier-separated). Per rank and parameter: elements that differ between the two runs. JSON: argv[1]."""
+import json
+import os
+import sys
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402
+import torch.multiprocessing as mp  # noqa: E402
+
+import test_gpu_dist as t  # noqa: E402
+
+
+def _worker(rank, world, port, out, R, serial):
+    t._init(rank, world, port)
+    import importlib
+    import indoor_nerf_amd as nerf
+    nerf.set_deterministic(True)
+    from indoor_nerf_amd.model import forward_backward
+    rmod = importlib.import_module("indoor_nerf_amd.render")
+    from tables import synthetic_rays
+    dev = torch.device("cuda:0")
+    rmod.pytest_shard(rank, world)
+    ro, rd = synthetic_rays(R, seed=21)
+    target = torch.rand(R, 3, generator=torch.Generator().manual_seed(5))
+    n = R // world
+    rays = (torch.from_numpy(ro[rank * n:(rank + 1) * n]).to(dev), torch.from_numpy(rd[rank * n:(rank + 1) * n]).to(dev))
+    tgt = target[rank * n:(rank + 1) * n].to(dev)
+    args, kw, opt, params = t._f10_model(nerf, dev, world)
+    arena = nerf.GradArena(params, defer_tables=True)
+
+    def fb():
+        forward_backward(rays, tgt, kw, opt, args, 1, loss_scale_sparsity=float(world),
+                         tv_generator=torch.Generator().manual_seed(7), zero_grad=arena.zero_)
+        torch.cuda.synchronize()
+
+    torch.distributed.barrier()
+    for r in range(world):
+        if r == rank or not serial:
+            if r == rank:
+                fb()
+        if serial:
+            torch.distributed.barrier()
+    if not serial:
+        torch.distributed.barrier()
+    pre = [p.grad.detach().cpu().clone() for p in params]
+    arena.allreduce_mean()
+    torch.cuda.synchronize()
+    post = [p.grad.detach().cpu().clone() for p in params]
+    torch.save({"pre": pre, "post": post}, os.path.join(out, f"a_{rank}.pt"))
+    torch.distributed.destroy_process_group()
+
+
+def main():
+    res = {}
+    for serial in (False, True):
+        runs = []
+        for k in range(2):
+            d = tempfile.mkdtemp()
+            mp.start_processes(_worker, args=(2, t._free_port(), d, 4096, serial), nprocs=2, join=True,
+                               start_method="spawn")
+            runs.append([torch.load(os.path.join(d, f"a_{r}.pt"), weights_only=True) for r in range(2)])
+        tag = "serial" if serial else "concurrent"
+        res[tag] = {f"rank{r}_{w}": [int((x != y).sum()) for x, y in zip(runs[0][r][w], runs[1][r][w])]
+                    for r in range(2) for w in ("pre", "post")}
+        print(tag, json.dumps(res[tag]), flush=True)
+    json.dump(res, open(sys.argv[1], "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
