@@ -3,7 +3,8 @@
 one-iteration all-reduced table gradients differ run to run): part (a) of tests/test_gpu_dist.py's
 _dp_worker only, deterministic mode, each rank's gradients saved BEFORE and AFTER the gloo all-reduce;
 two runs with both ranks computing at once on the one GPU and two with the ranks taking turns
-(barrier-separated). Per rank and parameter: elements that differ between the two runs. JSON: argv[1]."""
+(barrier-separated), and twice two runs exactly as _dp_worker's part (a) ("nosync": no device sync or
+barrier between the backward and the all-reduce; "pre" = stream-ordered device copies). Per rank and parameter: elements that differ between the two runs. JSON: argv[1]."""
 import json
 import os
 import sys
@@ -41,6 +42,16 @@ def _worker(rank, world, port, out, R, serial):
                          tv_generator=torch.Generator().manual_seed(7), zero_grad=arena.zero_)
         torch.cuda.synchronize()
 
+    if serial == "nosync":   # exactly as _dp_worker: no device sync or barrier between the backward and the
+        forward_backward(rays, tgt, kw, opt, args, 1, loss_scale_sparsity=float(world),   # all-reduce
+                         tv_generator=torch.Generator().manual_seed(7), zero_grad=arena.zero_)
+        pre = [p.grad.detach().clone() for p in params]   # stream-ordered device copies
+        arena.allreduce_mean()
+        torch.cuda.synchronize()
+        torch.save({"pre": [x.cpu() for x in pre], "post": [p.grad.detach().cpu().clone() for p in params]},
+                   os.path.join(out, f"a_{rank}.pt"))
+        torch.distributed.destroy_process_group()
+        return
     torch.distributed.barrier()
     for r in range(world):
         if r == rank or not serial:
@@ -60,14 +71,15 @@ def _worker(rank, world, port, out, R, serial):
 
 def main():
     res = {}
-    for serial in (False, True):
+    for serial in ("nosync", False, "nosync", True):
         runs = []
         for k in range(2):
             d = tempfile.mkdtemp()
             mp.start_processes(_worker, args=(2, t._free_port(), d, 4096, serial), nprocs=2, join=True,
                                start_method="spawn")
             runs.append([torch.load(os.path.join(d, f"a_{r}.pt"), weights_only=True) for r in range(2)])
-        tag = "serial" if serial else "concurrent"
+        tag = {"nosync": "nosync", False: "concurrent", True: "serial"}[serial]
+        tag = tag + ("_b" if tag in res else "")
         res[tag] = {f"rank{r}_{w}": [int((x != y).sum()) for x, y in zip(runs[0][r][w], runs[1][r][w])]
                     for r in range(2) for w in ("pre", "post")}
         print(tag, json.dumps(res[tag]), flush=True)
