@@ -4,7 +4,8 @@ one-iteration all-reduced table gradients differ run to run): part (a) of tests/
 _dp_worker only, deterministic mode, each rank's gradients saved BEFORE and AFTER the gloo all-reduce;
 two runs with both ranks computing at once on the one GPU and two with the ranks taking turns
 (barrier-separated), and twice two runs exactly as _dp_worker's part (a) ("nosync": no device sync or
-barrier between the backward and the all-reduce; "pre" = stream-ordered device copies). Per rank and parameter: elements that differ between the two runs. JSON: argv[1]."""
+barrier between the backward and the all-reduce; "pre" = stream-ordered device copies). --garbage: two
+synchronised runs whose caching allocators start filled with different seeded random values. Per rank and parameter: elements that differ between the two runs. JSON: argv[1]."""
 import json
 import os
 import sys
@@ -19,8 +20,13 @@ import torch.multiprocessing as mp  # noqa: E402
 import test_gpu_dist as t  # noqa: E402
 
 
-def _worker(rank, world, port, out, R, serial):
+def _worker(rank, world, port, out, R, serial, garbage=None):
     t._init(rank, world, port)
+    if garbage is not None:   # leave seeded random bytes in the caching allocator's blocks: a read of
+        g = torch.Generator(device="cuda:0").manual_seed(garbage)   # memory no kernel wrote shows up
+        x = torch.empty(1 << 31, device="cuda:0")                   # as a run-to-run difference
+        x.uniform_(-1e3, 1e3, generator=g)
+        del x
     import importlib
     import indoor_nerf_amd as nerf
     nerf.set_deterministic(True)
@@ -71,14 +77,16 @@ def _worker(rank, world, port, out, R, serial):
 
 def main():
     res = {}
-    for serial in ("nosync", False, "nosync", True):
+    modes = ("garbage",) if "--garbage" in sys.argv else ("nosync", False, "nosync", True)
+    for serial in modes:
         runs = []
         for k in range(2):
             d = tempfile.mkdtemp()
-            mp.start_processes(_worker, args=(2, t._free_port(), d, 4096, serial), nprocs=2, join=True,
-                               start_method="spawn")
+            gb = (11 + k) if serial == "garbage" else None
+            mp.start_processes(_worker, args=(2, t._free_port(), d, 4096, False if gb else serial, gb), nprocs=2,
+                               join=True, start_method="spawn")
             runs.append([torch.load(os.path.join(d, f"a_{r}.pt"), weights_only=True) for r in range(2)])
-        tag = {"nosync": "nosync", False: "concurrent", True: "serial"}[serial]
+        tag = {"nosync": "nosync", False: "concurrent", True: "serial", "garbage": "garbage_synced"}[serial]
         tag = tag + ("_b" if tag in res else "")
         res[tag] = {f"rank{r}_{w}": [int((x != y).sum()) for x, y in zip(runs[0][r][w], runs[1][r][w])]
                     for r in range(2) for w in ("pre", "post")}
