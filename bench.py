@@ -333,12 +333,19 @@ def cpu_model():
 
 
 def cpu_threads():
-    """Threads for the CPU leg: every core of this process's affinity mask, capped by the job's CPU
-    share (OMP_NUM_THREADS: 16 per GPU on the pool's boxes, whose affinity mask shows the whole
-    machine; unset here: the mask alone)."""
-    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    """Threads for the CPU legs: (logical CPUs of this process's affinity mask, the job's CPU share
+    (OMP_NUM_THREADS: 16 per GPU on the pool's boxes, whose affinity mask shows the whole machine;
+    unset here: the mask alone), physical cores of the mask (all physical cores))."""
+    cpus = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else list(range(os.cpu_count()))
     share = os.environ.get("OMP_NUM_THREADS")
-    return cores, max(1, min(cores, int(share))) if share else cores
+    physical = set()
+    for c in cpus:
+        base = f"/sys/devices/system/cpu/cpu{c}/topology/"
+        try:
+            physical.add((open(base + "physical_package_id").read().strip(), open(base + "core_id").read().strip()))
+        except OSError:
+            physical.add(("cpu", str(c)))
+    return len(cpus), max(1, min(len(cpus), int(share))) if share else len(cpus), max(1, len(physical))
 
 
 def cpu_leg(n_rays, finest, H, warmup, timed):
@@ -405,17 +412,26 @@ def cpu_baseline(n_rays, warmup, timed):
     the median of `timed` (3). The same leg at 1024 rays is reported beside it, so the batch-size
     effect is measured, and the chair leg is BASELINE configs[0] (chair 400x400,
     finest_res 512, the reference's CPU path: configs/chair.txt) at its own N_rand of 1024."""
-    cores, threads = cpu_threads()
-    torch.set_num_threads(threads)
+    logical, share, physical = cpu_threads()
+    # SURVEY §8(d): every physical core of the affinity mask (the pool's boxes show the whole machine in
+    # the mask; the job's share, OMP_NUM_THREADS, is reported beside it)
+    torch.set_num_threads(physical)
     lego = cpu_leg(n_rays, 1024, 800, warmup, timed)
-    lego_1k = cpu_leg(1024, 1024, 800, warmup, timed)
+    shared = None
+    if share < physical:
+        torch.set_num_threads(share)
+        shared = cpu_leg(n_rays, 1024, 800, warmup, timed)
+        shared["threads"] = share
+    torch.set_num_threads(min(physical, share))
     chair = cpu_leg(1024, 512, 400, warmup, timed)
-    return {"value": lego["value"], "unit": "rays/s", "cores": threads, "kind": "port",
+    chair["threads"] = min(physical, share)
+    return {"value": lego["value"], "unit": "rays/s", "cores": physical, "kind": "port",
             "render_only": lego["render_only"], "step_s": lego["step_s"],
             "sample": "lego leg: " + lego["sample"],
-            "cpu": cpu_model(), "affinity_cores": cores,
-            "threads_note": "torch.set_num_threads = the job's CPU share (OMP_NUM_THREADS) within the affinity mask",
-            "lego_1024_rays": lego_1k,
+            "cpu": cpu_model(), "affinity_cpus": logical, "physical_cores": physical, "job_share_threads": share,
+            "threads_note": "torch.set_num_threads = the physical cores of the affinity mask (SURVEY.md §8(d)); "
+                            "job_share_leg: the same leg at the job's CPU share (OMP_NUM_THREADS)",
+            "job_share_leg": shared,
             "chair": {**chair, "config": "BASELINE configs[0]: chair 400x400, finest_res 512 (configs/chair.txt)"}}
 
 
@@ -634,6 +650,8 @@ def main():
     if world > 1:
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
+    if gstep is not None:
+        gstep.check()              # every replay fetched its own scalar slot (outside the timed region)
     clocks = gpu_clocks() if rank == 0 else None
     recs = _lib.timing_records()
     _lib.set_timing(False)

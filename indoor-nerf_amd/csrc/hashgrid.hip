@@ -60,8 +60,11 @@ struct HashGradParams {
 // RAdam leaves its parameter and moments bit for bit as they are (+0 * beta + (+0 * g) * g = +0, and
 // p + (c * +0) / (sqrt(+0) + eps) = p), so only its gradient row is stored. Most rows of the coarse
 // levels' 2^19-row tables are never hashed to: the table step skips their 24 B of writes.
+// With eps == 0 the adaptive step of such a row is (c * 0) / (sqrt(0) + 0) = NaN in the reference
+// (radam.py:85), so mode 2 with eps == 0 takes the full update.
 __device__ __forceinline__ bool radam_idle(const nerf_radam_segment& s, float2 g, float2 m, float2 v) {
-    return s.decay_coef == 0.f && (__float_as_uint(g.x) | __float_as_uint(g.y) | __float_as_uint(m.x) |
+    return s.decay_coef == 0.f && (s.mode != 2 || s.eps > 0.f) &&
+           (__float_as_uint(g.x) | __float_as_uint(g.y) | __float_as_uint(m.x) |
                                    __float_as_uint(m.y) | __float_as_uint(v.x) | __float_as_uint(v.y)) == 0u;
 }
 
@@ -999,18 +1002,31 @@ extern "C" int nerf_hash_encode_fwd_q(const float* d_xyz, int64_t n_points, cons
         ++group;
     }
     if (group < 2) group = 0;
-    const unsigned gx0 = group > 0 ? (unsigned)blocks_for(2 * n_points, 256) : 0u;
-    const unsigned gx1 = (unsigned)blocks_for(2 * n_points, 256 * kFwdRowPts);
-    const size_t nblk = (size_t)gx0 + (size_t)gx1 * (size_t)(n_levels - (group > 0 ? group : 0));
-    NERF_REQUIRE(nblk < (1ull << 31), "hash_encode_fwd: %lld points", (long long)n_points);
-    const dim3 grid((unsigned)nblk);
-    if (q)
-        hipLaunchKernelGGL(hash_encode_fwd_pair_kernel<true>, grid, dim3(256), 0, as_stream(stream), d_xyz,
-                           n_points, hp, group, gx0, gx1, d_feat, feat_stride_point, feat_stride_level, d_keep, q);
-    else
-        hipLaunchKernelGGL(hash_encode_fwd_pair_kernel<false>, grid, dim3(256), 0, as_stream(stream), d_xyz,
-                           n_points, hp, group, gx0, gx1, d_feat, feat_stride_point, feat_stride_level, d_keep, q);
-    NERF_CHECK_LAUNCH("hash_encode_fwd");
+    // one-dimensional grid over every level row: gridDim.x * 256 work-items must stay below 2^32, so a
+    // call of more points than one launch holds runs as consecutive point ranges (rows stay
+    // level-major inside each)
+    auto blocks = [&](int64_t n, unsigned& gx0, unsigned& gx1) {
+        gx0 = group > 0 ? (unsigned)blocks_for(2 * n, 256) : 0u;
+        gx1 = (unsigned)blocks_for(2 * n, 256 * kFwdRowPts);
+        return (uint64_t)gx0 + (uint64_t)gx1 * (uint64_t)(n_levels - (group > 0 ? group : 0));
+    };
+    constexpr uint64_t kMaxBlocks = 0xFFFFFFFFull / 256;
+    int64_t span = n_points;
+    unsigned gx0, gx1;
+    while (blocks(span, gx0, gx1) > kMaxBlocks) span = ((span / 2) + 255) & ~(int64_t)255;
+    for (int64_t p0 = 0; p0 < n_points; p0 += span) {
+        const int64_t n = std::min(span, n_points - p0);
+        const dim3 grid((unsigned)blocks(n, gx0, gx1));
+        uint8_t* kp = d_keep ? d_keep + p0 : nullptr;
+        float* fp = d_feat + p0 * feat_stride_point;
+        if (q)
+            hipLaunchKernelGGL(hash_encode_fwd_pair_kernel<true>, grid, dim3(256), 0, as_stream(stream), d_xyz + 3 * p0,
+                               n, hp, group, gx0, gx1, fp, feat_stride_point, feat_stride_level, kp, q);
+        else
+            hipLaunchKernelGGL(hash_encode_fwd_pair_kernel<false>, grid, dim3(256), 0, as_stream(stream), d_xyz + 3 * p0,
+                               n, hp, group, gx0, gx1, fp, feat_stride_point, feat_stride_level, kp, q);
+        NERF_CHECK_LAUNCH("hash_encode_fwd");
+    }
     return NERF_OK;
 }
 

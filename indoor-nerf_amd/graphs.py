@@ -347,6 +347,17 @@ class GraphedTrainStep:
                 gate.join(stream)
             g.replay()
 
+    def check(self):
+        """A host sync point's check of the captured step's scalar ring (StepScalars.check): upload()
+        checks before every replay, so a replay that fetched another replay's slot is otherwise seen
+        only at the next upload — never after a run's final replay. Call it where the host waits for
+        the device anyway (end of training, checkpoint save; bench.py after its timed region). When it
+        raises, the flagged replay (and possibly the one after it) has already trained on that slot."""
+        sc = getattr(self, "scalars", None)
+        if sc is not None:
+            torch.cuda.synchronize(self.target.device)
+            sc.check()
+
     def _priors_active(self, global_step):
         from .model import DEFAULTS
         get = lambda k: getattr(self.args, k, DEFAULTS.get(k))  # noqa: E731
