@@ -26,8 +26,25 @@ def _free_port():
     return port
 
 
+# Each rank of a rehearsal runs on its own half of the GPU's compute units (HSA_CU_MASK, read when the
+# process opens its HSA queues: set before any HIP call). On a node each rank owns a GPU; two processes
+# whose waves share CUs of ONE MI355X were measured to lose loaded values now and then: in 9 of 24
+# two-rank runs one of the hash bin launches produced entries that a re-launch on unchanged inputs
+# (device-synchronised) did not reproduce — a wave's first dword of a d-feat load read as its
+# initial 0 — and never with disjoint CU sets (0 of 24 runs, 576 re-launches) or with one process,
+# alone or beside an unrelated GPU process (tools/det_repro_d.py, profiles/r06_det_cu_split.txt).
+MI355X_CUS = int(os.environ.get("NERF_TEST_CUS", "256"))
+
+
+def _cu_mask(rank, world):
+    if world > 1 and "HSA_CU_MASK" not in os.environ:
+        n = MI355X_CUS // world
+        os.environ["HSA_CU_MASK"] = f"0:{rank * n}-{rank * n + n - 1}"
+
+
 def _init(rank, world, port):
     import sys
+    _cu_mask(rank, world)
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     for p in (root, os.path.join(root, "tests", "golden")):
         if p not in sys.path:
@@ -146,33 +163,30 @@ def test_sharded_graphed_training_replicas_agree(tmp_path, overlap):
 def _gather_worker(rank, world, port, out):
     """ZeRO-1 with two buckets (MLP + levels 0-7 | levels 8-15), deterministic mode, 5 iterations, four
     ways: eager / graphed x all-gather in stream order (overlap_gather=False) / gated (the levels 8-15
-    bucket all-gathered on the side stream, joined by the next forward between its level ranges)."""
+    bucket all-gathered on the side stream, joined by the next forward between its level ranges). The
+    DP test's size: F10's trained-like state, each rank its half of a 4,096-ray batch."""
     _init(rank, world, port)
     import indoor_nerf_amd as nerf
     from indoor_nerf_amd import hashgrid
     from indoor_nerf_amd.graphs import GraphedTrainStep
-    from tables import blender_bbox, synthetic_rays
+    from tables import synthetic_rays
     nerf.set_deterministic(True)
     dev = torch.device("cuda:0")
-    lo, hi = blender_bbox()
+    R = 4096
+    n = R // world
+    ro, rd = synthetic_rays(R, seed=21)
+    rays = (torch.from_numpy(ro[rank * n:(rank + 1) * n]).to(dev), torch.from_numpy(rd[rank * n:(rank + 1) * n]).to(dev))
+    target = torch.rand(R, 3, generator=torch.Generator().manual_seed(5))[rank * n:(rank + 1) * n].to(dev)
     res = {}
     for graphed in (False, True):
         for gated in (False, True):
-            args = nerf.make_args(bounding_box=(torch.from_numpy(lo), torch.from_numpy(hi)), finest_res=1024,
-                                  N_samples=64, N_importance=128, white_bkgd=True, perturb=1.0, tv_loss_weight=1e-6)
-            torch.manual_seed(rank)
+            args, kw, opt, params = _f10_model(nerf, dev, world)
+            kw["pytest"] = False          # Philox jitter (a captured step draws on the device)
             nerf.manual_seed(77 + rank)
-            kw, _, _, grad_vars, opt = nerf.create_nerf(args, device=dev)
-            kw.update(near=2.0, far=6.0)
-            params = grad_vars + list(kw["embed_fn"].parameters())
-            nerf.broadcast_params(params)
             tabs = kw["embed_fn"].tables()
             arena = nerf.GradArena(params, pad_to=world * 64, defer_tables=True, bucket_starts=[tabs[8]])
             sh = nerf.ShardedOptimizer(opt, arena, overlap=True, overlap_gather=gated)
             assert sh.gate_levels() == ([8] if gated else [])
-            ro, rd = synthetic_rays(512, seed=50 + rank)
-            rays = (torch.from_numpy(ro).to(dev), torch.from_numpy(rd).to(dev))
-            target = torch.rand(512, 3, device=dev, generator=torch.Generator(device=dev).manual_seed(rank))
             common = dict(grad_hook=sh.reduce_grads, post_hook=sh.gather_params, loss_scale_sparsity=float(world),
                           tv_generator=torch.Generator().manual_seed(7), zero_grad=arena.zero_)
             st = GraphedTrainStep(rays, target, kw, opt, args, **common) if graphed else None
@@ -298,25 +312,23 @@ def _dp_worker(rank, world, port, out, R, overlap=False, det=False):
                          ids=["zero1", "zero1_overlap", "zero1_overlap_deterministic"])
 def test_dp_shards_match_one_batch(tmp_path, overlap, det):
     """SURVEY.md §8(e) through the HIP training step: 2 ranks x 2,048 rays (gloo, both ranks on the
-    one GPU) against 1 x 4,096 rays in one process — same weights (F10's trained-like state), the
-    same pytest draws (render.pytest_shard: each rank keeps its rows of the global batch's draws),
-    the same TV cuboids. After one iteration the all-reduced gradients match the single batch's:
-    table-gradient checksums to 1e-5 (fp32 atomics / per-rank rounding), MLP gradients to 2e-5 in
-    norm; after 7 iterations with the ZeRO-1 sharded optimizer the parameters match the single
-    process's plain RAdam within F10's bar (2e-5 relative + 1e-7 absolute), except at most
-    max(2, 3e-5 of the elements) within twice the tensor's largest RAdam displacement (measured:
-    one element of 1,048,576 in one table, 1.1e-6 off, on most runs; 16 on one run of three in round 4:
-    cancelling-gradient rows, see below, whose count follows the MLP gradients' float-atomic order).
-    Deterministic mode (fixed-order MLP weight-gradient sums, fixed-point owner sums on both sides):
-    the one-process side is bitwise reproducible run to run, but the two-rank rehearsal (two processes
-    sharing the one GPU) is not — its all-reduced fine-level table gradients differ between runs
-    (tools/det_repro.py, profiles/r05aw_det_dp_repro.json; an open issue), so its count
-    (measured 12 and 26 of 1,048,576) is held to the same max(2, 1e-4 of the elements) as the default
-    mode's.
-    The default mode's count follows the MLP gradients' float-atomic order from run to run (measured
-    over rounds 4-5: 1, 16, 59 elements of one 1,048,576-element table; 0-16 in most runs), so its bar
-    is max(2, 1e-4 of the elements); a wrong update (e.g. a stale parameter bucket) shows as errors
-    beyond twice the tensor's RAdam displacement, which the second assertion rejects in both modes."""
+    one GPU, each on its own half of the CUs: _init) against 1 x 4,096 rays in one process — same
+    weights (F10's trained-like state), the same pytest draws (render.pytest_shard: each rank keeps its
+    rows of the global batch's draws), the same TV cuboids.
+    (a) After one iteration the all-reduced gradients match the single batch's: every table-gradient
+    element within 1e-6 of itself + 1e-6 of the table's largest (measured: largest error <= 1.1e-7 of
+    the table's largest element, default and deterministic mode; the two sides sum each row's terms
+    in two halves vs one, profiles/r06_dp_equiv_stats.json), MLP gradients within 2e-5 in norm.
+    (b) After 7 iterations with the ZeRO-1 sharded optimizer the parameters match the single
+    process's plain RAdam within F10's bar (2e-5 relative + 1e-7 absolute), except a few elements
+    within twice the tensor's largest RAdam displacement: a row whose summed gradient is rounding
+    noise around zero takes RAdam's full-size step in a sign set by the summation order. Deterministic
+    mode (fixed-order MLP weight-gradient sums, fixed-point owner sums on both sides; two two-rank
+    runs are bitwise equal, eight of eight in profiles/r06_det_dp2_cusplit.log): measured 2 such
+    elements of 1,048,576, bar max(2, 1.5e-5 of the elements). Default mode (the MLP weight gradients
+    summed with float atomics in any order, on top of the split): measured 8, bar max(2, 3e-5 of the
+    elements). A wrong update (e.g. a stale parameter bucket) shows as errors beyond twice the
+    tensor's RAdam displacement, which the second assertion rejects in both modes."""
     R = 4096
     mp.start_processes(_dp_worker, args=(1, _free_port(), str(tmp_path), R, False, det), nprocs=1, join=True,
                        start_method="spawn")
@@ -333,11 +345,12 @@ def test_dp_shards_match_one_batch(tmp_path, overlap, det):
         if i < n_mlp:
             rel = float((a - b).norm() / a.norm())
             assert rel <= 2e-5, f"MLP param {i}: DP gradient differs from the single batch by {rel:.2e} in norm"
-        else:
-            cs_a = [float((a * a).sum()), float(a.abs().sum())]
-            cs_b = [float((b * b).sum()), float(b.abs().sum())]
-            assert all(abs(x - y) <= 1e-5 * abs(x) for x, y in zip(cs_a, cs_b)), (i, cs_a, cs_b)
-            assert abs(float(a.sum()) - float(b.sum())) <= 1e-5 * cs_a[1], (i, float(a.sum()), float(b.sum()))
+        else:   # elementwise
+            err = (a - b).abs()
+            bound = 1e-6 * a.abs() + 1e-6 * float(a.abs().max())
+            n_off = int((err > bound).sum())
+            assert n_off == 0, (f"table {i - n_mlp}: {n_off} gradient elements off, largest error "
+                                f"{float(err.max()):.3e} vs largest element {float(a.abs().max()):.3e}")
     for i, (a, b, c, p0) in enumerate(zip(one["params"], r0["params"], r1["params"], one["params0"])):
         assert torch.equal(b, c), f"param {i}: replicas differ after 7 sharded steps"
         # F10's bar elementwise; a row whose summed gradient is rounding noise around zero (its
@@ -347,7 +360,8 @@ def test_dp_shards_match_one_batch(tmp_path, overlap, det):
         err = (b - a).abs()
         bad = err > 2e-5 * a.abs() + 1e-7
         step = float((a - p0).abs().max())
-        assert int(bad.sum()) <= max(2, int(1e-4 * a.numel())), f"param {i}: {int(bad.sum())} elements off"
+        frac = 1.5e-5 if det else 3e-5
+        assert int(bad.sum()) <= max(2, int(frac * a.numel())), f"param {i}: {int(bad.sum())} elements off"
         assert float(err.max()) <= 2 * step + 1e-7, f"param {i}: {float(err.max()):.3e} vs displacement {step:.3e}"
     # per-rank losses are those of different halves; their mean is the single batch's loss
     for la, lb, lc in zip(one["losses"], r0["losses"], r1["losses"]):

@@ -16,7 +16,31 @@ import torch.multiprocessing as mp  # noqa: E402
 import test_gpu_dist as t  # noqa: E402
 
 
+def dp2_runs(dst, K):
+    """--runs K: K runs of the deterministic two-rank rehearsal (_dp_worker, ZeRO-1 with overlap and the
+    gated all-gather), each compared bit for bit with the first: one-iteration all-reduced gradients,
+    parameters after 7 steps, losses."""
+    res, first = [], None
+    for k in range(K):
+        d = tempfile.mkdtemp()
+        mp.start_processes(t._dp_worker, args=(2, t._free_port(), d, 4096, True, True), nprocs=2, join=True,
+                           start_method="spawn")
+        cur = [torch.load(os.path.join(d, f"dp2od_{r}.pt"), weights_only=True) for r in range(2)]
+        if first is None:
+            first = cur
+            continue
+        row = {f"rank{r}_{w}": [int((x != y).sum()) for x, y in zip(first[r][w], cur[r][w])]
+               for r in range(2) for w in ("grads", "params")}
+        row["losses_equal"] = all(first[r]["losses"] == cur[r]["losses"] for r in range(2))
+        res.append(row)
+        print(f"run {k}:", json.dumps({k_: v for k_, v in row.items() if not isinstance(v, list) or any(v)}),
+              flush=True)
+    json.dump({"runs": K, "vs_run0": res}, open(dst, "w"), indent=1)
+
+
 def main():
+    if "--runs" in sys.argv:
+        return dp2_runs(sys.argv[1], int(sys.argv[sys.argv.index("--runs") + 1]))
     out = {}
     runs = {}
     for tag, world, overlap in (("one", 1, False), ("dp2", 2, True)):

@@ -22,11 +22,17 @@ import test_gpu_dist as t  # noqa: E402
 
 def _worker(rank, world, port, out, R, serial, garbage=None):
     t._init(rank, world, port)
+    if serial == "nosync_garbage":
+        serial = "nosync"
     if garbage is not None:   # leave seeded random bytes in the caching allocator's blocks: a read of
-        g = torch.Generator(device="cuda:0").manual_seed(garbage)   # memory no kernel wrote shows up
+        g = torch.Generator(device="cuda:0").manual_seed(abs(garbage))   # memory no kernel wrote shows up
         x = torch.empty(1 << 31, device="cuda:0")                   # as a run-to-run difference
         x.uniform_(-1e3, 1e3, generator=g)
         del x
+        if garbage < 0:   # the small pool too (requests <= 1 MiB come from 2 MiB segments of their own)
+            xs = [torch.empty(n, device="cuda:0").uniform_(-1e3, 1e3, generator=g)
+                  for n in [64, 1000, 4096, 16384, 65536, 262144] * 300]
+            del xs
     import importlib
     import indoor_nerf_amd as nerf
     nerf.set_deterministic(True)
@@ -75,7 +81,50 @@ def _worker(rank, world, port, out, R, serial, garbage=None):
     torch.distributed.destroy_process_group()
 
 
+def nosync_runs(dst, K):
+    """--nosync-runs K: K fresh two-rank process pairs run exactly as _dp_worker's part (a); every run's
+    pre / post all-reduce gradients compared with the first run's."""
+    res, first = [], None
+    for k in range(K):
+        d = tempfile.mkdtemp()
+        mp.start_processes(_worker, args=(2, t._free_port(), d, 4096, "nosync", None), nprocs=2, join=True,
+                           start_method="spawn")
+        cur = [torch.load(os.path.join(d, f"a_{r}.pt"), weights_only=True) for r in range(2)]
+        if first is None:
+            first = cur
+            continue
+        row = {f"rank{r}_{w}": [int((x != y).sum()) for x, y in zip(first[r][w], cur[r][w])]
+               for r in range(2) for w in ("pre", "post")}
+        res.append(row)
+        print(f"run {k}:", json.dumps({k_: v for k_, v in row.items() if any(v)}), flush=True)
+    json.dump({"runs": K, "vs_run0": res}, open(dst, "w"), indent=1)
+
+
+def garbage_runs(dst, K):
+    """--garbage-runs K: K two-rank pairs run as _dp_worker's part (a) (nosync), each with the large
+    AND the small pool of the caching allocator filled with another seed's random values first;
+    pre / post all-reduce gradients compared with the first run's."""
+    res, first = [], None
+    for k in range(K):
+        d = tempfile.mkdtemp()
+        mp.start_processes(_worker, args=(2, t._free_port(), d, 4096, "nosync_garbage", -(101 + k)), nprocs=2,
+                           join=True, start_method="spawn")
+        cur = [torch.load(os.path.join(d, f"a_{r}.pt"), weights_only=True) for r in range(2)]
+        if first is None:
+            first = cur
+            continue
+        row = {f"rank{r}_{w}": [int((x != y).sum()) for x, y in zip(first[r][w], cur[r][w])]
+               for r in range(2) for w in ("pre", "post")}
+        res.append(row)
+        print(f"garbage run {k}:", json.dumps({k_: v for k_, v in row.items() if any(v)}), flush=True)
+    json.dump({"runs": K, "vs_run0": res}, open(dst, "w"), indent=1)
+
+
 def main():
+    if "--garbage-runs" in sys.argv:
+        return garbage_runs(sys.argv[1], int(sys.argv[sys.argv.index("--garbage-runs") + 1]))
+    if "--nosync-runs" in sys.argv:
+        return nosync_runs(sys.argv[1], int(sys.argv[sys.argv.index("--nosync-runs") + 1]))
     res = {}
     modes = ("garbage",) if "--garbage" in sys.argv else ("nosync", False, "nosync", True)
     for serial in modes:

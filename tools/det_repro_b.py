@@ -38,7 +38,23 @@ def _diff(a, b, levels=None):
     return int(ne.sum())
 
 
-def _worker(rank, world, port, out, R, reps, sync):
+def _detail(a, b):
+    """Where a float32 buffer's elements differ: count, rows (first 12), 2^12-row owner slices hit,
+    largest |a - b| relative to max |a| and to |a| at that element."""
+    ne = (a.view(torch.int32) != b.view(torch.int32)).reshape(a.shape[0], -1).any(1)
+    rows = ne.nonzero().flatten()
+    if rows.numel() == 0:
+        return None
+    d = (a.double() - b.double()).abs().reshape(a.shape[0], -1)[rows].max(1).values
+    ref = a.double().abs().reshape(a.shape[0], -1)[rows].max(1).values
+    k = int(d.argmax())
+    return {"rows": int(rows.numel()), "first": rows[:12].tolist(),
+            "slices": sorted(set((rows >> 12).tolist()))[:32],
+            "max_rel_to_tensor": float(d.max() / a.double().abs().max().clamp_min(1e-300)),
+            "at_max": [float(d[k]), float(ref[k])]}
+
+
+def _worker(rank, world, port, out, R, reps, sync, save=False):
     if world > 1:
         t._init(rank, world, port)
     else:
@@ -65,6 +81,7 @@ def _worker(rank, world, port, out, R, reps, sync):
     arena = nerf.GradArena(params, defer_tables=True)
 
     cap = {}     # name -> (tensor clone, levels)
+    ptrs = {}    # buffer addresses of this process (does a result follow them?)
 
     def keep(name, x, levels=None):
         if x is not None:
@@ -88,11 +105,13 @@ def _worker(rank, world, port, out, R, reps, sync):
     orig_jobs = field._run_field_jobs
 
     def run_field_jobs(jobs):
-        for j in jobs:
+        out = orig_jobs(jobs)
+        for j in jobs:      # after the launches: graw is written by the deferred compositing backward
             if isinstance(j, field._FieldJob):
                 keep("graw", j.g)
                 keep("feat", j.feat, j.feat.shape[0])
-        return orig_jobs(jobs)
+                ptrs[f"job{len(ptrs)}"] = [j.g.data_ptr(), j.feat.data_ptr(), j.pts.data_ptr()]
+        return out
     field._run_field_jobs = run_field_jobs
 
     orig_tv = hashgrid._PendingBins.add_tv
@@ -107,7 +126,7 @@ def _worker(rank, world, port, out, R, reps, sync):
 
     def run(self, lb, le):
         L, cap_ = self.L, self.cap
-        entries = L * cap_ * 8 * int(nerf._lib.load().nerf_hash_bwd_chunk_points())
+        entries = L * cap_ * 8 * int(nerf._lib.load().nerf_hash_bwd_chunk_points())   # kChunkCap per chunk
         up = lambda v: (v + 255) & ~255  # noqa: E731
         off_h = up(entries * 8)
         off_off = off_h + up(entries * 2)
@@ -130,6 +149,12 @@ def _worker(rank, world, port, out, R, reps, sync):
             keep(f"grad{i}", p.grad, 16 if i >= 10 else None)
         if sync:
             torch.cuda.synchronize()
+        if save and ref is None:    # --runs: rep 0's buffers to disk, compared across processes by main()
+            pb = hashgrid.pending_bins(dev)
+            ptrs["ws"] = pb.ws.data_ptr()
+            ptrs["grads"] = [p.grad.data_ptr() for p in params]
+            torch.save({"cap": {k: x.cpu() for k, (x, _) in cap.items()}, "levels": {k: lv for k, (_, lv) in cap.items()},
+                        "ptrs": ptrs}, os.path.join(out, f"run_{rank}.pt"))
         if ref is None:
             ref = dict(cap)
             continue
@@ -141,6 +166,8 @@ def _worker(rank, world, port, out, R, reps, sync):
             d = _diff(ref[name][0], x, levels)
             if d != 0 and d != [0] * (levels or 0):
                 row[name] = d
+                if name.startswith("grad") and x.dtype == torch.float32:
+                    row[name + "_detail"] = _detail(ref[name][0].cpu(), x.cpu())
         res.append(row)
     torch.cuda.synchronize()
     names = {n: list(x.shape) for n, (x, _) in ref.items()}
@@ -150,12 +177,55 @@ def _worker(rank, world, port, out, R, reps, sync):
         torch.distributed.destroy_process_group()
 
 
+def cross_runs(dst, runs, world, sync):
+    """--runs K: K fresh process sets (world ranks each, one forward_backward), every captured buffer
+    of each run compared with run 0's (per rank)."""
+    import shutil
+    base = tempfile.mkdtemp()
+    res = []
+    ref = None
+    for k in range(runs):
+        d = os.path.join(base, str(k))
+        os.makedirs(d)
+        mp.start_processes(_worker, args=(world, t._free_port(), d, 4096, 1, sync, True), nprocs=world, join=True,
+                           start_method="spawn")
+        cur = [torch.load(os.path.join(d, f"run_{r}.pt"), weights_only=True) for r in range(world)]
+        if ref is None:
+            ref = cur
+            shutil.rmtree(d)
+            continue
+        row = {}
+        for r in range(world):
+            a, b = ref[r], cur[r]
+            for name, x in b["cap"].items():
+                y = a["cap"].get(name)
+                if y is None:
+                    row[f"r{r}.{name}"] = "missing in run 0"
+                    continue
+                lv = b["levels"][name]
+                dd = _diff(y, x, lv)
+                if dd != 0 and dd != [0] * (lv or 0):
+                    row[f"r{r}.{name}"] = dd
+                    if x.dtype == torch.float32 and x.dim() >= 2:
+                        row[f"r{r}.{name}_detail"] = _detail(y.reshape(y.shape[0], -1), x.reshape(x.shape[0], -1))
+            row[f"r{r}.ptrs_same"] = a["ptrs"] == b["ptrs"]
+        res.append(row)
+        print(f"run {k}: {len([v for v in row if not v.endswith('ptrs_same')])} buffers differ from run 0;",
+              json.dumps(row)[:3000], flush=True)
+        shutil.rmtree(d)
+    json.dump({"runs": runs, "world": world, "sync": sync, "ptrs_run0": [x["ptrs"] for x in ref], "diffs": res},
+              open(dst, "w"), indent=1)
+    shutil.rmtree(base)
+
+
 def main():
     argv = sys.argv[1:]
     dst = argv[0]
     reps = int(argv[argv.index("--reps") + 1]) if "--reps" in argv else 10
     world = int(argv[argv.index("--world") + 1]) if "--world" in argv else 2
     sync = "--sync" in argv
+    if "--runs" in argv:
+        return cross_runs(dst, int(argv[argv.index("--runs") + 1]), world, sync)
     d = tempfile.mkdtemp()
     mp.start_processes(_worker, args=(world, t._free_port(), d, 4096, reps, sync), nprocs=world, join=True,
                        start_method="spawn")
