@@ -526,6 +526,9 @@ int nerf_rays_pack_z(const float* d_rays_o, const float* d_rays_d, int64_t n_ray
  *   0: moments only.
  * d_coef (may be NULL): device [n_segs][4] = (decay_coef, step_coef, mode, 0) overriding the
  * by-value ones (a step captured in a HIP graph reads this step's scalars from memory).
+ * grad_scale (ABI 9): g is read as g * grad_scale (0 = 1: unscaled) — a ZeRO-1 shard steps on the
+ * reduce-scatter's SUM of the ranks' gradients with grad_scale = float(1 / world), the mean the
+ * replicated path forms with a separate multiply, without that extra pass over the shard.
  */
 typedef struct {
     float* p;
@@ -535,6 +538,7 @@ typedef struct {
     int64_t n;
     float beta1, beta2, one_minus_beta1, one_minus_beta2, eps, decay_coef, step_coef;
     int mode;
+    float grad_scale;
 } nerf_radam_segment;
 
 int nerf_radam_step(const nerf_radam_segment* segs, int n_segs, const float* d_coef, void* stream);

@@ -94,7 +94,7 @@ class RAdamSegment(ctypes.Structure):
                 ("beta1", ctypes.c_float), ("beta2", ctypes.c_float),
                 ("one_minus_beta1", ctypes.c_float), ("one_minus_beta2", ctypes.c_float),
                 ("eps", ctypes.c_float), ("decay_coef", ctypes.c_float), ("step_coef", ctypes.c_float),
-                ("mode", c_int)]
+                ("mode", c_int), ("grad_scale", ctypes.c_float)]
 
 
 class RAdamTableStep(ctypes.Structure):

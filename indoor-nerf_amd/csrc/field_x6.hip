@@ -548,6 +548,29 @@ __device__ __forceinline__ void rgb_c2(const float* c2f, const floatx16 (&h3)[2]
     rgb[1] = e;
 }
 
+// Stage 1's ga3 = C2^T g_rgb (3 live k rows) on the exact fp32 matrix core (v_mfma_f32_32x32x2_f32):
+// two k = 2 MFMAs per 32-row tile (k = r, g | b, 0) replace six x6 MFMAs of a 16-deep k-chunk, and
+// no operand is split. A operand of tile t, MFMA m: lane (i, h) holds C2[2m + h][32t + i] (0 past
+// the three rows), stored [t][lane][m] so one ds_read_b64 per tile fetches both; B operand: lane
+// (j, h) holds g_rgb[2m + h] of point j. The accumulator layout equals the bf16 MFMA's.
+#ifndef NERF_X6_GA3_F32
+#define NERF_X6_GA3_F32 1
+#endif
+constexpr int C2B_FLOATS = 2 * 64 * 2;
+
+__device__ inline void fill_c2b(float* c2b, const nerf_mlp_weights& W) {
+    for (int idx = threadIdx.x; idx < C2B_FLOATS; idx += blockDim.x) {
+        const int t = idx >> 7, ln = (idx >> 1) & 63, m = idx & 1, k = 2 * m + (ln >> 5);
+        c2b[idx] = k < 3 ? W.c2[k * 64 + 32 * t + (ln & 31)] : 0.f;
+    }
+}
+
+__device__ __forceinline__ floatx16 ga3_f32(const float* c2b, int t, float b0, float b1, int lane) {
+    const float2 a = *reinterpret_cast<const float2*>(c2b + 2 * (64 * t + lane));
+    floatx16 c = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b0, zero16(), 0, 0, 0);
+    return __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b1, c, 0, 0, 0);
+}
+
 // ================================================================ forward kernel
 template <bool QUANT>
 // 512-thread blocks: the 66.8 KB weight image is shared by 8 waves, so two blocks per CU give 4
@@ -694,7 +717,7 @@ __device__ __forceinline__ void stage_arrF(float* actF, const float* v, int row0
 template <bool QUANT>
 __device__ __forceinline__ void bwd_chain_role(const MlpArgs& a, const __bf16* img, __bf16* stA, __bf16* stG,
                                                int* ready, int* ack, int p, int lane, const QuantRec& aq, int blk,
-                                               int nblk) {
+                                               int nblk, const float* c2b) {
     const int j = lane & 31, h = lane >> 5;
     float* actF = reinterpret_cast<float*>(stA);
     int seq = 0;
@@ -752,9 +775,17 @@ __device__ __forceinline__ void bwd_chain_role(const MlpArgs& a, const __bf16* i
 #pragma unroll
             for (int t = 0; t < 2; ++t) stage_tileF(actF, f.h3[t], 32 * t, j, h);
             publish();
+#if NERF_X6_GA3_F32
+            const float b0 = h ? g4.y : g4.x, b1 = h ? 0.f : g4.z;
+            (void)imt;
+#endif
 #pragma unroll
             for (int t = 0; t < 2; ++t) {
+#if NERF_X6_GA3_F32
+                ga3[t] = ga3_f32(c2b + opaque_zero(), t, b0, b1, lane);
+#else
                 ga3[t] = mma6(tr_read(imt, IM_PIECE, IM_C2, S64, 0, 32 * t, lane), GR, zero16());
+#endif
 #pragma unroll
                 for (int r = 0; r < 16; ++r) ga3[t][r] = f.h3[t][r] > 0.f ? ga3[t][r] : 0.f;
             }
@@ -1127,6 +1158,7 @@ template <bool QUANT>
 __global__ void __launch_bounds__(512, 1) mlp_bwd_x6cg_kernel(MlpBwdJobs jobs) {
     __shared__ __attribute__((aligned(16))) __bf16 lds[X6_CG_LDS / 2 + X6_ZBLK_ELEMS];
     __shared__ int flags[8];   // ready[0..3], ack[0..3]
+    __shared__ __attribute__((aligned(16))) float c2b[C2B_FLOATS];
     const bool second = (int)blockIdx.x >= jobs.split;
     const MlpArgs& a = second ? jobs.a[1] : jobs.a[0];
     const int blk = second ? (int)blockIdx.x - jobs.split : (int)blockIdx.x;
@@ -1137,6 +1169,7 @@ __global__ void __launch_bounds__(512, 1) mlp_bwd_x6cg_kernel(MlpBwdJobs jobs) {
     __bf16* stA = lds + 3 * IM_PIECE + p * ST_CG;   // fp32 activation image (actF)
     __bf16* stG = stA + 2 * ACTF_FLOATS;
     fill_images(img, a.W);
+    fill_c2b(c2b, a.W);
     for (int i = threadIdx.x; i < X6_ZBLK_ELEMS / 2; i += blockDim.x) reinterpret_cast<uint32_t*>(img + X6_ZBLK)[i] = 0u;
     if (threadIdx.x < 8) flags[threadIdx.x] = 0;
     __syncthreads();
@@ -1148,7 +1181,7 @@ __global__ void __launch_bounds__(512, 1) mlp_bwd_x6cg_kernel(MlpBwdJobs jobs) {
     } else {
         QuantRec aq{};
         if constexpr (QUANT) aq = *a.aq;
-        bwd_chain_role<QUANT>(a, img, stA, stG, flags + p, flags + 4 + p, p, lane, aq, blk, nblk);
+        bwd_chain_role<QUANT>(a, img, stA, stG, flags + p, flags + 4 + p, p, lane, aq, blk, nblk, c2b);
     }
 
     // ---- block reduction of the wgrad waves' tiles, one global flush per block. Each wgrad wave

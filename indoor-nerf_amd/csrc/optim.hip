@@ -29,11 +29,13 @@ __global__ void __launch_bounds__(kRAdamThreads) radam_kernel(RAdamSegs S) {
     }
     const int64_t i0 = ((b - S.block_start[si]) * kRAdamThreads + threadIdx.x) * kRAdamVec;
     if (i0 >= s.n) return;
+    const float gs = s.grad_scale != 0.f ? s.grad_scale : 1.f;   // g * 1 == g bit for bit
     const bool aligned = ((reinterpret_cast<uintptr_t>(s.p) | reinterpret_cast<uintptr_t>(s.g) |
                            reinterpret_cast<uintptr_t>(s.m) | reinterpret_cast<uintptr_t>(s.v)) & 15) == 0;
     if (aligned && i0 + kRAdamVec <= s.n) {
         float4 p = *reinterpret_cast<const float4*>(s.p + i0);
-        const float4 g = *reinterpret_cast<const float4*>(s.g + i0);
+        float4 g = *reinterpret_cast<const float4*>(s.g + i0);
+        g.x *= gs; g.y *= gs; g.z *= gs; g.w *= gs;
         float4 m = *reinterpret_cast<const float4*>(s.m + i0);
         float4 v = *reinterpret_cast<const float4*>(s.v + i0);
         radam_elem(s, p.x, g.x, m.x, v.x);
@@ -46,7 +48,7 @@ __global__ void __launch_bounds__(kRAdamThreads) radam_kernel(RAdamSegs S) {
     } else {
         for (int64_t i = i0; i < i0 + kRAdamVec && i < s.n; ++i) {
             float p = s.p[i], m = s.m[i], v = s.v[i];
-            radam_elem(s, p, s.g[i], m, v);
+            radam_elem(s, p, s.g[i] * gs, m, v);
             s.m[i] = m;
             s.v[i] = v;
             if (s.mode != 0) s.p[i] = p;

@@ -228,8 +228,9 @@ class ShardedOptimizer:
     GradArena(bucket_starts=...)) rank r owns the contiguous r-th 1/G of the bucket.
     Per iteration, instead of an all-reduce of the gradients and a dense RAdam pass over all 16.8 M
     elements on every rank:
-      reduce_grads()   reduce-scatter (sum) of the gradient buffer into this rank's shard, x 1/G
-      optimizer.step() RAdam on the shard only (the HIP kernel on sub-ranges of the tensors)
+      reduce_grads()   reduce-scatter (sum) of the gradient buffer into this rank's shard
+      optimizer.step() RAdam on the shard only (the HIP kernel on sub-ranges of the tensors, reading
+                       the summed gradient x 1/G: the mean without a pass of its own)
       gather_params()  all-gather of the updated parameter shards into every replica
     The collective bytes equal one all-reduce; the dense optimizer traffic drops by G. Elementwise
     RAdam on a shard is bit-identical to RAdam on the whole tensor (tests/test_gpu_dist.py).
@@ -282,7 +283,9 @@ class ShardedOptimizer:
                     r = (a - off, b - off)
                     shard[p] = (a - off, b - off, self.gshard[gp + a - lo:gp + b - lo])
             self.ranges.append(r)
-        optimizer.set_shard(shard if self.world > 1 else None)
+        # the reduce-scatter leaves the SUM of the ranks' gradients; the RAdam launch reads it x 1/G
+        # (nerf_radam_segment.grad_scale), so no pass over the shard forms the mean first
+        optimizer.set_shard(shard if self.world > 1 else None, grad_scale=1.0 / self.world)
         self.overlap = bool(overlap) and len(arena.buckets) > 1 and dev.type == "cuda"
         self.side = torch.cuda.Stream(device=dev) if self.overlap else None
         self._levels = None
@@ -329,9 +332,9 @@ class ShardedOptimizer:
         return self._levels[1]
 
     def reduce_grads(self):
-        """Reduce-scatter of each gradient bucket: this rank's shard of the mean gradient. The same
-        collective on every backend (RCCL on the device buffers; gloo on host copies of them). With
-        overlap and a held owner pass: every bucket's levels are summed and recorded first, then each
+        """Reduce-scatter of each gradient bucket: this rank's shard of the summed gradient (RAdam
+        reads it x 1/G). The same collective on every backend (RCCL on the device buffers; gloo on
+        host copies of them). With overlap and a held owner pass: every bucket's levels are summed and recorded first, then each
         bucket's reduce-scatter waits on the side stream for its own levels only."""
         from .hashgrid import pending_bins
         self.wait_params()      # the last all-gather wrote the parameter shards the update reads
@@ -353,10 +356,8 @@ class ShardedOptimizer:
                 self.side.wait_event(events[k])
                 with torch.cuda.stream(self.side):
                     _reduce_scatter(out, flat[s:e], self.group)
-                    out.mul_(1.0 / self.world)
             else:
                 _reduce_scatter(out, flat[s:e], self.group)
-                out.mul_(1.0 / self.world)
         if events:
             torch.cuda.current_stream(flat.device).wait_stream(self.side)
 

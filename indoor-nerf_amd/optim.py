@@ -33,15 +33,19 @@ class RAdam(Optimizer):
                         buffer=[[None, None, None] for _ in range(10)])
         super().__init__(params, defaults)
         self.shard = None
+        self.grad_scale = 1.0
         self._fused = set()    # ids of the parameters whose step of this iteration the owner pass ran
 
-    def set_shard(self, shard):
+    def set_shard(self, shard, grad_scale=1.0):
         """Data-parallel optimizer sharding (dist.ShardedOptimizer): `shard` maps a parameter to the
         (start, end, grad) element range this rank updates, `grad` a flat fp32 tensor of end - start
         reduced gradients (the rank's reduce-scatter output) or None for p.grad[start:end];
         parameters missing from the map are not updated here (their step count still advances, as
-        on the rank that owns them). None = every element of every parameter (the default)."""
+        on the rank that owns them). None = every element of every parameter (the default).
+        grad_scale: the kernel reads every sharded gradient as g * grad_scale (1 / world: the
+        reduce-scatter's sum becomes the mean inside the update, no separate pass)."""
         self.shard = shard
+        self.grad_scale = float(grad_scale) if shard is not None else 1.0
 
     def _scalars(self, group, step):
         beta1, beta2 = group["betas"]
@@ -90,6 +94,7 @@ class RAdam(Optimizer):
         s.eps = group["eps"]
         s.decay_coef, s.step_coef = self._coefs(group, mode, step_size)
         s.mode = mode
+        s.grad_scale = self.grad_scale
         return s
 
     @staticmethod

@@ -102,13 +102,14 @@ def test_shard_ranges_tile_every_parameter():
 
 
 class _SgdShard:
-    """Stand-in for RAdam.set_shard/step on CPU: p[a:b] -= 0.5 * grad shard."""
+    """Stand-in for RAdam.set_shard/step on CPU: p[a:b] -= 0.5 * (grad shard x grad_scale) (RAdam's
+    kernel reads the reduce-scatter's sum x 1/G the same way)."""
 
     def __init__(self, params):
-        self.params, self.shard = params, None
+        self.params, self.shard, self.grad_scale = params, None, 1.0
 
-    def set_shard(self, shard):
-        self.shard = shard
+    def set_shard(self, shard, grad_scale=1.0):
+        self.shard, self.grad_scale = shard, grad_scale
 
     def step(self):
         with torch.no_grad():
@@ -117,7 +118,7 @@ class _SgdShard:
                     p.view(-1).sub_(0.5 * p.grad.view(-1))
                 elif p in self.shard:
                     a, b, g = self.shard[p]
-                    p.view(-1)[a:b].sub_(0.5 * g)
+                    p.view(-1)[a:b].sub_(0.5 * (g * self.grad_scale))
 
 
 def _zero_worker(rank, world, port, out_dir, buckets=False):

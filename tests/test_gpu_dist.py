@@ -160,6 +160,73 @@ def test_sharded_graphed_training_replicas_agree(tmp_path, overlap):
         assert torch.equal(a, b)
 
 
+def _zero_vs_repl_worker(rank, world, port, out):
+    """Deterministic mode, F10's state, each rank its half of a 4,096-ray batch, 6 iterations, four
+    ways: eager / graphed x replicated (all-reduce mean, RAdam on every element) / ZeRO-1 (bucketed,
+    owner pass held and run by level range beside the reduce-scatters, RAdam on the rank's shard
+    reading the summed gradient x 1/G, gated all-gather)."""
+    _init(rank, world, port)
+    import indoor_nerf_amd as nerf
+    from indoor_nerf_amd.graphs import GraphedTrainStep
+    from tables import synthetic_rays
+    nerf.set_deterministic(True)
+    dev = torch.device("cuda:0")
+    R = 4096
+    n = R // world
+    ro, rd = synthetic_rays(R, seed=21)
+    rays = (torch.from_numpy(ro[rank * n:(rank + 1) * n]).to(dev), torch.from_numpy(rd[rank * n:(rank + 1) * n]).to(dev))
+    target = torch.rand(R, 3, generator=torch.Generator().manual_seed(5))[rank * n:(rank + 1) * n].to(dev)
+    res = {}
+    for graphed in (False, True):
+        for sharded in (False, True):
+            args, kw, opt, params = _f10_model(nerf, dev, world)
+            kw["pytest"] = False
+            nerf.manual_seed(77 + rank)
+            tabs = kw["embed_fn"].tables()
+            if sharded:
+                arena = nerf.GradArena(params, pad_to=world * 64, defer_tables=True, bucket_starts=[tabs[8]])
+                sh = nerf.ShardedOptimizer(opt, arena, overlap=True)
+                hooks = dict(grad_hook=sh.reduce_grads, post_hook=sh.gather_params)
+            else:
+                arena = nerf.GradArena(params, defer_tables=True)
+                hooks = dict(grad_hook=arena.allreduce_mean, post_hook=None)
+            common = dict(loss_scale_sparsity=float(world), tv_generator=torch.Generator().manual_seed(7),
+                          zero_grad=arena.zero_, **hooks)
+            st = GraphedTrainStep(rays, target, kw, opt, args, **common) if graphed else None
+            losses = []
+            for it in range(1, 7):
+                loss, _ = st(it) if graphed else nerf.train_step(rays, target, kw, opt, args, it, **common)
+                losses.append(float(loss))
+            if sharded:
+                sh.wait_params()
+            torch.cuda.synchronize()
+            res[f"{int(graphed)}{int(sharded)}"] = {"params": [p.detach().cpu() for p in params], "losses": losses}
+    torch.save(res, os.path.join(out, f"zvr_{rank}.pt"))
+    torch.distributed.destroy_process_group()
+
+
+def test_sharded_training_matches_replicated_bitwise(tmp_path):
+    """the ZeRO-1 step (reduce-scatter of the summed gradient, RAdam on the rank's
+    shard scaling it by 1/G inside the update, all-gather of the updated shards) against the
+    replicated step (all-reduce, x 1/G, RAdam on every element), deterministic mode, eager and
+    graphed: parameters and losses bit-identical after 6 iterations on both ranks (with two ranks the
+    collective sums two terms, so both paths see the same mean gradient bit for bit)."""
+    world = 2
+    mp.start_processes(_zero_vs_repl_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    r = [torch.load(tmp_path / f"zvr_{k}.pt", weights_only=True) for k in range(world)]
+    for k in range(world):
+        for g in ("0", "1"):
+            repl, shard = r[k][g + "0"], r[k][g + "1"]
+            assert repl["losses"] == shard["losses"], (k, g)
+            for i, (a, b) in enumerate(zip(repl["params"], shard["params"])):
+                assert torch.equal(a, b), f"rank {k}, graphed {g}: param {i} differs ({int((a != b).sum())} elements)"
+    for g in ("00", "01", "10", "11"):
+        for a, b in zip(r[0][g]["params"], r[1][g]["params"]):
+            assert torch.equal(a, b)          # replicas agree
+    assert len(set(r[0]["00"]["losses"])) > 1          # the parameters moved
+
+
 def _gather_worker(rank, world, port, out):
     """ZeRO-1 with two buckets (MLP + levels 0-7 | levels 8-15), deterministic mode, 5 iterations, four
     ways: eager / graphed x all-gather in stream order (overlap_gather=False) / gated (the levels 8-15
