@@ -105,9 +105,10 @@ KERNEL_VARIANTS = {
 
 
 def base_name(abi_name):
-    """nerf_mlp_fwd_q / nerf_mlp_fwd_ord -> nerf_mlp_fwd: the _q entry points are the same kernels with
-    optional A-CAQ records (NULL on the unquantized path), _ord with an optional point order."""
-    for suffix in ("_q", "_ord"):
+    """nerf_mlp_fwd_q / _ord / _h3 -> nerf_mlp_fwd: the _q entry points are the same kernels with
+    optional A-CAQ records (NULL on the unquantized path), _ord with an optional point order, _h3 also
+    storing layer C1's outputs for the backward."""
+    for suffix in ("_q", "_ord", "_h3"):
         if abi_name.endswith(suffix):
             return abi_name[:-len(suffix)]
     return abi_name
@@ -115,7 +116,7 @@ def base_name(abi_name):
 
 def traffic_file():
     """The newest committed PMC traffic summary (tools/profile_bench.sh), or None."""
-    for name in ("r05_traffic.json", "r04_traffic.json", "r03_traffic.json", "r02_traffic.json", "r01j_traffic.json"):
+    for name in ("r06_traffic.json", "r05_traffic.json", "r04_traffic.json", "r03_traffic.json", "r02_traffic.json", "r01j_traffic.json"):
         path = os.path.join(ROOT, "profiles", name)
         if os.path.exists(path):
             return path

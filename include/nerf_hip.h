@@ -293,6 +293,17 @@ typedef struct {
 } nerf_point_order;
 
 /* nerf_mlp_fwd_q in a point order (NULL order: the identity, seg_split = n_points). */
+/* Training forward (ABI 10): also stores layer C1's ReLU outputs into d_h3 (>= nerf_mlp_h3_bytes(n_points),
+ * 256 B per point, an opaque per-tile layout) for the backward job's `h3`, which then reads them
+ * instead of recomputing C1; bit-identical to the recompute. Not with A-CAQ (d_act_qrec). */
+size_t nerf_mlp_h3_bytes(int64_t n_points);
+int nerf_mlp_fwd_h3(const float* d_feat, int64_t feat_stride_point, int64_t feat_stride_level,
+                    const float* d_sh, int64_t sh_stride,
+                    const float* d_viewdirs, int64_t samples_per_ray,
+                    const uint8_t* d_keep, int64_t n_points,
+                    const nerf_mlp_weights* weights, float* d_raw, float* d_geo,
+                    const float* d_act_qrec, uint32_t* d_act_minmax, int64_t act_calib_points,
+                    const nerf_point_order* order, float* d_h3, void* stream);
 int nerf_mlp_fwd_ord(const float* d_feat, int64_t feat_stride_point, int64_t feat_stride_level,
                      const float* d_sh, int64_t sh_stride,
                      const float* d_viewdirs, int64_t samples_per_ray,
@@ -339,6 +350,8 @@ typedef struct {
     const int32_t* rows;         /* optional (with d_count): walk only the points rows[0 .. *d_count) — the active
                                     points of nerf_active_rows; the other points' d feat / d sh are not written */
     const int32_t* d_count;      /* device int: the number of rows */
+    const float* h3;             /* optional (ABI 10): the h3 the same points' nerf_mlp_fwd_h3 stored (NULL:
+                                    recomputed); not with act_qrec or rows; all jobs of a launch alike or split */
 } nerf_mlp_bwd_job;
 
 size_t nerf_mlp_bwd_det_workspace_bytes(void);

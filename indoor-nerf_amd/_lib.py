@@ -45,7 +45,8 @@ class MlpBwdJob(ctypes.Structure):
                 ("sh_stride", c_i64), ("viewdirs", c_vp), ("samples_per_ray", c_i64), ("keep", c_vp),
                 ("n_points", c_i64), ("weights", MlpWeights), ("graw", c_vp), ("grads", MlpGrads), ("dfeat", c_vp),
                 ("dsh", c_vp), ("dgeo", c_vp), ("act_qrec", c_vp), ("order", PointOrder),
-                ("dfeat_stride_point", c_i64), ("dfeat_stride_level", c_i64), ("rows", c_vp), ("d_count", c_vp)]
+                ("dfeat_stride_point", c_i64), ("dfeat_stride_level", c_i64), ("rows", c_vp), ("d_count", c_vp),
+                ("h3", c_vp)]
 
 
 PRIORS_MAX_RAYS = 8192   # NERF_PRIORS_MAX_RAYS
@@ -150,6 +151,8 @@ SIGNATURES = {
                        c_vp, c_vp, c_vp, c_vp, c_i64, c_vp],
     "nerf_mlp_fwd_ord": [c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, ctypes.POINTER(MlpWeights),
                          c_vp, c_vp, c_vp, c_vp, c_i64, ctypes.POINTER(PointOrder), c_vp],
+    "nerf_mlp_fwd_h3": [c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, ctypes.POINTER(MlpWeights),
+                        c_vp, c_vp, c_vp, c_vp, c_i64, ctypes.POINTER(PointOrder), c_vp, c_vp],
     "nerf_mlp_bwd_q": [c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, ctypes.POINTER(MlpWeights),
                        c_vp, ctypes.POINTER(MlpGrads), c_vp, c_vp, c_vp, c_vp, c_vp],
     "nerf_count_nonfinite": [ctypes.POINTER(c_vp), ctypes.POINTER(c_i64), c_int, c_vp, c_vp],
@@ -249,6 +252,9 @@ def load():
     lib.nerf_active_rows_workspace_bytes.argtypes = [c_i64]
     lib.nerf_quant_packed_bytes.restype = ctypes.c_size_t
     lib.nerf_quant_packed_bytes.argtypes = [c_int, c_int]
+    if hasattr(lib, "nerf_mlp_h3_bytes"):   # ABI 10 (an older A/B variant may lack it)
+        lib.nerf_mlp_h3_bytes.restype = ctypes.c_size_t
+        lib.nerf_mlp_h3_bytes.argtypes = [c_i64]
     for name, argtypes in SIGNATURES.items():
         # a library of an older tree (an A/B variant, tools/build_variant.py --rev) may lack newer
         # entries: they stay unbound and call() raises if one is used (test_abi holds the in-tree library
@@ -267,7 +273,8 @@ def exported_symbols():
 
             "nerf_hash_encode_bwd_workspace_bytes",
             "nerf_quant_packed_bytes", "nerf_mlp_bwd_det_workspace_bytes", "nerf_priors_workspace_bytes",
-            "nerf_normal_head_bwd_workspace_bytes", "nerf_active_rows_workspace_bytes"] + list(SIGNATURES)
+            "nerf_normal_head_bwd_workspace_bytes", "nerf_active_rows_workspace_bytes",
+            "nerf_mlp_h3_bytes"] + list(SIGNATURES)
 
 
 _TIMING = None   # when a list: (name, start_event, end_event) per launch, recorded on the current stream

@@ -67,11 +67,15 @@ extern "C" int nerf_sh4_fwd(const float* d_dirs, int64_t n, float* d_out, void* 
     return NERF_OK;
 }
 
-extern "C" int nerf_mlp_fwd_ord(const float* d_feat, int64_t feat_stride_point, int64_t feat_stride_level,
-                                const float* d_sh, int64_t sh_stride, const float* d_viewdirs, int64_t samples_per_ray,
-                                const uint8_t* d_keep, int64_t n_points, const nerf_mlp_weights* weights, float* d_raw,
-                                float* d_geo, const float* d_act_qrec, uint32_t* d_act_minmax,
-                                int64_t act_calib_points, const nerf_point_order* order, void* stream) {
+extern "C" size_t nerf_mlp_h3_bytes(int64_t n_points) {
+    return n_points > 0 ? (size_t)((n_points + 31) / 32) * 2048 * sizeof(float) : 0;
+}
+
+extern "C" int nerf_mlp_fwd_h3(const float* d_feat, int64_t feat_stride_point, int64_t feat_stride_level,
+                               const float* d_sh, int64_t sh_stride, const float* d_viewdirs, int64_t samples_per_ray,
+                               const uint8_t* d_keep, int64_t n_points, const nerf_mlp_weights* weights, float* d_raw,
+                               float* d_geo, const float* d_act_qrec, uint32_t* d_act_minmax,
+                               int64_t act_calib_points, const nerf_point_order* order, float* d_h3, void* stream) {
     MlpArgs a{};
     int rc = fill_args(a, d_feat, feat_stride_point, feat_stride_level, d_sh, sh_stride, d_viewdirs, samples_per_ray,
                        d_keep, n_points, weights);
@@ -79,14 +83,26 @@ extern "C" int nerf_mlp_fwd_ord(const float* d_feat, int64_t feat_stride_point, 
     rc = fill_order(a, order);
     if (rc) return rc;
     NERF_REQUIRE(n_points == 0 || d_raw || d_act_minmax, "mlp_fwd: null output");
+    NERF_REQUIRE(!d_h3 || (!d_act_qrec && !d_act_minmax), "mlp_fwd: saved h3 with A-CAQ (its backward recomputes)");
     if (n_points == 0) return NERF_OK;
     a.raw = d_raw;
     a.geo_out = d_geo;
     a.aq = reinterpret_cast<const QuantRec*>(d_act_qrec);
     a.act_minmax = d_act_minmax;
     a.calib_points = act_calib_points;
+    a.h3 = d_h3;
     // the calibration-only launch (d_act_minmax) computes layer 0 and its statistics, nothing else
     return a.act_minmax ? launch_mlp_act_minmax_x6(a, as_stream(stream)) : launch_mlp_fwd_x6(a, as_stream(stream));
+}
+
+extern "C" int nerf_mlp_fwd_ord(const float* d_feat, int64_t feat_stride_point, int64_t feat_stride_level,
+                                const float* d_sh, int64_t sh_stride, const float* d_viewdirs, int64_t samples_per_ray,
+                                const uint8_t* d_keep, int64_t n_points, const nerf_mlp_weights* weights, float* d_raw,
+                                float* d_geo, const float* d_act_qrec, uint32_t* d_act_minmax,
+                                int64_t act_calib_points, const nerf_point_order* order, void* stream) {
+    return nerf_mlp_fwd_h3(d_feat, feat_stride_point, feat_stride_level, d_sh, sh_stride, d_viewdirs, samples_per_ray,
+                           d_keep, n_points, weights, d_raw, d_geo, d_act_qrec, d_act_minmax, act_calib_points, order,
+                           nullptr, stream);
 }
 
 extern "C" int nerf_mlp_fwd_q(const float* d_feat, int64_t feat_stride_point, int64_t feat_stride_level,
@@ -156,10 +172,13 @@ extern "C" int nerf_mlp_bwd_batch(const nerf_mlp_bwd_job* jobs, int n_jobs, floa
         NERF_REQUIRE(!j.rows == !j.d_count, "mlp_bwd_batch: job %d: rows and d_count go together", k);
         x.rows = j.rows;
         x.count = j.d_count;
+        NERF_REQUIRE(!j.h3 || (!j.act_qrec && !j.rows), "mlp_bwd_batch: job %d: saved h3 with A-CAQ or active rows", k);
+        x.h3 = const_cast<float*>(j.h3);
         if (x.P > 0) ++n;   // empty jobs launch nothing
     }
     if (n == 0) return NERF_OK;
-    if (n == 2 && (a[0].aq != nullptr) != (a[1].aq != nullptr)) {   // one quantizer mode per launch
+    if (n == 2 && ((a[0].aq != nullptr) != (a[1].aq != nullptr) ||
+                   (a[0].h3 != nullptr) != (a[1].h3 != nullptr))) {   // one quantizer / h3 mode per launch
         int rc = launch_mlp_bwd_x6(&a[0], 1, d_det_workspace, as_stream(stream));
         return rc ? rc : launch_mlp_bwd_x6(&a[1], 1, d_det_workspace, as_stream(stream));
     }

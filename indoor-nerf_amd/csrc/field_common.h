@@ -49,6 +49,8 @@ struct MlpArgs {
     const QuantRec* aq;   // optional A-CAQ record of the layer-0 activation quantizer
     uint32_t* act_minmax; // calibration-only launch: min/max of relu(x W0^T) (order-preserving u32)
     int64_t calib_points;
+    float* h3;            // optional: layer C1's ReLU outputs per 32-point tile (field_x6.hip h3_at): the
+                          // forward stores them, the backward reads them instead of recomputing C1
 };
 
 // A-CAQ activation quantizer on a layer-0 accumulator tile (sigma_act_quantizers[0],

@@ -450,9 +450,14 @@ __device__ __forceinline__ floatx16 fold_rows16(const floatx16& acc) {
     return o;
 }
 
-// forward chain up to h3 (the output layer C2 is the caller's: forward kernel rgb_c2)
-template <bool QUANT>
-__device__ __forceinline__ void fwd_chain(const __bf16* img, const InX6& in, ActX6& f, int lane, const QuantRec& aq) {
+// forward chain up to h3 (the output layer C2 is the caller's: forward kernel rgb_c2); C1 = false: up to
+// h2 only (the backward with the forward's saved h3)
+struct NoHook {
+    __device__ __forceinline__ void operator()() const {}
+};
+template <bool QUANT, bool C1 = true, typename BeforeC0 = NoHook>
+__device__ __forceinline__ void fwd_chain(const __bf16* img, const InX6& in, ActX6& f, int lane, const QuantRec& aq,
+                                          const BeforeC0& before_c0 = BeforeC0{}) {
     const int m = lane & 31, h = lane >> 5;
     f.xb[0] = split_arr(in.x);
     f.xb[1] = split_arr(in.x + 8);
@@ -472,6 +477,7 @@ __device__ __forceinline__ void fwd_chain(const __bf16* img, const InX6& in, Act
             }
         f.o = fold_rows16(acc);
     }
+    before_c0();
     // C0: h2 = relu(C0' [o rows 0..15 ; sh])
     f.h2[0] = f.h2[1] = zero16();
     {
@@ -484,6 +490,7 @@ __device__ __forceinline__ void fwd_chain(const __bf16* img, const InX6& in, Act
         for (int t = 0; t < 2; ++t) f.h2[t] = mma6(row_read(img, IM_C0, S32, 32 * t + m, 16 + 4 * h), in.SH, f.h2[t]);
     }
     relu16i(f.h2[0]); relu16i(f.h2[1]);
+    if constexpr (!C1) return;
     // C1: h3 = relu(C1 h2)
     f.h3[0] = f.h3[1] = zero16();
 #pragma unroll
@@ -571,6 +578,18 @@ __device__ __forceinline__ floatx16 ga3_f32(const float* c2b, int t, float b0, f
     return __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b1, c, 0, 0, 0);
 }
 
+// Saved C1 outputs (training forward -> backward): per 32-point tile the 2 x 16 h3 registers of every lane
+// as float4 groups, [tile][t][q][lane][4] (one coalesced 16-B access per lane and group; 256 B per
+// point). The backward then skips C1's recompute (48 of the chain wave's MFMAs and the h2 split, 176
+// VALU, per tile). Nontemporal both ways: the buffer is written once and read once.
+typedef float f32x4_nt __attribute__((ext_vector_type(4)));
+#ifndef NERF_X6_H3_LOAD
+#define NERF_X6_H3_LOAD 1
+#endif
+__device__ __forceinline__ uint32_t h3_off(int64_t tile, int t, int q, int lane) {
+    return (((((uint32_t)tile * 2u + (uint32_t)t) * 4u + (uint32_t)q) * 64u) + (uint32_t)lane) * 4u;
+}
+
 // ================================================================ forward kernel
 template <bool QUANT>
 // 512-thread blocks: the 66.8 KB weight image is shared by 8 waves, so two blocks per CU give 4
@@ -592,6 +611,17 @@ __global__ void __launch_bounds__(512, 2) mlp_fwd_x6_kernel(MlpArgs a) {
         ActX6 f;
         const int z = opaque_zero();
         fwd_chain<QUANT>(img + z, in, f, lane, aq);
+        if constexpr (!QUANT) {
+            if (a.h3) {
+#pragma unroll
+                for (int t = 0; t < 2; ++t)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        __builtin_nontemporal_store(f32x4_nt{f.h3[t][4 * q], f.h3[t][4 * q + 1], f.h3[t][4 * q + 2],
+                                                             f.h3[t][4 * q + 3]},
+                                                    reinterpret_cast<f32x4_nt*>(a.h3 + h3_off(tile, t, q, lane)));
+            }
+        }
         float rgb[3];
         rgb_c2(c2f + z, f.h3, h, rgb);
         const uint32_t orow = in.valid ? io_row(a, in.pt) : 0u;
@@ -714,7 +744,7 @@ __device__ __forceinline__ void stage_arrF(float* actF, const float* v, int row0
     for (int i = 0; i < 8; ++i) actF[(row0 + 4 * h + (i & 3) + 8 * (i >> 2)) * SPF + j] = v[i];
 }
 
-template <bool QUANT>
+template <bool QUANT, bool SAVED>
 __device__ __forceinline__ void bwd_chain_role(const MlpArgs& a, const __bf16* img, __bf16* stA, __bf16* stG,
                                                int* ready, int* ack, int p, int lane, const QuantRec& aq, int blk,
                                                int nblk, const float* c2b) {
@@ -757,7 +787,30 @@ __device__ __forceinline__ void bwd_chain_role(const MlpArgs& a, const __bf16* i
         load_in_x6_bwd(a, n_pts, tile, j, h, in);
 #endif
         ActX6 f;
-        fwd_chain<QUANT>(imt, in, f, lane, aq);
+        if constexpr (SAVED) {   // h3 from the forward, in flight during layer C0 (NERF_X6_H3_LOAD: 0 before
+            f32x4_nt h3v[8];     // layer 0, 1 before C0, 2 after the chain)
+            auto load_h3 = [&]() {
+#pragma unroll
+                for (int k = 0; k < 8; ++k)
+                    h3v[k] = __builtin_nontemporal_load(
+                        reinterpret_cast<const f32x4_nt*>(a.h3 + h3_off(tile, k >> 2, k & 3, lane)));
+            };
+#if NERF_X6_H3_LOAD == 0
+            load_h3();
+            fwd_chain<QUANT, false>(imt, in, f, lane, aq);
+#elif NERF_X6_H3_LOAD == 1
+            fwd_chain<QUANT, false>(imt, in, f, lane, aq, load_h3);
+#else
+            fwd_chain<QUANT, false>(imt, in, f, lane, aq);
+            load_h3();
+#endif
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) f.h3[k >> 2][4 * (k & 3) + e] = h3v[k][e];
+        } else {
+            fwd_chain<QUANT>(imt, in, f, lane, aq);
+        }
 
         const uint32_t orow = io_row(a, in.valid ? in.pt : (uint32_t)(a.P - 1));
         float4 g4 = *reinterpret_cast<const float4*>(a.graw + 4u * orow);
@@ -1154,7 +1207,7 @@ struct MlpBwdJobs {
     float* det_ws;   // deterministic mode: per-block weight-gradient images [gridDim.x][GW_TOTAL]
 };
 
-template <bool QUANT>
+template <bool QUANT, bool SAVED>
 __global__ void __launch_bounds__(512, 1) mlp_bwd_x6cg_kernel(MlpBwdJobs jobs) {
     __shared__ __attribute__((aligned(16))) __bf16 lds[X6_CG_LDS / 2 + X6_ZBLK_ELEMS];
     __shared__ int flags[8];   // ready[0..3], ack[0..3]
@@ -1181,7 +1234,7 @@ __global__ void __launch_bounds__(512, 1) mlp_bwd_x6cg_kernel(MlpBwdJobs jobs) {
     } else {
         QuantRec aq{};
         if constexpr (QUANT) aq = *a.aq;
-        bwd_chain_role<QUANT>(a, img, stA, stG, flags + p, flags + 4 + p, p, lane, aq, blk, nblk, c2b);
+        bwd_chain_role<QUANT, SAVED>(a, img, stA, stG, flags + p, flags + 4 + p, p, lane, aq, blk, nblk, c2b);
     }
 
     // ---- block reduction of the wgrad waves' tiles, one global flush per block. Each wgrad wave
@@ -1260,11 +1313,12 @@ __global__ void __launch_bounds__(256) mlp_wgrad_reduce_kernel(const float* __re
 static bool fits_u32(const MlpArgs& a) {
     const int64_t lim = (int64_t)1 << 31;
     return a.P * a.sp + 16 * a.sl < lim && a.P * a.dsp + 16 * a.dsl < lim && a.P * a.sh_stride + 16 < lim &&
-           16 * (a.P + 32) < lim;
+           16 * (a.P + 32) < lim && (!a.h3 || 64 * (a.P + 31) < lim);
 }
 
 int launch_mlp_fwd_x6(const MlpArgs& a, hipStream_t stream) {
     NERF_REQUIRE(fits_u32(a), "mlp_fwd(x6): %lld points exceed 32-bit indexing", (long long)a.P);
+    NERF_REQUIRE(!a.h3 || !a.aq, "mlp_fwd(x6): saved h3 with A-CAQ (its backward recomputes)");
     const int64_t tiles = (a.P + 31) / 32;
     const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((tiles + 7) / 8, 256 * 2));
     if (a.aq)
@@ -1295,6 +1349,8 @@ int launch_mlp_bwd_x6(const MlpArgs* jobs, int n_jobs, float* det_ws, hipStream_
         NERF_REQUIRE(fits_u32(jobs[k]), "mlp_bwd(x6): %lld points exceed 32-bit indexing", (long long)jobs[k].P);
         NERF_REQUIRE(jobs[k].P > 0, "mlp_bwd(x6): empty job");
         NERF_REQUIRE((jobs[k].aq != nullptr) == (jobs[0].aq != nullptr), "mlp_bwd(x6): mixed quantizer modes");
+        NERF_REQUIRE((jobs[k].h3 != nullptr) == (jobs[0].h3 != nullptr), "mlp_bwd(x6): saved h3 on some jobs only");
+        NERF_REQUIRE(!jobs[k].h3 || (!jobs[k].aq && !jobs[k].rows), "mlp_bwd(x6): saved h3 with A-CAQ or active rows");
         tiles[k] = (jobs[k].P + 31) / 32;
         want[k] = (tiles[k] + 3) / 4;   // blocks of 4 wave pairs, one tile per pair
     }
@@ -1315,9 +1371,11 @@ int launch_mlp_bwd_x6(const MlpArgs* jobs, int n_jobs, float* det_ws, hipStream_
         J.split = (int)std::min<int64_t>(std::max<int64_t>(b0, 1), kMlpBwdMaxBlocks - 1);
     }
     if (jobs[0].aq)
-        hipLaunchKernelGGL(mlp_bwd_x6cg_kernel<true>, dim3((unsigned)blocks), dim3(512), 0, stream, J);
+        hipLaunchKernelGGL((mlp_bwd_x6cg_kernel<true, false>), dim3((unsigned)blocks), dim3(512), 0, stream, J);
+    else if (jobs[0].h3)
+        hipLaunchKernelGGL((mlp_bwd_x6cg_kernel<false, true>), dim3((unsigned)blocks), dim3(512), 0, stream, J);
     else
-        hipLaunchKernelGGL(mlp_bwd_x6cg_kernel<false>, dim3((unsigned)blocks), dim3(512), 0, stream, J);
+        hipLaunchKernelGGL((mlp_bwd_x6cg_kernel<false, false>), dim3((unsigned)blocks), dim3(512), 0, stream, J);
     NERF_CHECK_LAUNCH("mlp_bwd(x6)");
     if (det_ws) {
         for (int k = 0; k < n_jobs; ++k) {

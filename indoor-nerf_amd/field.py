@@ -7,6 +7,8 @@ and NeRFSmall it runs the fused path (FieldFn): hash encoding in a level-major l
 ray's view direction computed once per point inside the MLP kernel's prologue, and the
 sigma := 0 mask in its epilogue — no [P,48] concat and no per-sample SH tensor.
 """
+import os
+
 import torch
 import torch.nn as nn
 
@@ -223,9 +225,17 @@ class FieldFn(torch.autograd.Function):
             view_args = (None, 0, _lib.ptr(viewdirs, "viewdirs"))
         feat_args = (_lib.ptr_at(feat, 2 * row0, "feat"), 2, sl, *view_args, spr, keep_arg)
         w0q, arec = net.quant_state(lambda w0q: _act_calibration(feat_args, P, weights, w0q, n_calib))
-        _lib.call("nerf_mlp_fwd_ord", *feat_args, P, _weights_struct(weights, w0q), _lib.ptr(raw, "raw"),
+        # a training forward keeps layer C1's outputs for the backward (nerf_mlp_fwd_h3: 256 B per point;
+        # the backward then skips C1's recompute) — not with the activation quantizer (its backward
+        # recomputes) or active-point lists (the backward walks other tiles)
+        h3 = None
+        if (_SAVE_H3["on"] and arec is None and not _ACTIVE["on"] and P > 0
+                and any(ctx.needs_input_grad[7:7 + n_tab + 5])):
+            h3 = torch.empty(int(_lib.load().nerf_mlp_h3_bytes(P)) // 4, device=dev, dtype=torch.float32)
+        _lib.call("nerf_mlp_fwd_h3", *feat_args, P, _weights_struct(weights, w0q), _lib.ptr(raw, "raw"),
                   _lib.ptr(o16, "geo", allow_none=True), _lib.ptr(arec, "act_record", allow_none=True), None, 0,
-                  _point_order(order), _lib.stream())
+                  _point_order(order), _lib.ptr(h3, "h3", allow_none=True), _lib.stream())
+        ctx.h3 = h3
         if head:
             raw = _head_forward(o16, raw, keep, head)
         ctx.save_for_backward(pts, viewdirs, feat, keep, o16, w0q, arec, *params)
@@ -269,6 +279,7 @@ class _FieldJob:
         self.sh_rays = ctx.sh_rays
         self.reuse = ctx.reuse     # (role, render.CoarseReuse) or None
         self.frow0, self.order = ctx.frow0, ctx.order   # feature rows from frow0 of feat; the MLP's point order
+        self.h3 = getattr(ctx, "h3", None)               # the forward's saved C1 outputs (or None: recompute)
         self.stream = torch.cuda.current_stream()
 
     def alloc(self):
@@ -299,6 +310,8 @@ class _FieldJob:
         if getattr(self, "act", None) is not None:
             j.rows = _lib.ptr(self.act[0], "active_rows", torch.int32)
             j.d_count = self.count_ptr(0)
+        elif self.h3 is not None:
+            j.h3 = _lib.ptr(self.h3, "h3")
         return j
 
     def find_active(self, jobs):
@@ -342,6 +355,13 @@ class _FieldJob:
 
 
 _DETERMINISTIC = {"on": False, "ws": {}}
+_SAVE_H3 = {"on": os.environ.get("NERF_SAVE_H3", "1") != "0"}   # the env switch: A/B runs
+
+
+def set_save_h3(enabled=True):
+    """Keep layer C1's outputs of a training forward for the backward (default on: 256 B per point,
+    the backward skips C1's recompute, bit-identical); off = recompute (tests, A/B)."""
+    _SAVE_H3["on"] = bool(enabled)
 _BIN_BATCH = {"on": True}
 
 

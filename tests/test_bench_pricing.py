@@ -40,6 +40,7 @@ def test_kernel_variants_traffic_is_the_mean(tmp_path, monkeypatch):
     assert bench.pmc_traffic("nerf_composite_fwd") == 2000.0      # x 2 launches per step = both kernels
     assert bench.pmc_traffic("nerf_composite_bwd") is None         # kernels missing from the summary
     assert bench.base_name("nerf_mlp_fwd_ord") == bench.base_name("nerf_mlp_fwd_q") == "nerf_mlp_fwd"
+    assert bench.base_name("nerf_mlp_fwd_h3") == "nerf_mlp_fwd"
 
 
 def test_merged_compositing_calls_are_priced():

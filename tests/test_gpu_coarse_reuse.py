@@ -129,7 +129,7 @@ def test_coarse_reuse_matches_reencoding(nerf, gpu, parts, R):
 
 def test_coarse_reuse_is_taken(nerf, gpu):
     """The training forward takes the reuse path: two hash gathers (R*S coarse points, R*N importance
-    samples, not R*(S+N)) and the fine MLP in the reuse's point order (nerf_mlp_fwd_ord)."""
+    samples, not R*(S+N)) and the fine MLP in the reuse's point order (nerf_mlp_fwd_h3)."""
     import importlib
     from indoor_nerf_amd import _lib
     rmod = importlib.import_module("indoor_nerf_amd.render")
@@ -154,7 +154,7 @@ def test_coarse_reuse_is_taken(nerf, gpu):
     finally:
         _lib.set_timing(False)
         rmod.CoarseReuse.__init__, hmod.HashEmbedder.encode_into = orig_init, orig_enc
-    assert names.count("nerf_hash_encode_fwd_q") == 2 and names.count("nerf_mlp_fwd_ord") == 2
+    assert names.count("nerf_hash_encode_fwd_q") == 2 and names.count("nerf_mlp_fwd_h3") == 2
     assert gathered == [256 * 64, 256 * 128]
     assert len(plans) == 1 and plans[0].used
     assert out["pts"].shape == (256, 192, 3)

@@ -356,3 +356,53 @@ def test_check_numerics_flags_nan_and_inf(nerf, gpu):
         assert nerf.check_numerics({"rgb_map": out[0], "acc_map": out[2]}) == []
     finally:
         nerf.set_debug(False)
+
+
+def test_saved_h3_matches_recompute_bitwise(nerf, gpu):
+    """The training forward's saved C1 outputs (nerf_mlp_fwd_h3, the backward job's h3) against the
+    backward's own recompute of layer C1: one deterministic training iteration (both nets, coarse-
+    feature reuse, TV) gives bit-identical gradients of every parameter, and the render outputs are
+    the same bits (the forward's h3 is the same fwd_chain arithmetic as the recompute's)."""
+    from indoor_nerf_amd import field, model
+    lo, hi = blender_bbox()
+    args = nerf.make_args(bounding_box=(torch.from_numpy(lo), torch.from_numpy(hi)), finest_res=1024, N_samples=64,
+                          N_importance=128, white_bkgd=True, tv_loss_weight=1e-6)
+    torch.manual_seed(0)
+    kw, _, _, grad_vars, opt = nerf.create_nerf(args, device=gpu)
+    kw.update(near=2.0, far=6.0, pytest=True)
+    with torch.no_grad():
+        tab = closed_form_table(scale=0.2, salt=4)
+        for i, e in enumerate(kw["embed_fn"].embeddings):
+            e.weight.copy_(torch.from_numpy(tab[i]))
+    ro, rd = synthetic_rays(4096, seed=13)
+    rays = (torch.from_numpy(ro).to(gpu), torch.from_numpy(rd).to(gpu))
+    target = torch.rand(4096, 3, device=gpu, generator=torch.Generator(device=gpu).manual_seed(3))
+    calls = []
+    orig = nerf._lib.call
+
+    def spy(name, *a):
+        if name == "nerf_mlp_bwd_batch":   # the jobs' h3 pointers
+            calls.append([bool(a[0][k].h3) for k in range(a[1])])
+        return orig(name, *a)
+
+    def run(save):
+        field.set_save_h3(save)
+        nerf.set_deterministic(True)
+        nerf._lib.call = spy
+        try:
+            loss = model.forward_backward(rays, target, kw, opt, args, 1,
+                                          tv_generator=torch.Generator().manual_seed(5))[0]
+            torch.cuda.synchronize()
+            return float(loss), [p.grad.clone() for p in grad_vars + list(kw["embed_fn"].parameters())]
+        finally:
+            nerf._lib.call = orig
+            nerf.set_deterministic(False)
+            field.set_save_h3(True)
+
+    la, a = run(True)
+    assert calls == [[True, True]]          # both nets' backward read the saved h3
+    lb, b = run(False)
+    assert calls[1:] == [[False, False]]
+    assert la == lb
+    for i, (x, y) in enumerate(zip(a, b)):
+        assert torch.equal(x, y), f"parameter {i}: saved-h3 backward differs from the recompute"
