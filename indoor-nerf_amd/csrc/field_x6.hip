@@ -583,9 +583,6 @@ __device__ __forceinline__ floatx16 ga3_f32(const float* c2b, int t, float b0, f
 // point). The backward then skips C1's recompute (48 of the chain wave's MFMAs and the h2 split, 176
 // VALU, per tile). Nontemporal both ways: the buffer is written once and read once.
 typedef float f32x4_nt __attribute__((ext_vector_type(4)));
-#ifndef NERF_X6_H3_LOAD
-#define NERF_X6_H3_LOAD 1
-#endif
 __device__ __forceinline__ uint32_t h3_off(int64_t tile, int t, int q, int lane) {
     return (((((uint32_t)tile * 2u + (uint32_t)t) * 4u + (uint32_t)q) * 64u) + (uint32_t)lane) * 4u;
 }
@@ -787,23 +784,16 @@ __device__ __forceinline__ void bwd_chain_role(const MlpArgs& a, const __bf16* i
         load_in_x6_bwd(a, n_pts, tile, j, h, in);
 #endif
         ActX6 f;
-        if constexpr (SAVED) {   // h3 from the forward, in flight during layer C0 (NERF_X6_H3_LOAD: 0 before
-            f32x4_nt h3v[8];     // layer 0, 1 before C0, 2 after the chain)
+        if constexpr (SAVED) {   // h3 from the forward, the loads in flight during layer C0 (issued before
+            f32x4_nt h3v[8];     // layer 0 or after the chain instead: the same time, profiles/r06d_ab_saved_h3.jsonl;
+                                 // one tile ahead with the inputs: spills, 360 -> 452 us, tools/variants/)
             auto load_h3 = [&]() {
 #pragma unroll
                 for (int k = 0; k < 8; ++k)
                     h3v[k] = __builtin_nontemporal_load(
                         reinterpret_cast<const f32x4_nt*>(a.h3 + h3_off(tile, k >> 2, k & 3, lane)));
             };
-#if NERF_X6_H3_LOAD == 0
-            load_h3();
-            fwd_chain<QUANT, false>(imt, in, f, lane, aq);
-#elif NERF_X6_H3_LOAD == 1
             fwd_chain<QUANT, false>(imt, in, f, lane, aq, load_h3);
-#else
-            fwd_chain<QUANT, false>(imt, in, f, lane, aq);
-            load_h3();
-#endif
 #pragma unroll
             for (int k = 0; k < 8; ++k)
 #pragma unroll
