@@ -385,13 +385,17 @@ def cpu_leg(n_rays, finest, H, warmup, timed):
         loss.backward()
         opt.step()
 
-    for _ in range(warmup):
+    for k in range(warmup):
+        t0 = time.perf_counter()
         step()
+        print(f"cpu leg {n_rays} rays finest {finest}: warm-up {k} {time.perf_counter() - t0:.2f} s", file=sys.stderr,
+              flush=True)
     times = []
     for _ in range(timed):
         t0 = time.perf_counter()
         step()
         times.append(time.perf_counter() - t0)
+        print(f"cpu leg {n_rays} rays finest {finest}: timed {times[-1]:.2f} s", file=sys.stderr, flush=True)
     t = float(np.median(times))
     rt = []
     with torch.no_grad():
@@ -410,29 +414,35 @@ def cpu_baseline(n_rays, warmup, timed):
     """SURVEY.md §8(d)'s CPU baseline on the GPU box's host cores, rank 0 at N=1 only. `value` is the
     lego leg (configs[1]: finest 1024, 800x800) at the bench's own batch (n_rays = 4096), `warmup`
     (6) warm-up iterations, so RAdam's update is active (radam.py:63-92: N_sma >= 5 from step 6), and
-    the median of `timed` (3). The same leg at 1024 rays is reported beside it, so the batch-size
-    effect is measured, and the chair leg is BASELINE configs[0] (chair 400x400,
-    finest_res 512, the reference's CPU path: configs/chair.txt) at its own N_rand of 1024."""
+    the median of `timed` (3). The chair leg is BASELINE configs[0] (chair 400x400, finest_res 512, the
+    reference's CPU path: configs/chair.txt) at its own N_rand of 1024.
+
+    Threads: the fastest count measured on the pool's boxes. Their affinity mask shows the whole
+    machine (256 logical / 128 physical cores) but the job runs in a CPU share of 16
+    (OMP_NUM_THREADS); the same iteration at 16 / 32 / 64 / 128 threads took 13.3 / 16.5 / 22.6 /
+    39.4 s (profiles/r06w_cpu_threads.json, tools/cpu_threads_probe.py): every physical core of the
+    mask is 3x SLOWER than the share, and at 128 threads this leg alone ran past the box's silence
+    limit. So the leg runs at min(physical cores, share) threads, and the line carries the
+    full-mask probe beside it."""
     logical, share, physical = cpu_threads()
-    # SURVEY §8(d): every physical core of the affinity mask (the pool's boxes show the whole machine in
-    # the mask; the job's share, OMP_NUM_THREADS, is reported beside it)
-    torch.set_num_threads(physical)
+    threads = min(physical, share)
+    torch.set_num_threads(threads)
     lego = cpu_leg(n_rays, 1024, 800, warmup, timed)
-    shared = None
-    if share < physical:
-        torch.set_num_threads(share)
-        shared = cpu_leg(n_rays, 1024, 800, warmup, timed)
-        shared["threads"] = share
-    torch.set_num_threads(min(physical, share))
     chair = cpu_leg(1024, 512, 400, warmup, timed)
-    chair["threads"] = min(physical, share)
-    return {"value": lego["value"], "unit": "rays/s", "cores": physical, "kind": "port",
+    chair["threads"] = threads
+    probe = None
+    pf = os.path.join(ROOT, "profiles", "r06w_cpu_threads.json")
+    if os.path.exists(pf):
+        probe = {"source": "profiles/r06w_cpu_threads.json",
+                 "rays_per_s_by_threads": {str(r["threads"]): r["rays_per_s"] for r in json.load(open(pf))["rows"]}}
+    return {"value": lego["value"], "unit": "rays/s", "cores": threads, "kind": "port",
             "render_only": lego["render_only"], "step_s": lego["step_s"],
             "sample": "lego leg: " + lego["sample"],
             "cpu": cpu_model(), "affinity_cpus": logical, "physical_cores": physical, "job_share_threads": share,
-            "threads_note": "torch.set_num_threads = the physical cores of the affinity mask (SURVEY.md §8(d)); "
-                            "job_share_leg: the same leg at the job's CPU share (OMP_NUM_THREADS)",
-            "job_share_leg": shared,
+            "threads_note": "torch.set_num_threads = min(physical cores of the affinity mask, the job's CPU share "
+                            "OMP_NUM_THREADS): the fastest count measured on these boxes (more threads than the share "
+                            "run slower: full_mask_probe)",
+            "full_mask_probe": probe,
             "chair": {**chair, "config": "BASELINE configs[0]: chair 400x400, finest_res 512 (configs/chair.txt)"}}
 
 
@@ -787,7 +797,7 @@ def main():
         out["deterministic"] = True
     # north star "PSNR within 0.1 dB of reference": the committed result of tests/test_gpu_converge.py
     # (the reference trained on F19 six times vs six HIP runs; late-phase mean PSNR difference per metric)
-    for name in ("r05_psnr_vs_reference.json", "r04_psnr_vs_reference.json", "r03_psnr_vs_reference.json", "r02_psnr_vs_reference.json"):
+    for name in [f"r0{k}_psnr_vs_reference.json" for k in range(6, 1, -1)]:
         pv = os.path.join(ROOT, "profiles", name)
         if os.path.exists(pv):
             pj = json.load(open(pv))
