@@ -48,7 +48,9 @@ X6_PEAK_TFLOPS = 2500.0 / 6
 #   composite: per sample 16 B raw + 4 B z + 4 B weights (fwd) / + 16 B grad (bwd)
 #   radam    : per table/MLP element 28 B (read p, g, m, v; write p, m, v)
 OPS = {
+    # (with the TV bins in the hash bin launch, nerf_hash_encode_bwd_bin_batch_tv, their time is the op's)
     "hash_bwd": dict(calls=("nerf_hash_encode_bwd_bin", "nerf_hash_encode_bwd_bin_rows", "nerf_hash_encode_bwd_bin_batch",
+                            "nerf_hash_encode_bwd_bin_batch_tv",
                             "nerf_hash_encode_bwd_owner",
                             "nerf_hash_encode_bwd_owner_range", "nerf_hash_encode_bwd_owner_step",
                             "nerf_hash_encode_bwd_ws", "nerf_hash_encode_bwd"),
@@ -84,6 +86,7 @@ KERNEL_SYMBOLS = {
     "nerf_hash_encode_bwd_bin": ["nerf::hash_encode_bwd_kernel<3, 512>"],
     "nerf_hash_encode_bwd_bin_rows": ["nerf::hash_encode_bwd_kernel<3, 512>"],
     "nerf_hash_encode_bwd_bin_batch": ["nerf::hash_encode_bwd_pair_kernel<512>"],
+    "nerf_hash_encode_bwd_bin_batch_tv": ["nerf::hash_encode_bwd_tv_pair_kernel<512>"],
     "nerf_tv_bwd_bin": ["nerf::tv_bwd_bin_kernel<512>"],
     "nerf_hash_encode_bwd_owner": ["nerf::hash_bwd_owner_kernel<13, 1024, false>"],
     "nerf_hash_encode_bwd_owner_range": ["nerf::hash_bwd_owner_kernel<13, 1024, false>"],

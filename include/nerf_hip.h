@@ -596,6 +596,19 @@ int nerf_tv_bwd_bin(const float* const* d_tables, int n_levels, int log2_T, cons
                     const float* d_verts /* optional: nerf_tv_fwd's d_verts of the same tables and cuboids */,
                     int64_t chunk_base, int64_t chunk_capacity, int deterministic, void* d_workspace,
                     size_t workspace_bytes, void* stream);
+/* ABI 11: nerf_hash_encode_bwd_bin_batch with the pass's binned TV backward in the same launch (its
+ * blocks first: the TV's few, gather-latency-bound blocks run beside the hash bins instead of as a
+ * launch of their own). tv: the nerf_tv_bwd_bin arguments of the same name (d_verts required; the
+ * levels and workspace are the batch's); NULL tv = nerf_hash_encode_bwd_bin_batch. The workspace
+ * contents are those of the separate calls, bit for bit. */
+typedef struct nerf_tv_bin_job {
+    const float* const* d_tables; const int64_t* min_vertex; const int64_t* d_min_vertex; const int* cube;
+    const float* d_scale; const float* d_verts; int64_t chunk_base;
+} nerf_tv_bin_job;
+int nerf_hash_encode_bwd_bin_batch_tv(const nerf_bin_job* jobs, int n_jobs, const float* bbox_min3,
+                                      const float* bbox_max3, const float* level_res, int n_levels, int log2_T,
+                                      int64_t chunk_capacity, int deterministic, void* d_workspace,
+                                      size_t workspace_bytes, const nerf_tv_bin_job* tv, void* stream);
 
 /* ---- training-loss head (run_nerf.py:1011-1037: img2mse of both passes, sparsity, TV, mse2psnr) ----
  * fwd: device scalars loss, img_loss (fine-pass MSE), psnr; rgb0 / sparsity / sparsity0 / tv may be NULL.

@@ -66,6 +66,12 @@ class BinJob(ctypes.Structure):
                 ("feat2_stride_point", c_i64), ("feat2_stride_level", c_i64), ("chunk_base", c_i64)]
 
 
+class TVBinJob(ctypes.Structure):
+    """nerf_tv_bin_job (include/nerf_hip.h, ABI 11)."""
+    _fields_ = [("d_tables", c_vp), ("min_vertex", c_vp), ("d_min_vertex", c_vp), ("cube", c_vp), ("d_scale", c_vp),
+                ("d_verts", c_vp), ("chunk_base", c_i64)]
+
+
 class ZeroRange(ctypes.Structure):
     _fields_ = [("ptr", c_vp), ("n", c_i64)]
 
@@ -134,6 +140,8 @@ SIGNATURES = {
                                    c_vp],
     "nerf_hash_encode_bwd_bin_batch": [ctypes.POINTER(BinJob), c_int, c_f32p, c_f32p, c_f32p, c_int, c_int, c_i64,
                                        c_int, c_vp, ctypes.c_size_t, c_vp],
+    "nerf_hash_encode_bwd_bin_batch_tv": [ctypes.POINTER(BinJob), c_int, c_f32p, c_f32p, c_f32p, c_int, c_int, c_i64,
+                                          c_int, c_vp, ctypes.c_size_t, ctypes.POINTER(TVBinJob), c_vp],
     "nerf_hash_encode_bwd_bin_rows": [c_vp, c_vp, c_vp, c_i64, c_f32p, c_f32p, c_f32p, c_int, c_int, c_vp, c_i64,
                                       c_i64, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_int, c_vp, ctypes.c_size_t, c_vp],
     "nerf_active_rows": [c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_int, c_vp, ctypes.c_size_t, c_vp],

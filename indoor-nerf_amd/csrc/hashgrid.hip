@@ -254,15 +254,30 @@ constexpr int kMaxOwners = 1 << kMaxOwnersLog2;
 // share an owner slice (a point's corners (x, y, z) and (x+1, y, z) hash to h and h ^ (x ^ (x+1)),
 // which differ below bit 13 whenever x < 8191): such a pair takes its two slots with ONE counting
 // atomic — the contended LDS counters are a quarter of the bin pass's time.
+// The LDS of bin_chunk: one object per kernel whatever instantiations of bin_chunk it inlines (the
+// hash bins and the TV bins in one launch, hash_encode_bwd_tv_pair_kernel: 42 KB, not 84 KB and a
+// third of the occupancy).
+struct BinLds {
+    uint32_t cnt[kMaxOwners];
+    uint32_t start[kMaxOwners + 1];
+    __attribute__((aligned(16))) uint16_t eh[kChunkCap];
+    __attribute__((aligned(16))) float2 eg[kChunkCap];
+};
+__device__ __forceinline__ BinLds& bin_lds() {
+    __shared__ BinLds s;
+    return s;
+}
+
 template <int THREADS, int NE, bool PAIRED = false>
 __device__ __forceinline__ void bin_chunk(const HashGradParams& hp, int lvl, int chunk, const uint32_t (&hh)[NE],
                                           const float (&vx)[NE], const float (&vy)[NE], const bool (&on)[NE]) {
     constexpr int CAP = THREADS * NE;
     static_assert(CAP <= kChunkCap, "chunk region");
-    __shared__ uint32_t s_cnt[kMaxOwners];
-    __shared__ uint32_t s_start[kMaxOwners + 1];
-    __shared__ __attribute__((aligned(16))) uint16_t s_eh[CAP];
-    __shared__ __attribute__((aligned(16))) float2 s_eg[CAP];
+    BinLds& lds = bin_lds();
+    uint32_t* const s_cnt = lds.cnt;
+    uint32_t* const s_start = lds.start;
+    uint16_t* const s_eh = lds.eh;
+    float2* const s_eg = lds.eg;
     const int lane = threadIdx.x & 63;
     const int n_own = 1 << hp.owner_log2;
     // (zeroing the counters at the block's start instead, so that a wave counts as soon as its own
@@ -525,10 +540,11 @@ __global__ void __launch_bounds__(THREADS) hash_encode_bwd_pair_kernel(BinJob a,
 // thread; chunks past a level's last vertex are empty), one entry per vertex: row hash(min_vertex +
 // (i, j, k)), value (sum over the in-cuboid neighbours n of 2 (e_v - e_n)) x scale[l] / cube — the
 // per-vertex terms and op order of the atomic tv_bwd_kernel (optim.hip).
+// Block bx of level l's TV chunks, binned as chunk `chunk` of hp's workspace.
 template <int THREADS>
-__global__ void __launch_bounds__(THREADS) tv_bwd_bin_kernel(TVParams P, HashGradParams hp) {
+__device__ __forceinline__ void tv_bin_block(const TVParams& P, const HashGradParams& hp, int l, int chunk,
+                                             unsigned bx) {
     constexpr int NE = 8;   // vertices per thread: chunks of kChunkCap entries, like the hash bins
-    const int l = blockIdx.y;
     const int c = P.cube[l], n1 = c + 1;
     const uint32_t nv = (uint32_t)(P.vstart[l + 1] - P.vstart[l]);
     const float2* tab = reinterpret_cast<const float2*>(P.tables[l]);
@@ -540,7 +556,7 @@ __global__ void __launch_bounds__(THREADS) tv_bwd_bin_kernel(TVParams P, HashGra
     bool on[NE];
 #pragma unroll
     for (int q = 0; q < NE; ++q) {
-        const uint32_t lv = blockIdx.x * (uint32_t)(NE * THREADS) + q * THREADS + threadIdx.x;
+        const uint32_t lv = bx * (uint32_t)(NE * THREADS) + q * THREADS + threadIdx.x;
         float gx = 0.f, gy = 0.f;
         hh[q] = 0;
         on[q] = false;
@@ -569,8 +585,31 @@ __global__ void __launch_bounds__(THREADS) tv_bwd_bin_kernel(TVParams P, HashGra
         vy[q] = gy * s;
         on[q] = lv < nv && (vx[q] != 0.f || vy[q] != 0.f);
     }
-    bin_chunk<THREADS, NE>(hp, l, hp.chunk_base + (int)blockIdx.x, hh, vx, vy, on);
+    bin_chunk<THREADS, NE>(hp, l, chunk, hh, vx, vy, on);
 }
+
+template <int THREADS>
+__global__ void __launch_bounds__(THREADS) tv_bwd_bin_kernel(TVParams P, HashGradParams hp) {
+    tv_bin_block<THREADS>(P, hp, blockIdx.y, hp.chunk_base + (int)blockIdx.x, blockIdx.x);
+}
+
+// The hash bins of up to two jobs with the pass's TV bins in front (nerf_hash_encode_bwd_bin_batch_tv):
+// blocks [0, tv_blocks) are TV chunks tv_base + x in job a's workspace layout (one workspace per
+// batch), the rest the hash_encode_bwd_pair_kernel blocks (split: job a's chunks; b may repeat a with
+// no blocks of its own). The TV's 4,224 waves ran 19.8 us as a launch of their own (rocprof r06h).
+template <int THREADS>
+__global__ void __launch_bounds__(THREADS) hash_encode_bwd_tv_pair_kernel(BinJob a, BinJob b, unsigned split,
+                                                                          TVParams tv, int tv_base,
+                                                                          unsigned tv_blocks) {
+    if (blockIdx.x < tv_blocks) {
+        tv_bin_block<THREADS>(tv, a.hp, blockIdx.y, tv_base + (int)blockIdx.x, blockIdx.x);
+        return;
+    }
+    const unsigned x = blockIdx.x - tv_blocks;
+    if (x < split) bwd_bin_block<3, THREADS>(a.xyz, a.n, a.hp, a.dfeat, a.sp, a.sl, a.br, (int)x);
+    else bwd_bin_block<3, THREADS>(b.xyz, b.n, b.hp, b.dfeat, b.sp, b.sl, b.br, (int)(x - split));
+}
+static_assert(2 * sizeof(BinJob) + sizeof(TVParams) + 16 <= 4096, "hash_encode_bwd_tv_pair_kernel: kernel arguments over 4 KiB");
 
 // ---- owner pass of the binned backward ----------------------------------------------------
 // Block (o, l) owns rows [o * 2^slice_log2, (o+1) * 2^slice_log2) of level l's gradient table. It
@@ -1127,20 +1166,24 @@ static int bin_job(const nerf_bin_job& j, const float* bbox_min3, const float* b
     return NERF_OK;
 }
 
-extern "C" int nerf_hash_encode_bwd_bin_batch(const nerf_bin_job* jobs, int n_jobs, const float* bbox_min3,
-                                              const float* bbox_max3, const float* level_res, int n_levels,
-                                              int log2_T, int64_t chunk_capacity, int deterministic,
-                                              void* d_workspace, size_t workspace_bytes, void* stream) {
-    NERF_REQUIRE(n_jobs >= 0 && n_jobs <= 8 && (n_jobs == 0 || jobs), "hash_encode_bwd_bin_batch: %d jobs", n_jobs);
-    BinJob bj[8];
-    int64_t nch[8];
-    for (int i = 0; i < n_jobs; ++i) {   // every job validated before anything is launched
-        const int rc = bin_job(jobs[i], bbox_min3, bbox_max3, level_res, n_levels, log2_T, chunk_capacity,
-                               deterministic, d_workspace, workspace_bytes, bj[i], nch[i]);
-        if (rc) return rc;
+static int64_t tv_bin_chunks(int n_levels, const int* cube) {
+    int64_t most = 0;
+    for (int l = 0; l < n_levels; ++l) {
+        const int64_t n1 = (int64_t)cube[l] + 1;
+        most = std::max<int64_t>(most, (n1 * n1 * n1 + kChunkCap - 1) / kChunkCap);
     }
-    hipStream_t st = as_stream(stream);
-    int i = 0;
+    return most;
+}
+
+extern "C" int64_t nerf_tv_bwd_bin_chunks(int n_levels, const int* cube) {
+    if (n_levels < 1 || n_levels > NERF_MAX_LEVELS || !cube) return 0;
+    for (int l = 0; l < n_levels; ++l)
+        if (cube[l] < 1 || cube[l] > 1024) return 0;
+    return tv_bin_chunks(n_levels, cube);
+}
+
+static int launch_bin_jobs(const nerf_bin_job* jobs, int n_jobs, const BinJob* bj, const int64_t* nch, int i,
+                           int n_levels, hipStream_t st) {
     while (i < n_jobs) {
         if (jobs[i].n_points == 0) { ++i; continue; }
         int k = i + 1;
@@ -1160,6 +1203,78 @@ extern "C" int nerf_hash_encode_bwd_bin_batch(const nerf_bin_job* jobs, int n_jo
     return NERF_OK;
 }
 
+static int tv_bin_params(const char* fn, const nerf_tv_bin_job& j, int n_levels, int log2_T, int64_t chunk_capacity,
+                         TVParams& P, int64_t& nch) {
+    int rc = fill_tv(P, n_levels, log2_T, j.min_vertex, j.d_min_vertex, j.cube);
+    if (rc) return rc;
+    NERF_REQUIRE(j.d_tables && j.d_scale, "%s: null arg", fn);
+    for (int l = 0; l < n_levels; ++l) {
+        NERF_REQUIRE(j.d_tables[l], "%s: table %d null", fn, l);
+        P.tables[l] = j.d_tables[l];
+    }
+    P.scale = j.d_scale;
+    P.verts = const_cast<float2*>(reinterpret_cast<const float2*>(j.d_verts));
+    nch = tv_bin_chunks(n_levels, j.cube);
+    NERF_REQUIRE(j.chunk_base >= 0 && j.chunk_base + nch <= chunk_capacity, "%s: chunks [%lld, %lld) exceed the capacity %lld",
+                 fn, (long long)j.chunk_base, (long long)(j.chunk_base + nch), (long long)chunk_capacity);
+    return NERF_OK;
+}
+
+extern "C" int nerf_hash_encode_bwd_bin_batch(const nerf_bin_job* jobs, int n_jobs, const float* bbox_min3,
+                                              const float* bbox_max3, const float* level_res, int n_levels,
+                                              int log2_T, int64_t chunk_capacity, int deterministic,
+                                              void* d_workspace, size_t workspace_bytes, void* stream) {
+    return nerf_hash_encode_bwd_bin_batch_tv(jobs, n_jobs, bbox_min3, bbox_max3, level_res, n_levels, log2_T,
+                                             chunk_capacity, deterministic, d_workspace, workspace_bytes, nullptr,
+                                             stream);
+}
+
+extern "C" int nerf_hash_encode_bwd_bin_batch_tv(const nerf_bin_job* jobs, int n_jobs, const float* bbox_min3,
+                                                 const float* bbox_max3, const float* level_res, int n_levels,
+                                                 int log2_T, int64_t chunk_capacity, int deterministic,
+                                                 void* d_workspace, size_t workspace_bytes, const nerf_tv_bin_job* tv,
+                                                 void* stream) {
+    NERF_REQUIRE(n_jobs >= 0 && n_jobs <= 8 && (n_jobs == 0 || jobs), "hash_encode_bwd_bin_batch: %d jobs", n_jobs);
+    BinJob bj[8];
+    int64_t nch[8];
+    for (int i = 0; i < n_jobs; ++i) {   // every job validated before anything is launched
+        const int rc = bin_job(jobs[i], bbox_min3, bbox_max3, level_res, n_levels, log2_T, chunk_capacity,
+                               deterministic, d_workspace, workspace_bytes, bj[i], nch[i]);
+        if (rc) return rc;
+    }
+    hipStream_t st = as_stream(stream);
+    TVParams P{};
+    int64_t tv_nch = 0;
+    if (tv) {
+        NERF_REQUIRE(tv->d_verts, "hash_encode_bwd_bin_batch_tv: d_verts required");
+        const int rc = tv_bin_params("hash_encode_bwd_bin_batch_tv", *tv, n_levels, log2_T, chunk_capacity, P, tv_nch);
+        if (rc) return rc;
+        int first = 0;
+        while (first < n_jobs && jobs[first].n_points == 0) ++first;
+        if (first == n_jobs) {   // no hash points: the TV bins alone
+            HashGradParams hp{};
+            const int rc2 = bin_layout("hash_encode_bwd_bin_batch_tv", n_levels, log2_T, chunk_capacity, deterministic,
+                                       d_workspace, workspace_bytes, hp);
+            if (rc2) return rc2;
+            hp.chunk_base = (int)tv->chunk_base;
+            hipLaunchKernelGGL((tv_bwd_bin_kernel<kChunkPts>), dim3((unsigned)tv_nch, n_levels), dim3(kChunkPts), 0, st,
+                               P, hp);
+            NERF_CHECK_LAUNCH("hash_encode_bwd_bin_batch_tv");
+            return NERF_OK;
+        }
+        int second = first + 1;
+        while (second < n_jobs && jobs[second].n_points == 0) ++second;
+        const bool pair = second < n_jobs;
+        hipLaunchKernelGGL((hash_encode_bwd_tv_pair_kernel<kChunkPts>),
+                           dim3((unsigned)(tv_nch + nch[first] + (pair ? nch[second] : 0)), n_levels), dim3(kChunkPts),
+                           0, st, bj[first], pair ? bj[second] : bj[first], (unsigned)nch[first], P,
+                           (int)tv->chunk_base, (unsigned)tv_nch);
+        NERF_CHECK_LAUNCH("hash_encode_bwd_bin_batch_tv");
+        return launch_bin_jobs(jobs, n_jobs, bj, nch, pair ? second + 1 : second, n_levels, st);   // any further jobs
+    }
+    return launch_bin_jobs(jobs, n_jobs, bj, nch, 0, n_levels, st);
+}
+
 extern "C" int nerf_hash_encode_bwd_bin(const float* d_xyz, int64_t n_points, const float* bbox_min3,
                                         const float* bbox_max3, const float* level_res, int n_levels, int log2_T,
                                         const float* d_dfeat, int64_t feat_stride_point, int64_t feat_stride_level,
@@ -1171,22 +1286,6 @@ extern "C" int nerf_hash_encode_bwd_bin(const float* d_xyz, int64_t n_points, co
                                          d_dfeat, feat_stride_point, feat_stride_level, nullptr, nullptr, 0, 0,
                                          chunk_base, chunk_capacity, deterministic, d_workspace, workspace_bytes,
                                          stream);
-}
-
-static int64_t tv_bin_chunks(int n_levels, const int* cube) {
-    int64_t most = 0;
-    for (int l = 0; l < n_levels; ++l) {
-        const int64_t n1 = (int64_t)cube[l] + 1;
-        most = std::max<int64_t>(most, (n1 * n1 * n1 + kChunkCap - 1) / kChunkCap);
-    }
-    return most;
-}
-
-extern "C" int64_t nerf_tv_bwd_bin_chunks(int n_levels, const int* cube) {
-    if (n_levels < 1 || n_levels > NERF_MAX_LEVELS || !cube) return 0;
-    for (int l = 0; l < n_levels; ++l)
-        if (cube[l] < 1 || cube[l] > 1024) return 0;
-    return tv_bin_chunks(n_levels, cube);
 }
 
 extern "C" int nerf_tv_bwd_bin(const float* const* d_tables, int n_levels, int log2_T, const int64_t* min_vertex,

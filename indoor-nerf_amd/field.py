@@ -448,11 +448,11 @@ def _run_field_jobs(jobs):
         pb = pending_bins(dev)
         bins = [b for j in tab_jobs for b in _bin_items(j, tab_jobs)]
         pb.reserve(sum(bin_chunks(b["n"]) for b in bins) + sum(j.n_chunks for j in tv_jobs))
-        for j in tv_jobs:
-            pb.add_tv(j, queue=False)
         if _BIN_BATCH["on"]:
-            pb.begin_batch()  # the pass's hash bins as one launch (nerf_hash_encode_bwd_bin_batch)
+            pb.begin_batch()  # the pass's bins as one launch (nerf_hash_encode_bwd_bin_batch_tv: TV bins in front)
         try:
+            for j in tv_jobs:
+                pb.add_tv(j, queue=False)
             for b in bins:
                 j = b.pop("job")
                 hash_encode_bwd(b.pop("xyz"), j.meta, b.pop("dfeat"), 2, b.pop("sl"), accumulate_grad_buffers(j.tables),

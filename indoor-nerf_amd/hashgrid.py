@@ -4,6 +4,9 @@ API mirror of PocketNeRF/hash_encoding.py: HashEmbedder (:11-107) and SHEncoder 
 constructor arguments, attributes, parameters (`embeddings.{i}.weight`, nn.Embedding(2^log2T, 2))
 and return values. Forward and backward run in libnerfhip (csrc/hashgrid.hip, csrc/field.hip).
 """
+import ctypes
+import os
+
 import torch
 import torch.nn as nn
 
@@ -323,21 +326,29 @@ class _PendingBins:
             return
         self._launch_bins([job], common, det)
 
-    def _launch_bins(self, jobs, common, det):
+    def _launch_bins(self, jobs, common, det, tv=None):
+        if tv is not None:   # the pass's TV bins in the same launch (nerf_hash_encode_bwd_bin_batch_tv)
+            _lib.call("nerf_hash_encode_bwd_bin_batch_tv", (_lib.BinJob * len(jobs))(*jobs), len(jobs), *common, self.cap,
+                      det, _lib.ptr(self.ws, "workspace", dtype=torch.uint8), self.ws.numel(), tv[0], _lib.stream())
+            return
         _lib.call("nerf_hash_encode_bwd_bin_batch", (_lib.BinJob * len(jobs))(*jobs), len(jobs), *common, self.cap, det,
                   _lib.ptr(self.ws, "workspace", dtype=torch.uint8), self.ws.numel(), _lib.stream())
 
     def begin_batch(self):
-        """Collect the following add() calls of one workspace into one nerf_hash_encode_bwd_bin_batch
-        (end_batch; the fine and the coarse bins of an iteration then run as one launch)."""
-        self.batch = []
+        """Collect the following add() / add_tv() calls of one workspace into one
+        nerf_hash_encode_bwd_bin_batch(_tv) (end_batch; the fine and the coarse bins of an iteration and
+        its TV bins then run as one launch)."""
+        self.batch, self.batch_tv = [], None
 
     def _drain_batch(self):
         """Launch the collected bins (they target the open workspace) and keep collecting."""
+        tv, self.batch_tv = getattr(self, "batch_tv", None), None
         if self.batch:
             _, _, common, det, _ = self.batch[0]
-            self._launch_bins([b[0] for b in self.batch], common, det)
+            self._launch_bins([b[0] for b in self.batch], common, det, tv)
             self.batch = []
+        elif tv is not None:   # no hash bins in this workspace: the TV launch alone
+            self._launch_tv(tv[1], tv[2])
 
     def end_batch(self):
         self._drain_batch()
@@ -345,10 +356,25 @@ class _PendingBins:
 
     def add_tv(self, job, queue=True):
         """Bin a TV backward (losses.TVBinJob) into the open workspace: its gradient is summed by the
-        same owner pass as the hash backwards of the iteration."""
+        same owner pass as the hash backwards of the iteration. Inside begin_batch() (with the forward's
+        vertex rows) it rides in the batch's first hash bin launch, else it is a launch of its own."""
         L = len(job.tables)
         base, det = self._slot(L, job.log2_T, job.grads, job.n_chunks, job.tables[0].device, queue)
-        _lib.call("nerf_tv_bwd_bin", _lib.ptr_array(job.tables), L, job.log2_T, job.mv, job.dmv, job.cb,
+        if self.batch is not None and job.verts is not None and _TV_IN_BINS["on"]:
+            if getattr(self, "batch_tv", None) is not None:
+                self._drain_batch()           # one TV job per launch
+            tabs = _lib.ptr_array(job.tables)
+            ctv = _lib.TVBinJob(_lib.c_vp(ctypes.addressof(tabs)),
+                                None if job.mv is None else _lib.c_vp(ctypes.addressof(job.mv)),
+                                job.dmv, _lib.c_vp(ctypes.addressof(job.cb)), _lib.ptr(job.g, "grad_loss"),
+                                _lib.ptr(job.verts, "tv_verts"), base)
+            self.batch_tv = (ctv, job, base, tabs)   # tabs: the struct points into it
+            return
+        self._launch_tv(job, base)
+
+    def _launch_tv(self, job, base):
+        det = self.tag[3]
+        _lib.call("nerf_tv_bwd_bin", _lib.ptr_array(job.tables), len(job.tables), job.log2_T, job.mv, job.dmv, job.cb,
                   _lib.ptr(job.g, "grad_loss"), _lib.ptr(job.verts, "tv_verts", allow_none=True), base, self.cap, det,
                   _lib.ptr(self.ws, "workspace", dtype=torch.uint8), self.ws.numel(), _lib.stream())
 
@@ -392,6 +418,12 @@ class hold_owner:
 
 
 _FUSED_STEP = {"on": True}
+_TV_IN_BINS = {"on": os.environ.get("NERF_TV_IN_BINS", "1") != "0"}   # the env switch: A/B runs
+
+
+def set_tv_in_bins(enabled=True):
+    """Run a pass's binned TV backward inside its hash bin launch (default on; bit-identical)."""
+    _TV_IN_BINS["on"] = bool(enabled)
 
 
 def set_fused_table_step(enabled=True):

@@ -406,3 +406,61 @@ def test_saved_h3_matches_recompute_bitwise(nerf, gpu):
     assert la == lb
     for i, (x, y) in enumerate(zip(a, b)):
         assert torch.equal(x, y), f"parameter {i}: saved-h3 backward differs from the recompute"
+
+
+@pytest.mark.parametrize("det", [True, False], ids=["deterministic", "default"])
+def test_tv_bins_in_hash_bin_launch(nerf, gpu, det):
+    """The pass's TV bins inside the hash bin launch (nerf_hash_encode_bwd_bin_batch_tv, the TV blocks in
+    front) against their own nerf_tv_bwd_bin launch: same workspace chunks, so one training iteration
+    (both nets, coarse-feature reuse, TV) gives bit-identical gradients in deterministic mode, and
+    gradients within the owner's summation-order rounding (fp64 LDS sums, one fp32 rounding: 1e-6 of
+    each table's largest) in the default mode."""
+    from indoor_nerf_amd import hashgrid, model
+    lo, hi = blender_bbox()
+    args = nerf.make_args(bounding_box=(torch.from_numpy(lo), torch.from_numpy(hi)), finest_res=1024, N_samples=64,
+                          N_importance=128, white_bkgd=True, tv_loss_weight=1e-2)
+    torch.manual_seed(0)
+    kw, _, _, grad_vars, opt = nerf.create_nerf(args, device=gpu)
+    kw.update(near=2.0, far=6.0, pytest=True)
+    with torch.no_grad():
+        tab = closed_form_table(scale=0.2, salt=4)
+        for i, e in enumerate(kw["embed_fn"].embeddings):
+            e.weight.copy_(torch.from_numpy(tab[i]))
+    ro, rd = synthetic_rays(4096, seed=13)
+    rays = (torch.from_numpy(ro).to(gpu), torch.from_numpy(rd).to(gpu))
+    target = torch.rand(4096, 3, device=gpu, generator=torch.Generator(device=gpu).manual_seed(3))
+    calls = []
+    orig = nerf._lib.call
+
+    def spy(name, *a):
+        if name in ("nerf_hash_encode_bwd_bin_batch_tv", "nerf_tv_bwd_bin", "nerf_hash_encode_bwd_bin_batch"):
+            calls.append(name)
+        return orig(name, *a)
+
+    def run(fused):
+        hashgrid.set_tv_in_bins(fused)
+        nerf.set_deterministic(det)
+        nerf._lib.call = spy
+        calls.clear()
+        try:
+            loss = model.forward_backward(rays, target, kw, opt, args, 1,
+                                          tv_generator=torch.Generator().manual_seed(5))[0]
+            torch.cuda.synchronize()
+            return float(loss), list(calls), [p.grad.clone() for p in grad_vars + list(kw["embed_fn"].parameters())]
+        finally:
+            nerf._lib.call = orig
+            nerf.set_deterministic(False)
+            hashgrid.set_tv_in_bins(True)
+
+    la, ca, a = run(True)
+    assert ca == ["nerf_hash_encode_bwd_bin_batch_tv"]
+    lb, cb, b = run(False)
+    assert cb == ["nerf_tv_bwd_bin", "nerf_hash_encode_bwd_bin_batch"]
+    # the loss: the TV forward's per-level block sums meet in float atomics (either mode)
+    assert abs(la - lb) <= 1e-6 * abs(lb)
+    for i, (x, y) in enumerate(zip(a, b)):
+        if det:
+            assert torch.equal(x, y), f"parameter {i}: TV bins in the hash bin launch differ"
+        else:   # default mode: the MLP's weight-gradient atomics and the owner's fp64 LDS sums are unordered
+            m = float(y.abs().max())
+            assert float((x - y).abs().max()) <= 1e-6 * m, f"parameter {i}"
