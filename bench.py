@@ -545,7 +545,10 @@ def main():
     from indoor_nerf_amd.synthetic import blender_bbox, blender_rays, llff_bbox, llff_rays
 
     wl = WORKLOADS[a.workload]
-    rank, world, local = nerf.init_process_group()
+    # NERF_DIST_FORCE=1: a one-rank process group (RCCL on one GPU) running the N > 1 code path — ZeRO-1
+    # reduce-scatter / RAdam on the shard / gated all-gather — as a hardware rehearsal of it
+    force_dist = os.environ.get("NERF_DIST_FORCE") == "1"
+    rank, world, local = nerf.init_process_group(force=force_dist)
     dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))   # ranks > GPUs only in rehearsals
     torch.cuda.set_device(dev)
     strong = a.scaling == "strong"
@@ -594,7 +597,7 @@ def main():
         kw["embed_fn"].current_step = kw["embed_fn"].warmup_steps   # past the 500-call warm-up (hash_encoding.py:97)
     params = grad_vars + list(kw["embed_fn"].parameters())
     nerf.broadcast_params(params)
-    zero = world > 1 and a.zero and a.mode == "train"
+    zero = (world > 1 or force_dist) and a.zero and a.mode == "train"
     # defer_tables: no memset of the 64 MiB of table gradients; the owner pass overwrites them.
     # ZeRO-1 with --overlap: two gradient buckets (MLP + table levels 0..7 | levels 8..15), the first
     # reduce-scattered while the owner pass sums the second (dist.ShardedOptimizer)
@@ -613,7 +616,7 @@ def main():
         sharded = nerf.ShardedOptimizer(opt, arena, overlap=bool(a.overlap))
         hook, post = sharded.reduce_grads, sharded.gather_params
     else:
-        hook = (lambda: arena.allreduce_mean()) if world > 1 else None
+        hook = (lambda: arena.allreduce_mean()) if (world > 1 or force_dist) else None
 
     gstep = None
     if a.mode == "train" and a.graph:
@@ -798,6 +801,9 @@ def main():
     }
     if a.deterministic:
         out["deterministic"] = True
+    if force_dist:
+        out["dist_rehearsal"] = (f"one-rank {torch.distributed.get_backend()} process group: the N > 1 code path "
+                                 f"({'ZeRO-1' if zero else 'all-reduce'}), collectives of one rank")
     # north star "PSNR within 0.1 dB of reference": the committed result of tests/test_gpu_converge.py
     # (the reference trained on F19 six times vs six HIP runs; late-phase mean PSNR difference per metric)
     for name in [f"r0{k}_psnr_vs_reference.json" for k in range(6, 1, -1)]:

@@ -20,10 +20,11 @@ def env_rank_world():
     return int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1)), int(os.environ.get("LOCAL_RANK", 0))
 
 
-def init_process_group(backend=None):
-    """Init from torchrun's env (RANK/WORLD_SIZE/MASTER_*); no-op for a single process."""
+def init_process_group(backend=None, force=False):
+    """Init from torchrun's env (RANK/WORLD_SIZE/MASTER_*); no-op for a single process unless `force`
+    (a one-rank process group: the multi-rank code path over RCCL on one GPU, bench.py NERF_DIST_FORCE)."""
     rank, world, local = env_rank_world()
-    if world == 1 or (dist.is_available() and dist.is_initialized()):
+    if (world == 1 and not force) or (dist.is_available() and dist.is_initialized()):
         return rank, world, local
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29517")
