@@ -42,7 +42,7 @@ def _cu_mask(rank, world):
         os.environ["HSA_CU_MASK"] = f"0:{rank * n}-{rank * n + n - 1}"
 
 
-def _init(rank, world, port):
+def _init(rank, world, port, backend="gloo"):
     import sys
     _cu_mask(rank, world)
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -52,7 +52,7 @@ def _init(rank, world, port):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK="0")
     from indoor_nerf_amd.dist import init_process_group
-    init_process_group(backend="gloo")
+    init_process_group(backend=backend, force=True)   # force: a one-rank group too (the RCCL rehearsal)
     torch.cuda.set_device(0)
 
 
@@ -160,12 +160,12 @@ def test_sharded_graphed_training_replicas_agree(tmp_path, overlap):
         assert torch.equal(a, b)
 
 
-def _zero_vs_repl_worker(rank, world, port, out):
+def _zero_vs_repl_worker(rank, world, port, out, backend="gloo"):
     """Deterministic mode, F10's state, each rank its half of a 4,096-ray batch, 6 iterations, four
     ways: eager / graphed x replicated (all-reduce mean, RAdam on every element) / ZeRO-1 (bucketed,
     owner pass held and run by level range beside the reduce-scatters, RAdam on the rank's shard
     reading the summed gradient x 1/G, gated all-gather)."""
-    _init(rank, world, port)
+    _init(rank, world, port, backend)
     import indoor_nerf_amd as nerf
     from indoor_nerf_amd.graphs import GraphedTrainStep
     from tables import synthetic_rays
@@ -225,6 +225,22 @@ def test_sharded_training_matches_replicated_bitwise(tmp_path):
         for a, b in zip(r[0][g]["params"], r[1][g]["params"]):
             assert torch.equal(a, b)          # replicas agree
     assert len(set(r[0]["00"]["losses"])) > 1          # the parameters moved
+
+
+def test_rccl_one_rank_zero_matches_replicated_bitwise(tmp_path):
+    """The same four ways in a ONE-rank RCCL (nccl) process group: the N > 1 code path's collectives
+    (all_reduce, reduce_scatter_tensor, all_gather_into_tensor, the gated side-stream all-gather) on
+    the real backend and device streams — two ranks cannot share one GPU under RCCL, so this is the
+    hardware rehearsal of that path (the two-rank tests above run it over gloo)."""
+    mp.start_processes(_zero_vs_repl_worker, args=(1, _free_port(), str(tmp_path), "nccl"), nprocs=1, join=True,
+                       start_method="spawn")
+    r = torch.load(tmp_path / "zvr_0.pt", weights_only=True)
+    for g in ("0", "1"):
+        repl, shard = r[g + "0"], r[g + "1"]
+        assert repl["losses"] == shard["losses"], g
+        for i, (a, b) in enumerate(zip(repl["params"], shard["params"])):
+            assert torch.equal(a, b), f"graphed {g}: param {i} differs ({int((a != b).sum())} elements)"
+    assert len(set(r["00"]["losses"])) > 1
 
 
 def _gather_worker(rank, world, port, out):
