@@ -129,7 +129,8 @@ def _zero_worker(rank, world, port, out_dir, buckets=False):
                       LOCAL_RANK=str(rank))
     from indoor_nerf_amd.dist import (GradArena, ShardedOptimizer, allreduce_calibration_stats, allreduce_mean_,
                                       init_process_group)
-    init_process_group(backend="gloo")
+    init_process_group(backend="gloo", force=world == 1)   # world 1: the forced one-rank group (bench.py NERF_DIST_FORCE)
+    assert dist.is_initialized() and dist.get_world_size() == world
     g = torch.Generator().manual_seed(0)
     params = [torch.nn.Parameter(torch.randn(n, generator=g)) for n in (300, 77, 1024, 5)]
     opt = _SgdShard(params)
@@ -160,6 +161,21 @@ def _zero_worker(rank, world, port, out_dir, buckets=False):
     allreduce_mean_(m)
     np.save(os.path.join(out_dir, f"m_{rank}.npy"), m.numpy())
     dist.destroy_process_group()
+
+
+def test_sharded_optimizer_one_rank_group(tmp_path):
+    """The forced one-rank process group (dist.init_process_group(force=True), bench.py
+    NERF_DIST_FORCE=1): the ZeRO-1 collectives of one rank leave one process's own update."""
+    mp.start_processes(_zero_worker, args=(1, _free_port(), str(tmp_path), True), nprocs=1, join=True,
+                       start_method="spawn")
+    g = torch.Generator().manual_seed(0)
+    params = [torch.randn(n, generator=g) for n in (300, 77, 1024, 5)]
+    for step in range(3):
+        gr = torch.Generator().manual_seed(10 * step)
+        grads = [torch.randn(p.shape, generator=gr) for p in params]
+        for p, gp in zip(params, grads):
+            p.sub_(0.5 * gp)
+    np.testing.assert_array_equal(np.load(tmp_path / "p_0.npy"), torch.cat(params).numpy())
 
 
 @pytest.mark.parametrize("buckets", [False, True], ids=["one_bucket", "two_buckets"])
