@@ -111,9 +111,11 @@ class GradArena:
         self.attach()
 
     def allreduce_mean(self, group=None):
-        world = dist.get_world_size(group) if dist.is_initialized() else 1
-        if world == 1:
+        """Mean of the gradients over the process group (a one-rank group runs the collective too: the
+        RCCL rehearsal of bench.py NERF_DIST_FORCE; no group: nothing to do)."""
+        if not (dist.is_available() and dist.is_initialized()):
             return
+        world = dist.get_world_size(group)
         h = _staged(self.flat)
         dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
         h.mul_(1.0 / world)
@@ -253,8 +255,11 @@ class ShardedOptimizer:
 
     def __init__(self, optimizer, arena, group=None, overlap=False, overlap_gather=None):
         self.opt, self.arena, self.group = optimizer, arena, group
-        self.world = dist.get_world_size(group) if (dist.is_available() and dist.is_initialized()) else 1
-        self.rank = dist.get_rank(group) if self.world > 1 else 0
+        # grouped: a process group exists — its collectives run even at one rank (the one-GPU RCCL
+        # rehearsal of the N > 1 path, bench.py NERF_DIST_FORCE=1); without one every hook is local
+        self.grouped = dist.is_available() and dist.is_initialized()
+        self.world = dist.get_world_size(group) if self.grouped else 1
+        self.rank = dist.get_rank(group) if self.grouped else 0
         n_flat = arena.flat.numel()
         if any((e - s) % (self.world * _ALIGN) for s, e in arena.buckets):
             raise ValueError("ShardedOptimizer: build the GradArena with pad_to=world*64")
@@ -286,7 +291,7 @@ class ShardedOptimizer:
             self.ranges.append(r)
         # the reduce-scatter leaves the SUM of the ranks' gradients; the RAdam launch reads it x 1/G
         # (nerf_radam_segment.grad_scale), so no pass over the shard forms the mean first
-        optimizer.set_shard(shard if self.world > 1 else None, grad_scale=1.0 / self.world)
+        optimizer.set_shard(shard if self.grouped else None, grad_scale=1.0 / self.world)
         self.overlap = bool(overlap) and len(arena.buckets) > 1 and dev.type == "cuda"
         self.side = torch.cuda.Stream(device=dev) if self.overlap else None
         self._levels = None
@@ -340,7 +345,7 @@ class ShardedOptimizer:
         from .hashgrid import pending_bins
         self.wait_params()      # the last all-gather wrote the parameter shards the update reads
         held = pending_bins(self.arena.flat.device).take_held() if self.overlap else None
-        if self.world == 1:
+        if not self.grouped:
             if held is not None:
                 held.run(0, held.L)
             return
@@ -366,7 +371,7 @@ class ShardedOptimizer:
         """All-gather of each bucket's updated parameter shards (in place: the shard is a view of the
         output); with overlap_gather the table-only buckets after the first on the side stream,
         behind gates the next forward joins (class docstring)."""
-        if self.world == 1:
+        if not self.grouped:
             return
         from .hashgrid import TableGate, gate_tables
         dev = self.pflat.device
@@ -390,7 +395,7 @@ class ShardedOptimizer:
         tensors on every rank (each element is owned by exactly one rank; the others contribute
         zeros) with ONE all-reduce over both moments of every parameter laid out like the gradient
         arena, so the call count cannot differ between ranks whatever state each rank holds."""
-        if self.world == 1:
+        if not self.grouped:
             return
         self.wait_params()
         keys = ("exp_avg", "exp_avg_sq")

@@ -131,6 +131,17 @@ def _zero_worker(rank, world, port, out_dir, buckets=False):
                                       init_process_group)
     init_process_group(backend="gloo", force=world == 1)   # world 1: the forced one-rank group (bench.py NERF_DIST_FORCE)
     assert dist.is_initialized() and dist.get_world_size() == world
+    calls = {"rs": 0, "ag": 0}
+    rs, ag = dist.reduce_scatter_tensor, dist.all_gather_into_tensor
+
+    def rs_count(*a, **k):
+        calls["rs"] += 1
+        return rs(*a, **k)
+
+    def ag_count(*a, **k):
+        calls["ag"] += 1
+        return ag(*a, **k)
+    dist.reduce_scatter_tensor, dist.all_gather_into_tensor = rs_count, ag_count
     g = torch.Generator().manual_seed(0)
     params = [torch.nn.Parameter(torch.randn(n, generator=g)) for n in (300, 77, 1024, 5)]
     opt = _SgdShard(params)
@@ -147,6 +158,7 @@ def _zero_worker(rank, world, port, out_dir, buckets=False):
         opt.step()
         sh.gather_params()
     np.save(os.path.join(out_dir, f"p_{rank}.npy"), torch.cat([p.detach().view(-1) for p in params]).numpy())
+    np.save(os.path.join(out_dir, f"calls_{rank}.npy"), np.array([calls["rs"], calls["ag"]]))
     # A-CAQ calibration statistics: order-preserving uint32 images of (min, max) in int32
     vals = torch.tensor([[-3.0 + rank, 2.0 * rank], [0.5 * rank, -1.0 - rank]])
 
@@ -176,6 +188,8 @@ def test_sharded_optimizer_one_rank_group(tmp_path):
         for p, gp in zip(params, grads):
             p.sub_(0.5 * gp)
     np.testing.assert_array_equal(np.load(tmp_path / "p_0.npy"), torch.cat(params).numpy())
+    # the collectives ran (3 steps x 2 buckets each), not a local shortcut
+    assert np.load(tmp_path / "calls_0.npy").tolist() == [6, 6]
 
 
 @pytest.mark.parametrize("buckets", [False, True], ids=["one_bucket", "two_buckets"])

@@ -169,6 +169,17 @@ def _zero_vs_repl_worker(rank, world, port, out, backend="gloo"):
     import indoor_nerf_amd as nerf
     from indoor_nerf_amd.graphs import GraphedTrainStep
     from tables import synthetic_rays
+    calls = {"rs": 0, "ag": 0, "ar": 0}
+    dd = torch.distributed
+    rs, ag, ar = dd.reduce_scatter_tensor, dd.all_gather_into_tensor, dd.all_reduce
+
+    def counted(key, fn):
+        def f(*a, **k):
+            calls[key] += 1
+            return fn(*a, **k)
+        return f
+    dd.reduce_scatter_tensor, dd.all_gather_into_tensor, dd.all_reduce = (counted("rs", rs), counted("ag", ag),
+                                                                          counted("ar", ar))
     nerf.set_deterministic(True)
     dev = torch.device("cuda:0")
     R = 4096
@@ -201,6 +212,7 @@ def _zero_vs_repl_worker(rank, world, port, out, backend="gloo"):
                 sh.wait_params()
             torch.cuda.synchronize()
             res[f"{int(graphed)}{int(sharded)}"] = {"params": [p.detach().cpu() for p in params], "losses": losses}
+    res["calls"] = dict(calls)
     torch.save(res, os.path.join(out, f"zvr_{rank}.pt"))
     torch.distributed.destroy_process_group()
 
@@ -235,6 +247,8 @@ def test_rccl_one_rank_zero_matches_replicated_bitwise(tmp_path):
     mp.start_processes(_zero_vs_repl_worker, args=(1, _free_port(), str(tmp_path), "nccl"), nprocs=1, join=True,
                        start_method="spawn")
     r = torch.load(tmp_path / "zvr_0.pt", weights_only=True)
+    # the collectives ran on RCCL (no one-rank shortcut): 2 x 6 iterations of each kind of step
+    assert r["calls"]["rs"] >= 12 and r["calls"]["ag"] >= 12 and r["calls"]["ar"] >= 12, r["calls"]
     for g in ("0", "1"):
         repl, shard = r[g + "0"], r[g + "1"]
         assert repl["losses"] == shard["losses"], g
