@@ -65,7 +65,8 @@ OPS = {
     "mlp_fwd": dict(calls=("nerf_mlp_fwd",), bound="mfma", per_unit=18688, unit="point"),
     # the coarse pass's compositing runs in the sampler's launch (nerf_composite_sample_fine): its time
     # is the op's, the sampler's bytes are not priced (a lower bound on the op's fraction)
-    "composite_fwd": dict(calls=("nerf_composite_fwd", "nerf_composite_sample_fine"), bound="hbm", per_unit=24,
+    "composite_fwd": dict(calls=("nerf_composite_fwd", "nerf_composite_sample_fine", "nerf_composite_fwd_tv"),
+                          bound="hbm", per_unit=24,
                           unit="sample"),
     "composite_bwd": dict(calls=("nerf_composite_bwd", "nerf_composite_bwd_batch"), bound="hbm", per_unit=40,
                           unit="sample"),

@@ -596,6 +596,19 @@ int nerf_tv_bwd_bin(const float* const* d_tables, int n_levels, int log2_T, cons
                     const float* d_verts /* optional: nerf_tv_fwd's d_verts of the same tables and cuboids */,
                     int64_t chunk_base, int64_t chunk_capacity, int deterministic, void* d_workspace,
                     size_t workspace_bytes, void* stream);
+/* ABI 11: nerf_composite_fwd with the iteration's TV forward (nerf_tv_fwd) in the same launch: the TV's
+ * gather blocks run beside the fine pass's one-wave rays instead of as a launch of their own. tv: the
+ * nerf_tv_fwd arguments of the same name for n_levels tables of 2^log2_T rows (d_loss accumulates as
+ * there, d_verts optional); NULL tv = nerf_composite_fwd. Outputs are those of the two separate calls
+ * (the TV loss up to its float atomics' order). */
+typedef struct nerf_tv_fwd_job {
+    const float* const* d_tables; const int64_t* min_vertex; const int64_t* d_min_vertex; const int* cube;
+    float* d_loss; float* d_verts;
+} nerf_tv_fwd_job;
+int nerf_composite_fwd_tv(const float* d_raw, int raw_channels, const float* d_z, const float* d_rays_d,
+                          const float* d_noise, int64_t n_rays, int n_samples, int white_bkgd, float* d_rgb,
+                          float* d_disp, float* d_acc, float* d_weights, float* d_depth, float* d_entropy,
+                          float* d_normal, const nerf_tv_fwd_job* tv, int n_levels, int log2_T, void* stream);
 /* ABI 11: nerf_hash_encode_bwd_bin_batch with the pass's binned TV backward in the same launch (its
  * blocks first: the TV's few, gather-latency-bound blocks run beside the hash bins instead of as a
  * launch of their own). tv: the nerf_tv_bwd_bin arguments of the same name (d_verts required; the

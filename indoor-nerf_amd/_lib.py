@@ -72,6 +72,12 @@ class TVBinJob(ctypes.Structure):
                 ("d_verts", c_vp), ("chunk_base", c_i64)]
 
 
+class TVFwdJob(ctypes.Structure):
+    """nerf_tv_fwd_job (include/nerf_hip.h, ABI 11)."""
+    _fields_ = [("d_tables", c_vp), ("min_vertex", c_vp), ("d_min_vertex", c_vp), ("cube", c_vp), ("d_loss", c_vp),
+                ("d_verts", c_vp)]
+
+
 class ZeroRange(ctypes.Structure):
     _fields_ = [("ptr", c_vp), ("n", c_i64)]
 
@@ -175,6 +181,8 @@ SIGNATURES = {
                              ctypes.POINTER(NormalHeadGrads), c_vp, ctypes.c_size_t, c_vp],
     "nerf_composite_fwd": [c_vp, c_int, c_vp, c_vp, c_vp, c_i64, c_int, c_int,
                            c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
+    "nerf_composite_fwd_tv": [c_vp, c_int, c_vp, c_vp, c_vp, c_i64, c_int, c_int,
+                              c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(TVFwdJob), c_int, c_int, c_vp],
     "nerf_composite_bwd": [c_vp, c_int, c_vp, c_vp, c_vp, c_i64, c_int, c_int,
                            c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
     "nerf_composite_bwd_batch": [ctypes.POINTER(CompositeBwdJob), c_int, c_vp],

@@ -4,6 +4,7 @@
 //   U_j = sum_{k>j} gw_k alpha_k prod_{j<m<k} t_m,   dL/dalpha_j = T_j (gw_j - U_j)
 // is a wave-level suffix scan of affine maps (X, P) -> X + P*U in fp64.
 #include "composite_common.h"
+#include "hash_common.h"   // TVParams, fill_tv, tv_fwd_block (the TV forward beside the fine compositing)
 
 namespace nerf {
 
@@ -15,6 +16,26 @@ __global__ void __launch_bounds__(256) composite_fwd_kernel(CompositeArgs a) {
     composite_fwd_ray<K>(a, ray, lane, nullptr);
 }
 
+
+// The fine pass's compositing with the iteration's TV forward in the same launch
+// (nerf_composite_fwd_tv): blocks [0, tv_blocks) are TV blocks (level = x / kTVFusedBlocks, four
+// vertices per thread: the composite rays' registers), the rest one ray per wave as
+// composite_fwd_kernel. The TV's gathers (17.5 us as a launch of their own, rocprof r06h) run beside
+// the 4,096 one-wave rays (10 us).
+constexpr int kTVFusedBlocks = 136, kTVFusedUnroll = 4;   // 136 x 256 x 4 >= 51^3: one round per thread
+template <int K>
+__global__ void __launch_bounds__(256) composite_fwd_tv_kernel(CompositeArgs a, TVParams tv, unsigned tv_blocks) {
+    if (blockIdx.x < tv_blocks) {
+        tv_fwd_block<kTVFusedUnroll>(tv, (int)(blockIdx.x / kTVFusedBlocks), blockIdx.x % kTVFusedBlocks,
+                                     kTVFusedBlocks);
+        return;
+    }
+    const int lane = threadIdx.x & 63;
+    const int64_t ray = (int64_t)(blockIdx.x - tv_blocks) * 4 + (threadIdx.x >> 6);
+    if (ray >= a.R) return;   // wave-uniform
+    composite_fwd_ray<K>(a, ray, lane, nullptr);
+}
+static_assert(sizeof(CompositeArgs) + sizeof(TVParams) + 16 <= 4096, "composite_fwd_tv_kernel: kernel arguments");
 
 // The backward of one ray (the wave's).
 template <int K>
@@ -187,6 +208,49 @@ extern "C" int nerf_composite_fwd(const float* d_raw, int raw_channels, const fl
     dim3 grid(blocks_for(n_rays, 4));
     NERF_COMPOSITE_DISPATCH(composite_fwd_kernel, n_samples, grid, as_stream(stream), a);
     NERF_CHECK_LAUNCH("composite_fwd");
+    return NERF_OK;
+}
+
+extern "C" int nerf_composite_fwd_tv(const float* d_raw, int raw_channels, const float* d_z, const float* d_rays_d,
+                                     const float* d_noise, int64_t n_rays, int n_samples, int white_bkgd,
+                                     float* d_rgb, float* d_disp, float* d_acc, float* d_weights, float* d_depth,
+                                     float* d_entropy, float* d_normal, const nerf_tv_fwd_job* tv, int n_levels,
+                                     int log2_T, void* stream) {
+    if (!tv)
+        return nerf_composite_fwd(d_raw, raw_channels, d_z, d_rays_d, d_noise, n_rays, n_samples, white_bkgd, d_rgb,
+                                  d_disp, d_acc, d_weights, d_depth, d_entropy, d_normal, stream);
+    NERF_REQUIRE(n_rays >= 0 && n_samples >= 1 && n_samples <= 512, "composite_fwd_tv: R=%lld S=%d (S must be 1..512)",
+                 (long long)n_rays, n_samples);
+    NERF_REQUIRE(raw_channels == 4 || raw_channels == 7, "composite_fwd_tv: raw_channels %d", raw_channels);
+    NERF_REQUIRE(n_rays == 0 || (d_raw && d_z && d_rays_d && d_weights), "composite_fwd_tv: null arg");
+    NERF_REQUIRE(!(d_normal && raw_channels != 7), "composite_fwd_tv: normal output needs 7 raw channels");
+    TVParams P{};
+    const int rc = fill_tv(P, n_levels, log2_T, tv->min_vertex, tv->d_min_vertex, tv->cube);
+    if (rc) return rc;
+    NERF_REQUIRE(tv->d_tables && tv->d_loss, "composite_fwd_tv: null TV arg");
+    for (int l = 0; l < n_levels; ++l) {
+        NERF_REQUIRE(tv->d_tables[l], "composite_fwd_tv: TV table %d null", l);
+        P.tables[l] = tv->d_tables[l];
+    }
+    P.loss = tv->d_loss;
+    P.verts = reinterpret_cast<float2*>(tv->d_verts);
+    CompositeArgs a{};
+    a.raw = d_raw; a.C = raw_channels; a.z = d_z; a.rays_d = d_rays_d; a.noise = d_noise;
+    a.R = n_rays; a.S = n_samples; a.white = white_bkgd;
+    a.rgb = d_rgb; a.disp = d_disp; a.acc = d_acc; a.weights = d_weights; a.depth = d_depth;
+    a.entropy = d_entropy; a.normal = d_normal;
+    const unsigned tvb = (unsigned)(kTVFusedBlocks * n_levels);
+    const dim3 grid((unsigned)(tvb + blocks_for(n_rays, 4)));
+    hipStream_t st = as_stream(stream);
+    switch (pick_k(n_samples)) {
+        case 1: hipLaunchKernelGGL(composite_fwd_tv_kernel<1>, grid, dim3(256), 0, st, a, P, tvb); break;
+        case 2: hipLaunchKernelGGL(composite_fwd_tv_kernel<2>, grid, dim3(256), 0, st, a, P, tvb); break;
+        case 3: hipLaunchKernelGGL(composite_fwd_tv_kernel<3>, grid, dim3(256), 0, st, a, P, tvb); break;
+        case 4: hipLaunchKernelGGL(composite_fwd_tv_kernel<4>, grid, dim3(256), 0, st, a, P, tvb); break;
+        case 5: case 6: hipLaunchKernelGGL(composite_fwd_tv_kernel<6>, grid, dim3(256), 0, st, a, P, tvb); break;
+        default: hipLaunchKernelGGL(composite_fwd_tv_kernel<8>, grid, dim3(256), 0, st, a, P, tvb); break;
+    }
+    NERF_CHECK_LAUNCH("composite_fwd_tv");
     return NERF_OK;
 }
 

@@ -62,57 +62,10 @@ __global__ void __launch_bounds__(kRAdamThreads) radam_kernel(RAdamSegs S) {
 // serialise at its address: a one-vertex-per-thread grid of ~2,300 blocks took 41 instead of 21 us).
 // tv_fwd issues the gathers of up to kTVUnroll of a thread's vertices before the first add (the
 // finest levels' 51^3 cuboids are ~5.4 vertices per thread: one round trip instead of five).
-constexpr int kTVBlocks = 96;
-constexpr int kTVUnroll = 8;
 constexpr uint32_t kTVSkip = 0xFFFFFFFFu;
 
-// cube vertex (i,j,k) = min_vertex + (i,j,k) in meshgrid 'ij' order (loss.py:25-27)
 __global__ void __launch_bounds__(256) tv_fwd_kernel(TVParams P) {
-    const int l = blockIdx.y;
-    const int c = P.cube[l], n1 = c + 1;
-    const uint32_t nv = (uint32_t)(P.vstart[l + 1] - P.vstart[l]);
-    const float2* tab = reinterpret_cast<const float2*>(P.tables[l]);
-    int mvd[3];
-    tv_corner(P, l, mvd);
-    const int* mv = mvd;
-    const uint32_t stride = gridDim.x * 256u;
-    float part = 0.f;
-    for (uint32_t lv0 = blockIdx.x * 256u + threadIdx.x; lv0 < nv; lv0 += kTVUnroll * stride) {
-        float2 e[kTVUnroll], f[kTVUnroll][3];
-        bool nb[kTVUnroll][3];
-#pragma unroll
-        for (int u = 0; u < kTVUnroll; ++u) {
-            const uint32_t lv = lv0 + u * stride;
-            const bool ok = lv < nv;
-            int i = 0, j = 0, k = 0;
-            if (ok) tv_vertex(lv, n1, i, j, k);
-            nb[u][0] = ok && i < c; nb[u][1] = ok && j < c; nb[u][2] = ok && k < c;
-            e[u] = ok ? tv_fetch(tab, mv, i, j, k, P.mask) : make_float2(0.f, 0.f);
-            f[u][0] = nb[u][0] ? tv_fetch(tab, mv, i + 1, j, k, P.mask) : e[u];
-            f[u][1] = nb[u][1] ? tv_fetch(tab, mv, i, j + 1, k, P.mask) : e[u];
-            f[u][2] = nb[u][2] ? tv_fetch(tab, mv, i, j, k + 1, P.mask) : e[u];
-        }
-#pragma unroll
-        for (int u = 0; u < kTVUnroll; ++u) {
-            const uint32_t lv = lv0 + u * stride;
-            if (lv < nv) {
-                if (P.verts) P.verts[P.vstart[l] + lv] = e[u];
-                float acc = 0.f;
-#pragma unroll
-                for (int d = 0; d < 3; ++d)
-                    if (nb[u][d]) { const float dx = f[u][d].x - e[u].x, dy = f[u][d].y - e[u].y; acc += dx * dx + dy * dy; }
-                part += acc / (float)c;
-            }
-        }
-    }
-    __shared__ float s_part[4];
-    const float w = wave_sum(part);
-    if ((threadIdx.x & 63) == 0) s_part[threadIdx.x >> 6] = w;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const float t = (s_part[0] + s_part[1]) + (s_part[2] + s_part[3]);
-        if (t != 0.f) atomicAdd(P.loss + l, t);
-    }
+    tv_fwd_block(P, blockIdx.y, blockIdx.x, gridDim.x);
 }
 
 __global__ void __launch_bounds__(256) tv_bwd_kernel(TVParams P) {

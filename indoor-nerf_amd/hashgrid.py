@@ -417,6 +417,44 @@ class hold_owner:
         return False
 
 
+class EarlyTV:
+    """A captured training step's TV forward (losses.tv_forward_early) awaiting the step's fine-pass
+    compositing, which launches it (render.CompositeFn, nerf_composite_fwd_tv: the TV blocks beside the
+    one-wave rays); total_variation_all takes it back after render. dmv: the device
+    corner slots (drawn before every replay by a filler registered after render: the draw order of
+    the separate launch); out: the zeroed [L] loss accumulator; verts: the vertex rows for the
+    backward."""
+
+    def __init__(self, tables, dmv, slot_off, cubes, log2_T, out, verts):
+        self.tables, self.dmv, self.slot_off, self.cubes, self.log2_T = list(tables), dmv, slot_off, cubes, log2_T
+        self.out, self.verts, self.launched = out, verts, False
+        self.ptrs = _lib.ptr_array(self.tables)
+        self.cb = (_lib.c_int * len(cubes))(*cubes)
+
+
+_EARLY_TV = {}
+_TV_FWD_FUSED = {"on": os.environ.get("NERF_TV_FWD_FUSED", "1") != "0"}   # the env switch: A/B runs
+
+
+def set_tv_fwd_fused(enabled=True):
+    """Launch a captured step's TV forward inside its fine-pass compositing launch (default on)."""
+    _TV_FWD_FUSED["on"] = bool(enabled)
+
+
+def early_tv(device):
+    """The pending EarlyTV of `device` not launched yet, or None."""
+    job = _EARLY_TV.get(torch.device(device).index)
+    return job if job is not None and not job.launched else None
+
+
+def register_early_tv(job):
+    _EARLY_TV[job.out.device.index] = job
+
+
+def take_early_tv(device):
+    return _EARLY_TV.pop(torch.device(device).index, None)
+
+
 _FUSED_STEP = {"on": True}
 _TV_IN_BINS = {"on": os.environ.get("NERF_TV_IN_BINS", "1") != "0"}   # the env switch: A/B runs
 

@@ -28,7 +28,7 @@ class TVFn(torch.autograd.Function):
     """min_vertex: host [L,3] cuboid corners, or an int device address of [L,3] int64 slots that a
     captured step refreshes before every replay (graphs.StepScalars)."""
     @staticmethod
-    def forward(ctx, min_vertex, cubes, log2_T, out, *tables):
+    def forward(ctx, min_vertex, cubes, log2_T, out, early, *tables):
         L = len(tables)
         if isinstance(min_vertex, int):
             mv, dmv = None, _lib.c_vp(min_vertex)
@@ -36,8 +36,13 @@ class TVFn(torch.autograd.Function):
             mv, dmv = (_lib.c_i64 * (3 * L))(*[int(v) for v in min_vertex.reshape(-1).tolist()]), None
         cb = (_lib.c_int * L)(*[int(c) for c in cubes])
         dev = tables[0].device
+        if early is not None and early.launched:   # already run inside the fine compositing launch
+            ctx.save_for_backward(*tables)
+            ctx.mv, ctx.dmv, ctx.cb, ctx.log2_T, ctx.verts = mv, dmv, cb, log2_T, early.verts
+            return early.out
         # the cuboid vertices' rows, gathered once here: the backward's stencil reads them densely
-        verts = torch.empty(2 * sum((int(c) + 1) ** 3 for c in cubes), device=dev, dtype=torch.float32)
+        verts = (early.verts if early is not None else
+                 torch.empty(2 * sum((int(c) + 1) ** 3 for c in cubes), device=dev, dtype=torch.float32))
         if out is None:
             loss = torch.zeros(L, device=dev, dtype=torch.float32)
         else:   # a zeroed accumulator (tv_accumulator: its fill rides along in render()'s first launch)
@@ -77,7 +82,7 @@ class TVFn(torch.autograd.Function):
                 hashgrid.materialize_zero(grads)
                 _lib.call("nerf_tv_bwd", _lib.ptr_array(tables), L, ctx.log2_T, ctx.mv, ctx.dmv, ctx.cb,
                           _lib.ptr(g, "grad_loss"), _lib.ptr_array(grads, "grad_tables"), _lib.stream())
-        return (None, None, None, None) + (None,) * len(tables)
+        return (None, None, None, None, None) + (None,) * len(tables)
 
 
 class TVBinJob:
@@ -109,28 +114,53 @@ def tv_accumulator(embedder):
     return acc
 
 
-def total_variation_all(embedder, min_vertex=None, generator=None, out=None):
-    """Per-level TV losses [L] of all levels of `embedder` (sum them for the reference's TV_loss).
-    out: an accumulator from tv_accumulator (None: a fresh zeroed one)."""
+def tv_forward_early(embedder, out):
+    """Before render() of a captured step: have the step's TV forward launched inside the fine pass's
+    compositing (hashgrid.EarlyTV, nerf_composite_fwd_tv) instead of as a launch of its own after
+    render. Only the corner slots and the vertex buffer are allocated here; the corners are still drawn
+    after render (total_variation_all registers their filler), so the host draw order is unchanged.
+    Returns the job for total_variation_all(..., early=), or None (not capturing, no accumulator, off)."""
     from . import graphs
     sc = graphs.active()
+    if sc is None or out is None or not hashgrid._TV_FWD_FUSED["on"]:
+        return None
+    L = embedder.n_levels
+    off, ptr = sc.alloc_i64(3 * L)
+    cubes = [tv_cube(l, embedder.base_resolution, embedder.finest_resolution, L)[1] for l in range(L)]
+    verts = torch.empty(2 * sum((c + 1) ** 3 for c in cubes), device=out.device, dtype=torch.float32)
+    job = hashgrid.EarlyTV(embedder.tables(), _lib.c_vp(ptr), off, cubes, embedder.log2_hashmap_size, out, verts)
+    hashgrid.register_early_tv(job)
+    return job
+
+
+def total_variation_all(embedder, min_vertex=None, generator=None, out=None, early=None):
+    """Per-level TV losses [L] of all levels of `embedder` (sum them for the reference's TV_loss).
+    out: an accumulator from tv_accumulator (None: a fresh zeroed one). early: tv_forward_in_hash's job
+    (its forward may already have run inside the coarse hash forward)."""
+    from . import graphs
+    sc = graphs.active()
+    if early is not None:
+        hashgrid.take_early_tv(early.out.device)
     if sc is not None and min_vertex is None:
         # captured step: the corners are drawn by the same host code before every replay
         L = embedder.n_levels
-        off, ptr = sc.alloc_i64(3 * L)
+        if early is not None:
+            off, ptr = early.slot_off, early.dmv.value
+        else:
+            off, ptr = sc.alloc_i64(3 * L)
 
         def fill(hi, hf, off=off):
             mv, _ = draw_min_vertices(embedder, generator)
             hi[off:off + 3 * L] = mv.reshape(-1).numpy()
         sc.add_filler(fill)
         cubes = [tv_cube(l, embedder.base_resolution, embedder.finest_resolution, L)[1] for l in range(L)]
-        return TVFn.apply(ptr, cubes, embedder.log2_hashmap_size, out, *embedder.tables())
+        return TVFn.apply(ptr, cubes, embedder.log2_hashmap_size, out, early, *embedder.tables())
     if min_vertex is None:
         min_vertex, cubes = draw_min_vertices(embedder, generator)
     else:
         cubes = [tv_cube(l, embedder.base_resolution, embedder.finest_resolution, embedder.n_levels)[1]
                  for l in range(embedder.n_levels)]
-    return TVFn.apply(torch.as_tensor(min_vertex), cubes, embedder.log2_hashmap_size, out, *embedder.tables())
+    return TVFn.apply(torch.as_tensor(min_vertex), cubes, embedder.log2_hashmap_size, out, None, *embedder.tables())
 
 
 def total_variation_loss(embeddings, min_resolution, max_resolution, level, log2_hashmap_size, n_levels=16,
@@ -139,7 +169,8 @@ def total_variation_loss(embeddings, min_resolution, max_resolution, level, log2
     res, cube = tv_cube(level, min_resolution, max_resolution, n_levels)
     if min_vertex is None:
         min_vertex = torch.randint(0, res - cube, (3,))
-    return TVFn.apply(torch.as_tensor(min_vertex).reshape(1, 3), [cube], log2_hashmap_size, None, embeddings.weight)[0]
+    return TVFn.apply(torch.as_tensor(min_vertex).reshape(1, 3), [cube], log2_hashmap_size, None, None,
+                      embeddings.weight)[0]
 
 
 class TrainLossFn(torch.autograd.Function):

@@ -13,7 +13,7 @@ import torch
 
 from .field import NeRFSmall, run_network
 from .hashgrid import HashEmbedder, SHEncoder
-from .losses import total_variation_all, train_loss, tv_accumulator
+from .losses import total_variation_all, train_loss, tv_accumulator, tv_forward_early
 from .optim import RAdam
 from .render import render
 from . import _lib, hashgrid
@@ -193,10 +193,12 @@ def _forward_backward(batch_rays, target_s, render_kwargs_train, optimizer, args
         zero_grad()
     tv_w = get("tv_loss_weight")
     tv_acc = tv_accumulator(render_kwargs_train["embed_fn"]) if tv_w > 0 else None
+    # a captured step's TV forward runs inside the fine compositing launch (corners drawn after render)
+    tv_early = tv_forward_early(render_kwargs_train["embed_fn"], tv_acc) if tv_w > 0 else None
     rgb, depth, acc, extras = render(H, W, K, chunk=get("chunk"), rays=batch_rays, retraw=True,
                                      **render_kwargs_train)
     # run_nerf.py:1011-1037 (img2mse x2, sparsity, TV, mse2psnr) fused into one launch (csrc/loss.hip)
-    tv = (total_variation_all(render_kwargs_train["embed_fn"], generator=tv_generator, out=tv_acc)
+    tv = (total_variation_all(render_kwargs_train["embed_fn"], generator=tv_generator, out=tv_acc, early=tv_early)
           if tv_w > 0 else None)
     loss, img_loss, psnr = train_loss(rgb, extras.get("rgb0"), target_s, extras.get("sparsity_loss"),
                                       extras.get("sparsity_loss0"), tv, get("sparse_loss_weight") * loss_scale_sparsity,

@@ -10,12 +10,14 @@ Randomness: pytest=True reproduces the reference's np.random.seed(0) draws exact
 stratified jitter and importance uniforms are drawn in-kernel (Philox4x32-10) from a seed taken
 from torch's CPU generator, and raw noise uses torch.randn like the reference.
 """
+import ctypes
 import os
 
 import numpy as np
 import torch
 
 from . import _lib
+from .hashgrid import early_tv
 
 img2mse = lambda x, y: torch.mean((x - y) ** 2)  # noqa: E731
 # The reference divides by torch.log(torch.Tensor([10.])) (a [1] float32 tensor): same value and shape
@@ -141,7 +143,16 @@ class CompositeFn(torch.autograd.Function):
                  _lib.ptr(noise, "noise", allow_none=True), R, S, int(bool(white_bkgd)), _lib.ptr(rgb, "rgb"),
                  _lib.ptr(disp, "disp"), _lib.ptr(acc, "acc"), _lib.ptr(weights, "weights"), _lib.ptr(depth, "depth"),
                  _lib.ptr(ent, "entropy"), _lib.ptr(normal, "normal", allow_none=True))
-        if sampler is None:
+        tv = early_tv(dev) if sampler is None else None
+        if tv is not None:   # a captured step's TV forward in the same launch (losses.tv_forward_early)
+            from .hashgrid import join_tables
+            join_tables(dev)                    # a pending all-gather of table levels (dist.py): TV reads them all
+            _lib.flush_zero_fills([tv.out])     # its accumulator's fill: normally done by nerf_rays_pack_z
+            job = _lib.TVFwdJob(_lib.c_vp(ctypes.addressof(tv.ptrs)), None, tv.dmv, _lib.c_vp(ctypes.addressof(tv.cb)),
+                                _lib.ptr(tv.out, "tv_loss"), _lib.ptr(tv.verts, "tv_verts"))
+            _lib.call("nerf_composite_fwd_tv", *cargs, ctypes.byref(job), len(tv.tables), tv.log2_T, _lib.stream())
+            tv.launched = True
+        elif sampler is None:
             _lib.call("nerf_composite_fwd", *cargs, _lib.stream())
         else:   # the coarse pass: the hierarchical sampler on these weights in the same launch
             _lib.call("nerf_composite_sample_fine", *cargs, *sampler, _lib.stream())

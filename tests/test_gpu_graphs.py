@@ -22,7 +22,7 @@ pytestmark = pytest.mark.gpu
 def _setup(nerf, gpu, R=1024, **extra):
     lo, hi = blender_bbox()
     args = nerf.make_args(bounding_box=(torch.from_numpy(lo), torch.from_numpy(hi)), finest_res=1024, N_samples=64,
-                          N_importance=128, white_bkgd=True, perturb=1.0, tv_loss_weight=1e-6, **extra)
+                          N_importance=128, white_bkgd=True, perturb=1.0, **{"tv_loss_weight": 1e-6, **extra})
     torch.manual_seed(0)
     kw, _, _, grad_vars, opt = nerf.create_nerf(args, device=gpu)
     kw.update(near=2.0, far=6.0)
@@ -85,6 +85,30 @@ def test_graphed_train_step_recaptures_at_tv_switch_off(nerf, gpu):
     le, pe, _, _ = _run(nerf, gpu, False, steps)
     lg, pg, st, _ = _run(nerf, gpu, True, steps)
     assert st.captures == 2, st.captures
+    np.testing.assert_allclose(lg, le, rtol=1e-5)
+    _check_params(pg, pe)
+
+
+def test_graphed_tv_forward_fused_matches_eager(nerf, gpu):
+    """The captured step runs its TV forward inside the fine pass's compositing launch
+    (nerf_composite_fwd_tv; corners from the device slots, drawn after render as in the eager step)
+    and no nerf_tv_fwd launch; with a TV weight that makes the TV a large share of the loss, the
+    replays' losses and parameters match the eager steps (which launch nerf_tv_fwd after render)."""
+    calls = []
+    orig = nerf._lib.call
+
+    def spy(name, *a):
+        calls.append(name)
+        return orig(name, *a)
+    steps = list(range(1, 5))
+    le, pe, _, _ = _run(nerf, gpu, False, steps, tv_loss_weight=1e-2)
+    nerf._lib.call = spy
+    try:
+        lg, pg, st, _ = _run(nerf, gpu, True, steps, tv_loss_weight=1e-2)
+    finally:
+        nerf._lib.call = orig
+    assert st.captures == 1
+    assert "nerf_composite_fwd_tv" in calls and "nerf_tv_fwd" not in calls[calls.index("nerf_composite_fwd_tv"):]
     np.testing.assert_allclose(lg, le, rtol=1e-5)
     _check_params(pg, pe)
 
