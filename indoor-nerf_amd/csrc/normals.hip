@@ -88,8 +88,14 @@ __global__ void __launch_bounds__(256) normal_head_fwd_kernel(NormalArgs a) {
     const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= a.P) return;
     float geo[NH_GEO], h[NH_HID], n[3];
-#pragma unroll
-    for (int k = 0; k < NH_GEO; ++k) geo[k] = a.o16[p * 16 + 1 + k];
+    {   // o16 = [sigma, geo 0..14]: four 16-B loads instead of fifteen 4-B ones
+        const float4* src = reinterpret_cast<const float4*>(a.o16 + p * 16);
+        const float4 v0 = src[0], v1 = src[1], v2 = src[2], v3 = src[3];
+        geo[0] = v0.y; geo[1] = v0.z; geo[2] = v0.w;
+        geo[3] = v1.x; geo[4] = v1.y; geo[5] = v1.z; geo[6] = v1.w;
+        geo[7] = v2.x; geo[8] = v2.y; geo[9] = v2.z; geo[10] = v2.w;
+        geo[11] = v3.x; geo[12] = v3.y; geo[13] = v3.z; geo[14] = v3.w;
+    }
     head_forward(s, geo, h, n);
     // F.normalize(x, dim=-1): x / max(||x||_2, 1e-12)
     const float nrm = fmaxf(sqrtf(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]), 1e-12f);
@@ -103,48 +109,81 @@ __global__ void __launch_bounds__(256) normal_head_fwd_kernel(NormalArgs a) {
 }
 
 constexpr int NH_TILE = 128;
-constexpr int NH_OWN = (NH_ALL + NH_TILE - 1) / NH_TILE;   // gradient values per thread (5)
+// LDS row strides (floats): d hidden and relu(hidden) rows of 32 + 4 (relu's column 32 = 1: db1 as one
+// more product column), geo rows of 16 + 4 (column 15 = 1: db0 as N0's 16th column; stride 20 keeps the
+// ds_write_b128 of eight consecutive rows on 32 distinct banks), d n rows of 4 (column 3 = 0)
+constexpr int NH_SDH = 36, NH_SR = 36, NH_SG = 20;
+constexpr int NH_R1 = 36;   // columns of the d N1 image (32 hidden + the ones column + 3 pad)
 
-// at most 128 VGPRs (the LDS allows 3 blocks of 128 threads per CU; unconstrained, the compiler
-// unrolls everything into 256 registers and runs one wave per SIMD)
-__global__ void __launch_bounds__(NH_TILE) __attribute__((amdgpu_waves_per_eu(4))) normal_head_bwd_kernel(NormalArgs a) {
+// One thread per point for the per-point part (the head's forward recompute, the normalize backward,
+// d hidden, d geo); then the tile's weight gradients as register-blocked outer products: each of the
+// 128 threads owns a 4 x 4 block of [dN0 | db0] (32 x 16) over a quarter of the tile's points (two
+// ds_read_b128 feed 16 FMAs), threads 0..71 also a 4 x 4 block of [dN1 | db1] (4 x 36) over 16 points.
+// Blocks keep their sums in registers over all their tiles; at the end the quarters / point groups are
+// added in a fixed order and each block stores its 611 totals (normal_head_wgrad_reduce_kernel sums
+// the blocks in order: deterministic). The earlier form (every thread 5 gradient values, each a
+// 128-step dot product of two LDS reads per FMA) ran 248 us per launch at the ScanNet config, latency-
+// bound on its 1,280 dependent LDS reads per wave and tile.
+__global__ void __launch_bounds__(NH_TILE) __attribute__((amdgpu_waves_per_eu(2))) normal_head_bwd_kernel(NormalArgs a) {
     __shared__ __attribute__((aligned(16))) float s[LH_ALL];
-    __shared__ float s_dh[NH_TILE][NH_HID + 1];   // d pre-ReLU hidden
-    __shared__ float s_hr[NH_TILE][NH_HID + 1];   // pre-ReLU hidden (relu applied where read)
-    __shared__ float s_geo[NH_TILE][NH_GEO + 1];
-    __shared__ float s_dn[NH_TILE][4];            // d pre-normalize n
+    __shared__ __attribute__((aligned(16))) float s_dh[NH_TILE * NH_SDH];   // d pre-ReLU hidden
+    __shared__ __attribute__((aligned(16))) float s_r[NH_TILE * NH_SR];     // relu(hidden), column 32 = 1
+    __shared__ __attribute__((aligned(16))) float s_geo[NH_TILE * NH_SG];   // geo, column 15 = 1
+    __shared__ __attribute__((aligned(16))) float s_dn[NH_TILE * 4];        // d pre-normalize n, column 3 = 0
     load_head(s, a.W);
     const int tid = threadIdx.x;
-    float acc[NH_OWN];
+    const int blk0 = tid & 31, quarter = tid >> 5, rg = blk0 >> 2, cg = blk0 & 3;   // [dN0 | db0] block
+    const bool own1 = tid < 72;
+    const int blk1 = tid % 9, grp1 = tid / 9;                                      // [dN1 | db1] block
+    float acc0[16], acc1[16];
 #pragma unroll
-    for (int j = 0; j < NH_OWN; ++j) acc[j] = 0.f;
+    for (int j = 0; j < 16; ++j) { acc0[j] = 0.f; acc1[j] = 0.f; }
     for (int64_t base = (int64_t)blockIdx.x * NH_TILE; base < a.P; base += (int64_t)gridDim.x * NH_TILE) {
         const int64_t p = base + tid;
         const bool valid = p < a.P;
-        float geo[NH_GEO];
+        float geo[16];
+        {
+            const float4* src = reinterpret_cast<const float4*>(a.o16 + (valid ? p : 0) * 16);
+            float4 v[4];
 #pragma unroll
-        for (int k = 0; k < NH_GEO; ++k) geo[k] = valid ? a.o16[p * 16 + 1 + k] : 0.f;
-        // forward, one hidden unit at a time (the hidden layer goes to LDS, not registers)
-        float n[3] = {s[LH_B1], s[LH_B1 + 1], s[LH_B1 + 2]}, nacc[3] = {0.f, 0.f, 0.f};
-#pragma unroll 2
-        for (int i = 0; i < NH_HID; ++i) {
-            float hi = 0.f;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const float4 t = ld4(s, LH_N0 + 16 * i + 4 * q);
-                hi = fmaf(t.x, geo[4 * q], hi);
-                hi = fmaf(t.y, geo[4 * q + 1], hi);
-                hi = fmaf(t.z, geo[4 * q + 2], hi);
-                if (q < 3) hi = fmaf(t.w, geo[4 * q + 3], hi);
-            }
-            hi = hi + s[LH_B0 + i];
-            s_hr[tid][i] = hi;
-            const float r = fmaxf(hi, 0.f);
-#pragma unroll
-            for (int c = 0; c < 3; ++c) nacc[c] = fmaf(s[LH_N1 + c * NH_HID + i], r, nacc[c]);
+            for (int q = 0; q < 4; ++q) v[q] = valid ? src[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+            // o16 = [sigma, geo 0..14]: geo k at element k + 1
+            geo[0] = v[0].y; geo[1] = v[0].z; geo[2] = v[0].w;
+            geo[3] = v[1].x; geo[4] = v[1].y; geo[5] = v[1].z; geo[6] = v[1].w;
+            geo[7] = v[2].x; geo[8] = v[2].y; geo[9] = v[2].z; geo[10] = v[2].w;
+            geo[11] = v[3].x; geo[12] = v[3].y; geo[13] = v[3].z; geo[14] = v[3].w;
+            geo[15] = 1.f;
         }
+        // forward, four hidden units at a time (relu(hidden) to this thread's LDS row: its sign is the
+        // ReLU mask of the backward below), the same fp32 op order as head_forward
+        float* rdh = s_dh + tid * NH_SDH;
+        float* rr = s_r + tid * NH_SR;
+        float nacc[3] = {0.f, 0.f, 0.f};
+#pragma unroll 1
+        for (int i4 = 0; i4 < NH_HID; i4 += 4) {
+            float r4[4];
 #pragma unroll
-        for (int c = 0; c < 3; ++c) n[c] = nacc[c] + n[c];
+            for (int e = 0; e < 4; ++e) {
+                const int i = i4 + e;
+                float hi = 0.f;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const float4 t = ld4(s, LH_N0 + 16 * i + 4 * q);
+                    hi = fmaf(t.x, geo[4 * q], hi);
+                    hi = fmaf(t.y, geo[4 * q + 1], hi);
+                    hi = fmaf(t.z, geo[4 * q + 2], hi);
+                    if (q < 3) hi = fmaf(t.w, geo[4 * q + 3], hi);
+                }
+                hi = hi + s[LH_B0 + i];
+                r4[e] = fmaxf(hi, 0.f);
+#pragma unroll
+                for (int c = 0; c < 3; ++c) nacc[c] = fmaf(s[LH_N1 + c * NH_HID + i], r4[e], nacc[c]);
+            }
+            *reinterpret_cast<float4*>(rr + i4) = make_float4(r4[0], r4[1], r4[2], r4[3]);
+        }
+        float n[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) n[c] = nacc[c] + s[LH_B1 + c];
         float dn[3] = {0.f, 0.f, 0.f};
         if (valid) {
             const float* g7 = a.graw7 + 7 * p;
@@ -162,62 +201,95 @@ __global__ void __launch_bounds__(NH_TILE) __attribute__((amdgpu_waves_per_eu(4)
         float dg[NH_GEO];
 #pragma unroll
         for (int k = 0; k < NH_GEO; ++k) dg[k] = 0.f;
-#pragma unroll 2
-        for (int i = 0; i < NH_HID; ++i) {
-            const float dh = s_hr[tid][i] > 0.f ? (s[LH_N1 + i] * dn[0] + s[LH_N1 + NH_HID + i] * dn[1]) +
-                                                       s[LH_N1 + 2 * NH_HID + i] * dn[2]
-                                                : 0.f;
-            s_dh[tid][i] = dh;
+#pragma unroll 1
+        for (int i4 = 0; i4 < NH_HID; i4 += 4) {
+            const float4 rv = *reinterpret_cast<const float4*>(rr + i4);
+            const float r4[4] = {rv.x, rv.y, rv.z, rv.w};
+            float dh4[4];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const float4 t = ld4(s, LH_N0 + 16 * i + 4 * q);
-                dg[4 * q] = fmaf(t.x, dh, dg[4 * q]);
-                dg[4 * q + 1] = fmaf(t.y, dh, dg[4 * q + 1]);
-                dg[4 * q + 2] = fmaf(t.z, dh, dg[4 * q + 2]);
-                if (q < 3) dg[4 * q + 3] = fmaf(t.w, dh, dg[4 * q + 3]);
+            for (int e = 0; e < 4; ++e) {
+                const int i = i4 + e;
+                dh4[e] = r4[e] > 0.f ? (s[LH_N1 + i] * dn[0] + s[LH_N1 + NH_HID + i] * dn[1]) +
+                                           s[LH_N1 + 2 * NH_HID + i] * dn[2]
+                                     : 0.f;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const float4 t = ld4(s, LH_N0 + 16 * i + 4 * q);
+                    dg[4 * q] = fmaf(t.x, dh4[e], dg[4 * q]);
+                    dg[4 * q + 1] = fmaf(t.y, dh4[e], dg[4 * q + 1]);
+                    dg[4 * q + 2] = fmaf(t.z, dh4[e], dg[4 * q + 2]);
+                    if (q < 3) dg[4 * q + 3] = fmaf(t.w, dh4[e], dg[4 * q + 3]);
+                }
             }
+            *reinterpret_cast<float4*>(rdh + i4) = make_float4(dh4[0], dh4[1], dh4[2], dh4[3]);
         }
+        *reinterpret_cast<float4*>(rr + NH_HID) = make_float4(1.f, 0.f, 0.f, 0.f);
 #pragma unroll
-        for (int k = 0; k < NH_GEO; ++k) s_geo[tid][k] = geo[k];
-#pragma unroll
-        for (int c = 0; c < 3; ++c) s_dn[tid][c] = dn[c];
+        for (int q = 0; q < 4; ++q)
+            *reinterpret_cast<float4*>(s_geo + tid * NH_SG + 4 * q) =
+                make_float4(geo[4 * q], geo[4 * q + 1], geo[4 * q + 2], geo[4 * q + 3]);
+        *reinterpret_cast<float4*>(s_dn + tid * 4) = make_float4(dn[0], dn[1], dn[2], 0.f);
         if (valid) {
-            float* d = a.dgeo + p * 16;
-            d[0] = 0.f;
-#pragma unroll
-            for (int k = 0; k < NH_GEO; ++k) d[1 + k] = dg[k];
+            float4* d = reinterpret_cast<float4*>(a.dgeo + p * 16);
+            d[0] = make_float4(0.f, dg[0], dg[1], dg[2]);
+            d[1] = make_float4(dg[3], dg[4], dg[5], dg[6]);
+            d[2] = make_float4(dg[7], dg[8], dg[9], dg[10]);
+            d[3] = make_float4(dg[11], dg[12], dg[13], dg[14]);
         }
-    __syncthreads();
-        // gradient value v = tid + NH_TILE j: N0 [i][k] | b0 [i] | N1 [c][i] | b1 [c], summed over the tile
+        __syncthreads();
+        // [dN0 | db0] += d hidden^T [geo | 1] over this thread's quarter of the tile
+#pragma unroll 4
+        for (int u = 0; u < NH_TILE / 4; ++u) {
+            const int q = quarter * (NH_TILE / 4) + u;
+            const float4 d4 = *reinterpret_cast<const float4*>(s_dh + q * NH_SDH + 4 * rg);
+            const float4 g4 = *reinterpret_cast<const float4*>(s_geo + q * NH_SG + 4 * cg);
+            const float dv[4] = {d4.x, d4.y, d4.z, d4.w}, gv[4] = {g4.x, g4.y, g4.z, g4.w};
 #pragma unroll
-        for (int j = 0; j < NH_OWN; ++j) {
-            const int v = tid + NH_TILE * j;
-            float t = 0.f;
-            if (v < NH_B0) {
-                const int i = v / NH_GEO, k = v % NH_GEO;
-#pragma unroll 8
-                for (int q = 0; q < NH_TILE; ++q) t = fmaf(s_dh[q][i], s_geo[q][k], t);
-            } else if (v < NH_N1) {
-#pragma unroll 8
-                for (int q = 0; q < NH_TILE; ++q) t += s_dh[q][v - NH_B0];
-            } else if (v < NH_B1) {
-                const int c = (v - NH_N1) / NH_HID, i = (v - NH_N1) % NH_HID;
-#pragma unroll 8
-                for (int q = 0; q < NH_TILE; ++q) t = fmaf(s_dn[q][c], fmaxf(s_hr[q][i], 0.f), t);
-            } else if (v < NH_ALL) {
-#pragma unroll 8
-                for (int q = 0; q < NH_TILE; ++q) t += s_dn[q][v - NH_B1];
+            for (int x = 0; x < 4; ++x)
+#pragma unroll
+                for (int y = 0; y < 4; ++y) acc0[4 * x + y] = fmaf(dv[x], gv[y], acc0[4 * x + y]);
+        }
+        if (own1) {   // [dN1 | db1] += d n^T [relu(hidden) | 1] over 16 points
+#pragma unroll 4
+            for (int u = 0; u < 16; ++u) {
+                const int q = grp1 * 16 + u;
+                const float4 n4 = *reinterpret_cast<const float4*>(s_dn + q * 4);
+                const float4 r4 = *reinterpret_cast<const float4*>(s_r + q * NH_SR + 4 * blk1);
+                const float nv[4] = {n4.x, n4.y, n4.z, n4.w}, rv[4] = {r4.x, r4.y, r4.z, r4.w};
+#pragma unroll
+                for (int x = 0; x < 4; ++x)
+#pragma unroll
+                    for (int y = 0; y < 4; ++y) acc1[4 * x + y] = fmaf(nv[x], rv[y], acc1[4 * x + y]);
             }
-            acc[j] += t;
         }
         __syncthreads();
     }
-    // per-block sums, reduced over blocks in order by normal_head_wgrad_reduce_kernel: every block
-    // adding its 611 values with atomics serialises ~1000 adds on each address at the L2
+    // the block's totals: quarters / point groups added in a fixed order (the LDS tiles reused)
+    float* part0 = s_dh;   // [4 quarters][32 x 16]
+    float* part1 = s_r;    // [8 groups][4 x 36]
 #pragma unroll
-    for (int j = 0; j < NH_OWN; ++j) {
-        const int v = tid + NH_TILE * j;
-        if (v < NH_ALL) a.partials[(size_t)blockIdx.x * NH_ALL + v] = acc[j];
+    for (int x = 0; x < 4; ++x)
+#pragma unroll
+        for (int y = 0; y < 4; ++y) part0[quarter * 512 + (4 * rg + x) * 16 + 4 * cg + y] = acc0[4 * x + y];
+    if (own1) {
+#pragma unroll
+        for (int x = 0; x < 4; ++x)
+#pragma unroll
+            for (int y = 0; y < 4; ++y) part1[grp1 * 144 + x * NH_R1 + 4 * blk1 + y] = acc1[4 * x + y];
+    }
+    __syncthreads();
+    for (int v = tid; v < NH_ALL; v += NH_TILE) {
+        float t = 0.f;
+        if (v < NH_N1) {   // N0 [i][k] | b0 [i] = column 15
+            const int idx = v < NH_B0 ? (v / NH_GEO) * 16 + v % NH_GEO : (v - NH_B0) * 16 + 15;
+#pragma unroll
+            for (int qq = 0; qq < 4; ++qq) t += part0[qq * 512 + idx];
+        } else {           // N1 [c][i] | b1 [c] = column 32
+            const int idx = v < NH_B1 ? ((v - NH_N1) / NH_HID) * NH_R1 + (v - NH_N1) % NH_HID : (v - NH_B1) * NH_R1 + NH_HID;
+#pragma unroll
+            for (int gg = 0; gg < 8; ++gg) t += part1[gg * 144 + idx];
+        }
+        a.partials[(size_t)blockIdx.x * NH_ALL + v] = t;
     }
 }
 
@@ -239,10 +311,13 @@ __global__ void __launch_bounds__(256) normal_head_wgrad_reduce_kernel(const flo
 }
 
 constexpr int kHeadBwdBlocks = 1024;
+constexpr int kHeadBwdResident = 768;
+static_assert(kHeadBwdResident <= kHeadBwdBlocks, "workspace");
 
 static int fill_normal(NormalArgs& a, const float* o16, const uint8_t* keep, int64_t P, const nerf_normal_head* W) {
     NERF_REQUIRE(P >= 0, "normal_head: n_points < 0");
     NERF_REQUIRE((P == 0 || o16) && W && W->n0 && W->b0 && W->n1 && W->b1, "normal_head: null argument");
+    NERF_REQUIRE(((uintptr_t)o16 & 15) == 0, "normal_head: geo rows must be 16-B aligned (16-float rows)");
     a.o16 = o16;
     a.keep = keep;
     a.P = P;
@@ -281,6 +356,7 @@ extern "C" int nerf_normal_head_bwd(const float* d_o16, const uint8_t* d_keep, i
     if (rc) return rc;
     NERF_REQUIRE((n_points == 0 || (d_graw7 && d_graw4 && d_dgeo)) && grads && grads->n0 && grads->b0 && grads->n1 && grads->b1,
                  "normal_head_bwd: null buffer");
+    NERF_REQUIRE((((uintptr_t)d_graw4 | (uintptr_t)d_dgeo) & 15) == 0, "normal_head_bwd: d raw4 / d geo must be 16-B aligned");
     NERF_REQUIRE(d_workspace && workspace_bytes >= nerf_normal_head_bwd_workspace_bytes(),
                  "normal_head_bwd: workspace %zu B < %zu B", workspace_bytes, nerf_normal_head_bwd_workspace_bytes());
     if (n_points == 0) return NERF_OK;
@@ -289,7 +365,8 @@ extern "C" int nerf_normal_head_bwd(const float* d_o16, const uint8_t* d_keep, i
     a.dgeo = d_dgeo;
     a.G = *grads;
     a.partials = d_workspace;
-    const unsigned blocks = (unsigned)std::min<int64_t>(blocks_for(n_points, NH_TILE), kHeadBwdBlocks);
+    // one round of resident blocks (51.6 KB of LDS each: 3 per CU on 256 CUs), at most the workspace's
+    const unsigned blocks = (unsigned)std::min<int64_t>(blocks_for(n_points, NH_TILE), kHeadBwdResident);
     hipLaunchKernelGGL(normal_head_bwd_kernel, dim3(blocks), dim3(NH_TILE), 0, as_stream(stream), a);
     NERF_CHECK_LAUNCH("normal_head_bwd");
     hipLaunchKernelGGL(normal_head_wgrad_reduce_kernel, dim3((NH_ALL + 3) / 4), dim3(256), 0, as_stream(stream),

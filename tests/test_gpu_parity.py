@@ -825,3 +825,43 @@ def test_sample_fine_merge_vs_torch_sort(nerf, gpu, S, N, det, shuffle):
         assert (want[:, 1:] == want[:, :-1]).any(), "the case must contain ties"
     else:
         assert not bool((samples[:, 1:] >= samples[:, :-1]).all()), "importance samples must arrive unsorted"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P", [1, 127, 100_003, 786_432])
+def test_normal_head_bwd_vs_torch_fp64(nerf, gpu, P):
+    """The normals head's backward kernel (csrc/normals.hip: per-point part, register-blocked weight
+    gradients over 128-point tiles, per-block partials summed in order) against torch fp64 autograd of
+    n = normalize(N1 relu(N0 geo + b0) + b1) with run_network's n_z mask, at ragged sizes up to the
+    ScanNet step's 786,432 points: d raw4, d geo and the four weight gradients."""
+    from indoor_nerf_amd import field
+    g = torch.Generator().manual_seed(P)
+    o16 = torch.randn(P, 16, generator=g) * 0.5
+    keep = torch.rand(P, generator=g) > 0.1
+    head = [torch.randn(32, 15, generator=g) * 0.3, torch.randn(32, generator=g) * 0.1,
+            torch.randn(3, 32, generator=g) * 0.3, torch.randn(3, generator=g) * 0.1]
+    g7 = torch.randn(P, 7, generator=g)
+    dev = [t.to(gpu).requires_grad_(True) for t in head]
+    for t in dev:
+        t.grad = None
+    graw4, dgeo = field._head_backward(o16.to(gpu), keep.to(gpu), dev, g7.to(gpu), [True] * 4)
+    torch.cuda.synchronize()
+    # fp64 reference
+    ref = [t.double().requires_grad_(True) for t in head]
+    geo = o16[:, 1:].double().requires_grad_(True)
+    hdn = geo @ ref[0].T + ref[1]
+    nn_ = torch.relu(hdn) @ ref[2].T + ref[3]
+    nrm = torch.nn.functional.normalize(nn_, dim=-1)
+    mask = torch.ones(P, 3, dtype=torch.float64)
+    mask[:, 2] = keep.double()
+    (nrm * mask * g7[:, 4:].double()).sum().backward()
+    np.testing.assert_array_equal(graw4.cpu().numpy(), g7[:, :4].numpy())
+    d = dgeo.cpu().double()
+    assert torch.all(d[:, 0] == 0)
+    # fp32 per-point arithmetic (the op order of the head's forward / normalize backward): 1e-4 absolute
+    # covers the few points whose ||n|| is small enough to amplify one rounding (1 in 1.5 M at 1e-5)
+    np.testing.assert_allclose(d[:, 1:].numpy(), geo.grad.numpy(), rtol=1e-4, atol=1e-4)
+    for i, (mine, r) in enumerate(zip(dev, ref)):
+        m = float(r.grad.abs().max())
+        err = float((mine.grad.cpu().double() - r.grad).abs().max())
+        assert err <= 1e-5 * m + 1e-6 * (P ** 0.5), (i, err, m)
