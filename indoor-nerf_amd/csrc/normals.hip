@@ -52,42 +52,12 @@ __device__ __forceinline__ void load_head(float* s, const nerf_normal_head& W) {
 
 __device__ __forceinline__ float4 ld4(const float* s, int i) { return *reinterpret_cast<const float4*>(s + i); }
 
-// F.linear with bias (addmm: bias + x W^T); fp32 dot products in input order
-__device__ __forceinline__ void head_forward(const float* s, const float* geo, float* h, float* n) {
-#pragma unroll 4
-    for (int i = 0; i < NH_HID; ++i) {
-        float w[16];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const float4 t = ld4(s, LH_N0 + 16 * i + 4 * q);
-            w[4 * q] = t.x; w[4 * q + 1] = t.y; w[4 * q + 2] = t.z; w[4 * q + 3] = t.w;
-        }
-        float acc = 0.f;
-#pragma unroll
-        for (int k = 0; k < NH_GEO; ++k) acc = fmaf(w[k], geo[k], acc);
-        h[i] = acc + s[LH_B0 + i];
-    }
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-        float acc = 0.f;
-#pragma unroll
-        for (int i = 0; i < NH_HID; i += 4) {
-            const float4 t = ld4(s, LH_N1 + c * NH_HID + i);
-            acc = fmaf(t.x, fmaxf(h[i], 0.f), acc);
-            acc = fmaf(t.y, fmaxf(h[i + 1], 0.f), acc);
-            acc = fmaf(t.z, fmaxf(h[i + 2], 0.f), acc);
-            acc = fmaf(t.w, fmaxf(h[i + 3], 0.f), acc);
-        }
-        n[c] = acc + s[LH_B1 + c];
-    }
-}
-
 __global__ void __launch_bounds__(256) normal_head_fwd_kernel(NormalArgs a) {
     __shared__ __attribute__((aligned(16))) float s[LH_ALL];
     load_head(s, a.W);
     const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= a.P) return;
-    float geo[NH_GEO], h[NH_HID], n[3];
+    float geo[NH_GEO], n[3];
     {   // o16 = [sigma, geo 0..14]: four 16-B loads instead of fifteen 4-B ones
         const float4* src = reinterpret_cast<const float4*>(a.o16 + p * 16);
         const float4 v0 = src[0], v1 = src[1], v2 = src[2], v3 = src[3];
@@ -96,7 +66,33 @@ __global__ void __launch_bounds__(256) normal_head_fwd_kernel(NormalArgs a) {
         geo[7] = v2.x; geo[8] = v2.y; geo[9] = v2.z; geo[10] = v2.w;
         geo[11] = v3.x; geo[12] = v3.y; geo[13] = v3.z; geo[14] = v3.w;
     }
-    head_forward(s, geo, h, n);
+    // F.linear with bias (addmm: bias + x W^T), fp32 dot products in input order; one hidden unit's N1
+    // terms added as it is formed: no [32] hidden array, four units per loop trip (unrolled whole, the compiler held every
+    // weight in registers: 174 VGPRs, two waves per SIMD)
+    {
+        float nacc[3] = {0.f, 0.f, 0.f};
+#pragma unroll 1
+        for (int i4 = 0; i4 < NH_HID; i4 += 4) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int i = i4 + e;
+                float acc = 0.f;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const float4 t = ld4(s, LH_N0 + 16 * i + 4 * q);
+                    acc = fmaf(t.x, geo[4 * q], acc);
+                    acc = fmaf(t.y, geo[4 * q + 1], acc);
+                    acc = fmaf(t.z, geo[4 * q + 2], acc);
+                    if (q < 3) acc = fmaf(t.w, geo[4 * q + 3], acc);
+                }
+                const float r = fmaxf(acc + s[LH_B0 + i], 0.f);
+#pragma unroll
+                for (int c = 0; c < 3; ++c) nacc[c] = fmaf(s[LH_N1 + c * NH_HID + i], r, nacc[c]);
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < 3; ++c) n[c] = nacc[c] + s[LH_B1 + c];
+    }
     // F.normalize(x, dim=-1): x / max(||x||_2, 1e-12)
     const float nrm = fmaxf(sqrtf(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]), 1e-12f);
     const float4 r = *reinterpret_cast<const float4*>(a.raw4 + 4 * p);
@@ -155,7 +151,7 @@ __global__ void __launch_bounds__(NH_TILE) __attribute__((amdgpu_waves_per_eu(2)
             geo[15] = 1.f;
         }
         // forward, four hidden units at a time (relu(hidden) to this thread's LDS row: its sign is the
-        // ReLU mask of the backward below), the same fp32 op order as head_forward
+        // ReLU mask of the backward below), the same fp32 op order as normal_head_fwd_kernel
         float* rdh = s_dh + tid * NH_SDH;
         float* rr = s_r + tid * NH_SR;
         float nacc[3] = {0.f, 0.f, 0.f};
