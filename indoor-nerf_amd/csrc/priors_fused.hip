@@ -360,10 +360,22 @@ __global__ void __launch_bounds__(64) priors_svd_kernel(PriorsArgs a) {
 }
 
 // ---- bitonic sort of up to 8192 64-bit keys in LDS (device-mode randperm) ------------------------
+// A stage of stride <= 64 pairs keys inside 128-key runs, and thread t's pairs lie in run t >> 6 (and
+// t >> 6 + 16, ... for t + kPT): every wave touches only its own runs, so such a stage after another
+// one needs a wave barrier, not a block barrier (4,096 keys: 15 block barriers instead of 78; the same
+// compare-swaps, so the same order bit for bit).
 __device__ void bitonic_sort(uint64_t* k, int M) {
+    int prev = 1 << 30;   // stride of the previous stage (the first stage follows the keys' stores)
     for (int size = 2; size <= M; size <<= 1)
         for (int stride = size >> 1; stride > 0; stride >>= 1) {
-            __syncthreads();
+            if (stride >= 128 || prev >= 128) {
+                __syncthreads();
+            } else {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
+            prev = stride;
             for (int t = threadIdx.x; t < M / 2; t += kPT) {
                 const int lo = 2 * t - (t & (stride - 1));
                 const int hi = lo + stride;
