@@ -381,6 +381,14 @@ typedef struct {
 
 int nerf_normal_head_fwd(const float* d_o16, const float* d_raw4, const uint8_t* d_keep, int64_t n_points,
                          const nerf_normal_head* head, float* d_raw7, void* stream);
+/* ABI 12: the forward over a permuted point order — source point q (its keep flag d_keep[q]) sits at
+ * merged row d_rows[q] of d_o16 / d_raw4 / d_raw7, and its keep flag is scattered to d_keep_out[d_rows[q]]
+ * (the merged-order mask nerf_normal_head_bwd reads). d_rows must be a permutation of [0, n_points);
+ * NULL rows = nerf_normal_head_fwd (d_keep_out NULL too). Replaces FieldFn's keep scatter on the fine
+ * pass with coarse-feature reuse (render.CoarseReuse: the MLP walks the importance-first order). */
+int nerf_normal_head_fwd_rows(const float* d_o16, const float* d_raw4, const uint8_t* d_keep, const int32_t* d_rows,
+                              int64_t n_points, const nerf_normal_head* head, float* d_raw7, uint8_t* d_keep_out,
+                              void* stream);
 size_t nerf_normal_head_bwd_workspace_bytes(void);
 int nerf_normal_head_bwd(const float* d_o16, const uint8_t* d_keep, int64_t n_points,
                          const nerf_normal_head* head, const float* d_graw7, float* d_graw4, float* d_dgeo,

@@ -177,6 +177,7 @@ SIGNATURES = {
                         c_vp, c_vp],
     "nerf_mlp_bwd_batch": [ctypes.POINTER(MlpBwdJob), c_int, c_vp, ctypes.c_size_t, c_vp],
     "nerf_normal_head_fwd": [c_vp, c_vp, c_vp, c_i64, ctypes.POINTER(NormalHead), c_vp, c_vp],
+    "nerf_normal_head_fwd_rows": [c_vp, c_vp, c_vp, c_vp, c_i64, ctypes.POINTER(NormalHead), c_vp, c_vp, c_vp],
     "nerf_normal_head_bwd": [c_vp, c_vp, c_i64, ctypes.POINTER(NormalHead), c_vp, c_vp, c_vp,
                              ctypes.POINTER(NormalHeadGrads), c_vp, ctypes.c_size_t, c_vp],
     "nerf_composite_fwd": [c_vp, c_int, c_vp, c_vp, c_vp, c_i64, c_int, c_int,

@@ -19,4 +19,4 @@ void set_error(const char* fmt, ...) {
 
 extern "C" const char* nerf_last_error(void) { return nerf::g_last_error; }
 
-extern "C" int nerf_abi_version(void) { return 11; }
+extern "C" int nerf_abi_version(void) { return 12; }

@@ -22,7 +22,9 @@ constexpr int NH_N0 = 0, NH_B0 = NH_N0 + NH_HID * NH_GEO, NH_N1 = NH_B0 + NH_HID
 struct NormalArgs {
     const float* o16;      // [P,16] = [sigma, geo 15] (MLP geo output)
     const float* raw4;     // [P,4]
-    const uint8_t* keep;   // [P] or null
+    const uint8_t* keep;   // [P] or null (fwd with rows: indexed in the source order)
+    const int32_t* rows;   // fwd: null, or the merged row of each source-order point (a permutation of [0, P))
+    uint8_t* keep_out;     // fwd with rows: keep scattered to the merged rows (what the backward reads)
     int64_t P;
     nerf_normal_head W;
     float* raw7;           // fwd out [P,7]
@@ -55,8 +57,11 @@ __device__ __forceinline__ float4 ld4(const float* s, int i) { return *reinterpr
 __global__ void __launch_bounds__(256) normal_head_fwd_kernel(NormalArgs a) {
     __shared__ __attribute__((aligned(16))) float s[LH_ALL];
     load_head(s, a.W);
-    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= a.P) return;
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= a.P) return;
+    // with rows, thread q takes source point q at its merged row p (the fine pass's importance-first
+    // walk): its keep flag lands at p for the backward, replacing a scatter of its own
+    const int64_t p = a.rows ? (int64_t)a.rows[q] : q;
     float geo[NH_GEO], n[3];
     {   // o16 = [sigma, geo 0..14]: four 16-B loads instead of fifteen 4-B ones
         const float4* src = reinterpret_cast<const float4*>(a.o16 + p * 16);
@@ -96,7 +101,8 @@ __global__ void __launch_bounds__(256) normal_head_fwd_kernel(NormalArgs a) {
     // F.normalize(x, dim=-1): x / max(||x||_2, 1e-12)
     const float nrm = fmaxf(sqrtf(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]), 1e-12f);
     const float4 r = *reinterpret_cast<const float4*>(a.raw4 + 4 * p);
-    const bool keep = a.keep ? a.keep[p] != 0 : true;
+    const bool keep = a.keep ? a.keep[q] != 0 : true;
+    if (a.keep_out) a.keep_out[p] = keep ? 1 : 0;
     float* o = a.raw7 + 7 * p;
     o[0] = r.x; o[1] = r.y; o[2] = r.z; o[3] = r.w;
     o[4] = n[0] / nrm;
@@ -325,18 +331,28 @@ static int fill_normal(NormalArgs& a, const float* o16, const uint8_t* keep, int
 
 using namespace nerf;
 
-extern "C" int nerf_normal_head_fwd(const float* d_o16, const float* d_raw4, const uint8_t* d_keep, int64_t n_points,
-                                    const nerf_normal_head* head, float* d_raw7, void* stream) {
+extern "C" int nerf_normal_head_fwd_rows(const float* d_o16, const float* d_raw4, const uint8_t* d_keep,
+                                         const int32_t* d_rows, int64_t n_points, const nerf_normal_head* head,
+                                         float* d_raw7, uint8_t* d_keep_out, void* stream) {
     NormalArgs a{};
     int rc = fill_normal(a, d_o16, d_keep, n_points, head);
     if (rc) return rc;
     NERF_REQUIRE(n_points == 0 || (d_raw4 && d_raw7), "normal_head_fwd: null buffer");
+    NERF_REQUIRE(!d_rows || n_points <= INT32_MAX, "normal_head_fwd: rows are int32");
+    NERF_REQUIRE(!d_keep_out || d_keep, "normal_head_fwd: keep_out needs keep");
     if (n_points == 0) return NERF_OK;
+    a.rows = d_rows;
+    a.keep_out = d_keep_out;
     a.raw4 = d_raw4;
     a.raw7 = d_raw7;
     hipLaunchKernelGGL(normal_head_fwd_kernel, dim3(blocks_for(n_points, 256)), dim3(256), 0, as_stream(stream), a);
     NERF_CHECK_LAUNCH("normal_head_fwd");
     return NERF_OK;
+}
+
+extern "C" int nerf_normal_head_fwd(const float* d_o16, const float* d_raw4, const uint8_t* d_keep, int64_t n_points,
+                                    const nerf_normal_head* head, float* d_raw7, void* stream) {
+    return nerf_normal_head_fwd_rows(d_o16, d_raw4, d_keep, nullptr, n_points, head, d_raw7, nullptr, stream);
 }
 
 extern "C" size_t nerf_normal_head_bwd_workspace_bytes(void) {

@@ -56,14 +56,24 @@ def _head_struct(head):
     return h
 
 
-def _head_forward(o16, raw4, keep, head):
-    """raw [P,7] = [raw4, normals] (csrc/normals.hip); keep masks n_z like run_network."""
+def _head_forward(o16, raw4, keep, head, rows=None):
+    """raw [P,7] = [raw4, normals] (csrc/normals.hip); keep masks n_z like run_network. rows (int32):
+    keep is in a source order whose point q sits at merged row rows[q]; then returns (raw7, the keep
+    flags scattered to the merged rows), else raw7."""
     P = raw4.shape[0]
     raw7 = torch.empty(P, 7, device=raw4.device, dtype=torch.float32)
-    _lib.call("nerf_normal_head_fwd", _lib.ptr(o16, "geo"), _lib.ptr(raw4, "raw4"),
-              _lib.ptr(keep, "keep", dtype=torch.bool, allow_none=True), P, _head_struct(head),
-              _lib.ptr(raw7, "raw7"), _lib.stream())
-    return raw7
+    if rows is None:
+        _lib.call("nerf_normal_head_fwd", _lib.ptr(o16, "geo"), _lib.ptr(raw4, "raw4"),
+                  _lib.ptr(keep, "keep", dtype=torch.bool, allow_none=True), P, _head_struct(head),
+                  _lib.ptr(raw7, "raw7"), _lib.stream())
+        return raw7
+    if rows.shape[0] < P:
+        raise ValueError(f"normal head: {rows.shape[0]} rows for {P} points")
+    keep_m = torch.empty_like(keep)
+    _lib.call("nerf_normal_head_fwd_rows", _lib.ptr(o16, "geo"), _lib.ptr(raw4, "raw4"),
+              _lib.ptr(keep, "keep", dtype=torch.bool), _lib.ptr(rows, "rows", torch.int32), P, _head_struct(head),
+              _lib.ptr(raw7, "raw7"), _lib.ptr(keep_m, "keep_out", dtype=torch.bool), _lib.stream())
+    return raw7, keep_m
 
 
 def _head_backward(o16, keep, head, g7, needs):
@@ -217,8 +227,6 @@ class FieldFn(torch.autograd.Function):
         # with the normals head, run_network's mask lands on n_z, not sigma (run_nerf.py:66); the head
         # runs in the merged order of raw / geo
         keep_arg = None if head else _lib.ptr(keep, "keep", dtype=torch.bool)
-        if head and order is not None:
-            keep = torch.empty_like(keep).index_put_((order[0].long(),), keep)
         if sh_rays is not None:
             view_args = (_lib.ptr(sh_rays, "sh_rows"), 0, None)
         else:
@@ -236,7 +244,9 @@ class FieldFn(torch.autograd.Function):
                   _lib.ptr(o16, "geo", allow_none=True), _lib.ptr(arec, "act_record", allow_none=True), None, 0,
                   _point_order(order), _lib.ptr(h3, "h3", allow_none=True), _lib.stream())
         ctx.h3 = h3
-        if head:
+        if head and order is not None:   # keep scattered to the merged rows by the head's own launch
+            raw, keep = _head_forward(o16, raw, keep, head, rows=order[0])
+        elif head:
             raw = _head_forward(o16, raw, keep, head)
         ctx.save_for_backward(pts, viewdirs, feat, keep, o16, w0q, arec, *params)
         ctx.spr, ctx.embedder, ctx.n_tab, ctx.n_head = spr, embedder, n_tab, len(head)

@@ -22,7 +22,7 @@ def test_library_exports_every_declared_symbol(nerf):
     for name in declared:
         assert hasattr(lib, name), f"libnerfhip.so does not export {name}"
     assert sorted(L.exported_symbols()) == declared, "ctypes signature table out of sync with the header"
-    assert lib.nerf_abi_version() == 11   # 11: TV bins in the hash bin launch (nerf_hash_encode_bwd_bin_batch_tv); 10: saved h3 (nerf_mlp_fwd_h3, job.h3); 9: RAdam grad_scale
+    assert lib.nerf_abi_version() == 12   # 12: nerf_normal_head_fwd_rows; 11: TV bins in the hash bin launch (nerf_hash_encode_bwd_bin_batch_tv); 10: saved h3 (nerf_mlp_fwd_h3, job.h3); 9: RAdam grad_scale
 
 
 def test_error_path_reports_message(nerf):

@@ -865,3 +865,25 @@ def test_normal_head_bwd_vs_torch_fp64(nerf, gpu, P):
         m = float(r.grad.abs().max())
         err = float((mine.grad.cpu().double() - r.grad).abs().max())
         assert err <= 1e-5 * m + 1e-6 * (P ** 0.5), (i, err, m)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P", [1, 255, 786_432])
+def test_normal_head_fwd_rows_matches_scatter(nerf, gpu, P):
+    """nerf_normal_head_fwd_rows (the fine pass with coarse-feature reuse: keep flags in the MLP's
+    importance-first order, rows = the merged row of each) against the plain forward after the
+    scatter it replaces (keep_m[rows] = keep): raw7 and the merged keep flags bit for bit."""
+    from indoor_nerf_amd import field
+    g = torch.Generator().manual_seed(P + 7)
+    o16 = (torch.randn(P, 16, generator=g) * 0.5).to(gpu)
+    raw4 = torch.randn(P, 4, generator=g).to(gpu)
+    keep = (torch.rand(P, generator=g) > 0.2).to(gpu)
+    rows = torch.randperm(P, generator=g).to(torch.int32).to(gpu)
+    head = [(torch.randn(32, 15, generator=g) * 0.3).to(gpu), (torch.randn(32, generator=g) * 0.1).to(gpu),
+            (torch.randn(3, 32, generator=g) * 0.3).to(gpu), (torch.randn(3, generator=g) * 0.1).to(gpu)]
+    raw7, keep_m = field._head_forward(o16, raw4, keep, head, rows=rows)
+    want_keep = torch.empty_like(keep).index_put_((rows.long(),), keep)
+    want = field._head_forward(o16, raw4, want_keep, head)
+    torch.cuda.synchronize()
+    assert torch.equal(keep_m, want_keep)
+    assert torch.equal(raw7, want)
