@@ -21,8 +21,13 @@ for e in prof.events():
         continue
     if not e.kernels:
         continue
-    frames = [f for f in (e.stack or []) if "indoor-nerf_amd" in f or "bench.py" in f]
-    key = (e.name, frames[0] if frames else "?")
+    chain, x, frames = [e.name], e, []
+    while x is not None and not frames:   # an op nested in another (copy_ in contiguous) has no stack of its own
+        frames = [f for f in (x.stack or []) if "indoor-nerf_amd" in f or "bench.py" in f]
+        x = x.cpu_parent
+        if x is not None and not frames:
+            chain.append(x.name)
+    key = ("<".join(chain[:4]) + " [" + e.kernels[0].name[:40] + "]", frames[0] if frames else "?")
     seen[key] = seen.get(key, 0) + 1
 for (name, fr), n in sorted(seen.items(), key=lambda kv: -kv[1]):
     print(f"{n:5d}  {name:28s} {fr}")
