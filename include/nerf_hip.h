@@ -747,6 +747,12 @@ int nerf_priors_prep(const float* d_depth, const float* d_normals, const float* 
 int nerf_priors_loss(const float* d_depth, const float* d_normals, const float* d_coords, int64_t n_rays,
                      const nerf_priors_config* cfg, void* d_workspace, size_t workspace_bytes, float* d_loss,
                      float* d_parts, void* stream);
+/* ABI 12: nerf_priors_loss with *d_loss = *d_addend + total (one fp32 add: the training step's
+ * `loss + structural_loss`, run_nerf.py:1131, without a launch of its own); d_addend NULL = total.
+ * d_parts of both entries is written by the loss launch itself (no device copy after it). */
+int nerf_priors_loss_add(const float* d_depth, const float* d_normals, const float* d_coords, int64_t n_rays,
+                         const nerf_priors_config* cfg, void* d_workspace, size_t workspace_bytes,
+                         const float* d_addend, float* d_loss, float* d_parts, void* stream);
 int nerf_priors_bwd(const float* d_depth, const float* d_normals, const float* d_coords, int64_t n_rays,
                     const nerf_priors_config* cfg, void* d_workspace, size_t workspace_bytes,
                     const float* d_grad_loss, float* d_grad_depth, float* d_grad_normals, void* stream);

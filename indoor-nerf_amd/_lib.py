@@ -173,6 +173,8 @@ SIGNATURES = {
     "nerf_priors_prep": [c_vp, c_vp, c_vp, c_i64, ctypes.POINTER(PriorsConfig), c_vp, ctypes.c_size_t, c_vp, c_vp],
     "nerf_priors_loss": [c_vp, c_vp, c_vp, c_i64, ctypes.POINTER(PriorsConfig), c_vp, ctypes.c_size_t, c_vp, c_vp,
                          c_vp],
+    "nerf_priors_loss_add": [c_vp, c_vp, c_vp, c_i64, ctypes.POINTER(PriorsConfig), c_vp, ctypes.c_size_t, c_vp, c_vp,
+                             c_vp, c_vp],
     "nerf_priors_bwd": [c_vp, c_vp, c_vp, c_i64, ctypes.POINTER(PriorsConfig), c_vp, ctypes.c_size_t, c_vp, c_vp,
                         c_vp, c_vp],
     "nerf_mlp_bwd_batch": [ctypes.POINTER(MlpBwdJob), c_int, c_vp, ctypes.c_size_t, c_vp],

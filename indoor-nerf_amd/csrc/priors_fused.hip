@@ -18,6 +18,8 @@
 //                        backward), and (device mode) the 3x3 SVD of the centres;
 //   priors_loss_kernel : frame, the three losses, their sum;
 //   priors_bwd_kernel  : d depth, d normals from d loss.
+// With pixel coordinates the loss launch stops after the consistency queries: the nearest-pixel
+// search runs one block per query (priors_nearest_kernel) and priors_loss_tail_kernel finishes.
 // Randomness: the reference draws torch.randn (k-means init), torch.randperm (planarity pairs) and
 // torch.randint (consistency queries). Replay mode takes those draws as inputs (the Python layer
 // makes them with torch's generators in the reference's order); device mode draws them from
@@ -73,6 +75,8 @@ struct PriorsArgs {
     int8_t* assign;           // [10][N] k-means assignment per round (-1: not kept)
     int32_t* members;         // [3][N] class members in index order
     float* loss;              // [1]
+    const float* addend;      // loss: optional [1] added to the total in the loss word (the iteration's other losses)
+    float* parts_out;         // loss: optional [7] copy of PriorsState::parts
     const float* d_loss;      // bwd: [1] upstream gradient
     float* d_depth;           // bwd: [N]
     float* d_normals;         // bwd: [N, 3]
@@ -388,6 +392,34 @@ __device__ void bitonic_sort(uint64_t* k, int M) {
 }
 
 // ================================================================ losses
+// normal consistency over the ncons (idx1, idx2, dist) triples of st, then the total, the loss word
+// (+ the caller's addend) and the parts; every thread of the block calls it
+__device__ void consistency_and_total(const PriorsArgs& a, PriorsState& st, int ncons, float scale, float mloss,
+                                      float ploss, float pf, float pw, float pg, float* s_red) {
+    const bool xy = a.coords != nullptr;
+    float cs = 0.f;
+    for (int q = threadIdx.x; q < ncons; q += kPT) {
+        float n1[3], n2[3], l1, l2;
+        const int i1 = st.idx1[q], i2 = st.idx2[q];
+        load_nz(a, i1, n1, l1);
+        load_nz(a, i2, n2, l2);
+        const float dsim = expf(-fabsf(a.depth[i1] - a.depth[i2]));
+        const float wq = xy ? expf(-st.dist[q] * 0.1f) * dsim : dsim;
+        cs += wq * (1.0f - dot3(n1, n2));
+    }
+    cs = block_sum(cs, s_red);
+    const float closs = (a.use_c && ncons > 0) ? a.w_c * scale * (cs / (float)ncons) : 0.f;
+    if (threadIdx.x == 0) {
+        const float total = ((0.f + mloss) + ploss) + closs;
+        st.parts[5] = closs; st.parts[6] = total;
+        *a.loss = a.addend ? *a.addend + total : total;   // the caller's `loss + total`, one fp32 add
+        if (a.parts_out) {
+            const float pv[7] = {pf, pw, pg, mloss, ploss, closs, total};
+            for (int k = 0; k < 7; ++k) a.parts_out[k] = pv[k];
+        }
+    }
+}
+
 __global__ void __launch_bounds__(kPT) priors_loss_kernel(PriorsArgs a) {
     __shared__ float s_red[17 * 4];
     __shared__ int s_ired[16];
@@ -538,55 +570,61 @@ __global__ void __launch_bounds__(kPT) priors_loss_kernel(PriorsArgs a) {
         }
     }
     __syncthreads();
-    if (xy) {   // nearest other pixel per query: one wave per query, first index on ties
-        const int lane = tid & 63, w = tid >> 6;
-        for (int q = w; q < ncons; q += kPT / 64) {
-            const int self = st.idx1[q];
-            const float qx = a.coords[2 * self], qy = a.coords[2 * self + 1];
-            float best = INFINITY;
-            int bi = N;
-            for (int i = lane; i < N; i += 64) {
-                const float dx = a.coords[2 * i] - qx, dy = a.coords[2 * i + 1] - qy;
-                const float d2 = i == self ? INFINITY : dx * dx + dy * dy;
-                if (d2 < best) { best = d2; bi = i; }
-            }
-            for (int o = 32; o > 0; o >>= 1) {
-                const float ob = __shfl_xor(best, o, 64);
-                const int oi = __shfl_xor(bi, o, 64);
-                if (ob < best || (ob == best && oi < bi)) { best = ob; bi = oi; }
-            }
-            if (lane == 0) {
-                if (bi >= N) bi = self == 0 ? 1 : 0;
-                st.idx2[q] = bi;
-                st.dist[q] = sqrtf(best);
-            }
-        }
-    } else {
-        for (int q = tid; q < ncons; q += kPT) { st.idx2[q] = st.idx1[q] + 1; st.dist[q] = 0.f; }
-    }
-    __syncthreads();
-    float cs = 0.f;
-    for (int q = tid; q < ncons; q += kPT) {
-        float n1[3], n2[3], l1, l2;
-        const int i1 = st.idx1[q], i2 = st.idx2[q];
-        load_nz(a, i1, n1, l1);
-        load_nz(a, i2, n2, l2);
-        const float dsim = expf(-fabsf(a.depth[i1] - a.depth[i2]));
-        const float wq = xy ? expf(-st.dist[q] * 0.1f) * dsim : dsim;
-        cs += wq * (1.0f - dot3(n1, n2));
-    }
-    cs = block_sum(cs, s_red);
-    const float closs = (a.use_c && ncons > 0) ? a.w_c * scale * (cs / (float)ncons) : 0.f;
-    if (tid == 0) {
-        const float total = ((0.f + mloss) + ploss) + closs;
+    if (tid == 0) {   // the tail's inputs (priors_loss_tail_kernel reads them back with pixel coordinates)
         st.M = M;
         st.n_sure = nsure;
         st.pair_n[0] = npair[0]; st.pair_n[1] = npair[1]; st.pair_n[2] = npair[2];
         st.n_cons = ncons;
         st.parts[0] = pf; st.parts[1] = pw; st.parts[2] = pg;
-        st.parts[3] = mloss; st.parts[4] = ploss; st.parts[5] = closs; st.parts[6] = total;
-        *a.loss = total;
+        st.parts[3] = mloss; st.parts[4] = ploss;
     }
+    if (xy) return;   // nearest pixels: priors_nearest_kernel (one block per query), then the tail
+    for (int q = tid; q < ncons; q += kPT) { st.idx2[q] = st.idx1[q] + 1; st.dist[q] = 0.f; }
+    __syncthreads();
+    consistency_and_total(a, st, ncons, scale, mloss, ploss, pf, pw, pg, s_red);
+}
+
+// Pixel-coordinate mode (spatial_coords given, :333-346): the nearest other pixel of query q, one
+// block per query over all N candidates (a single workgroup scanning 200 x N took ~90 us on one CU),
+// the lowest index on ties (torch.argmin), the same comparisons as nerf_nearest_pixel.
+__global__ void __launch_bounds__(256) priors_nearest_kernel(PriorsArgs a) {
+    PriorsState& st = *a.st;
+    const int q = blockIdx.x, N = a.N;
+    if (q >= st.n_cons) return;
+    const int self = st.idx1[q];
+    const float qx = a.coords[2 * self], qy = a.coords[2 * self + 1];
+    float best = INFINITY;
+    int bi = N;
+    for (int i = threadIdx.x; i < N; i += blockDim.x) {
+        const float dx = a.coords[2 * i] - qx, dy = a.coords[2 * i + 1] - qy;
+        const float d2 = i == self ? INFINITY : dx * dx + dy * dy;
+        if (d2 < best) { best = d2; bi = i; }   // strided ascending scan: first minimum per thread
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const float ob = __shfl_xor(best, o, 64);
+        const int oi = __shfl_xor(bi, o, 64);
+        if (ob < best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+    }
+    __shared__ float s_b[4];
+    __shared__ int s_i[4];
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { s_b[w] = best; s_i[w] = bi; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int k = 1; k < 4; ++k)
+            if (s_b[k] < best || (s_b[k] == best && s_i[k] < bi)) { best = s_b[k]; bi = s_i[k]; }
+        if (bi >= N) bi = self == 0 ? 1 : 0;
+        st.idx2[q] = bi;
+        st.dist[q] = sqrtf(best);
+    }
+}
+
+__global__ void __launch_bounds__(kPT) priors_loss_tail_kernel(PriorsArgs a) {
+    __shared__ float s_red[17 * 4];
+    PriorsState& st = *a.st;
+    const float scale = a.d_scale ? *a.d_scale : 1.0f;
+    consistency_and_total(a, st, st.n_cons, scale, st.parts[3], st.parts[4], st.parts[0], st.parts[1], st.parts[2],
+                          s_red);
 }
 
 // ================================================================ backward
@@ -847,28 +885,36 @@ extern "C" int nerf_priors_prep(const float* d_depth, const float* d_normals, co
     return NERF_OK;
 }
 
-extern "C" int nerf_priors_loss(const float* d_depth, const float* d_normals, const float* d_coords, int64_t n_rays,
-                                const nerf_priors_config* cfg, void* d_workspace, size_t workspace_bytes,
-                                float* d_loss, float* d_parts, void* stream) {
+extern "C" int nerf_priors_loss_add(const float* d_depth, const float* d_normals, const float* d_coords,
+                                    int64_t n_rays, const nerf_priors_config* cfg, void* d_workspace,
+                                    size_t workspace_bytes, const float* d_addend, float* d_loss, float* d_parts,
+                                    void* stream) {
     PriorsArgs a{};
     int rc = priors_args(a, d_depth, d_normals, d_coords, n_rays, cfg, d_workspace, workspace_bytes);
     if (rc) return rc;
     NERF_REQUIRE(d_loss, "priors_loss: null loss");
     a.loss = d_loss;
+    a.addend = d_addend;
+    a.parts_out = d_parts;   // floor, wall, general, manhattan, planarity, consistency, total: stored by the kernel
     int M2 = 1;
     while (M2 < n_rays) M2 <<= 1;
     const size_t lds = cfg->perm ? 0 : (size_t)M2 * sizeof(uint64_t);
     hipLaunchKernelGGL(priors_loss_kernel, dim3(1), dim3(kPT), lds, as_stream(stream), a);
     NERF_CHECK_LAUNCH("priors_loss");
-    if (d_parts) {   // floor, wall, general, manhattan, planarity, consistency, total, + counts as floats
-        const hipError_t e = hipMemcpyAsync(d_parts, a.st->parts, 7 * sizeof(float), hipMemcpyDeviceToDevice,
-                                            as_stream(stream));
-        if (e != hipSuccess) {
-            set_error("priors_loss: hipMemcpyAsync failed");
-            return NERF_E_LAUNCH;
-        }
+    if (d_coords) {   // the nearest-pixel queries (n_cons <= kMaxCons, read by each block) and the tail
+        hipLaunchKernelGGL(priors_nearest_kernel, dim3(kMaxCons), dim3(256), 0, as_stream(stream), a);
+        NERF_CHECK_LAUNCH("priors_loss (nearest)");
+        hipLaunchKernelGGL(priors_loss_tail_kernel, dim3(1), dim3(kPT), 0, as_stream(stream), a);
+        NERF_CHECK_LAUNCH("priors_loss (tail)");
     }
     return NERF_OK;
+}
+
+extern "C" int nerf_priors_loss(const float* d_depth, const float* d_normals, const float* d_coords, int64_t n_rays,
+                                const nerf_priors_config* cfg, void* d_workspace, size_t workspace_bytes,
+                                float* d_loss, float* d_parts, void* stream) {
+    return nerf_priors_loss_add(d_depth, d_normals, d_coords, n_rays, cfg, d_workspace, workspace_bytes, nullptr,
+                                d_loss, d_parts, stream);
 }
 
 extern "C" int nerf_priors_bwd(const float* d_depth, const float* d_normals, const float* d_coords, int64_t n_rays,

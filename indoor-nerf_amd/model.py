@@ -206,7 +206,7 @@ def _forward_backward(batch_rays, target_s, render_kwargs_train, optimizer, args
     if schedule and global_step > 1000:
         args.tv_loss_weight = 0.0
     if get("use_structural_priors") and global_step >= get("structural_loss_start_iter"):
-        loss = loss + structural_loss(depth, extras, args, global_step, spatial_coords)
+        loss = structural_loss(depth, extras, args, global_step, spatial_coords, addend=loss)
     _lib.flush_zero_fills()       # fills no launch took (render() without rays to pack)
     loss.backward(_unit_seed(loss))
     hashgrid.materialize_zero()   # table gradients whose deferred zero no owner pass consumed
@@ -237,7 +237,7 @@ def fused_priors_eligible(args, n_rays):
             and 1 <= int(n_rays) <= _lib.PRIORS_MAX_RAYS)
 
 
-def structural_loss(depth, extras, args, global_step, spatial_coords=None):
+def structural_loss(depth, extras, args, global_step, spatial_coords=None, addend=None):
     """run_nerf.py:1068-1131: the structural-prior weights ramp from 10 % to 100 % over
     structural_loss_ramp_iters, then combine_structural_losses_v2 on the fine pass's depth and normal
     maps. Default: the device path (priors.fused_structural_losses, csrc/priors_fused.hip: no host
@@ -246,7 +246,8 @@ def structural_loss(depth, extras, args, global_step, spatial_coords=None):
     path (priors.combine_structural_losses_v2, the reference's RNG draws; its estimators persist
     across iterations, run_nerf.py:939-940). The overfitting-driven weight reduction (:1073-1094)
     needs train()'s test-set PSNR history and is left to the caller. Failures are swallowed as in
-    the reference (:1144-1148)."""
+    the reference (:1144-1148). addend (the iteration's other losses): returns addend + the structural
+    loss (the device path forms the sum in its loss launch)."""
     from . import graphs
     from .priors import (ManhattanFrameEstimator, SemanticPlaneDetector, combine_structural_losses_v2,
                          fused_structural_losses)
@@ -269,7 +270,7 @@ def structural_loss(depth, extras, args, global_step, spatial_coords=None):
             scale = sc.dev_f[off:off + 1]
         else:
             scale = torch.full((1,), ramp_of(global_step), device=depth.device)
-        total, _ = fused_structural_losses(depth, normals, spatial_coords, base, 0.4, 0.5, scale=scale)
+        total, _ = fused_structural_losses(depth, normals, spatial_coords, base, 0.4, 0.5, scale=scale, addend=addend)
         return total
     if getattr(args, "_priors", None) is None:
         args._priors = (ManhattanFrameEstimator(confidence_threshold=0.4), SemanticPlaneDetector(normal_threshold=0.5))
@@ -280,8 +281,8 @@ def structural_loss(depth, extras, args, global_step, spatial_coords=None):
                                                 *args._priors)
     except Exception as e:   # noqa: BLE001 - the reference's policy
         print(f"  ⚠️  Structural priors V2 failed: {e}")
-        return 0.0
-    return total
+        total = 0.0
+    return total if addend is None else addend + total
 
 
 def structural_overfit_update(args, global_step, psnr_list):

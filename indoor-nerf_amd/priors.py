@@ -271,10 +271,11 @@ def _fused_workspace(n, device):
 
 
 class _FusedPriorsFn(torch.autograd.Function):
-    """(depth [N], normals [N,3]) -> total structural loss (0-dim), d depth / d normals in backward."""
+    """(depth [N], normals [N,3]) -> total structural loss (0-dim), d depth / d normals in backward.
+    With addend (a 0-dim loss), returns addend + total from the same launch (its gradient passes through)."""
 
     @staticmethod
-    def forward(ctx, depth, normals, coords, spec):
+    def forward(ctx, depth, normals, coords, addend, spec):
         dev = depth.device
         N = depth.shape[0]
         d = depth.detach().float().contiguous()
@@ -315,8 +316,11 @@ class _FusedPriorsFn(torch.autograd.Function):
             _lib.call("nerf_priors_prep", *args, ctypes_ref(cfg), *wsp, None, _lib.stream())
         loss = torch.empty(1, device=dev)
         parts = torch.empty(7, device=dev)
-        _lib.call("nerf_priors_loss", *args, ctypes_ref(cfg), *wsp, _lib.ptr(loss, "loss"), _lib.ptr(parts, "parts"),
-                  _lib.stream())
+        if addend is not None:
+            addend = addend.detach().float().reshape(1).contiguous()
+            keep_alive.append(addend)
+        _lib.call("nerf_priors_loss_add", *args, ctypes_ref(cfg), *wsp, _lib.ptr(addend, "addend", allow_none=True),
+                  _lib.ptr(loss, "loss"), _lib.ptr(parts, "parts"), _lib.stream())
         ctx.save_for_backward(d, n, xy if xy is not None else torch.empty(0, device=dev))
         ctx.cfg, ctx.ws, ctx.keep, ctx.has_xy, ctx.parts = cfg, ws, keep_alive, xy is not None, parts
         spec["parts"] = parts
@@ -332,7 +336,7 @@ class _FusedPriorsFn(torch.autograd.Function):
                   _lib.ptr(xy, "coords") if ctx.has_xy else None, N, ctypes_ref(ctx.cfg),
                   _lib.ptr(ctx.ws, "workspace", dtype=torch.uint8), ctx.ws.numel(), _lib.ptr(g1, "grad_loss"),
                   _lib.ptr(gd, "grad_depth"), _lib.ptr(gn, "grad_normals"), _lib.stream())
-        return gd, gn, None, None
+        return gd, gn, None, (g if ctx.needs_input_grad[3] else None), None
 
 
 def ctypes_ref(cfg):
@@ -383,15 +387,17 @@ def _replay_draws(cfg, n, xy, N, spec, keep_alive):
 
 
 def fused_structural_losses(depth_pred, normals, spatial_coords=None, weights=None, confidence_threshold=0.4,
-                            normal_threshold=0.5, scale=None, replay=False, workspace=None):
+                            normal_threshold=0.5, scale=None, replay=False, workspace=None, addend=None):
     """combine_structural_losses_v2 on the device (csrc/priors_fused.hip): same losses, branches and
     autograd graph, no host synchronisation (capturable in a HIP graph). scale: optional device [1]
     multiplier of the weights (the train() ramp, a per-step graph slot). replay=True draws the
     reference's torch.randn/randperm/randint in its order and takes the frame's SVD from LAPACK
     (host syncs; the golden F18 parity mode). workspace: optional uint8 device tensor of at least
     nerf_priors_workspace_bytes(N) for this call's state (default: a fresh one per call; pass one to
-    inspect the PriorsState afterwards). Returns (total, parts) with parts a device [7] tensor
-    (floor, wall, general, manhattan, planarity, consistency, total)."""
+    inspect the PriorsState afterwards). addend: optional 0-dim loss; then the first result is
+    addend + total, formed in the loss launch (nerf_priors_loss_add: the training step's
+    `loss + structural_loss` without an add of its own). Returns (total, parts) with parts a device
+    [7] tensor (floor, wall, general, manhattan, planarity, consistency, total)."""
     if weights is None:
         weights = {"manhattan": 1.0, "planarity": 1.0, "normal_consistency": 0.5}
     N = depth_pred.shape[0]
@@ -399,5 +405,9 @@ def fused_structural_losses(depth_pred, normals, spatial_coords=None, weights=No
         raise ValueError(f"fused_structural_losses: need depth [N] and normals [N,3], 1 <= N <= {_lib.PRIORS_MAX_RAYS}")
     spec = dict(weights=weights, confidence=float(confidence_threshold), normal_threshold=float(normal_threshold),
                 scale=scale, replay=bool(replay), workspace=workspace)
-    total = _FusedPriorsFn.apply(depth_pred, normals, spatial_coords, spec)
+    if addend is not None and addend.numel() != 1:
+        raise ValueError("fused_structural_losses: addend must hold one value")
+    total = _FusedPriorsFn.apply(depth_pred, normals, spatial_coords, addend, spec)
+    if addend is not None:
+        total = total.reshape(addend.shape)
     return total, spec["parts"]

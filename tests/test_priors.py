@@ -216,6 +216,34 @@ def test_fused_priors_device_mode(nerf, gpu, golden):
 
 
 @pytest.mark.gpu
+def test_fused_priors_addend_in_loss_launch(nerf, gpu, golden):
+    """addend (the training step's other losses) summed inside the loss launch
+    (nerf_priors_loss_add): bit-identical to `addend + total` as two tensors, the same parts, the same
+    depth / normals gradients, and the addend's gradient passed through."""
+    from indoor_nerf_amd import priors
+    g = golden("f18_priors")
+    xy = torch.from_numpy(g["a_coords"]).to(gpu)
+    outs = []
+    for fused in (False, True):
+        d = torch.from_numpy(g["a_depth"]).to(gpu).requires_grad_(True)
+        n = torch.from_numpy(g["a_normals"]).to(gpu).requires_grad_(True)
+        base = (torch.tensor(0.731, device=gpu) * torch.ones((), device=gpu)).requires_grad_(True)
+        nerf.manual_seed(9)
+        if fused:
+            loss, parts = priors.fused_structural_losses(d, n, xy, addend=base)
+        else:
+            total, parts = priors.fused_structural_losses(d, n, xy)
+            loss = base + total
+        assert loss.shape == ()
+        (loss * 3.0).backward()
+        outs.append((loss.detach(), parts.clone(), d.grad, n.grad, base.grad))
+    (l0, p0, dd0, dn0, b0), (l1, p1, dd1, dn1, b1) = outs
+    assert torch.equal(l0, l1) and torch.equal(p0, p1)
+    assert torch.equal(dd0, dd1) and torch.equal(dn0, dn1)
+    assert float(b0) == float(b1) == 3.0
+
+
+@pytest.mark.gpu
 def test_fused_priors_ramp_and_state_per_call(nerf, gpu, golden):
     """The ramp reaches the backward intact when the caller's scale tensor is a temporary (freed and
     its memory reused before backward), and every forward keeps its own state: a second forward in
