@@ -36,6 +36,8 @@ constexpr int kPriorsMaxRays = NERF_PRIORS_MAX_RAYS;
 constexpr int kCapPairs[3] = {100, 100, 50};
 constexpr float kClassScale[3] = {2.0f, 1.5f, 0.1f};
 constexpr int kMaxCons = 200;
+constexpr int kSelSeg = 512;               // selected keys per class (>= 2 x the largest pair cap)
+static_assert(kSelSeg >= 2 * 100 && (kSelSeg & (kSelSeg - 1)) == 0, "segment");
 
 // Device state shared by the three launches (lives at the start of the workspace).
 struct PriorsState {
@@ -368,9 +370,11 @@ __global__ void __launch_bounds__(64) priors_svd_kernel(PriorsArgs a) {
 // t >> 6 + 16, ... for t + kPT): every wave touches only its own runs, so such a stage after another
 // one needs a wave barrier, not a block barrier (4,096 keys: 15 block barriers instead of 78; the same
 // compare-swaps, so the same order bit for bit).
-__device__ void bitonic_sort(uint64_t* k, int M) {
+// seg < M: each seg-key segment sorted ascending on its own (the merge directions of the last stage
+// all ascending), the same network as a sort of seg keys per segment.
+__device__ void bitonic_sort(uint64_t* k, int M, int seg) {
     int prev = 1 << 30;   // stride of the previous stage (the first stage follows the keys' stores)
-    for (int size = 2; size <= M; size <<= 1)
+    for (int size = 2; size <= seg; size <<= 1)
         for (int stride = size >> 1; stride > 0; stride >>= 1) {
             if (stride >= 128 || prev >= 128) {
                 __syncthreads();
@@ -383,7 +387,7 @@ __device__ void bitonic_sort(uint64_t* k, int M) {
             for (int t = threadIdx.x; t < M / 2; t += kPT) {
                 const int lo = 2 * t - (t & (stride - 1));
                 const int hi = lo + stride;
-                const bool up = (lo & size) == 0;
+                const bool up = size == seg || (lo & size) == 0;
                 const uint64_t x = k[lo], y = k[hi];
                 if ((x > y) == up) { k[lo] = y; k[hi] = x; }
             }
@@ -425,7 +429,9 @@ __global__ void __launch_bounds__(kPT) priors_loss_kernel(PriorsArgs a) {
     __shared__ int s_ired[16];
     __shared__ float s_f[9];
     __shared__ int s_cnt[3];
-    extern __shared__ uint64_t s_keys[];   // device mode: [M] sort keys
+    __shared__ int s_hist[3 * 256];
+    __shared__ int s_bin[3];
+    extern __shared__ uint64_t s_keys[];   // device mode: max(M2, 4 x 512) sort keys
     PriorsState& st = *a.st;
     const int N = a.N, tid = threadIdx.x;
     const float scale = a.d_scale ? *a.d_scale : 1.0f;
@@ -499,27 +505,74 @@ __global__ void __launch_bounds__(kPT) priors_loss_kernel(PriorsArgs a) {
         const bool on = N >= 10 && ncls[k] > 5 && ncls[k] > 1;
         npair[k] = on ? min(kCapPairs[k], ncls[k] / 2) : 0;
     }
-    if (!a.perm && (npair[0] | npair[1] | npair[2])) {   // device randperm: sort members by random key
+    if (!a.perm && (npair[0] | npair[1] | npair[2])) {   // device randperm: members ordered by random key
+        // key = class << 40 | 24 random bits << 14 | index; a class's pairs are the 2 npair smallest keys
+        // of the class. Selected, then sorted: a histogram of the random bits' top 8 per class finds the
+        // bin holding the (2 npair)-th smallest, the keys up to that bin (~2 npair + N / 256) go to a
+        // 512-key segment per class, and the segments are sorted — the same keys in the same order as
+        // the sort of all M2 keys (which remains the path when a segment would overflow).
         int M2 = 1;
         while (M2 < N) M2 <<= 1;
         uint64_t sd, of;
         rng_of(a, sd, of);
-        for (int i = tid; i < M2; i += kPT) {
-            uint64_t key = ~0ull;
-            if (i < N) {
-                const uint8_t c = a.cls[i];
-                const uint64_t k = (c & 1) ? 0 : (c & 2) ? 1 : 2;
-                const uint32_t r = (uint32_t)(philox_uniform(sd, of, 64 + (uint64_t)i) * 16777216.0f);
-                key = (k << 40) | ((uint64_t)r << 14) | (uint64_t)i;
-            }
-            s_keys[i] = key;
+        auto key_of = [&](int i) -> uint64_t {
+            const uint8_t c = a.cls[i];
+            const uint64_t k = (c & 1) ? 0 : (c & 2) ? 1 : 2;
+            const uint32_t r = (uint32_t)(philox_uniform(sd, of, 64 + (uint64_t)i) * 16777216.0f);
+            return (k << 40) | ((uint64_t)r << 14) | (uint64_t)i;
+        };
+        for (int i = tid; i < 3 * 256; i += kPT) s_hist[i] = 0;
+        if (tid < 3) s_cnt[tid] = 0;
+        __syncthreads();
+        for (int i = tid; i < N; i += kPT) {
+            const uint64_t key = key_of(i);
+            atomicAdd(&s_hist[(int)(key >> 40) * 256 + (int)((key >> 30) & 255)], 1);
         }
-        bitonic_sort(s_keys, M2);
+        __syncthreads();
+        if (tid < 3 * 64) {   // wave k: the bin of class k's (2 npair)-th smallest key (-1: no pairs)
+            const int k = tid >> 6, lane = tid & 63, need = 2 * npair[k];
+            int c4[4], run = 0;
+            for (int j = 0; j < 4; ++j) { c4[j] = s_hist[k * 256 + 4 * lane + j]; run += c4[j]; }
+            int incl = run;   // inclusive scan of the lanes' 4-bin sums
+            for (int o = 1; o < 64; o <<= 1) {
+                const int v = __shfl_up(incl, o, 64);
+                if (lane >= o) incl += v;
+            }
+            int below = incl - run, bin = 1 << 30;
+            for (int j = 0; j < 4; ++j) {
+                if (below < need && below + c4[j] >= need) bin = 4 * lane + j;
+                below += c4[j];
+            }
+            for (int o = 32; o > 0; o >>= 1) bin = min(bin, __shfl_xor(bin, o, 64));
+            if (lane == 0) s_bin[k] = need > 0 ? bin : -1;
+        }
+        __syncthreads();
+        uint64_t* seg = s_keys;   // [4][512]: classes 0..2, the fourth all padding
+        for (int i = tid; i < N; i += kPT) {
+            const uint64_t key = key_of(i);
+            const int k = (int)(key >> 40);
+            if ((int)((key >> 30) & 255) <= s_bin[k]) {
+                const int pos = atomicAdd(&s_cnt[k], 1);
+                if (pos < kSelSeg) seg[k * kSelSeg + pos] = key;
+            }
+        }
+        __syncthreads();
+        const bool fits = s_cnt[0] <= kSelSeg && s_cnt[1] <= kSelSeg && s_cnt[2] <= kSelSeg;
+        if (fits) {
+            for (int i = tid; i < 4 * kSelSeg; i += kPT)
+                if (i >= 3 * kSelSeg || (i & (kSelSeg - 1)) >= s_cnt[i / kSelSeg]) seg[i] = ~0ull;
+            bitonic_sort(seg, 4 * kSelSeg, kSelSeg);
+        } else {   // a bin too full for its segment: every key, one sort
+            __syncthreads();
+            for (int i = tid; i < M2; i += kPT) s_keys[i] = i < N ? key_of(i) : ~0ull;
+            bitonic_sort(s_keys, M2, M2);
+        }
         int off = 0, start = 0;   // sorted: class 0 (floor), 1 (wall), 2 (other), random order inside a class
         for (int k = 0; k < 3; ++k) {
+            const int s0 = fits ? k * kSelSeg : start;
             for (int t = tid; t < npair[k]; t += kPT) {
-                st.pair_a[off + t] = (int)(s_keys[start + t] & 0x3FFF);
-                st.pair_b[off + t] = (int)(s_keys[start + npair[k] + t] & 0x3FFF);
+                st.pair_a[off + t] = (int)(s_keys[s0 + t] & 0x3FFF);
+                st.pair_b[off + t] = (int)(s_keys[s0 + npair[k] + t] & 0x3FFF);
             }
             off += kCapPairs[k];
             start += ncls[k];
@@ -898,7 +951,7 @@ extern "C" int nerf_priors_loss_add(const float* d_depth, const float* d_normals
     a.parts_out = d_parts;   // floor, wall, general, manhattan, planarity, consistency, total: stored by the kernel
     int M2 = 1;
     while (M2 < n_rays) M2 <<= 1;
-    const size_t lds = cfg->perm ? 0 : (size_t)M2 * sizeof(uint64_t);
+    const size_t lds = cfg->perm ? 0 : (size_t)std::max(M2, 4 * kSelSeg) * sizeof(uint64_t);
     hipLaunchKernelGGL(priors_loss_kernel, dim3(1), dim3(kPT), lds, as_stream(stream), a);
     NERF_CHECK_LAUNCH("priors_loss");
     if (d_coords) {   // the nearest-pixel queries (n_cons <= kMaxCons, read by each block) and the tail

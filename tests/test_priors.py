@@ -243,6 +243,64 @@ def test_fused_priors_addend_in_loss_launch(nerf, gpu, golden):
     assert float(b0) == float(b1) == 3.0
 
 
+def _philox_r24(seed, offset, index):
+    """The device draws' 24 random bits (csrc/common.h philox_uniform, uniform * 2^24 exactly):
+    Philox4x32-10 of counter (index >> 2, offset), key seed, component index & 3, shifted right 8."""
+    idx = np.asarray(index, dtype=np.uint64)
+    M = np.uint64(0xFFFFFFFF)
+    blk = idx >> np.uint64(2)
+    c0, c1 = blk & M, blk >> np.uint64(32)
+    c2 = np.full_like(c0, np.uint64(offset) & M)
+    c3 = np.full_like(c0, np.uint64(offset) >> np.uint64(32))
+    k0, k1 = np.uint64(seed) & M, np.uint64(seed) >> np.uint64(32)
+    for _ in range(10):
+        p0, p1 = np.uint64(0xD2511F53) * c0, np.uint64(0xCD9E8D57) * c2
+        hi0, lo0, hi1, lo1 = p0 >> np.uint64(32), p0 & M, p1 >> np.uint64(32), p1 & M
+        c0, c1, c2, c3 = hi1 ^ c1 ^ k0, lo1, hi0 ^ c3 ^ k1, lo0
+        k0, k1 = (k0 + np.uint64(0x9E3779B9)) & M, (k1 + np.uint64(0xBB67AE85)) & M
+    comp = np.stack([c0, c1, c2, c3])[(idx & np.uint64(3)).astype(np.int64), np.arange(idx.size)]
+    return comp >> np.uint64(8)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N", [4096, 777, 8192, 12])
+def test_fused_priors_device_pairs_are_the_sorted_keys(nerf, gpu, N):
+    """Device-mode planarity pairs (the randperm of each class as an order by random key): the
+    selection kernel's pairs equal those of sorting ALL keys (class << 40 | Philox 24 bits << 14 |
+    index) on the host — the 2 npair smallest keys of each class, in order."""
+    import sys
+    from indoor_nerf_amd import _lib, priors
+    render = sys.modules["indoor_nerf_amd.render"]   # the module (the package exports its render())
+    g = torch.Generator().manual_seed(N)
+    n = torch.randn(N, 3, generator=g)
+    n[: N // 3] = torch.tensor([0.05, 0.02, 1.0]) + 0.1 * torch.randn(N // 3, 3, generator=g)
+    n[N // 3: 2 * N // 3, 2] *= 0.05
+    d = (torch.rand(N, generator=g) * 3 + 0.5).to(gpu)
+    n = n.to(gpu)
+    nerf.manual_seed(77)
+    seed, off = render._draw_seed()
+    nerf.manual_seed(77)
+    ws = torch.empty(int(_lib.load().nerf_priors_workspace_bytes(N)), dtype=torch.uint8, device=gpu)
+    priors.fused_structural_losses(d, n, None, workspace=ws)
+    torch.cuda.synchronize()
+    st = ws[:4704].view(torch.int32).cpu().numpy()
+    npair = st[8:11]
+    cls = ws[4864:4864 + N].cpu().numpy()
+    k = np.where(cls & 1, 0, np.where(cls & 2, 1, 2)).astype(np.uint64)
+    r = _philox_r24(int(seed), int(off), 64 + np.arange(N, dtype=np.uint64))
+    keys = np.sort((k << np.uint64(40)) | (r << np.uint64(14)) | np.arange(N, dtype=np.uint64))
+    pair_a, pair_b = st[76:326], st[326:576]
+    caps, o, start = (100, 100, 50), 0, 0
+    assert npair.sum() > 0 or N < 20
+    for c in range(3):
+        members = keys[(keys >> np.uint64(40)) == c]
+        want = (members & np.uint64(0x3FFF)).astype(np.int64)
+        p = int(npair[c])
+        np.testing.assert_array_equal(pair_a[o:o + p], want[:p])
+        np.testing.assert_array_equal(pair_b[o:o + p], want[p:2 * p])
+        o += caps[c]
+
+
 @pytest.mark.gpu
 def test_fused_priors_ramp_and_state_per_call(nerf, gpu, golden):
     """The ramp reaches the backward intact when the caller's scale tensor is a temporary (freed and
