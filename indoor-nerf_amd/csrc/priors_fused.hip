@@ -334,19 +334,33 @@ __global__ void __launch_bounds__(kPT) priors_prep_kernel(PriorsArgs a) {
             }
             a.assign[(size_t)it * N + i] = asg;
         }
-        block_sum_vec<12>(red, s_red);
-        __syncthreads();
+        // the 16 waves' partials to LDS; thread k < 3 alone adds centre k's four (in block_sum_vec's
+        // order, the same bits) and updates it: two block barriers per round instead of five
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {   // centre = F.normalize(mean); an empty cluster keeps its centre
-            if (tid == k && red[9 + k] > 0.f) {
-                const float m[3] = {red[3 * k] / red[9 + k], red[3 * k + 1] / red[9 + k], red[3 * k + 2] / red[9 + k]};
+        for (int k = 0; k < 12; ++k) red[k] = wave_total(red[k]);
+        if ((tid & 63) == 0)
+#pragma unroll
+            for (int k = 0; k < 12; ++k) s_red[(tid >> 6) * 12 + k] = red[k];
+        __syncthreads();
+        if (tid < 3) {   // centre = F.normalize(mean); an empty cluster keeps its centre
+            const int k = tid;
+            const int col[4] = {3 * k, 3 * k + 1, 3 * k + 2, 9 + k};
+            float t4[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                float t = 0.f;
+                for (int j = 0; j < kPT / 64; ++j) t += s_red[j * 12 + col[q]];
+                t4[q] = t;
+            }
+            if (t4[3] > 0.f) {
+                const float m[3] = {t4[0] / t4[3], t4[1] / t4[3], t4[2] / t4[3]};
                 const float d = fmaxf(norm3(m[0], m[1], m[2]), 1e-12f);
                 for (int c = 0; c < 3; ++c) {
                     s_c[3 * k + c] = m[c] / d;
                     st.means[3 * k + c] = m[c];
                 }
                 st.centre_iter[k] = it;
-                st.centre_count[k] = (int)red[9 + k];
+                st.centre_count[k] = (int)t4[3];
             }
         }
         __syncthreads();

@@ -219,7 +219,8 @@ def test_fused_priors_device_mode(nerf, gpu, golden):
 def test_fused_priors_addend_in_loss_launch(nerf, gpu, golden):
     """addend (the training step's other losses) summed inside the loss launch
     (nerf_priors_loss_add): bit-identical to `addend + total` as two tensors, the same parts, the same
-    depth / normals gradients, and the addend's gradient passed through."""
+    depth / normals gradients (to the backward's atomic-order rounding), and the addend's gradient
+    passed through."""
     from indoor_nerf_amd import priors
     g = golden("f18_priors")
     xy = torch.from_numpy(g["a_coords"]).to(gpu)
@@ -239,7 +240,8 @@ def test_fused_priors_addend_in_loss_launch(nerf, gpu, golden):
         outs.append((loss.detach(), parts.clone(), d.grad, n.grad, base.grad))
     (l0, p0, dd0, dn0, b0), (l1, p1, dd1, dn1, b1) = outs
     assert torch.equal(l0, l1) and torch.equal(p0, p1)
-    assert torch.equal(dd0, dd1) and torch.equal(dn0, dn1)
+    for x, y in ((dd0, dd1), (dn0, dn1)):   # the backward's LDS float atomics: order-dependent last bits
+        torch.testing.assert_close(x, y, rtol=0, atol=1e-6 * float(x.abs().max()))
     assert float(b0) == float(b1) == 3.0
 
 
