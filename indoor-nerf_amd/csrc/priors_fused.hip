@@ -15,8 +15,9 @@
 //
 // Three single-workgroup launches (N <= 8192 rays, one 1024-thread block):
 //   priors_prep_kernel : normals -> masks, counts, k-means (assignments of every round kept for the
-//                        backward), and (device mode) the 3x3 SVD of the centres;
-//   priors_loss_kernel : frame, the three losses, their sum;
+//                        backward);
+//   priors_loss_kernel : (device mode) the 3x3 SVD of the centres on one thread (fp64 registers, no
+//                        scratch at this kernel's 70 VGPRs), frame, the three losses, their sum;
 //   priors_bwd_kernel  : d depth, d normals from d loss.
 // With pixel coordinates the loss launch stops after the consistency queries: the nearest-pixel
 // search runs one block per query (priors_nearest_kernel) and priors_loss_tail_kernel finishes.
@@ -368,17 +369,6 @@ __global__ void __launch_bounds__(kPT) priors_prep_kernel(PriorsArgs a) {
     if (tid < 9) st.centres[tid] = s_c[tid];
 }
 
-// Device SVD of A = centres^T (fp64 Jacobi), its own one-wave launch: inside the 1024-thread prep
-// kernel (128 VGPRs per lane) the fp64 matrices spill to scratch.
-__global__ void __launch_bounds__(64) priors_svd_kernel(PriorsArgs a) {
-    PriorsState& st = *a.st;
-    if (threadIdx.x != 0 || !st.kmeans) return;
-    float A[9];
-    for (int r = 0; r < 3; ++r)
-        for (int c = 0; c < 3; ++c) A[3 * r + c] = st.centres[3 * c + r];
-    svd3(A, st.U, st.S, st.V);
-}
-
 // ---- bitonic sort of up to 8192 64-bit keys in LDS (device-mode randperm) ------------------------
 // A stage of stride <= 64 pairs keys inside 128-key runs, and thread t's pairs lie in run t >> 6 (and
 // t >> 6 + 16, ... for t + kPT): every wave touches only its own runs, so such a stage after another
@@ -454,7 +444,12 @@ __global__ void __launch_bounds__(kPT) priors_loss_kernel(PriorsArgs a) {
         float f[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
         int flip = 0;
         if (st.kmeans) {
-            if (a.usv) {
+            if (!a.usv) {   // device mode: the SVD of A = centres^T (fp64 Jacobi) here, not a launch of its own
+                float A[9];
+                for (int r = 0; r < 3; ++r)
+                    for (int c = 0; c < 3; ++c) A[3 * r + c] = st.centres[3 * c + r];
+                svd3(A, st.U, st.S, st.V);
+            } else {
                 for (int k = 0; k < 9; ++k) { st.U[k] = a.usv[k]; st.V[k] = a.usv[12 + k]; }
                 for (int k = 0; k < 3; ++k) st.S[k] = a.usv[9 + k];
             }
@@ -937,10 +932,6 @@ extern "C" int nerf_priors_prep(const float* d_depth, const float* d_normals, co
     if (rc) return rc;
     hipLaunchKernelGGL(priors_prep_kernel, dim3(1), dim3(kPT), (size_t)3 * n_rays * sizeof(float), as_stream(stream), a);
     NERF_CHECK_LAUNCH("priors_prep");
-    if (!cfg->usv) {
-        hipLaunchKernelGGL(priors_svd_kernel, dim3(1), dim3(64), 0, as_stream(stream), a);
-        NERF_CHECK_LAUNCH("priors_prep (svd)");
-    }
     if (d_centres_out) {   // the final k-means centres [3,3] (rows), for the host SVD of replay mode
         const hipError_t e = hipMemcpyAsync(d_centres_out, a.st->centres, 9 * sizeof(float), hipMemcpyDeviceToDevice,
                                             as_stream(stream));
