@@ -267,7 +267,9 @@ def raw2outputs(raw, z_vals, rays_d, raw_noise_std=0, white_bkgd=False, pytest=F
         if pytest:
             noise = _pytest_uniforms((R, S), raw.device) * raw_noise_std
         else:
-            noise = torch.randn(R, S, device=raw.device) * raw_noise_std
+            # torch.randn(R, S) * raw_noise_std (run_nerf.py) in one launch: normal_'s transform z * std + 0
+            # rounds like the product, from the same generator draws (tests/test_gpu_parity.py)
+            noise = torch.empty(R, S, device=raw.device).normal_(0.0, raw_noise_std)
     if raw.shape[-1] not in (4, 7):
         raise ValueError(f"raw2outputs: raw must have 4 or 7 channels, got {raw.shape[-1]}")
     if not predict_normals and raw.shape[-1] == 7:

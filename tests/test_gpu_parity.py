@@ -887,3 +887,16 @@ def test_normal_head_fwd_rows_matches_scatter(nerf, gpu, P):
     torch.cuda.synchronize()
     assert torch.equal(keep_m, want_keep)
     assert torch.equal(raw7, want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("std", [1.0, 0.37, 1e-3])
+def test_raw_noise_one_launch_matches_randn_times_std(gpu, std):
+    """raw2outputs' noise as normal_(0, std) in one launch: bit-identical to the reference's
+    torch.randn(shape) * raw_noise_std from the same generator state (odd sizes included)."""
+    for shape in ((4096, 64), (37, 13)):
+        torch.manual_seed(123)
+        want = torch.randn(*shape, device=gpu) * std
+        torch.manual_seed(123)
+        got = torch.empty(*shape, device=gpu).normal_(0.0, std)
+        assert torch.equal(got, want), (shape, std)
